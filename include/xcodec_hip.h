@@ -1,0 +1,123 @@
+/*
+ * xcodec_hip.h — C ABI of the MI355X-native XCodec codec (libxcodec_hip.so).
+ *
+ * Plain C: opaque handles, plain pointers and sizes, int status (0 = ok,
+ * negative errno-style on failure).  No exceptions cross this boundary and
+ * no torch / HIP types appear in the signatures (streams are passed as void*,
+ * NULL = the context's own stream).
+ *
+ * Each entry point names the reference interface it replaces
+ * (bramfeld/wanproxy, file:line).  INTEGRATION.md shows the reference-side
+ * binding (the C++ facade a maintainer drops under xcodec/).
+ *
+ * Semantics are the reference's, bit for bit: a batch is processed as if its
+ * buffers were fed, in index order, each to a fresh XCodecEncoder
+ * (encode + flush) / XCodecDecoder (one decode call) sharing one
+ * XCodecMemoryCache (xcodec/xcodec_cache.h:162-211).
+ */
+#ifndef XCODEC_HIP_H
+#define XCODEC_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define XC_SEGMENT_LENGTH 2048 /* xcodec/xcodec.h:78 */
+
+#define XC_OK 0
+#define XC_EINVAL (-22)
+#define XC_ENOMEM (-12)
+#define XC_ENOSPC (-28)  /* device cache capacity exhausted */
+#define XC_EDEVICE (-5)  /* HIP runtime error */
+#define XC_ENOENT (-2)
+
+typedef struct xc_ctx xc_ctx;     /* one per GPU; use from one host thread at a time */
+typedef struct xc_cache xc_cache; /* replaces XCodecMemoryCache (xcodec/xcodec_cache.h:162-211) */
+typedef struct xc_plan xc_plan;   /* a device-resident batch layout + workspace */
+
+/* Number of visible HIP devices. */
+int xc_device_count(int *n);
+
+/* Context on device `dev` with its own HIP stream. */
+int xc_ctx_create(int dev, xc_ctx **out);
+int xc_ctx_destroy(xc_ctx *ctx);
+/* The context's hipStream_t, as void*. */
+void *xc_ctx_stream(xc_ctx *ctx);
+/* Wait for all work queued on the context stream. */
+int xc_ctx_sync(xc_ctx *ctx);
+
+/* XCodecMemoryCache(UUID, size) (xcodec/xcodec_cache.h:169-172), device resident.
+ * cap_segments bounds the segments the cache can hold (the reference map is unbounded;
+ * exceeding cap fails the batch with XC_ENOSPC instead of evicting). */
+int xc_cache_create(xc_ctx *ctx, uint64_t cap_segments, xc_cache **out);
+int xc_cache_destroy(xc_cache *c);
+int xc_cache_count(xc_cache *c, uint64_t *n);
+/* Remember the current contents; xc_cache_restore() rolls every later enter() back. */
+int xc_cache_snapshot(xc_cache *c);
+int xc_cache_restore(xc_cache *c);
+/* XCodecCache::lookup (xcodec/xcodec_cache.h:190-210): *found = 1 and 2048 bytes to out (host). */
+int xc_cache_lookup(xc_cache *c, uint64_t hash, uint8_t *out, int *found);
+/* XCodecCache::enter (xcodec/xcodec_cache.h:182-188): seg = 2048 host bytes. */
+int xc_cache_enter(xc_cache *c, uint64_t hash, const uint8_t *seg);
+
+/* XCodecHash::hash (xcodec/xcodec_hash.h:166-174) of n device-resident, 2048-byte-strided
+ * segments -> n hashes (device).  stream may be NULL. */
+int xc_hash_segments(xc_ctx *ctx, const uint8_t *d_segs, uint64_t n, uint64_t *d_out, void *stream);
+
+/* The encoder's rolling hash (xcodec/xcodec_hash.h:93-164 as driven by
+ * xcodec/xcodec_encoder.cc:72-84) at every window end of one device buffer:
+ * d_out[p] = H(d_in[p-2047..p]) for p >= 2047, 0 below. */
+int xc_window_hashes(xc_ctx *ctx, const uint8_t *d_in, uint64_t n, uint64_t *d_out, void *stream);
+
+/* ---- batch encode: XCodecEncoder::encode + flush (xcodec/xcodec_encoder.cc:60-201) ----
+ *
+ * A plan fixes the buffer lengths of a batch and owns the device workspace.
+ * Input arena layout: buffer i at in_off[i] (256-byte aligned), output arena:
+ * buffer i's encoded stream at out_off[i] with capacity 2*len+16
+ * (the reference's worst case is 2*len: every byte an escaped 0xF1). */
+int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint64_t nbuf, xc_plan **out);
+int xc_plan_destroy(xc_plan *p);
+/* Arena sizes and per-buffer offsets (host arrays of nbuf, may be NULL). */
+int xc_plan_layout(xc_plan *p, uint64_t *in_off, uint64_t *out_off, uint64_t *in_bytes,
+                   uint64_t *out_bytes);
+/* Device-resident encode: d_in / d_out are device arenas in the plan's layout, d_out_len
+ * receives nbuf uint64 lengths (device).  Blocks the host until the batch is decided
+ * (the codec's sequential-order fix-ups need a host decision), results are on the device. */
+int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_out_len);
+/* Host-to-host convenience: pinned H2D, xc_encode_run, D2H.  out_len receives nbuf lengths. */
+int xc_encode_batch_host(xc_cache *c, const uint8_t *in, const uint64_t *in_off,
+                         const uint64_t *in_len, uint64_t nbuf, uint8_t *out,
+                         const uint64_t *out_off, const uint64_t *out_cap, uint64_t *out_len);
+
+/* Counters of the last run (for benchmarks / profiling). */
+typedef struct {
+    uint64_t n_extract;  /* EXTRACT tokens emitted (segments declared) */
+    uint64_t n_ref;      /* REF tokens emitted */
+    uint64_t in_bytes, out_bytes;
+    uint32_t sub_batches, walk_rounds, outer_rounds, dense_chunks;
+} xc_run_stats;
+int xc_plan_stats(xc_plan *p, xc_run_stats *st);
+
+/* ---- batch decode: XCodecDecoder::decode (xcodec/xcodec_decoder.cc:76-176) ----
+ * status[i] = 1 (decode returned true) or 0 (false); consumed[i] = input bytes the
+ * reference removes from its Buffer; has_unknown[i]/unknown[i] = the REF hash the
+ * reference inserted into unknown_hashes and stopped on. */
+int xc_decode_batch_host(xc_cache *c, const uint8_t *in, const uint64_t *in_off,
+                         const uint64_t *in_len, uint64_t nbuf, uint8_t *out,
+                         const uint64_t *out_off, const uint64_t *out_cap, uint64_t *out_len,
+                         uint64_t *consumed, int32_t *status, uint64_t *unknown,
+                         int32_t *has_unknown);
+
+/* Library self-test of the wave primitives on device (returns XC_OK or a negative code). */
+int xc_selftest(xc_ctx *ctx);
+
+/* Human-readable text of the last error recorded on this thread. */
+const char *xc_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

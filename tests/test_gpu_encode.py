@@ -1,0 +1,213 @@
+"""GPU parity tests: the HIP encode path (through the C ABI) against the oracle.
+
+Bit-exact byte streams are required (integer/byte work)."""
+import numpy as np
+import pytest
+
+from wanproxy_amd import workloads as W
+
+pytestmark = pytest.mark.gpu
+
+
+def _esc(n, seed, frac=0.3):
+    rng = np.random.default_rng(seed)
+    b = rng.integers(0, 256, n, dtype=np.uint8)
+    b[rng.random(n) < frac] = 0xF1
+    return b
+
+
+def _collision_pair(seed=1):
+    rng = np.random.default_rng(seed)
+    x = (rng.integers(2, 126, 2048, dtype=np.int64) * 2 + 1).astype(np.uint8)
+    y = x.copy()
+    y[100] += 2; y[101] -= 2; y[1500] -= 2; y[1501] += 2
+    return x, y
+
+
+def _gpu_encode(ctx, bufs, warm=None, cap=1 << 16):
+    import wanproxy_amd as w
+    cache = w.XCodecCache(ctx, cap)
+    enc = w.XCodecEncoder(cache)
+    if warm:
+        for batch in warm:
+            enc.encode_batch(batch)
+    return enc.encode_batch(bufs), cache
+
+
+def _check(ctx, oracle_mod, bufs, warm=None):
+    oc = oracle_mod.Cache()
+    if warm:
+        for batch in warm:
+            oc.encode_batch(batch)
+    want = oc.encode_batch(bufs)
+    got, cache = _gpu_encode(ctx, bufs, warm)
+    assert len(got) == len(want)
+    for i, (g, e) in enumerate(zip(got, want)):
+        if g != e:
+            n = min(len(g), len(e))
+            d = next((k for k in range(n) if g[k] != e[k]), n)
+            pytest.fail(f"buffer {i}: len gpu {len(g)} oracle {len(e)}, first diff at {d}")
+    assert len(cache) == len(oc)
+    return got
+
+
+def test_selftest(gpu_ctx):
+    gpu_ctx.selftest()
+
+
+def test_window_hashes(gpu_ctx, oracle_mod):
+    import torch
+    import wanproxy_amd.xcodec as X
+    for d in [W.gen(7, 300_000), _esc(70_000, 3), np.full(10_000, 0xF1, np.uint8)]:
+        t = torch.zeros(len(d) + 256, dtype=torch.uint8, device="cuda")
+        t[:len(d)] = torch.from_numpy(d)
+        out = torch.zeros(len(d), dtype=torch.int64, device="cuda")
+        X.window_hashes(gpu_ctx, t.data_ptr(), len(d), out.data_ptr())
+        gpu_ctx.sync()
+        got = out.cpu().numpy().view(np.uint64)
+        assert np.array_equal(got, oracle_mod.window_hashes(d))
+
+
+def test_segment_hash_kats(gpu_ctx):
+    import json
+    import os
+    import torch
+    import wanproxy_amd.xcodec as X
+    kats = [int(x, 16) for x in json.load(open(os.path.join(
+        os.path.dirname(__file__), "golden", "hash_kats.json")))["kats"]]
+    segs = torch.arange(256, dtype=torch.uint8).repeat_interleave(2048).cuda()
+    out = torch.zeros(256, dtype=torch.int64, device="cuda")
+    X.hash_segments(gpu_ctx, segs.data_ptr(), 256, out.data_ptr())
+    gpu_ctx.sync()
+    assert out.cpu().numpy().view(np.uint64).tolist() == kats
+
+
+def test_cache_enter_lookup(gpu_ctx, oracle_mod):
+    import wanproxy_amd as w
+    c = w.XCodecCache(gpu_ctx, 64)
+    seg = W.gen(5, 2048)
+    h = oracle_mod.hash_segment(seg)
+    assert c.lookup(h) is None
+    c.enter(h, seg)
+    assert c.lookup(h) == seg.tobytes()
+    assert len(c) == 1
+    c.snapshot()
+    seg2 = W.gen(6, 2048)
+    c.enter(oracle_mod.hash_segment(seg2), seg2)
+    assert len(c) == 2
+    c.restore()
+    assert len(c) == 1 and c.lookup(oracle_mod.hash_segment(seg2)) is None
+    assert c.lookup(h) == seg.tobytes()
+
+
+def test_tiny_and_boundaries(gpu_ctx, oracle_mod):
+    bufs = [W.gen(5, 0), W.gen(5, 1), W.gen(5, 100), W.gen(6, 2047), W.gen(7, 2048),
+            W.gen(8, 2049), W.gen(9, 4095), W.gen(10, 4096), W.gen(11, 4097), W.gen(12, 6143),
+            W.gen(13, 8191), W.gen(14, 8192), W.gen(15, 8193), W.gen(16, 12345)]
+    _check(gpu_ctx, oracle_mod, bufs)
+
+
+def test_cfg1_roundtrip_1mib(gpu_ctx, oracle_mod):
+    d = W.gen(1, 1 << 20)
+    got = _check(gpu_ctx, oracle_mod, [d])
+    assert len(got[0]) == 1049600
+
+
+def test_warm_second_pass_all_refs(gpu_ctx, oracle_mod):
+    d = W.gen(1, 1 << 20)
+    got = _check(gpu_ctx, oracle_mod, [d], warm=[[d]])
+    assert len(got[0]) == 512 * 10
+
+
+def test_cfg2_random(gpu_ctx, oracle_mod):
+    _check(gpu_ctx, oracle_mod, W.random_buffers(64))
+
+
+def test_cfg3_repeats_warm(gpu_ctx, oracle_mod):
+    pool = W.pool(1024)
+    warm = [[pool[i:i + 65536] for i in range(0, len(pool), 65536)]]
+    bufs = W.repeat_buffers(48, 0x77, np_segments=1024, pool_bytes=pool)
+    _check(gpu_ctx, oracle_mod, bufs, warm=warm)
+
+
+def test_cfg4_variant_90pct(gpu_ctx, oracle_mod):
+    pool = W.pool(512)
+    warm = [[pool[i:i + 65536] for i in range(0, len(pool), 65536)]]
+    bufs = W.repeat_buffers(32, 0x88, repeat_pct=90, np_segments=512, pool_bytes=pool)
+    _check(gpu_ctx, oracle_mod, bufs, warm=warm)
+
+
+@pytest.mark.parametrize("ch", [0, 0xF1, 0x41])
+def test_charrun_self_references(gpu_ctx, oracle_mod, ch):
+    """Dense self-references (xcodec-encode-decode1 intent): 1 EXTRACT + REFs."""
+    bufs = [np.full(512 * 1024, ch, np.uint8), np.full(70000, ch, np.uint8)]
+    got = _check(gpu_ctx, oracle_mod, bufs)
+    assert len(got[0]) == 4600
+
+
+def test_escape_heavy(gpu_ctx, oracle_mod):
+    _check(gpu_ctx, oracle_mod, [_esc(20000, 5), _esc(70000, 6), _esc(3000, 7, 1.0),
+                                 np.full(5000, 0xF1, np.uint8)])
+
+
+def test_cross_buffer_duplicates(gpu_ctx, oracle_mod):
+    """Later buffers reference segments first declared by earlier buffers of the same batch."""
+    a = W.gen(21, 65536)
+    b = np.concatenate([W.gen(22, 3000), a[:30000], W.gen(23, 5000)])
+    c = np.concatenate([a[10000:40000], b[:20000]])
+    d = a.copy()
+    _check(gpu_ctx, oracle_mod, [a, b, c, d, W.gen(24, 65536), a[::-1].copy()])
+
+
+def test_shifted_repeats(gpu_ctx, oracle_mod):
+    """Repeats at unaligned offsets inside one buffer and across buffers."""
+    base = W.gen(31, 20000)
+    bufs = []
+    for k in range(8):
+        parts = [W.gen(100 + k, 777 * k + 5), base[k * 333:k * 333 + 9000], W.gen(200 + k, 1234),
+                 base[:7000]]
+        bufs.append(np.concatenate(parts))
+    _check(gpu_ctx, oracle_mod, bufs)
+
+
+def test_collisions(gpu_ctx, oracle_mod):
+    x, y = _collision_pair()
+    bufs = [np.concatenate([W.gen(3, 500), y, W.gen(4, 5000)]),
+            np.concatenate([y, x, y, W.gen(5, 3000)])]
+    _check(gpu_ctx, oracle_mod, bufs, warm=[[x]])
+    _check(gpu_ctx, oracle_mod, [x, np.concatenate([y, W.gen(6, 4000)]), np.concatenate([x, y])])
+
+
+def test_device_resident_plan_and_restore(gpu_ctx, oracle_mod):
+    import torch
+    import wanproxy_amd as w
+    pool = W.pool(256)
+    warm = [pool[i:i + 65536] for i in range(0, len(pool), 65536)]
+    bufs = W.repeat_buffers(40, 0x5555, np_segments=256, pool_bytes=pool)
+    oc = oracle_mod.Cache()
+    oc.encode_batch(warm)
+    want = oc.encode_batch(bufs)
+
+    cache = w.XCodecCache(gpu_ctx, 1 << 14)
+    w.XCodecEncoder(cache).encode_batch(warm)
+    cache.snapshot()
+    plan = w.EncodePlan(cache, [len(b) for b in bufs])
+    arena = np.zeros(plan.in_bytes, np.uint8)
+    for i, b in enumerate(bufs):
+        arena[int(plan.in_off[i]):int(plan.in_off[i]) + len(b)] = b
+    d_in = torch.from_numpy(arena).cuda()
+    d_out = torch.zeros(plan.out_bytes, dtype=torch.uint8, device="cuda")
+    d_len = torch.zeros(len(bufs), dtype=torch.int64, device="cuda")
+    for it in range(3):
+        cache.restore()
+        d_out.zero_()
+        torch.cuda.synchronize()
+        plan.run(d_in.data_ptr(), d_out.data_ptr(), d_len.data_ptr())
+        gpu_ctx.sync()
+        out = d_out.cpu().numpy()
+        lens = d_len.cpu().numpy()
+        for i in range(len(bufs)):
+            o = int(plan.out_off[i])
+            assert out[o:o + int(lens[i])].tobytes() == want[i], (it, i)
+    st = plan.stats()
+    assert st.n_extract + st.n_ref > 0

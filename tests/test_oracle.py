@@ -1,0 +1,141 @@
+"""CPU tests: the oracle (oracle/xc_oracle.c) against the reference's own fixtures.
+
+The oracle is test infrastructure — the checker for the HIP path."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from wanproxy_amd import workloads as W
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def test_hash_kats(oracle_mod):
+    """256 single-character KATs (xcodec/test/xcodec-hash1/xcodec-hash1.cc:34-291)."""
+    kats = [int(x, 16) for x in json.load(open(os.path.join(GOLD, "hash_kats.json")))["kats"]]
+    assert len(kats) == 256
+    for i, k in enumerate(kats):
+        assert oracle_mod.hash_segment(np.full(2048, i, np.uint8)) == k, i
+
+
+def test_window_hashes_vs_reference_class(oracle_mod):
+    """H at 8192 positions, fixture computed by the reference XCodecHash class."""
+    z = np.load(os.path.join(GOLD, "window_hashes.npz"))
+    data = {"random": W.gen(7, 256 * 1024)}
+    rng = np.random.default_rng(3)
+    b = rng.integers(0, 256, 64 * 1024, dtype=np.uint8)
+    b[rng.random(64 * 1024) < 0.3] = 0xF1
+    data["escape"] = b
+    for name, d in data.items():
+        h = oracle_mod.window_hashes(d)
+        pos = z[name + "_pos"].astype(np.int64)
+        assert np.array_equal(h[pos], z[name + "_hash"]), name
+
+
+def test_window_hashes_live_reference(oracle_mod):
+    rl = oracle_mod.ref_hash_lib()
+    if rl is None:
+        pytest.skip("oracle/_ref not built (reference sources absent)")
+    d = W.gen(99, 300_000)
+    a = oracle_mod.window_hashes(d)
+    b = np.zeros_like(a)
+    rl.xcref_window_hashes(d, len(d), b)
+    assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("ch", [0, 1, 0x7F, 0xF1, 0xFF])
+def test_charrun_roundtrip(oracle_mod, ch):
+    """Intent of xcodec/test/xcodec-encode-decode1/xcodec-encode-decode1.cc:38-105:
+    512 KiB of one byte -> 1 EXTRACT + 255 REF = 4600 bytes, decodes back."""
+    buf = np.full(512 * 1024, ch, np.uint8)
+    enc = oracle_mod.Cache().encode_batch([buf])[0]
+    assert len(enc) == 4600
+    st, dec, cons, unk = oracle_mod.Cache().decode_batch([enc])[0]
+    assert st == 1 and unk is None and cons == len(enc) and dec == buf.tobytes()
+
+
+def test_encode_vectors(oracle_mod):
+    vec = {v["case"]: v for v in json.load(open(os.path.join(GOLD, "encode_vectors.json")))}
+    rng3 = np.random.default_rng(5)
+
+    def esc(n, seed):
+        rng = np.random.default_rng(seed)
+        b = rng.integers(0, 256, n, dtype=np.uint8)
+        b[rng.random(n) < 0.3] = 0xF1
+        return b
+    cases = {
+        "cfg1_gen1_1MiB": [W.gen(1, 1 << 20)],
+        "tiny": [W.gen(5, 100), W.gen(6, 2047), W.gen(7, 2048), W.gen(8, 2049), W.gen(9, 4095),
+                 W.gen(10, 4096), W.gen(11, 6143)],
+        "charrun_f1_64k": [np.full(65536, 0xF1, np.uint8)],
+        "escape_heavy": [esc(20000, 5), esc(70000, 6)],
+        "cfg2_16": W.random_buffers(16),
+    }
+    del rng3
+    for name, bufs in cases.items():
+        outs = oracle_mod.Cache().encode_batch(bufs)
+        assert [len(o) for o in outs] == vec[name]["lens"], name
+        assert [hashlib.sha256(o).hexdigest() for o in outs] == vec[name]["sha256"], name
+
+
+def test_cfg1_roundtrip(oracle_mod):
+    d = W.gen(1, 1 << 20)
+    c = oracle_mod.Cache()
+    enc = c.encode_batch([d])[0]
+    assert len(enc) == 1049600  # 512 EXTRACTs of 2050 bytes
+    st, dec, cons, unk = oracle_mod.Cache().decode_batch([enc])[0]
+    assert st == 1 and dec == d.tobytes()
+    # warm pass: every segment is now a REF
+    enc2 = c.encode_batch([d])[0]
+    assert len(enc2) == 512 * 10
+
+
+def test_cfg2_ratio_matches_survey(oracle_mod):
+    """the reference encoder's cfg2 out/in = 1.0010."""
+    bufs = W.random_buffers(64)
+    outs = oracle_mod.Cache().encode_batch(bufs)
+    assert round(sum(map(len, outs)) / sum(map(len, bufs)), 4) == 1.0010
+
+
+def test_decoder_error_paths(oracle_mod):
+    c = oracle_mod.Cache()
+    # bad opcode -> false, input left at the F1
+    st, dec, cons, unk = c.decode_batch([b"abc\xf1\x07xyz"])[0]
+    assert st == 0 and dec == b"abc" and cons == 3
+    # unknown REF -> true, stops at the REF
+    st, dec, cons, unk = c.decode_batch([b"ab\xf1\x02" + bytes(range(8)) + b"tail"])[0]
+    assert st == 1 and unk == int.from_bytes(bytes(range(8)), "big") and cons == 2 and dec == b"ab"
+    # truncated EXTRACT / REF / lone F1 -> true, waits
+    for s in [b"q\xf1\x01" + b"z" * 100, b"q\xf1\x02\x00", b"q\xf1"]:
+        st, dec, cons, unk = c.decode_batch([s])[0]
+        assert st == 1 and dec == b"q" and cons == 1 and unk is None
+    # escape
+    st, dec, cons, unk = c.decode_batch([b"\xf1\x00\xf1\x00x"])[0]
+    assert st == 1 and dec == b"\xf1\xf1x" and cons == 5
+
+
+def collision_pair(seed=1):
+    """Two different 2048-byte windows with the same XCodec hash: odd bytes keep ffs()=1,
+    +2/-2/-2/+2 at (i, i+1, j, j+1) keeps both S1 and S2 (xcodec/xcodec_hash.h:43-70)."""
+    rng = np.random.default_rng(seed)
+    x = (rng.integers(2, 126, 2048, dtype=np.int64) * 2 + 1).astype(np.uint8)
+    y = x.copy()
+    i, j = 100, 1500
+    y[i] += 2; y[i + 1] -= 2; y[j] -= 2; y[j + 1] += 2
+    return x, y
+
+
+def test_collision_semantics(oracle_mod):
+    x, y = collision_pair()
+    assert oracle_mod.hash_segment(x) == oracle_mod.hash_segment(y)
+    assert not np.array_equal(x, y)
+    c = oracle_mod.Cache()
+    c.encode_batch([x])
+    out = c.encode_batch([np.concatenate([y, W.gen(3, 5000)])])[0]
+    # the collision at the first window suppresses that candidate
+    assert len(out) > 0
+    st, dec, cons, unk = c.clone().decode_batch([b"\xf1\x01" + y.tobytes()])[0]
+    assert st == 0

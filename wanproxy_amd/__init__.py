@@ -1,0 +1,12 @@
+"""wanproxy_amd — MI355X-native XCodec (WANProxy's deduplicating stream codec).
+
+The hot path (rolling window hash, cache probe, encode state machine, decode
+reference expansion) runs as hand-written gfx950 HIP kernels in
+``libxcodec_hip.so`` behind the C ABI declared in ``include/xcodec_hip.h``.
+"""
+from . import workloads  # noqa: F401
+from .xcodec import (Context, EncodePlan, XCodecCache, XCodecDecoder, XCodecEncoder,  # noqa: F401
+                     XCodecError, device_count, load_library)
+
+__all__ = ["Context", "EncodePlan", "XCodecCache", "XCodecDecoder", "XCodecEncoder",
+           "XCodecError", "device_count", "load_library", "workloads"]

@@ -1,0 +1,247 @@
+// xc_device.h — wave64 primitives and the XCodec window-hash arithmetic for gfx950.
+//
+// The hash (xcodec/xcodec_hash.h:32-164) of the 2048-byte window ending at p depends
+// only on the window's bytes.  With w = byte+1 and
+// f = ffs(byte):
+//   S1 = sum w_i,   S2 = sum (p+1-i) w_i        (same for f)   all mod 2^32
+//   bytes_hash = (S1w << 20) + S2w,  bits_hash = (S1f << 16) + S2f
+//   H = (uint64(bits_hash) << 36) + bytes_hash
+// so H.lo32 == bytes_hash and H.hi32 == bits_hash << 4.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define XC_SEG 2048u
+#define XC_MAGIC 0xF1u
+
+namespace xc {
+
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+// ---- DPP wave scans (gfx9 DPP: row_shr 1/2/4/8, row_bcast 15/31) ----------------
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ uint32_t dpp0(uint32_t x)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWMASK, 0xf, false);
+}
+
+// Inclusive prefix sum over the 64 lanes (mod 2^32).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)
+{
+    x += dpp0<0x111, 0xf>(x);  // row_shr:1
+    x += dpp0<0x112, 0xf>(x);  // row_shr:2
+    x += dpp0<0x114, 0xf>(x);  // row_shr:4
+    x += dpp0<0x118, 0xf>(x);  // row_shr:8
+    x += dpp0<0x142, 0xa>(x);  // row_bcast:15 -> rows 1,3
+    x += dpp0<0x143, 0xc>(x);  // row_bcast:31 -> rows 2,3
+    return x;
+}
+
+__device__ __forceinline__ uint32_t readlane(uint32_t x, int l)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, l);
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) { return readlane(wave_incl_scan(x), 63); }
+
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+
+// Number of set bits of m below this lane.
+__device__ __forceinline__ uint32_t mbcnt(uint64_t m)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ uint32_t uniform(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+
+// ---- byte helpers -------------------------------------------------------------
+__device__ __forceinline__ uint32_t ffs8(uint32_t b) { return b ? (uint32_t)__builtin_ctz(b) + 1u : 0u; }
+
+// 32 bytes at an arbitrary address as 8 little-endian dwords (aligned loads + alignbyte).
+__device__ __forceinline__ void load32_unaligned(const uint8_t *p, uint32_t out[8])
+{
+    uintptr_t a = (uintptr_t)p;
+    const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
+    uint32_t sh = (uint32_t)(a & 3);
+    uint32_t d[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) d[k] = w[k];
+#pragma unroll
+    for (int k = 0; k < 8; k++) out[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+}
+
+// Per-lane partial sums of 32 bytes at local offsets 0..31:
+//   A = sum w, B = sum j*w for w = byte+1   (and the same with f = ffs(byte))
+struct Sums4 {
+    uint32_t aw, bw, af, bf;
+};
+
+__device__ __forceinline__ Sums4 chunk_sums32(const uint32_t w[8])
+{
+    Sums4 s = {0, 0, 0, 0};
+    uint32_t sb = 0, jb = 0;
+#pragma unroll
+    for (int d = 0; d < 8; d++) {
+        // weights (4d, 4d+1, 4d+2, 4d+3) packed as bytes
+        const uint32_t wt = (uint32_t)(4 * d) * 0x01010101u + 0x03020100u;
+        sb = __builtin_amdgcn_udot4(w[d], 0x01010101u, sb, false);
+        jb = __builtin_amdgcn_udot4(w[d], wt, jb, false);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            uint32_t f = ffs8((w[d] >> (8 * k)) & 0xffu);
+            s.af += f;
+            s.bf += (uint32_t)(4 * d + k) * f;
+        }
+    }
+    s.aw = sb + 32u;         // sum (b+1)
+    s.bw = jb + 496u;        // sum j*(b+1), sum j = 496
+    return s;
+}
+
+// Full hash of the 2048 bytes at p (any alignment); every lane returns the result.
+__device__ __forceinline__ uint64_t wave_window_hash(const uint8_t *p)
+{
+    const uint32_t l = lane_id();
+    uint32_t w[8];
+    load32_unaligned(p + 32u * l, w);
+    Sums4 s = chunk_sums32(w);
+    const uint32_t k = XC_SEG - 32u * l;  // weight of this lane's byte 0 is (2048 - 32l)
+    uint32_t s1w = wave_sum(s.aw);
+    uint32_t s2w = wave_sum(k * s.aw - s.bw);
+    uint32_t s1f = wave_sum(s.af);
+    uint32_t s2f = wave_sum(k * s.af - s.bf);
+    uint32_t bytes_hash = (s1w << 20) + s2w;
+    uint32_t bits_hash = (s1f << 16) + s2f;
+    return ((uint64_t)bits_hash << 36) + (uint64_t)bytes_hash;
+}
+
+// 2048-byte equality of two windows (any alignment); wave-uniform result.
+__device__ __forceinline__ bool wave_equal2048(const uint8_t *a, const uint8_t *b)
+{
+    const uint32_t l = lane_id();
+    uint32_t x[8], y[8];
+    load32_unaligned(a + 32u * l, x);
+    load32_unaligned(b + 32u * l, y);
+    uint32_t diff = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) diff |= x[k] ^ y[k];
+    return ballot(diff != 0) == 0;
+}
+
+// Wave-cooperative copy of n bytes, any alignments.  Body uses 16-byte aligned stores;
+// head/tail bytes are single-byte stores (never a read-modify-write of a neighbour's word).
+__device__ __forceinline__ void wave_copy(uint8_t *dst, const uint8_t *src, uint32_t n)
+{
+    const uint32_t l = lane_id();
+    uintptr_t d = (uintptr_t)dst;
+    uint32_t head = (uint32_t)((16u - (d & 15u)) & 15u);
+    if (head > n) head = n;
+    if (l < head) dst[l] = src[l];
+    uint32_t body = (n - head) & ~15u;
+    for (uint32_t o = head + 16u * l; o < head + body; o += 1024u) {
+        const uint8_t *s = src + o;
+        uintptr_t a = (uintptr_t)s;
+        const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
+        uint32_t sh = (uint32_t)(a & 3);
+        uint32_t v0 = w[0], v1 = w[1], v2 = w[2], v3 = w[3], v4 = sh ? w[4] : 0u;
+        uint4 o4;
+        o4.x = __builtin_amdgcn_alignbyte(v1, v0, sh);
+        o4.y = __builtin_amdgcn_alignbyte(v2, v1, sh);
+        o4.z = __builtin_amdgcn_alignbyte(v3, v2, sh);
+        o4.w = __builtin_amdgcn_alignbyte(v4, v3, sh);
+        *(uint4 *)(dst + o) = o4;
+    }
+    uint32_t t0 = head + body;
+    if (t0 + l < n) dst[t0 + l] = src[t0 + l];
+}
+
+// ---- membership sets -------------------------------------------------------------
+// A set of 64-bit hashes: level-1 bitmap (LDS-loaded by the scan), exact lo32 set,
+// full-key table with a 64-bit value.  Used for the cache (value = segment index)
+// and for a batch's declarations (value = buffer<<32 | declaration position, min-wins).
+#define XC_FILT_LOG2 20u
+#define XC_FILT_WORDS (1u << (XC_FILT_LOG2 - 5u))  // 32768 words = 128 KB
+#define XC_EMPTY64 0xFFFFFFFFFFFFFFFFull           // H never has bits 32..35 set
+
+struct DevSet {
+    uint32_t *filt;     // XC_FILT_WORDS
+    uint32_t *lo_keys;  // lo32 set (0 = empty; a zero key is flagged in *lo_zero)
+    uint32_t *lo_zero;
+    uint32_t lo_mask;
+    uint32_t mask;      // full table
+    uint64_t *keys;
+    uint64_t *vals;
+};
+
+__device__ __forceinline__ uint32_t filt_bit(uint32_t lo) { return lo >> (32u - XC_FILT_LOG2); }
+__device__ __forceinline__ uint32_t lo_slot(uint32_t lo, uint32_t mask) { return (lo * 0x9E3779B1u) >> 7 & mask; }
+__device__ __forceinline__ uint32_t key_slot(uint64_t h, uint32_t mask)
+{
+    uint32_t lo = (uint32_t)h, hi = (uint32_t)(h >> 32);
+    return ((lo * 0x9E3779B1u) ^ (hi * 0x85EBCA6Bu)) >> 5 & mask;
+}
+
+__device__ __forceinline__ bool set_has_lo(const DevSet &s, uint32_t lo)
+{
+    if (lo == 0u) return *s.lo_zero != 0u;
+    uint32_t i = lo_slot(lo, s.lo_mask);
+    for (;;) {
+        uint32_t k = s.lo_keys[i];
+        if (k == lo) return true;
+        if (k == 0u) return false;
+        i = (i + 1u) & s.lo_mask;
+    }
+}
+
+// Returns true and *val if present.
+__device__ __forceinline__ bool set_find(const DevSet &s, uint64_t h, uint64_t *val)
+{
+    uint32_t i = key_slot(h, s.mask);
+    for (;;) {
+        uint64_t k = s.keys[i];
+        if (k == h) { *val = s.vals[i]; return true; }
+        if (k == XC_EMPTY64) return false;
+        i = (i + 1u) & s.mask;
+    }
+}
+
+// Insert (h, val).  Returns 1 if newly inserted, 0 if h was present.  With min_merge the
+// value is atomicMin-merged (vals must start at ~0); otherwise a fresh value is stored.
+// *slot_out / *lo_slot_out receive the full-table slot and the newly used lo32 slot
+// (NONE when the lo32 key was already present) for undo logs.
+__device__ __forceinline__ int set_insert(const DevSet &s, uint64_t h, uint64_t val, bool min_merge,
+                                          uint32_t *slot_out, uint32_t *lo_slot_out)
+{
+    uint32_t i = key_slot(h, s.mask);
+    int fresh = 0;
+    for (;;) {
+        uint64_t prev = atomicCAS((unsigned long long *)&s.keys[i], (unsigned long long)XC_EMPTY64,
+                                  (unsigned long long)h);
+        if (prev == XC_EMPTY64) { fresh = 1; break; }
+        if (prev == h) break;
+        i = (i + 1u) & s.mask;
+    }
+    if (min_merge) atomicMin((unsigned long long *)&s.vals[i], (unsigned long long)val);
+    else if (fresh) s.vals[i] = val;
+    if (slot_out) *slot_out = i;
+    uint32_t los = 0xFFFFFFFFu;
+    if (fresh) {
+        uint32_t lo = (uint32_t)h;
+        if (lo == 0u) atomicOr(s.lo_zero, 1u);
+        else {
+            uint32_t j = lo_slot(lo, s.lo_mask);
+            for (;;) {
+                uint32_t prev = atomicCAS(&s.lo_keys[j], 0u, lo);
+                if (prev == 0u) { los = j; break; }
+                if (prev == lo) break;
+                j = (j + 1u) & s.lo_mask;
+            }
+        }
+        uint32_t b = filt_bit(lo);
+        atomicOr(&s.filt[b >> 5], 1u << (b & 31u));
+    }
+    if (lo_slot_out) *lo_slot_out = los;
+    return fresh;
+}
+
+}  // namespace xc

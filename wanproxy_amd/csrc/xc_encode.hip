@@ -1,0 +1,689 @@
+// xc_encode.hip — XCodec batch encoder kernels for gfx950 (CDNA4).
+//
+// Reference path: XCodecEncoder::encode/flush (xcodec/xcodec_encoder.cc:60-260) over a
+// shared XCodecMemoryCache (xcodec/xcodec_cache.h:162-211).  DESIGN.md explains the
+// pipeline; in short, per sub-batch of buffers:
+//
+//   k_scan(S)     every window end p: lo32 of H(p) by the rolling recurrence, level-1 LDS
+//                 bitmap, exact lo32 probe -> sparse/dense event layer S (cache hits)
+//   k_resolve(S)  per event: full 64-bit H, cache probe, 2048-byte compare -> EQUAL / COLL
+//   k_walk        per buffer: the sequential candidate/declare/reference state machine
+//                 (xcodec_encoder.cc:77-170) over the sparse events -> tokens
+//   k_declhash    per EXTRACT: H(segment) (xcodec_hash.h:166-174); declaration set D
+//   k_scan(D), k_resolve(D), k_walk, k_declhash  until D stops growing (self references)
+//   k_emit        tokens -> F1-escaped wire bytes; EXTRACT payloads entered in the cache
+//
+// Buffers are processed as if in index order against one cache: a buffer whose lookups
+// would have hit an earlier buffer's new declaration is detected (first_cross) and the
+// host re-runs the batch from that buffer after committing everything before it.
+#include "xc_kernels.h"
+
+namespace xc {
+
+// ---------------------------------------------------------------- k_scan ----------------
+
+__device__ __forceinline__ void scan_record(const ScanArgs &a, uint32_t c, uint32_t c0, bool match, uint32_t pos,
+                                            uint32_t &ev_n, bool &dense)
+{
+    uint64_t m = ballot(match);
+    if (!m) return;
+    const uint32_t k = (uint32_t)__popcll(m);
+    const uint32_t W = a.P.chunk_len / 32u;
+    if (!dense && ev_n + k <= EV_CAP) {
+        if (match) a.L.pos[c * EV_CAP + ev_n + mbcnt(m)] = pos;
+        ev_n += k;
+        return;
+    }
+    if (!dense) {
+        dense = true;
+        uint32_t *bits = a.L.bits + (size_t)c * W;
+        for (uint32_t i = lane_id(); i < W; i += 64u) bits[i] = 0u;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        for (uint32_t i = lane_id(); i < ev_n; i += 64u) {
+            uint32_t q = a.L.pos[c * EV_CAP + i] - c0;
+            atomicOr(&bits[q >> 5], 1u << (q & 31u));
+        }
+    }
+    if (match) {
+        uint32_t q = pos - c0;
+        atomicOr(&a.L.bits[(size_t)c * W + (q >> 5)], 1u << (q & 31u));
+    }
+}
+
+__device__ __forceinline__ void scan_flush(const ScanArgs &a, uint2 *queue, uint32_t &qn, uint32_t c, uint32_t c0,
+                                           uint32_t &ev_n, bool &dense)
+{
+    for (uint32_t r = 0; r < qn; r += 64u) {
+        const uint32_t i = r + lane_id();
+        bool match = false;
+        uint32_t pos = 0;
+        if (i < qn) {
+            uint2 e = queue[i];
+            pos = e.x;
+            match = set_has_lo(a.set, e.y);
+        }
+        scan_record(a, c, c0, match, pos, ev_n, dense);
+    }
+    qn = 0;
+}
+
+// Exclusive-scan helpers for the per-lane chunk sums of one 2048-byte block.
+struct BlockSums {
+    uint32_t preA, preC, totA, totC;
+};
+
+__device__ __forceinline__ BlockSums block_sums(const uint32_t w[8], uint32_t l)
+{
+    uint32_t sb = 0, jb = 0;
+#pragma unroll
+    for (int d = 0; d < 8; d++) {
+        const uint32_t wt = (uint32_t)(4 * d) * 0x01010101u + 0x03020100u;
+        sb = __builtin_amdgcn_udot4(w[d], 0x01010101u, sb, false);
+        jb = __builtin_amdgcn_udot4(w[d], wt, jb, false);
+    }
+    const uint32_t A = sb + 32u;               // sum (b+1) over the lane's 32 bytes
+    const uint32_t C = 32u * l * A + jb + 496u; // 32*l*A + sum j*(b+1)
+    const uint32_t ia = wave_incl_scan(A), ic = wave_incl_scan(C);
+    BlockSums s;
+    s.totA = readlane(ia, 63);
+    s.totC = readlane(ic, 63);
+    s.preA = ia - A;
+    s.preC = ic - C;
+    return s;
+}
+
+__device__ __forceinline__ void load32_aligned(const uint8_t *p, uint32_t w[8])
+{
+    const uint4 *q = (const uint4 *)p;
+    uint4 x = q[0], y = q[1];
+    w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w;
+    w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
+}
+
+__global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
+{
+    extern __shared__ uint32_t smem[];
+    uint32_t *filt = smem;
+    const uint32_t wave = threadIdx.x >> 6;
+    uint2 *queue = (uint2 *)(smem + XC_FILT_WORDS) + wave * Q_CAP;
+    const uint32_t l = lane_id();
+
+    for (uint32_t i = threadIdx.x * 4u; i < XC_FILT_WORDS; i += 4096u)
+        *(uint4 *)(filt + i) = *(const uint4 *)(a.set.filt + i);
+    __syncthreads();
+
+    for (uint32_t c = a.ck_lo + blockIdx.x * SCAN_WAVES + wave; c < a.ck_hi; c += gridDim.x * SCAN_WAVES) {
+        const uint2 ck = a.P.chunks[c];
+        const uint32_t b = ck.x, c0 = ck.y;
+        const uint32_t len = a.P.buf_len[b];
+        const uint8_t *base = a.P.in + a.P.buf_off[b];
+        const uint32_t c1 = min(c0 + a.P.chunk_len, len);
+        uint32_t ev_n = 0, qn = 0;
+        bool dense = false;
+
+        uint32_t pw[8];
+        BlockSums ps;
+        uint32_t s;
+        if (c0 == 0) {
+            load32_aligned(base + 32u * l, pw);
+            ps = block_sums(pw, l);
+            if (len >= XC_SEG) {
+                // window ending at 2047 = the whole first block
+                const uint32_t lo = (ps.totA << 20) + (XC_SEG * ps.totA - ps.totC);
+                const uint32_t bit = filt_bit(lo);
+                const bool t = (filt[bit >> 5] >> (bit & 31u)) & 1u;
+                if (t && l == 0) queue[0] = make_uint2(XC_SEG - 1u, lo);
+                qn = t ? 1u : 0u;
+            }
+            s = XC_SEG;
+        } else {
+            load32_aligned(base + c0 - XC_SEG + 32u * l, pw);
+            ps = block_sums(pw, l);
+            s = c0;
+        }
+
+        for (; s < c1; s += XC_SEG) {
+            uint32_t w[8];
+            load32_aligned(base + s + 32u * l, w);
+            const BlockSums cs = block_sums(w, l);
+            // window ending just before this lane's first position q = s + 32 l:
+            // out-chunks of lanes >= l (previous block) + in-chunks of lanes < l.
+            const uint32_t sufA = ps.totA - ps.preA, sufC = ps.totC - ps.preC;
+            const uint32_t S1 = sufA + cs.preA;
+            const uint32_t S2 = (XC_SEG + 32u * l) * sufA - sufC + 32u * l * cs.preA - cs.preC;
+            uint32_t U = S1 - XC_SEG;          // S1 - 2048
+            uint32_t V = S2 + 0x80000000u;     // S2 + (2048 << 20)
+            const uint32_t q = s + 32u * l;
+            const uint32_t vmask = (q + 32u <= c1) ? 0xFFFFFFFFu : (q >= c1 ? 0u : ((1u << (c1 - q)) - 1u));
+            // two halves of 16 positions keep the live lo32 values at 16 VGPRs
+#pragma unroll
+            for (int half = 0; half < 2; half++) {
+                uint32_t lo[16];
+                uint32_t hit = 0;
+#pragma unroll
+                for (int d = 0; d < 4; d++) {
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        const uint32_t ib = (w[half * 4 + d] >> (8 * k)) & 0xffu;
+                        const uint32_t ob = (pw[half * 4 + d] >> (8 * k)) & 0xffu;
+                        U += ib - ob;
+                        V += U - (ob << 11);
+                        const uint32_t x = (U << 20) + V;
+                        lo[d * 4 + k] = x;
+                        const uint32_t bit = filt_bit(x);
+                        hit |= ((filt[bit >> 5] >> (bit & 31u)) & 1u) << (d * 4 + k);
+                    }
+                }
+                hit &= vmask >> (16 * half);
+#pragma unroll
+                for (int j = 0; j < 16; j++) {
+                    const bool t = (hit >> j) & 1u;
+                    const uint64_t m = ballot(t);
+                    if (m) {
+                        if (t) queue[qn + mbcnt(m)] = make_uint2(q + (uint32_t)(16 * half + j), lo[j]);
+                        qn += (uint32_t)__popcll(m);
+                        if (qn > Q_CAP - 64u) scan_flush(a, queue, qn, c, c0, ev_n, dense);
+                    }
+                }
+            }
+#pragma unroll
+            for (int d = 0; d < 8; d++) pw[d] = w[d];
+            ps = cs;
+        }
+        if (qn) scan_flush(a, queue, qn, c, c0, ev_n, dense);
+        if (l == 0) {
+            a.L.cnt[c] = dense ? (EV_DENSE | ev_n) : ev_n;
+            if (dense) atomicAdd(&a.P.ctl[CTL_DENSE], 1u);
+        }
+    }
+}
+
+// ------------------------------------------------------------- k_resolve ----------------
+// One wave per chunk: sort the sparse list, then resolve every event exactly.
+
+__device__ __forceinline__ uint32_t resolve_one(const PlanDev &P, int dmode, const uint8_t *win, uint64_t *h_out,
+                                                uint64_t *val_out)
+{
+    const uint64_t h = wave_window_hash(win);
+    *h_out = h;
+    uint64_t v = 0;
+    if (!dmode) {
+        if (!set_find(P.cache, h, &v)) { *val_out = 0; return ST_MISS; }
+        *val_out = v;
+        return wave_equal2048(win, P.segs + v * XC_SEG) ? ST_EQUAL : ST_COLL;
+    }
+    if (!set_find(P.dset, h, &v)) { *val_out = 0; return ST_MISS; }
+    *val_out = v;
+    return ST_MATCH;
+}
+
+__global__ __launch_bounds__(256) void k_resolve(ResolveArgs a)
+{
+    const uint32_t c = a.ck_lo + blockIdx.x * 4u + (threadIdx.x >> 6);
+    if (c >= a.ck_hi) return;
+    const uint32_t cnt = a.L.cnt[c];
+    if (cnt == 0 || (cnt & EV_DENSE)) return;
+    const uint32_t l = lane_id();
+    const uint2 ck = a.P.chunks[c];
+    const uint8_t *base = a.P.in + a.P.buf_off[ck.x];
+    uint32_t p = l < cnt ? a.L.pos[c * EV_CAP + l] : NONE;
+    uint32_t rank = 0;
+    for (uint32_t k = 0; k < cnt; k++) rank += readlane(p, (int)k) < p ? 1u : 0u;
+    for (uint32_t k = 0; k < cnt; k++) {
+        const uint64_t m = ballot(rank == k && l < cnt);
+        const uint32_t q = readlane(p, (int)__ffsll((unsigned long long)m) - 1);
+        uint64_t h, v;
+        const uint32_t st = resolve_one(a.P, a.dmode, base + q - (XC_SEG - 1u), &h, &v);
+        if (l == 0) {
+            a.L.pos[c * EV_CAP + k] = q;
+            a.L.stat[c * EV_CAP + k] = st;
+            a.L.h[c * EV_CAP + k] = h;
+            a.L.val[c * EV_CAP + k] = v;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- k_walk ----------------
+struct Cursor {
+    uint32_t k, i;
+};
+
+// First set bit at chunk offset >= from, or NONE.
+__device__ __forceinline__ uint32_t dense_find(const uint32_t *bits, uint32_t from, uint32_t W)
+{
+    const uint32_t l = lane_id();
+    for (uint32_t w0 = from >> 5; w0 < W; w0 += 64u) {
+        const uint32_t wi = w0 + l;
+        uint32_t v = wi < W ? bits[wi] : 0u;
+        if (wi == (from >> 5)) v &= ~0u << (from & 31u);
+        if (wi < (from >> 5)) v = 0u;
+        const uint64_t m = ballot(v != 0u);
+        if (m) {
+            const int f = __ffsll((unsigned long long)m) - 1;
+            const uint32_t vv = readlane(v, f);
+            return (w0 + (uint32_t)f) * 32u + (uint32_t)(__builtin_ctz(vv));
+        }
+    }
+    return NONE;
+}
+
+// Next event position >= p in layer L for the chunks [cur.k, ck1) of one buffer.
+__device__ __forceinline__ uint32_t next_event(const PlanDev &P, const Layer &L, Cursor &cur, uint32_t ck1,
+                                               uint32_t p)
+{
+    const uint32_t W = P.chunk_len / 32u;
+    while (cur.k < ck1) {
+        const uint32_t cnt = uniform(L.cnt[cur.k]);
+        const uint32_t cs = uniform(P.chunks[cur.k].y);
+        if (cnt & EV_DENSE) {
+            const uint32_t from = p > cs ? p - cs : 0u;
+            if (from < P.chunk_len) {
+                const uint32_t r = dense_find(L.bits + (size_t)cur.k * W, from, W);
+                if (r != NONE) return cs + r;
+            }
+        } else {
+            while (cur.i < cnt && uniform(L.pos[cur.k * EV_CAP + cur.i]) < p) cur.i++;
+            if (cur.i < cnt) return uniform(L.pos[cur.k * EV_CAP + cur.i]);
+        }
+        cur.k++;
+        cur.i = 0;
+    }
+    return NONE;
+}
+
+struct EvInfo {
+    uint32_t st;
+    uint64_t h, v;
+};
+
+// Event of layer L exactly at q (cursor already advanced to >= q by next_event), or st=NONE.
+__device__ __forceinline__ EvInfo event_at(const PlanDev &P, const Layer &L, Cursor &cur, uint32_t ck1, uint32_t q,
+                                           int dmode, const uint8_t *base)
+{
+    EvInfo e;
+    e.st = NONE;
+    e.h = 0;
+    e.v = 0;
+    if (next_event(P, L, cur, ck1, q) != q) return e;
+    const uint32_t cnt = uniform(L.cnt[cur.k]);
+    if (cnt & EV_DENSE) {
+        e.st = resolve_one(P, dmode, base + q - (XC_SEG - 1u), &e.h, &e.v);
+    } else {
+        const uint32_t idx = cur.k * EV_CAP + cur.i;
+        e.st = uniform(L.stat[idx]);
+        e.h = L.h[idx];
+        e.v = L.val[idx];
+        e.h = ((uint64_t)uniform((uint32_t)(e.h >> 32)) << 32) | uniform((uint32_t)e.h);
+        e.v = ((uint64_t)uniform((uint32_t)(e.v >> 32)) << 32) | uniform((uint32_t)e.v);
+    }
+    return e;
+}
+
+
+constexpr uint32_t R_MISS = 0, R_HIT = 1, R_COLL = 2;
+
+__global__ __launch_bounds__(64) void k_walk(WalkArgs a)
+{
+    __shared__ uint32_t d_cand[MAX_DECL];
+    __shared__ uint64_t d_hash[MAX_DECL];
+    __shared__ uint32_t d_known[MAX_DECL];
+    const PlanDev &P = a.P;
+    const uint32_t b = a.j0 + blockIdx.x;
+    if (b >= a.j1) return;
+    const uint32_t l = lane_id();
+    const uint32_t len = P.buf_len[b];
+    const uint8_t *base = P.in + P.buf_off[b];
+    const uint32_t ck0 = P.buf_chunk0[b], ck1 = P.buf_chunk0[b + 1];
+    const uint32_t tb = P.tok_base[b];
+    const uint32_t tcap = 2u * (len / XC_SEG) + 3u;
+    Cursor cs = {ck0, 0}, cd = {ck0, 0};
+    uint32_t ntok = 0, nd = 0;
+    uint32_t basep = 0;
+    int cand = -1;
+    uint64_t cand_h = 0;
+    uint32_t cand_known = 0;
+    uint32_t p = XC_SEG - 1u;
+    bool cross = false;
+
+    auto emit = [&](uint32_t op, uint32_t lb, uint32_t le, uint32_t seg, uint32_t dpos, uint64_t h) {
+        if (ntok < tcap && l == 0) {
+            P.tok_op[tb + ntok] = op;
+            P.tok_lb[tb + ntok] = lb;
+            P.tok_le[tb + ntok] = le;
+            P.tok_seg[tb + ntok] = seg;
+            P.tok_dpos[tb + ntok] = dpos;
+            P.tok_h[tb + ntok] = h;
+        }
+        ntok++;
+    };
+
+    // Lookup at q (xcodec_encoder.cc:89-118 + xcodec_cache.h:190-210): the cache as of the
+    // batch start (layer S) or a segment this buffer declared earlier (layer D).
+    auto lookup = [&](uint32_t q, uint64_t *hout) -> uint32_t {
+        EvInfo s = event_at(P, P.S, cs, ck1, q, 0, base);
+        if (s.st == ST_EQUAL) { *hout = s.h; return R_HIT; }
+        if (s.st == ST_COLL) return R_COLL;
+        if (!a.use_d) return R_MISS;
+        EvInfo d = event_at(P, P.D, cd, ck1, q, 1, base);
+        if (d.st != ST_MATCH) return R_MISS;
+        for (uint32_t i = 0; i < nd; i++) {
+            if (d_known[i] && d_hash[i] == d.h) {
+                *hout = d.h;
+                return wave_equal2048(base + q - (XC_SEG - 1u), base + d_cand[i]) ? R_HIT : R_COLL;
+            }
+        }
+        if ((uint32_t)(d.v >> 32) < b) cross = true;  // an earlier buffer declared it
+        return R_MISS;
+    };
+
+    while (p < len) {
+        if (cand < 0) {
+            uint64_t h = 0;
+            const uint32_t r = lookup(p, &h);
+            if (r == R_HIT) {
+                emit(OP_REF, basep, p - (XC_SEG - 1u), p - (XC_SEG - 1u), 0, h);
+                basep = p + 1u;
+                p = basep + (XC_SEG - 1u);
+                continue;
+            }
+            if (r == R_COLL) { p++; continue; }
+            cand = (int)(p - (XC_SEG - 1u));
+            cand_known = 0;
+            cand_h = 0;
+            if (a.use_d) {
+                EvInfo d = event_at(P, P.D, cd, ck1, p, 1, base);
+                if (d.st == ST_MATCH) { cand_known = 1; cand_h = d.h; }
+            }
+            p++;
+            continue;
+        }
+        const uint32_t dp = (uint32_t)cand + 2u * XC_SEG - 1u;
+        uint32_t e = next_event(P, P.S, cs, ck1, p);
+        if (a.use_d) e = min(e, next_event(P, P.D, cd, ck1, p));
+        if (e < dp && e < len) {
+            uint64_t h = 0;
+            const uint32_t r = lookup(e, &h);
+            if (r == R_HIT) {
+                emit(OP_REF, basep, e - (XC_SEG - 1u), e - (XC_SEG - 1u), 0, h);
+                basep = e + 1u;
+                cand = -1;
+                p = basep + (XC_SEG - 1u);
+            } else {
+                p = e + 1u;
+            }
+            continue;
+        }
+        if (dp >= len) break;
+        // declaration (xcodec_encoder.cc:77-82, 203-215)
+        emit(OP_EXTRACT, basep, (uint32_t)cand, (uint32_t)cand, dp, cand_h);
+        if (nd < MAX_DECL) {
+            if (l == 0) {
+                d_cand[nd] = (uint32_t)cand;
+                d_hash[nd] = cand_h;
+                d_known[nd] = cand_known;
+            }
+            nd++;
+        }
+        basep = (uint32_t)cand + XC_SEG;
+        cand = -1;
+        p = dp;
+    }
+    // flush (xcodec_encoder.cc:175-201)
+    if (cand >= 0) {
+        emit(OP_EXTRACT, basep, (uint32_t)cand, (uint32_t)cand, DPOS_FLUSH, cand_h);
+        basep = (uint32_t)cand + XC_SEG;
+    }
+    emit(OP_END, basep, len, 0, 0, 0);
+    if (l == 0) {
+        P.tok_cnt[b] = ntok;
+        if (ntok > tcap) atomicOr(&P.ctl[CTL_ERROR], ERR_TOKENS);
+        if (cross) atomicMin(&P.ctl[CTL_FIRST_CROSS], b);
+    }
+}
+
+// ------------------------------------------------------------ k_declhash ----------------
+// grid (buffers, 8): wave y of buffer b hashes EXTRACT tokens y, y+8, ... and enters them
+// into the declaration set (value = b<<32 | declaration position, min-merged).
+
+__global__ __launch_bounds__(64) void k_declhash(DeclArgs a)
+{
+    const PlanDev &P = a.P;
+    const uint32_t b = a.j0 + blockIdx.x;
+    if (b >= a.j1) return;
+    const uint8_t *base = P.in + P.buf_off[b];
+    const uint32_t tb = P.tok_base[b], n = P.tok_cnt[b];
+    for (uint32_t t = blockIdx.y; t < n; t += gridDim.y) {
+        if (uniform(P.tok_op[tb + t]) != OP_EXTRACT) continue;
+        const uint32_t seg = uniform(P.tok_seg[tb + t]);
+        const uint64_t h = wave_window_hash(base + seg);
+        if (lane_id() == 0) {
+            P.tok_h[tb + t] = h;
+            const uint64_t v = ((uint64_t)b << 32) | P.tok_dpos[tb + t];
+            if (set_insert(P.dset, h, v, true, nullptr, nullptr)) atomicOr(&P.ctl[CTL_GREW], 1u);
+        }
+    }
+}
+
+// -------------------------------------------------------------- k_emit ------------------
+// One workgroup (4 waves) per buffer in [j0, j1): token sizes, offsets, wire bytes; every
+// EXTRACT payload is entered in the cache (xcodec_encoder.cc:203-215).
+
+constexpr uint32_t MAX_TOK = 2u * (MAX_BUF / XC_SEG) + 3u;
+
+__device__ __forceinline__ uint32_t count_magic(const uint8_t *p, uint32_t n)
+{
+    uint32_t c = 0;
+    for (uint32_t o = 4u * lane_id(); o < n; o += 256u) {
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++)
+            if (o + k < n) c += p[o + k] == XC_MAGIC ? 1u : 0u;
+    }
+    return wave_sum(c);
+}
+
+// encode_escape (xcodec_encoder.cc:217-239): bytes, with F1 -> F1 00.  Returns bytes written.
+__device__ __forceinline__ uint32_t write_escaped(uint8_t *dst, const uint8_t *p, uint32_t n)
+{
+    uint32_t o = 0;
+    for (uint32_t x = 0; x < n; x += 256u) {
+        const uint32_t s = x + 4u * lane_id();
+        uint32_t v[4], cnt = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            v[k] = (s + k < n) ? p[s + k] : 0x100u;
+            cnt += v[k] == 0x100u ? 0u : (v[k] == XC_MAGIC ? 2u : 1u);
+        }
+        const uint32_t inc = wave_incl_scan(cnt);
+        uint32_t q = o + inc - cnt;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            if (v[k] == 0x100u) continue;
+            dst[q++] = (uint8_t)v[k];
+            if (v[k] == XC_MAGIC) dst[q++] = 0;
+        }
+        o += readlane(inc, 63);
+    }
+    return o;
+}
+
+__global__ __launch_bounds__(256) void k_emit(EmitArgs a)
+{
+    __shared__ uint32_t sz[MAX_TOK];
+    const PlanDev &P = a.P;
+    const uint32_t b = a.j0 + blockIdx.x;
+    if (b >= a.j1) return;
+    const uint32_t wave = threadIdx.x >> 6, l = lane_id();
+    const uint8_t *base = P.in + P.buf_off[b];
+    uint8_t *out = P.out + P.out_off[b];
+    const uint32_t tb = P.tok_base[b], n = min(P.tok_cnt[b], MAX_TOK);
+
+    for (uint32_t t = wave; t < n; t += 4u) {
+        const uint32_t lb = P.tok_lb[tb + t], le = P.tok_le[tb + t], op = P.tok_op[tb + t];
+        const uint32_t esc = (le - lb) + count_magic(base + lb, le - lb);
+        if (l == 0) sz[t] = esc + (op == OP_EXTRACT ? 2u + XC_SEG : op == OP_REF ? 10u : 0u);
+    }
+    __syncthreads();
+    if (wave == 0) {
+        uint32_t carry = 0;
+        for (uint32_t t0 = 0; t0 < n; t0 += 64u) {
+            const uint32_t t = t0 + l;
+            const uint32_t v = t < n ? sz[t] : 0u;
+            const uint32_t inc = wave_incl_scan(v);
+            if (t < n) sz[t] = carry + inc - v;
+            carry += readlane(inc, 63);
+        }
+        if (l == 0) P.out_len[b] = carry;
+    }
+    __syncthreads();
+    uint32_t n_ext = 0, n_ref = 0;
+    for (uint32_t t = wave; t < n; t += 4u) {
+        const uint32_t lb = P.tok_lb[tb + t], le = P.tok_le[tb + t], op = P.tok_op[tb + t];
+        uint8_t *o = out + sz[t];
+        o += write_escaped(o, base + lb, le - lb);
+        if (op == OP_REF) {
+            const uint64_t h = P.tok_h[tb + t];
+            if (l < 10) o[l] = l == 0 ? (uint8_t)XC_MAGIC : l == 1 ? (uint8_t)OP_REF : (uint8_t)(h >> (8 * (9 - l)));
+            n_ref++;
+        } else if (op == OP_EXTRACT) {
+            const uint32_t seg = P.tok_seg[tb + t];
+            if (l == 0) { o[0] = (uint8_t)XC_MAGIC; o[1] = (uint8_t)OP_EXTRACT; }
+            wave_copy(o + 2, base + seg, XC_SEG);
+            // XCodecMemoryCache::enter (xcodec_cache.h:182-188)
+            uint32_t idx = 0;
+            if (l == 0) idx = atomicAdd(P.seg_count, 1u);
+            idx = readlane(idx, 0);
+            if (idx < P.seg_cap) {
+                wave_copy(P.segs + (size_t)idx * XC_SEG, base + seg, XC_SEG);
+                if (l == 0) {
+                    uint32_t s1, s2;
+                    set_insert(P.cache, P.tok_h[tb + t], idx, false, &s1, &s2);
+                    P.undo[idx] = make_uint2(s1, s2);
+                }
+            } else if (l == 0) {
+                atomicOr(&P.ctl[CTL_ERROR], ERR_CAPACITY);
+            }
+            n_ext++;
+        }
+    }
+    if (l == 0) {
+        if (n_ext) atomicAdd(&P.ctl[CTL_NEXTRACT], n_ext);
+        if (n_ref) atomicAdd(&P.ctl[CTL_NREF], n_ref);
+    }
+}
+
+// ------------------------------------------------------------ utilities -----------------
+__global__ __launch_bounds__(64) void k_hash_segments(const uint8_t *segs, uint64_t n, uint64_t *out)
+{
+    for (uint64_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const uint64_t h = wave_window_hash(segs + i * XC_SEG);
+        if (lane_id() == 0) out[i] = h;
+    }
+}
+
+// Plain per-position hashes (window ends p >= 2047) via the same block recurrence as k_scan.
+__global__ __launch_bounds__(64) void k_window_hashes(const uint8_t *in, uint32_t n, uint64_t *out)
+{
+    const uint32_t l = lane_id();
+    const uint32_t blk = blockIdx.x;  // window ends [2048*blk, 2048*blk + 2048)
+    const uint32_t s = blk * XC_SEG;
+    if (s >= n) return;
+    if (blk == 0) {
+        for (uint32_t i = l; i < min(n, XC_SEG - 1u); i += 64u) out[i] = 0;
+        if (n >= XC_SEG) {
+            const uint64_t h = wave_window_hash(in);
+            if (l == 0) out[XC_SEG - 1u] = h;
+        }
+        return;
+    }
+    // full hash at the lane's window ending q-1, then roll 32 positions (both components)
+    const uint32_t q = s + 32u * l;
+    uint32_t w[8], pw[8];
+    // padded reads are in bounds of the arena (caller pads by >= 64 bytes)
+    load32_unaligned(in + q, w);
+    load32_unaligned(in + q - XC_SEG, pw);
+    // window sums ending at q-1: recompute directly (2048 bytes per lane; test utility only)
+    uint32_t s1w = 0, s2w = 0, s1f = 0, s2f = 0;
+    for (uint32_t i = 0; i < XC_SEG; i++) {
+        const uint32_t by = in[q - XC_SEG + i];
+        s1w += by + 1u;
+        s2w += (XC_SEG - i) * (by + 1u);
+        const uint32_t f = ffs8(by);
+        s1f += f;
+        s2f += (XC_SEG - i) * f;
+    }
+#pragma unroll
+    for (int d = 0; d < 8; d++) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t ib = (w[d] >> (8 * k)) & 0xffu, ob = (pw[d] >> (8 * k)) & 0xffu;
+            const uint32_t fi = ffs8(ib), fo = ffs8(ob);
+            s1w += ib - ob;
+            s2w = s2w - XC_SEG * (ob + 1u) + s1w;
+            s1f += fi - fo;
+            s2f = s2f - XC_SEG * fo + s1f;
+            const uint32_t p = q + (uint32_t)(d * 4 + k);
+            if (p < n) {
+                const uint32_t bytes_hash = (s1w << 20) + s2w, bits_hash = (s1f << 16) + s2f;
+                out[p] = ((uint64_t)bits_hash << 36) + bytes_hash;
+            }
+        }
+    }
+}
+
+// Cache restore: clear every table slot entered after the snapshot.
+__global__ void k_undo(DevSet cache, const uint2 *undo, uint32_t from, uint32_t to)
+{
+    for (uint32_t i = from + blockIdx.x * blockDim.x + threadIdx.x; i < to; i += gridDim.x * blockDim.x) {
+        const uint2 u = undo[i];
+        cache.keys[u.x] = XC_EMPTY64;
+        if (u.y != NONE) cache.lo_keys[u.y] = 0u;
+    }
+}
+
+// Cache enter from the host API (single segment).
+__global__ void k_enter_one(PlanDev P, uint64_t h, const uint8_t *seg)
+{
+    if (uniform(P.seg_count[0]) >= P.seg_cap) {
+        if (lane_id() == 0) atomicOr(&P.ctl[CTL_ERROR], ERR_CAPACITY);
+        return;
+    }
+    uint64_t v;
+    if (set_find(P.cache, h, &v)) {  // release-build XCodecMemoryCache::enter overwrites
+        wave_copy(P.segs + v * XC_SEG, seg, XC_SEG);
+        return;
+    }
+    const uint32_t idx = uniform(P.seg_count[0]);
+    wave_copy(P.segs + (size_t)idx * XC_SEG, seg, XC_SEG);
+    if (lane_id() == 0) {
+        uint32_t s1, s2;
+        set_insert(P.cache, h, idx, false, &s1, &s2);
+        P.undo[idx] = make_uint2(s1, s2);
+        P.seg_count[0] = idx + 1u;
+    }
+}
+
+__global__ void k_lookup_one(PlanDev P, uint64_t h, uint8_t *out, uint32_t *found)
+{
+    uint64_t v;
+    if (set_find(P.cache, h, &v)) {
+        wave_copy(out, P.segs + v * XC_SEG, XC_SEG);
+        if (lane_id() == 0) *found = 1u;
+    } else if (lane_id() == 0) {
+        *found = 0u;
+    }
+}
+
+// Wave primitive self-test: scan against a serial loop, hash against the rolling form.
+__global__ void k_selftest(uint32_t *err)
+{
+    const uint32_t l = lane_id();
+    uint32_t x = l * 2654435761u + 12345u;
+    const uint32_t inc = wave_incl_scan(x);
+    uint32_t ref = 0;
+    for (uint32_t k = 0; k <= l; k++) ref += k * 2654435761u + 12345u;
+    if (inc != ref) atomicOr(err, 1u);
+    const uint64_t m = ballot((l & 3) == 1);
+    if (mbcnt(m) != (l + 2) / 4) atomicOr(err, 2u);
+}
+
+}  // namespace xc

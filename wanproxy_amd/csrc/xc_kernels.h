@@ -1,0 +1,115 @@
+// xc_kernels.h — device-side data layout shared by the encode/decode kernels and the host runtime.
+#pragma once
+#include <stdint.h>
+
+#include "xc_device.h"
+
+namespace xc {
+
+constexpr uint32_t EV_CAP = 32;          // sparse events per scan chunk before it turns dense
+constexpr uint32_t EV_DENSE = 0x80000000u;
+constexpr uint32_t Q_CAP = 128;          // per-wave LDS queue of level-1 filter positives
+constexpr uint32_t SCAN_WAVES = 16;      // waves per scan workgroup (1024 threads)
+constexpr uint32_t SCAN_LDS = XC_FILT_WORDS * 4u + SCAN_WAVES * Q_CAP * 8u;
+constexpr uint32_t MAX_BUF = 1u << 20;   // longest single buffer accepted (1 MiB)
+constexpr uint32_t MAX_DECL = MAX_BUF / XC_SEG + 2u;
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr uint32_t DPOS_FLUSH = 0xFFFFFFFEu;  // declared by flush()
+
+// event status (resolve / walk)
+constexpr uint32_t ST_MISS = 0;  // lo32 matched, full hash did not
+constexpr uint32_t ST_EQUAL = 1; // cache: hash present, bytes equal -> REF
+constexpr uint32_t ST_COLL = 2;  // cache: hash present, bytes differ -> collision
+constexpr uint32_t ST_MATCH = 3; // declaration set: hash present (val = buf<<32 | decl pos)
+
+// token ops
+constexpr uint32_t OP_END = 0, OP_EXTRACT = 1, OP_REF = 2;
+
+// ctl words
+enum : uint32_t {
+    CTL_GREW = 0,
+    CTL_FIRST_CROSS = 1,
+    CTL_ERROR = 2,
+    CTL_DENSE = 3,
+    CTL_NEXTRACT = 4,
+    CTL_NREF = 5,
+    CTL_UNDO = 6,
+    CTL_WORDS = 16
+};
+constexpr uint32_t ERR_CAPACITY = 1, ERR_TOKENS = 2, ERR_DECLS = 4;
+
+// One scan layer: per chunk a sorted sparse list (cnt < EV_CAP) or a dense bitmask.
+struct Layer {
+    uint32_t *cnt;   // [nchunks]  count | EV_DENSE
+    uint32_t *pos;   // [nchunks * EV_CAP]  positions (relative to the buffer)
+    uint32_t *stat;  // [nchunks * EV_CAP]
+    uint64_t *h;     // [nchunks * EV_CAP]  full hash (resolved)
+    uint64_t *val;   // [nchunks * EV_CAP]  table value (resolved)
+    uint32_t *bits;  // [nchunks * chunk_len/32]
+};
+
+struct PlanDev {
+    const uint8_t *in;
+    const uint64_t *buf_off;
+    const uint32_t *buf_len;
+    uint32_t nb;
+    const uint2 *chunks;       // (buffer, first position) per chunk
+    const uint32_t *buf_chunk0;  // [nb+1]
+    uint32_t chunk_len;
+    Layer S, D;
+    DevSet cache;
+    uint8_t *segs;
+    uint32_t *seg_count;
+    uint32_t seg_cap;
+    uint2 *undo;               // [seg_cap] (full slot, lo slot) of every enter()
+    DevSet dset;
+    const uint32_t *tok_base;  // [nb]
+    uint32_t *tok_cnt;
+    uint32_t *tok_lb, *tok_le, *tok_seg, *tok_op, *tok_dpos;
+    uint64_t *tok_h;
+    uint8_t *out;
+    const uint64_t *out_off;
+    uint64_t *out_len;
+    uint32_t *ctl;
+};
+
+// kernel argument blocks (shared by xc_encode.hip and xc_runtime.hip)
+struct ScanArgs {
+    PlanDev P;
+    Layer L;
+    DevSet set;
+    uint32_t ck_lo, ck_hi;
+};
+struct ResolveArgs {
+    PlanDev P;
+    Layer L;
+    int dmode;  // 0: cache layer, 1: declaration layer
+    uint32_t ck_lo, ck_hi;
+};
+struct WalkArgs {
+    PlanDev P;
+    uint32_t j0, j1;
+    int use_d;  // 0 on the first round (no declaration layer yet)
+};
+struct DeclArgs {
+    PlanDev P;
+    uint32_t j0, j1;
+};
+struct EmitArgs {
+    PlanDev P;
+    uint32_t j0, j1;
+};
+
+__global__ void k_scan(ScanArgs a);
+__global__ void k_resolve(ResolveArgs a);
+__global__ void k_walk(WalkArgs a);
+__global__ void k_declhash(DeclArgs a);
+__global__ void k_emit(EmitArgs a);
+__global__ void k_hash_segments(const uint8_t *segs, uint64_t n, uint64_t *out);
+__global__ void k_window_hashes(const uint8_t *in, uint32_t n, uint64_t *out);
+__global__ void k_undo(DevSet cache, const uint2 *undo, uint32_t from, uint32_t to);
+__global__ void k_enter_one(PlanDev P, uint64_t h, const uint8_t *seg);
+__global__ void k_lookup_one(PlanDev P, uint64_t h, uint8_t *out, uint32_t *found);
+__global__ void k_selftest(uint32_t *err);
+
+}  // namespace xc

@@ -1,0 +1,701 @@
+// xc_runtime.hip — host runtime behind include/xcodec_hip.h.
+//
+// Owns device contexts, the device-resident segment cache (XCodecMemoryCache,
+// xcodec/xcodec_cache.h:162-211) and batch plans, and sequences the encode pipeline of
+// xc_encode.hip.  The reference's order semantics (one cache shared by buffers fed in
+// index order, xcodec/xcodec_filter.cc:146-157) are kept by committing a batch prefix
+// only after every buffer in it is known not to depend on an earlier buffer's new
+// declarations (see DESIGN.md "Sequential semantics").
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/xcodec_hip.h"
+#include "xc_kernels.h"
+
+
+using namespace xc;
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string &msg)
+{
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(x)                                                                           \
+    do {                                                                                    \
+        hipError_t e_ = (x);                                                                \
+        if (e_ != hipSuccess)                                                               \
+            return fail(XC_EDEVICE, std::string(#x) + ": " + hipGetErrorString(e_));       \
+    } while (0)
+
+extern "C" const char *xc_last_error(void) { return g_err.c_str(); }
+
+
+// ------------------------------------------------------------------ context ----------
+struct xc_ctx {
+    int dev;
+    hipStream_t stream;
+    int n_cu;
+    uint32_t *d_scratch;  // small device scratch (flags)
+    uint8_t *d_seg;       // one segment of device scratch
+};
+
+static int set_dev(xc_ctx *ctx)
+{
+    HIPCHK(hipSetDevice(ctx->dev));
+    return XC_OK;
+}
+
+extern "C" int xc_device_count(int *n)
+{
+    if (!n) return fail(XC_EINVAL, "null");
+    HIPCHK(hipGetDeviceCount(n));
+    return XC_OK;
+}
+
+extern "C" int xc_ctx_create(int dev, xc_ctx **out)
+{
+    if (!out) return fail(XC_EINVAL, "null");
+    int n = 0;
+    HIPCHK(hipGetDeviceCount(&n));
+    if (dev < 0 || dev >= n) return fail(XC_EINVAL, "no such device");
+    HIPCHK(hipSetDevice(dev));
+    xc_ctx *c = new xc_ctx();
+    c->dev = dev;
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, dev));
+    c->n_cu = prop.multiProcessorCount;
+    HIPCHK(hipMalloc(&c->d_scratch, 4096));
+    HIPCHK(hipMalloc(&c->d_seg, 4096));
+    HIPCHK(hipFuncSetAttribute((const void *)k_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)SCAN_LDS));
+    *out = c;
+    return XC_OK;
+}
+
+extern "C" int xc_ctx_destroy(xc_ctx *ctx)
+{
+    if (!ctx) return XC_OK;
+    hipSetDevice(ctx->dev);
+    hipStreamSynchronize(ctx->stream);
+    hipFree(ctx->d_scratch);
+    hipFree(ctx->d_seg);
+    hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return XC_OK;
+}
+
+extern "C" void *xc_ctx_stream(xc_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+
+extern "C" int xc_ctx_sync(xc_ctx *ctx)
+{
+    if (!ctx) return fail(XC_EINVAL, "null");
+    HIPCHK(hipSetDevice(ctx->dev));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return XC_OK;
+}
+
+// ------------------------------------------------------------------ sets ----------
+static uint32_t pow2_at_least(uint64_t x, uint32_t minimum)
+{
+    uint64_t p = minimum;
+    while (p < x) p <<= 1;
+    return (uint32_t)p;
+}
+
+struct HostSet {
+    DevSet d{};
+    uint32_t n_lo = 0, n_full = 0;
+    int alloc(uint64_t entries)
+    {
+        n_full = pow2_at_least(entries * 2, 1024);
+        n_lo = pow2_at_least(entries * 4, 1024);
+        if (n_full > (1u << 27) || n_lo > (1u << 25)) return fail(XC_EINVAL, "set too large");
+        HIPCHK(hipMalloc(&d.filt, XC_FILT_WORDS * 4));
+        HIPCHK(hipMalloc(&d.lo_keys, (size_t)n_lo * 4));
+        HIPCHK(hipMalloc(&d.lo_zero, 4));
+        HIPCHK(hipMalloc(&d.keys, (size_t)n_full * 8));
+        HIPCHK(hipMalloc(&d.vals, (size_t)n_full * 8));
+        d.lo_mask = n_lo - 1;
+        d.mask = n_full - 1;
+        return XC_OK;
+    }
+    int clear(hipStream_t s)
+    {
+        HIPCHK(hipMemsetAsync(d.filt, 0, XC_FILT_WORDS * 4, s));
+        HIPCHK(hipMemsetAsync(d.lo_keys, 0, (size_t)n_lo * 4, s));
+        HIPCHK(hipMemsetAsync(d.lo_zero, 0, 4, s));
+        HIPCHK(hipMemsetAsync(d.keys, 0xFF, (size_t)n_full * 8, s));
+        HIPCHK(hipMemsetAsync(d.vals, 0xFF, (size_t)n_full * 8, s));
+        return XC_OK;
+    }
+    void release()
+    {
+        hipFree(d.filt);
+        hipFree(d.lo_keys);
+        hipFree(d.lo_zero);
+        hipFree(d.keys);
+        hipFree(d.vals);
+        d = DevSet{};
+    }
+};
+
+// ------------------------------------------------------------------ cache ----------
+struct xc_cache {
+    xc_ctx *ctx;
+    uint64_t cap;
+    HostSet set;
+    uint8_t *segs;
+    uint32_t *count;   // device
+    uint2 *undo;       // device [cap]
+    uint32_t *ctl;     // device scratch ctl for single-op kernels
+    // snapshot
+    bool has_snap = false;
+    uint32_t snap_count = 0;
+    uint32_t *snap_filt = nullptr;
+    uint32_t *snap_lo_zero = nullptr;
+};
+
+static PlanDev cache_plandev(xc_cache *c)
+{
+    PlanDev P{};
+    P.cache = c->set.d;
+    P.segs = c->segs;
+    P.seg_count = c->count;
+    P.seg_cap = (uint32_t)c->cap;
+    P.undo = c->undo;
+    P.ctl = c->ctl;
+    return P;
+}
+
+extern "C" int xc_cache_create(xc_ctx *ctx, uint64_t cap, xc_cache **out)
+{
+    if (!ctx || !out || cap == 0 || cap > (1ull << 23)) return fail(XC_EINVAL, "bad cache capacity");
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    xc_cache *c = new xc_cache();
+    c->ctx = ctx;
+    c->cap = cap;
+    if ((rc = c->set.alloc(cap))) return rc;
+    HIPCHK(hipMalloc(&c->segs, (size_t)cap * XC_SEG + 4096));
+    HIPCHK(hipMalloc(&c->count, 4));
+    HIPCHK(hipMalloc(&c->undo, (size_t)cap * sizeof(uint2)));
+    HIPCHK(hipMalloc(&c->ctl, CTL_WORDS * 4));
+    HIPCHK(hipMalloc(&c->snap_filt, XC_FILT_WORDS * 4));
+    HIPCHK(hipMalloc(&c->snap_lo_zero, 4));
+    if ((rc = c->set.clear(ctx->stream))) return rc;
+    HIPCHK(hipMemsetAsync(c->count, 0, 4, ctx->stream));
+    HIPCHK(hipMemsetAsync(c->ctl, 0, CTL_WORDS * 4, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    *out = c;
+    return XC_OK;
+}
+
+extern "C" int xc_cache_destroy(xc_cache *c)
+{
+    if (!c) return XC_OK;
+    hipSetDevice(c->ctx->dev);
+    hipStreamSynchronize(c->ctx->stream);
+    c->set.release();
+    hipFree(c->segs);
+    hipFree(c->count);
+    hipFree(c->undo);
+    hipFree(c->ctl);
+    hipFree(c->snap_filt);
+    hipFree(c->snap_lo_zero);
+    delete c;
+    return XC_OK;
+}
+
+static int cache_count_host(xc_cache *c, uint32_t *n)
+{
+    HIPCHK(hipMemcpyAsync(n, c->count, 4, hipMemcpyDeviceToHost, c->ctx->stream));
+    HIPCHK(hipStreamSynchronize(c->ctx->stream));
+    return XC_OK;
+}
+
+extern "C" int xc_cache_count(xc_cache *c, uint64_t *n)
+{
+    if (!c || !n) return fail(XC_EINVAL, "null");
+    int rc = set_dev(c->ctx);
+    if (rc) return rc;
+    uint32_t v = 0;
+    if ((rc = cache_count_host(c, &v))) return rc;
+    *n = std::min<uint64_t>(v, c->cap);
+    return XC_OK;
+}
+
+extern "C" int xc_cache_snapshot(xc_cache *c)
+{
+    if (!c) return fail(XC_EINVAL, "null");
+    int rc = set_dev(c->ctx);
+    if (rc) return rc;
+    if ((rc = cache_count_host(c, &c->snap_count))) return rc;
+    hipStream_t s = c->ctx->stream;
+    HIPCHK(hipMemcpyAsync(c->snap_filt, c->set.d.filt, XC_FILT_WORDS * 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->snap_lo_zero, c->set.d.lo_zero, 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+    c->has_snap = true;
+    return XC_OK;
+}
+
+// Enqueue the restore on the context stream (no host sync): for timed loops.
+static int cache_restore_async(xc_cache *c, uint32_t cur_count)
+{
+    hipStream_t s = c->ctx->stream;
+    uint32_t to = std::min<uint32_t>(cur_count, (uint32_t)c->cap);
+    if (to > c->snap_count) {
+        uint32_t n = to - c->snap_count;
+        uint32_t blocks = std::min<uint32_t>((n + 255) / 256, 4096);
+        hipLaunchKernelGGL(k_undo, dim3(blocks), dim3(256), 0, s, c->set.d, (const uint2 *)c->undo,
+                           c->snap_count, to);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipMemcpyAsync(c->set.d.filt, c->snap_filt, XC_FILT_WORDS * 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->set.d.lo_zero, c->snap_lo_zero, 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->count, &c->snap_count, 4, hipMemcpyHostToDevice, s));
+    return XC_OK;
+}
+
+extern "C" int xc_cache_restore(xc_cache *c)
+{
+    if (!c) return fail(XC_EINVAL, "null");
+    if (!c->has_snap) return fail(XC_EINVAL, "no snapshot");
+    int rc = set_dev(c->ctx);
+    if (rc) return rc;
+    uint32_t cur = 0;
+    if ((rc = cache_count_host(c, &cur))) return rc;
+    if ((rc = cache_restore_async(c, cur))) return rc;
+    HIPCHK(hipStreamSynchronize(c->ctx->stream));
+    return XC_OK;
+}
+
+extern "C" int xc_cache_lookup(xc_cache *c, uint64_t h, uint8_t *out, int *found)
+{
+    if (!c || !out || !found) return fail(XC_EINVAL, "null");
+    int rc = set_dev(c->ctx);
+    if (rc) return rc;
+    hipStream_t s = c->ctx->stream;
+    uint32_t *d_found = c->ctx->d_scratch;
+    hipLaunchKernelGGL(k_lookup_one, dim3(1), dim3(64), 0, s, cache_plandev(c), h, c->ctx->d_seg, d_found);
+    HIPCHK(hipGetLastError());
+    uint32_t f = 0;
+    HIPCHK(hipMemcpyAsync(&f, d_found, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(out, c->ctx->d_seg, XC_SEG, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    *found = (int)f;
+    return XC_OK;
+}
+
+extern "C" int xc_cache_enter(xc_cache *c, uint64_t h, const uint8_t *seg)
+{
+    if (!c || !seg) return fail(XC_EINVAL, "null");
+    int rc = set_dev(c->ctx);
+    if (rc) return rc;
+    hipStream_t s = c->ctx->stream;
+    HIPCHK(hipMemcpyAsync(c->ctx->d_seg, seg, XC_SEG, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemsetAsync(c->ctl, 0, CTL_WORDS * 4, s));
+    hipLaunchKernelGGL(k_enter_one, dim3(1), dim3(64), 0, s, cache_plandev(c), h, (const uint8_t *)c->ctx->d_seg);
+    HIPCHK(hipGetLastError());
+    uint32_t ctl[CTL_WORDS];
+    HIPCHK(hipMemcpyAsync(ctl, c->ctl, sizeof ctl, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (ctl[CTL_ERROR] & ERR_CAPACITY) return fail(XC_ENOSPC, "cache full");
+    return XC_OK;
+}
+
+extern "C" int xc_hash_segments(xc_ctx *ctx, const uint8_t *d_segs, uint64_t n, uint64_t *d_out, void *stream)
+{
+    if (!ctx) return fail(XC_EINVAL, "null");
+    if (n == 0) return XC_OK;
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    uint32_t blocks = (uint32_t)std::min<uint64_t>(n, 65536);
+    hipLaunchKernelGGL(k_hash_segments, dim3(blocks), dim3(64), 0, s, d_segs, n, d_out);
+    HIPCHK(hipGetLastError());
+    return XC_OK;
+}
+
+extern "C" int xc_window_hashes(xc_ctx *ctx, const uint8_t *d_in, uint64_t n, uint64_t *d_out, void *stream)
+{
+    if (!ctx) return fail(XC_EINVAL, "null");
+    if (n == 0) return XC_OK;
+    if (n > 0xFFFFFFF0ull) return fail(XC_EINVAL, "too long");
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    uint32_t blocks = (uint32_t)((n + XC_SEG - 1) / XC_SEG);
+    hipLaunchKernelGGL(k_window_hashes, dim3(blocks), dim3(64), 0, s, d_in, (uint32_t)n, d_out);
+    HIPCHK(hipGetLastError());
+    return XC_OK;
+}
+
+// ------------------------------------------------------------------ plan ----------
+static const uint32_t CHUNK_LEN = 8192;
+static const uint64_t SUB_BYTES = 256ull << 20;  // sub-batch: bound on input bytes
+static const uint32_t SUB_BUFS = 8192;           // sub-batch: bound on buffers
+static const uint32_t MAX_ROUNDS = 64;
+
+struct HostLayer {
+    Layer d{};
+    int alloc(uint32_t nchunks, uint32_t chunk_len)
+    {
+        size_t n = std::max<uint32_t>(nchunks, 1);
+        HIPCHK(hipMalloc(&d.cnt, n * 4));
+        HIPCHK(hipMalloc(&d.pos, n * EV_CAP * 4));
+        HIPCHK(hipMalloc(&d.stat, n * EV_CAP * 4));
+        HIPCHK(hipMalloc(&d.h, n * EV_CAP * 8));
+        HIPCHK(hipMalloc(&d.val, n * EV_CAP * 8));
+        HIPCHK(hipMalloc(&d.bits, n * (chunk_len / 32) * 4));
+        return XC_OK;
+    }
+    void release()
+    {
+        hipFree(d.cnt);
+        hipFree(d.pos);
+        hipFree(d.stat);
+        hipFree(d.h);
+        hipFree(d.val);
+        hipFree(d.bits);
+    }
+};
+
+struct xc_plan {
+    xc_cache *cache;
+    uint32_t nb;
+    std::vector<uint64_t> len, in_off, out_off;
+    uint64_t in_bytes, out_bytes;
+    std::vector<uint32_t> chunk0;   // host copy of buf_chunk0
+    std::vector<uint32_t> sub;      // sub-batch boundaries (buffer indices), sub.back() = nb
+    uint32_t nchunks;
+    PlanDev P{};
+    HostLayer S, D;
+    HostSet dset;
+    // device arrays owned
+    uint64_t *d_buf_off, *d_out_off;
+    uint32_t *d_buf_len, *d_chunk0, *d_tok_base;
+    uint2 *d_chunks;
+    xc_run_stats stats{};
+};
+
+extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint64_t nbuf, xc_plan **out)
+{
+    if (!c || !out || (!lengths && nbuf)) return fail(XC_EINVAL, "null");
+    if (nbuf > (1u << 24)) return fail(XC_EINVAL, "too many buffers");
+    int rc = set_dev(c->ctx);
+    if (rc) return rc;
+    xc_plan *p = new xc_plan();
+    p->cache = c;
+    p->nb = (uint32_t)nbuf;
+    p->len.assign(lengths, lengths + nbuf);
+    p->in_off.resize(nbuf);
+    p->out_off.resize(nbuf);
+    std::vector<uint32_t> blen(nbuf), chunk0(nbuf + 1), tok_base(nbuf + 1);
+    std::vector<uint2> chunks;
+    uint64_t io = 0, oo = 0;
+    uint64_t toks = 0;
+    for (uint64_t i = 0; i < nbuf; i++) {
+        uint64_t n = lengths[i];
+        if (n > MAX_BUF) return fail(XC_EINVAL, "buffer longer than 1 MiB");
+        blen[i] = (uint32_t)n;
+        p->in_off[i] = io;
+        io += (n + 255) / 256 * 256;
+        p->out_off[i] = oo;
+        oo += (2 * n + 16 + 255) / 256 * 256;
+        chunk0[i] = (uint32_t)chunks.size();
+        if (n >= XC_SEG)
+            for (uint32_t s = 0; s < n; s += CHUNK_LEN) chunks.push_back(make_uint2((uint32_t)i, s));
+        tok_base[i] = (uint32_t)toks;
+        toks += 2 * (n / XC_SEG) + 3;
+    }
+    chunk0[nbuf] = (uint32_t)chunks.size();
+    if (toks > 0xFFFFFFF0ull) return fail(XC_EINVAL, "batch too large");
+    p->in_bytes = io + 4096;
+    p->out_bytes = oo + 256;
+    p->nchunks = (uint32_t)chunks.size();
+    p->chunk0 = chunk0;
+    // sub-batches
+    p->sub.push_back(0);
+    {
+        uint64_t bytes = 0;
+        uint32_t cnt = 0;
+        uint64_t decl = 0, maxdecl = 0;
+        for (uint32_t i = 0; i < nbuf; i++) {
+            if (cnt && (bytes + lengths[i] > SUB_BYTES || cnt >= SUB_BUFS)) {
+                p->sub.push_back(i);
+                maxdecl = std::max(maxdecl, decl);
+                bytes = 0;
+                cnt = 0;
+                decl = 0;
+            }
+            bytes += lengths[i];
+            cnt++;
+            decl += lengths[i] / XC_SEG + 1;
+        }
+        maxdecl = std::max(maxdecl, decl);
+        if (p->sub.back() != nbuf) p->sub.push_back((uint32_t)nbuf);
+        if ((rc = p->dset.alloc(std::max<uint64_t>(maxdecl, 64)))) return rc;
+    }
+    if ((rc = p->S.alloc(p->nchunks, CHUNK_LEN))) return rc;
+    if ((rc = p->D.alloc(p->nchunks, CHUNK_LEN))) return rc;
+
+    size_t nb1 = std::max<uint64_t>(nbuf, 1);
+    HIPCHK(hipMalloc(&p->d_buf_off, nb1 * 8));
+    HIPCHK(hipMalloc(&p->d_out_off, nb1 * 8));
+    HIPCHK(hipMalloc(&p->d_buf_len, nb1 * 4));
+    HIPCHK(hipMalloc(&p->d_chunk0, (nbuf + 1) * 4));
+    HIPCHK(hipMalloc(&p->d_tok_base, (nbuf + 1) * 4));
+    HIPCHK(hipMalloc(&p->d_chunks, std::max<size_t>(chunks.size(), 1) * sizeof(uint2)));
+    hipStream_t s = c->ctx->stream;
+    if (nbuf) {
+        HIPCHK(hipMemcpyAsync(p->d_buf_off, p->in_off.data(), nbuf * 8, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(p->d_out_off, p->out_off.data(), nbuf * 8, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(p->d_buf_len, blen.data(), nbuf * 4, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(p->d_tok_base, tok_base.data(), nbuf * 4, hipMemcpyHostToDevice, s));
+    }
+    HIPCHK(hipMemcpyAsync(p->d_chunk0, chunk0.data(), (nbuf + 1) * 4, hipMemcpyHostToDevice, s));
+    if (!chunks.empty())
+        HIPCHK(hipMemcpyAsync(p->d_chunks, chunks.data(), chunks.size() * sizeof(uint2), hipMemcpyHostToDevice, s));
+
+    PlanDev &P = p->P;
+    P = cache_plandev(c);
+    P.buf_off = p->d_buf_off;
+    P.buf_len = p->d_buf_len;
+    P.nb = (uint32_t)nbuf;
+    P.chunks = p->d_chunks;
+    P.buf_chunk0 = p->d_chunk0;
+    P.chunk_len = CHUNK_LEN;
+    P.S = p->S.d;
+    P.D = p->D.d;
+    P.dset = p->dset.d;
+    P.tok_base = p->d_tok_base;
+    size_t nt = std::max<uint64_t>(toks, 1);
+    HIPCHK(hipMalloc(&P.tok_cnt, nb1 * 4));
+    HIPCHK(hipMalloc(&P.tok_lb, nt * 4));
+    HIPCHK(hipMalloc(&P.tok_le, nt * 4));
+    HIPCHK(hipMalloc(&P.tok_seg, nt * 4));
+    HIPCHK(hipMalloc(&P.tok_op, nt * 4));
+    HIPCHK(hipMalloc(&P.tok_dpos, nt * 4));
+    HIPCHK(hipMalloc(&P.tok_h, nt * 8));
+    HIPCHK(hipMalloc(&P.ctl, CTL_WORDS * 4));
+    P.out_off = p->d_out_off;
+    HIPCHK(hipStreamSynchronize(s));
+    *out = p;
+    return XC_OK;
+}
+
+extern "C" int xc_plan_destroy(xc_plan *p)
+{
+    if (!p) return XC_OK;
+    hipSetDevice(p->cache->ctx->dev);
+    hipStreamSynchronize(p->cache->ctx->stream);
+    p->S.release();
+    p->D.release();
+    p->dset.release();
+    hipFree(p->d_buf_off);
+    hipFree(p->d_out_off);
+    hipFree(p->d_buf_len);
+    hipFree(p->d_chunk0);
+    hipFree(p->d_tok_base);
+    hipFree(p->d_chunks);
+    hipFree(p->P.tok_cnt);
+    hipFree(p->P.tok_lb);
+    hipFree(p->P.tok_le);
+    hipFree(p->P.tok_seg);
+    hipFree(p->P.tok_op);
+    hipFree(p->P.tok_dpos);
+    hipFree(p->P.tok_h);
+    hipFree(p->P.ctl);
+    delete p;
+    return XC_OK;
+}
+
+extern "C" int xc_plan_layout(xc_plan *p, uint64_t *in_off, uint64_t *out_off, uint64_t *in_bytes,
+                              uint64_t *out_bytes)
+{
+    if (!p) return fail(XC_EINVAL, "null");
+    if (in_off) std::copy(p->in_off.begin(), p->in_off.end(), in_off);
+    if (out_off) std::copy(p->out_off.begin(), p->out_off.end(), out_off);
+    if (in_bytes) *in_bytes = p->in_bytes;
+    if (out_bytes) *out_bytes = p->out_bytes;
+    return XC_OK;
+}
+
+extern "C" int xc_plan_stats(xc_plan *p, xc_run_stats *st)
+{
+    if (!p || !st) return fail(XC_EINVAL, "null");
+    *st = p->stats;
+    return XC_OK;
+}
+
+static int read_ctl(xc_plan *p, uint32_t *ctl)
+{
+    hipStream_t s = p->cache->ctx->stream;
+    HIPCHK(hipMemcpyAsync(ctl, p->P.ctl, CTL_WORDS * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return XC_OK;
+}
+
+static int launch_scan(xc_plan *p, const Layer &L, const DevSet &set, uint32_t ck_lo, uint32_t ck_hi)
+{
+    if (ck_hi <= ck_lo) return XC_OK;
+    xc_ctx *ctx = p->cache->ctx;
+    ScanArgs a{p->P, L, set, ck_lo, ck_hi};
+    uint32_t need = (ck_hi - ck_lo + SCAN_WAVES - 1) / SCAN_WAVES;
+    uint32_t grid = std::min<uint32_t>(need, (uint32_t)ctx->n_cu);
+    hipLaunchKernelGGL(k_scan, dim3(grid), dim3(64 * SCAN_WAVES), SCAN_LDS, ctx->stream, a);
+    HIPCHK(hipGetLastError());
+    return XC_OK;
+}
+
+static int launch_resolve(xc_plan *p, const Layer &L, int dmode, uint32_t ck_lo, uint32_t ck_hi)
+{
+    if (ck_hi <= ck_lo) return XC_OK;
+    ResolveArgs a{p->P, L, dmode, ck_lo, ck_hi};
+    hipLaunchKernelGGL(k_resolve, dim3((ck_hi - ck_lo + 3) / 4), dim3(256), 0, p->cache->ctx->stream, a);
+    HIPCHK(hipGetLastError());
+    return XC_OK;
+}
+
+static int launch_walk_round(xc_plan *p, uint32_t j0, uint32_t j1, int use_d)
+{
+    hipStream_t s = p->cache->ctx->stream;
+    const uint32_t none = NONE;
+    HIPCHK(hipMemsetAsync(p->P.ctl + CTL_GREW, 0, 4, s));
+    HIPCHK(hipMemcpyAsync(p->P.ctl + CTL_FIRST_CROSS, &none, 4, hipMemcpyHostToDevice, s));
+    WalkArgs w{p->P, j0, j1, use_d};
+    hipLaunchKernelGGL(k_walk, dim3(j1 - j0), dim3(64), 0, s, w);
+    HIPCHK(hipGetLastError());
+    DeclArgs d{p->P, j0, j1};
+    hipLaunchKernelGGL(k_declhash, dim3(j1 - j0, 8), dim3(64), 0, s, d);
+    HIPCHK(hipGetLastError());
+    p->stats.walk_rounds++;
+    return XC_OK;
+}
+
+extern "C" int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_out_len)
+{
+    if (!p || (!d_in && p->nb) || (!d_out && p->nb) || (!d_out_len && p->nb)) return fail(XC_EINVAL, "null");
+    int rc = set_dev(p->cache->ctx);
+    if (rc) return rc;
+    hipStream_t s = p->cache->ctx->stream;
+    p->P.in = d_in;
+    p->P.out = d_out;
+    p->P.out_len = d_out_len;
+    p->stats = xc_run_stats{};
+    HIPCHK(hipMemsetAsync(p->P.ctl, 0, CTL_WORDS * 4, s));
+    uint32_t ctl[CTL_WORDS];
+    for (size_t si = 0; si + 1 < p->sub.size(); si++) {
+        const uint32_t s1 = p->sub[si + 1];
+        uint32_t j0 = p->sub[si];
+        p->stats.sub_batches++;
+        while (j0 < s1) {
+            p->stats.outer_rounds++;
+            const uint32_t ck_lo = p->chunk0[j0], ck_hi = p->chunk0[s1];
+            if ((rc = launch_scan(p, p->P.S, p->P.cache, ck_lo, ck_hi))) return rc;
+            if ((rc = launch_resolve(p, p->P.S, 0, ck_lo, ck_hi))) return rc;
+            if ((rc = p->dset.clear(s))) return rc;
+            if ((rc = launch_walk_round(p, j0, s1, 0))) return rc;
+            uint32_t rounds = 0;
+            for (;;) {
+                // declaration layer against every hash declared so far, then walk again
+                if ((rc = launch_scan(p, p->P.D, p->P.dset, ck_lo, ck_hi))) return rc;
+                if ((rc = launch_resolve(p, p->P.D, 1, ck_lo, ck_hi))) return rc;
+                if ((rc = launch_walk_round(p, j0, s1, 1))) return rc;
+                if ((rc = read_ctl(p, ctl))) return rc;
+                if (ctl[CTL_ERROR]) break;
+                if (!ctl[CTL_GREW]) break;
+                if (++rounds > MAX_ROUNDS) return fail(XC_EDEVICE, "declaration rounds did not converge");
+            }
+            if (ctl[CTL_ERROR]) break;
+            uint32_t jc = std::min<uint32_t>(ctl[CTL_FIRST_CROSS], s1);
+            if (jc <= j0) jc = j0 + 1;  // cannot happen (buffer j0 has no earlier buffer); progress guard
+            EmitArgs e{p->P, j0, jc};
+            hipLaunchKernelGGL(k_emit, dim3(jc - j0), dim3(256), 0, s, e);
+            HIPCHK(hipGetLastError());
+            j0 = jc;
+        }
+    }
+    if ((rc = read_ctl(p, ctl))) return rc;
+    p->stats.n_extract = ctl[CTL_NEXTRACT];
+    p->stats.n_ref = ctl[CTL_NREF];
+    p->stats.dense_chunks = ctl[CTL_DENSE];
+    if (ctl[CTL_ERROR] & ERR_CAPACITY) {
+        uint32_t cap = (uint32_t)p->cache->cap;
+        hipMemcpyAsync(p->cache->count, &cap, 4, hipMemcpyHostToDevice, s);
+        hipStreamSynchronize(s);
+        return fail(XC_ENOSPC, "device cache capacity exhausted");
+    }
+    if (ctl[CTL_ERROR]) return fail(XC_EDEVICE, "internal encode error " + std::to_string(ctl[CTL_ERROR]));
+    return XC_OK;
+}
+
+extern "C" int xc_encode_batch_host(xc_cache *c, const uint8_t *in, const uint64_t *in_off, const uint64_t *in_len,
+                                    uint64_t nbuf, uint8_t *out, const uint64_t *out_off, const uint64_t *out_cap,
+                                    uint64_t *out_len)
+{
+    if (!c || (nbuf && (!in || !in_off || !in_len || !out || !out_off || !out_cap || !out_len)))
+        return fail(XC_EINVAL, "null");
+    xc_plan *p = nullptr;
+    int rc = xc_encode_plan_create(c, in_len, nbuf, &p);
+    if (rc) return rc;
+    hipStream_t s = c->ctx->stream;
+    uint8_t *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
+    uint64_t *d_len = nullptr;
+    std::vector<uint64_t> lens(nbuf);
+    HIPCHK(hipHostMalloc(&h_in, p->in_bytes));
+    HIPCHK(hipHostMalloc(&h_out, p->out_bytes));
+    HIPCHK(hipMalloc(&d_in, p->in_bytes));
+    HIPCHK(hipMalloc(&d_out, p->out_bytes));
+    HIPCHK(hipMalloc(&d_len, std::max<uint64_t>(nbuf, 1) * 8));
+    memset(h_in, 0, p->in_bytes);
+    for (uint64_t i = 0; i < nbuf; i++) memcpy(h_in + p->in_off[i], in + in_off[i], in_len[i]);
+    HIPCHK(hipMemcpyAsync(d_in, h_in, p->in_bytes, hipMemcpyHostToDevice, s));
+    rc = xc_encode_run(p, d_in, d_out, d_len);
+    if (!rc) {
+        HIPCHK(hipMemcpyAsync(h_out, d_out, p->out_bytes, hipMemcpyDeviceToHost, s));
+        if (nbuf) HIPCHK(hipMemcpyAsync(lens.data(), d_len, nbuf * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        for (uint64_t i = 0; i < nbuf; i++) {
+            out_len[i] = lens[i];
+            if (lens[i] > out_cap[i]) { rc = fail(XC_EINVAL, "output capacity too small"); continue; }
+            memcpy(out + out_off[i], h_out + p->out_off[i], lens[i]);
+        }
+    }
+    hipHostFree(h_in);
+    hipHostFree(h_out);
+    hipFree(d_in);
+    hipFree(d_out);
+    hipFree(d_len);
+    xc_plan_destroy(p);
+    return rc;
+}
+
+extern "C" int xc_selftest(xc_ctx *ctx)
+{
+    if (!ctx) return fail(XC_EINVAL, "null");
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    hipStream_t s = ctx->stream;
+    HIPCHK(hipMemsetAsync(ctx->d_scratch, 0, 4, s));
+    hipLaunchKernelGGL(k_selftest, dim3(1), dim3(64), 0, s, ctx->d_scratch);
+    HIPCHK(hipGetLastError());
+    uint32_t err = 0;
+    HIPCHK(hipMemcpyAsync(&err, ctx->d_scratch, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (err) return fail(XC_EDEVICE, "selftest failed: " + std::to_string(err));
+    return XC_OK;
+}
+
+extern "C" int xc_decode_batch_host(xc_cache *c, const uint8_t *in, const uint64_t *in_off, const uint64_t *in_len,
+                                    uint64_t nbuf, uint8_t *out, const uint64_t *out_off, const uint64_t *out_cap,
+                                    uint64_t *out_len, uint64_t *consumed, int32_t *status, uint64_t *unknown,
+                                    int32_t *has_unknown);

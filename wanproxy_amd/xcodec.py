@@ -1,0 +1,292 @@
+"""Python host binding of libxcodec_hip.so (the C ABI in include/xcodec_hip.h).
+
+Mirrors the reference's XCodec objects (bramfeld/wanproxy xcodec/):
+
+* :class:`XCodecCache`  — XCodecMemoryCache (xcodec/xcodec_cache.h:162-211), device resident
+* :class:`XCodecEncoder` — XCodecEncoder::encode + flush per buffer (xcodec/xcodec_encoder.cc:60-201)
+* :class:`XCodecDecoder` — XCodecDecoder::decode per stream (xcodec/xcodec_decoder.cc:76-176)
+* :class:`EncodePlan`   — a device-resident batch (inputs already in HBM) for benchmarks
+
+There is no CPU fallback: if the HIP library or a GPU is missing, construction raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libxcodec_hip.so")
+SEGMENT_LENGTH = 2048
+
+SYMBOLS = [
+    "xc_device_count", "xc_ctx_create", "xc_ctx_destroy", "xc_ctx_stream", "xc_ctx_sync",
+    "xc_cache_create", "xc_cache_destroy", "xc_cache_count", "xc_cache_snapshot",
+    "xc_cache_restore", "xc_cache_lookup", "xc_cache_enter", "xc_hash_segments",
+    "xc_window_hashes", "xc_encode_plan_create", "xc_plan_destroy", "xc_plan_layout",
+    "xc_encode_run", "xc_encode_batch_host", "xc_plan_stats", "xc_decode_batch_host",
+    "xc_selftest", "xc_last_error",
+]
+
+
+class XCodecError(RuntimeError):
+    pass
+
+
+class RunStats(C.Structure):
+    _fields_ = [("n_extract", C.c_uint64), ("n_ref", C.c_uint64), ("in_bytes", C.c_uint64),
+                ("out_bytes", C.c_uint64), ("sub_batches", C.c_uint32),
+                ("walk_rounds", C.c_uint32), ("outer_rounds", C.c_uint32),
+                ("dense_chunks", C.c_uint32)]
+
+
+_LIB = None
+_u64p = np.ctypeslib.ndpointer(np.uint64, flags="C")
+_u8p = np.ctypeslib.ndpointer(np.uint8, flags="C")
+_i32p = np.ctypeslib.ndpointer(np.int32, flags="C")
+_vp = C.c_void_p
+
+
+def load_library(path: str = LIB_PATH) -> C.CDLL:
+    """Load libxcodec_hip.so (raises if it was not built)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    # One HIP runtime per process: PyTorch ships its own libamdhip64 (same soname).  Loading
+    # torch first makes this library bind to that copy instead of a second /opt/rocm one.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    if not os.path.exists(path):
+        raise XCodecError(f"{path} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = C.CDLL(path)
+    for name in SYMBOLS:
+        getattr(lib, name)  # every declared entry point must be exported
+    lib.xc_last_error.restype = C.c_char_p
+    lib.xc_ctx_stream.restype = _vp
+    lib.xc_ctx_stream.argtypes = [_vp]
+    lib.xc_device_count.argtypes = [C.POINTER(C.c_int)]
+    lib.xc_ctx_create.argtypes = [C.c_int, C.POINTER(_vp)]
+    lib.xc_ctx_destroy.argtypes = [_vp]
+    lib.xc_ctx_sync.argtypes = [_vp]
+    lib.xc_cache_create.argtypes = [_vp, C.c_uint64, C.POINTER(_vp)]
+    lib.xc_cache_destroy.argtypes = [_vp]
+    lib.xc_cache_count.argtypes = [_vp, C.POINTER(C.c_uint64)]
+    lib.xc_cache_snapshot.argtypes = [_vp]
+    lib.xc_cache_restore.argtypes = [_vp]
+    lib.xc_cache_lookup.argtypes = [_vp, C.c_uint64, _u8p, C.POINTER(C.c_int)]
+    lib.xc_cache_enter.argtypes = [_vp, C.c_uint64, _u8p]
+    lib.xc_hash_segments.argtypes = [_vp, _vp, C.c_uint64, _vp, _vp]
+    lib.xc_window_hashes.argtypes = [_vp, _vp, C.c_uint64, _vp, _vp]
+    lib.xc_encode_plan_create.argtypes = [_vp, _u64p, C.c_uint64, C.POINTER(_vp)]
+    lib.xc_plan_destroy.argtypes = [_vp]
+    lib.xc_plan_layout.argtypes = [_vp, _u64p, _u64p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+    lib.xc_encode_run.argtypes = [_vp, _vp, _vp, _vp]
+    lib.xc_plan_stats.argtypes = [_vp, C.POINTER(RunStats)]
+    lib.xc_encode_batch_host.argtypes = [_vp, _u8p, _u64p, _u64p, C.c_uint64, _u8p, _u64p, _u64p,
+                                         _u64p]
+    lib.xc_decode_batch_host.argtypes = [_vp, _u8p, _u64p, _u64p, C.c_uint64, _u8p, _u64p, _u64p,
+                                         _u64p, _u64p, _i32p, _u64p, _i32p]
+    lib.xc_selftest.argtypes = [_vp]
+    _LIB = lib
+    return lib
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        raise XCodecError(f"xcodec_hip error {rc}: {load_library().xc_last_error().decode()}")
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    _check(load_library().xc_device_count(C.byref(n)))
+    return n.value
+
+
+class Context:
+    """One GPU (xc_ctx) with its own HIP stream."""
+
+    def __init__(self, device: int = 0):
+        lib = load_library()
+        self.h = _vp()
+        _check(lib.xc_ctx_create(device, C.byref(self.h)))
+        self.device = device
+
+    @property
+    def stream(self) -> int:
+        return load_library().xc_ctx_stream(self.h)
+
+    def sync(self) -> None:
+        _check(load_library().xc_ctx_sync(self.h))
+
+    def selftest(self) -> None:
+        _check(load_library().xc_selftest(self.h))
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            load_library().xc_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _as_u8(b) -> np.ndarray:
+    if isinstance(b, (bytes, bytearray, memoryview)):
+        return np.frombuffer(bytes(b), dtype=np.uint8)
+    return np.ascontiguousarray(b, dtype=np.uint8)
+
+
+def _pack(bufs):
+    lens = np.array([len(b) for b in bufs], dtype=np.uint64)
+    offs = np.zeros(len(bufs), dtype=np.uint64)
+    if len(bufs) > 1:
+        offs[1:] = np.cumsum(lens)[:-1]
+    arena = np.concatenate([_as_u8(b) for b in bufs]) if len(bufs) else np.zeros(0, np.uint8)
+    if arena.size == 0:
+        arena = np.zeros(1, np.uint8)
+    return np.ascontiguousarray(arena), offs, lens
+
+
+class XCodecCache:
+    """XCodecMemoryCache (xcodec/xcodec_cache.h:162-211) held in HBM.
+
+    ``capacity`` bounds the number of 2048-byte segments (the reference map grows without
+    bound; here an overflow raises instead of evicting)."""
+
+    def __init__(self, ctx: Context, capacity: int = 1 << 16):
+        self.ctx = ctx
+        self.h = _vp()
+        _check(load_library().xc_cache_create(ctx.h, capacity, C.byref(self.h)))
+        self.capacity = capacity
+
+    def __len__(self) -> int:
+        n = C.c_uint64()
+        _check(load_library().xc_cache_count(self.h, C.byref(n)))
+        return n.value
+
+    def lookup(self, h: int) -> bytes | None:
+        out = np.zeros(SEGMENT_LENGTH, np.uint8)
+        found = C.c_int(0)
+        _check(load_library().xc_cache_lookup(self.h, h, out, C.byref(found)))
+        return out.tobytes() if found.value else None
+
+    def enter(self, h: int, seg) -> None:
+        seg = _as_u8(seg)
+        assert seg.size == SEGMENT_LENGTH
+        _check(load_library().xc_cache_enter(self.h, h, np.ascontiguousarray(seg)))
+
+    def snapshot(self) -> None:
+        _check(load_library().xc_cache_snapshot(self.h))
+
+    def restore(self) -> None:
+        _check(load_library().xc_cache_restore(self.h))
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            load_library().xc_cache_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class XCodecEncoder:
+    """Batch form of XCodecEncoder: each buffer is ``encode(out, buf); flush(out)`` on a fresh
+    encoder, buffers in index order, one shared cache (xcodec/xcodec_encoder.cc:60-201)."""
+
+    def __init__(self, cache: XCodecCache):
+        self.cache = cache
+
+    def encode_batch(self, bufs) -> list[bytes]:
+        arena, offs, lens = _pack(bufs)
+        cap = lens * 2 + 16
+        ooff = np.zeros(len(bufs), dtype=np.uint64)
+        if len(bufs) > 1:
+            ooff[1:] = np.cumsum(cap)[:-1]
+        out = np.zeros(max(1, int(cap.sum())), np.uint8)
+        olen = np.zeros(len(bufs), np.uint64)
+        _check(load_library().xc_encode_batch_host(self.cache.h, arena, offs, lens, len(bufs),
+                                                   out, ooff, cap, olen))
+        return [out[int(o):int(o) + int(n)].tobytes() for o, n in zip(ooff, olen)]
+
+
+class XCodecDecoder:
+    """Batch form of XCodecDecoder::decode (xcodec/xcodec_decoder.cc:76-176): one decode call
+    per stream, streams in index order, one shared cache.  Returns, per stream,
+    ``(status, decoded_bytes, consumed, unknown_hash_or_None)``."""
+
+    def __init__(self, cache: XCodecCache):
+        self.cache = cache
+
+    def decode_batch(self, streams, out_cap: int | None = None):
+        arena, offs, lens = _pack(streams)
+        cap = (lens * 205 + 16) if out_cap is None else np.full(len(streams), out_cap, np.uint64)
+        ooff = np.zeros(len(streams), dtype=np.uint64)
+        if len(streams) > 1:
+            ooff[1:] = np.cumsum(cap)[:-1]
+        out = np.zeros(max(1, int(cap.sum())), np.uint8)
+        olen = np.zeros(len(streams), np.uint64)
+        cons = np.zeros(len(streams), np.uint64)
+        st = np.zeros(len(streams), np.int32)
+        unk = np.zeros(len(streams), np.uint64)
+        hu = np.zeros(len(streams), np.int32)
+        _check(load_library().xc_decode_batch_host(self.cache.h, arena, offs, lens, len(streams),
+                                                   out, ooff, cap, olen, cons, st, unk, hu))
+        return [(int(st[i]), out[int(ooff[i]):int(ooff[i]) + int(olen[i])].tobytes(),
+                 int(cons[i]), int(unk[i]) if hu[i] else None) for i in range(len(streams))]
+
+
+class EncodePlan:
+    """A device-resident encode batch: fixed buffer lengths, inputs/outputs in HBM arenas.
+
+    ``run(d_in, d_out, d_len)`` takes raw device pointers (e.g. ``tensor.data_ptr()``)."""
+
+    def __init__(self, cache: XCodecCache, lengths):
+        self.cache = cache
+        lens = np.ascontiguousarray(lengths, dtype=np.uint64)
+        self.nbuf = len(lens)
+        self.lengths = lens
+        self.h = _vp()
+        _check(load_library().xc_encode_plan_create(cache.h, lens, self.nbuf, C.byref(self.h)))
+        self.in_off = np.zeros(self.nbuf, np.uint64)
+        self.out_off = np.zeros(self.nbuf, np.uint64)
+        ib, ob = C.c_uint64(), C.c_uint64()
+        _check(load_library().xc_plan_layout(self.h, self.in_off, self.out_off, C.byref(ib),
+                                             C.byref(ob)))
+        self.in_bytes, self.out_bytes = ib.value, ob.value
+
+    def run(self, d_in: int, d_out: int, d_len: int) -> None:
+        _check(load_library().xc_encode_run(self.h, d_in, d_out, d_len))
+
+    def stats(self) -> RunStats:
+        st = RunStats()
+        _check(load_library().xc_plan_stats(self.h, C.byref(st)))
+        return st
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            load_library().xc_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def hash_segments(ctx: Context, d_segs: int, n: int, d_out: int, stream: int | None = None) -> None:
+    _check(load_library().xc_hash_segments(ctx.h, d_segs, n, d_out, stream))
+
+
+def window_hashes(ctx: Context, d_in: int, n: int, d_out: int, stream: int | None = None) -> None:
+    _check(load_library().xc_window_hashes(ctx.h, d_in, n, d_out, stream))
