@@ -1,0 +1,216 @@
+#!/usr/bin/env python3
+"""bench.py — XCodec encode GiB/s, device resident, on MI355X.
+
+Workload (BASELINE.json configs[4], the config the metric's 1/2/4/8-GPU figures are quoted
+on): 32768 x 64 KiB buffers, 50 % repeated segments (splitmix64 seed 0x5555), buffer i ->
+rank i mod N, every rank with its own cache warmed with the 8192-segment pool.  Total work
+is fixed as N grows ("scaling": "strong").
+
+One step = restore the warm cache snapshot (enqueued, inside the timed region) + encode the
+rank's whole shard, inputs already resident in HBM.  Every buffer is encode()+flush() on a
+fresh XCodecEncoder against the rank's cache, buffers in index order
+(xcodec/xcodec_encoder.cc:60-201), bit-exact with the reference.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+SEG = 2048
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--total", type=int, default=32768, help="buffers in the whole job")
+    ap.add_argument("--cpu-sample", type=int, default=8192, help="buffers in the CPU baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--verify", type=int, default=16, help="buffers checked against the oracle (rank 0)")
+    ap.add_argument("--no-e2e", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
+
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        # barrier and max-reduction of the step time only: the path shards with no collective
+        dist.init_process_group("gloo")
+
+    import wanproxy_amd as w
+    from wanproxy_amd import workloads as W
+
+    ctx = w.Context(local_rank)
+    shard = W.repeat_shard(args.total, 0x5555, rank, world)  # (n_local, 65536)
+    n_local = shard.shape[0]
+    pool = W.pool()
+    warm = [pool[i:i + W.BUF] for i in range(0, len(pool), W.BUF)]
+
+    cache = w.XCodecCache(ctx, W.POOL_SEGMENTS + n_local * (W.BUF // SEG + 1) + 1024)
+    w.XCodecEncoder(cache).encode_batch(warm)
+    cache.snapshot()
+
+    lens = np.full(n_local, W.BUF, dtype=np.uint64)
+    plan = w.EncodePlan(cache, lens)
+    assert all(int(plan.in_off[i]) == i * W.BUF for i in range(n_local))
+    d_in = torch.zeros(plan.in_bytes, dtype=torch.uint8, device="cuda")
+    d_in[:n_local * W.BUF] = torch.from_numpy(shard.reshape(-1)).cuda()
+    d_out = torch.zeros(plan.out_bytes, dtype=torch.uint8, device="cuda")
+    d_len = torch.zeros(n_local, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+
+    def step():
+        cache.restore_async()
+        plan.run(d_in.data_ptr(), d_out.data_ptr(), d_len.data_ptr())
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    verified = None
+    if rank == 0 and args.verify > 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle  # checker only
+        oc = oracle.Cache()
+        oc.encode_batch(warm)
+        want = oc.encode_batch([shard[i] for i in range(min(args.verify, n_local))])
+        out = d_out[:int(plan.out_off[len(want) - 1]) + 2 * W.BUF + 16].cpu().numpy()
+        got_len = d_len.cpu().numpy()
+        verified = all(out[int(plan.out_off[i]):int(plan.out_off[i]) + int(got_len[i])].tobytes() == want[i]
+                       for i in range(len(want)))
+        if not verified:
+            raise SystemExit("bench: GPU output differs from the oracle")
+
+    plan.set_timing(True)
+    plan.kernel_times(reset=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    plan.set_timing(False)
+    kt = plan.kernel_times()
+    st = plan.stats()
+    out_bytes = int(d_len.sum().item())
+
+    in_bytes_rank = n_local * W.BUF
+    total_in = args.total * W.BUF if world > 1 else in_bytes_rank
+    value = total_in * args.steps / elapsed / 2**30
+
+    # algorithmic bytes of one step on this rank:
+    # in + out + 2048 * (segments declared + references verified)
+    alg_step = in_bytes_rank + out_bytes + SEG * (int(st.n_extract) + int(st.n_ref))
+    step_s = elapsed / args.steps
+    # dominant kernel: most device time in the timed region
+    dom = max(kt["ms"], key=lambda k: kt["ms"][k])
+    launches = max(1, kt["launches"][dom])
+    avg_ms = kt["ms"][dom] / launches
+    if dom == "scan":
+        bytes_per_launch = kt["scan_bytes"] / launches  # every input byte read once per scan
+    else:
+        bytes_per_launch = alg_step * args.steps / launches
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+
+    result = {
+        "metric": "XCodec encode GiB/s device-resident (cfg5: 32768 x 64 KiB, 50% repeats, warm per-GPU cache)",
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(step_s * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (splitmix64, SURVEY.md §8(d))",
+        "config": {"workload": "cfg5", "buffers_total": args.total, "buffer_bytes": W.BUF,
+                   "repeat_pct": 50, "seed": "0x5555", "cache": "warm pool, 8192 segments per GPU",
+                   "buffers_per_gpu": n_local, "parallelism": f"shard{world}"},
+        "roofline": {"bound": "hbm", "kernel": f"k_{dom}", "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": None, "avg_launch_ms": round(avg_ms, 4),
+                     "alg_bytes_per_launch": int(bytes_per_launch)},
+        "pipeline_roofline": {"alg_bytes_per_step": alg_step,
+                              "achieved_GBs": round(alg_step / step_s / 1e9, 1),
+                              "frac": round(alg_step / step_s / 1e9 / HBM_PEAK_GBS, 4)},
+        "kernel_ms_per_step": {k: round(v / args.steps, 4) for k, v in kt["ms"].items()},
+        "stats": {"n_extract": int(st.n_extract), "n_ref": int(st.n_ref),
+                  "out_over_in": round(out_bytes / in_bytes_rank, 4),
+                  "sub_batches": int(st.sub_batches), "outer_rounds": int(st.outer_rounds),
+                  "walk_rounds": int(st.walk_rounds), "dense_chunks": int(st.dense_chunks)},
+        "verified_buffers": args.verify if verified else 0,
+        "cpu_baseline": None,
+    }
+
+    if rank == 0 and world == 1 and not args.no_e2e:
+        # end-to-end from pinned host memory: H2D of the input arena, encode, D2H of the output arena
+        h_in = torch.empty(plan.in_bytes, dtype=torch.uint8).pin_memory()
+        h_in.copy_(d_in.cpu())
+        h_out = torch.empty(plan.out_bytes, dtype=torch.uint8).pin_memory()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        d_in.copy_(h_in, non_blocking=True)
+        torch.cuda.synchronize()
+        step()
+        h_out.copy_(d_out, non_blocking=True)
+        torch.cuda.synchronize()
+        e2e = time.perf_counter() - t0
+        result["e2e_host_gibs"] = round(in_bytes_rank / e2e / 2**30, 3)
+        result["e2e_note"] = "pinned H2D of the input arena + encode + D2H of the whole output arena (2n+16 per buffer)"
+
+    if rank == 0 and world == 1 and not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle  # CPU baseline: the C restatement (port) of the reference encoder
+        nthreads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        sample = [shard[i] for i in range(min(args.cpu_sample, n_local))]
+        oc = oracle.Cache()
+        oc.encode_batch(warm)
+        secs, _ = oc.encode_sharded_timed(sample, nthreads)
+        result["cpu_baseline"] = {
+            "value": round(len(sample) * W.BUF / secs / 2**30, 4), "unit": "GiB/s", "cores": nthreads,
+            "kind": "port",
+            "sample": f"first {len(sample)} cfg5 buffers ({len(sample) * W.BUF >> 20} MiB), "
+                      f"round-robin over {nthreads} threads, each with a private clone of the warm cache",
+            "seconds": round(secs, 3)}
+
+    if rank == 0:
+        print(json.dumps(result))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

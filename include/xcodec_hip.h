@@ -92,6 +92,25 @@ int xc_encode_batch_host(xc_cache *c, const uint8_t *in, const uint64_t *in_off,
                          const uint64_t *in_len, uint64_t nbuf, uint8_t *out,
                          const uint64_t *out_off, const uint64_t *out_cap, uint64_t *out_len);
 
+/* Enqueue xc_cache_restore() on the context stream without blocking the host. */
+int xc_cache_restore_async(xc_cache *c);
+
+/* Per-kernel device time of the plan's runs, from HIP events recorded on the context
+ * stream around every launch while timing is enabled (kernel ids: XC_K_*). */
+#define XC_K_SCAN 0
+#define XC_K_RESOLVE 1
+#define XC_K_WALK 2
+#define XC_K_DECLHASH 3
+#define XC_K_EMIT 4
+#define XC_K_COUNT 5
+typedef struct {
+    double ms[XC_K_COUNT];        /* summed device time */
+    uint64_t launches[XC_K_COUNT];
+    uint64_t scan_bytes;          /* input bytes covered by the scan launches */
+} xc_kernel_times;
+int xc_plan_set_timing(xc_plan *p, int enable);
+int xc_plan_kernel_times(xc_plan *p, xc_kernel_times *out, int reset);
+
 /* Counters of the last run (for benchmarks / profiling). */
 typedef struct {
     uint64_t n_extract;  /* EXTRACT tokens emitted (segments declared) */

@@ -1,0 +1,8 @@
+set -e
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+run() { timeout -k 10 240 rocprofv3 --pmc $1 --kernel-include-regex "k_scan|k_emit|k_walk" --output-format csv -d gpurun_out/pmc/$2 -o run -- python3 bench.py --steps 1 --warmup 0 --verify 0 --no-cpu --no-e2e > gpurun_out/pmc_$2.log 2>&1; }
+run "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" p1
+run "SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM" p2
+run "FETCH_SIZE" p3
+run "WRITE_SIZE" p4
+echo done

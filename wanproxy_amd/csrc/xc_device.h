@@ -159,8 +159,10 @@ __device__ __forceinline__ void wave_copy(uint8_t *dst, const uint8_t *src, uint
 // A set of 64-bit hashes: level-1 bitmap (LDS-loaded by the scan), exact lo32 set,
 // full-key table with a 64-bit value.  Used for the cache (value = segment index)
 // and for a batch's declarations (value = buffer<<32 | declaration position, min-wins).
-#define XC_FILT_LOG2 20u
-#define XC_FILT_WORDS (1u << (XC_FILT_LOG2 - 5u))  // 32768 words = 128 KB
+// Level-1 filter: a blocked k=2 Bloom filter of 16384 64-bit words (128 KB, one scan
+// workgroup's LDS image).  lo32 (the hash's bytes_hash half) picks word lo>>18; the key sets
+// bit lo[4:0] of the word's low dword and bit lo[9:5] of its high dword.
+#define XC_FILT_WORDS 32768u  // in 32-bit words
 #define XC_EMPTY64 0xFFFFFFFFFFFFFFFFull           // H never has bits 32..35 set
 
 struct DevSet {
@@ -173,7 +175,11 @@ struct DevSet {
     uint64_t *vals;
 };
 
-__device__ __forceinline__ uint32_t filt_bit(uint32_t lo) { return lo >> (32u - XC_FILT_LOG2); }
+__device__ __forceinline__ uint32_t filt_test(const uint2 *f, uint32_t lo)
+{
+    const uint2 w = f[lo >> 18];
+    return (w.x >> (lo & 31u)) & (w.y >> ((lo >> 5) & 31u)) & 1u;
+}
 __device__ __forceinline__ uint32_t lo_slot(uint32_t lo, uint32_t mask) { return (lo * 0x9E3779B1u) >> 7 & mask; }
 __device__ __forceinline__ uint32_t key_slot(uint64_t h, uint32_t mask)
 {
@@ -237,8 +243,9 @@ __device__ __forceinline__ int set_insert(const DevSet &s, uint64_t h, uint64_t 
                 j = (j + 1u) & s.lo_mask;
             }
         }
-        uint32_t b = filt_bit(lo);
-        atomicOr(&s.filt[b >> 5], 1u << (b & 31u));
+        const uint32_t wi = (lo >> 18) * 2u;
+        atomicOr(&s.filt[wi], 1u << (lo & 31u));
+        atomicOr(&s.filt[wi + 1u], 1u << ((lo >> 5) & 31u));
     }
     if (lo_slot_out) *lo_slot_out = los;
     return fresh;

@@ -50,6 +50,66 @@ __device__ __forceinline__ void scan_record(const ScanArgs &a, uint32_t c, uint3
     }
 }
 
+// Exact lo32 membership for queued filter positives, split in two halves so the global
+// probe latency overlaps the next 2048-position iteration: issue() moves up to 128 queued
+// (position, lo32) pairs into registers and starts their lo32-set loads (two consecutive
+// slots each); complete() consumes them one iteration later.
+struct Pending {
+    uint32_t n;          // entries (uniform); 0 = nothing pending
+    uint32_t c, c0;      // chunk the entries belong to
+    uint32_t pos[2], lo[2], k0[2], k1[2];
+};
+
+__device__ __forceinline__ void pend_issue(const ScanArgs &a, Pending &pd, const uint2 *queue, uint32_t qn,
+                                           uint32_t c, uint32_t c0)
+{
+    pd.n = qn;
+    pd.c = c;
+    pd.c0 = c0;
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+        const uint32_t i = lane_id() + 64u * s;
+        pd.pos[s] = 0;
+        pd.lo[s] = 0;
+        pd.k0[s] = 0;
+        pd.k1[s] = 0;
+        if (i < qn) {
+            const uint2 e = queue[i];
+            pd.pos[s] = e.x;
+            pd.lo[s] = e.y;
+            if (e.y == 0u) {
+                pd.k0[s] = *a.set.lo_zero;
+            } else {
+                const uint32_t j = lo_slot(e.y, a.set.lo_mask);
+                pd.k0[s] = a.set.lo_keys[j];
+                pd.k1[s] = a.set.lo_keys[(j + 1u) & a.set.lo_mask];
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void pend_complete(const ScanArgs &a, Pending &pd, uint32_t &ev_n, bool &dense)
+{
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+        if (64u * s >= pd.n) break;
+        const uint32_t i = lane_id() + 64u * s;
+        bool match = false;
+        if (i < pd.n) {
+            const uint32_t lo = pd.lo[s];
+            if (lo == 0u) {
+                match = pd.k0[s] != 0u;
+            } else if (pd.k0[s] == lo || pd.k1[s] == lo) {
+                match = true;
+            } else if (pd.k0[s] != 0u && pd.k1[s] != 0u) {
+                match = set_has_lo(a.set, lo);  // long probe chain: rare
+            }
+        }
+        scan_record(a, pd.c, pd.c0, match, pd.pos[s], ev_n, dense);
+    }
+    pd.n = 0;
+}
+
 __device__ __forceinline__ void scan_flush(const ScanArgs &a, uint2 *queue, uint32_t &qn, uint32_t c, uint32_t c0,
                                            uint32_t &ev_n, bool &dense)
 {
@@ -100,51 +160,79 @@ __device__ __forceinline__ void load32_aligned(const uint8_t *p, uint32_t w[8])
     w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
 }
 
+// The two blocks a chunk starts from: pw = the 2048 bytes before c0 (block 0 when c0 == 0)
+// and w = the block at c0 (block 1 when c0 == 0).
+__device__ __forceinline__ void first_blocks(const uint8_t *base, uint32_t c0, uint32_t l, uint32_t pw[8],
+                                             uint32_t w[8])
+{
+    const uint32_t s = c0 == 0 ? XC_SEG : c0;
+    load32_aligned(base + s - XC_SEG + 32u * l, pw);
+    load32_aligned(base + s + 32u * l, w);
+}
+
+__device__ __forceinline__ const uint8_t *desc_base(const ScanArgs &a, const uint4 &d)
+{
+    return a.P.in + (((uint64_t)uniform(d.w) << 32) | uniform(d.z));
+}
+
 __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
 {
-    extern __shared__ uint32_t smem[];
-    uint32_t *filt = smem;
+    __shared__ uint2 filt[XC_FILT_WORDS / 2];
+    __shared__ uint2 queues[SCAN_WAVES][Q_CAP];
     const uint32_t wave = threadIdx.x >> 6;
-    uint2 *queue = (uint2 *)(smem + XC_FILT_WORDS) + wave * Q_CAP;
+    uint2 *queue = queues[wave];
     const uint32_t l = lane_id();
 
-    for (uint32_t i = threadIdx.x * 4u; i < XC_FILT_WORDS; i += 4096u)
-        *(uint4 *)(filt + i) = *(const uint4 *)(a.set.filt + i);
+    for (uint32_t i = threadIdx.x * 2u; i < XC_FILT_WORDS / 2; i += 2048u)
+        *(uint4 *)(filt + i) = *(const uint4 *)(a.set.filt + 2 * i);
     __syncthreads();
 
-    for (uint32_t c = a.ck_lo + blockIdx.x * SCAN_WAVES + wave; c < a.ck_hi; c += gridDim.x * SCAN_WAVES) {
-        const uint2 ck = a.P.chunks[c];
-        const uint32_t b = ck.x, c0 = ck.y;
-        const uint32_t len = a.P.buf_len[b];
-        const uint8_t *base = a.P.in + a.P.buf_off[b];
-        const uint32_t c1 = min(c0 + a.P.chunk_len, len);
+    const uint32_t stride = gridDim.x * SCAN_WAVES;
+    uint32_t c = a.ck_lo + blockIdx.x * SCAN_WAVES + wave;
+    if (c >= a.ck_hi) return;
+
+    // chunk descriptors: {c0, c1, arena offset lo, hi}; the next one is always in flight
+    uint4 dsc = a.P.chunk_desc[c];
+    uint32_t pw[8], w[8];
+    first_blocks(desc_base(a, dsc), uniform(dsc.x), l, pw, w);
+    uint4 dn = make_uint4(0, 0, 0, 0);
+    if (c + stride < a.ck_hi) dn = a.P.chunk_desc[c + stride];
+
+    Pending pd;
+    pd.n = 0;
+    uint32_t prev_c = NONE, prev_ev = 0;
+    bool prev_dense = false;
+
+    for (;;) {
+        const uint32_t c0 = uniform(dsc.x), c1 = uniform(dsc.y);
+        const uint8_t *base = desc_base(a, dsc);
+        const bool has_next = c + stride < a.ck_hi;
         uint32_t ev_n = 0, qn = 0;
         bool dense = false;
+        uint32_t npw[8], nw[8];
+        bool next_loaded = false;
 
-        uint32_t pw[8];
-        BlockSums ps;
-        uint32_t s;
+        BlockSums ps = block_sums(pw, l);
+        uint32_t s = c0;
         if (c0 == 0) {
-            load32_aligned(base + 32u * l, pw);
-            ps = block_sums(pw, l);
-            if (len >= XC_SEG) {
-                // window ending at 2047 = the whole first block
-                const uint32_t lo = (ps.totA << 20) + (XC_SEG * ps.totA - ps.totC);
-                const uint32_t bit = filt_bit(lo);
-                const bool t = (filt[bit >> 5] >> (bit & 31u)) & 1u;
-                if (t && l == 0) queue[0] = make_uint2(XC_SEG - 1u, lo);
-                qn = t ? 1u : 0u;
-            }
+            // window ending at 2047 = the whole first block (every chunk has len >= 2048)
+            const uint32_t lo = (ps.totA << 20) + (XC_SEG * ps.totA - ps.totC);
+            const uint32_t t = filt_test(filt, lo);
+            if (t && l == 0) queue[0] = make_uint2(XC_SEG - 1u, lo);
+            qn = t;
             s = XC_SEG;
-        } else {
-            load32_aligned(base + c0 - XC_SEG + 32u * l, pw);
-            ps = block_sums(pw, l);
-            s = c0;
         }
 
         for (; s < c1; s += XC_SEG) {
-            uint32_t w[8];
-            load32_aligned(base + s + 32u * l, w);
+            // prefetch: the next block of this chunk, or the next chunk's first two blocks
+            uint32_t wn[8];
+            const bool last = s + XC_SEG >= c1;
+            if (!last) {
+                load32_aligned(base + s + XC_SEG + 32u * l, wn);
+            } else if (has_next) {
+                first_blocks(desc_base(a, dn), uniform(dn.x), l, npw, nw);
+                next_loaded = true;
+            }
             const BlockSums cs = block_sums(w, l);
             // window ending just before this lane's first position q = s + 32 l:
             // out-chunks of lanes >= l (previous block) + in-chunks of lanes < l.
@@ -155,7 +243,6 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
             uint32_t V = S2 + 0x80000000u;     // S2 + (2048 << 20)
             const uint32_t q = s + 32u * l;
             const uint32_t vmask = (q + 32u <= c1) ? 0xFFFFFFFFu : (q >= c1 ? 0u : ((1u << (c1 - q)) - 1u));
-            // two halves of 16 positions keep the live lo32 values at 16 VGPRs
 #pragma unroll
             for (int half = 0; half < 2; half++) {
                 uint32_t lo[16];
@@ -167,33 +254,85 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
                         const uint32_t ib = (w[half * 4 + d] >> (8 * k)) & 0xffu;
                         const uint32_t ob = (pw[half * 4 + d] >> (8 * k)) & 0xffu;
                         U += ib - ob;
-                        V += U - (ob << 11);
+                        V += U + (uint32_t)__mul24((int)ob, -2048);
                         const uint32_t x = (U << 20) + V;
                         lo[d * 4 + k] = x;
-                        const uint32_t bit = filt_bit(x);
-                        hit |= ((filt[bit >> 5] >> (bit & 31u)) & 1u) << (d * 4 + k);
+                        hit |= filt_test(filt, x) << (d * 4 + k);
                     }
                 }
                 hit &= vmask >> (16 * half);
-#pragma unroll
-                for (int j = 0; j < 16; j++) {
-                    const bool t = (hit >> j) & 1u;
-                    const uint64_t m = ballot(t);
-                    if (m) {
-                        if (t) queue[qn + mbcnt(m)] = make_uint2(q + (uint32_t)(16 * half + j), lo[j]);
-                        qn += (uint32_t)__popcll(m);
-                        if (qn > Q_CAP - 64u) scan_flush(a, queue, qn, c, c0, ev_n, dense);
+                if (ballot(hit != 0u)) {
+#pragma unroll 1
+                    for (uint32_t j = 0; j < 16u; j++) {
+                        const bool t = (hit >> j) & 1u;
+                        const uint64_t m = ballot(t);
+                        if (m) {
+                            if (t) queue[qn + mbcnt(m)] = make_uint2(q + 16u * half + j, lo[j]);
+                            qn = uniform(qn + (uint32_t)__popcll(m));
+                            if (qn > Q_CAP - 64u) scan_flush(a, queue, qn, c, c0, ev_n, dense);
+                        }
                     }
                 }
             }
+            // iteration boundary: finish the previous probe batch, start this one
+            if (pd.n) {
+                if (pd.c == c) {
+                    pend_complete(a, pd, ev_n, dense);
+                } else {
+                    pend_complete(a, pd, prev_ev, prev_dense);
+                    if (l == 0) a.L.cnt[prev_c] = prev_dense ? (EV_DENSE | prev_ev) : prev_ev;
+                    if (l == 0 && prev_dense) atomicAdd(&a.P.ctl[CTL_DENSE], 1u);
+                    prev_c = NONE;
+                }
+            }
+            if (qn) {
+                pend_issue(a, pd, queue, qn, c, c0);
+                qn = 0;
+            }
+            if (!last) {
 #pragma unroll
-            for (int d = 0; d < 8; d++) pw[d] = w[d];
-            ps = cs;
+                for (int d = 0; d < 8; d++) { pw[d] = w[d]; w[d] = wn[d]; }
+                ps = cs;
+            }
         }
-        if (qn) scan_flush(a, queue, qn, c, c0, ev_n, dense);
-        if (l == 0) {
-            a.L.cnt[c] = dense ? (EV_DENSE | ev_n) : ev_n;
-            if (dense) atomicAdd(&a.P.ctl[CTL_DENSE], 1u);
+        if (qn) {  // chunk whose only position is 2047: no iteration ran
+            if (pd.n) {
+                if (pd.c == c) pend_complete(a, pd, ev_n, dense);
+                else {
+                    pend_complete(a, pd, prev_ev, prev_dense);
+                    if (l == 0) a.L.cnt[prev_c] = prev_dense ? (EV_DENSE | prev_ev) : prev_ev;
+                    if (l == 0 && prev_dense) atomicAdd(&a.P.ctl[CTL_DENSE], 1u);
+                    prev_c = NONE;
+                }
+            }
+            pend_issue(a, pd, queue, qn, c, c0);
+            qn = 0;
+        }
+        // chunk end: its count is final now, or once its pending probes complete
+        if (pd.n && pd.c == c) {
+            prev_c = c;
+            prev_ev = ev_n;
+            prev_dense = dense;
+        } else {
+            if (l == 0) a.L.cnt[c] = dense ? (EV_DENSE | ev_n) : ev_n;
+            if (l == 0 && dense) atomicAdd(&a.P.ctl[CTL_DENSE], 1u);
+        }
+        if (!has_next) break;
+        c += stride;
+        dsc = dn;
+        if (next_loaded) {
+#pragma unroll
+            for (int d = 0; d < 8; d++) { pw[d] = npw[d]; w[d] = nw[d]; }
+        } else {
+            first_blocks(desc_base(a, dsc), uniform(dsc.x), l, pw, w);
+        }
+        if (c + stride < a.ck_hi) dn = a.P.chunk_desc[c + stride];
+    }
+    if (pd.n) {
+        if (pd.c == prev_c) {
+            pend_complete(a, pd, prev_ev, prev_dense);
+            if (l == 0) a.L.cnt[prev_c] = prev_dense ? (EV_DENSE | prev_ev) : prev_ev;
+            if (l == 0 && prev_dense) atomicAdd(&a.P.ctl[CTL_DENSE], 1u);
         }
     }
 }
@@ -244,9 +383,41 @@ __global__ __launch_bounds__(256) void k_resolve(ResolveArgs a)
 }
 
 // ---------------------------------------------------------------- k_walk ----------------
+// Walk cursor over one layer of one buffer: the current chunk's sorted sparse events live
+// in registers, lane i holding event i, so finding the next event is one ballot.
 struct Cursor {
-    uint32_t k, i;
+    uint32_t k, cnt, cs;  // chunk index, count|EV_DENSE, first position (uniform)
+    uint32_t pos, stat;   // lane-held event (pos = NONE past cnt)
+    uint64_t h, v;
 };
+
+__device__ __forceinline__ void cur_load(const PlanDev &P, const Layer &L, Cursor &c, uint32_t ck1)
+{
+    c.pos = NONE;
+    if (c.k >= ck1) return;
+    c.cnt = uniform(L.cnt[c.k]);
+    c.cs = uniform(P.chunks[c.k].y);
+    const uint32_t l = lane_id();
+    if (!(c.cnt & EV_DENSE) && l < c.cnt) {
+        const uint32_t i = c.k * EV_CAP + l;
+        c.pos = L.pos[i];
+        c.stat = L.stat[i];
+        c.h = L.h[i];
+        c.v = L.val[i];
+    }
+}
+
+__device__ __forceinline__ Cursor cur_begin(const PlanDev &P, const Layer &L, uint32_t ck0, uint32_t ck1)
+{
+    Cursor c;
+    c.k = ck0;
+    c.cnt = 0;
+    c.cs = 0;
+    c.stat = 0;
+    c.h = c.v = 0;
+    cur_load(P, L, c, ck1);
+    return c;
+}
 
 // First set bit at chunk offset >= from, or NONE.
 __device__ __forceinline__ uint32_t dense_find(const uint32_t *bits, uint32_t from, uint32_t W)
@@ -256,7 +427,6 @@ __device__ __forceinline__ uint32_t dense_find(const uint32_t *bits, uint32_t fr
         const uint32_t wi = w0 + l;
         uint32_t v = wi < W ? bits[wi] : 0u;
         if (wi == (from >> 5)) v &= ~0u << (from & 31u);
-        if (wi < (from >> 5)) v = 0u;
         const uint64_t m = ballot(v != 0u);
         if (m) {
             const int f = __ffsll((unsigned long long)m) - 1;
@@ -267,26 +437,24 @@ __device__ __forceinline__ uint32_t dense_find(const uint32_t *bits, uint32_t fr
     return NONE;
 }
 
-// Next event position >= p in layer L for the chunks [cur.k, ck1) of one buffer.
+// Next event position >= p in the layer (chunks [cur.k, ck1) of one buffer), or NONE.
 __device__ __forceinline__ uint32_t next_event(const PlanDev &P, const Layer &L, Cursor &cur, uint32_t ck1,
                                                uint32_t p)
 {
     const uint32_t W = P.chunk_len / 32u;
     while (cur.k < ck1) {
-        const uint32_t cnt = uniform(L.cnt[cur.k]);
-        const uint32_t cs = uniform(P.chunks[cur.k].y);
-        if (cnt & EV_DENSE) {
-            const uint32_t from = p > cs ? p - cs : 0u;
+        if (cur.cnt & EV_DENSE) {
+            const uint32_t from = p > cur.cs ? p - cur.cs : 0u;
             if (from < P.chunk_len) {
                 const uint32_t r = dense_find(L.bits + (size_t)cur.k * W, from, W);
-                if (r != NONE) return cs + r;
+                if (r != NONE) return cur.cs + r;
             }
         } else {
-            while (cur.i < cnt && uniform(L.pos[cur.k * EV_CAP + cur.i]) < p) cur.i++;
-            if (cur.i < cnt) return uniform(L.pos[cur.k * EV_CAP + cur.i]);
+            const uint64_t m = ballot(cur.pos != NONE && cur.pos >= p);
+            if (m) return readlane(cur.pos, __ffsll((unsigned long long)m) - 1);
         }
         cur.k++;
-        cur.i = 0;
+        cur_load(P, L, cur, ck1);
     }
     return NONE;
 }
@@ -296,7 +464,12 @@ struct EvInfo {
     uint64_t h, v;
 };
 
-// Event of layer L exactly at q (cursor already advanced to >= q by next_event), or st=NONE.
+__device__ __forceinline__ uint64_t readlane64(uint64_t x, int l)
+{
+    return ((uint64_t)readlane((uint32_t)(x >> 32), l) << 32) | readlane((uint32_t)x, l);
+}
+
+// Event of the layer exactly at q, or st = NONE.
 __device__ __forceinline__ EvInfo event_at(const PlanDev &P, const Layer &L, Cursor &cur, uint32_t ck1, uint32_t q,
                                            int dmode, const uint8_t *base)
 {
@@ -305,20 +478,16 @@ __device__ __forceinline__ EvInfo event_at(const PlanDev &P, const Layer &L, Cur
     e.h = 0;
     e.v = 0;
     if (next_event(P, L, cur, ck1, q) != q) return e;
-    const uint32_t cnt = uniform(L.cnt[cur.k]);
-    if (cnt & EV_DENSE) {
+    if (cur.cnt & EV_DENSE) {
         e.st = resolve_one(P, dmode, base + q - (XC_SEG - 1u), &e.h, &e.v);
     } else {
-        const uint32_t idx = cur.k * EV_CAP + cur.i;
-        e.st = uniform(L.stat[idx]);
-        e.h = L.h[idx];
-        e.v = L.val[idx];
-        e.h = ((uint64_t)uniform((uint32_t)(e.h >> 32)) << 32) | uniform((uint32_t)e.h);
-        e.v = ((uint64_t)uniform((uint32_t)(e.v >> 32)) << 32) | uniform((uint32_t)e.v);
+        const int f = __ffsll((unsigned long long)ballot(cur.pos == q)) - 1;
+        e.st = readlane(cur.stat, f);
+        e.h = readlane64(cur.h, f);
+        e.v = readlane64(cur.v, f);
     }
     return e;
 }
-
 
 constexpr uint32_t R_MISS = 0, R_HIT = 1, R_COLL = 2;
 
@@ -336,7 +505,8 @@ __global__ __launch_bounds__(64) void k_walk(WalkArgs a)
     const uint32_t ck0 = P.buf_chunk0[b], ck1 = P.buf_chunk0[b + 1];
     const uint32_t tb = P.tok_base[b];
     const uint32_t tcap = 2u * (len / XC_SEG) + 3u;
-    Cursor cs = {ck0, 0}, cd = {ck0, 0};
+    Cursor cs = cur_begin(P, P.S, ck0, ck1);
+    Cursor cd = cur_begin(P, P.D, ck0, a.use_d ? ck1 : ck0);
     uint32_t ntok = 0, nd = 0;
     uint32_t basep = 0;
     int cand = -1;
@@ -345,7 +515,10 @@ __global__ __launch_bounds__(64) void k_walk(WalkArgs a)
     uint32_t p = XC_SEG - 1u;
     bool cross = false;
 
+    uint32_t n_ext = 0, n_ref = 0;
     auto emit = [&](uint32_t op, uint32_t lb, uint32_t le, uint32_t seg, uint32_t dpos, uint64_t h) {
+        n_ext += op == OP_EXTRACT ? 1u : 0u;
+        n_ref += op == OP_REF ? 1u : 0u;
         if (ntok < tcap && l == 0) {
             P.tok_op[tb + ntok] = op;
             P.tok_lb[tb + ntok] = lb;
@@ -436,6 +609,8 @@ __global__ __launch_bounds__(64) void k_walk(WalkArgs a)
     emit(OP_END, basep, len, 0, 0, 0);
     if (l == 0) {
         P.tok_cnt[b] = ntok;
+        P.buf_next[b] = n_ext;
+        P.buf_nref[b] = n_ref;
         if (ntok > tcap) atomicOr(&P.ctl[CTL_ERROR], ERR_TOKENS);
         if (cross) atomicMin(&P.ctl[CTL_FIRST_CROSS], b);
     }
@@ -459,7 +634,9 @@ __global__ __launch_bounds__(64) void k_declhash(DeclArgs a)
         if (lane_id() == 0) {
             P.tok_h[tb + t] = h;
             const uint64_t v = ((uint64_t)b << 32) | P.tok_dpos[tb + t];
-            if (set_insert(P.dset, h, v, true, nullptr, nullptr)) atomicOr(&P.ctl[CTL_GREW], 1u);
+            if (set_insert(P.dset, h, v, true, nullptr, nullptr) &&
+                __hip_atomic_load(&P.ctl[CTL_GREW], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+                atomicOr(&P.ctl[CTL_GREW], 1u);
         }
     }
 }
@@ -509,6 +686,7 @@ __device__ __forceinline__ uint32_t write_escaped(uint8_t *dst, const uint8_t *p
 __global__ __launch_bounds__(256) void k_emit(EmitArgs a)
 {
     __shared__ uint32_t sz[MAX_TOK];
+    __shared__ uint32_t ord[MAX_TOK];
     const PlanDev &P = a.P;
     const uint32_t b = a.j0 + blockIdx.x;
     if (b >= a.j1) return;
@@ -520,22 +698,26 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a)
     for (uint32_t t = wave; t < n; t += 4u) {
         const uint32_t lb = P.tok_lb[tb + t], le = P.tok_le[tb + t], op = P.tok_op[tb + t];
         const uint32_t esc = (le - lb) + count_magic(base + lb, le - lb);
-        if (l == 0) sz[t] = esc + (op == OP_EXTRACT ? 2u + XC_SEG : op == OP_REF ? 10u : 0u);
+        if (l == 0) {
+            sz[t] = esc + (op == OP_EXTRACT ? 2u + XC_SEG : op == OP_REF ? 10u : 0u);
+            ord[t] = op == OP_EXTRACT ? 1u : 0u;
+        }
     }
     __syncthreads();
     if (wave == 0) {
-        uint32_t carry = 0;
+        uint32_t carry = 0, ocarry = 0;
         for (uint32_t t0 = 0; t0 < n; t0 += 64u) {
             const uint32_t t = t0 + l;
-            const uint32_t v = t < n ? sz[t] : 0u;
-            const uint32_t inc = wave_incl_scan(v);
-            if (t < n) sz[t] = carry + inc - v;
+            const uint32_t v = t < n ? sz[t] : 0u, o = t < n ? ord[t] : 0u;
+            const uint32_t inc = wave_incl_scan(v), oinc = wave_incl_scan(o);
+            if (t < n) { sz[t] = carry + inc - v; ord[t] = ocarry + oinc - o; }
             carry += readlane(inc, 63);
+            ocarry += readlane(oinc, 63);
         }
         if (l == 0) P.out_len[b] = carry;
     }
     __syncthreads();
-    uint32_t n_ext = 0, n_ref = 0;
+    const uint32_t slot0 = P.buf_slot[b];
     for (uint32_t t = wave; t < n; t += 4u) {
         const uint32_t lb = P.tok_lb[tb + t], le = P.tok_le[tb + t], op = P.tok_op[tb + t];
         uint8_t *o = out + sz[t];
@@ -543,15 +725,12 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a)
         if (op == OP_REF) {
             const uint64_t h = P.tok_h[tb + t];
             if (l < 10) o[l] = l == 0 ? (uint8_t)XC_MAGIC : l == 1 ? (uint8_t)OP_REF : (uint8_t)(h >> (8 * (9 - l)));
-            n_ref++;
         } else if (op == OP_EXTRACT) {
             const uint32_t seg = P.tok_seg[tb + t];
             if (l == 0) { o[0] = (uint8_t)XC_MAGIC; o[1] = (uint8_t)OP_EXTRACT; }
             wave_copy(o + 2, base + seg, XC_SEG);
-            // XCodecMemoryCache::enter (xcodec_cache.h:182-188)
-            uint32_t idx = 0;
-            if (l == 0) idx = atomicAdd(P.seg_count, 1u);
-            idx = readlane(idx, 0);
+            // XCodecMemoryCache::enter (xcodec_cache.h:182-188) into the slot k_alloc reserved
+            const uint32_t idx = slot0 + ord[t];
             if (idx < P.seg_cap) {
                 wave_copy(P.segs + (size_t)idx * XC_SEG, base + seg, XC_SEG);
                 if (l == 0) {
@@ -562,12 +741,48 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a)
             } else if (l == 0) {
                 atomicOr(&P.ctl[CTL_ERROR], ERR_CAPACITY);
             }
-            n_ext++;
         }
     }
-    if (l == 0) {
-        if (n_ext) atomicAdd(&P.ctl[CTL_NEXTRACT], n_ext);
-        if (n_ref) atomicAdd(&P.ctl[CTL_NREF], n_ref);
+}
+
+// One workgroup: cache slots for the declarations of buffers [j0, j1) in buffer order
+// (exclusive prefix of buf_next on top of the current segment count), plus run totals.
+__global__ __launch_bounds__(1024) void k_alloc(EmitArgs a)
+{
+    __shared__ uint32_t wsum[16][2];
+    __shared__ uint32_t carry[2];
+    const PlanDev &P = a.P;
+    const uint32_t wave = threadIdx.x >> 6, l = lane_id();
+    if (threadIdx.x == 0) { carry[0] = *P.seg_count; carry[1] = 0; }
+    __syncthreads();
+    const uint32_t start = carry[0];
+    uint32_t nref_tot = 0;
+    for (uint32_t b0 = a.j0; b0 < a.j1; b0 += 1024u) {
+        const uint32_t b = b0 + threadIdx.x;
+        const uint32_t v = b < a.j1 ? P.buf_next[b] : 0u;
+        const uint32_t r = b < a.j1 ? P.buf_nref[b] : 0u;
+        const uint32_t inc = wave_incl_scan(v);
+        const uint32_t rs = wave_sum(r);
+        if (l == 63) { wsum[wave][0] = inc; wsum[wave][1] = rs; }
+        __syncthreads();
+        uint32_t off = carry[0];
+        for (uint32_t k = 0; k < wave; k++) off += wsum[k][0];
+        if (b < a.j1) P.buf_slot[b] = off + inc - v;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t tot = 0, rt = 0;
+            for (uint32_t k = 0; k < 16; k++) { tot += wsum[k][0]; rt += wsum[k][1]; }
+            carry[0] += tot;
+            carry[1] += rt;
+        }
+        __syncthreads();
+    }
+    (void)nref_tot;
+    if (threadIdx.x == 0) {
+        *P.seg_count = carry[0];
+        P.ctl[CTL_NEXTRACT] += carry[0] - start;
+        P.ctl[CTL_NREF] += carry[1];
+        if (carry[0] > P.seg_cap) P.ctl[CTL_ERROR] |= ERR_CAPACITY;
     }
 }
 
@@ -633,6 +848,17 @@ __global__ __launch_bounds__(64) void k_window_hashes(const uint8_t *in, uint32_
 // Cache restore: clear every table slot entered after the snapshot.
 __global__ void k_undo(DevSet cache, const uint2 *undo, uint32_t from, uint32_t to)
 {
+    for (uint32_t i = from + blockIdx.x * blockDim.x + threadIdx.x; i < to; i += gridDim.x * blockDim.x) {
+        const uint2 u = undo[i];
+        cache.keys[u.x] = XC_EMPTY64;
+        if (u.y != NONE) cache.lo_keys[u.y] = 0u;
+    }
+}
+
+// Same, reading the current count on the device (no host round trip).
+__global__ void k_undo_dev(DevSet cache, const uint2 *undo, uint32_t from, const uint32_t *count, uint32_t cap)
+{
+    const uint32_t to = min(*count, cap);
     for (uint32_t i = from + blockIdx.x * blockDim.x + threadIdx.x; i < to; i += gridDim.x * blockDim.x) {
         const uint2 u = undo[i];
         cache.keys[u.x] = XC_EMPTY64;

@@ -6,7 +6,7 @@
 
 namespace xc {
 
-constexpr uint32_t EV_CAP = 32;          // sparse events per scan chunk before it turns dense
+constexpr uint32_t EV_CAP = 64;          // sparse events per scan chunk before it turns dense
 constexpr uint32_t EV_DENSE = 0x80000000u;
 constexpr uint32_t Q_CAP = 128;          // per-wave LDS queue of level-1 filter positives
 constexpr uint32_t SCAN_WAVES = 16;      // waves per scan workgroup (1024 threads)
@@ -54,6 +54,7 @@ struct PlanDev {
     const uint32_t *buf_len;
     uint32_t nb;
     const uint2 *chunks;       // (buffer, first position) per chunk
+    const uint4 *chunk_desc;   // (first position, end position, arena offset lo, hi) per chunk
     const uint32_t *buf_chunk0;  // [nb+1]
     uint32_t chunk_len;
     Layer S, D;
@@ -67,6 +68,9 @@ struct PlanDev {
     uint32_t *tok_cnt;
     uint32_t *tok_lb, *tok_le, *tok_seg, *tok_op, *tok_dpos;
     uint64_t *tok_h;
+    uint32_t *buf_next;   // [nb] EXTRACT tokens of the buffer (walk)
+    uint32_t *buf_nref;   // [nb] REF tokens of the buffer (walk)
+    uint32_t *buf_slot;   // [nb] first cache slot of the buffer's declarations (k_alloc)
     uint8_t *out;
     const uint64_t *out_off;
     uint64_t *out_len;
@@ -105,9 +109,11 @@ __global__ void k_resolve(ResolveArgs a);
 __global__ void k_walk(WalkArgs a);
 __global__ void k_declhash(DeclArgs a);
 __global__ void k_emit(EmitArgs a);
+__global__ void k_alloc(EmitArgs a);
 __global__ void k_hash_segments(const uint8_t *segs, uint64_t n, uint64_t *out);
 __global__ void k_window_hashes(const uint8_t *in, uint32_t n, uint64_t *out);
 __global__ void k_undo(DevSet cache, const uint2 *undo, uint32_t from, uint32_t to);
+__global__ void k_undo_dev(DevSet cache, const uint2 *undo, uint32_t from, const uint32_t *count, uint32_t cap);
 __global__ void k_enter_one(PlanDev P, uint64_t h, const uint8_t *seg);
 __global__ void k_lookup_one(PlanDev P, uint64_t h, uint8_t *out, uint32_t *found);
 __global__ void k_selftest(uint32_t *err);

@@ -75,7 +75,6 @@ extern "C" int xc_ctx_create(int dev, xc_ctx **out)
     c->n_cu = prop.multiProcessorCount;
     HIPCHK(hipMalloc(&c->d_scratch, 4096));
     HIPCHK(hipMalloc(&c->d_seg, 4096));
-    HIPCHK(hipFuncSetAttribute((const void *)k_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)SCAN_LDS));
     *out = c;
     return XC_OK;
 }
@@ -161,6 +160,7 @@ struct xc_cache {
     uint32_t snap_count = 0;
     uint32_t *snap_filt = nullptr;
     uint32_t *snap_lo_zero = nullptr;
+    uint32_t *snap_count_dev = nullptr;
 };
 
 static PlanDev cache_plandev(xc_cache *c)
@@ -190,6 +190,7 @@ extern "C" int xc_cache_create(xc_ctx *ctx, uint64_t cap, xc_cache **out)
     HIPCHK(hipMalloc(&c->ctl, CTL_WORDS * 4));
     HIPCHK(hipMalloc(&c->snap_filt, XC_FILT_WORDS * 4));
     HIPCHK(hipMalloc(&c->snap_lo_zero, 4));
+    HIPCHK(hipMalloc(&c->snap_count_dev, 4));
     if ((rc = c->set.clear(ctx->stream))) return rc;
     HIPCHK(hipMemsetAsync(c->count, 0, 4, ctx->stream));
     HIPCHK(hipMemsetAsync(c->ctl, 0, CTL_WORDS * 4, ctx->stream));
@@ -210,6 +211,7 @@ extern "C" int xc_cache_destroy(xc_cache *c)
     hipFree(c->ctl);
     hipFree(c->snap_filt);
     hipFree(c->snap_lo_zero);
+    hipFree(c->snap_count_dev);
     delete c;
     return XC_OK;
 }
@@ -241,6 +243,7 @@ extern "C" int xc_cache_snapshot(xc_cache *c)
     hipStream_t s = c->ctx->stream;
     HIPCHK(hipMemcpyAsync(c->snap_filt, c->set.d.filt, XC_FILT_WORDS * 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(c->snap_lo_zero, c->set.d.lo_zero, 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->snap_count_dev, c->count, 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipStreamSynchronize(s));
     c->has_snap = true;
     return XC_OK;
@@ -261,6 +264,26 @@ static int cache_restore_async(xc_cache *c, uint32_t cur_count)
     HIPCHK(hipMemcpyAsync(c->set.d.filt, c->snap_filt, XC_FILT_WORDS * 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(c->set.d.lo_zero, c->snap_lo_zero, 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(c->count, &c->snap_count, 4, hipMemcpyHostToDevice, s));
+    return XC_OK;
+}
+
+extern "C" int xc_cache_restore_async(xc_cache *c)
+{
+    if (!c) return fail(XC_EINVAL, "null");
+    if (!c->has_snap) return fail(XC_EINVAL, "no snapshot");
+    int rc = set_dev(c->ctx);
+    if (rc) return rc;
+    hipStream_t s = c->ctx->stream;
+    if (c->cap > c->snap_count) {
+        uint32_t n = (uint32_t)(c->cap - c->snap_count);
+        uint32_t blocks = std::min<uint32_t>((n + 255) / 256, 2048);
+        hipLaunchKernelGGL(k_undo_dev, dim3(blocks), dim3(256), 0, s, c->set.d, (const uint2 *)c->undo,
+                           c->snap_count, (const uint32_t *)c->count, (uint32_t)c->cap);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipMemcpyAsync(c->set.d.filt, c->snap_filt, XC_FILT_WORDS * 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->set.d.lo_zero, c->snap_lo_zero, 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->count, c->snap_count_dev, 4, hipMemcpyDeviceToDevice, s));
     return XC_OK;
 }
 
@@ -339,7 +362,7 @@ extern "C" int xc_window_hashes(xc_ctx *ctx, const uint8_t *d_in, uint64_t n, ui
 }
 
 // ------------------------------------------------------------------ plan ----------
-static const uint32_t CHUNK_LEN = 8192;
+static const uint32_t CHUNK_LEN = 16384;
 static const uint64_t SUB_BYTES = 256ull << 20;  // sub-batch: bound on input bytes
 static const uint32_t SUB_BUFS = 8192;           // sub-batch: bound on buffers
 static const uint32_t MAX_ROUNDS = 64;
@@ -383,8 +406,61 @@ struct xc_plan {
     uint64_t *d_buf_off, *d_out_off;
     uint32_t *d_buf_len, *d_chunk0, *d_tok_base;
     uint2 *d_chunks;
+    uint4 *d_desc;
     xc_run_stats stats{};
+    // per-kernel HIP-event timing
+    bool timing = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev_live;
+    xc_kernel_times ktimes{};
+    std::vector<uint64_t> chunk_bytes;  // prefix of input bytes covered by chunks
 };
+
+static hipEvent_t ev_get(xc_plan *p)
+{
+    if (p->ev_pool.empty()) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        return e;
+    }
+    hipEvent_t e = p->ev_pool.back();
+    p->ev_pool.pop_back();
+    return e;
+}
+
+struct KSpan {
+    xc_plan *p;
+    int k;
+    hipEvent_t a = nullptr, b = nullptr;
+    KSpan(xc_plan *p_, int k_) : p(p_), k(k_)
+    {
+        if (!p->timing) return;
+        a = ev_get(p);
+        b = ev_get(p);
+        if (a) hipEventRecord(a, p->cache->ctx->stream);
+    }
+    ~KSpan()
+    {
+        if (!a || !b) return;
+        hipEventRecord(b, p->cache->ctx->stream);
+        p->ev_live.push_back({k, {a, b}});
+    }
+};
+
+// After a stream sync: fold the recorded spans into ktimes.
+static void ev_collect(xc_plan *p)
+{
+    for (auto &x : p->ev_live) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, x.second.first, x.second.second) == hipSuccess) {
+            p->ktimes.ms[x.first] += ms;
+            p->ktimes.launches[x.first] += 1;
+        }
+        p->ev_pool.push_back(x.second.first);
+        p->ev_pool.push_back(x.second.second);
+    }
+    p->ev_live.clear();
+}
 
 extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint64_t nbuf, xc_plan **out)
 {
@@ -400,6 +476,7 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     p->out_off.resize(nbuf);
     std::vector<uint32_t> blen(nbuf), chunk0(nbuf + 1), tok_base(nbuf + 1);
     std::vector<uint2> chunks;
+    std::vector<uint4> descs;
     uint64_t io = 0, oo = 0;
     uint64_t toks = 0;
     for (uint64_t i = 0; i < nbuf; i++) {
@@ -412,7 +489,11 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
         oo += (2 * n + 16 + 255) / 256 * 256;
         chunk0[i] = (uint32_t)chunks.size();
         if (n >= XC_SEG)
-            for (uint32_t s = 0; s < n; s += CHUNK_LEN) chunks.push_back(make_uint2((uint32_t)i, s));
+            for (uint32_t s = 0; s < n; s += CHUNK_LEN) {
+                chunks.push_back(make_uint2((uint32_t)i, s));
+                descs.push_back(make_uint4(s, (uint32_t)std::min<uint64_t>(s + CHUNK_LEN, n),
+                                           (uint32_t)p->in_off[i], (uint32_t)(p->in_off[i] >> 32)));
+            }
         tok_base[i] = (uint32_t)toks;
         toks += 2 * (n / XC_SEG) + 3;
     }
@@ -422,6 +503,12 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     p->out_bytes = oo + 256;
     p->nchunks = (uint32_t)chunks.size();
     p->chunk0 = chunk0;
+    p->chunk_bytes.assign(chunks.size() + 1, 0);
+    for (size_t k = 0; k < chunks.size(); k++) {
+        uint64_t n = lengths[chunks[k].x];
+        uint64_t e = std::min<uint64_t>(chunks[k].y + CHUNK_LEN, n);
+        p->chunk_bytes[k + 1] = p->chunk_bytes[k] + (e - chunks[k].y);
+    }
     // sub-batches
     p->sub.push_back(0);
     {
@@ -454,6 +541,7 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     HIPCHK(hipMalloc(&p->d_chunk0, (nbuf + 1) * 4));
     HIPCHK(hipMalloc(&p->d_tok_base, (nbuf + 1) * 4));
     HIPCHK(hipMalloc(&p->d_chunks, std::max<size_t>(chunks.size(), 1) * sizeof(uint2)));
+    HIPCHK(hipMalloc(&p->d_desc, std::max<size_t>(chunks.size(), 1) * sizeof(uint4)));
     hipStream_t s = c->ctx->stream;
     if (nbuf) {
         HIPCHK(hipMemcpyAsync(p->d_buf_off, p->in_off.data(), nbuf * 8, hipMemcpyHostToDevice, s));
@@ -462,8 +550,10 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
         HIPCHK(hipMemcpyAsync(p->d_tok_base, tok_base.data(), nbuf * 4, hipMemcpyHostToDevice, s));
     }
     HIPCHK(hipMemcpyAsync(p->d_chunk0, chunk0.data(), (nbuf + 1) * 4, hipMemcpyHostToDevice, s));
-    if (!chunks.empty())
+    if (!chunks.empty()) {
         HIPCHK(hipMemcpyAsync(p->d_chunks, chunks.data(), chunks.size() * sizeof(uint2), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(p->d_desc, descs.data(), descs.size() * sizeof(uint4), hipMemcpyHostToDevice, s));
+    }
 
     PlanDev &P = p->P;
     P = cache_plandev(c);
@@ -471,6 +561,7 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     P.buf_len = p->d_buf_len;
     P.nb = (uint32_t)nbuf;
     P.chunks = p->d_chunks;
+    P.chunk_desc = p->d_desc;
     P.buf_chunk0 = p->d_chunk0;
     P.chunk_len = CHUNK_LEN;
     P.S = p->S.d;
@@ -485,6 +576,9 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     HIPCHK(hipMalloc(&P.tok_op, nt * 4));
     HIPCHK(hipMalloc(&P.tok_dpos, nt * 4));
     HIPCHK(hipMalloc(&P.tok_h, nt * 8));
+    HIPCHK(hipMalloc(&P.buf_next, nb1 * 4));
+    HIPCHK(hipMalloc(&P.buf_nref, nb1 * 4));
+    HIPCHK(hipMalloc(&P.buf_slot, nb1 * 4));
     HIPCHK(hipMalloc(&P.ctl, CTL_WORDS * 4));
     P.out_off = p->d_out_off;
     HIPCHK(hipStreamSynchronize(s));
@@ -506,6 +600,7 @@ extern "C" int xc_plan_destroy(xc_plan *p)
     hipFree(p->d_chunk0);
     hipFree(p->d_tok_base);
     hipFree(p->d_chunks);
+    hipFree(p->d_desc);
     hipFree(p->P.tok_cnt);
     hipFree(p->P.tok_lb);
     hipFree(p->P.tok_le);
@@ -513,7 +608,12 @@ extern "C" int xc_plan_destroy(xc_plan *p)
     hipFree(p->P.tok_op);
     hipFree(p->P.tok_dpos);
     hipFree(p->P.tok_h);
+    hipFree(p->P.buf_next);
+    hipFree(p->P.buf_nref);
+    hipFree(p->P.buf_slot);
     hipFree(p->P.ctl);
+    for (auto &x : p->ev_live) { hipEventDestroy(x.second.first); hipEventDestroy(x.second.second); }
+    for (auto e : p->ev_pool) hipEventDestroy(e);
     delete p;
     return XC_OK;
 }
@@ -529,6 +629,21 @@ extern "C" int xc_plan_layout(xc_plan *p, uint64_t *in_off, uint64_t *out_off, u
     return XC_OK;
 }
 
+extern "C" int xc_plan_set_timing(xc_plan *p, int enable)
+{
+    if (!p) return fail(XC_EINVAL, "null");
+    p->timing = enable != 0;
+    return XC_OK;
+}
+
+extern "C" int xc_plan_kernel_times(xc_plan *p, xc_kernel_times *out, int reset)
+{
+    if (!p) return fail(XC_EINVAL, "null");
+    if (out) *out = p->ktimes;
+    if (reset) p->ktimes = xc_kernel_times{};
+    return XC_OK;
+}
+
 extern "C" int xc_plan_stats(xc_plan *p, xc_run_stats *st)
 {
     if (!p || !st) return fail(XC_EINVAL, "null");
@@ -541,6 +656,7 @@ static int read_ctl(xc_plan *p, uint32_t *ctl)
     hipStream_t s = p->cache->ctx->stream;
     HIPCHK(hipMemcpyAsync(ctl, p->P.ctl, CTL_WORDS * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    ev_collect(p);
     return XC_OK;
 }
 
@@ -549,9 +665,11 @@ static int launch_scan(xc_plan *p, const Layer &L, const DevSet &set, uint32_t c
     if (ck_hi <= ck_lo) return XC_OK;
     xc_ctx *ctx = p->cache->ctx;
     ScanArgs a{p->P, L, set, ck_lo, ck_hi};
+    KSpan span(p, XC_K_SCAN);
+    if (p->timing) p->ktimes.scan_bytes += p->chunk_bytes[ck_hi] - p->chunk_bytes[ck_lo];
     uint32_t need = (ck_hi - ck_lo + SCAN_WAVES - 1) / SCAN_WAVES;
     uint32_t grid = std::min<uint32_t>(need, (uint32_t)ctx->n_cu);
-    hipLaunchKernelGGL(k_scan, dim3(grid), dim3(64 * SCAN_WAVES), SCAN_LDS, ctx->stream, a);
+    hipLaunchKernelGGL(k_scan, dim3(grid), dim3(64 * SCAN_WAVES), 0, ctx->stream, a);
     HIPCHK(hipGetLastError());
     return XC_OK;
 }
@@ -560,6 +678,7 @@ static int launch_resolve(xc_plan *p, const Layer &L, int dmode, uint32_t ck_lo,
 {
     if (ck_hi <= ck_lo) return XC_OK;
     ResolveArgs a{p->P, L, dmode, ck_lo, ck_hi};
+    KSpan span(p, XC_K_RESOLVE);
     hipLaunchKernelGGL(k_resolve, dim3((ck_hi - ck_lo + 3) / 4), dim3(256), 0, p->cache->ctx->stream, a);
     HIPCHK(hipGetLastError());
     return XC_OK;
@@ -572,11 +691,17 @@ static int launch_walk_round(xc_plan *p, uint32_t j0, uint32_t j1, int use_d)
     HIPCHK(hipMemsetAsync(p->P.ctl + CTL_GREW, 0, 4, s));
     HIPCHK(hipMemcpyAsync(p->P.ctl + CTL_FIRST_CROSS, &none, 4, hipMemcpyHostToDevice, s));
     WalkArgs w{p->P, j0, j1, use_d};
-    hipLaunchKernelGGL(k_walk, dim3(j1 - j0), dim3(64), 0, s, w);
-    HIPCHK(hipGetLastError());
+    {
+        KSpan span(p, XC_K_WALK);
+        hipLaunchKernelGGL(k_walk, dim3(j1 - j0), dim3(64), 0, s, w);
+        HIPCHK(hipGetLastError());
+    }
     DeclArgs d{p->P, j0, j1};
-    hipLaunchKernelGGL(k_declhash, dim3(j1 - j0, 8), dim3(64), 0, s, d);
-    HIPCHK(hipGetLastError());
+    {
+        KSpan span(p, XC_K_DECLHASH);
+        hipLaunchKernelGGL(k_declhash, dim3(j1 - j0, 8), dim3(64), 0, s, d);
+        HIPCHK(hipGetLastError());
+    }
     p->stats.walk_rounds++;
     return XC_OK;
 }
@@ -619,12 +744,18 @@ extern "C" int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, ui
             uint32_t jc = std::min<uint32_t>(ctl[CTL_FIRST_CROSS], s1);
             if (jc <= j0) jc = j0 + 1;  // cannot happen (buffer j0 has no earlier buffer); progress guard
             EmitArgs e{p->P, j0, jc};
-            hipLaunchKernelGGL(k_emit, dim3(jc - j0), dim3(256), 0, s, e);
+            hipLaunchKernelGGL(k_alloc, dim3(1), dim3(1024), 0, s, e);
             HIPCHK(hipGetLastError());
+            {
+                KSpan span(p, XC_K_EMIT);
+                hipLaunchKernelGGL(k_emit, dim3(jc - j0), dim3(256), 0, s, e);
+                HIPCHK(hipGetLastError());
+            }
             j0 = jc;
         }
     }
     if ((rc = read_ctl(p, ctl))) return rc;
+    for (uint64_t i = 0; i < p->nb; i++) p->stats.in_bytes += p->len[i];
     p->stats.n_extract = ctl[CTL_NEXTRACT];
     p->stats.n_ref = ctl[CTL_NREF];
     p->stats.dense_chunks = ctl[CTL_DENSE];

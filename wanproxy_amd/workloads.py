@@ -98,6 +98,38 @@ def repeat_buffers(count: int, seed: int, repeat_pct: int = 50, slots: int = 32,
     return out
 
 
+def gen_segments(seeds: np.ndarray, seg: int = SEG) -> np.ndarray:
+    """Vectorised ``gen(seed, seg)`` for many seeds -> (len(seeds), seg) uint8."""
+    seeds = np.asarray(seeds, dtype=np.uint64)
+    words = seg // 8
+    out = np.empty((len(seeds), seg), dtype=np.uint8)
+    k = np.arange(1, words + 1, dtype=np.uint64) * GAMMA
+    with np.errstate(over="ignore"):
+        for i in range(0, len(seeds), 8192):
+            z = _mix(seeds[i:i + 8192, None] + k[None, :])
+            out[i:i + 8192] = z.astype("<u8").view(np.uint8).reshape(-1, seg)
+    return out
+
+
+def repeat_shard(total: int, seed: int, rank: int = 0, world: int = 1, repeat_pct: int = 50,
+                 slots: int = 32, np_segments: int = POOL_SEGMENTS,
+                 pool_bytes: np.ndarray | None = None) -> np.ndarray:
+    """cfg5: buffers i = rank, rank + world, ... of the ``total``-buffer repeat workload
+    (same draws as :func:`repeat_buffers`), as an array (n_local, slots * SEG)."""
+    p = (pool(np_segments) if pool_bytes is None else pool_bytes).reshape(np_segments, SEG)
+    draws = SplitMix64(seed).take(total * slots).reshape(total, slots)[rank::world]
+    if repeat_pct == 50:
+        rep = (draws & np.uint64(1)).astype(bool)
+    else:
+        rep = (draws % np.uint64(10)) < np.uint64(9)
+    out = np.empty((draws.shape[0], slots, SEG), dtype=np.uint8)
+    idx = ((draws >> np.uint64(1)) % np.uint64(np_segments)).astype(np.int64)
+    out[rep] = p[idx[rep]]
+    fresh = ~rep
+    out[fresh] = gen_segments(draws[fresh])
+    return out.reshape(draws.shape[0], slots * SEG)
+
+
 def pack(buffers: list[np.ndarray], align: int = 256) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
     """Concatenate buffers into one arena with ``align``-byte aligned starts.
 

@@ -26,12 +26,19 @@ SYMBOLS = [
     "xc_cache_restore", "xc_cache_lookup", "xc_cache_enter", "xc_hash_segments",
     "xc_window_hashes", "xc_encode_plan_create", "xc_plan_destroy", "xc_plan_layout",
     "xc_encode_run", "xc_encode_batch_host", "xc_plan_stats", "xc_decode_batch_host",
-    "xc_selftest", "xc_last_error",
+    "xc_selftest", "xc_last_error", "xc_cache_restore_async", "xc_plan_set_timing",
+    "xc_plan_kernel_times",
 ]
+
+KERNELS = ["scan", "resolve", "walk", "declhash", "emit"]
 
 
 class XCodecError(RuntimeError):
     pass
+
+
+class KernelTimes(C.Structure):
+    _fields_ = [("ms", C.c_double * 5), ("launches", C.c_uint64 * 5), ("scan_bytes", C.c_uint64)]
 
 
 class RunStats(C.Structure):
@@ -90,6 +97,9 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.xc_decode_batch_host.argtypes = [_vp, _u8p, _u64p, _u64p, C.c_uint64, _u8p, _u64p, _u64p,
                                          _u64p, _u64p, _i32p, _u64p, _i32p]
     lib.xc_selftest.argtypes = [_vp]
+    lib.xc_cache_restore_async.argtypes = [_vp]
+    lib.xc_plan_set_timing.argtypes = [_vp, C.c_int]
+    lib.xc_plan_kernel_times.argtypes = [_vp, C.POINTER(KernelTimes), C.c_int]
     _LIB = lib
     return lib
 
@@ -187,6 +197,10 @@ class XCodecCache:
     def restore(self) -> None:
         _check(load_library().xc_cache_restore(self.h))
 
+    def restore_async(self) -> None:
+        """Enqueue the restore on the context stream (no host synchronisation)."""
+        _check(load_library().xc_cache_restore_async(self.h))
+
     def close(self) -> None:
         if getattr(self, "h", None):
             load_library().xc_cache_destroy(self.h)
@@ -266,6 +280,16 @@ class EncodePlan:
 
     def run(self, d_in: int, d_out: int, d_len: int) -> None:
         _check(load_library().xc_encode_run(self.h, d_in, d_out, d_len))
+
+    def set_timing(self, enable: bool) -> None:
+        _check(load_library().xc_plan_set_timing(self.h, 1 if enable else 0))
+
+    def kernel_times(self, reset: bool = False) -> dict:
+        kt = KernelTimes()
+        _check(load_library().xc_plan_kernel_times(self.h, C.byref(kt), 1 if reset else 0))
+        return {"ms": {k: kt.ms[i] for i, k in enumerate(KERNELS)},
+                "launches": {k: int(kt.launches[i]) for i, k in enumerate(KERNELS)},
+                "scan_bytes": int(kt.scan_bytes)}
 
     def stats(self) -> RunStats:
         st = RunStats()
