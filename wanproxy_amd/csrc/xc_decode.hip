@@ -1,10 +1,654 @@
-// xc_decode.hip — XCodec batch decoder (placeholder until the device decoder lands).
+// xc_decode.hip — XCodec batch decoder for gfx950 (CDNA4).
+//
+// Reference: XCodecDecoder::decode (xcodec/xcodec_decoder.cc:76-176), one call per stream,
+// streams in index order, one shared XCodecMemoryCache.  Pipeline:
+//
+//   k_dtok     one wave per stream: F1 search by ballot over 256-byte windows -> tokens
+//              (literal run [lb, le) with F1 00 escapes, then the op at le)
+//   k_dhash    H of every EXTRACT payload (xcodec_hash.h:166-174)
+//   k_dres1    EXTRACT vs the cache: equal -> ok, different -> collision (decode returns
+//              false, xcodec_decoder.cc:120-132); absent -> candidate provider, min-merged
+//              by (stream, token) into the batch table
+//   k_dres2    every token against cache + earlier providers: REF data source or unknown
+//              (xcodec_decoder.cc:142-166); later duplicate EXTRACTs compared with the first
+//   k_dstop    per stream: first token that stops the decode
+//   (host)     re-resolve if a provider lies past its own stream's stop (rare)
+//   k_dsize    per stream: output offsets of the executed tokens
+//   k_demit    unescape literals, copy EXTRACT payloads, gather REF segments
+//   k_dcommit  enter first-seen EXTRACT segments in the cache
 #include <hip/hip_runtime.h>
-#include "../../include/xcodec_hip.h"
 
-extern "C" int xc_decode_batch_host(xc_cache *, const uint8_t *, const uint64_t *, const uint64_t *, uint64_t,
-                                    uint8_t *, const uint64_t *, const uint64_t *, uint64_t *, uint64_t *,
-                                    int32_t *, uint64_t *, int32_t *)
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/xcodec_hip.h"
+#include "xc_kernels.h"
+
+namespace xc {
+
+constexpr uint32_t T_EXTRACT = 1, T_REF = 2, T_END = 3, T_WAIT = 4, T_BADOP = 5;
+constexpr uint32_t R_OKCACHE = 1, R_ENTER = 2, R_OKPROV = 3, R_UNKNOWN = 4, R_COLL = 5, R_PENDING = 6;
+constexpr uint64_t SRC_PROV = 1ull << 63;
+
+struct DecDev {
+    const uint8_t *in;
+    const uint64_t *in_off;
+    const uint32_t *in_len;
+    uint32_t ns;
+    const uint32_t *tok_base;  // [ns]
+    uint32_t *tok_cnt;         // [ns]
+    uint32_t *t_lb, *t_le, *t_op, *t_stat;
+    uint64_t *t_h, *t_src;
+    uint32_t *s_stop;          // executed tokens per stream (the stop token included: its literal runs)
+    uint32_t *s_lim;           // tokens eligible as EXTRACT providers this round
+    uint32_t *s_slot;          // first cache slot of the stream's entered segments
+    uint64_t *s_outoff;        // unused placeholder
+    uint8_t *out;
+    const uint64_t *out_off;
+    const uint64_t *out_cap;
+    uint64_t *out_len, *consumed, *unknown;
+    int32_t *status, *has_unknown;
+    DevSet cache;
+    uint8_t *segs;
+    uint32_t *seg_count;
+    uint32_t seg_cap;
+    uint2 *undo;
+    DevSet dset;
+    uint32_t *ctl;
+};
+
+enum : uint32_t { DCTL_FIX = 0, DCTL_ERR = 1, DCTL_NENTER = 2 };
+
+// First F1 at or after p in [p, n), or n.
+__device__ __forceinline__ uint32_t find_magic(const uint8_t *s, uint32_t p, uint32_t n)
 {
-    return XC_EINVAL;
+    const uint32_t l = lane_id();
+    for (uint32_t w0 = p & ~255u; w0 < n; w0 += 256u) {
+        const uint32_t o = w0 + 4u * l;
+        uint32_t m = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            const uint32_t i = o + k;
+            if (i >= p && i < n && s[i] == XC_MAGIC) m |= 1u << k;
+        }
+        const uint64_t b = ballot(m != 0u);
+        if (b) {
+            const int f = __ffsll((unsigned long long)b) - 1;
+            return w0 + 4u * (uint32_t)f + (uint32_t)__builtin_ctz(readlane(m, f));
+        }
+    }
+    return n;
+}
+
+// Tokenizer (xcodec_decoder.cc:85-173).  fill = false only counts tokens.
+__global__ __launch_bounds__(64) void k_dtok(DecDev D, int fill)
+{
+    const uint32_t j = blockIdx.x;
+    if (j >= D.ns) return;
+    const uint8_t *s = D.in + D.in_off[j];
+    const uint32_t n = D.in_len[j];
+    const uint32_t tb = fill ? D.tok_base[j] : 0u;
+    uint32_t nt = 0, lb = 0, p = 0;
+    auto put = [&](uint32_t op, uint32_t le, uint64_t h) {
+        if (fill && lane_id() == 0) {
+            D.t_lb[tb + nt] = lb;
+            D.t_le[tb + nt] = le;
+            D.t_op[tb + nt] = op;
+            D.t_h[tb + nt] = h;
+        }
+        nt++;
+    };
+    for (;;) {
+        const uint32_t q = find_magic(s, p, n);
+        if (q >= n) { put(T_END, n, 0); break; }
+        if (q + 1u >= n) { put(T_WAIT, q, 0); break; }
+        const uint32_t op = s[q + 1];
+        if (op == 0x00u) { p = q + 2u; continue; }  // escape stays inside the literal run
+        if (op == 0x01u) {
+            if (n - q < 2u + XC_SEG) { put(T_WAIT, q, 0); break; }
+            put(T_EXTRACT, q, 0);
+            lb = p = q + 2u + XC_SEG;
+            continue;
+        }
+        if (op == 0x02u) {
+            if (n - q < 10u) { put(T_WAIT, q, 0); break; }
+            uint64_t h = 0;
+            for (uint32_t k = 0; k < 8; k++) h = (h << 8) | s[q + 2 + k];
+            put(T_REF, q, h);
+            lb = p = q + 10u;
+            continue;
+        }
+        put(T_BADOP, q, 0);
+        break;
+    }
+    if (lane_id() == 0) D.tok_cnt[j] = nt;
+}
+
+__global__ __launch_bounds__(64) void k_dhash(DecDev D)
+{
+    const uint32_t j = blockIdx.x;
+    if (j >= D.ns) return;
+    const uint8_t *s = D.in + D.in_off[j];
+    const uint32_t tb = D.tok_base[j], n = D.tok_cnt[j];
+    for (uint32_t t = blockIdx.y; t < n; t += gridDim.y) {
+        if (uniform(D.t_op[tb + t]) != T_EXTRACT) continue;
+        const uint64_t h = wave_window_hash(s + D.t_le[tb + t] + 2u);
+        if (lane_id() == 0) D.t_h[tb + t] = h;
+    }
+}
+
+// EXTRACTs against the cache; absent ones become provider candidates in the batch table.
+__global__ __launch_bounds__(64) void k_dres1(DecDev D)
+{
+    const uint32_t j = blockIdx.x;
+    if (j >= D.ns) return;
+    const uint8_t *s = D.in + D.in_off[j];
+    const uint32_t tb = D.tok_base[j], n = D.tok_cnt[j];
+    const uint32_t lim = D.s_lim[j];
+    for (uint32_t t = blockIdx.y; t < n; t += gridDim.y) {
+        if (uniform(D.t_op[tb + t]) != T_EXTRACT) continue;
+        const uint64_t h = D.t_h[tb + t];
+        const uint8_t *pay = s + D.t_le[tb + t] + 2u;
+        uint64_t v;
+        uint32_t st;
+        if (set_find(D.cache, h, &v)) {
+            st = wave_equal2048(pay, D.segs + v * XC_SEG) ? R_OKCACHE : R_COLL;
+        } else {
+            st = R_PENDING;
+            if (lane_id() == 0 && t < lim) set_insert(D.dset, h, ((uint64_t)j << 32) | t, true, nullptr, nullptr);
+        }
+        if (lane_id() == 0) {
+            D.t_stat[tb + t] = st;
+            D.t_src[tb + t] = st == R_OKCACHE ? v : 0;
+        }
+    }
+}
+
+// Provider resolution in (stream, token) order.
+__global__ __launch_bounds__(64) void k_dres2(DecDev D)
+{
+    const uint32_t j = blockIdx.x;
+    if (j >= D.ns) return;
+    const uint8_t *s = D.in + D.in_off[j];
+    const uint32_t tb = D.tok_base[j], n = D.tok_cnt[j];
+    for (uint32_t t = blockIdx.y; t < n; t += gridDim.y) {
+        const uint32_t op = uniform(D.t_op[tb + t]);
+        const uint64_t self = ((uint64_t)j << 32) | t;
+        uint64_t v;
+        if (op == T_EXTRACT) {
+            if (uniform(D.t_stat[tb + t]) != R_PENDING) continue;
+            const uint64_t h = D.t_h[tb + t];
+            uint32_t st = R_ENTER;
+            uint64_t src = 0;
+            if (set_find(D.dset, h, &v) && v < self) {
+                const uint32_t pj = (uint32_t)(v >> 32), pt = (uint32_t)v;
+                const uint8_t *pp = D.in + D.in_off[pj] + D.t_le[D.tok_base[pj] + pt] + 2u;
+                st = wave_equal2048(s + D.t_le[tb + t] + 2u, pp) ? R_OKPROV : R_COLL;
+                src = SRC_PROV | v;
+            }
+            if (lane_id() == 0) {
+                D.t_stat[tb + t] = st;
+                D.t_src[tb + t] = src;
+            }
+        } else if (op == T_REF) {
+            const uint64_t h = D.t_h[tb + t];
+            uint32_t st = R_UNKNOWN;
+            uint64_t src = 0;
+            if (set_find(D.cache, h, &v)) {
+                st = R_OKCACHE;
+                src = v;
+            } else if (set_find(D.dset, h, &v) && v < self) {
+                st = R_OKPROV;
+                src = SRC_PROV | v;
+            }
+            if (lane_id() == 0) {
+                D.t_stat[tb + t] = st;
+                D.t_src[tb + t] = src;
+            }
+        } else if (lane_id() == 0) {
+            D.t_stat[tb + t] = 0;
+        }
+    }
+}
+
+// Per stream: executed token count and the decode's status / consumed bytes.
+__global__ __launch_bounds__(64) void k_dstop(DecDev D)
+{
+    const uint32_t j = blockIdx.x * 64u + lane_id();
+    if (j >= D.ns) return;
+    const uint32_t tb = D.tok_base[j], n = D.tok_cnt[j];
+    uint32_t t = 0;
+    for (; t < n; t++) {
+        const uint32_t op = D.t_op[tb + t], st = D.t_stat[tb + t];
+        if (op != T_EXTRACT && op != T_REF) break;
+        if (st == R_UNKNOWN || st == R_COLL) break;
+    }
+    // t = stopping token (terminal, unknown REF or colliding EXTRACT); its literal is output
+    D.s_stop[j] = t + 1u;
+    const uint32_t op = D.t_op[tb + t], st = D.t_stat[tb + t], le = D.t_le[tb + t];
+    int32_t status = 1, hu = 0;
+    uint64_t cons = le, unk = 0;
+    if (op == T_BADOP) status = 0;
+    else if (op == T_REF) { hu = 1; unk = D.t_h[tb + t]; }              // unknown REF
+    else if (op == T_EXTRACT) { status = 0; cons = le + 2u; }           // collision
+    (void)st;
+    D.status[j] = status;
+    D.consumed[j] = cons;
+    D.has_unknown[j] = hu;
+    D.unknown[j] = unk;
+}
+
+// Consistency of a resolution round: every provider used by an executed token must itself be
+// executed, and (after round 0) the executed tokens must be exactly the eligible providers.
+__global__ __launch_bounds__(64) void k_dcheck(DecDev D, int round)
+{
+    const uint32_t j = blockIdx.x;
+    if (j >= D.ns) return;
+    const uint32_t tb = D.tok_base[j], ex = D.s_stop[j] - 1u;
+    if (round > 0 && lane_id() == 0 && ex != D.s_lim[j]) atomicOr(&D.ctl[DCTL_FIX], 1u);
+    for (uint32_t t = lane_id(); t < ex; t += 64u) {
+        const uint64_t src = D.t_src[tb + t];
+        const uint32_t st = D.t_stat[tb + t];
+        if ((st == R_OKPROV || st == R_COLL) && (src & SRC_PROV)) {
+            const uint32_t pj = (uint32_t)((src >> 32) & 0x7FFFFFFFu), pt = (uint32_t)src;
+            if (pt + 1u >= D.s_stop[pj]) atomicOr(&D.ctl[DCTL_FIX], 1u);
+        }
+    }
+}
+
+__global__ void k_dlim(DecDev D, int init)
+{
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < D.ns) D.s_lim[j] = init ? 0xFFFFFFFFu : D.s_stop[j] - 1u;
+}
+
+__device__ __forceinline__ uint32_t count_magic_d(const uint8_t *p, uint32_t n)
+{
+    uint32_t c = 0;
+    for (uint32_t o = 4u * lane_id(); o < n; o += 256u) {
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++)
+            if (o + k < n) c += p[o + k] == XC_MAGIC ? 1u : 0u;
+    }
+    return wave_sum(c);
+}
+
+// Unescape a literal run: every F1 is followed by the escape's 00, which is dropped.
+__device__ __forceinline__ void write_unescaped(uint8_t *dst, const uint8_t *p, uint32_t n)
+{
+    uint32_t o = 0;
+    for (uint32_t x = 0; x < n; x += 256u) {
+        const uint32_t s = x + 4u * lane_id();
+        uint32_t v[4], keep = 0, cnt = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            const uint32_t i = s + k;
+            v[k] = i < n ? p[i] : 0u;
+            const bool drop = i >= n || (i > 0 && p[i - 1] == XC_MAGIC);
+            if (!drop) { keep |= 1u << k; cnt++; }
+        }
+        const uint32_t inc = wave_incl_scan(cnt);
+        uint32_t q = o + inc - cnt;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++)
+            if (keep & (1u << k)) dst[q++] = (uint8_t)v[k];
+        o += readlane(inc, 63);
+    }
+}
+
+constexpr uint32_t DMAX_TOK = 2048;
+
+// Output offsets (executed tokens only), then the bytes.  One workgroup (4 waves) per
+// stream, tokens in blocks of DMAX_TOK.
+__global__ __launch_bounds__(256) void k_demit(DecDev D)
+{
+    __shared__ uint64_t off[DMAX_TOK + 1];
+    __shared__ uint64_t base_off;
+    const uint32_t j = blockIdx.x;
+    if (j >= D.ns) return;
+    const uint32_t wave = threadIdx.x >> 6, l = lane_id();
+    const uint8_t *s = D.in + D.in_off[j];
+    uint8_t *out = D.out + D.out_off[j];
+    const uint32_t tb = D.tok_base[j];
+    const uint32_t lim = min(D.tok_cnt[j], D.s_stop[j]);
+    if (threadIdx.x == 0) base_off = 0;
+    for (uint32_t t0 = 0; t0 < lim; t0 += DMAX_TOK) {
+        const uint32_t nb = min(DMAX_TOK, lim - t0);
+        __syncthreads();
+        for (uint32_t i = wave; i < nb; i += 4u) {
+            const uint32_t t = t0 + i;
+            const uint32_t lb = D.t_lb[tb + t], le = D.t_le[tb + t], op = D.t_op[tb + t];
+            uint32_t sz = (le - lb) - count_magic_d(s + lb, le - lb);
+            if (t + 1u != lim && (op == T_EXTRACT || op == T_REF)) sz += XC_SEG;
+            if (l == 0) off[i] = sz;
+        }
+        __syncthreads();
+        if (wave == 0) {
+            uint64_t carry = base_off;
+            for (uint32_t i0 = 0; i0 < nb; i0 += 64u) {
+                const uint32_t i = i0 + l;
+                const uint32_t v = i < nb ? (uint32_t)off[i] : 0u;
+                const uint32_t inc = wave_incl_scan(v);
+                if (i < nb) off[i] = carry + inc - v;
+                carry += readlane(inc, 63);
+            }
+            if (l == 0) { off[nb] = carry; base_off = carry; }
+        }
+        __syncthreads();
+        if (off[nb] > D.out_cap[j]) {
+            if (threadIdx.x == 0) atomicOr(&D.ctl[DCTL_ERR], 1u);
+            return;
+        }
+        for (uint32_t i = wave; i < nb; i += 4u) {
+            const uint32_t t = t0 + i;
+            const uint32_t lb = D.t_lb[tb + t], le = D.t_le[tb + t], op = D.t_op[tb + t];
+            write_unescaped(out + off[i], s + lb, le - lb);
+            if (t + 1u == lim) continue;  // the stop token contributes its literal only
+            uint8_t *o = out + off[i + 1] - XC_SEG;
+            if (op == T_EXTRACT) {
+                wave_copy(o, s + le + 2u, XC_SEG);
+            } else if (op == T_REF) {
+                const uint64_t src = D.t_src[tb + t];
+                const uint8_t *from;
+                if (src & SRC_PROV) {
+                    const uint32_t pj = (uint32_t)((src >> 32) & 0x7FFFFFFFu), pt = (uint32_t)src;
+                    from = D.in + D.in_off[pj] + D.t_le[D.tok_base[pj] + pt] + 2u;
+                } else {
+                    from = D.segs + src * XC_SEG;
+                }
+                wave_copy(o, from, XC_SEG);
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) D.out_len[j] = base_off;
+}
+
+// Count ENTER tokens per stream (executed only) -> s_slot via one-workgroup prefix.
+__global__ __launch_bounds__(1024) void k_dalloc(DecDev D)
+{
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t carry;
+    const uint32_t wave = threadIdx.x >> 6, l = lane_id();
+    if (threadIdx.x == 0) carry = *D.seg_count;
+    __syncthreads();
+    const uint32_t start = carry;
+    for (uint32_t j0 = 0; j0 < D.ns; j0 += 1024u) {
+        const uint32_t j = j0 + threadIdx.x;
+        uint32_t v = 0;
+        if (j < D.ns) {
+            const uint32_t tb = D.tok_base[j], lim = min(D.tok_cnt[j], D.s_stop[j] - 1u);
+            for (uint32_t t = 0; t < lim; t++) v += D.t_stat[tb + t] == R_ENTER ? 1u : 0u;
+        }
+        const uint32_t inc = wave_incl_scan(v);
+        if (l == 63) wsum[wave] = inc;
+        __syncthreads();
+        uint32_t o = carry;
+        for (uint32_t k = 0; k < wave; k++) o += wsum[k];
+        if (j < D.ns) D.s_slot[j] = o + inc - v;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t tot = 0;
+            for (uint32_t k = 0; k < 16; k++) tot += wsum[k];
+            carry += tot;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        *D.seg_count = carry;
+        D.ctl[DCTL_NENTER] = carry - start;
+        if (carry > D.seg_cap) D.ctl[DCTL_ERR] |= 2u;
+    }
+}
+
+// XCodecMemoryCache::enter for first-seen EXTRACT payloads (xcodec_decoder.cc:133-135).
+__global__ __launch_bounds__(64) void k_dcommit(DecDev D)
+{
+    const uint32_t j = blockIdx.x;
+    if (j >= D.ns) return;
+    const uint8_t *s = D.in + D.in_off[j];
+    const uint32_t tb = D.tok_base[j], lim = min(D.tok_cnt[j], D.s_stop[j] - 1u);
+    uint32_t k = 0;
+    for (uint32_t t = 0; t < lim; t++) {
+        if (uniform(D.t_stat[tb + t]) != R_ENTER) continue;
+        const uint32_t idx = D.s_slot[j] + k++;
+        if (idx >= D.seg_cap) continue;
+        wave_copy(D.segs + (size_t)idx * XC_SEG, s + D.t_le[tb + t] + 2u, XC_SEG);
+        if (lane_id() == 0) {
+            uint32_t s1, s2;
+            set_insert(D.cache, D.t_h[tb + t], idx, false, &s1, &s2);
+            D.undo[idx] = make_uint2(s1, s2);
+        }
+    }
+}
+
+}  // namespace xc
+
+using namespace xc;
+
+// ------------------------------------------------------------------ host side ----------
+// The cache object is defined in xc_runtime.hip; these accessors expose what we need.
+extern "C" int xc__cache_devset(xc_cache *c, void *devset, uint8_t **segs, uint32_t **count, uint32_t *cap,
+                                uint2 **undo, void **stream, int *dev);
+extern "C" int xc__set_error(int code, const char *msg);
+
+#define DCHK(x)                                                                        \
+    do {                                                                               \
+        hipError_t e_ = (x);                                                           \
+        if (e_ != hipSuccess) { rc = xc__set_error(XC_EDEVICE, hipGetErrorString(e_)); goto done; } \
+    } while (0)
+
+template <class T>
+static hipError_t dalloc(T **p, size_t n)
+{
+    return hipMalloc((void **)p, std::max<size_t>(n, 1) * sizeof(T));
+}
+
+extern "C" int xc_decode_batch_host(xc_cache *c, const uint8_t *in, const uint64_t *in_off, const uint64_t *in_len,
+                                    uint64_t nbuf, uint8_t *out, const uint64_t *out_off, const uint64_t *out_cap,
+                                    uint64_t *out_len, uint64_t *consumed, int32_t *status, uint64_t *unknown,
+                                    int32_t *has_unknown)
+{
+    if (!c || (nbuf && (!in || !in_off || !in_len || !out || !out_off || !out_cap || !out_len || !consumed ||
+                        !status || !unknown || !has_unknown)))
+        return xc__set_error(XC_EINVAL, "null");
+    if (nbuf == 0) return XC_OK;
+    if (nbuf > (1u << 24)) return xc__set_error(XC_EINVAL, "too many streams");
+    DecDev D{};
+    void *streamv = nullptr;
+    int dev = 0;
+    uint32_t cap = 0;
+    int rc = xc__cache_devset(c, &D.cache, &D.segs, &D.seg_count, &cap, &D.undo, &streamv, &dev);
+    if (rc) return rc;
+    D.seg_cap = cap;
+    hipStream_t s = (hipStream_t)streamv;
+    const uint32_t ns = (uint32_t)nbuf;
+    D.ns = ns;
+    std::vector<uint64_t> ioff(ns), ooff(ns);
+    std::vector<uint32_t> ilen(ns), tcnt(ns), tbase(ns);
+    uint64_t itot = 0, otot = 0, ntok = 0;
+    for (uint32_t j = 0; j < ns; j++) {
+        if (in_len[j] > 0xFFFFFFF0ull) return xc__set_error(XC_EINVAL, "stream too long");
+        ioff[j] = itot;
+        itot += (in_len[j] + 255) / 256 * 256;
+        ilen[j] = (uint32_t)in_len[j];
+        ooff[j] = otot;
+        otot += (out_cap[j] + 255) / 256 * 256;
+    }
+    uint8_t *d_in = nullptr, *h_in = nullptr, *d_out = nullptr, *h_out = nullptr;
+    uint64_t *d_ioff = nullptr, *d_ooff = nullptr, *d_ocap = nullptr, *d_olen = nullptr, *d_cons = nullptr,
+             *d_unk = nullptr;
+    uint32_t *d_ilen = nullptr, *d_tbase = nullptr, *d_tcnt = nullptr, *d_stop = nullptr, *d_slot = nullptr,
+             *d_ctl = nullptr, *d_lim = nullptr;
+    int32_t *d_st = nullptr, *d_hu = nullptr;
+    DevSet &ds = D.dset;
+    uint32_t n_full = 0, n_lo = 0;
+    uint32_t ctl[4] = {0, 0, 0, 0};
+    std::vector<uint64_t> olen(ns), cons(ns), unk(ns);
+    std::vector<int32_t> st(ns), hu(ns);
+    int rounds = 0;
+
+    DCHK(hipSetDevice(dev));
+    DCHK(hipHostMalloc((void **)&h_in, itot + 4096));
+    DCHK(dalloc(&d_in, itot + 4096));
+    memset(h_in, 0, itot + 4096);
+    for (uint32_t j = 0; j < ns; j++) memcpy(h_in + ioff[j], in + in_off[j], in_len[j]);
+    DCHK(hipMemcpyAsync(d_in, h_in, itot + 4096, hipMemcpyHostToDevice, s));
+    DCHK(dalloc(&d_ioff, ns));
+    DCHK(dalloc(&d_ilen, ns));
+    DCHK(dalloc(&d_tcnt, ns));
+    DCHK(dalloc(&d_tbase, ns));
+    DCHK(dalloc(&d_stop, ns));
+    DCHK(dalloc(&d_slot, ns));
+    DCHK(dalloc(&d_lim, ns));
+    DCHK(dalloc(&d_ooff, ns));
+    DCHK(dalloc(&d_ocap, ns));
+    DCHK(dalloc(&d_olen, ns));
+    DCHK(dalloc(&d_cons, ns));
+    DCHK(dalloc(&d_unk, ns));
+    DCHK(dalloc(&d_st, ns));
+    DCHK(dalloc(&d_hu, ns));
+    DCHK(dalloc(&d_ctl, 4));
+    DCHK(dalloc(&d_out, otot + 256));
+    DCHK(hipMemcpyAsync(d_ioff, ioff.data(), ns * 8, hipMemcpyHostToDevice, s));
+    DCHK(hipMemcpyAsync(d_ilen, ilen.data(), ns * 4, hipMemcpyHostToDevice, s));
+    DCHK(hipMemcpyAsync(d_ooff, ooff.data(), ns * 8, hipMemcpyHostToDevice, s));
+    DCHK(hipMemcpyAsync(d_ocap, out_cap, ns * 8, hipMemcpyHostToDevice, s));
+    DCHK(hipMemsetAsync(d_ctl, 0, 16, s));
+    D.in = d_in;
+    D.in_off = d_ioff;
+    D.in_len = d_ilen;
+    D.tok_cnt = d_tcnt;
+    D.tok_base = d_tbase;
+    D.s_stop = d_stop;
+    D.s_slot = d_slot;
+    D.s_lim = d_lim;
+    D.out = d_out;
+    D.out_off = d_ooff;
+    D.out_cap = d_ocap;
+    D.out_len = d_olen;
+    D.consumed = d_cons;
+    D.unknown = d_unk;
+    D.status = d_st;
+    D.has_unknown = d_hu;
+    D.ctl = d_ctl;
+
+    // tokens: count, prefix, fill
+    hipLaunchKernelGGL(k_dtok, dim3(ns), dim3(64), 0, s, D, 0);
+    DCHK(hipGetLastError());
+    DCHK(hipMemcpyAsync(tcnt.data(), d_tcnt, ns * 4, hipMemcpyDeviceToHost, s));
+    DCHK(hipStreamSynchronize(s));
+    for (uint32_t j = 0; j < ns; j++) {
+        tbase[j] = (uint32_t)ntok;
+        ntok += tcnt[j];
+    }
+    if (ntok > 0xFFFFFFF0ull) { rc = xc__set_error(XC_EINVAL, "too many tokens"); goto done; }
+    DCHK(hipMemcpyAsync(d_tbase, tbase.data(), ns * 4, hipMemcpyHostToDevice, s));
+    DCHK(dalloc(&D.t_lb, ntok));
+    DCHK(dalloc(&D.t_le, ntok));
+    DCHK(dalloc(&D.t_op, ntok));
+    DCHK(dalloc(&D.t_stat, ntok));
+    DCHK(dalloc(&D.t_h, ntok));
+    DCHK(dalloc(&D.t_src, ntok));
+    hipLaunchKernelGGL(k_dtok, dim3(ns), dim3(64), 0, s, D, 1);
+    DCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_dhash, dim3(ns, 8), dim3(64), 0, s, D);
+    DCHK(hipGetLastError());
+    // batch provider table
+    n_full = 1024;
+    while (n_full < 2 * ntok + 2) n_full <<= 1;
+    n_lo = 1024;
+    while (n_lo < 4 * ntok + 4) n_lo <<= 1;
+    DCHK(dalloc(&ds.filt, XC_FILT_WORDS));
+    DCHK(dalloc(&ds.lo_keys, n_lo));
+    DCHK(dalloc(&ds.lo_zero, 1));
+    DCHK(dalloc(&ds.keys, n_full));
+    DCHK(dalloc(&ds.vals, n_full));
+    ds.mask = n_full - 1;
+    ds.lo_mask = n_lo - 1;
+    hipLaunchKernelGGL(k_dlim, dim3((ns + 255) / 256), dim3(256), 0, s, D, 1);
+    DCHK(hipGetLastError());
+    for (;;) {
+        DCHK(hipMemsetAsync(ds.filt, 0, XC_FILT_WORDS * 4, s));
+        DCHK(hipMemsetAsync(ds.lo_keys, 0, (size_t)n_lo * 4, s));
+        DCHK(hipMemsetAsync(ds.lo_zero, 0, 4, s));
+        DCHK(hipMemsetAsync(ds.keys, 0xFF, (size_t)n_full * 8, s));
+        DCHK(hipMemsetAsync(ds.vals, 0xFF, (size_t)n_full * 8, s));
+        DCHK(hipMemsetAsync(d_ctl, 0, 4, s));
+        hipLaunchKernelGGL(k_dres1, dim3(ns, 8), dim3(64), 0, s, D);
+        DCHK(hipGetLastError());
+        hipLaunchKernelGGL(k_dres2, dim3(ns, 8), dim3(64), 0, s, D);
+        DCHK(hipGetLastError());
+        hipLaunchKernelGGL(k_dstop, dim3((ns + 63) / 64), dim3(64), 0, s, D);
+        DCHK(hipGetLastError());
+        hipLaunchKernelGGL(k_dcheck, dim3(ns), dim3(64), 0, s, D, rounds);
+        DCHK(hipGetLastError());
+        DCHK(hipMemcpyAsync(ctl, d_ctl, 16, hipMemcpyDeviceToHost, s));
+        DCHK(hipStreamSynchronize(s));
+        if (!ctl[DCTL_FIX]) break;
+        hipLaunchKernelGGL(k_dlim, dim3((ns + 255) / 256), dim3(256), 0, s, D, 0);
+        DCHK(hipGetLastError());
+        if (++rounds > 64) { rc = xc__set_error(XC_EDEVICE, "decode provider resolution did not converge"); goto done; }
+    }
+    hipLaunchKernelGGL(k_demit, dim3(ns), dim3(256), 0, s, D);
+    DCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_dalloc, dim3(1), dim3(1024), 0, s, D);
+    DCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_dcommit, dim3(ns), dim3(64), 0, s, D);
+    DCHK(hipGetLastError());
+    DCHK(hipMemcpyAsync(ctl, d_ctl, 16, hipMemcpyDeviceToHost, s));
+    DCHK(hipMemcpyAsync(olen.data(), d_olen, ns * 8, hipMemcpyDeviceToHost, s));
+    DCHK(hipMemcpyAsync(cons.data(), d_cons, ns * 8, hipMemcpyDeviceToHost, s));
+    DCHK(hipMemcpyAsync(unk.data(), d_unk, ns * 8, hipMemcpyDeviceToHost, s));
+    DCHK(hipMemcpyAsync(st.data(), d_st, ns * 4, hipMemcpyDeviceToHost, s));
+    DCHK(hipMemcpyAsync(hu.data(), d_hu, ns * 4, hipMemcpyDeviceToHost, s));
+    DCHK(hipHostMalloc((void **)&h_out, otot + 256));
+    DCHK(hipMemcpyAsync(h_out, d_out, otot + 256, hipMemcpyDeviceToHost, s));
+    DCHK(hipStreamSynchronize(s));
+    if (ctl[DCTL_ERR] & 2u) { rc = xc__set_error(XC_ENOSPC, "device cache capacity exhausted"); goto done; }
+    if (ctl[DCTL_ERR] & 1u) { rc = xc__set_error(XC_EINVAL, "output capacity too small"); goto done; }
+    for (uint32_t j = 0; j < ns; j++) {
+        out_len[j] = olen[j];
+        consumed[j] = cons[j];
+        unknown[j] = unk[j];
+        status[j] = st[j];
+        has_unknown[j] = hu[j];
+        memcpy(out + out_off[j], h_out + ooff[j], olen[j]);
+    }
+    rc = XC_OK;
+done:
+    hipStreamSynchronize(s);
+    hipHostFree(h_in);
+    hipHostFree(h_out);
+    hipFree(d_in);
+    hipFree(d_out);
+    hipFree(d_ioff);
+    hipFree(d_ilen);
+    hipFree(d_tcnt);
+    hipFree(d_tbase);
+    hipFree(d_stop);
+    hipFree(d_slot);
+    hipFree(d_lim);
+    hipFree(d_ooff);
+    hipFree(d_ocap);
+    hipFree(d_olen);
+    hipFree(d_cons);
+    hipFree(d_unk);
+    hipFree(d_st);
+    hipFree(d_hu);
+    hipFree(d_ctl);
+    hipFree(D.t_lb);
+    hipFree(D.t_le);
+    hipFree(D.t_op);
+    hipFree(D.t_stat);
+    hipFree(D.t_h);
+    hipFree(D.t_src);
+    hipFree(ds.filt);
+    hipFree(ds.lo_keys);
+    hipFree(ds.lo_zero);
+    hipFree(ds.keys);
+    hipFree(ds.vals);
+    return rc;
 }

@@ -810,6 +810,23 @@ extern "C" int xc_encode_batch_host(xc_cache *c, const uint8_t *in, const uint64
     return rc;
 }
 
+// Internal accessors for xc_decode.hip (not part of the public header).
+extern "C" int xc__cache_devset(xc_cache *c, void *devset, uint8_t **segs, uint32_t **count, uint32_t *cap,
+                                uint2 **undo, void **stream, int *dev)
+{
+    if (!c) return fail(XC_EINVAL, "null");
+    *(DevSet *)devset = c->set.d;
+    *segs = c->segs;
+    *count = c->count;
+    *cap = (uint32_t)c->cap;
+    *undo = c->undo;
+    *stream = (void *)c->ctx->stream;
+    *dev = c->ctx->dev;
+    return XC_OK;
+}
+
+extern "C" int xc__set_error(int code, const char *msg) { return fail(code, msg); }
+
 extern "C" int xc_selftest(xc_ctx *ctx)
 {
     if (!ctx) return fail(XC_EINVAL, "null");
@@ -826,7 +843,4 @@ extern "C" int xc_selftest(xc_ctx *ctx)
     return XC_OK;
 }
 
-extern "C" int xc_decode_batch_host(xc_cache *c, const uint8_t *in, const uint64_t *in_off, const uint64_t *in_len,
-                                    uint64_t nbuf, uint8_t *out, const uint64_t *out_off, const uint64_t *out_cap,
-                                    uint64_t *out_len, uint64_t *consumed, int32_t *status, uint64_t *unknown,
-                                    int32_t *has_unknown);
+

@@ -11,8 +11,10 @@ There is no CPU fallback: if the HIP library or a GPU is missing, construction r
 """
 from __future__ import annotations
 
+import atexit
 import ctypes as C
 import os
+import weakref
 
 import numpy as np
 
@@ -104,6 +106,21 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     return lib
 
 
+# Native objects must be destroyed before the context they live on and before the HIP runtime
+# tears itself down at process exit: keep weak references and release them in order at exit.
+_LIVE = {"plan": weakref.WeakSet(), "cache": weakref.WeakSet(), "ctx": weakref.WeakSet()}
+
+
+@atexit.register
+def _teardown() -> None:
+    for kind in ("plan", "cache", "ctx"):
+        for obj in list(_LIVE[kind]):
+            try:
+                obj.close()
+            except Exception:
+                pass
+
+
 def _check(rc: int) -> None:
     if rc != 0:
         raise XCodecError(f"xcodec_hip error {rc}: {load_library().xc_last_error().decode()}")
@@ -123,6 +140,7 @@ class Context:
         self.h = _vp()
         _check(lib.xc_ctx_create(device, C.byref(self.h)))
         self.device = device
+        _LIVE["ctx"].add(self)
 
     @property
     def stream(self) -> int:
@@ -135,7 +153,12 @@ class Context:
         _check(load_library().xc_selftest(self.h))
 
     def close(self) -> None:
+        """Destroy the context; every cache / plan created on it is released first."""
         if getattr(self, "h", None):
+            for kind in ("plan", "cache"):
+                for obj in list(_LIVE[kind]):
+                    if obj._ctx() is self:
+                        obj.close()
             load_library().xc_ctx_destroy(self.h)
             self.h = None
 
@@ -174,6 +197,10 @@ class XCodecCache:
         self.h = _vp()
         _check(load_library().xc_cache_create(ctx.h, capacity, C.byref(self.h)))
         self.capacity = capacity
+        _LIVE["cache"].add(self)
+
+    def _ctx(self):
+        return self.ctx
 
     def __len__(self) -> int:
         n = C.c_uint64()
@@ -203,6 +230,9 @@ class XCodecCache:
 
     def close(self) -> None:
         if getattr(self, "h", None):
+            for obj in list(_LIVE["plan"]):
+                if obj.cache is self:
+                    obj.close()
             load_library().xc_cache_destroy(self.h)
             self.h = None
 
@@ -277,6 +307,10 @@ class EncodePlan:
         _check(load_library().xc_plan_layout(self.h, self.in_off, self.out_off, C.byref(ib),
                                              C.byref(ob)))
         self.in_bytes, self.out_bytes = ib.value, ob.value
+        _LIVE["plan"].add(self)
+
+    def _ctx(self):
+        return self.cache.ctx
 
     def run(self, d_in: int, d_out: int, d_len: int) -> None:
         _check(load_library().xc_encode_run(self.h, d_in, d_out, d_len))
