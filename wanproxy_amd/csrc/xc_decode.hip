@@ -562,6 +562,7 @@ extern "C" int xc_decode_batch_host(xc_cache *c, const uint8_t *in, const uint64
     n_lo = 1024;
     while (n_lo < 4 * ntok + 4) n_lo <<= 1;
     DCHK(dalloc(&ds.filt, XC_FILT_WORDS));
+    DCHK(dalloc(&ds.l2, 2 * (size_t)XC_L2_WORDS));
     DCHK(dalloc(&ds.lo_keys, n_lo));
     DCHK(dalloc(&ds.lo_zero, 1));
     DCHK(dalloc(&ds.keys, n_full));
@@ -572,6 +573,7 @@ extern "C" int xc_decode_batch_host(xc_cache *c, const uint8_t *in, const uint64
     DCHK(hipGetLastError());
     for (;;) {
         DCHK(hipMemsetAsync(ds.filt, 0, XC_FILT_WORDS * 4, s));
+        DCHK(hipMemsetAsync(ds.l2, 0, (size_t)XC_L2_WORDS * 8, s));
         DCHK(hipMemsetAsync(ds.lo_keys, 0, (size_t)n_lo * 4, s));
         DCHK(hipMemsetAsync(ds.lo_zero, 0, 4, s));
         DCHK(hipMemsetAsync(ds.keys, 0xFF, (size_t)n_full * 8, s));
@@ -646,6 +648,7 @@ done:
     hipFree(D.t_h);
     hipFree(D.t_src);
     hipFree(ds.filt);
+    hipFree(ds.l2);
     hipFree(ds.lo_keys);
     hipFree(ds.lo_zero);
     hipFree(ds.keys);

@@ -165,8 +165,24 @@ __device__ __forceinline__ void wave_copy(uint8_t *dst, const uint8_t *src, uint
 #define XC_FILT_WORDS 32768u  // in 32-bit words
 #define XC_EMPTY64 0xFFFFFFFFFFFFFFFFull           // H never has bits 32..35 set
 
+// Level-2 filter: a blocked k=2 Bloom filter of 2^18 64-bit words (2 MB, sized to stay in an
+// XCD's L2) keyed by a remix of lo32, independent of the level-1 bits.
+#define XC_L2_WORDS (1u << 18)
+
+__device__ __forceinline__ uint32_t l2_mix(uint32_t lo)
+{
+    uint32_t g = (lo ^ (lo >> 15)) * 0x2C1B3C6Du;
+    return g ^ (g >> 12);
+}
+
+__device__ __forceinline__ bool l2_test(uint2 w, uint32_t g)
+{
+    return ((w.x >> (g & 31u)) & (w.y >> ((g >> 5) & 31u)) & 1u) != 0u;
+}
+
 struct DevSet {
     uint32_t *filt;     // XC_FILT_WORDS
+    uint32_t *l2;       // 2 * XC_L2_WORDS (level-2 filter)
     uint32_t *lo_keys;  // lo32 set (0 = empty; a zero key is flagged in *lo_zero)
     uint32_t *lo_zero;
     uint32_t lo_mask;
@@ -246,6 +262,9 @@ __device__ __forceinline__ int set_insert(const DevSet &s, uint64_t h, uint64_t 
         const uint32_t wi = (lo >> 18) * 2u;
         atomicOr(&s.filt[wi], 1u << (lo & 31u));
         atomicOr(&s.filt[wi + 1u], 1u << ((lo >> 5) & 31u));
+        const uint32_t g = l2_mix(lo), gi = (g >> 14) * 2u;
+        atomicOr(&s.l2[gi], 1u << (g & 31u));
+        atomicOr(&s.l2[gi + 1u], 1u << ((g >> 5) & 31u));
     }
     if (lo_slot_out) *lo_slot_out = los;
     return fresh;

@@ -54,10 +54,15 @@ __device__ __forceinline__ void scan_record(const ScanArgs &a, uint32_t c, uint3
 // probe latency overlaps the next 2048-position iteration: issue() moves up to 128 queued
 // (position, lo32) pairs into registers and starts their lo32-set loads (two consecutive
 // slots each); complete() consumes them one iteration later.
+// Exact lo32 membership for queued level-1 positives, split in two halves so the latency
+// overlaps the next 2048-position iteration: issue() moves up to 128 queued (position, lo32)
+// pairs into registers and starts their level-2 filter loads (one 8-byte L2 read each);
+// complete() tests them one iteration later and probes the exact lo32 sets for survivors.
 struct Pending {
     uint32_t n;          // entries (uniform); 0 = nothing pending
     uint32_t c, c0;      // chunk the entries belong to
-    uint32_t pos[2], lo[2], k0[2], k1[2];
+    uint32_t pos[2], lo[2];
+    uint2 w[2];
 };
 
 __device__ __forceinline__ void pend_issue(const ScanArgs &a, Pending &pd, const uint2 *queue, uint32_t qn,
@@ -71,19 +76,12 @@ __device__ __forceinline__ void pend_issue(const ScanArgs &a, Pending &pd, const
         const uint32_t i = lane_id() + 64u * s;
         pd.pos[s] = 0;
         pd.lo[s] = 0;
-        pd.k0[s] = 0;
-        pd.k1[s] = 0;
+        pd.w[s] = make_uint2(0, 0);
         if (i < qn) {
             const uint2 e = queue[i];
             pd.pos[s] = e.x;
             pd.lo[s] = e.y;
-            if (e.y == 0u) {
-                pd.k0[s] = *a.set.lo_zero;
-            } else {
-                const uint32_t j = lo_slot(e.y, a.set.lo_mask);
-                pd.k0[s] = a.set.lo_keys[j];
-                pd.k1[s] = a.set.lo_keys[(j + 1u) & a.set.lo_mask];
-            }
+            pd.w[s] = a.l2[l2_mix(e.y) >> 14];
         }
     }
 }
@@ -95,15 +93,9 @@ __device__ __forceinline__ void pend_complete(const ScanArgs &a, Pending &pd, ui
         if (64u * s >= pd.n) break;
         const uint32_t i = lane_id() + 64u * s;
         bool match = false;
-        if (i < pd.n) {
+        if (i < pd.n && l2_test(pd.w[s], l2_mix(pd.lo[s]))) {
             const uint32_t lo = pd.lo[s];
-            if (lo == 0u) {
-                match = pd.k0[s] != 0u;
-            } else if (pd.k0[s] == lo || pd.k1[s] == lo) {
-                match = true;
-            } else if (pd.k0[s] != 0u && pd.k1[s] != 0u) {
-                match = set_has_lo(a.set, lo);  // long probe chain: rare
-            }
+            match = set_has_lo(a.set, lo) || (a.has2 && set_has_lo(a.set2, lo));
         }
         scan_record(a, pd.c, pd.c0, match, pd.pos[s], ev_n, dense);
     }
@@ -120,7 +112,9 @@ __device__ __forceinline__ void scan_flush(const ScanArgs &a, uint2 *queue, uint
         if (i < qn) {
             uint2 e = queue[i];
             pos = e.x;
-            match = set_has_lo(a.set, e.y);
+            const uint32_t g = l2_mix(e.y);
+            if (l2_test(a.l2[g >> 14], g))
+                match = set_has_lo(a.set, e.y) || (a.has2 && set_has_lo(a.set2, e.y));
         }
         scan_record(a, c, c0, match, pos, ev_n, dense);
     }
@@ -154,8 +148,10 @@ __device__ __forceinline__ BlockSums block_sums(const uint32_t w[8], uint32_t l)
 
 __device__ __forceinline__ void load32_aligned(const uint8_t *p, uint32_t w[8])
 {
-    const uint4 *q = (const uint4 *)p;
-    uint4 x = q[0], y = q[1];
+    // streamed once: non-temporal, so the level-2 filter keeps its place in L2
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const v4u *q = (const v4u *)p;
+    const v4u x = __builtin_nontemporal_load(q), y = __builtin_nontemporal_load(q + 1);
     w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w;
     w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
 }
@@ -183,8 +179,14 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
     uint2 *queue = queues[wave];
     const uint32_t l = lane_id();
 
-    for (uint32_t i = threadIdx.x * 2u; i < XC_FILT_WORDS / 2; i += 2048u)
-        *(uint4 *)(filt + i) = *(const uint4 *)(a.set.filt + 2 * i);
+    for (uint32_t i = threadIdx.x * 2u; i < XC_FILT_WORDS / 2; i += 2048u) {
+        uint4 f = *(const uint4 *)(a.set.filt + 2 * i);
+        if (a.has2) {
+            const uint4 g = *(const uint4 *)(a.set2.filt + 2 * i);
+            f.x |= g.x; f.y |= g.y; f.z |= g.z; f.w |= g.w;
+        }
+        *(uint4 *)(filt + i) = f;
+    }
     __syncthreads();
 
     const uint32_t stride = gridDim.x * SCAN_WAVES;
@@ -209,8 +211,6 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
         const bool has_next = c + stride < a.ck_hi;
         uint32_t ev_n = 0, qn = 0;
         bool dense = false;
-        uint32_t npw[8], nw[8];
-        bool next_loaded = false;
 
         BlockSums ps = block_sums(pw, l);
         uint32_t s = c0;
@@ -227,12 +227,7 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
             // prefetch: the next block of this chunk, or the next chunk's first two blocks
             uint32_t wn[8];
             const bool last = s + XC_SEG >= c1;
-            if (!last) {
-                load32_aligned(base + s + XC_SEG + 32u * l, wn);
-            } else if (has_next) {
-                first_blocks(desc_base(a, dn), uniform(dn.x), l, npw, nw);
-                next_loaded = true;
-            }
+            if (!last) load32_aligned(base + s + XC_SEG + 32u * l, wn);
             const BlockSums cs = block_sums(w, l);
             // window ending just before this lane's first position q = s + 32 l:
             // out-chunks of lanes >= l (previous block) + in-chunks of lanes < l.
@@ -244,7 +239,7 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
             const uint32_t q = s + 32u * l;
             const uint32_t vmask = (q + 32u <= c1) ? 0xFFFFFFFFu : (q >= c1 ? 0u : ((1u << (c1 - q)) - 1u));
 #pragma unroll
-            for (int half = 0; half < 2; half++) {
+            for (int half = 0; half < (a.mode == 2 ? 0 : 2); half++) {
                 uint32_t lo[16];
                 uint32_t hit = 0;
 #pragma unroll
@@ -257,7 +252,8 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
                         V += U + (uint32_t)__mul24((int)ob, -2048);
                         const uint32_t x = (U << 20) + V;
                         lo[d * 4 + k] = x;
-                        hit |= filt_test(filt, x) << (d * 4 + k);
+                        if (a.mode == 0) hit |= filt_test(filt, x) << (d * 4 + k);
+                        else hit |= (x == 0x12345678u) ? 1u << (d * 4 + k) : 0u;
                     }
                 }
                 hit &= vmask >> (16 * half);
@@ -320,12 +316,7 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
         if (!has_next) break;
         c += stride;
         dsc = dn;
-        if (next_loaded) {
-#pragma unroll
-            for (int d = 0; d < 8; d++) { pw[d] = npw[d]; w[d] = nw[d]; }
-        } else {
-            first_blocks(desc_base(a, dsc), uniform(dsc.x), l, pw, w);
-        }
+        first_blocks(desc_base(a, dsc), uniform(dsc.x), l, pw, w);
         if (c + stride < a.ck_hi) dn = a.P.chunk_desc[c + stride];
     }
     if (pd.n) {
@@ -340,20 +331,31 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
 // ------------------------------------------------------------- k_resolve ----------------
 // One wave per chunk: sort the sparse list, then resolve every event exactly.
 
-__device__ __forceinline__ uint32_t resolve_one(const PlanDev &P, int dmode, const uint8_t *win, uint64_t *h_out,
-                                                uint64_t *val_out)
+// Resolve the window ending at q of buffer b: full hash (from the aligned-block table when the
+// window is a block), then the cache (EQUAL / COLL) and / or the declaration set (MATCH).
+__device__ __forceinline__ uint32_t resolve_one(const PlanDev &P, int dmode, uint32_t b, const uint8_t *base,
+                                                uint32_t q, uint64_t *h_out, uint64_t *val_out)
 {
-    const uint64_t h = wave_window_hash(win);
+    const uint8_t *win = base + q - (XC_SEG - 1u);
+    uint64_t h;
+    if (((q + 1u) & (XC_SEG - 1u)) == 0u && P.blk_h) {
+        const uint32_t bi = uniform(P.blk_base[b]) + (q + 1u) / XC_SEG - 1u;
+        h = ((uint64_t)uniform((uint32_t)(P.blk_h[bi] >> 32)) << 32) | uniform((uint32_t)P.blk_h[bi]);
+    } else {
+        h = wave_window_hash(win);
+    }
     *h_out = h;
     uint64_t v = 0;
-    if (!dmode) {
-        if (!set_find(P.cache, h, &v)) { *val_out = 0; return ST_MISS; }
+    if (dmode != 1 && set_find(P.cache, h, &v)) {
         *val_out = v;
         return wave_equal2048(win, P.segs + v * XC_SEG) ? ST_EQUAL : ST_COLL;
     }
-    if (!set_find(P.dset, h, &v)) { *val_out = 0; return ST_MISS; }
-    *val_out = v;
-    return ST_MATCH;
+    if (dmode != 0 && set_find(P.dset, h, &v)) {
+        *val_out = v;
+        return ST_MATCH;
+    }
+    *val_out = 0;
+    return ST_MISS;
 }
 
 __global__ __launch_bounds__(256) void k_resolve(ResolveArgs a)
@@ -372,7 +374,7 @@ __global__ __launch_bounds__(256) void k_resolve(ResolveArgs a)
         const uint64_t m = ballot(rank == k && l < cnt);
         const uint32_t q = readlane(p, (int)__ffsll((unsigned long long)m) - 1);
         uint64_t h, v;
-        const uint32_t st = resolve_one(a.P, a.dmode, base + q - (XC_SEG - 1u), &h, &v);
+        const uint32_t st = resolve_one(a.P, a.dmode, ck.x, base, q, &h, &v);
         if (l == 0) {
             a.L.pos[c * EV_CAP + k] = q;
             a.L.stat[c * EV_CAP + k] = st;
@@ -471,7 +473,7 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t x, int l)
 
 // Event of the layer exactly at q, or st = NONE.
 __device__ __forceinline__ EvInfo event_at(const PlanDev &P, const Layer &L, Cursor &cur, uint32_t ck1, uint32_t q,
-                                           int dmode, const uint8_t *base)
+                                           int dmode, uint32_t b, const uint8_t *base)
 {
     EvInfo e;
     e.st = NONE;
@@ -479,7 +481,7 @@ __device__ __forceinline__ EvInfo event_at(const PlanDev &P, const Layer &L, Cur
     e.v = 0;
     if (next_event(P, L, cur, ck1, q) != q) return e;
     if (cur.cnt & EV_DENSE) {
-        e.st = resolve_one(P, dmode, base + q - (XC_SEG - 1u), &e.h, &e.v);
+        e.st = resolve_one(P, dmode, b, base, q, &e.h, &e.v);
     } else {
         const int f = __ffsll((unsigned long long)ballot(cur.pos == q)) - 1;
         e.st = readlane(cur.stat, f);
@@ -505,7 +507,7 @@ __global__ __launch_bounds__(64) void k_walk(WalkArgs a)
     const uint32_t ck0 = P.buf_chunk0[b], ck1 = P.buf_chunk0[b + 1];
     const uint32_t tb = P.tok_base[b];
     const uint32_t tcap = 2u * (len / XC_SEG) + 3u;
-    Cursor cs = cur_begin(P, P.S, ck0, ck1);
+    Cursor cs = cur_begin(P, P.S, ck0, ck1);  // cache + predicted declarations
     Cursor cd = cur_begin(P, P.D, ck0, a.use_d ? ck1 : ck0);
     uint32_t ntok = 0, nd = 0;
     uint32_t basep = 0;
@@ -516,11 +518,13 @@ __global__ __launch_bounds__(64) void k_walk(WalkArgs a)
     bool cross = false;
 
     uint32_t n_ext = 0, n_ref = 0;
-    auto emit = [&](uint32_t op, uint32_t lb, uint32_t le, uint32_t seg, uint32_t dpos, uint64_t h) {
+    auto emit = [&](uint32_t op, uint32_t lb, uint32_t le, uint32_t seg, uint32_t dpos, uint64_t h,
+                    uint32_t known) {
         n_ext += op == OP_EXTRACT ? 1u : 0u;
         n_ref += op == OP_REF ? 1u : 0u;
         if (ntok < tcap && l == 0) {
             P.tok_op[tb + ntok] = op;
+            P.tok_known[tb + ntok] = known;
             P.tok_lb[tb + ntok] = lb;
             P.tok_le[tb + ntok] = le;
             P.tok_seg[tb + ntok] = seg;
@@ -530,20 +534,35 @@ __global__ __launch_bounds__(64) void k_walk(WalkArgs a)
         ntok++;
     };
 
+    // Own declarations with a known hash equal to h (lanes search 64 at a time).
+    auto own_decl = [&](uint64_t h) -> uint32_t {
+        for (uint32_t i0 = 0; i0 < nd; i0 += 64u) {
+            const uint32_t i = i0 + l;
+            const uint64_t m = ballot(i < nd && d_known[i] && d_hash[i] == h);
+            if (m) return i0 + (uint32_t)(__ffsll((unsigned long long)m) - 1);
+        }
+        return NONE;
+    };
+
     // Lookup at q (xcodec_encoder.cc:89-118 + xcodec_cache.h:190-210): the cache as of the
-    // batch start (layer S) or a segment this buffer declared earlier (layer D).
+    // batch start, or a segment this buffer declared earlier.  Layer S holds cache hits
+    // (EQUAL / COLL) and predicted-declaration matches (MATCH); layer D, used only when the
+    // walk declared hashes nobody predicted, holds matches against every declaration.
+    // (layer D, when present, is the fresher view: table values can only have decreased)
+    auto decl_info = [&](uint32_t q, EvInfo s) -> EvInfo {
+        if (!a.use_d) return s;
+        return event_at(P, P.D, cd, ck1, q, 1, b, base);
+    };
     auto lookup = [&](uint32_t q, uint64_t *hout) -> uint32_t {
-        EvInfo s = event_at(P, P.S, cs, ck1, q, 0, base);
+        EvInfo s = event_at(P, P.S, cs, ck1, q, 2, b, base);
         if (s.st == ST_EQUAL) { *hout = s.h; return R_HIT; }
         if (s.st == ST_COLL) return R_COLL;
-        if (!a.use_d) return R_MISS;
-        EvInfo d = event_at(P, P.D, cd, ck1, q, 1, base);
+        EvInfo d = decl_info(q, s);
         if (d.st != ST_MATCH) return R_MISS;
-        for (uint32_t i = 0; i < nd; i++) {
-            if (d_known[i] && d_hash[i] == d.h) {
-                *hout = d.h;
-                return wave_equal2048(base + q - (XC_SEG - 1u), base + d_cand[i]) ? R_HIT : R_COLL;
-            }
+        const uint32_t i = own_decl(d.h);
+        if (i != NONE) {
+            *hout = d.h;
+            return wave_equal2048(base + q - (XC_SEG - 1u), base + d_cand[i]) ? R_HIT : R_COLL;
         }
         if ((uint32_t)(d.v >> 32) < b) cross = true;  // an earlier buffer declared it
         return R_MISS;
@@ -554,7 +573,7 @@ __global__ __launch_bounds__(64) void k_walk(WalkArgs a)
             uint64_t h = 0;
             const uint32_t r = lookup(p, &h);
             if (r == R_HIT) {
-                emit(OP_REF, basep, p - (XC_SEG - 1u), p - (XC_SEG - 1u), 0, h);
+                emit(OP_REF, basep, p - (XC_SEG - 1u), p - (XC_SEG - 1u), 0, h, 1);
                 basep = p + 1u;
                 p = basep + (XC_SEG - 1u);
                 continue;
@@ -563,8 +582,8 @@ __global__ __launch_bounds__(64) void k_walk(WalkArgs a)
             cand = (int)(p - (XC_SEG - 1u));
             cand_known = 0;
             cand_h = 0;
-            if (a.use_d) {
-                EvInfo d = event_at(P, P.D, cd, ck1, p, 1, base);
+            {
+                const EvInfo d = decl_info(p, event_at(P, P.S, cs, ck1, p, 2, b, base));
                 if (d.st == ST_MATCH) { cand_known = 1; cand_h = d.h; }
             }
             p++;
@@ -577,7 +596,7 @@ __global__ __launch_bounds__(64) void k_walk(WalkArgs a)
             uint64_t h = 0;
             const uint32_t r = lookup(e, &h);
             if (r == R_HIT) {
-                emit(OP_REF, basep, e - (XC_SEG - 1u), e - (XC_SEG - 1u), 0, h);
+                emit(OP_REF, basep, e - (XC_SEG - 1u), e - (XC_SEG - 1u), 0, h, 1);
                 basep = e + 1u;
                 cand = -1;
                 p = basep + (XC_SEG - 1u);
@@ -588,7 +607,7 @@ __global__ __launch_bounds__(64) void k_walk(WalkArgs a)
         }
         if (dp >= len) break;
         // declaration (xcodec_encoder.cc:77-82, 203-215)
-        emit(OP_EXTRACT, basep, (uint32_t)cand, (uint32_t)cand, dp, cand_h);
+        emit(OP_EXTRACT, basep, (uint32_t)cand, (uint32_t)cand, dp, cand_h, cand_known);
         if (nd < MAX_DECL) {
             if (l == 0) {
                 d_cand[nd] = (uint32_t)cand;
@@ -603,10 +622,10 @@ __global__ __launch_bounds__(64) void k_walk(WalkArgs a)
     }
     // flush (xcodec_encoder.cc:175-201)
     if (cand >= 0) {
-        emit(OP_EXTRACT, basep, (uint32_t)cand, (uint32_t)cand, DPOS_FLUSH, cand_h);
+        emit(OP_EXTRACT, basep, (uint32_t)cand, (uint32_t)cand, DPOS_FLUSH, cand_h, cand_known);
         basep = (uint32_t)cand + XC_SEG;
     }
-    emit(OP_END, basep, len, 0, 0, 0);
+    emit(OP_END, basep, len, 0, 0, 0, 0);
     if (l == 0) {
         P.tok_cnt[b] = ntok;
         P.buf_next[b] = n_ext;
@@ -629,14 +648,38 @@ __global__ __launch_bounds__(64) void k_declhash(DeclArgs a)
     const uint32_t tb = P.tok_base[b], n = P.tok_cnt[b];
     for (uint32_t t = blockIdx.y; t < n; t += gridDim.y) {
         if (uniform(P.tok_op[tb + t]) != OP_EXTRACT) continue;
+        // a known hash came from a resolved match against the scanned declaration set
+        if (uniform(P.tok_known[tb + t])) continue;
         const uint32_t seg = uniform(P.tok_seg[tb + t]);
         const uint64_t h = wave_window_hash(base + seg);
         if (lane_id() == 0) {
             P.tok_h[tb + t] = h;
             const uint64_t v = ((uint64_t)b << 32) | P.tok_dpos[tb + t];
-            if (set_insert(P.dset, h, v, true, nullptr, nullptr) &&
-                __hip_atomic_load(&P.ctl[CTL_GREW], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+            set_insert(P.dset, h, v, true, nullptr, nullptr);
+            // not in the set the positions were scanned against: another round is needed
+            if (__hip_atomic_load(&P.ctl[CTL_GREW], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
                 atomicOr(&P.ctl[CTL_GREW], 1u);
+        }
+    }
+}
+
+// grid (buffers, 4): hash of every aligned 2048-byte block; blocks absent from the cache are
+// the predicted declarations (hit-free data declares exactly these, xcodec_encoder.cc:77-82)
+// and enter the declaration set before the scan.
+__global__ __launch_bounds__(64) void k_blockhash(DeclArgs a)
+{
+    const PlanDev &P = a.P;
+    const uint32_t b = a.j0 + blockIdx.x;
+    if (b >= a.j1) return;
+    const uint8_t *base = P.in + P.buf_off[b];
+    const uint32_t nblk = P.buf_len[b] / XC_SEG, bb = P.blk_base[b];
+    for (uint32_t k = blockIdx.y; k < nblk; k += gridDim.y) {
+        const uint64_t h = wave_window_hash(base + (size_t)k * XC_SEG);
+        uint64_t v;
+        const bool cached = set_find(P.cache, h, &v);
+        if (lane_id() == 0) {
+            P.blk_h[bb + k] = h;
+            if (!cached) set_insert(P.dset, h, ((uint64_t)b << 32) | (k * XC_SEG + 2u * XC_SEG - 1u), true, nullptr, nullptr);
         }
     }
 }
@@ -842,6 +885,18 @@ __global__ __launch_bounds__(64) void k_window_hashes(const uint8_t *in, uint32_
                 out[p] = ((uint64_t)bits_hash << 36) + bytes_hash;
             }
         }
+    }
+}
+
+__global__ void k_or_words(uint4 *dst, const uint4 *a, const uint4 *b, uint32_t n)
+{
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        uint4 x = a[i];
+        if (b) {
+            const uint4 y = b[i];
+            x.x |= y.x; x.y |= y.y; x.z |= y.z; x.w |= y.w;
+        }
+        dst[i] = x;
     }
 }
 

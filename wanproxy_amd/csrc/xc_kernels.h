@@ -67,6 +67,9 @@ struct PlanDev {
     const uint32_t *tok_base;  // [nb]
     uint32_t *tok_cnt;
     uint32_t *tok_lb, *tok_le, *tok_seg, *tok_op, *tok_dpos;
+    uint32_t *tok_known;       // EXTRACT hash known from a resolved event (no rehash needed)
+    const uint32_t *blk_base;  // [nb] first aligned-block index of the buffer
+    uint64_t *blk_h;           // hash of every aligned 2048-byte block (k_blockhash)
     uint64_t *tok_h;
     uint32_t *buf_next;   // [nb] EXTRACT tokens of the buffer (walk)
     uint32_t *buf_nref;   // [nb] REF tokens of the buffer (walk)
@@ -83,11 +86,15 @@ struct ScanArgs {
     Layer L;
     DevSet set;
     uint32_t ck_lo, ck_hi;
+    uint32_t mode;  // ablation (timing only): 0 full, 1 no filter test, 2 loads + block sums only
+    DevSet set2;    // optional second set tested in the same pass (predicted declarations)
+    int has2;
+    const uint2 *l2;  // level-2 filter of set (| set2): one 8-byte L2 read per level-1 positive
 };
 struct ResolveArgs {
     PlanDev P;
     Layer L;
-    int dmode;  // 0: cache layer, 1: declaration layer
+    int dmode;  // 0: cache layer, 1: declaration layer, 2: cache + predicted declarations
     uint32_t ck_lo, ck_hi;
 };
 struct WalkArgs {
@@ -108,6 +115,8 @@ __global__ void k_scan(ScanArgs a);
 __global__ void k_resolve(ResolveArgs a);
 __global__ void k_walk(WalkArgs a);
 __global__ void k_declhash(DeclArgs a);
+__global__ void k_blockhash(DeclArgs a);
+__global__ void k_or_words(uint4 *dst, const uint4 *a, const uint4 *b, uint32_t n);
 __global__ void k_emit(EmitArgs a);
 __global__ void k_alloc(EmitArgs a);
 __global__ void k_hash_segments(const uint8_t *segs, uint64_t n, uint64_t *out);

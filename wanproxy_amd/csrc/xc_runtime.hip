@@ -118,6 +118,7 @@ struct HostSet {
         n_lo = pow2_at_least(entries * 4, 1024);
         if (n_full > (1u << 27) || n_lo > (1u << 25)) return fail(XC_EINVAL, "set too large");
         HIPCHK(hipMalloc(&d.filt, XC_FILT_WORDS * 4));
+        HIPCHK(hipMalloc(&d.l2, (size_t)XC_L2_WORDS * 8));
         HIPCHK(hipMalloc(&d.lo_keys, (size_t)n_lo * 4));
         HIPCHK(hipMalloc(&d.lo_zero, 4));
         HIPCHK(hipMalloc(&d.keys, (size_t)n_full * 8));
@@ -129,6 +130,7 @@ struct HostSet {
     int clear(hipStream_t s)
     {
         HIPCHK(hipMemsetAsync(d.filt, 0, XC_FILT_WORDS * 4, s));
+        HIPCHK(hipMemsetAsync(d.l2, 0, (size_t)XC_L2_WORDS * 8, s));
         HIPCHK(hipMemsetAsync(d.lo_keys, 0, (size_t)n_lo * 4, s));
         HIPCHK(hipMemsetAsync(d.lo_zero, 0, 4, s));
         HIPCHK(hipMemsetAsync(d.keys, 0xFF, (size_t)n_full * 8, s));
@@ -138,6 +140,7 @@ struct HostSet {
     void release()
     {
         hipFree(d.filt);
+        hipFree(d.l2);
         hipFree(d.lo_keys);
         hipFree(d.lo_zero);
         hipFree(d.keys);
@@ -161,6 +164,7 @@ struct xc_cache {
     uint32_t *snap_filt = nullptr;
     uint32_t *snap_lo_zero = nullptr;
     uint32_t *snap_count_dev = nullptr;
+    uint32_t *snap_l2 = nullptr;
 };
 
 static PlanDev cache_plandev(xc_cache *c)
@@ -191,6 +195,7 @@ extern "C" int xc_cache_create(xc_ctx *ctx, uint64_t cap, xc_cache **out)
     HIPCHK(hipMalloc(&c->snap_filt, XC_FILT_WORDS * 4));
     HIPCHK(hipMalloc(&c->snap_lo_zero, 4));
     HIPCHK(hipMalloc(&c->snap_count_dev, 4));
+    HIPCHK(hipMalloc(&c->snap_l2, (size_t)XC_L2_WORDS * 8));
     if ((rc = c->set.clear(ctx->stream))) return rc;
     HIPCHK(hipMemsetAsync(c->count, 0, 4, ctx->stream));
     HIPCHK(hipMemsetAsync(c->ctl, 0, CTL_WORDS * 4, ctx->stream));
@@ -212,6 +217,7 @@ extern "C" int xc_cache_destroy(xc_cache *c)
     hipFree(c->snap_filt);
     hipFree(c->snap_lo_zero);
     hipFree(c->snap_count_dev);
+    hipFree(c->snap_l2);
     delete c;
     return XC_OK;
 }
@@ -244,6 +250,7 @@ extern "C" int xc_cache_snapshot(xc_cache *c)
     HIPCHK(hipMemcpyAsync(c->snap_filt, c->set.d.filt, XC_FILT_WORDS * 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(c->snap_lo_zero, c->set.d.lo_zero, 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(c->snap_count_dev, c->count, 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->snap_l2, c->set.d.l2, (size_t)XC_L2_WORDS * 8, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipStreamSynchronize(s));
     c->has_snap = true;
     return XC_OK;
@@ -264,6 +271,7 @@ static int cache_restore_async(xc_cache *c, uint32_t cur_count)
     HIPCHK(hipMemcpyAsync(c->set.d.filt, c->snap_filt, XC_FILT_WORDS * 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(c->set.d.lo_zero, c->snap_lo_zero, 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(c->count, &c->snap_count, 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->set.d.l2, c->snap_l2, (size_t)XC_L2_WORDS * 8, hipMemcpyDeviceToDevice, s));
     return XC_OK;
 }
 
@@ -284,6 +292,7 @@ extern "C" int xc_cache_restore_async(xc_cache *c)
     HIPCHK(hipMemcpyAsync(c->set.d.filt, c->snap_filt, XC_FILT_WORDS * 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(c->set.d.lo_zero, c->snap_lo_zero, 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(c->count, c->snap_count_dev, 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->set.d.l2, c->snap_l2, (size_t)XC_L2_WORDS * 8, hipMemcpyDeviceToDevice, s));
     return XC_OK;
 }
 
@@ -407,6 +416,8 @@ struct xc_plan {
     uint32_t *d_buf_len, *d_chunk0, *d_tok_base;
     uint2 *d_chunks;
     uint4 *d_desc;
+    uint32_t *d_blk_base;
+    uint32_t *d_l2mix;  // level-2 filter of cache | declaration set for the combined scan
     xc_run_stats stats{};
     // per-kernel HIP-event timing
     bool timing = false;
@@ -474,7 +485,8 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     p->len.assign(lengths, lengths + nbuf);
     p->in_off.resize(nbuf);
     p->out_off.resize(nbuf);
-    std::vector<uint32_t> blen(nbuf), chunk0(nbuf + 1), tok_base(nbuf + 1);
+    std::vector<uint32_t> blen(nbuf), chunk0(nbuf + 1), tok_base(nbuf + 1), blk_base(nbuf + 1);
+    uint64_t nblk = 0;
     std::vector<uint2> chunks;
     std::vector<uint4> descs;
     uint64_t io = 0, oo = 0;
@@ -495,6 +507,8 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
                                            (uint32_t)p->in_off[i], (uint32_t)(p->in_off[i] >> 32)));
             }
         tok_base[i] = (uint32_t)toks;
+        blk_base[i] = (uint32_t)nblk;
+        nblk += n / XC_SEG;
         toks += 2 * (n / XC_SEG) + 3;
     }
     chunk0[nbuf] = (uint32_t)chunks.size();
@@ -576,6 +590,12 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     HIPCHK(hipMalloc(&P.tok_op, nt * 4));
     HIPCHK(hipMalloc(&P.tok_dpos, nt * 4));
     HIPCHK(hipMalloc(&P.tok_h, nt * 8));
+    HIPCHK(hipMalloc(&P.tok_known, nt * 4));
+    HIPCHK(hipMalloc(&P.blk_h, std::max<uint64_t>(nblk, 1) * 8));
+    HIPCHK(hipMalloc(&p->d_blk_base, nb1 * 4));
+    HIPCHK(hipMalloc(&p->d_l2mix, (size_t)XC_L2_WORDS * 8));
+    if (nbuf) HIPCHK(hipMemcpyAsync(p->d_blk_base, blk_base.data(), nbuf * 4, hipMemcpyHostToDevice, s));
+    P.blk_base = p->d_blk_base;
     HIPCHK(hipMalloc(&P.buf_next, nb1 * 4));
     HIPCHK(hipMalloc(&P.buf_nref, nb1 * 4));
     HIPCHK(hipMalloc(&P.buf_slot, nb1 * 4));
@@ -608,6 +628,10 @@ extern "C" int xc_plan_destroy(xc_plan *p)
     hipFree(p->P.tok_op);
     hipFree(p->P.tok_dpos);
     hipFree(p->P.tok_h);
+    hipFree(p->P.tok_known);
+    hipFree(p->P.blk_h);
+    hipFree(p->d_blk_base);
+    hipFree(p->d_l2mix);
     hipFree(p->P.buf_next);
     hipFree(p->P.buf_nref);
     hipFree(p->P.buf_slot);
@@ -660,11 +684,20 @@ static int read_ctl(xc_plan *p, uint32_t *ctl)
     return XC_OK;
 }
 
-static int launch_scan(xc_plan *p, const Layer &L, const DevSet &set, uint32_t ck_lo, uint32_t ck_hi)
+static int launch_scan(xc_plan *p, const Layer &L, const DevSet &set, uint32_t ck_lo, uint32_t ck_hi,
+                       const DevSet *set2 = nullptr)
 {
     if (ck_hi <= ck_lo) return XC_OK;
     xc_ctx *ctx = p->cache->ctx;
-    ScanArgs a{p->P, L, set, ck_lo, ck_hi};
+    ScanArgs a{p->P, L, set, ck_lo, ck_hi, 0, DevSet{}, 0, (const uint2 *)set.l2};
+    if (set2) {
+        a.set2 = *set2;
+        a.has2 = 1;
+        hipLaunchKernelGGL(k_or_words, dim3(512), dim3(256), 0, ctx->stream, (uint4 *)p->d_l2mix,
+                           (const uint4 *)set.l2, (const uint4 *)set2->l2, XC_L2_WORDS / 2);
+        HIPCHK(hipGetLastError());
+        a.l2 = (const uint2 *)p->d_l2mix;
+    }
     KSpan span(p, XC_K_SCAN);
     if (p->timing) p->ktimes.scan_bytes += p->chunk_bytes[ck_hi] - p->chunk_bytes[ck_lo];
     uint32_t need = (ck_hi - ck_lo + SCAN_WAVES - 1) / SCAN_WAVES;
@@ -725,20 +758,28 @@ extern "C" int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, ui
         while (j0 < s1) {
             p->stats.outer_rounds++;
             const uint32_t ck_lo = p->chunk0[j0], ck_hi = p->chunk0[s1];
-            if ((rc = launch_scan(p, p->P.S, p->P.cache, ck_lo, ck_hi))) return rc;
-            if ((rc = launch_resolve(p, p->P.S, 0, ck_lo, ck_hi))) return rc;
+            // predicted declarations (aligned blocks absent from the cache), then one scan of
+            // every position against cache + predictions
             if ((rc = p->dset.clear(s))) return rc;
+            {
+                DeclArgs d{p->P, j0, s1};
+                KSpan span(p, XC_K_DECLHASH);
+                hipLaunchKernelGGL(k_blockhash, dim3(s1 - j0, 4), dim3(64), 0, s, d);
+                HIPCHK(hipGetLastError());
+            }
+            if ((rc = launch_scan(p, p->P.S, p->P.cache, ck_lo, ck_hi, &p->P.dset))) return rc;
+            if ((rc = launch_resolve(p, p->P.S, 2, ck_lo, ck_hi))) return rc;
             if ((rc = launch_walk_round(p, j0, s1, 0))) return rc;
+            if ((rc = read_ctl(p, ctl))) return rc;
             uint32_t rounds = 0;
-            for (;;) {
-                // declaration layer against every hash declared so far, then walk again
+            while (!ctl[CTL_ERROR] && ctl[CTL_GREW]) {
+                // a walk declared hashes nobody predicted: match every position against the
+                // whole declaration set and walk again
+                if (++rounds > MAX_ROUNDS) return fail(XC_EDEVICE, "declaration rounds did not converge");
                 if ((rc = launch_scan(p, p->P.D, p->P.dset, ck_lo, ck_hi))) return rc;
                 if ((rc = launch_resolve(p, p->P.D, 1, ck_lo, ck_hi))) return rc;
                 if ((rc = launch_walk_round(p, j0, s1, 1))) return rc;
                 if ((rc = read_ctl(p, ctl))) return rc;
-                if (ctl[CTL_ERROR]) break;
-                if (!ctl[CTL_GREW]) break;
-                if (++rounds > MAX_ROUNDS) return fail(XC_EDEVICE, "declaration rounds did not converge");
             }
             if (ctl[CTL_ERROR]) break;
             uint32_t jc = std::min<uint32_t>(ctl[CTL_FIRST_CROSS], s1);
@@ -826,6 +867,32 @@ extern "C" int xc__cache_devset(xc_cache *c, void *devset, uint8_t **segs, uint3
 }
 
 extern "C" int xc__set_error(int code, const char *msg) { return fail(code, msg); }
+
+// Internal: time `iters` launches of the scan of the whole plan against the cache set in an
+// ablation mode (ScanArgs::mode); returns microseconds per launch.  Needs P.in set by a run.
+extern "C" double xc__scan_ablation(xc_plan *p, const uint8_t *d_in, int mode, int iters)
+{
+    xc_ctx *ctx = p->cache->ctx;
+    hipSetDevice(ctx->dev);
+    p->P.in = d_in;
+    ScanArgs a{p->P, p->P.S, p->P.cache, 0, p->nchunks, (uint32_t)mode, DevSet{}, 0, (const uint2 *)p->P.cache.l2};
+    uint32_t need = (p->nchunks + SCAN_WAVES - 1) / SCAN_WAVES;
+    uint32_t grid = std::min<uint32_t>(need, (uint32_t)ctx->n_cu);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    hipLaunchKernelGGL(k_scan, dim3(grid), dim3(64 * SCAN_WAVES), 0, ctx->stream, a);
+    hipEventRecord(e0, ctx->stream);
+    for (int i = 0; i < iters; i++)
+        hipLaunchKernelGGL(k_scan, dim3(grid), dim3(64 * SCAN_WAVES), 0, ctx->stream, a);
+    hipEventRecord(e1, ctx->stream);
+    hipEventSynchronize(e1);
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    return 1000.0 * ms / iters;
+}
 
 extern "C" int xc_selftest(xc_ctx *ctx)
 {
