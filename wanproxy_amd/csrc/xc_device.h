@@ -155,6 +155,41 @@ __device__ __forceinline__ void wave_copy(uint8_t *dst, const uint8_t *src, uint
     if (t0 + l < n) dst[t0 + l] = src[t0 + l];
 }
 
+// Copy 2048 bytes from src (any alignment) to dst1 (any alignment) and dst2 (16-byte
+// aligned), reading the source once.  Lane l owns 32 bytes.
+__device__ __forceinline__ void wave_copy2048_dual(uint8_t *dst1, uint8_t *dst2, const uint8_t *src)
+{
+    const uint32_t l = lane_id();
+    uint32_t w[8];
+    load32_unaligned(src + 32u * l, w);
+    uint4 *d2 = (uint4 *)(dst2 + 32u * l);
+    d2[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    d2[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    const uintptr_t a = (uintptr_t)(dst1 + 32u * l);
+    if ((a & 3u) == 0) {
+        uint32_t *d1 = (uint32_t *)a;
+#pragma unroll
+        for (int k = 0; k < 8; k++) d1[k] = w[k];
+    } else {
+        // unaligned destination: the lane's 32 bytes as 4-byte-aligned dwords inside, byte
+        // stores at the two partial ends (never a read-modify-write of a neighbour's bytes)
+        uint8_t *d1 = (uint8_t *)a;
+        const uint32_t head = 4u - (uint32_t)(a & 3u);
+#pragma unroll
+        for (uint32_t k = 0; k < 3; k++)
+            if (k < head) d1[k] = (uint8_t)(w[0] >> (8 * k));
+        uint32_t *dw = (uint32_t *)(d1 + head);
+        const uint32_t sh = head;  // output dword i = bytes [head + 4i, head + 4i + 4)
+#pragma unroll
+        for (int k = 0; k < 7; k++) dw[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+#pragma unroll
+        for (uint32_t k = 0; k < 3; k++) {
+            const uint32_t i = head + 28u + k;  // remaining tail bytes 28+head .. 31
+            if (i < 32u) d1[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3u)));
+        }
+    }
+}
+
 // ---- membership sets -------------------------------------------------------------
 // A set of 64-bit hashes: level-1 bitmap (LDS-loaded by the scan), exact lo32 set,
 // full-key table with a 64-bit value.  Used for the cache (value = segment index)

@@ -726,7 +726,9 @@ __device__ __forceinline__ uint32_t write_escaped(uint8_t *dst, const uint8_t *p
     return o;
 }
 
-__global__ __launch_bounds__(256) void k_emit(EmitArgs a)
+constexpr uint32_t EMIT_WAVES = 8;
+
+__global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
 {
     __shared__ uint32_t sz[MAX_TOK];
     __shared__ uint32_t ord[MAX_TOK];
@@ -738,10 +740,23 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a)
     uint8_t *out = P.out + P.out_off[b];
     const uint32_t tb = P.tok_base[b], n = min(P.tok_cnt[b], MAX_TOK);
 
-    for (uint32_t t = wave; t < n; t += 4u) {
-        const uint32_t lb = P.tok_lb[tb + t], le = P.tok_le[tb + t], op = P.tok_op[tb + t];
-        const uint32_t esc = (le - lb) + count_magic(base + lb, le - lb);
-        if (l == 0) {
+    // token sizes: escaped literal run + op bytes; EXTRACT ordinals for the cache slots
+    for (uint32_t t0 = wave * 64u; t0 < n; t0 += 64u * EMIT_WAVES) {
+        const uint32_t t = t0 + l;
+        uint32_t lb = 0, le = 0, op = OP_END;
+        if (t < n) { lb = P.tok_lb[tb + t]; le = P.tok_le[tb + t]; op = P.tok_op[tb + t]; }
+        uint32_t esc = le - lb;
+        if (ballot(le > lb)) {  // count F1 bytes of non-empty literal runs, one run at a time
+            uint64_t m = ballot(le > lb);
+            while (m) {
+                const int f = __ffsll((unsigned long long)m) - 1;
+                m &= m - 1;
+                const uint32_t flb = readlane(lb, f), fle = readlane(le, f);
+                const uint32_t c = count_magic(base + flb, fle - flb);
+                if ((int)l == f) esc += c;
+            }
+        }
+        if (t < n) {
             sz[t] = esc + (op == OP_EXTRACT ? 2u + XC_SEG : op == OP_REF ? 10u : 0u);
             ord[t] = op == OP_EXTRACT ? 1u : 0u;
         }
@@ -761,30 +776,47 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a)
     }
     __syncthreads();
     const uint32_t slot0 = P.buf_slot[b];
-    for (uint32_t t = wave; t < n; t += 4u) {
+    for (uint32_t t = wave; t < n; t += EMIT_WAVES) {
         const uint32_t lb = P.tok_lb[tb + t], le = P.tok_le[tb + t], op = P.tok_op[tb + t];
         uint8_t *o = out + sz[t];
-        o += write_escaped(o, base + lb, le - lb);
+        if (le > lb) o += write_escaped(o, base + lb, le - lb);
         if (op == OP_REF) {
             const uint64_t h = P.tok_h[tb + t];
             if (l < 10) o[l] = l == 0 ? (uint8_t)XC_MAGIC : l == 1 ? (uint8_t)OP_REF : (uint8_t)(h >> (8 * (9 - l)));
         } else if (op == OP_EXTRACT) {
             const uint32_t seg = P.tok_seg[tb + t];
             if (l == 0) { o[0] = (uint8_t)XC_MAGIC; o[1] = (uint8_t)OP_EXTRACT; }
-            wave_copy(o + 2, base + seg, XC_SEG);
-            // XCodecMemoryCache::enter (xcodec_cache.h:182-188) into the slot k_alloc reserved
+            // the payload goes to the wire and into the slot k_alloc reserved
             const uint32_t idx = slot0 + ord[t];
+            if (idx < P.seg_cap) wave_copy2048_dual(o + 2, P.segs + (size_t)idx * XC_SEG, base + seg);
+            else wave_copy(o + 2, base + seg, XC_SEG);
+        }
+    }
+}
+
+// XCodecMemoryCache::enter (xcodec_cache.h:182-188) of every declaration of buffers
+// [j0, j1): one lane per EXTRACT token, inserts in parallel.
+__global__ __launch_bounds__(64) void k_commit(EmitArgs a)
+{
+    const PlanDev &P = a.P;
+    const uint32_t b = a.j0 + blockIdx.x;
+    if (b >= a.j1) return;
+    const uint32_t tb = P.tok_base[b], n = min(P.tok_cnt[b], MAX_TOK);
+    const uint32_t l = lane_id();
+    uint32_t slot = P.buf_slot[b];
+    for (uint32_t t0 = 0; t0 < n; t0 += 64u) {
+        const uint32_t t = t0 + l;
+        const bool ext = t < n && P.tok_op[tb + t] == OP_EXTRACT;
+        const uint64_t m = ballot(ext);
+        if (ext) {
+            const uint32_t idx = slot + mbcnt(m);
             if (idx < P.seg_cap) {
-                wave_copy(P.segs + (size_t)idx * XC_SEG, base + seg, XC_SEG);
-                if (l == 0) {
-                    uint32_t s1, s2;
-                    set_insert(P.cache, P.tok_h[tb + t], idx, false, &s1, &s2);
-                    P.undo[idx] = make_uint2(s1, s2);
-                }
-            } else if (l == 0) {
-                atomicOr(&P.ctl[CTL_ERROR], ERR_CAPACITY);
+                uint32_t s1, s2;
+                set_insert(P.cache, P.tok_h[tb + t], idx, false, &s1, &s2);
+                P.undo[idx] = make_uint2(s1, s2);
             }
         }
+        slot += (uint32_t)__popcll(m);
     }
 }
 

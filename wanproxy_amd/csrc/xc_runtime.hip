@@ -789,7 +789,9 @@ extern "C" int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, ui
             HIPCHK(hipGetLastError());
             {
                 KSpan span(p, XC_K_EMIT);
-                hipLaunchKernelGGL(k_emit, dim3(jc - j0), dim3(256), 0, s, e);
+                hipLaunchKernelGGL(k_emit, dim3(jc - j0), dim3(512), 0, s, e);
+                HIPCHK(hipGetLastError());
+                hipLaunchKernelGGL(k_commit, dim3(jc - j0), dim3(64), 0, s, e);
                 HIPCHK(hipGetLastError());
             }
             j0 = jc;
