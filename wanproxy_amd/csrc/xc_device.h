@@ -37,6 +37,18 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)
     return x;
 }
 
+// OR over the 64 lanes, result in lane 63 (same DPP pattern as the scan).
+__device__ __forceinline__ uint32_t wave_incl_or(uint32_t x)
+{
+    x |= dpp0<0x111, 0xf>(x);
+    x |= dpp0<0x112, 0xf>(x);
+    x |= dpp0<0x114, 0xf>(x);
+    x |= dpp0<0x118, 0xf>(x);
+    x |= dpp0<0x142, 0xa>(x);
+    x |= dpp0<0x143, 0xc>(x);
+    return x;
+}
+
 __device__ __forceinline__ uint32_t readlane(uint32_t x, int l)
 {
     return (uint32_t)__builtin_amdgcn_readlane((int)x, l);
@@ -98,12 +110,11 @@ __device__ __forceinline__ Sums4 chunk_sums32(const uint32_t w[8])
     return s;
 }
 
-// Full hash of the 2048 bytes at p (any alignment); every lane returns the result.
-__device__ __forceinline__ uint64_t wave_window_hash(const uint8_t *p)
+// Full hash of a 2048-byte window held as 32 bytes per lane (lane l: bytes 32l..32l+31);
+// every lane returns the result.
+__device__ __forceinline__ uint64_t wave_hash_regs(const uint32_t w[8])
 {
     const uint32_t l = lane_id();
-    uint32_t w[8];
-    load32_unaligned(p + 32u * l, w);
     Sums4 s = chunk_sums32(w);
     const uint32_t k = XC_SEG - 32u * l;  // weight of this lane's byte 0 is (2048 - 32l)
     uint32_t s1w = wave_sum(s.aw);
@@ -113,6 +124,41 @@ __device__ __forceinline__ uint64_t wave_window_hash(const uint8_t *p)
     uint32_t bytes_hash = (s1w << 20) + s2w;
     uint32_t bits_hash = (s1f << 16) + s2f;
     return ((uint64_t)bits_hash << 36) + (uint64_t)bytes_hash;
+}
+
+// Full hash of the 2048 bytes at p (any alignment); every lane returns the result.
+__device__ __forceinline__ uint64_t wave_window_hash(const uint8_t *p)
+{
+    uint32_t w[8];
+    load32_unaligned(p + 32u * lane_id(), w);
+    return wave_hash_regs(w);
+}
+
+// Hashes of n <= G consecutive 16-byte-aligned blocks at p: all loads are issued first, then
+// lane i (< n) receives block i's hash.
+template <int G>
+__device__ __forceinline__ uint64_t wave_block_hashes(const uint8_t *p, uint32_t n)
+{
+    const uint32_t l = lane_id();
+    uint32_t w[G][8];
+#pragma unroll
+    for (int i = 0; i < G; i++) {
+        if ((uint32_t)i < n) {
+            const uint4 *q = (const uint4 *)(p + (size_t)i * XC_SEG + 32u * l);
+            const uint4 x = q[0], y = q[1];
+            w[i][0] = x.x; w[i][1] = x.y; w[i][2] = x.z; w[i][3] = x.w;
+            w[i][4] = y.x; w[i][5] = y.y; w[i][6] = y.z; w[i][7] = y.w;
+        }
+    }
+    uint64_t mine = 0;
+#pragma unroll
+    for (int i = 0; i < G; i++) {
+        if ((uint32_t)i < n) {
+            const uint64_t h = wave_hash_regs(w[i]);
+            if (l == (uint32_t)i) mine = h;
+        }
+    }
+    return mine;
 }
 
 // 2048-byte equality of two windows (any alignment); wave-uniform result.

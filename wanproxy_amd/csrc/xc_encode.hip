@@ -171,8 +171,10 @@ __device__ __forceinline__ const uint8_t *desc_base(const ScanArgs &a, const uin
     return a.P.in + (((uint64_t)uniform(d.w) << 32) | uniform(d.z));
 }
 
+template <int MODE>
 __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
 {
+    if (aborted(a.P)) return;
     __shared__ uint2 filt[XC_FILT_WORDS / 2];
     __shared__ uint2 queues[SCAN_WAVES][Q_CAP];
     const uint32_t wave = threadIdx.x >> 6;
@@ -202,6 +204,7 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
 
     Pending pd;
     pd.n = 0;
+    uint32_t sink = 0;  // MODE 3 ablation: filter tests kept alive without queueing
     uint32_t prev_c = NONE, prev_ev = 0;
     bool prev_dense = false;
 
@@ -234,12 +237,13 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
             const uint32_t sufA = ps.totA - ps.preA, sufC = ps.totC - ps.preC;
             const uint32_t S1 = sufA + cs.preA;
             const uint32_t S2 = (XC_SEG + 32u * l) * sufA - sufC + 32u * l * cs.preA - cs.preC;
+            if (MODE == 2) sink = sink * 31u + (S1 ^ S2);
             uint32_t U = S1 - XC_SEG;          // S1 - 2048
             uint32_t V = S2 + 0x80000000u;     // S2 + (2048 << 20)
             const uint32_t q = s + 32u * l;
             const uint32_t vmask = (q + 32u <= c1) ? 0xFFFFFFFFu : (q >= c1 ? 0u : ((1u << (c1 - q)) - 1u));
 #pragma unroll
-            for (int half = 0; half < (a.mode == 2 ? 0 : 2); half++) {
+            for (int half = 0; half < (MODE == 2 ? 0 : 2); half++) {
                 uint32_t lo[16];
                 uint32_t hit = 0;
 #pragma unroll
@@ -252,12 +256,31 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
                         V += U + (uint32_t)__mul24((int)ob, -2048);
                         const uint32_t x = (U << 20) + V;
                         lo[d * 4 + k] = x;
-                        if (a.mode == 0) hit |= filt_test(filt, x) << (d * 4 + k);
+                        if (MODE == 0 || MODE == 3) hit |= filt_test(filt, x) << (d * 4 + k);
                         else hit |= (x == 0x12345678u) ? 1u << (d * 4 + k) : 0u;
                     }
                 }
                 hit &= vmask >> (16 * half);
-                if (ballot(hit != 0u)) {
+                if (MODE == 3) { sink = sink * 31u + hit; hit = 0; }
+                const uint32_t cnt = (uint32_t)__popc(hit);
+                const uint32_t incl = wave_incl_scan(cnt);
+                const uint32_t tot = readlane(incl, 63);
+                if (tot && qn + tot > Q_CAP) scan_flush(a, queue, qn, c, c0, ev_n, dense);
+                if (tot && tot <= Q_CAP) {
+                    // lane-parallel append: this lane's hits go to [qn + excl, qn + excl + cnt);
+                    // loop only over the offsets j where some lane hit
+                    const uint32_t slot = qn + incl - cnt;
+                    uint32_t m = readlane(wave_incl_or(hit), 63);
+#pragma unroll 1
+                    while (m) {
+                        const uint32_t j = (uint32_t)__builtin_ctz(m);
+                        m &= m - 1u;
+                        if ((hit >> j) & 1u)
+                            queue[slot + (uint32_t)__popc(hit & ((1u << j) - 1u))] =
+                                make_uint2(q + 16u * half + j, lo[j]);
+                    }
+                    qn += tot;
+                } else if (tot) {
 #pragma unroll 1
                     for (uint32_t j = 0; j < 16u; j++) {
                         const bool t = (hit >> j) & 1u;
@@ -319,6 +342,7 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
         first_blocks(desc_base(a, dsc), uniform(dsc.x), l, pw, w);
         if (c + stride < a.ck_hi) dn = a.P.chunk_desc[c + stride];
     }
+    if (MODE >= 2 && sink == 0x7FFFFFF0u - a.ck_hi) a.P.ctl[CTL_ERROR] = sink;  // never true; keeps ablations honest
     if (pd.n) {
         if (pd.c == prev_c) {
             pend_complete(a, pd, prev_ev, prev_dense);
@@ -327,6 +351,11 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
         }
     }
 }
+
+template __global__ void k_scan<0>(ScanArgs);
+template __global__ void k_scan<1>(ScanArgs);
+template __global__ void k_scan<2>(ScanArgs);
+template __global__ void k_scan<3>(ScanArgs);
 
 // ------------------------------------------------------------- k_resolve ----------------
 // One wave per chunk: sort the sparse list, then resolve every event exactly.
@@ -358,29 +387,60 @@ __device__ __forceinline__ uint32_t resolve_one(const PlanDev &P, int dmode, uin
     return ST_MISS;
 }
 
+__device__ __forceinline__ uint64_t readlane64(uint64_t x, int l)
+{
+    return ((uint64_t)readlane((uint32_t)(x >> 32), l) << 32) | readlane((uint32_t)x, l);
+}
+
 __global__ __launch_bounds__(256) void k_resolve(ResolveArgs a)
 {
+    if (aborted(a.P)) return;
     const uint32_t c = a.ck_lo + blockIdx.x * 4u + (threadIdx.x >> 6);
     if (c >= a.ck_hi) return;
     const uint32_t cnt = a.L.cnt[c];
     if (cnt == 0 || (cnt & EV_DENSE)) return;
+    const PlanDev &P = a.P;
     const uint32_t l = lane_id();
-    const uint2 ck = a.P.chunks[c];
-    const uint8_t *base = a.P.in + a.P.buf_off[ck.x];
-    uint32_t p = l < cnt ? a.L.pos[c * EV_CAP + l] : NONE;
+    const bool live = l < cnt;
+    const uint2 ck = P.chunks[c];
+    const uint8_t *base = P.in + P.buf_off[ck.x];
+    // sort: lane l ends up holding the event of rank l
+    const uint32_t p0 = live ? a.L.pos[c * EV_CAP + l] : NONE;
     uint32_t rank = 0;
-    for (uint32_t k = 0; k < cnt; k++) rank += readlane(p, (int)k) < p ? 1u : 0u;
-    for (uint32_t k = 0; k < cnt; k++) {
-        const uint64_t m = ballot(rank == k && l < cnt);
-        const uint32_t q = readlane(p, (int)__ffsll((unsigned long long)m) - 1);
-        uint64_t h, v;
-        const uint32_t st = resolve_one(a.P, a.dmode, ck.x, base, q, &h, &v);
-        if (l == 0) {
-            a.L.pos[c * EV_CAP + k] = q;
-            a.L.stat[c * EV_CAP + k] = st;
-            a.L.h[c * EV_CAP + k] = h;
-            a.L.val[c * EV_CAP + k] = v;
-        }
+    for (uint32_t k = 0; k < cnt; k++) rank += readlane(p0, (int)k) < p0 ? 1u : 0u;
+    const uint32_t q = (uint32_t)__builtin_amdgcn_ds_permute((int)(4u * (live ? rank : l)), (int)p0);
+    // full hashes: aligned windows from the block table (lane-parallel), the rest per wave
+    const bool aligned = live && ((q + 1u) & (XC_SEG - 1u)) == 0u && P.blk_h;
+    uint64_t h = 0;
+    if (aligned) h = P.blk_h[P.blk_base[ck.x] + (q + 1u) / XC_SEG - 1u];
+    for (uint64_t m = ballot(live && !aligned); m; m &= m - 1) {
+        const int f = __ffsll((unsigned long long)m) - 1;
+        const uint32_t qf = readlane(q, f);
+        const uint64_t hf = wave_window_hash(base + qf - (XC_SEG - 1u));
+        if ((int)l == f) h = hf;
+    }
+    // cache then declaration-set probes, lane-parallel
+    uint64_t v = 0;
+    uint32_t st = ST_MISS;
+    if (live && a.dmode != 1 && set_find(P.cache, h, &v)) st = ST_EQUAL;
+    if (live && st == ST_MISS && a.dmode != 0) {
+        if (set_find(P.dset, h, &v)) st = ST_MATCH;
+        else v = 0;
+    }
+    // 2048-byte comparisons against the cached segments, one wave-wide compare each
+    for (uint64_t m = ballot(st == ST_EQUAL); m; m &= m - 1) {
+        const int f = __ffsll((unsigned long long)m) - 1;
+        const uint32_t qf = readlane(q, f);
+        const uint64_t vf = readlane64(v, f);
+        const bool eq = wave_equal2048(base + qf - (XC_SEG - 1u), P.segs + vf * XC_SEG);
+        if ((int)l == f && !eq) st = ST_COLL;
+    }
+    if (live) {
+        const uint32_t i = c * EV_CAP + l;
+        a.L.pos[i] = q;
+        a.L.stat[i] = st;
+        a.L.h[i] = h;
+        a.L.val[i] = v;
     }
 }
 
@@ -466,10 +526,6 @@ struct EvInfo {
     uint64_t h, v;
 };
 
-__device__ __forceinline__ uint64_t readlane64(uint64_t x, int l)
-{
-    return ((uint64_t)readlane((uint32_t)(x >> 32), l) << 32) | readlane((uint32_t)x, l);
-}
 
 // Event of the layer exactly at q, or st = NONE.
 __device__ __forceinline__ EvInfo event_at(const PlanDev &P, const Layer &L, Cursor &cur, uint32_t ck1, uint32_t q,
@@ -495,6 +551,7 @@ constexpr uint32_t R_MISS = 0, R_HIT = 1, R_COLL = 2;
 
 __global__ __launch_bounds__(64) void k_walk(WalkArgs a)
 {
+    if (aborted(a.P)) return;
     __shared__ uint32_t d_cand[MAX_DECL];
     __shared__ uint64_t d_hash[MAX_DECL];
     __shared__ uint32_t d_known[MAX_DECL];
@@ -641,6 +698,7 @@ __global__ __launch_bounds__(64) void k_walk(WalkArgs a)
 
 __global__ __launch_bounds__(64) void k_declhash(DeclArgs a)
 {
+    if (aborted(a.P)) return;
     const PlanDev &P = a.P;
     const uint32_t b = a.j0 + blockIdx.x;
     if (b >= a.j1) return;
@@ -665,21 +723,28 @@ __global__ __launch_bounds__(64) void k_declhash(DeclArgs a)
 
 // grid (buffers, 4): hash of every aligned 2048-byte block; blocks absent from the cache are
 // the predicted declarations (hit-free data declares exactly these, xcodec_encoder.cc:77-82)
-// and enter the declaration set before the scan.
+// and enter the declaration set before the scan.  A wave hashes 8 blocks with all loads in
+// flight together, then its lanes probe / insert the 8 hashes in parallel.
+constexpr uint32_t BLK_GROUP = 8;
+
 __global__ __launch_bounds__(64) void k_blockhash(DeclArgs a)
 {
+    if (aborted(a.P)) return;
     const PlanDev &P = a.P;
     const uint32_t b = a.j0 + blockIdx.x;
     if (b >= a.j1) return;
     const uint8_t *base = P.in + P.buf_off[b];
     const uint32_t nblk = P.buf_len[b] / XC_SEG, bb = P.blk_base[b];
-    for (uint32_t k = blockIdx.y; k < nblk; k += gridDim.y) {
-        const uint64_t h = wave_window_hash(base + (size_t)k * XC_SEG);
-        uint64_t v;
-        const bool cached = set_find(P.cache, h, &v);
-        if (lane_id() == 0) {
-            P.blk_h[bb + k] = h;
-            if (!cached) set_insert(P.dset, h, ((uint64_t)b << 32) | (k * XC_SEG + 2u * XC_SEG - 1u), true, nullptr, nullptr);
+    const uint32_t l = lane_id();
+    for (uint32_t k0 = blockIdx.y * BLK_GROUP; k0 < nblk; k0 += gridDim.y * BLK_GROUP) {
+        const uint32_t n = min(BLK_GROUP, nblk - k0);
+        const uint64_t h = wave_block_hashes<BLK_GROUP>(base + (size_t)k0 * XC_SEG, n);
+        if (l < n) {
+            uint64_t v;
+            P.blk_h[bb + k0 + l] = h;
+            if (!set_find(P.cache, h, &v))
+                set_insert(P.dset, h, ((uint64_t)b << 32) | ((k0 + l) * XC_SEG + 2u * XC_SEG - 1u), true, nullptr,
+                           nullptr);
         }
     }
 }
@@ -730,6 +795,7 @@ constexpr uint32_t EMIT_WAVES = 8;
 
 __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
 {
+    if (aborted(a.P)) return;
     __shared__ uint32_t sz[MAX_TOK];
     __shared__ uint32_t ord[MAX_TOK];
     const PlanDev &P = a.P;
@@ -798,6 +864,7 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
 // [j0, j1): one lane per EXTRACT token, inserts in parallel.
 __global__ __launch_bounds__(64) void k_commit(EmitArgs a)
 {
+    if (aborted(a.P)) return;
     const PlanDev &P = a.P;
     const uint32_t b = a.j0 + blockIdx.x;
     if (b >= a.j1) return;
@@ -824,6 +891,7 @@ __global__ __launch_bounds__(64) void k_commit(EmitArgs a)
 // (exclusive prefix of buf_next on top of the current segment count), plus run totals.
 __global__ __launch_bounds__(1024) void k_alloc(EmitArgs a)
 {
+    if (aborted(a.P)) return;
     __shared__ uint32_t wsum[16][2];
     __shared__ uint32_t carry[2];
     const PlanDev &P = a.P;
@@ -917,6 +985,17 @@ __global__ __launch_bounds__(64) void k_window_hashes(const uint8_t *in, uint32_
                 out[p] = ((uint64_t)bits_hash << 36) + bytes_hash;
             }
         }
+    }
+}
+
+// Async sub-batch pipeline gate: after sub-batch sb's first walk round, stop the enqueued
+// pipeline if the host has to step in (declaration growth, a cross-buffer conflict, an error).
+__global__ void k_gate(PlanDev P, uint32_t sb, uint32_t s1)
+{
+    if (threadIdx.x != 0 || P.ctl[CTL_ABORT]) return;
+    if (P.ctl[CTL_GREW] || P.ctl[CTL_FIRST_CROSS] < s1 || P.ctl[CTL_ERROR]) {
+        P.ctl[CTL_ABORT_SB] = sb;
+        P.ctl[CTL_ABORT] = 1u;
     }
 }
 

@@ -34,6 +34,8 @@ enum : uint32_t {
     CTL_NEXTRACT = 4,
     CTL_NREF = 5,
     CTL_UNDO = 6,
+    CTL_ABORT = 7,     // set by k_gate: a sub-batch needs the host (growth, cross-buffer, error)
+    CTL_ABORT_SB = 8,  // ... and which one; every later pipeline kernel exits at once
     CTL_WORDS = 16
 };
 constexpr uint32_t ERR_CAPACITY = 1, ERR_TOKENS = 2, ERR_DECLS = 4;
@@ -81,6 +83,12 @@ struct PlanDev {
 };
 
 // kernel argument blocks (shared by xc_encode.hip and xc_runtime.hip)
+// Pipeline kernels exit at once when the async sub-batch pipeline has been stopped.
+__device__ __forceinline__ bool aborted(const PlanDev &P)
+{
+    return __builtin_amdgcn_readfirstlane((int)*(volatile const uint32_t *)&P.ctl[CTL_ABORT]) != 0;
+}
+
 struct ScanArgs {
     PlanDev P;
     Layer L;
@@ -111,7 +119,7 @@ struct EmitArgs {
     uint32_t j0, j1;
 };
 
-__global__ void k_scan(ScanArgs a);
+template <int MODE> __global__ void k_scan(ScanArgs a);
 __global__ void k_resolve(ResolveArgs a);
 __global__ void k_walk(WalkArgs a);
 __global__ void k_declhash(DeclArgs a);
@@ -120,6 +128,7 @@ __global__ void k_or_words(uint4 *dst, const uint4 *a, const uint4 *b, uint32_t 
 __global__ void k_emit(EmitArgs a);
 __global__ void k_alloc(EmitArgs a);
 __global__ void k_commit(EmitArgs a);
+__global__ void k_gate(PlanDev P, uint32_t sb, uint32_t s1);
 __global__ void k_hash_segments(const uint8_t *segs, uint64_t n, uint64_t *out);
 __global__ void k_window_hashes(const uint8_t *in, uint32_t n, uint64_t *out);
 __global__ void k_undo(DevSet cache, const uint2 *undo, uint32_t from, uint32_t to);

@@ -600,6 +600,7 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     HIPCHK(hipMalloc(&P.buf_nref, nb1 * 4));
     HIPCHK(hipMalloc(&P.buf_slot, nb1 * 4));
     HIPCHK(hipMalloc(&P.ctl, CTL_WORDS * 4));
+    HIPCHK(hipMemsetAsync(P.ctl, 0, CTL_WORDS * 4, s));
     P.out_off = p->d_out_off;
     HIPCHK(hipStreamSynchronize(s));
     *out = p;
@@ -702,7 +703,7 @@ static int launch_scan(xc_plan *p, const Layer &L, const DevSet &set, uint32_t c
     if (p->timing) p->ktimes.scan_bytes += p->chunk_bytes[ck_hi] - p->chunk_bytes[ck_lo];
     uint32_t need = (ck_hi - ck_lo + SCAN_WAVES - 1) / SCAN_WAVES;
     uint32_t grid = std::min<uint32_t>(need, (uint32_t)ctx->n_cu);
-    hipLaunchKernelGGL(k_scan, dim3(grid), dim3(64 * SCAN_WAVES), 0, ctx->stream, a);
+    hipLaunchKernelGGL(k_scan<0>, dim3(grid), dim3(64 * SCAN_WAVES), 0, ctx->stream, a);
     HIPCHK(hipGetLastError());
     return XC_OK;
 }
@@ -720,9 +721,8 @@ static int launch_resolve(xc_plan *p, const Layer &L, int dmode, uint32_t ck_lo,
 static int launch_walk_round(xc_plan *p, uint32_t j0, uint32_t j1, int use_d)
 {
     hipStream_t s = p->cache->ctx->stream;
-    const uint32_t none = NONE;
     HIPCHK(hipMemsetAsync(p->P.ctl + CTL_GREW, 0, 4, s));
-    HIPCHK(hipMemcpyAsync(p->P.ctl + CTL_FIRST_CROSS, &none, 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(p->P.ctl + CTL_FIRST_CROSS), NONE, 1, s));
     WalkArgs w{p->P, j0, j1, use_d};
     {
         KSpan span(p, XC_K_WALK);
@@ -739,6 +739,83 @@ static int launch_walk_round(xc_plan *p, uint32_t j0, uint32_t j1, int use_d)
     return XC_OK;
 }
 
+static int launch_emit(xc_plan *p, uint32_t j0, uint32_t jc)
+{
+    hipStream_t s = p->cache->ctx->stream;
+    EmitArgs e{p->P, j0, jc};
+    hipLaunchKernelGGL(k_alloc, dim3(1), dim3(1024), 0, s, e);
+    HIPCHK(hipGetLastError());
+    KSpan span(p, XC_K_EMIT);
+    hipLaunchKernelGGL(k_emit, dim3(jc - j0), dim3(512), 0, s, e);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_commit, dim3(jc - j0), dim3(64), 0, s, e);
+    HIPCHK(hipGetLastError());
+    return XC_OK;
+}
+
+// Predicted declarations (aligned blocks absent from the cache), then one scan of every
+// position of buffers [j0, s1) against cache + predictions, resolve, first walk round.
+static int launch_first_round(xc_plan *p, uint32_t j0, uint32_t s1)
+{
+    hipStream_t s = p->cache->ctx->stream;
+    int rc;
+    const uint32_t ck_lo = p->chunk0[j0], ck_hi = p->chunk0[s1];
+    p->stats.outer_rounds++;
+    if ((rc = p->dset.clear(s))) return rc;
+    {
+        DeclArgs d{p->P, j0, s1};
+        KSpan span(p, XC_K_DECLHASH);
+        hipLaunchKernelGGL(k_blockhash, dim3(s1 - j0, 4), dim3(64), 0, s, d);
+        HIPCHK(hipGetLastError());
+    }
+    if ((rc = launch_scan(p, p->P.S, p->P.cache, ck_lo, ck_hi, &p->P.dset))) return rc;
+    if ((rc = launch_resolve(p, p->P.S, 2, ck_lo, ck_hi))) return rc;
+    return launch_walk_round(p, j0, s1, 0);
+}
+
+// Sub-batch sb with no host synchronisation: first round, gate, emit of the whole sub-batch.
+static int encode_sub_async(xc_plan *p, uint32_t sb)
+{
+    const uint32_t j0 = p->sub[sb], s1 = p->sub[sb + 1];
+    int rc;
+    p->stats.sub_batches++;
+    if ((rc = launch_first_round(p, j0, s1))) return rc;
+    hipLaunchKernelGGL(k_gate, dim3(1), dim3(64), 0, p->cache->ctx->stream, p->P, sb, s1);
+    HIPCHK(hipGetLastError());
+    return launch_emit(p, j0, s1);
+}
+
+// Sub-batch sb step by step: declaration-growth rounds until D is closed, then emit up to the
+// first buffer whose lookups an earlier buffer's new declarations would change, and repeat
+// from there (outer rounds).
+static int encode_sub_sync(xc_plan *p, uint32_t sb, uint32_t *ctl)
+{
+    const uint32_t s1 = p->sub[sb + 1];
+    uint32_t j0 = p->sub[sb];
+    int rc;
+    while (j0 < s1) {
+        const uint32_t ck_lo = p->chunk0[j0], ck_hi = p->chunk0[s1];
+        if ((rc = launch_first_round(p, j0, s1))) return rc;
+        if ((rc = read_ctl(p, ctl))) return rc;
+        uint32_t rounds = 0;
+        while (!ctl[CTL_ERROR] && ctl[CTL_GREW]) {
+            // a walk declared hashes nobody predicted: match every position against the
+            // whole declaration set and walk again
+            if (++rounds > MAX_ROUNDS) return fail(XC_EDEVICE, "declaration rounds did not converge");
+            if ((rc = launch_scan(p, p->P.D, p->P.dset, ck_lo, ck_hi))) return rc;
+            if ((rc = launch_resolve(p, p->P.D, 1, ck_lo, ck_hi))) return rc;
+            if ((rc = launch_walk_round(p, j0, s1, 1))) return rc;
+            if ((rc = read_ctl(p, ctl))) return rc;
+        }
+        if (ctl[CTL_ERROR]) return XC_OK;
+        uint32_t jc = std::min<uint32_t>(ctl[CTL_FIRST_CROSS], s1);
+        if (jc <= j0) jc = j0 + 1;  // cannot happen (buffer j0 has no earlier buffer); progress guard
+        if ((rc = launch_emit(p, j0, jc))) return rc;
+        j0 = jc;
+    }
+    return XC_OK;
+}
+
 extern "C" int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_out_len)
 {
     if (!p || (!d_in && p->nb) || (!d_out && p->nb) || (!d_out_len && p->nb)) return fail(XC_EINVAL, "null");
@@ -751,51 +828,22 @@ extern "C" int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, ui
     p->stats = xc_run_stats{};
     HIPCHK(hipMemsetAsync(p->P.ctl, 0, CTL_WORDS * 4, s));
     uint32_t ctl[CTL_WORDS];
-    for (size_t si = 0; si + 1 < p->sub.size(); si++) {
-        const uint32_t s1 = p->sub[si + 1];
-        uint32_t j0 = p->sub[si];
-        p->stats.sub_batches++;
-        while (j0 < s1) {
-            p->stats.outer_rounds++;
-            const uint32_t ck_lo = p->chunk0[j0], ck_hi = p->chunk0[s1];
-            // predicted declarations (aligned blocks absent from the cache), then one scan of
-            // every position against cache + predictions
-            if ((rc = p->dset.clear(s))) return rc;
-            {
-                DeclArgs d{p->P, j0, s1};
-                KSpan span(p, XC_K_DECLHASH);
-                hipLaunchKernelGGL(k_blockhash, dim3(s1 - j0, 4), dim3(64), 0, s, d);
-                HIPCHK(hipGetLastError());
-            }
-            if ((rc = launch_scan(p, p->P.S, p->P.cache, ck_lo, ck_hi, &p->P.dset))) return rc;
-            if ((rc = launch_resolve(p, p->P.S, 2, ck_lo, ck_hi))) return rc;
-            if ((rc = launch_walk_round(p, j0, s1, 0))) return rc;
-            if ((rc = read_ctl(p, ctl))) return rc;
-            uint32_t rounds = 0;
-            while (!ctl[CTL_ERROR] && ctl[CTL_GREW]) {
-                // a walk declared hashes nobody predicted: match every position against the
-                // whole declaration set and walk again
-                if (++rounds > MAX_ROUNDS) return fail(XC_EDEVICE, "declaration rounds did not converge");
-                if ((rc = launch_scan(p, p->P.D, p->P.dset, ck_lo, ck_hi))) return rc;
-                if ((rc = launch_resolve(p, p->P.D, 1, ck_lo, ck_hi))) return rc;
-                if ((rc = launch_walk_round(p, j0, s1, 1))) return rc;
-                if ((rc = read_ctl(p, ctl))) return rc;
-            }
-            if (ctl[CTL_ERROR]) break;
-            uint32_t jc = std::min<uint32_t>(ctl[CTL_FIRST_CROSS], s1);
-            if (jc <= j0) jc = j0 + 1;  // cannot happen (buffer j0 has no earlier buffer); progress guard
-            EmitArgs e{p->P, j0, jc};
-            hipLaunchKernelGGL(k_alloc, dim3(1), dim3(1024), 0, s, e);
-            HIPCHK(hipGetLastError());
-            {
-                KSpan span(p, XC_K_EMIT);
-                hipLaunchKernelGGL(k_emit, dim3(jc - j0), dim3(512), 0, s, e);
-                HIPCHK(hipGetLastError());
-                hipLaunchKernelGGL(k_commit, dim3(jc - j0), dim3(64), 0, s, e);
-                HIPCHK(hipGetLastError());
-            }
-            j0 = jc;
-        }
+    const size_t nsub = p->sub.size() - 1;
+    size_t si = 0;
+    while (si < nsub) {
+        // Async pass: enqueue every remaining sub-batch with no host round trip.  k_gate
+        // stops the device pipeline at the first sub-batch that needs the host.
+        for (size_t k = si; k < nsub; k++)
+            if ((rc = encode_sub_async(p, (uint32_t)k))) return rc;
+        if ((rc = read_ctl(p, ctl))) return rc;
+        if (!ctl[CTL_ABORT]) break;
+        si = ctl[CTL_ABORT_SB];
+        HIPCHK(hipMemsetAsync(p->P.ctl + CTL_ABORT, 0, 4, s));
+        if (ctl[CTL_ERROR]) break;
+        // that sub-batch, step by step (its pipeline state is discarded and redone)
+        if ((rc = encode_sub_sync(p, (uint32_t)si, ctl))) return rc;
+        if (ctl[CTL_ERROR]) break;
+        si++;
     }
     if ((rc = read_ctl(p, ctl))) return rc;
     for (uint64_t i = 0; i < p->nb; i++) p->stats.in_bytes += p->len[i];
@@ -883,10 +931,11 @@ extern "C" double xc__scan_ablation(xc_plan *p, const uint8_t *d_in, int mode, i
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    hipLaunchKernelGGL(k_scan, dim3(grid), dim3(64 * SCAN_WAVES), 0, ctx->stream, a);
+    auto kern = mode == 0 ? k_scan<0> : mode == 1 ? k_scan<1> : mode == 2 ? k_scan<2> : k_scan<3>;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * SCAN_WAVES), 0, ctx->stream, a);
     hipEventRecord(e0, ctx->stream);
     for (int i = 0; i < iters; i++)
-        hipLaunchKernelGGL(k_scan, dim3(grid), dim3(64 * SCAN_WAVES), 0, ctx->stream, a);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * SCAN_WAVES), 0, ctx->stream, a);
     hipEventRecord(e1, ctx->stream);
     hipEventSynchronize(e1);
     float ms = 0;
