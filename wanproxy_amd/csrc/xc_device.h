@@ -201,48 +201,50 @@ __device__ __forceinline__ void wave_copy(uint8_t *dst, const uint8_t *src, uint
     if (t0 + l < n) dst[t0 + l] = src[t0 + l];
 }
 
-// Copy 2048 bytes from src (any alignment) to dst1 (any alignment) and dst2 (16-byte
-// aligned), reading the source once.  Lane l owns 32 bytes.
-__device__ __forceinline__ void wave_copy2048_dual(uint8_t *dst1, uint8_t *dst2, const uint8_t *src)
+// 16 bytes at an arbitrary address (aligned dword loads + alignbyte).
+__device__ __forceinline__ uint4 load16_unaligned(const uint8_t *p)
+{
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    const uint32_t v0 = w[0], v1 = w[1], v2 = w[2], v3 = w[3], v4 = sh ? w[4] : 0u;
+    return make_uint4(__builtin_amdgcn_alignbyte(v1, v0, sh), __builtin_amdgcn_alignbyte(v2, v1, sh),
+                      __builtin_amdgcn_alignbyte(v3, v2, sh), __builtin_amdgcn_alignbyte(v4, v3, sh));
+}
+
+// A 2048-byte payload from src (any alignment) to the wire at out (any alignment) and to a
+// cache slot at seg (16-byte aligned).  Every store is a whole 16-byte aligned store except
+// the wire copy's head and tail bytes; the second read of src hits the cache.
+__device__ __forceinline__ void wave_copy_payload(uint8_t *out, uint8_t *seg, const uint8_t *src)
 {
     const uint32_t l = lane_id();
-    uint32_t w[8];
-    load32_unaligned(src + 32u * l, w);
-    uint4 *d2 = (uint4 *)(dst2 + 32u * l);
-    d2[0] = make_uint4(w[0], w[1], w[2], w[3]);
-    d2[1] = make_uint4(w[4], w[5], w[6], w[7]);
-    const uintptr_t a = (uintptr_t)(dst1 + 32u * l);
-    if ((a & 3u) == 0) {
-        uint32_t *d1 = (uint32_t *)a;
-#pragma unroll
-        for (int k = 0; k < 8; k++) d1[k] = w[k];
-    } else {
-        // unaligned destination: the lane's 32 bytes as 4-byte-aligned dwords inside, byte
-        // stores at the two partial ends (never a read-modify-write of a neighbour's bytes)
-        uint8_t *d1 = (uint8_t *)a;
-        const uint32_t head = 4u - (uint32_t)(a & 3u);
-#pragma unroll
-        for (uint32_t k = 0; k < 3; k++)
-            if (k < head) d1[k] = (uint8_t)(w[0] >> (8 * k));
-        uint32_t *dw = (uint32_t *)(d1 + head);
-        const uint32_t sh = head;  // output dword i = bytes [head + 4i, head + 4i + 4)
-#pragma unroll
-        for (int k = 0; k < 7; k++) dw[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
-#pragma unroll
-        for (uint32_t k = 0; k < 3; k++) {
-            const uint32_t i = head + 28u + k;  // remaining tail bytes 28+head .. 31
-            if (i < 32u) d1[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3u)));
-        }
+    const uint32_t head = (uint32_t)((16u - ((uintptr_t)out & 15u)) & 15u);
+    const uint32_t nbody = (XC_SEG - head) >> 4;
+    const uint4 a0 = load16_unaligned(src + 16u * l), a1 = load16_unaligned(src + 1024u + 16u * l);
+    uint4 b0 = a0, b1 = a1;
+    if (head) {
+        if (l < nbody) b0 = load16_unaligned(src + head + 16u * l);
+        if (l + 64u < nbody) b1 = load16_unaligned(src + head + 1024u + 16u * l);
     }
+    uint8_t h = 0, t = 0;
+    const uint32_t t0 = head + 16u * nbody;
+    if (l < head) h = src[l];
+    if (t0 + l < XC_SEG) t = src[t0 + l];
+    ((uint4 *)seg)[l] = a0;
+    ((uint4 *)seg)[l + 64u] = a1;
+    if (l < nbody) *(uint4 *)(out + head + 16u * l) = b0;
+    if (l + 64u < nbody) *(uint4 *)(out + head + 1024u + 16u * l) = b1;
+    if (l < head) out[l] = h;
+    if (t0 + l < XC_SEG) out[t0 + l] = t;
 }
 
 // ---- membership sets -------------------------------------------------------------
 // A set of 64-bit hashes: level-1 bitmap (LDS-loaded by the scan), exact lo32 set,
 // full-key table with a 64-bit value.  Used for the cache (value = segment index)
 // and for a batch's declarations (value = buffer<<32 | declaration position, min-wins).
-// Level-1 filter: a blocked k=2 Bloom filter of 16384 64-bit words (128 KB, one scan
-// workgroup's LDS image).  lo32 (the hash's bytes_hash half) picks word lo>>18; the key sets
-// bit lo[4:0] of the word's low dword and bit lo[9:5] of its high dword.
+// Level-1 filter: a blocked k=2 Bloom filter of 32768 32-bit words (128 KB, one scan
+// workgroup's LDS image).  lo32 (the hash's bytes_hash half) picks word lo>>17; the key sets
+// bits lo[4:0] and lo[9:5] of that word.  One ds_read_b32 per tested position.
 #define XC_FILT_WORDS 32768u  // in 32-bit words
 #define XC_EMPTY64 0xFFFFFFFFFFFFFFFFull           // H never has bits 32..35 set
 
@@ -272,10 +274,10 @@ struct DevSet {
     uint64_t *vals;
 };
 
-__device__ __forceinline__ uint32_t filt_test(const uint2 *f, uint32_t lo)
+__device__ __forceinline__ uint32_t filt_test(const uint32_t *f, uint32_t lo)
 {
-    const uint2 w = f[lo >> 18];
-    return (w.x >> (lo & 31u)) & (w.y >> ((lo >> 5) & 31u)) & 1u;
+    const uint32_t w = f[lo >> 17];
+    return (w >> (lo & 31u)) & (w >> ((lo >> 5) & 31u)) & 1u;
 }
 __device__ __forceinline__ uint32_t lo_slot(uint32_t lo, uint32_t mask) { return (lo * 0x9E3779B1u) >> 7 & mask; }
 __device__ __forceinline__ uint32_t key_slot(uint64_t h, uint32_t mask)
@@ -340,9 +342,7 @@ __device__ __forceinline__ int set_insert(const DevSet &s, uint64_t h, uint64_t 
                 j = (j + 1u) & s.lo_mask;
             }
         }
-        const uint32_t wi = (lo >> 18) * 2u;
-        atomicOr(&s.filt[wi], 1u << (lo & 31u));
-        atomicOr(&s.filt[wi + 1u], 1u << ((lo >> 5) & 31u));
+        atomicOr(&s.filt[lo >> 17], (1u << (lo & 31u)) | (1u << ((lo >> 5) & 31u)));
         const uint32_t g = l2_mix(lo), gi = (g >> 14) * 2u;
         atomicOr(&s.l2[gi], 1u << (g & 31u));
         atomicOr(&s.l2[gi + 1u], 1u << ((g >> 5) & 31u));

@@ -58,6 +58,25 @@ __device__ __forceinline__ void scan_record(const ScanArgs &a, uint32_t c, uint3
 // overlaps the next 2048-position iteration: issue() moves up to 128 queued (position, lo32)
 // pairs into registers and starts their level-2 filter loads (one 8-byte L2 read each);
 // complete() tests them one iteration later and probes the exact lo32 sets for survivors.
+// Exact lo32 membership in set | set2: the first slots of both tables are loaded together.
+__device__ __forceinline__ bool scan_has_lo(const ScanArgs &a, uint32_t lo)
+{
+    if (lo == 0u) return *a.set.lo_zero != 0u || (a.has2 && *a.set2.lo_zero != 0u);
+    uint32_t i1 = lo_slot(lo, a.set.lo_mask), i2 = a.has2 ? lo_slot(lo, a.set2.lo_mask) : 0u;
+    uint32_t k1 = a.set.lo_keys[i1];
+    uint32_t k2 = a.has2 ? a.set2.lo_keys[i2] : 0u;
+    while (k1 != 0u && k1 != lo) {
+        i1 = (i1 + 1u) & a.set.lo_mask;
+        k1 = a.set.lo_keys[i1];
+    }
+    if (k1 == lo) return true;
+    while (k2 != 0u && k2 != lo) {
+        i2 = (i2 + 1u) & a.set2.lo_mask;
+        k2 = a.set2.lo_keys[i2];
+    }
+    return k2 == lo;
+}
+
 struct Pending {
     uint32_t n;          // entries (uniform); 0 = nothing pending
     uint32_t c, c0;      // chunk the entries belong to
@@ -94,8 +113,7 @@ __device__ __forceinline__ void pend_complete(const ScanArgs &a, Pending &pd, ui
         const uint32_t i = lane_id() + 64u * s;
         bool match = false;
         if (i < pd.n && l2_test(pd.w[s], l2_mix(pd.lo[s]))) {
-            const uint32_t lo = pd.lo[s];
-            match = set_has_lo(a.set, lo) || (a.has2 && set_has_lo(a.set2, lo));
+            match = scan_has_lo(a, pd.lo[s]);
         }
         scan_record(a, pd.c, pd.c0, match, pd.pos[s], ev_n, dense);
     }
@@ -114,7 +132,7 @@ __device__ __forceinline__ void scan_flush(const ScanArgs &a, uint2 *queue, uint
             pos = e.x;
             const uint32_t g = l2_mix(e.y);
             if (l2_test(a.l2[g >> 14], g))
-                match = set_has_lo(a.set, e.y) || (a.has2 && set_has_lo(a.set2, e.y));
+                match = scan_has_lo(a, e.y);
         }
         scan_record(a, c, c0, match, pos, ev_n, dense);
     }
@@ -175,32 +193,36 @@ template <int MODE>
 __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
 {
     if (aborted(a.P)) return;
-    __shared__ uint2 filt[XC_FILT_WORDS / 2];
+    __shared__ uint32_t filt[XC_FILT_WORDS];
     __shared__ uint2 queues[SCAN_WAVES][Q_CAP];
     const uint32_t wave = threadIdx.x >> 6;
     uint2 *queue = queues[wave];
     const uint32_t l = lane_id();
 
-    for (uint32_t i = threadIdx.x * 2u; i < XC_FILT_WORDS / 2; i += 2048u) {
-        uint4 f = *(const uint4 *)(a.set.filt + 2 * i);
+    for (uint32_t i = threadIdx.x * 4u; i < XC_FILT_WORDS; i += 4096u) {
+        uint4 f = *(const uint4 *)(a.set.filt + i);
         if (a.has2) {
-            const uint4 g = *(const uint4 *)(a.set2.filt + 2 * i);
+            const uint4 g = *(const uint4 *)(a.set2.filt + i);
             f.x |= g.x; f.y |= g.y; f.z |= g.z; f.w |= g.w;
         }
         *(uint4 *)(filt + i) = f;
     }
     __syncthreads();
 
-    const uint32_t stride = gridDim.x * SCAN_WAVES;
-    uint32_t c = a.ck_lo + blockIdx.x * SCAN_WAVES + wave;
-    if (c >= a.ck_hi) return;
+    // each wave scans a contiguous run of chunks, so consecutive chunks of one buffer continue
+    // the block stream (and its prefetch) without a restart
+    const uint32_t nwaves = gridDim.x * SCAN_WAVES, nck = a.ck_hi - a.ck_lo;
+    const uint32_t per = (nck + nwaves - 1u) / nwaves;
+    uint32_t c = a.ck_lo + (blockIdx.x * SCAN_WAVES + wave) * per;
+    const uint32_t c_end = min(c + per, a.ck_hi);
+    if (c >= c_end) return;
 
     // chunk descriptors: {c0, c1, arena offset lo, hi}; the next one is always in flight
     uint4 dsc = a.P.chunk_desc[c];
     uint32_t pw[8], w[8];
     first_blocks(desc_base(a, dsc), uniform(dsc.x), l, pw, w);
     uint4 dn = make_uint4(0, 0, 0, 0);
-    if (c + stride < a.ck_hi) dn = a.P.chunk_desc[c + stride];
+    if (c + 1u < c_end) dn = a.P.chunk_desc[c + 1u];
 
     Pending pd;
     pd.n = 0;
@@ -211,7 +233,10 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
     for (;;) {
         const uint32_t c0 = uniform(dsc.x), c1 = uniform(dsc.y);
         const uint8_t *base = desc_base(a, dsc);
-        const bool has_next = c + stride < a.ck_hi;
+        const bool has_next = c + 1u < c_end;
+        // the next chunk continues this one (same buffer, starts at c1): keep streaming
+        const bool contig = has_next && uniform(dn.x) == c1 && uniform(dn.z) == uniform(dsc.z) &&
+                            uniform(dn.w) == uniform(dsc.w);
         uint32_t ev_n = 0, qn = 0;
         bool dense = false;
 
@@ -229,7 +254,7 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
         for (; s < c1; s += XC_SEG) {
             // prefetch: the next block of this chunk, or the next chunk's first two blocks
             uint32_t wn[8];
-            const bool last = s + XC_SEG >= c1;
+            const bool last = s + XC_SEG >= c1 && !contig;
             if (!last) load32_aligned(base + s + XC_SEG + 32u * l, wn);
             const BlockSums cs = block_sums(w, l);
             // window ending just before this lane's first position q = s + 32 l:
@@ -337,10 +362,10 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
             if (l == 0 && dense) atomicAdd(&a.P.ctl[CTL_DENSE], 1u);
         }
         if (!has_next) break;
-        c += stride;
+        c += 1u;
         dsc = dn;
-        first_blocks(desc_base(a, dsc), uniform(dsc.x), l, pw, w);
-        if (c + stride < a.ck_hi) dn = a.P.chunk_desc[c + stride];
+        if (!contig) first_blocks(desc_base(a, dsc), uniform(dsc.x), l, pw, w);
+        if (c + 1u < c_end) dn = a.P.chunk_desc[c + 1u];
     }
     if (MODE >= 2 && sink == 0x7FFFFFF0u - a.ck_hi) a.P.ctl[CTL_ERROR] = sink;  // never true; keeps ablations honest
     if (pd.n) {
@@ -395,6 +420,10 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t x, int l)
 __global__ __launch_bounds__(256) void k_resolve(ResolveArgs a)
 {
     if (aborted(a.P)) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // the walk that follows reports afresh
+        a.P.ctl[CTL_GREW] = 0u;
+        a.P.ctl[CTL_FIRST_CROSS] = NONE;
+    }
     const uint32_t c = a.ck_lo + blockIdx.x * 4u + (threadIdx.x >> 6);
     if (c >= a.ck_hi) return;
     const uint32_t cnt = a.L.cnt[c];
@@ -427,13 +456,32 @@ __global__ __launch_bounds__(256) void k_resolve(ResolveArgs a)
         if (set_find(P.dset, h, &v)) st = ST_MATCH;
         else v = 0;
     }
-    // 2048-byte comparisons against the cached segments, one wave-wide compare each
-    for (uint64_t m = ballot(st == ST_EQUAL); m; m &= m - 1) {
-        const int f = __ffsll((unsigned long long)m) - 1;
-        const uint32_t qf = readlane(q, f);
-        const uint64_t vf = readlane64(v, f);
-        const bool eq = wave_equal2048(base + qf - (XC_SEG - 1u), P.segs + vf * XC_SEG);
-        if ((int)l == f && !eq) st = ST_COLL;
+    // 2048-byte comparisons against the cached segments: up to 4 per pass, all loads in flight
+    for (uint64_t m = ballot(st == ST_EQUAL); m;) {
+        int f[4];
+        uint32_t x[4][8], y[4][8];
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            f[g] = m ? __ffsll((unsigned long long)m) - 1 : -1;
+            if (m) m &= m - 1;
+            if (f[g] >= 0) {
+                const uint32_t qf = readlane(q, f[g]);
+                const uint64_t vf = readlane64(v, f[g]);
+                load32_unaligned(base + qf - (XC_SEG - 1u) + 32u * l, x[g]);
+                const uint4 *sp = (const uint4 *)(P.segs + vf * XC_SEG + 32u * l);
+                const uint4 s0 = sp[0], s1 = sp[1];
+                y[g][0] = s0.x; y[g][1] = s0.y; y[g][2] = s0.z; y[g][3] = s0.w;
+                y[g][4] = s1.x; y[g][5] = s1.y; y[g][6] = s1.z; y[g][7] = s1.w;
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            if (f[g] < 0) continue;
+            uint32_t diff = 0;
+#pragma unroll
+            for (int k = 0; k < 8; k++) diff |= x[g][k] ^ y[g][k];
+            if (ballot(diff != 0u) && (int)l == f[g]) st = ST_COLL;
+        }
     }
     if (live) {
         const uint32_t i = c * EV_CAP + l;
@@ -721,15 +769,12 @@ __global__ __launch_bounds__(64) void k_declhash(DeclArgs a)
     }
 }
 
-// grid (buffers, 4): hash of every aligned 2048-byte block; blocks absent from the cache are
-// the predicted declarations (hit-free data declares exactly these, xcodec_encoder.cc:77-82)
-// and enter the declaration set before the scan.  A wave hashes 8 blocks with all loads in
-// flight together, then its lanes probe / insert the 8 hashes in parallel.
+// grid (buffers, 4): hash of every aligned 2048-byte block (a wave hashes 8 blocks with all
+// loads in flight together).  Depends on the input only, so it runs ahead on a side stream.
 constexpr uint32_t BLK_GROUP = 8;
 
 __global__ __launch_bounds__(64) void k_blockhash(DeclArgs a)
 {
-    if (aborted(a.P)) return;
     const PlanDev &P = a.P;
     const uint32_t b = a.j0 + blockIdx.x;
     if (b >= a.j1) return;
@@ -739,12 +784,28 @@ __global__ __launch_bounds__(64) void k_blockhash(DeclArgs a)
     for (uint32_t k0 = blockIdx.y * BLK_GROUP; k0 < nblk; k0 += gridDim.y * BLK_GROUP) {
         const uint32_t n = min(BLK_GROUP, nblk - k0);
         const uint64_t h = wave_block_hashes<BLK_GROUP>(base + (size_t)k0 * XC_SEG, n);
-        if (l < n) {
-            uint64_t v;
-            P.blk_h[bb + k0 + l] = h;
-            if (!set_find(P.cache, h, &v))
-                set_insert(P.dset, h, ((uint64_t)b << 32) | ((k0 + l) * XC_SEG + 2u * XC_SEG - 1u), true, nullptr,
-                           nullptr);
+        if (l < n) P.blk_h[bb + k0 + l] = h;
+    }
+}
+
+// One wave per buffer, one lane per aligned block: blocks absent from the cache are the
+// predicted declarations (hit-free data declares exactly these, xcodec_encoder.cc:77-82);
+// they enter the declaration set and the combined level-2 filter before the scan.
+__global__ __launch_bounds__(64) void k_blockpredict(DeclArgs a)
+{
+    if (aborted(a.P)) return;
+    const PlanDev &P = a.P;
+    const uint32_t b = a.j0 + blockIdx.x;
+    if (b >= a.j1) return;
+    const uint32_t nblk = P.buf_len[b] / XC_SEG, bb = P.blk_base[b];
+    for (uint32_t k = lane_id(); k < nblk; k += 64u) {
+        const uint64_t h = P.blk_h[bb + k];
+        uint64_t v;
+        if (!set_find(P.cache, h, &v) &&
+            set_insert(P.dset, h, ((uint64_t)b << 32) | (k * XC_SEG + 2u * XC_SEG - 1u), true, nullptr, nullptr)) {
+            const uint32_t g = l2_mix((uint32_t)h), gi = (g >> 14) * 2u;
+            atomicOr(&P.l2mix[gi], 1u << (g & 31u));
+            atomicOr(&P.l2mix[gi + 1u], 1u << ((g >> 5) & 31u));
         }
     }
 }
@@ -842,6 +903,21 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
     }
     __syncthreads();
     const uint32_t slot0 = P.buf_slot[b];
+    if (wave == 0) {
+        // XCodecMemoryCache::enter (xcodec_cache.h:182-188) of this buffer's declarations,
+        // one lane per EXTRACT token, into the slots k_alloc reserved
+        for (uint32_t t0 = 0; t0 < n; t0 += 64u) {
+            const uint32_t t = t0 + l;
+            if (t < n && P.tok_op[tb + t] == OP_EXTRACT) {
+                const uint32_t idx = slot0 + ord[t];
+                if (idx < P.seg_cap) {
+                    uint32_t s1, s2;
+                    set_insert(P.cache, P.tok_h[tb + t], idx, false, &s1, &s2);
+                    P.undo[idx] = make_uint2(s1, s2);
+                }
+            }
+        }
+    }
     for (uint32_t t = wave; t < n; t += EMIT_WAVES) {
         const uint32_t lb = P.tok_lb[tb + t], le = P.tok_le[tb + t], op = P.tok_op[tb + t];
         uint8_t *o = out + sz[t];
@@ -854,36 +930,9 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
             if (l == 0) { o[0] = (uint8_t)XC_MAGIC; o[1] = (uint8_t)OP_EXTRACT; }
             // the payload goes to the wire and into the slot k_alloc reserved
             const uint32_t idx = slot0 + ord[t];
-            if (idx < P.seg_cap) wave_copy2048_dual(o + 2, P.segs + (size_t)idx * XC_SEG, base + seg);
+            if (idx < P.seg_cap) wave_copy_payload(o + 2, P.segs + (size_t)idx * XC_SEG, base + seg);
             else wave_copy(o + 2, base + seg, XC_SEG);
         }
-    }
-}
-
-// XCodecMemoryCache::enter (xcodec_cache.h:182-188) of every declaration of buffers
-// [j0, j1): one lane per EXTRACT token, inserts in parallel.
-__global__ __launch_bounds__(64) void k_commit(EmitArgs a)
-{
-    if (aborted(a.P)) return;
-    const PlanDev &P = a.P;
-    const uint32_t b = a.j0 + blockIdx.x;
-    if (b >= a.j1) return;
-    const uint32_t tb = P.tok_base[b], n = min(P.tok_cnt[b], MAX_TOK);
-    const uint32_t l = lane_id();
-    uint32_t slot = P.buf_slot[b];
-    for (uint32_t t0 = 0; t0 < n; t0 += 64u) {
-        const uint32_t t = t0 + l;
-        const bool ext = t < n && P.tok_op[tb + t] == OP_EXTRACT;
-        const uint64_t m = ballot(ext);
-        if (ext) {
-            const uint32_t idx = slot + mbcnt(m);
-            if (idx < P.seg_cap) {
-                uint32_t s1, s2;
-                set_insert(P.cache, P.tok_h[tb + t], idx, false, &s1, &s2);
-                P.undo[idx] = make_uint2(s1, s2);
-            }
-        }
-        slot += (uint32_t)__popcll(m);
     }
 }
 
@@ -892,6 +941,21 @@ __global__ __launch_bounds__(64) void k_commit(EmitArgs a)
 __global__ __launch_bounds__(1024) void k_alloc(EmitArgs a)
 {
     if (aborted(a.P)) return;
+    if (a.gate_sb != NONE) {
+        // async pipeline gate: stop here (and every later launch) if sub-batch gate_sb needs
+        // the host: declaration growth, a cross-buffer conflict or an error
+        __shared__ uint32_t stop;
+        if (threadIdx.x == 0) {
+            const uint32_t *ctl = a.P.ctl;
+            stop = (ctl[CTL_GREW] || ctl[CTL_FIRST_CROSS] < a.j1 || ctl[CTL_ERROR]) ? 1u : 0u;
+            if (stop) {
+                a.P.ctl[CTL_ABORT_SB] = a.gate_sb;
+                a.P.ctl[CTL_ABORT] = 1u;
+            }
+        }
+        __syncthreads();
+        if (stop) return;
+    }
     __shared__ uint32_t wsum[16][2];
     __shared__ uint32_t carry[2];
     const PlanDev &P = a.P;
@@ -988,15 +1052,24 @@ __global__ __launch_bounds__(64) void k_window_hashes(const uint8_t *in, uint32_
     }
 }
 
-// Async sub-batch pipeline gate: after sub-batch sb's first walk round, stop the enqueued
-// pipeline if the host has to step in (declaration growth, a cross-buffer conflict, an error).
-__global__ void k_gate(PlanDev P, uint32_t sb, uint32_t s1)
+// Clear a declaration set (all of its tables) and seed the combined level-2 filter with the
+// cache's: one launch instead of a memset per table.
+__global__ void k_clear_set(DevSet s, uint32_t n_lo, uint32_t n_full, uint4 *l2mix, const uint4 *cache_l2)
 {
-    if (threadIdx.x != 0 || P.ctl[CTL_ABORT]) return;
-    if (P.ctl[CTL_GREW] || P.ctl[CTL_FIRST_CROSS] < s1 || P.ctl[CTL_ERROR]) {
-        P.ctl[CTL_ABORT_SB] = sb;
-        P.ctl[CTL_ABORT] = 1u;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint4 z = make_uint4(0, 0, 0, 0), ones = make_uint4(~0u, ~0u, ~0u, ~0u);
+    for (uint32_t i = i0; i < XC_FILT_WORDS / 4; i += stride) ((uint4 *)s.filt)[i] = z;
+    for (uint32_t i = i0; i < XC_L2_WORDS / 2; i += stride) {
+        ((uint4 *)s.l2)[i] = z;
+        l2mix[i] = cache_l2[i];
     }
+    for (uint32_t i = i0; i < n_lo / 4; i += stride) ((uint4 *)s.lo_keys)[i] = z;
+    for (uint32_t i = i0; i < n_full / 2; i += stride) {
+        ((uint4 *)s.keys)[i] = ones;
+        ((uint4 *)s.vals)[i] = ones;
+    }
+    if (i0 == 0) *s.lo_zero = 0u;
 }
 
 __global__ void k_or_words(uint4 *dst, const uint4 *a, const uint4 *b, uint32_t n)

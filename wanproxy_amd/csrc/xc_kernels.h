@@ -80,6 +80,7 @@ struct PlanDev {
     const uint64_t *out_off;
     uint64_t *out_len;
     uint32_t *ctl;
+    uint32_t *l2mix;  // level-2 filter of cache | predicted declarations (combined scan)
 };
 
 // kernel argument blocks (shared by xc_encode.hip and xc_runtime.hip)
@@ -117,6 +118,7 @@ struct DeclArgs {
 struct EmitArgs {
     PlanDev P;
     uint32_t j0, j1;
+    uint32_t gate_sb;  // k_alloc: async-pipeline gate for sub-batch gate_sb (NONE: no gate)
 };
 
 template <int MODE> __global__ void k_scan(ScanArgs a);
@@ -124,11 +126,11 @@ __global__ void k_resolve(ResolveArgs a);
 __global__ void k_walk(WalkArgs a);
 __global__ void k_declhash(DeclArgs a);
 __global__ void k_blockhash(DeclArgs a);
+__global__ void k_blockpredict(DeclArgs a);
 __global__ void k_or_words(uint4 *dst, const uint4 *a, const uint4 *b, uint32_t n);
 __global__ void k_emit(EmitArgs a);
 __global__ void k_alloc(EmitArgs a);
-__global__ void k_commit(EmitArgs a);
-__global__ void k_gate(PlanDev P, uint32_t sb, uint32_t s1);
+__global__ void k_clear_set(DevSet s, uint32_t n_lo, uint32_t n_full, uint4 *l2mix, const uint4 *cache_l2);
 __global__ void k_hash_segments(const uint8_t *segs, uint64_t n, uint64_t *out);
 __global__ void k_window_hashes(const uint8_t *in, uint32_t n, uint64_t *out);
 __global__ void k_undo(DevSet cache, const uint2 *undo, uint32_t from, uint32_t to);

@@ -425,6 +425,12 @@ struct xc_plan {
     std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev_live;
     xc_kernel_times ktimes{};
     std::vector<uint64_t> chunk_bytes;  // prefix of input bytes covered by chunks
+    // block hashing runs ahead on a side stream (it reads only the input), overlapping the
+    // scans; sub-batch k's prediction step waits for ev_hash[k]
+    hipStream_t hs = nullptr;
+    hipEvent_t ev_start = nullptr;
+    std::vector<hipEvent_t> ev_hash, ev_go;
+    uint32_t next_hash = 0;  // first sub-batch not yet enqueued for hashing in this run
 };
 
 static hipEvent_t ev_get(xc_plan *p)
@@ -443,17 +449,18 @@ struct KSpan {
     xc_plan *p;
     int k;
     hipEvent_t a = nullptr, b = nullptr;
-    KSpan(xc_plan *p_, int k_) : p(p_), k(k_)
+    hipStream_t st;
+    KSpan(xc_plan *p_, int k_, hipStream_t s_ = nullptr) : p(p_), k(k_), st(s_ ? s_ : p_->cache->ctx->stream)
     {
         if (!p->timing) return;
         a = ev_get(p);
         b = ev_get(p);
-        if (a) hipEventRecord(a, p->cache->ctx->stream);
+        if (a) hipEventRecord(a, st);
     }
     ~KSpan()
     {
         if (!a || !b) return;
-        hipEventRecord(b, p->cache->ctx->stream);
+        hipEventRecord(b, st);
         p->ev_live.push_back({k, {a, b}});
     }
 };
@@ -594,6 +601,13 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     HIPCHK(hipMalloc(&P.blk_h, std::max<uint64_t>(nblk, 1) * 8));
     HIPCHK(hipMalloc(&p->d_blk_base, nb1 * 4));
     HIPCHK(hipMalloc(&p->d_l2mix, (size_t)XC_L2_WORDS * 8));
+    P.l2mix = p->d_l2mix;
+    HIPCHK(hipStreamCreateWithFlags(&p->hs, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&p->ev_start, hipEventDisableTiming));
+    p->ev_hash.assign(p->sub.size(), nullptr);
+    p->ev_go.assign(p->sub.size(), nullptr);
+    for (auto &e : p->ev_hash) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (auto &e : p->ev_go) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (nbuf) HIPCHK(hipMemcpyAsync(p->d_blk_base, blk_base.data(), nbuf * 4, hipMemcpyHostToDevice, s));
     P.blk_base = p->d_blk_base;
     HIPCHK(hipMalloc(&P.buf_next, nb1 * 4));
@@ -639,6 +653,15 @@ extern "C" int xc_plan_destroy(xc_plan *p)
     hipFree(p->P.ctl);
     for (auto &x : p->ev_live) { hipEventDestroy(x.second.first); hipEventDestroy(x.second.second); }
     for (auto e : p->ev_pool) hipEventDestroy(e);
+    if (p->hs) {
+        hipStreamSynchronize(p->hs);
+        hipStreamDestroy(p->hs);
+    }
+    if (p->ev_start) hipEventDestroy(p->ev_start);
+    for (auto e : p->ev_hash)
+        if (e) hipEventDestroy(e);
+    for (auto e : p->ev_go)
+        if (e) hipEventDestroy(e);
     delete p;
     return XC_OK;
 }
@@ -694,10 +717,7 @@ static int launch_scan(xc_plan *p, const Layer &L, const DevSet &set, uint32_t c
     if (set2) {
         a.set2 = *set2;
         a.has2 = 1;
-        hipLaunchKernelGGL(k_or_words, dim3(512), dim3(256), 0, ctx->stream, (uint4 *)p->d_l2mix,
-                           (const uint4 *)set.l2, (const uint4 *)set2->l2, XC_L2_WORDS / 2);
-        HIPCHK(hipGetLastError());
-        a.l2 = (const uint2 *)p->d_l2mix;
+        a.l2 = (const uint2 *)p->d_l2mix;  // cache | set2, built by k_clear_set + k_blockhash
     }
     KSpan span(p, XC_K_SCAN);
     if (p->timing) p->ktimes.scan_bytes += p->chunk_bytes[ck_hi] - p->chunk_bytes[ck_lo];
@@ -710,10 +730,10 @@ static int launch_scan(xc_plan *p, const Layer &L, const DevSet &set, uint32_t c
 
 static int launch_resolve(xc_plan *p, const Layer &L, int dmode, uint32_t ck_lo, uint32_t ck_hi)
 {
-    if (ck_hi <= ck_lo) return XC_OK;
     ResolveArgs a{p->P, L, dmode, ck_lo, ck_hi};
     KSpan span(p, XC_K_RESOLVE);
-    hipLaunchKernelGGL(k_resolve, dim3((ck_hi - ck_lo + 3) / 4), dim3(256), 0, p->cache->ctx->stream, a);
+    hipLaunchKernelGGL(k_resolve, dim3(std::max<uint32_t>(1u, (ck_hi - ck_lo + 3) / 4)), dim3(256), 0,
+                       p->cache->ctx->stream, a);
     HIPCHK(hipGetLastError());
     return XC_OK;
 }
@@ -721,8 +741,7 @@ static int launch_resolve(xc_plan *p, const Layer &L, int dmode, uint32_t ck_lo,
 static int launch_walk_round(xc_plan *p, uint32_t j0, uint32_t j1, int use_d)
 {
     hipStream_t s = p->cache->ctx->stream;
-    HIPCHK(hipMemsetAsync(p->P.ctl + CTL_GREW, 0, 4, s));
-    HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(p->P.ctl + CTL_FIRST_CROSS), NONE, 1, s));
+    // (k_resolve, always launched just before, reset GREW / FIRST_CROSS)
     WalkArgs w{p->P, j0, j1, use_d};
     {
         KSpan span(p, XC_K_WALK);
@@ -739,34 +758,60 @@ static int launch_walk_round(xc_plan *p, uint32_t j0, uint32_t j1, int use_d)
     return XC_OK;
 }
 
-static int launch_emit(xc_plan *p, uint32_t j0, uint32_t jc)
+static int launch_emit(xc_plan *p, uint32_t j0, uint32_t jc, uint32_t gate_sb = NONE)
 {
     hipStream_t s = p->cache->ctx->stream;
-    EmitArgs e{p->P, j0, jc};
+    EmitArgs e{p->P, j0, jc, gate_sb};
     hipLaunchKernelGGL(k_alloc, dim3(1), dim3(1024), 0, s, e);
     HIPCHK(hipGetLastError());
     KSpan span(p, XC_K_EMIT);
     hipLaunchKernelGGL(k_emit, dim3(jc - j0), dim3(512), 0, s, e);
-    HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_commit, dim3(jc - j0), dim3(64), 0, s, e);
     HIPCHK(hipGetLastError());
     return XC_OK;
 }
 
 // Predicted declarations (aligned blocks absent from the cache), then one scan of every
 // position of buffers [j0, s1) against cache + predictions, resolve, first walk round.
-static int launch_first_round(xc_plan *p, uint32_t j0, uint32_t s1)
+// Hash sub-batch k's aligned blocks on the side stream once `after` (an event of the main
+// stream) has passed; ev_hash[k] marks completion.
+static int enqueue_block_hash(xc_plan *p, uint32_t k, hipEvent_t after)
+{
+    HIPCHK(hipStreamWaitEvent(p->hs, after, 0));
+    DeclArgs d{p->P, p->sub[k], p->sub[k + 1]};
+    {
+        KSpan span(p, XC_K_DECLHASH, p->hs);
+        hipLaunchKernelGGL(k_blockhash, dim3(p->sub[k + 1] - p->sub[k], 4), dim3(64), 0, p->hs, d);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipEventRecord(p->ev_hash[k], p->hs));
+    p->next_hash = k + 1;
+    return XC_OK;
+}
+
+static int launch_first_round(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t s1)
 {
     hipStream_t s = p->cache->ctx->stream;
     int rc;
     const uint32_t ck_lo = p->chunk0[j0], ck_hi = p->chunk0[s1];
     p->stats.outer_rounds++;
-    if ((rc = p->dset.clear(s))) return rc;
+    if (p->next_hash <= sb) {  // first sub-batch of the run: nothing to overlap with
+        HIPCHK(hipEventRecord(p->ev_start, s));
+        if ((rc = enqueue_block_hash(p, sb, p->ev_start))) return rc;
+    }
+    HIPCHK(hipStreamWaitEvent(s, p->ev_hash[sb], 0));
+    hipLaunchKernelGGL(k_clear_set, dim3(1024), dim3(256), 0, s, p->P.dset, p->dset.n_lo, p->dset.n_full,
+                       (uint4 *)p->d_l2mix, (const uint4 *)p->P.cache.l2);
+    HIPCHK(hipGetLastError());
     {
         DeclArgs d{p->P, j0, s1};
         KSpan span(p, XC_K_DECLHASH);
-        hipLaunchKernelGGL(k_blockhash, dim3(s1 - j0, 4), dim3(64), 0, s, d);
+        hipLaunchKernelGGL(k_blockpredict, dim3(s1 - j0), dim3(64), 0, s, d);
         HIPCHK(hipGetLastError());
+    }
+    // the next sub-batch's block hashes run beside this scan (memory-bound beside LDS/L2-bound)
+    if (p->next_hash == sb + 1 && sb + 2 < p->sub.size()) {
+        HIPCHK(hipEventRecord(p->ev_go[sb], s));
+        if ((rc = enqueue_block_hash(p, sb + 1, p->ev_go[sb]))) return rc;
     }
     if ((rc = launch_scan(p, p->P.S, p->P.cache, ck_lo, ck_hi, &p->P.dset))) return rc;
     if ((rc = launch_resolve(p, p->P.S, 2, ck_lo, ck_hi))) return rc;
@@ -779,10 +824,8 @@ static int encode_sub_async(xc_plan *p, uint32_t sb)
     const uint32_t j0 = p->sub[sb], s1 = p->sub[sb + 1];
     int rc;
     p->stats.sub_batches++;
-    if ((rc = launch_first_round(p, j0, s1))) return rc;
-    hipLaunchKernelGGL(k_gate, dim3(1), dim3(64), 0, p->cache->ctx->stream, p->P, sb, s1);
-    HIPCHK(hipGetLastError());
-    return launch_emit(p, j0, s1);
+    if ((rc = launch_first_round(p, sb, j0, s1))) return rc;
+    return launch_emit(p, j0, s1, sb);
 }
 
 // Sub-batch sb step by step: declaration-growth rounds until D is closed, then emit up to the
@@ -795,7 +838,7 @@ static int encode_sub_sync(xc_plan *p, uint32_t sb, uint32_t *ctl)
     int rc;
     while (j0 < s1) {
         const uint32_t ck_lo = p->chunk0[j0], ck_hi = p->chunk0[s1];
-        if ((rc = launch_first_round(p, j0, s1))) return rc;
+        if ((rc = launch_first_round(p, sb, j0, s1))) return rc;
         if ((rc = read_ctl(p, ctl))) return rc;
         uint32_t rounds = 0;
         while (!ctl[CTL_ERROR] && ctl[CTL_GREW]) {
@@ -828,6 +871,7 @@ extern "C" int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, ui
     p->stats = xc_run_stats{};
     HIPCHK(hipMemsetAsync(p->P.ctl, 0, CTL_WORDS * 4, s));
     uint32_t ctl[CTL_WORDS];
+    p->next_hash = 0;
     const size_t nsub = p->sub.size() - 1;
     size_t si = 0;
     while (si < nsub) {
