@@ -221,8 +221,7 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
     uint4 dsc = a.P.chunk_desc[c];
     uint32_t pw[8], w[8];
     first_blocks(desc_base(a, dsc), uniform(dsc.x), l, pw, w);
-    uint4 dn = make_uint4(0, 0, 0, 0);
-    if (c + 1u < c_end) dn = a.P.chunk_desc[c + 1u];
+    uint4 dn = a.P.chunk_desc[min(c + 1u, c_end - 1u)];
 
     Pending pd;
     pd.n = 0;
@@ -231,23 +230,20 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
     bool prev_dense = false;
 
     for (;;) {
-        const uint32_t c0 = uniform(dsc.x), c1 = uniform(dsc.y);
+        const uint32_t c0 = uniform(dsc.x), c1 = uniform(dsc.y) & 0x7FFFFFFFu;
         const uint8_t *base = desc_base(a, dsc);
         const bool has_next = c + 1u < c_end;
         // the next chunk continues this one (same buffer, starts at c1): keep streaming
-        const bool contig = has_next && uniform(dn.x) == c1 && uniform(dn.z) == uniform(dsc.z) &&
-                            uniform(dn.w) == uniform(dsc.w);
+        const bool contig = has_next && (uniform(dsc.y) >> 31) != 0u;
         uint32_t ev_n = 0, qn = 0;
         bool dense = false;
 
         BlockSums ps = block_sums(pw, l);
         uint32_t s = c0;
         if (c0 == 0) {
-            // window ending at 2047 = the whole first block (every chunk has len >= 2048)
-            const uint32_t lo = (ps.totA << 20) + (XC_SEG * ps.totA - ps.totC);
-            const uint32_t t = filt_test(filt, lo);
-            if (t && l == 0) queue[0] = make_uint2(XC_SEG - 1u, lo);
-            qn = t;
+            // window ending at 2047 = the whole first block (every chunk has len >= 2048); an
+            // aligned window is always an event: its block is cached or a predicted declaration
+            scan_record(a, c, c0, l == 0u, XC_SEG - 1u, ev_n, dense);
             s = XC_SEG;
         }
 
@@ -255,7 +251,9 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
             // prefetch: the next block of this chunk, or the next chunk's first two blocks
             uint32_t wn[8];
             const bool last = s + XC_SEG >= c1 && !contig;
-            if (!last) load32_aligned(base + s + XC_SEG + 32u * l, wn);
+            // unconditional (re-reads this block when there is no next one): a conditional load
+            // makes the compiler drain every outstanding load before the block sums below
+            load32_aligned(base + (last ? s : s + XC_SEG) + 32u * l, wn);
             const BlockSums cs = block_sums(w, l);
             // window ending just before this lane's first position q = s + 32 l:
             // out-chunks of lanes >= l (previous block) + in-chunks of lanes < l.
@@ -286,6 +284,7 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
                     }
                 }
                 hit &= vmask >> (16 * half);
+                if (half == 1 && l == 63u) hit &= 0x7FFFu;  // aligned window: recorded below
                 if (MODE == 3) { sink = sink * 31u + hit; hit = 0; }
                 const uint32_t cnt = (uint32_t)__popc(hit);
                 const uint32_t incl = wave_incl_scan(cnt);
@@ -318,6 +317,9 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
                     }
                 }
             }
+            // the aligned window ending at s + 2047 is an event without a probe: k_blockpredict
+            // put its block in the declaration set unless the cache holds it (k_resolve decides)
+            scan_record(a, c, c0, l == 63u && s + XC_SEG - 1u < c1, s + XC_SEG - 1u, ev_n, dense);
             // iteration boundary: finish the previous probe batch, start this one
             if (pd.n) {
                 if (pd.c == c) {
@@ -365,7 +367,7 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
         c += 1u;
         dsc = dn;
         if (!contig) first_blocks(desc_base(a, dsc), uniform(dsc.x), l, pw, w);
-        if (c + 1u < c_end) dn = a.P.chunk_desc[c + 1u];
+        dn = a.P.chunk_desc[min(c + 1u, c_end - 1u)];
     }
     if (MODE >= 2 && sink == 0x7FFFFFF0u - a.ck_hi) a.P.ctl[CTL_ERROR] = sink;  // never true; keeps ablations honest
     if (pd.n) {

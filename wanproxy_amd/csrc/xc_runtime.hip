@@ -510,7 +510,9 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
         if (n >= XC_SEG)
             for (uint32_t s = 0; s < n; s += CHUNK_LEN) {
                 chunks.push_back(make_uint2((uint32_t)i, s));
-                descs.push_back(make_uint4(s, (uint32_t)std::min<uint64_t>(s + CHUNK_LEN, n),
+                // bit 31 of the end position: the next chunk continues this buffer
+                const uint32_t more = s + CHUNK_LEN < n ? 0x80000000u : 0u;
+                descs.push_back(make_uint4(s, (uint32_t)std::min<uint64_t>(s + CHUNK_LEN, n) | more,
                                            (uint32_t)p->in_off[i], (uint32_t)(p->in_off[i] >> 32)));
             }
         tok_base[i] = (uint32_t)toks;
