@@ -213,29 +213,54 @@ __device__ __forceinline__ uint4 load16_unaligned(const uint8_t *p)
 }
 
 // A 2048-byte payload from src (any alignment) to the wire at out (any alignment) and to a
-// cache slot at seg (16-byte aligned).  Every store is a whole 16-byte aligned store except
-// the wire copy's head and tail bytes; the second read of src hits the cache.
-__device__ __forceinline__ void wave_copy_payload(uint8_t *out, uint8_t *seg, const uint8_t *src)
+// cache slot (16-byte aligned), split into a load half and a store half so that a wave can
+// have several payloads in flight.  Every store is a whole 16-byte aligned store except the
+// wire copy's head and tail bytes; the wire-aligned reads of src hit the cache.
+struct PayloadRegs {
+    uint4 a0, a1;  // slot-aligned chunks: src + 16 l, src + 1024 + 16 l
+    uint4 b0, b1;  // wire-aligned chunks
+    uint32_t hb, tb;
+};
+
+__device__ __forceinline__ void payload_load(const uint8_t *src, const uint8_t *out, PayloadRegs &r)
 {
     const uint32_t l = lane_id();
     const uint32_t head = (uint32_t)((16u - ((uintptr_t)out & 15u)) & 15u);
     const uint32_t nbody = (XC_SEG - head) >> 4;
-    const uint4 a0 = load16_unaligned(src + 16u * l), a1 = load16_unaligned(src + 1024u + 16u * l);
-    uint4 b0 = a0, b1 = a1;
+    r.a0 = load16_unaligned(src + 16u * l);
+    r.a1 = load16_unaligned(src + 1024u + 16u * l);
+    r.b0 = r.a0;
+    r.b1 = r.a1;
     if (head) {
-        if (l < nbody) b0 = load16_unaligned(src + head + 16u * l);
-        if (l + 64u < nbody) b1 = load16_unaligned(src + head + 1024u + 16u * l);
+        if (l < nbody) r.b0 = load16_unaligned(src + head + 16u * l);
+        if (l + 64u < nbody) r.b1 = load16_unaligned(src + head + 1024u + 16u * l);
     }
-    uint8_t h = 0, t = 0;
     const uint32_t t0 = head + 16u * nbody;
-    if (l < head) h = src[l];
-    if (t0 + l < XC_SEG) t = src[t0 + l];
-    ((uint4 *)seg)[l] = a0;
-    ((uint4 *)seg)[l + 64u] = a1;
-    if (l < nbody) *(uint4 *)(out + head + 16u * l) = b0;
-    if (l + 64u < nbody) *(uint4 *)(out + head + 1024u + 16u * l) = b1;
-    if (l < head) out[l] = h;
-    if (t0 + l < XC_SEG) out[t0 + l] = t;
+    r.hb = l < head ? src[l] : 0u;
+    r.tb = t0 + l < XC_SEG ? src[t0 + l] : 0u;
+}
+
+__device__ __forceinline__ void payload_store(uint8_t *out, uint8_t *seg, const PayloadRegs &r)
+{
+    const uint32_t l = lane_id();
+    const uint32_t head = (uint32_t)((16u - ((uintptr_t)out & 15u)) & 15u);
+    const uint32_t nbody = (XC_SEG - head) >> 4;
+    const uint32_t t0 = head + 16u * nbody;
+    if (seg) {
+        ((uint4 *)seg)[l] = r.a0;
+        ((uint4 *)seg)[l + 64u] = r.a1;
+    }
+    if (l < nbody) *(uint4 *)(out + head + 16u * l) = r.b0;
+    if (l + 64u < nbody) *(uint4 *)(out + head + 1024u + 16u * l) = r.b1;
+    if (l < head) out[l] = (uint8_t)r.hb;
+    if (t0 + l < XC_SEG) out[t0 + l] = (uint8_t)r.tb;
+}
+
+__device__ __forceinline__ void wave_copy_payload(uint8_t *out, uint8_t *seg, const uint8_t *src)
+{
+    PayloadRegs r;
+    payload_load(src, out, r);
+    payload_store(out, seg, r);
 }
 
 // ---- membership sets -------------------------------------------------------------

@@ -174,14 +174,15 @@ __device__ __forceinline__ void load32_aligned(const uint8_t *p, uint32_t w[8])
     w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
 }
 
-// The two blocks a chunk starts from: pw = the 2048 bytes before c0 (block 0 when c0 == 0)
-// and w = the block at c0 (block 1 when c0 == 0).
+// The blocks a chunk starts from: pw = the 2048 bytes before its first iteration's block
+// (block 0 when c0 == 0), w = that block, wn = the one after (prefetch ring, 2 deep).
 __device__ __forceinline__ void first_blocks(const uint8_t *base, uint32_t c0, uint32_t l, uint32_t pw[8],
-                                             uint32_t w[8])
+                                             uint32_t w[8], uint32_t wn[8])
 {
     const uint32_t s = c0 == 0 ? XC_SEG : c0;
     load32_aligned(base + s - XC_SEG + 32u * l, pw);
     load32_aligned(base + s + 32u * l, w);
+    load32_aligned(base + s + XC_SEG + 32u * l, wn);  // may lie past the buffer: arena slack
 }
 
 __device__ __forceinline__ const uint8_t *desc_base(const ScanArgs &a, const uint4 &d)
@@ -219,8 +220,8 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
 
     // chunk descriptors: {c0, c1, arena offset lo, hi}; the next one is always in flight
     uint4 dsc = a.P.chunk_desc[c];
-    uint32_t pw[8], w[8];
-    first_blocks(desc_base(a, dsc), uniform(dsc.x), l, pw, w);
+    uint32_t pw[8], w[8], wn[8];
+    first_blocks(desc_base(a, dsc), uniform(dsc.x), l, pw, w, wn);
     uint4 dn = a.P.chunk_desc[min(c + 1u, c_end - 1u)];
 
     Pending pd;
@@ -230,7 +231,7 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
     bool prev_dense = false;
 
     for (;;) {
-        const uint32_t c0 = uniform(dsc.x), c1 = uniform(dsc.y) & 0x7FFFFFFFu;
+        const uint32_t c0 = uniform(dsc.x), c1 = uniform(dsc.y) & 0x3FFFFFFFu;
         const uint8_t *base = desc_base(a, dsc);
         const bool has_next = c + 1u < c_end;
         // the next chunk continues this one (same buffer, starts at c1): keep streaming
@@ -247,13 +248,14 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
             s = XC_SEG;
         }
 
+        const bool next_long = (uniform(dsc.y) >> 30 & 1u) != 0u;  // next chunk passes c1 + 2048
         for (; s < c1; s += XC_SEG) {
-            // prefetch: the next block of this chunk, or the next chunk's first two blocks
-            uint32_t wn[8];
-            const bool last = s + XC_SEG >= c1 && !contig;
-            // unconditional (re-reads this block when there is no next one): a conditional load
-            // makes the compiler drain every outstanding load before the block sums below
-            load32_aligned(base + (last ? s : s + XC_SEG) + 32u * l, wn);
+            // prefetch ring: w = block s (ready), wn = block s+2048 (in flight), wn2 = block
+            // s+4096 issued now when the stream reaches it.  Unconditional (re-reads block s
+            // otherwise): a conditional load makes the compiler drain every outstanding load.
+            uint32_t wn2[8];
+            const bool need2 = s + 2u * XC_SEG < c1 || (contig && (s + 2u * XC_SEG == c1 || next_long));
+            load32_aligned(base + (need2 ? s + 2u * XC_SEG : s) + 32u * l, wn2);
             const BlockSums cs = block_sums(w, l);
             // window ending just before this lane's first position q = s + 32 l:
             // out-chunks of lanes >= l (previous block) + in-chunks of lanes < l.
@@ -335,11 +337,9 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
                 pend_issue(a, pd, queue, qn, c, c0);
                 qn = 0;
             }
-            if (!last) {
 #pragma unroll
-                for (int d = 0; d < 8; d++) { pw[d] = w[d]; w[d] = wn[d]; }
-                ps = cs;
-            }
+            for (int d = 0; d < 8; d++) { pw[d] = w[d]; w[d] = wn[d]; wn[d] = wn2[d]; }
+            ps = cs;
         }
         if (qn) {  // chunk whose only position is 2047: no iteration ran
             if (pd.n) {
@@ -366,7 +366,7 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
         if (!has_next) break;
         c += 1u;
         dsc = dn;
-        if (!contig) first_blocks(desc_base(a, dsc), uniform(dsc.x), l, pw, w);
+        if (!contig) first_blocks(desc_base(a, dsc), uniform(dsc.x), l, pw, w, wn);
         dn = a.P.chunk_desc[min(c + 1u, c_end - 1u)];
     }
     if (MODE >= 2 && sink == 0x7FFFFFF0u - a.ck_hi) a.P.ctl[CTL_ERROR] = sink;  // never true; keeps ablations honest
@@ -905,7 +905,7 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
     }
     __syncthreads();
     const uint32_t slot0 = P.buf_slot[b];
-    if (wave == 0) {
+    if (wave == EMIT_WAVES - 1u) {  // the wave with the smallest token group (wave 0 did the prefix)
         // XCodecMemoryCache::enter (xcodec_cache.h:182-188) of this buffer's declarations,
         // one lane per EXTRACT token, into the slots k_alloc reserved
         for (uint32_t t0 = 0; t0 < n; t0 += 64u) {
@@ -920,20 +920,59 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
             }
         }
     }
-    for (uint32_t t = wave; t < n; t += EMIT_WAVES) {
-        const uint32_t lb = P.tok_lb[tb + t], le = P.tok_le[tb + t], op = P.tok_op[tb + t];
-        uint8_t *o = out + sz[t];
-        if (le > lb) o += write_escaped(o, base + lb, le - lb);
-        if (op == OP_REF) {
-            const uint64_t h = P.tok_h[tb + t];
-            if (l < 10) o[l] = l == 0 ? (uint8_t)XC_MAGIC : l == 1 ? (uint8_t)OP_REF : (uint8_t)(h >> (8 * (9 - l)));
-        } else if (op == OP_EXTRACT) {
-            const uint32_t seg = P.tok_seg[tb + t];
-            if (l == 0) { o[0] = (uint8_t)XC_MAGIC; o[1] = (uint8_t)OP_EXTRACT; }
-            // the payload goes to the wire and into the slot k_alloc reserved
-            const uint32_t idx = slot0 + ord[t];
-            if (idx < P.seg_cap) wave_copy_payload(o + 2, P.segs + (size_t)idx * XC_SEG, base + seg);
-            else wave_copy(o + 2, base + seg, XC_SEG);
+    // wire bytes: wave w takes a contiguous group of tokens, one per lane, so the group's
+    // metadata arrives in one round trip and two payloads are in flight at a time
+    const uint32_t G = (n + EMIT_WAVES - 1u) / EMIT_WAVES;
+    const uint32_t g_end = min(n, (wave + 1u) * G);
+    for (uint32_t g0 = wave * G; g0 < g_end; g0 += 64u) {
+        const uint32_t t = g0 + l;
+        const bool live = t < g_end;
+        uint32_t lb = 0, le = 0, op = OP_END, seg = 0, off = 0;
+        uint64_t h = 0;
+        if (live) {
+            lb = P.tok_lb[tb + t];
+            le = P.tok_le[tb + t];
+            op = P.tok_op[tb + t];
+            seg = P.tok_seg[tb + t];
+            h = P.tok_h[tb + t];
+            off = sz[t];
+        }
+        // literal runs, F1-escaped (wave-cooperative, one run at a time)
+        for (uint64_t m = ballot(live && le > lb); m; m &= m - 1) {
+            const int f = __ffsll((unsigned long long)m) - 1;
+            const uint32_t flb = readlane(lb, f);
+            const uint32_t len = write_escaped(out + readlane(off, f), base + flb, readlane(le, f) - flb);
+            if ((int)l == f) off += len;
+        }
+        uint8_t *o = out + off;
+        if (live && op == OP_REF) {
+            o[0] = (uint8_t)XC_MAGIC;
+            o[1] = (uint8_t)OP_REF;
+#pragma unroll
+            for (int k = 0; k < 8; k++) o[2 + k] = (uint8_t)(h >> (8 * (7 - k)));
+        } else if (live && op == OP_EXTRACT) {
+            o[0] = (uint8_t)XC_MAGIC;
+            o[1] = (uint8_t)OP_EXTRACT;
+        }
+        // payloads to the wire and into the slots k_alloc reserved, two at a time
+        for (uint64_t m = ballot(live && op == OP_EXTRACT); m;) {
+            const int f0 = __ffsll((unsigned long long)m) - 1;
+            m &= m - 1;
+            const int f1 = m ? __ffsll((unsigned long long)m) - 1 : -1;
+            if (m) m &= m - 1;
+            const uint32_t i0 = slot0 + ord[g0 + (uint32_t)f0];
+            uint8_t *d0 = out + readlane(off, f0) + 2u;
+            PayloadRegs r0, r1;
+            payload_load(base + readlane(seg, f0), d0, r0);
+            uint8_t *d1 = nullptr;
+            uint32_t i1 = 0;
+            if (f1 >= 0) {
+                i1 = slot0 + ord[g0 + (uint32_t)f1];
+                d1 = out + readlane(off, f1) + 2u;
+                payload_load(base + readlane(seg, f1), d1, r1);
+            }
+            payload_store(d0, i0 < P.seg_cap ? P.segs + (size_t)i0 * XC_SEG : nullptr, r0);
+            if (f1 >= 0) payload_store(d1, i1 < P.seg_cap ? P.segs + (size_t)i1 * XC_SEG : nullptr, r1);
         }
     }
 }

@@ -56,7 +56,7 @@ struct PlanDev {
     const uint32_t *buf_len;
     uint32_t nb;
     const uint2 *chunks;       // (buffer, first position) per chunk
-    const uint4 *chunk_desc;   // (first position, end position | more<<31, arena offset lo, hi) per chunk
+    const uint4 *chunk_desc;   // (first position, end position | more<<31 | more2<<30, arena offset lo, hi)
     const uint32_t *buf_chunk0;  // [nb+1]
     uint32_t chunk_len;
     Layer S, D;

@@ -510,8 +510,10 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
         if (n >= XC_SEG)
             for (uint32_t s = 0; s < n; s += CHUNK_LEN) {
                 chunks.push_back(make_uint2((uint32_t)i, s));
-                // bit 31 of the end position: the next chunk continues this buffer
-                const uint32_t more = s + CHUNK_LEN < n ? 0x80000000u : 0u;
+                // bit 31 of the end position: the next chunk continues this buffer; bit 30: and
+                // it reaches past its first block (the scan's 2-deep prefetch ring needs to know)
+                const uint32_t more = (s + CHUNK_LEN < n ? 0x80000000u : 0u) |
+                                      (s + CHUNK_LEN + XC_SEG < n ? 0x40000000u : 0u);
                 descs.push_back(make_uint4(s, (uint32_t)std::min<uint64_t>(s + CHUNK_LEN, n) | more,
                                            (uint32_t)p->in_off[i], (uint32_t)(p->in_off[i] >> 32)));
             }
@@ -522,7 +524,7 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     }
     chunk0[nbuf] = (uint32_t)chunks.size();
     if (toks > 0xFFFFFFF0ull) return fail(XC_EINVAL, "batch too large");
-    p->in_bytes = io + 4096;
+    p->in_bytes = io + 8192;  // slack: the scan prefetches up to two blocks past a buffer
     p->out_bytes = oo + 256;
     p->nchunks = (uint32_t)chunks.size();
     p->chunk0 = chunk0;
