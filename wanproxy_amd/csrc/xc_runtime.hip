@@ -372,8 +372,16 @@ extern "C" int xc_window_hashes(xc_ctx *ctx, const uint8_t *d_in, uint64_t n, ui
 
 // ------------------------------------------------------------------ plan ----------
 static const uint32_t CHUNK_LEN = 16384;
-static const uint64_t SUB_BYTES = 256ull << 20;  // sub-batch: bound on input bytes
-static const uint32_t SUB_BUFS = 8192;           // sub-batch: bound on buffers
+static const uint64_t SUB_BYTES_DEFAULT = 512ull << 20;  // sub-batch: bound on input bytes (tuned on cfg5)
+static const uint32_t SUB_BUFS = 32768;                  // sub-batch: bound on buffers
+
+// XC_SUB_MB overrides the sub-batch byte bound (tuning experiments).
+static uint64_t sub_bytes()
+{
+    const char *e = getenv("XC_SUB_MB");
+    const long v = e ? atol(e) : 0;
+    return v > 0 ? (uint64_t)v << 20 : SUB_BYTES_DEFAULT;
+}
 static const uint32_t MAX_ROUNDS = 64;
 
 struct HostLayer {
@@ -540,8 +548,9 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
         uint64_t bytes = 0;
         uint32_t cnt = 0;
         uint64_t decl = 0, maxdecl = 0;
+        const uint64_t sub_max = sub_bytes();
         for (uint32_t i = 0; i < nbuf; i++) {
-            if (cnt && (bytes + lengths[i] > SUB_BYTES || cnt >= SUB_BUFS)) {
+            if (cnt && (bytes + lengths[i] > sub_max || cnt >= SUB_BUFS)) {
                 p->sub.push_back(i);
                 maxdecl = std::max(maxdecl, decl);
                 bytes = 0;
