@@ -95,14 +95,16 @@ int xc_encode_batch_host(xc_cache *c, const uint8_t *in, const uint64_t *in_off,
 /* Enqueue xc_cache_restore() on the context stream without blocking the host. */
 int xc_cache_restore_async(xc_cache *c);
 
-/* Per-kernel device time of the plan's runs, from HIP events recorded on the context
- * stream around every launch while timing is enabled (kernel ids: XC_K_*). */
+/* Per-kernel device time of the plan's runs, from HIP events recorded on the stream of every
+ * launch while timing is enabled (kernel ids: XC_K_*).  XC_K_BLOCKHASH runs on a side stream,
+ * concurrently with the scans, so its time overlaps theirs. */
 #define XC_K_SCAN 0
 #define XC_K_RESOLVE 1
 #define XC_K_WALK 2
-#define XC_K_DECLHASH 3
+#define XC_K_DECLHASH 3   /* declaration prediction (k_blockpredict) and unknown declarations */
 #define XC_K_EMIT 4
-#define XC_K_COUNT 5
+#define XC_K_BLOCKHASH 5
+#define XC_K_COUNT 6
 typedef struct {
     double ms[XC_K_COUNT];        /* summed device time */
     uint64_t launches[XC_K_COUNT];

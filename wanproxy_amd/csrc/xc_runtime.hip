@@ -792,7 +792,7 @@ static int enqueue_block_hash(xc_plan *p, uint32_t k, hipEvent_t after)
     HIPCHK(hipStreamWaitEvent(p->hs, after, 0));
     DeclArgs d{p->P, p->sub[k], p->sub[k + 1]};
     {
-        KSpan span(p, XC_K_DECLHASH, p->hs);
+        KSpan span(p, XC_K_BLOCKHASH, p->hs);
         hipLaunchKernelGGL(k_blockhash, dim3(p->sub[k + 1] - p->sub[k], 4), dim3(64), 0, p->hs, d);
         HIPCHK(hipGetLastError());
     }

@@ -32,7 +32,7 @@ SYMBOLS = [
     "xc_plan_kernel_times",
 ]
 
-KERNELS = ["scan", "resolve", "walk", "declhash", "emit"]
+KERNELS = ["scan", "resolve", "walk", "declhash", "emit", "blockhash"]
 
 
 class XCodecError(RuntimeError):
@@ -40,7 +40,8 @@ class XCodecError(RuntimeError):
 
 
 class KernelTimes(C.Structure):
-    _fields_ = [("ms", C.c_double * 5), ("launches", C.c_uint64 * 5), ("scan_bytes", C.c_uint64)]
+    _fields_ = [("ms", C.c_double * len(KERNELS)), ("launches", C.c_uint64 * len(KERNELS)),
+                ("scan_bytes", C.c_uint64)]
 
 
 class RunStats(C.Structure):
