@@ -56,7 +56,10 @@ def main():
     import torch
     import torch.distributed as dist
 
-    torch.cuda.set_device(local_rank)
+    # one process per GPU; on a box with fewer GPUs than ranks (rehearsal only) ranks share them
+    ndev = torch.cuda.device_count()
+    dev = local_rank if local_rank < ndev else local_rank % max(ndev, 1)
+    torch.cuda.set_device(dev)
     if world > 1:
         # barrier and max-reduction of the step time only: the path shards with no collective
         dist.init_process_group("gloo")
@@ -64,7 +67,7 @@ def main():
     import wanproxy_amd as w
     from wanproxy_amd import workloads as W
 
-    ctx = w.Context(local_rank)
+    ctx = w.Context(dev)
     shard = W.repeat_shard(args.total, 0x5555, rank, world)  # (n_local, 65536)
     n_local = shard.shape[0]
     pool = W.pool()

@@ -211,3 +211,34 @@ def test_device_resident_plan_and_restore(gpu_ctx, oracle_mod):
             assert out[o:o + int(lens[i])].tobytes() == want[i], (it, i)
     st = plan.stats()
     assert st.n_extract + st.n_ref > 0
+
+
+def test_many_subbatches_async_pipeline(gpu_ctx, oracle_mod, monkeypatch):
+    """1 MiB sub-batches: the asynchronous pipeline runs ~10 sub-batches back to back, and the
+    gate stops it at every sub-batch that needs the host (a buffer whose lookups hit an earlier
+    buffer's new declaration in the same sub-batch, self-referencing char runs, collisions); the
+    host then redoes that sub-batch step by step and restarts the pass after it."""
+    monkeypatch.setenv("XC_SUB_MB", "1")
+    x, y = _collision_pair(7)
+    a = W.gen(51, 65536)
+    pool = W.pool(64)
+    bufs = []
+    for k in range(40):
+        kind = k % 8
+        if kind == 0:
+            bufs.append(W.gen(300 + k, 60000 + 1111 * k))
+        elif kind == 1:
+            bufs.append(np.concatenate([W.gen(400 + k, 999), a[k * 100:k * 100 + 30000]]))
+        elif kind == 2:
+            bufs.append(np.full(50000 + k, k & 0xFF, np.uint8))
+        elif kind == 3:
+            bufs.append(np.concatenate([y, W.gen(500 + k, 3000), x]))
+        elif kind == 4:
+            bufs.append(pool[(k % 16) * 65536:(k % 16) * 65536 + 65536].copy())
+        elif kind == 5:
+            bufs.append(bufs[-4][5:].copy())  # shifted copy of a recent buffer
+        elif kind == 6:
+            bufs.append(_esc(40000, k))
+        else:
+            bufs.append(a.copy())
+    _check(gpu_ctx, oracle_mod, bufs, warm=[[pool[i:i + 65536] for i in range(0, 8 * 65536, 65536)]])
