@@ -28,6 +28,6 @@ torch.cuda.synchronize()
 lib = w.load_library()
 lib.xc__scan_ablation.restype = C.c_double
 lib.xc__scan_ablation.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int]
-for mode, name in [(2, "loads+block sums"), (1, "hash, no filter"), (3, "hash+filter, no queue"), (0, "full")]:
+for mode, name in [(2, "loads+block sums"), (1, "hash, no filter"), (3, "hash+filter, no queue"), (4, "queue appends only"), (5, "L2 filter, no exact"), (0, "full")]:
     us = lib.xc__scan_ablation(plan.h, d_in.data_ptr(), mode, 20)
     print(f"mode {mode} {name:18s} {us:8.1f} us  {n * W.BUF / us / 1e3:7.1f} GB/s")

@@ -267,10 +267,11 @@ __device__ __forceinline__ void wave_copy_payload(uint8_t *out, uint8_t *seg, co
 // A set of 64-bit hashes: level-1 bitmap (LDS-loaded by the scan), exact lo32 set,
 // full-key table with a 64-bit value.  Used for the cache (value = segment index)
 // and for a batch's declarations (value = buffer<<32 | declaration position, min-wins).
-// Level-1 filter: a blocked k=2 Bloom filter of 32768 32-bit words (128 KB, one scan
-// workgroup's LDS image).  lo32 (the hash's bytes_hash half) picks word lo>>17; the key sets
+// Level-1 filter: a blocked k=2 Bloom filter of 36864 32-bit words (144 KB: with the scan's
+// 16 KB of positive queues it fills a CU's 160 KB of LDS).  lo32 (the hash's bytes_hash half)
+// picks word floor(lo[31:8] * 36864 / 2^24) (one full-rate v_mul_hi_u32_u24); the key sets
 // bits lo[4:0] and lo[9:5] of that word.  One ds_read_b32 per tested position.
-#define XC_FILT_WORDS 32768u  // in 32-bit words
+#define XC_FILT_WORDS 36864u  // in 32-bit words (a multiple of 4096)
 #define XC_EMPTY64 0xFFFFFFFFFFFFFFFFull           // H never has bits 32..35 set
 
 // Level-2 filter: a blocked k=2 Bloom filter of 2^18 64-bit words (2 MB, sized to stay in an
@@ -299,9 +300,13 @@ struct DevSet {
     uint64_t *vals;
 };
 
+__device__ __forceinline__ uint32_t filt_word(uint32_t lo)
+{
+    return (uint32_t)(((uint64_t)(lo >> 8) * (uint64_t)(XC_FILT_WORDS << 8)) >> 32);
+}
 __device__ __forceinline__ uint32_t filt_test(const uint32_t *f, uint32_t lo)
 {
-    const uint32_t w = f[lo >> 17];
+    const uint32_t w = f[filt_word(lo)];
     return (w >> (lo & 31u)) & (w >> ((lo >> 5) & 31u)) & 1u;
 }
 __device__ __forceinline__ uint32_t lo_slot(uint32_t lo, uint32_t mask) { return (lo * 0x9E3779B1u) >> 7 & mask; }
@@ -367,7 +372,7 @@ __device__ __forceinline__ int set_insert(const DevSet &s, uint64_t h, uint64_t 
                 j = (j + 1u) & s.lo_mask;
             }
         }
-        atomicOr(&s.filt[lo >> 17], (1u << (lo & 31u)) | (1u << ((lo >> 5) & 31u)));
+        atomicOr(&s.filt[filt_word(lo)], (1u << (lo & 31u)) | (1u << ((lo >> 5) & 31u)));
         const uint32_t g = l2_mix(lo), gi = (g >> 14) * 2u;
         atomicOr(&s.l2[gi], 1u << (g & 31u));
         atomicOr(&s.l2[gi + 1u], 1u << ((g >> 5) & 31u));

@@ -105,6 +105,7 @@ __device__ __forceinline__ void pend_issue(const ScanArgs &a, Pending &pd, const
     }
 }
 
+template <int MODE>
 __device__ __forceinline__ void pend_complete(const ScanArgs &a, Pending &pd, uint32_t &ev_n, bool &dense)
 {
 #pragma unroll
@@ -113,29 +114,26 @@ __device__ __forceinline__ void pend_complete(const ScanArgs &a, Pending &pd, ui
         const uint32_t i = lane_id() + 64u * s;
         bool match = false;
         if (i < pd.n && l2_test(pd.w[s], l2_mix(pd.lo[s]))) {
-            match = scan_has_lo(a, pd.lo[s]);
+            match = MODE == 5 ? pd.lo[s] == 0x12345u : scan_has_lo(a, pd.lo[s]);
         }
         scan_record(a, pd.c, pd.c0, match, pd.pos[s], ev_n, dense);
     }
     pd.n = 0;
 }
 
+template <int MODE>
 __device__ __forceinline__ void scan_flush(const ScanArgs &a, uint2 *queue, uint32_t &qn, uint32_t c, uint32_t c0,
                                            uint32_t &ev_n, bool &dense)
 {
-    for (uint32_t r = 0; r < qn; r += 64u) {
-        const uint32_t i = r + lane_id();
-        bool match = false;
-        uint32_t pos = 0;
-        if (i < qn) {
-            uint2 e = queue[i];
-            pos = e.x;
-            const uint32_t g = l2_mix(e.y);
-            if (l2_test(a.l2[g >> 14], g))
-                match = scan_has_lo(a, e.y);
-        }
-        scan_record(a, c, c0, match, pos, ev_n, dense);
+    if (MODE == 4) {  // ablation: queue appends only
+        qn = 0;
+        return;
     }
+    static_assert(Q_CAP == 128u, "Pending holds 2 x 64 entries");
+    // Q_CAP = 2 x 64: every entry's level-2 word is in flight before the first test
+    Pending f;
+    pend_issue(a, f, queue, qn, c, c0);
+    pend_complete<MODE>(a, f, ev_n, dense);
     qn = 0;
 }
 
@@ -200,6 +198,7 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
     uint2 *queue = queues[wave];
     const uint32_t l = lane_id();
 
+    static_assert(XC_FILT_WORDS % 4096u == 0u, "filter load loop");
     for (uint32_t i = threadIdx.x * 4u; i < XC_FILT_WORDS; i += 4096u) {
         uint4 f = *(const uint4 *)(a.set.filt + i);
         if (a.has2) {
@@ -281,7 +280,7 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
                         V += U + (uint32_t)__mul24((int)ob, -2048);
                         const uint32_t x = (U << 20) + V;
                         lo[d * 4 + k] = x;
-                        if (MODE == 0 || MODE == 3) hit |= filt_test(filt, x) << (d * 4 + k);
+                        if (MODE == 0 || MODE >= 3) hit |= filt_test(filt, x) << (d * 4 + k);
                         else hit |= (x == 0x12345678u) ? 1u << (d * 4 + k) : 0u;
                     }
                 }
@@ -291,19 +290,17 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
                 const uint32_t cnt = (uint32_t)__popc(hit);
                 const uint32_t incl = wave_incl_scan(cnt);
                 const uint32_t tot = readlane(incl, 63);
-                if (tot && qn + tot > Q_CAP) scan_flush(a, queue, qn, c, c0, ev_n, dense);
+                if (tot && qn + tot > Q_CAP) scan_flush<MODE>(a, queue, qn, c, c0, ev_n, dense);
                 if (tot && tot <= Q_CAP) {
                     // lane-parallel append: this lane's hits go to [qn + excl, qn + excl + cnt);
-                    // loop only over the offsets j where some lane hit
-                    const uint32_t slot = qn + incl - cnt;
-                    uint32_t m = readlane(wave_incl_or(hit), 63);
-#pragma unroll 1
-                    while (m) {
-                        const uint32_t j = (uint32_t)__builtin_ctz(m);
-                        m &= m - 1u;
-                        if ((hit >> j) & 1u)
-                            queue[slot + (uint32_t)__popc(hit & ((1u << j) - 1u))] =
-                                make_uint2(q + 16u * half + j, lo[j]);
+                    // (offsets j unrolled: lo[j] stays a static register)
+                    uint32_t slot = qn + incl - cnt;
+#pragma unroll
+                    for (int j = 0; j < 16; j++) {
+                        if ((hit >> j) & 1u) {
+                            queue[slot] = make_uint2(q + 16u * half + (uint32_t)j, lo[j]);
+                            slot++;
+                        }
                     }
                     qn += tot;
                 } else if (tot) {
@@ -314,7 +311,7 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
                         if (m) {
                             if (t) queue[qn + mbcnt(m)] = make_uint2(q + 16u * half + j, lo[j]);
                             qn = uniform(qn + (uint32_t)__popcll(m));
-                            if (qn > Q_CAP - 64u) scan_flush(a, queue, qn, c, c0, ev_n, dense);
+                            if (qn > Q_CAP - 64u) scan_flush<MODE>(a, queue, qn, c, c0, ev_n, dense);
                         }
                     }
                 }
@@ -325,14 +322,15 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
             // iteration boundary: finish the previous probe batch, start this one
             if (pd.n) {
                 if (pd.c == c) {
-                    pend_complete(a, pd, ev_n, dense);
+                    pend_complete<MODE>(a, pd, ev_n, dense);
                 } else {
-                    pend_complete(a, pd, prev_ev, prev_dense);
+                    pend_complete<MODE>(a, pd, prev_ev, prev_dense);
                     if (l == 0) a.L.cnt[prev_c] = prev_dense ? (EV_DENSE | prev_ev) : prev_ev;
                     if (l == 0 && prev_dense) atomicAdd(&a.P.ctl[CTL_DENSE], 1u);
                     prev_c = NONE;
                 }
             }
+            if (MODE == 4) { sink = sink * 31u + qn + queue[l & 63u].y; qn = 0; }
             if (qn) {
                 pend_issue(a, pd, queue, qn, c, c0);
                 qn = 0;
@@ -343,9 +341,9 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
         }
         if (qn) {  // chunk whose only position is 2047: no iteration ran
             if (pd.n) {
-                if (pd.c == c) pend_complete(a, pd, ev_n, dense);
+                if (pd.c == c) pend_complete<MODE>(a, pd, ev_n, dense);
                 else {
-                    pend_complete(a, pd, prev_ev, prev_dense);
+                    pend_complete<MODE>(a, pd, prev_ev, prev_dense);
                     if (l == 0) a.L.cnt[prev_c] = prev_dense ? (EV_DENSE | prev_ev) : prev_ev;
                     if (l == 0 && prev_dense) atomicAdd(&a.P.ctl[CTL_DENSE], 1u);
                     prev_c = NONE;
@@ -372,7 +370,7 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
     if (MODE >= 2 && sink == 0x7FFFFFF0u - a.ck_hi) a.P.ctl[CTL_ERROR] = sink;  // never true; keeps ablations honest
     if (pd.n) {
         if (pd.c == prev_c) {
-            pend_complete(a, pd, prev_ev, prev_dense);
+            pend_complete<MODE>(a, pd, prev_ev, prev_dense);
             if (l == 0) a.L.cnt[prev_c] = prev_dense ? (EV_DENSE | prev_ev) : prev_ev;
             if (l == 0 && prev_dense) atomicAdd(&a.P.ctl[CTL_DENSE], 1u);
         }
@@ -383,6 +381,8 @@ template __global__ void k_scan<0>(ScanArgs);
 template __global__ void k_scan<1>(ScanArgs);
 template __global__ void k_scan<2>(ScanArgs);
 template __global__ void k_scan<3>(ScanArgs);
+template __global__ void k_scan<4>(ScanArgs);
+template __global__ void k_scan<5>(ScanArgs);
 
 // ------------------------------------------------------------- k_resolve ----------------
 // One wave per chunk: sort the sparse list, then resolve every event exactly.

@@ -988,7 +988,7 @@ extern "C" double xc__scan_ablation(xc_plan *p, const uint8_t *d_in, int mode, i
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    auto kern = mode == 0 ? k_scan<0> : mode == 1 ? k_scan<1> : mode == 2 ? k_scan<2> : k_scan<3>;
+    auto kern = mode == 0 ? k_scan<0> : mode == 1 ? k_scan<1> : mode == 2 ? k_scan<2> : mode == 3 ? k_scan<3> : mode == 4 ? k_scan<4> : k_scan<5>;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * SCAN_WAVES), 0, ctx->stream, a);
     hipEventRecord(e0, ctx->stream);
     for (int i = 0; i < iters; i++)
