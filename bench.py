@@ -182,7 +182,8 @@ def main():
         "stats": {"n_extract": int(st.n_extract), "n_ref": int(st.n_ref),
                   "out_over_in": round(out_bytes / in_bytes_rank, 4),
                   "sub_batches": int(st.sub_batches), "outer_rounds": int(st.outer_rounds),
-                  "walk_rounds": int(st.walk_rounds), "dense_chunks": int(st.dense_chunks)},
+                  "walk_rounds": int(st.walk_rounds), "dense_chunks": int(st.dense_chunks),
+                  "redone": int(st.redone), "shadow_misses": int(st.shadow_misses)},
         "verified_buffers": args.verify if verified else 0,
         "cpu_baseline": None,
     }

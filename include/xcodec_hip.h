@@ -119,6 +119,8 @@ typedef struct {
     uint64_t n_ref;      /* REF tokens emitted */
     uint64_t in_bytes, out_bytes;
     uint32_t sub_batches, walk_rounds, outer_rounds, dense_chunks;
+    uint32_t redone;     /* sub-batches the asynchronous pass handed back to the host */
+    uint32_t shadow_misses; /* ... of which because a predicted REF was not emitted */
 } xc_run_stats;
 int xc_plan_stats(xc_plan *p, xc_run_stats *st);
 

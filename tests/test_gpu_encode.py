@@ -242,3 +242,55 @@ def test_many_subbatches_async_pipeline(gpu_ctx, oracle_mod, monkeypatch):
         else:
             bufs.append(a.copy())
     _check(gpu_ctx, oracle_mod, bufs, warm=[[pool[i:i + 65536] for i in range(0, 8 * 65536, 65536)]])
+
+
+def test_ref_shadow_misses(gpu_ctx, oracle_mod, monkeypatch):
+    """REF shadows: the scan skips the windows after a predicted REF (an aligned block found in
+    the cache) and the walk verifies that the REF was emitted.  Here predicted REFs do not
+    happen: an unaligned REF just before resets the hash past the aligned position, or the
+    cached block is a hash collision, so the gate must stop the asynchronous pass and the
+    sub-batch must be redone scanning every position."""
+    monkeypatch.setenv("XC_SUB_MB", "1")
+    a = W.gen(61, 2048)
+    x = np.concatenate([W.gen(62, 100), a, W.gen(63, 65536 - 2148)])      # REF at 2147 hides 4095
+    cx, cy = _collision_pair(11)
+    y = np.concatenate([W.gen(64, 4096), cy, W.gen(65, 20000)])           # block 2 collides
+    z = np.concatenate([W.gen(66, 6144), a, W.gen(67, 9000)])             # a clean aligned REF
+    pool = W.pool(16)
+    warm = [[a, x[2048:4096].copy(), cx], [pool[i:i + 65536] for i in range(0, 8 * 65536, 65536)]]
+    bufs = []
+    for k in range(24):
+        bufs.append([x, y, z, pool[(k % 8) * 65536:(k % 8) * 65536 + 65536].copy()][k % 4])
+    _check(gpu_ctx, oracle_mod, bufs, warm=warm)
+    # the same batch as a device-resident plan: every sub-batch with x or y is handed back
+    st = _plan_run(gpu_ctx, oracle_mod, bufs, warm)
+    assert st.shadow_misses >= 1 and st.redone >= st.shadow_misses, (st.redone, st.shadow_misses)
+    st = _plan_run(gpu_ctx, oracle_mod, [z, z[::-1].copy()] * 4, warm)
+    assert st.shadow_misses == 0
+
+
+def _plan_run(ctx, oracle_mod, bufs, warm):
+    import torch
+    import wanproxy_amd as w
+    oc = oracle_mod.Cache()
+    for batch in warm:
+        oc.encode_batch(batch)
+    want = oc.encode_batch(bufs)
+    cache = w.XCodecCache(ctx, 1 << 14)
+    for batch in warm:
+        w.XCodecEncoder(cache).encode_batch(batch)
+    plan = w.EncodePlan(cache, [len(b) for b in bufs])
+    arena = np.zeros(plan.in_bytes, np.uint8)
+    for i, b in enumerate(bufs):
+        arena[int(plan.in_off[i]):int(plan.in_off[i]) + len(b)] = b
+    d_in = torch.from_numpy(arena).cuda()
+    d_out = torch.zeros(plan.out_bytes, dtype=torch.uint8, device="cuda")
+    d_len = torch.zeros(len(bufs), dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    plan.run(d_in.data_ptr(), d_out.data_ptr(), d_len.data_ptr())
+    ctx.sync()
+    out, lens = d_out.cpu().numpy(), d_len.cpu().numpy()
+    for i in range(len(bufs)):
+        o = int(plan.out_off[i])
+        assert out[o:o + int(lens[i])].tobytes() == want[i], i
+    return plan.stats()

@@ -88,25 +88,43 @@ struct Sums4 {
     uint32_t aw, bw, af, bf;
 };
 
+// ffbl of byte K of x, minus... exactly: v_ffbl_b32 on the zero-extended byte, which the
+// hardware defines as 0xFFFFFFFF for a zero byte, so ffbl + 1 == ffs(byte) with ffs(0) == 0
+// (xcodec/xcodec_hash.h:95-96) and no compare/select.  Inline asm: the compiler's cttz would
+// add the zero test back.
+template <int K>
+__device__ __forceinline__ uint32_t ffbl_byte(uint32_t x)
+{
+    uint32_t r;
+    if (K == 0) asm("v_ffbl_b32_sdwa %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0" : "=v"(r) : "v"(x));
+    if (K == 1) asm("v_ffbl_b32_sdwa %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1" : "=v"(r) : "v"(x));
+    if (K == 2) asm("v_ffbl_b32_sdwa %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2" : "=v"(r) : "v"(x));
+    if (K == 3) asm("v_ffbl_b32_sdwa %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3" : "=v"(r) : "v"(x));
+    return r;
+}
+
 __device__ __forceinline__ Sums4 chunk_sums32(const uint32_t w[8])
 {
     Sums4 s = {0, 0, 0, 0};
-    uint32_t sb = 0, jb = 0;
+    uint32_t sb = 0, jb = 0, sf = 0, jf = 0;
 #pragma unroll
     for (int d = 0; d < 8; d++) {
         // weights (4d, 4d+1, 4d+2, 4d+3) packed as bytes
         const uint32_t wt = (uint32_t)(4 * d) * 0x01010101u + 0x03020100u;
         sb = __builtin_amdgcn_udot4(w[d], 0x01010101u, sb, false);
         jb = __builtin_amdgcn_udot4(w[d], wt, jb, false);
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            uint32_t f = ffs8((w[d] >> (8 * k)) & 0xffu);
-            s.af += f;
-            s.bf += (uint32_t)(4 * d + k) * f;
-        }
+        // f - 1 per byte (ffbl): sum and j-weighted sum; the +1s are added back below
+        const uint32_t f0 = ffbl_byte<0>(w[d]), f1 = ffbl_byte<1>(w[d]);
+        const uint32_t f2 = ffbl_byte<2>(w[d]), f3 = ffbl_byte<3>(w[d]);
+        sf += f0 + f1 + f2 + f3;
+        // signed 24-bit multiplies (v_mad_i32_i24): ffbl(0) = -1 stays -1 in 24 bits
+        jf += (uint32_t)(__mul24((int)f0, 4 * d) + __mul24((int)f1, 4 * d + 1) + __mul24((int)f2, 4 * d + 2) +
+                         __mul24((int)f3, 4 * d + 3));
     }
     s.aw = sb + 32u;         // sum (b+1)
     s.bw = jb + 496u;        // sum j*(b+1), sum j = 496
+    s.af = sf + 32u;         // sum ffs(b) = sum (ffbl(b) + 1)
+    s.bf = jf + 496u;        // sum j*ffs(b)
     return s;
 }
 

@@ -219,6 +219,7 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
 
     // chunk descriptors: {c0, c1, arena offset lo, hi}; the next one is always in flight
     uint4 dsc = a.P.chunk_desc[c];
+    uint32_t gblk = a.shadow ? uniform(a.P.chunk_blk[c]) : 0u;
     uint32_t pw[8], w[8], wn[8];
     first_blocks(desc_base(a, dsc), uniform(dsc.x), l, pw, w, wn);
     uint4 dn = a.P.chunk_desc[min(c + 1u, c_end - 1u)];
@@ -256,6 +257,9 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
             const bool need2 = s + 2u * XC_SEG < c1 || (contig && (s + 2u * XC_SEG == c1 || next_long));
             load32_aligned(base + (need2 ? s + 2u * XC_SEG : s) + 32u * l, wn2);
             const BlockSums cs = block_sums(w, l);
+            // REF shadow: the block before s is a predicted REF, after which the reference looks
+            // nothing up until s + 2047 (recorded below); k_walk verifies the REF happened
+            const bool shadowed = a.shadow && uniform(a.P.blk_pref[gblk + (s >> 11) - 1u]) != 0u;
             // window ending just before this lane's first position q = s + 32 l:
             // out-chunks of lanes >= l (previous block) + in-chunks of lanes < l.
             const uint32_t sufA = ps.totA - ps.preA, sufC = ps.totC - ps.preC;
@@ -268,6 +272,7 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
             const uint32_t vmask = (q + 32u <= c1) ? 0xFFFFFFFFu : (q >= c1 ? 0u : ((1u << (c1 - q)) - 1u));
 #pragma unroll
             for (int half = 0; half < (MODE == 2 ? 0 : 2); half++) {
+                if (shadowed) break;
                 uint32_t lo[16];
                 uint32_t hit = 0;
 #pragma unroll
@@ -364,6 +369,7 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
         if (!has_next) break;
         c += 1u;
         dsc = dn;
+        if (a.shadow) gblk = uniform(a.P.chunk_blk[c]);
         if (!contig) first_blocks(desc_base(a, dsc), uniform(dsc.x), l, pw, w, wn);
         dn = a.P.chunk_desc[min(c + 1u, c_end - 1u)];
     }
@@ -425,6 +431,7 @@ __global__ __launch_bounds__(256) void k_resolve(ResolveArgs a)
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // the walk that follows reports afresh
         a.P.ctl[CTL_GREW] = 0u;
         a.P.ctl[CTL_FIRST_CROSS] = NONE;
+        a.P.ctl[CTL_SHADOW] = 0u;
     }
     const uint32_t c = a.ck_lo + blockIdx.x * 4u + (threadIdx.x >> 6);
     if (c >= a.ck_hi) return;
@@ -605,6 +612,7 @@ __global__ __launch_bounds__(64) void k_walk(WalkArgs a)
     __shared__ uint32_t d_cand[MAX_DECL];
     __shared__ uint64_t d_hash[MAX_DECL];
     __shared__ uint32_t d_known[MAX_DECL];
+    __shared__ uint32_t ref_done[MAX_BUF / XC_SEG / 32u];  // aligned REFs emitted, per block
     const PlanDev &P = a.P;
     const uint32_t b = a.j0 + blockIdx.x;
     if (b >= a.j1) return;
@@ -624,11 +632,17 @@ __global__ __launch_bounds__(64) void k_walk(WalkArgs a)
     uint32_t p = XC_SEG - 1u;
     bool cross = false;
 
+    if (a.shadow)
+        for (uint32_t i = l; i < MAX_BUF / XC_SEG / 32u; i += 64u) ref_done[i] = 0u;
     uint32_t n_ext = 0, n_ref = 0;
     auto emit = [&](uint32_t op, uint32_t lb, uint32_t le, uint32_t seg, uint32_t dpos, uint64_t h,
                     uint32_t known) {
         n_ext += op == OP_EXTRACT ? 1u : 0u;
         n_ref += op == OP_REF ? 1u : 0u;
+        if (a.shadow && op == OP_REF && (seg & (XC_SEG - 1u)) == 0u && l == 0) {
+            const uint32_t k = seg / XC_SEG;  // the REF covers aligned block k
+            ref_done[k >> 5] |= 1u << (k & 31u);
+        }
         if (ntok < tcap && l == 0) {
             P.tok_op[tb + ntok] = op;
             P.tok_known[tb + ntok] = known;
@@ -733,6 +747,16 @@ __global__ __launch_bounds__(64) void k_walk(WalkArgs a)
         basep = (uint32_t)cand + XC_SEG;
     }
     emit(OP_END, basep, len, 0, 0, 0, 0);
+    if (a.shadow) {
+        // every predicted REF whose following block the scan skipped must have been emitted
+        __syncthreads();
+        const uint32_t nblk = len / XC_SEG, bb = P.blk_base[b];
+        bool miss = false;
+        for (uint32_t k = l; k < nblk; k += 64u)
+            if ((k + 1u) * XC_SEG < len && P.blk_pref[bb + k] && !((ref_done[k >> 5] >> (k & 31u)) & 1u))
+                miss = true;
+        if (ballot(miss) && l == 0) atomicOr(&P.ctl[CTL_SHADOW], 1u);
+    }
     if (l == 0) {
         P.tok_cnt[b] = ntok;
         P.buf_next[b] = n_ext;
@@ -803,7 +827,9 @@ __global__ __launch_bounds__(64) void k_blockpredict(DeclArgs a)
     for (uint32_t k = lane_id(); k < nblk; k += 64u) {
         const uint64_t h = P.blk_h[bb + k];
         uint64_t v;
-        if (!set_find(P.cache, h, &v) &&
+        const bool cached = set_find(P.cache, h, &v);
+        P.blk_pref[bb + k] = cached ? 1u : 0u;  // a predicted REF (REF shadows, k_scan / k_walk)
+        if (!cached &&
             set_insert(P.dset, h, ((uint64_t)b << 32) | (k * XC_SEG + 2u * XC_SEG - 1u), true, nullptr, nullptr)) {
             const uint32_t g = l2_mix((uint32_t)h), gi = (g >> 14) * 2u;
             atomicOr(&P.l2mix[gi], 1u << (g & 31u));
@@ -984,11 +1010,11 @@ __global__ __launch_bounds__(1024) void k_alloc(EmitArgs a)
     if (aborted(a.P)) return;
     if (a.gate_sb != NONE) {
         // async pipeline gate: stop here (and every later launch) if sub-batch gate_sb needs
-        // the host: declaration growth, a cross-buffer conflict or an error
+        // the host: declaration growth, a missed REF shadow, a cross-buffer conflict or an error
         __shared__ uint32_t stop;
         if (threadIdx.x == 0) {
             const uint32_t *ctl = a.P.ctl;
-            stop = (ctl[CTL_GREW] || ctl[CTL_FIRST_CROSS] < a.j1 || ctl[CTL_ERROR]) ? 1u : 0u;
+            stop = (ctl[CTL_GREW] || ctl[CTL_SHADOW] || ctl[CTL_FIRST_CROSS] < a.j1 || ctl[CTL_ERROR]) ? 1u : 0u;
             if (stop) {
                 a.P.ctl[CTL_ABORT_SB] = a.gate_sb;
                 a.P.ctl[CTL_ABORT] = 1u;

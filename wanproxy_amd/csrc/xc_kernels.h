@@ -36,6 +36,7 @@ enum : uint32_t {
     CTL_UNDO = 6,
     CTL_ABORT = 7,     // set by k_gate: a sub-batch needs the host (growth, cross-buffer, error)
     CTL_ABORT_SB = 8,  // ... and which one; every later pipeline kernel exits at once
+    CTL_SHADOW = 9,    // a walk did not emit a predicted REF whose shadow the scan skipped
     CTL_WORDS = 16
 };
 constexpr uint32_t ERR_CAPACITY = 1, ERR_TOKENS = 2, ERR_DECLS = 4;
@@ -81,6 +82,12 @@ struct PlanDev {
     uint64_t *out_len;
     uint32_t *ctl;
     uint32_t *l2mix;  // level-2 filter of cache | predicted declarations (combined scan)
+    // REF shadows: blk_pref[g] = 1 when aligned block g (global index) is in the cache, so the
+    // window ending at its last byte is a predicted REF; the reference looks nothing up in the
+    // 2047 positions after a REF (xcodec_encoder.cc:111-118 resets the hash), so the scan may
+    // skip the next block's windows and the walk verifies that the REF happened.
+    uint32_t *blk_pref;
+    const uint32_t *chunk_blk;  // [nchunks] global index of the chunk's buffer's block 0
 };
 
 // kernel argument blocks (shared by xc_encode.hip and xc_runtime.hip)
@@ -99,6 +106,7 @@ struct ScanArgs {
     DevSet set2;    // optional second set tested in the same pass (predicted declarations)
     int has2;
     const uint2 *l2;  // level-2 filter of set (| set2): one 8-byte L2 read per level-1 positive
+    int shadow;       // skip the windows in the shadow of predicted REFs (P.blk_pref)
 };
 struct ResolveArgs {
     PlanDev P;
@@ -110,6 +118,7 @@ struct WalkArgs {
     PlanDev P;
     uint32_t j0, j1;
     int use_d;  // 0 on the first round (no declaration layer yet)
+    int shadow; // the scan skipped predicted-REF shadows: verify every such REF was emitted
 };
 struct DeclArgs {
     PlanDev P;

@@ -439,6 +439,8 @@ struct xc_plan {
     hipEvent_t ev_start = nullptr;
     std::vector<hipEvent_t> ev_hash, ev_go;
     uint32_t next_hash = 0;  // first sub-batch not yet enqueued for hashing in this run
+    int shadow = 1;          // REF shadows in the async pass (XC_NO_SHADOW=1 disables)
+    uint32_t *d_chunk_blk = nullptr;
 };
 
 static hipEvent_t ev_get(xc_plan *p)
@@ -612,6 +614,17 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     HIPCHK(hipMalloc(&P.tok_h, nt * 8));
     HIPCHK(hipMalloc(&P.tok_known, nt * 4));
     HIPCHK(hipMalloc(&P.blk_h, std::max<uint64_t>(nblk, 1) * 8));
+    HIPCHK(hipMalloc(&P.blk_pref, std::max<uint64_t>(nblk, 1) * 4));
+    HIPCHK(hipMemsetAsync(P.blk_pref, 0, std::max<uint64_t>(nblk, 1) * 4, s));
+    {
+        std::vector<uint32_t> cb(std::max<size_t>(chunks.size(), 1), 0);
+        for (size_t k = 0; k < chunks.size(); k++) cb[k] = blk_base[chunks[k].x];
+        HIPCHK(hipMalloc(&p->d_chunk_blk, cb.size() * 4));
+        HIPCHK(hipMemcpyAsync(p->d_chunk_blk, cb.data(), cb.size() * 4, hipMemcpyHostToDevice, s));
+        P.chunk_blk = p->d_chunk_blk;
+        const char *e = getenv("XC_NO_SHADOW");
+        p->shadow = (e && atoi(e)) ? 0 : 1;
+    }
     HIPCHK(hipMalloc(&p->d_blk_base, nb1 * 4));
     HIPCHK(hipMalloc(&p->d_l2mix, (size_t)XC_L2_WORDS * 8));
     P.l2mix = p->d_l2mix;
@@ -658,6 +671,8 @@ extern "C" int xc_plan_destroy(xc_plan *p)
     hipFree(p->P.tok_h);
     hipFree(p->P.tok_known);
     hipFree(p->P.blk_h);
+    hipFree(p->P.blk_pref);
+    hipFree(p->d_chunk_blk);
     hipFree(p->d_blk_base);
     hipFree(p->d_l2mix);
     hipFree(p->P.buf_next);
@@ -722,11 +737,11 @@ static int read_ctl(xc_plan *p, uint32_t *ctl)
 }
 
 static int launch_scan(xc_plan *p, const Layer &L, const DevSet &set, uint32_t ck_lo, uint32_t ck_hi,
-                       const DevSet *set2 = nullptr)
+                       const DevSet *set2 = nullptr, int shadow = 0)
 {
     if (ck_hi <= ck_lo) return XC_OK;
     xc_ctx *ctx = p->cache->ctx;
-    ScanArgs a{p->P, L, set, ck_lo, ck_hi, 0, DevSet{}, 0, (const uint2 *)set.l2};
+    ScanArgs a{p->P, L, set, ck_lo, ck_hi, 0, DevSet{}, 0, (const uint2 *)set.l2, shadow};
     if (set2) {
         a.set2 = *set2;
         a.has2 = 1;
@@ -751,11 +766,11 @@ static int launch_resolve(xc_plan *p, const Layer &L, int dmode, uint32_t ck_lo,
     return XC_OK;
 }
 
-static int launch_walk_round(xc_plan *p, uint32_t j0, uint32_t j1, int use_d)
+static int launch_walk_round(xc_plan *p, uint32_t j0, uint32_t j1, int use_d, int shadow = 0)
 {
     hipStream_t s = p->cache->ctx->stream;
-    // (k_resolve, always launched just before, reset GREW / FIRST_CROSS)
-    WalkArgs w{p->P, j0, j1, use_d};
+    // (k_resolve, always launched just before, reset GREW / FIRST_CROSS / SHADOW)
+    WalkArgs w{p->P, j0, j1, use_d, shadow};
     {
         KSpan span(p, XC_K_WALK);
         hipLaunchKernelGGL(k_walk, dim3(j1 - j0), dim3(64), 0, s, w);
@@ -801,7 +816,9 @@ static int enqueue_block_hash(xc_plan *p, uint32_t k, hipEvent_t after)
     return XC_OK;
 }
 
-static int launch_first_round(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t s1)
+// shadow: skip the windows in predicted-REF shadows (async pass; the step-by-step redo of a
+// sub-batch scans every position).
+static int launch_first_round(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t s1, int shadow)
 {
     hipStream_t s = p->cache->ctx->stream;
     int rc;
@@ -826,9 +843,9 @@ static int launch_first_round(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t s1)
         HIPCHK(hipEventRecord(p->ev_go[sb], s));
         if ((rc = enqueue_block_hash(p, sb + 1, p->ev_go[sb]))) return rc;
     }
-    if ((rc = launch_scan(p, p->P.S, p->P.cache, ck_lo, ck_hi, &p->P.dset))) return rc;
+    if ((rc = launch_scan(p, p->P.S, p->P.cache, ck_lo, ck_hi, &p->P.dset, shadow))) return rc;
     if ((rc = launch_resolve(p, p->P.S, 2, ck_lo, ck_hi))) return rc;
-    return launch_walk_round(p, j0, s1, 0);
+    return launch_walk_round(p, j0, s1, 0, shadow);
 }
 
 // Sub-batch sb with no host synchronisation: first round, gate, emit of the whole sub-batch.
@@ -837,7 +854,7 @@ static int encode_sub_async(xc_plan *p, uint32_t sb)
     const uint32_t j0 = p->sub[sb], s1 = p->sub[sb + 1];
     int rc;
     p->stats.sub_batches++;
-    if ((rc = launch_first_round(p, sb, j0, s1))) return rc;
+    if ((rc = launch_first_round(p, sb, j0, s1, p->shadow))) return rc;
     return launch_emit(p, j0, s1, sb);
 }
 
@@ -851,7 +868,7 @@ static int encode_sub_sync(xc_plan *p, uint32_t sb, uint32_t *ctl)
     int rc;
     while (j0 < s1) {
         const uint32_t ck_lo = p->chunk0[j0], ck_hi = p->chunk0[s1];
-        if ((rc = launch_first_round(p, sb, j0, s1))) return rc;
+        if ((rc = launch_first_round(p, sb, j0, s1, 0))) return rc;
         if ((rc = read_ctl(p, ctl))) return rc;
         uint32_t rounds = 0;
         while (!ctl[CTL_ERROR] && ctl[CTL_GREW]) {
@@ -897,6 +914,8 @@ extern "C" int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, ui
         si = ctl[CTL_ABORT_SB];
         HIPCHK(hipMemsetAsync(p->P.ctl + CTL_ABORT, 0, 4, s));
         if (ctl[CTL_ERROR]) break;
+        p->stats.redone++;
+        if (ctl[CTL_SHADOW]) p->stats.shadow_misses++;
         // that sub-batch, step by step (its pipeline state is discarded and redone)
         if ((rc = encode_sub_sync(p, (uint32_t)si, ctl))) return rc;
         if (ctl[CTL_ERROR]) break;

@@ -48,7 +48,8 @@ class RunStats(C.Structure):
     _fields_ = [("n_extract", C.c_uint64), ("n_ref", C.c_uint64), ("in_bytes", C.c_uint64),
                 ("out_bytes", C.c_uint64), ("sub_batches", C.c_uint32),
                 ("walk_rounds", C.c_uint32), ("outer_rounds", C.c_uint32),
-                ("dense_chunks", C.c_uint32)]
+                ("dense_chunks", C.c_uint32), ("redone", C.c_uint32),
+                ("shadow_misses", C.c_uint32)]
 
 
 _LIB = None
