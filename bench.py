@@ -189,20 +189,33 @@ def main():
     }
 
     if rank == 0 and world == 1 and not args.no_e2e:
-        # end-to-end from pinned host memory: H2D of the input arena, encode, D2H of the output arena
-        h_in = torch.empty(plan.in_bytes, dtype=torch.uint8).pin_memory()
-        h_in.copy_(d_in.cpu())
-        h_out = torch.empty(plan.out_bytes, dtype=torch.uint8).pin_memory()
+        # end-to-end from host memory (xc_encode_run_host): the input arena in pinned host
+        # memory, each sub-batch copied in on a copy stream while earlier ones encode, and every
+        # sub-batch's encoded streams packed into pinned host memory by a kernel as it is emitted
+        h_in = w.HostBuffer(ctx, plan.in_bytes)
+        h_in.array[:] = d_in.cpu().numpy()
+        h_out = w.HostBuffer(ctx, plan.out_bytes)
+        cache.restore_async()
+        plan.run_host(h_in, h_out)  # warm-up (device arenas of the host path)
+        reps = 3
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        d_in.copy_(h_in, non_blocking=True)
-        torch.cuda.synchronize()
-        step()
-        h_out.copy_(d_out, non_blocking=True)
-        torch.cuda.synchronize()
-        e2e = time.perf_counter() - t0
+        for _ in range(reps):
+            cache.restore_async()
+            lens, pos = plan.run_host(h_in, h_out)
+        e2e = (time.perf_counter() - t0) / reps
+        packed = int(lens.sum())
+        if packed != out_bytes:
+            raise SystemExit("bench: host path output size differs from the device-resident run")
+        if verified:
+            for i in range(len(want)):
+                if h_out.array[int(pos[i]):int(pos[i]) + int(lens[i])].tobytes() != want[i]:
+                    raise SystemExit("bench: host path output differs from the oracle")
         result["e2e_host_gibs"] = round(in_bytes_rank / e2e / 2**30, 3)
-        result["e2e_note"] = "pinned H2D of the input arena + encode + D2H of the whole output arena (2n+16 per buffer)"
+        result["e2e_ms"] = round(e2e * 1e3, 2)
+        result["e2e_note"] = ("xc_encode_run_host: pinned host input arena -> per-sub-batch H2D "
+                              "overlapping the encode -> streams packed into pinned host memory "
+                              f"({packed >> 20} MiB) by a kernel after each sub-batch")
 
     if rank == 0 and world == 1 and not args.no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))

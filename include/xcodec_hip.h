@@ -92,6 +92,20 @@ int xc_encode_batch_host(xc_cache *c, const uint8_t *in, const uint64_t *in_off,
                          const uint64_t *in_len, uint64_t nbuf, uint8_t *out,
                          const uint64_t *out_off, const uint64_t *out_cap, uint64_t *out_len);
 
+/* Pinned, device-mapped host memory (hipHostMalloc) for the end-to-end host path. */
+int xc_host_alloc(xc_ctx *ctx, uint64_t bytes, void **out);
+int xc_host_free(void *ptr);
+
+/* End-to-end from host memory, the proxy's path (socket buffers in, encoded frames out):
+ * h_in is a host arena in the plan's input layout (xc_plan_layout in_off), h_out pinned host
+ * memory from xc_host_alloc.  Each sub-batch's input is copied to the device on a copy stream
+ * while earlier sub-batches encode, and each sub-batch's encoded streams are packed in buffer
+ * order straight into h_out by a kernel as soon as they are emitted (buffer i at h_pos[i],
+ * h_len[i] bytes; h_pos may be NULL).  Fails with XC_EINVAL if they exceed h_out_cap.
+ * Same results as xc_encode_run; device arenas are owned by the plan. */
+int xc_encode_run_host(xc_plan *p, const uint8_t *h_in, uint8_t *h_out, uint64_t h_out_cap,
+                       uint64_t *h_len, uint64_t *h_pos);
+
 /* Enqueue xc_cache_restore() on the context stream without blocking the host. */
 int xc_cache_restore_async(xc_cache *c);
 

@@ -294,3 +294,52 @@ def _plan_run(ctx, oracle_mod, bufs, warm):
         o = int(plan.out_off[i])
         assert out[o:o + int(lens[i])].tobytes() == want[i], i
     return plan.stats()
+
+
+def _host_path(ctx, oracle_mod, bufs, warm, cap=None):
+    import wanproxy_amd as w
+    oc = oracle_mod.Cache()
+    for batch in warm:
+        oc.encode_batch(batch)
+    want = oc.encode_batch(bufs)
+    cache = w.XCodecCache(ctx, 1 << 15)
+    for batch in warm:
+        w.XCodecEncoder(cache).encode_batch(batch)
+    plan = w.EncodePlan(cache, [len(b) for b in bufs])
+    h_in = w.HostBuffer(ctx, plan.in_bytes)
+    for i, b in enumerate(bufs):
+        h_in.array[int(plan.in_off[i]):int(plan.in_off[i]) + len(b)] = b
+    h_out = w.HostBuffer(ctx, cap if cap is not None else sum(2 * len(b) + 16 for b in bufs))
+    lens, pos = plan.run_host(h_in, h_out)
+    assert int(pos[0]) == 0
+    for i in range(len(bufs)):
+        if i:
+            assert int(pos[i]) == int(pos[i - 1]) + int(lens[i - 1])
+        got = h_out.array[int(pos[i]):int(pos[i]) + int(lens[i])].tobytes()
+        assert got == want[i], i
+    return plan.stats()
+
+
+def test_host_path_packed(gpu_ctx, oracle_mod, monkeypatch):
+    """xc_encode_run_host: per-sub-batch H2D on a copy stream, encoded streams packed into pinned
+    host memory by the packing kernels; with 1 MiB sub-batches, some redone by the host (shadow
+    misses, cross-buffer declarations), which must be packed in order too."""
+    monkeypatch.setenv("XC_SUB_MB", "1")
+    pool = W.pool(16)
+    a = W.gen(61, 2048)
+    x = np.concatenate([W.gen(62, 100), a, W.gen(63, 65536 - 2148)])
+    c = W.gen(70, 40000)
+    warm = [[a, x[2048:4096].copy()], [pool[i:i + 65536] for i in range(0, 8 * 65536, 65536)]]
+    bufs = []
+    for k in range(30):
+        bufs.append([x, c, np.concatenate([W.gen(80 + k, 3000), c[:20000]]), _esc(30000, k),
+                     pool[(k % 8) * 65536:(k % 8) * 65536 + 65536].copy(), W.gen(90 + k, 777)][k % 6])
+    st = _host_path(gpu_ctx, oracle_mod, bufs, warm)
+    assert st.redone >= 1
+    _host_path(gpu_ctx, oracle_mod, [W.gen(5, 65536) for _ in range(4)], [])
+
+
+def test_host_path_capacity(gpu_ctx, oracle_mod):
+    import wanproxy_amd as w
+    with pytest.raises(w.XCodecError):
+        _host_path(gpu_ctx, oracle_mod, [W.gen(9, 65536)], [], cap=1000)

@@ -5,8 +5,8 @@ reference expansion) runs as hand-written gfx950 HIP kernels in
 ``libxcodec_hip.so`` behind the C ABI declared in ``include/xcodec_hip.h``.
 """
 from . import workloads  # noqa: F401
-from .xcodec import (Context, EncodePlan, XCodecCache, XCodecDecoder, XCodecEncoder,  # noqa: F401
-                     XCodecError, device_count, load_library)
+from .xcodec import (Context, EncodePlan, HostBuffer, XCodecCache, XCodecDecoder,  # noqa: F401
+                     XCodecEncoder, XCodecError, device_count, load_library)
 
-__all__ = ["Context", "EncodePlan", "XCodecCache", "XCodecDecoder", "XCodecEncoder",
+__all__ = ["Context", "EncodePlan", "HostBuffer", "XCodecCache", "XCodecDecoder", "XCodecEncoder",
            "XCodecError", "device_count", "load_library", "workloads"]

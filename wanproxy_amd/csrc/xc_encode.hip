@@ -609,10 +609,13 @@ constexpr uint32_t R_MISS = 0, R_HIT = 1, R_COLL = 2;
 __global__ __launch_bounds__(64) void k_walk(WalkArgs a)
 {
     if (aborted(a.P)) return;
-    __shared__ uint32_t d_cand[MAX_DECL];
-    __shared__ uint64_t d_hash[MAX_DECL];
-    __shared__ uint32_t d_known[MAX_DECL];
-    __shared__ uint32_t ref_done[MAX_BUF / XC_SEG / 32u];  // aligned REFs emitted, per block
+    // declarations of this buffer (sized by the plan's longest buffer, so short buffers leave
+    // room for many walk waves per CU) and the aligned REFs emitted, one bit per block
+    extern __shared__ uint64_t walk_lds[];
+    uint64_t *d_hash = walk_lds;
+    uint32_t *d_cand = (uint32_t *)(walk_lds + a.max_decl);
+    uint32_t *d_known = d_cand + a.max_decl;
+    uint32_t *ref_done = d_known + a.max_decl;
     const PlanDev &P = a.P;
     const uint32_t b = a.j0 + blockIdx.x;
     if (b >= a.j1) return;
@@ -633,7 +636,7 @@ __global__ __launch_bounds__(64) void k_walk(WalkArgs a)
     bool cross = false;
 
     if (a.shadow)
-        for (uint32_t i = l; i < MAX_BUF / XC_SEG / 32u; i += 64u) ref_done[i] = 0u;
+        for (uint32_t i = l; i < a.max_decl / 32u + 1u; i += 64u) ref_done[i] = 0u;
     uint32_t n_ext = 0, n_ref = 0;
     auto emit = [&](uint32_t op, uint32_t lb, uint32_t le, uint32_t seg, uint32_t dpos, uint64_t h,
                     uint32_t known) {
@@ -729,7 +732,7 @@ __global__ __launch_bounds__(64) void k_walk(WalkArgs a)
         if (dp >= len) break;
         // declaration (xcodec_encoder.cc:77-82, 203-215)
         emit(OP_EXTRACT, basep, (uint32_t)cand, (uint32_t)cand, dp, cand_h, cand_known);
-        if (nd < MAX_DECL) {
+        if (nd < a.max_decl) {
             if (l == 0) {
                 d_cand[nd] = (uint32_t)cand;
                 d_hash[nd] = cand_h;
@@ -1058,6 +1061,62 @@ __global__ __launch_bounds__(1024) void k_alloc(EmitArgs a)
         P.ctl[CTL_NREF] += carry[1];
         if (carry[0] > P.seg_cap) P.ctl[CTL_ERROR] |= ERR_CAPACITY;
     }
+}
+
+// -------------------------------------------------------------- k_pack ------------------
+// Packed offsets of buffers [j0, j1) after the running total (one workgroup), then one
+// workgroup per buffer copies its encoded stream to dst + offset.  With dst in pinned host
+// memory the copy is the device-to-host transfer, overlapping the next sub-batch's encode.
+
+__global__ __launch_bounds__(1024) void k_pack_offsets(PackArgs a)
+{
+    if (aborted(a.P)) return;
+    __shared__ uint64_t wsum[16];
+    __shared__ uint64_t carry;
+    const uint32_t wave = threadIdx.x >> 6, l = lane_id();
+    if (threadIdx.x == 0) carry = *a.total;
+    __syncthreads();
+    for (uint32_t b0 = a.j0; b0 < a.j1; b0 += 1024u) {
+        const uint32_t b = b0 + threadIdx.x;
+        const uint64_t v = b < a.j1 ? a.P.out_len[b] : 0u;
+        // a buffer's stream is < 2^21 bytes, so 64 of them sum below 2^32
+        const uint32_t lo = wave_incl_scan((uint32_t)v);
+        if (l == 63) wsum[wave] = lo;
+        __syncthreads();
+        uint64_t off = carry;
+        for (uint32_t k = 0; k < wave; k++) off += wsum[k];
+        if (b < a.j1) a.pos[b] = off + lo - v;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint64_t t = 0;
+            for (uint32_t k = 0; k < 16; k++) t += wsum[k];
+            carry += t;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        *a.total = carry;
+        if (carry > a.cap) atomicOr(&a.P.ctl[CTL_ERROR], ERR_PACK_CAP);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_pack_copy(PackArgs a)
+{
+    if (aborted(a.P)) return;
+    const uint32_t b = a.j0 + blockIdx.x;
+    if (b >= a.j1) return;
+    const uint64_t n = a.P.out_len[b], o = a.pos[b];
+    if (o + n > a.cap) return;  // flagged by k_pack_offsets
+    const uint8_t *src = a.P.out + a.P.out_off[b];
+    uint8_t *dst = a.dst + o;
+    // four waves, each a contiguous quarter cut at a 16-byte boundary of dst
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint64_t head = (16u - ((uintptr_t)dst & 15u)) & 15u;
+    const uint64_t body = n > head ? (n - head) & ~15ull : 0u;
+    const uint64_t q = (body / 64u) * 16u;  // 16-byte multiple per wave
+    uint64_t s0 = wave == 0 ? 0 : head + q * wave, s1 = wave == 3 ? n : head + q * (wave + 1u);
+    if (s1 > n) s1 = n;
+    if (s0 < s1) wave_copy(dst + s0, src + s0, (uint32_t)(s1 - s0));
 }
 
 // ------------------------------------------------------------ utilities -----------------

@@ -39,7 +39,7 @@ enum : uint32_t {
     CTL_SHADOW = 9,    // a walk did not emit a predicted REF whose shadow the scan skipped
     CTL_WORDS = 16
 };
-constexpr uint32_t ERR_CAPACITY = 1, ERR_TOKENS = 2, ERR_DECLS = 4;
+constexpr uint32_t ERR_CAPACITY = 1, ERR_TOKENS = 2, ERR_DECLS = 4;  // (ERR_PACK_CAP = 8 below)
 
 // One scan layer: per chunk a sorted sparse list (cnt < EV_CAP) or a dense bitmask.
 struct Layer {
@@ -119,7 +119,10 @@ struct WalkArgs {
     uint32_t j0, j1;
     int use_d;  // 0 on the first round (no declaration layer yet)
     int shadow; // the scan skipped predicted-REF shadows: verify every such REF was emitted
+    uint32_t max_decl;  // >= declarations of any buffer (longest buffer / 2048 + 2)
 };
+// dynamic LDS of k_walk
+__host__ __device__ constexpr uint32_t walk_lds_bytes(uint32_t max_decl) { return max_decl * 16u + 8u * (max_decl / 32u + 1u); }
 struct DeclArgs {
     PlanDev P;
     uint32_t j0, j1;
@@ -130,7 +133,21 @@ struct EmitArgs {
     uint32_t gate_sb;  // k_alloc: async-pipeline gate for sub-batch gate_sb (NONE: no gate)
 };
 
+// Packing a sub-batch's encoded streams, in buffer order, into one caller buffer (pinned host
+// memory written over PCIe by the kernel, or device memory): the end-to-end host path.
+struct PackArgs {
+    PlanDev P;
+    uint32_t j0, j1;
+    uint8_t *dst;        // device-visible pointer of the packed output
+    uint64_t cap;        // its capacity
+    uint64_t *total;     // running packed length (device)
+    uint64_t *pos;       // [nb] packed offset of every buffer (device)
+};
+constexpr uint32_t ERR_PACK_CAP = 8;
+
 template <int MODE> __global__ void k_scan(ScanArgs a);
+__global__ void k_pack_offsets(PackArgs a);
+__global__ void k_pack_copy(PackArgs a);
 __global__ void k_resolve(ResolveArgs a);
 __global__ void k_walk(WalkArgs a);
 __global__ void k_declhash(DeclArgs a);

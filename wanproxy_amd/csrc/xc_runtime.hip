@@ -439,7 +439,17 @@ struct xc_plan {
     hipEvent_t ev_start = nullptr;
     std::vector<hipEvent_t> ev_hash, ev_go;
     uint32_t next_hash = 0;  // first sub-batch not yet enqueued for hashing in this run
+    // end-to-end host path (xc_encode_run_host): per-sub-batch H2D on a copy stream, packing
+    // kernels after every emitted sub-batch
+    bool host_path = false;
+    hipStream_t cs = nullptr;
+    std::vector<hipEvent_t> ev_h2d;
+    uint8_t *e_in = nullptr, *e_out = nullptr;
+    uint64_t *e_len = nullptr, *e_pos = nullptr, *e_total = nullptr;
+    uint8_t *pack_dst = nullptr;
+    uint64_t pack_cap = 0;
     int shadow = 1;          // REF shadows in the async pass (XC_NO_SHADOW=1 disables)
+    uint32_t max_decl = 2;   // longest buffer / 2048 + 2 (k_walk's LDS)
     uint32_t *d_chunk_blk = nullptr;
 };
 
@@ -527,6 +537,7 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
                 descs.push_back(make_uint4(s, (uint32_t)std::min<uint64_t>(s + CHUNK_LEN, n) | more,
                                            (uint32_t)p->in_off[i], (uint32_t)(p->in_off[i] >> 32)));
             }
+        p->max_decl = std::max<uint32_t>(p->max_decl, (uint32_t)(n / XC_SEG) + 2u);
         tok_base[i] = (uint32_t)toks;
         blk_base[i] = (uint32_t)nblk;
         nblk += n / XC_SEG;
@@ -686,6 +697,17 @@ extern "C" int xc_plan_destroy(xc_plan *p)
         hipStreamDestroy(p->hs);
     }
     if (p->ev_start) hipEventDestroy(p->ev_start);
+    if (p->cs) {
+        hipStreamSynchronize(p->cs);
+        hipStreamDestroy(p->cs);
+    }
+    for (auto e : p->ev_h2d)
+        if (e) hipEventDestroy(e);
+    hipFree(p->e_in);
+    hipFree(p->e_out);
+    hipFree(p->e_len);
+    hipFree(p->e_pos);
+    hipFree(p->e_total);
     for (auto e : p->ev_hash)
         if (e) hipEventDestroy(e);
     for (auto e : p->ev_go)
@@ -770,10 +792,10 @@ static int launch_walk_round(xc_plan *p, uint32_t j0, uint32_t j1, int use_d, in
 {
     hipStream_t s = p->cache->ctx->stream;
     // (k_resolve, always launched just before, reset GREW / FIRST_CROSS / SHADOW)
-    WalkArgs w{p->P, j0, j1, use_d, shadow};
+    WalkArgs w{p->P, j0, j1, use_d, shadow, p->max_decl};
     {
         KSpan span(p, XC_K_WALK);
-        hipLaunchKernelGGL(k_walk, dim3(j1 - j0), dim3(64), 0, s, w);
+        hipLaunchKernelGGL(k_walk, dim3(j1 - j0), dim3(64), walk_lds_bytes(p->max_decl), s, w);
         HIPCHK(hipGetLastError());
     }
     DeclArgs d{p->P, j0, j1};
@@ -805,6 +827,7 @@ static int launch_emit(xc_plan *p, uint32_t j0, uint32_t jc, uint32_t gate_sb = 
 static int enqueue_block_hash(xc_plan *p, uint32_t k, hipEvent_t after)
 {
     HIPCHK(hipStreamWaitEvent(p->hs, after, 0));
+    if (p->host_path) HIPCHK(hipStreamWaitEvent(p->hs, p->ev_h2d[k], 0));  // its input has landed
     DeclArgs d{p->P, p->sub[k], p->sub[k + 1]};
     {
         KSpan span(p, XC_K_BLOCKHASH, p->hs);
@@ -848,6 +871,19 @@ static int launch_first_round(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t s1,
     return launch_walk_round(p, j0, s1, 0, shadow);
 }
 
+// Host path: pack buffers [j0, j1) (emitted) to the caller's buffer.
+static int launch_pack(xc_plan *p, uint32_t j0, uint32_t j1)
+{
+    if (!p->host_path || j1 <= j0) return XC_OK;
+    hipStream_t s = p->cache->ctx->stream;
+    PackArgs a{p->P, j0, j1, p->pack_dst, p->pack_cap, p->e_total, p->e_pos};
+    hipLaunchKernelGGL(k_pack_offsets, dim3(1), dim3(1024), 0, s, a);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_pack_copy, dim3(j1 - j0), dim3(256), 0, s, a);
+    HIPCHK(hipGetLastError());
+    return XC_OK;
+}
+
 // Sub-batch sb with no host synchronisation: first round, gate, emit of the whole sub-batch.
 static int encode_sub_async(xc_plan *p, uint32_t sb)
 {
@@ -855,7 +891,8 @@ static int encode_sub_async(xc_plan *p, uint32_t sb)
     int rc;
     p->stats.sub_batches++;
     if ((rc = launch_first_round(p, sb, j0, s1, p->shadow))) return rc;
-    return launch_emit(p, j0, s1, sb);
+    if ((rc = launch_emit(p, j0, s1, sb))) return rc;
+    return launch_pack(p, j0, s1);
 }
 
 // Sub-batch sb step by step: declaration-growth rounds until D is closed, then emit up to the
@@ -919,6 +956,7 @@ extern "C" int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, ui
         // that sub-batch, step by step (its pipeline state is discarded and redone)
         if ((rc = encode_sub_sync(p, (uint32_t)si, ctl))) return rc;
         if (ctl[CTL_ERROR]) break;
+        if ((rc = launch_pack(p, p->sub[si], p->sub[si + 1]))) return rc;
         si++;
     }
     if ((rc = read_ctl(p, ctl))) return rc;
@@ -932,7 +970,71 @@ extern "C" int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, ui
         hipStreamSynchronize(s);
         return fail(XC_ENOSPC, "device cache capacity exhausted");
     }
+    if (ctl[CTL_ERROR] & ERR_PACK_CAP) return fail(XC_EINVAL, "packed output capacity too small");
     if (ctl[CTL_ERROR]) return fail(XC_EDEVICE, "internal encode error " + std::to_string(ctl[CTL_ERROR]));
+    return XC_OK;
+}
+
+extern "C" int xc_host_alloc(xc_ctx *ctx, uint64_t bytes, void **out)
+{
+    if (!ctx || !out) return fail(XC_EINVAL, "null");
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    HIPCHK(hipHostMalloc(out, std::max<uint64_t>(bytes, 1), hipHostMallocMapped | hipHostMallocPortable));
+    return XC_OK;
+}
+
+extern "C" int xc_host_free(void *ptr)
+{
+    if (ptr) HIPCHK(hipHostFree(ptr));
+    return XC_OK;
+}
+
+extern "C" int xc_encode_run_host(xc_plan *p, const uint8_t *h_in, uint8_t *h_out, uint64_t h_out_cap,
+                                  uint64_t *h_len, uint64_t *h_pos)
+{
+    if (!p || (p->nb && (!h_in || !h_out || !h_len))) return fail(XC_EINVAL, "null");
+    int rc = set_dev(p->cache->ctx);
+    if (rc) return rc;
+    hipStream_t s = p->cache->ctx->stream;
+    if (!p->e_in) {  // device arenas and the copy stream, kept for later runs
+        HIPCHK(hipMalloc(&p->e_in, p->in_bytes));
+        HIPCHK(hipMalloc(&p->e_out, p->out_bytes));
+        HIPCHK(hipMalloc(&p->e_len, std::max<uint64_t>(p->nb, 1) * 8));
+        HIPCHK(hipMalloc(&p->e_pos, std::max<uint64_t>(p->nb, 1) * 8));
+        HIPCHK(hipMalloc(&p->e_total, 8));
+        HIPCHK(hipStreamCreateWithFlags(&p->cs, hipStreamNonBlocking));
+        p->ev_h2d.assign(p->sub.size(), nullptr);
+        for (auto &e : p->ev_h2d) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    void *dev_out = nullptr;
+    if (hipHostGetDevicePointer(&dev_out, h_out, 0) != hipSuccess || !dev_out)
+        return fail(XC_EINVAL, "h_out is not pinned host memory (use xc_host_alloc)");
+    // every sub-batch's input on the copy stream, in order; sub-batch k's block hashing (the
+    // first kernel to read it) waits for its event
+    HIPCHK(hipEventRecord(p->ev_start, s));
+    HIPCHK(hipStreamWaitEvent(p->cs, p->ev_start, 0));
+    for (size_t k = 0; k + 1 < p->sub.size(); k++) {
+        const uint64_t a = p->nb ? p->in_off[p->sub[k]] : 0;
+        const uint64_t b = p->sub[k + 1] < p->nb ? p->in_off[p->sub[k + 1]] : p->in_bytes;
+        if (b > a) HIPCHK(hipMemcpyAsync(p->e_in + a, h_in + a, b - a, hipMemcpyHostToDevice, p->cs));
+        HIPCHK(hipEventRecord(p->ev_h2d[k], p->cs));
+    }
+    HIPCHK(hipMemsetAsync(p->e_total, 0, 8, s));
+    p->host_path = true;
+    p->pack_dst = (uint8_t *)dev_out;
+    p->pack_cap = h_out_cap;
+    rc = xc_encode_run(p, p->e_in, p->e_out, p->e_len);
+    p->host_path = false;
+    if (rc) {
+        hipStreamSynchronize(p->cs);
+        return rc;
+    }
+    if (p->nb) {
+        HIPCHK(hipMemcpyAsync(h_len, p->e_len, p->nb * 8, hipMemcpyDeviceToHost, s));
+        if (h_pos) HIPCHK(hipMemcpyAsync(h_pos, p->e_pos, p->nb * 8, hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
     return XC_OK;
 }
 

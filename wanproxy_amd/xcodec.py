@@ -29,7 +29,7 @@ SYMBOLS = [
     "xc_window_hashes", "xc_encode_plan_create", "xc_plan_destroy", "xc_plan_layout",
     "xc_encode_run", "xc_encode_batch_host", "xc_plan_stats", "xc_decode_batch_host",
     "xc_selftest", "xc_last_error", "xc_cache_restore_async", "xc_plan_set_timing",
-    "xc_plan_kernel_times",
+    "xc_plan_kernel_times", "xc_host_alloc", "xc_host_free", "xc_encode_run_host",
 ]
 
 KERNELS = ["scan", "resolve", "walk", "declhash", "emit", "blockhash"]
@@ -104,6 +104,9 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.xc_cache_restore_async.argtypes = [_vp]
     lib.xc_plan_set_timing.argtypes = [_vp, C.c_int]
     lib.xc_plan_kernel_times.argtypes = [_vp, C.POINTER(KernelTimes), C.c_int]
+    lib.xc_host_alloc.argtypes = [_vp, C.c_uint64, C.POINTER(_vp)]
+    lib.xc_host_free.argtypes = [_vp]
+    lib.xc_encode_run_host.argtypes = [_vp, _vp, _vp, C.c_uint64, _u64p, _u64p]
     _LIB = lib
     return lib
 
@@ -317,6 +320,15 @@ class EncodePlan:
     def run(self, d_in: int, d_out: int, d_len: int) -> None:
         _check(load_library().xc_encode_run(self.h, d_in, d_out, d_len))
 
+    def run_host(self, h_in: "HostBuffer", h_out: "HostBuffer"):
+        """End-to-end from host memory (xc_encode_run_host): ``h_in`` holds the input arena in
+        the plan's layout, the encoded streams come back packed in ``h_out``.  Returns
+        ``(lengths, positions)`` of every buffer's stream inside ``h_out``."""
+        lens = np.zeros(max(self.nbuf, 1), np.uint64)
+        pos = np.zeros(max(self.nbuf, 1), np.uint64)
+        _check(load_library().xc_encode_run_host(self.h, h_in.ptr, h_out.ptr, h_out.nbytes, lens, pos))
+        return lens[:self.nbuf], pos[:self.nbuf]
+
     def set_timing(self, enable: bool) -> None:
         _check(load_library().xc_plan_set_timing(self.h, 1 if enable else 0))
 
@@ -336,6 +348,38 @@ class EncodePlan:
         if getattr(self, "h", None):
             load_library().xc_plan_destroy(self.h)
             self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class HostBuffer:
+    """Pinned, device-mapped host memory (xc_host_alloc) viewed as a numpy uint8 array."""
+
+    def __init__(self, ctx: Context, nbytes: int):
+        self.ctx = ctx
+        self.nbytes = int(nbytes)
+        p = _vp()
+        _check(load_library().xc_host_alloc(ctx.h, self.nbytes, C.byref(p)))
+        self.ptr = p.value
+        self.array = np.ctypeslib.as_array((C.c_uint8 * max(self.nbytes, 1)).from_address(self.ptr))
+        _LIVE["plan"].add(self)  # released with the plans, before the context
+
+    def _ctx(self):
+        return self.ctx
+
+    @property
+    def cache(self):
+        return None
+
+    def close(self) -> None:
+        if getattr(self, "ptr", None):
+            self.array = None
+            load_library().xc_host_free(self.ptr)
+            self.ptr = None
 
     def __del__(self):
         try:
