@@ -619,6 +619,7 @@ __global__ __launch_bounds__(64) void k_walk(WalkArgs a)
     const PlanDev &P = a.P;
     const uint32_t b = a.j0 + blockIdx.x;
     if (b >= a.j1) return;
+    if (a.only_slow && !P.walk_slow[b]) return;  // k_walk_blocks walked it
     const uint32_t l = lane_id();
     const uint32_t len = P.buf_len[b];
     const uint8_t *base = P.in + P.buf_off[b];
@@ -766,6 +767,98 @@ __global__ __launch_bounds__(64) void k_walk(WalkArgs a)
         P.buf_nref[b] = n_ref;
         if (ntok > tcap) atomicOr(&P.ctl[CTL_ERROR], ERR_TOKENS);
         if (cross) atomicMin(&P.ctl[CTL_FIRST_CROSS], b);
+    }
+}
+
+// ----------------------------------------------------------- k_walk_blocks --------------
+// The first-round walk of a buffer whose events decide nothing between its aligned windows
+// (hit-free data and block-aligned repeats: every cfg workload), lane-parallel.  In k_walk's
+// state machine (xcodec_encoder.cc:77-170) a lookup with no candidate pending happens only at
+// aligned positions p_k = 2048k + 2047 as long as every aligned lookup either
+//   hits the cache with equal bytes -> REF of block k (the hash resets; next lookup p_{k+1}), or
+//   misses                          -> candidate = block k, declared at p_{k+1} = cand + 4095
+//                                      (or by flush() for the last block) just before p_{k+1}
+//                                      is looked up,
+// and every unaligned event in between is a plain miss (a lo32 match whose full hash is
+// absent: it changes nothing).  Then block k's token depends on the event at p_k alone.  The
+// reduction fails on a collision (the next candidate becomes unaligned), an unaligned event
+// that is a hit / collision / declaration match, a dense chunk, or a block repeating an earlier
+// new block of the same buffer (a self-REF that needs a byte compare; the declaration set's
+// min-merged value tells).  Such buffers are flagged in P.walk_slow for the sequential k_walk.
+__global__ __launch_bounds__(64) void k_walk_blocks(WalkArgs a)
+{
+    if (aborted(a.P)) return;
+    const PlanDev &P = a.P;
+    const uint32_t b = a.j0 + blockIdx.x;
+    if (b >= a.j1) return;
+    const uint32_t l = lane_id();
+    const uint32_t len = P.buf_len[b];
+    const uint32_t nblk = len / XC_SEG;
+    const uint32_t ck0 = P.buf_chunk0[b], ck1 = P.buf_chunk0[b + 1];
+    const uint32_t tb = P.tok_base[b];
+    bool ok = true, cross = false;
+    uint32_t n_ext = 0, n_ref = 0;
+    for (uint32_t c = ck0; c < ck1 && ballot(!ok) == 0; c++) {
+        const uint32_t cnt = uniform(P.S.cnt[c]);
+        const uint32_t c0 = (c - ck0) * P.chunk_len;
+        const uint32_t want = min(c0 + P.chunk_len, len) / XC_SEG - c0 / XC_SEG;  // aligned ends
+        if (cnt & EV_DENSE) { ok = false; break; }
+        bool aligned = false;
+        if (l < cnt) {
+            const uint32_t e = c * EV_CAP + l;
+            const uint32_t q = P.S.pos[e], st = P.S.stat[e];
+            aligned = ((q + 1u) & (XC_SEG - 1u)) == 0u;
+            if (!aligned) {
+                if (st != ST_MISS) ok = false;
+            } else {
+                const uint32_t k = q / XC_SEG;
+                const uint64_t h = P.S.h[e], v = P.S.val[e];
+                const uint32_t dpos = q + XC_SEG;  // declaration point cand + 4095
+                if (st == ST_COLL) ok = false;
+                if (st == ST_MATCH && (uint32_t)(v >> 32) == b && (uint32_t)v < dpos) ok = false;  // self-REF
+                if (st == ST_MATCH && (uint32_t)(v >> 32) < b) cross = true;
+                const uint32_t t = tb + k;
+                if (st == ST_EQUAL) {
+                    P.tok_op[t] = OP_REF;
+                    P.tok_known[t] = 1u;
+                    P.tok_dpos[t] = 0u;
+                    P.tok_h[t] = h;
+                    n_ref++;
+                } else {
+                    P.tok_op[t] = OP_EXTRACT;
+                    P.tok_known[t] = st == ST_MATCH ? 1u : 0u;
+                    P.tok_dpos[t] = dpos < len ? dpos : DPOS_FLUSH;
+                    P.tok_h[t] = st == ST_MATCH ? h : 0u;
+                    n_ext++;
+                }
+                P.tok_lb[t] = k * XC_SEG;
+                P.tok_le[t] = k * XC_SEG;
+                P.tok_seg[t] = k * XC_SEG;
+            }
+        }
+        if ((uint32_t)__popcll(ballot(aligned)) != want) ok = false;  // each aligned end, once
+    }
+    if (ballot(!ok)) {
+        if (l == 0) P.walk_slow[b] = 1u;
+        return;
+    }
+    n_ext = wave_sum(n_ext);
+    n_ref = wave_sum(n_ref);
+    const bool any_cross = ballot(cross) != 0;
+    if (l == 0) {
+        const uint32_t t = tb + nblk;  // END: the tail after the last block, escaped by flush()
+        P.tok_op[t] = OP_END;
+        P.tok_known[t] = 0u;
+        P.tok_lb[t] = nblk * XC_SEG;
+        P.tok_le[t] = len;
+        P.tok_seg[t] = 0u;
+        P.tok_dpos[t] = 0u;
+        P.tok_h[t] = 0u;
+        P.tok_cnt[b] = nblk + 1u;
+        P.buf_next[b] = n_ext;
+        P.buf_nref[b] = n_ref;
+        P.walk_slow[b] = 0u;
+        if (any_cross) atomicMin(&P.ctl[CTL_FIRST_CROSS], b);
     }
 }
 

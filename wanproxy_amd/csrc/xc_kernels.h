@@ -88,6 +88,7 @@ struct PlanDev {
     // skip the next block's windows and the walk verifies that the REF happened.
     uint32_t *blk_pref;
     const uint32_t *chunk_blk;  // [nchunks] global index of the chunk's buffer's block 0
+    uint32_t *walk_slow;        // [nb] k_walk_blocks left this buffer to the sequential walk
 };
 
 // kernel argument blocks (shared by xc_encode.hip and xc_runtime.hip)
@@ -120,6 +121,7 @@ struct WalkArgs {
     int use_d;  // 0 on the first round (no declaration layer yet)
     int shadow; // the scan skipped predicted-REF shadows: verify every such REF was emitted
     uint32_t max_decl;  // >= declarations of any buffer (longest buffer / 2048 + 2)
+    int only_slow;      // k_walk: only the buffers k_walk_blocks flagged in P.walk_slow
 };
 // dynamic LDS of k_walk
 __host__ __device__ constexpr uint32_t walk_lds_bytes(uint32_t max_decl) { return max_decl * 16u + 8u * (max_decl / 32u + 1u); }
@@ -150,6 +152,7 @@ __global__ void k_pack_offsets(PackArgs a);
 __global__ void k_pack_copy(PackArgs a);
 __global__ void k_resolve(ResolveArgs a);
 __global__ void k_walk(WalkArgs a);
+__global__ void k_walk_blocks(WalkArgs a);
 __global__ void k_declhash(DeclArgs a);
 __global__ void k_blockhash(DeclArgs a);
 __global__ void k_blockpredict(DeclArgs a);

@@ -647,6 +647,7 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     for (auto &e : p->ev_go) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (nbuf) HIPCHK(hipMemcpyAsync(p->d_blk_base, blk_base.data(), nbuf * 4, hipMemcpyHostToDevice, s));
     P.blk_base = p->d_blk_base;
+    HIPCHK(hipMalloc(&P.walk_slow, nb1 * 4));
     HIPCHK(hipMalloc(&P.buf_next, nb1 * 4));
     HIPCHK(hipMalloc(&P.buf_nref, nb1 * 4));
     HIPCHK(hipMalloc(&P.buf_slot, nb1 * 4));
@@ -686,6 +687,7 @@ extern "C" int xc_plan_destroy(xc_plan *p)
     hipFree(p->d_chunk_blk);
     hipFree(p->d_blk_base);
     hipFree(p->d_l2mix);
+    hipFree(p->P.walk_slow);
     hipFree(p->P.buf_next);
     hipFree(p->P.buf_nref);
     hipFree(p->P.buf_slot);
@@ -792,9 +794,15 @@ static int launch_walk_round(xc_plan *p, uint32_t j0, uint32_t j1, int use_d, in
 {
     hipStream_t s = p->cache->ctx->stream;
     // (k_resolve, always launched just before, reset GREW / FIRST_CROSS / SHADOW)
-    WalkArgs w{p->P, j0, j1, use_d, shadow, p->max_decl};
+    // first round: the block-parallel walk (k_walk_blocks), then the sequential walk for the
+    // buffers it flagged; later rounds (declaration layer) walk every buffer sequentially
+    WalkArgs w{p->P, j0, j1, use_d, shadow, p->max_decl, use_d ? 0 : 1};
     {
         KSpan span(p, XC_K_WALK);
+        if (!use_d) {
+            hipLaunchKernelGGL(k_walk_blocks, dim3(j1 - j0), dim3(64), 0, s, w);
+            HIPCHK(hipGetLastError());
+        }
         hipLaunchKernelGGL(k_walk, dim3(j1 - j0), dim3(64), walk_lds_bytes(p->max_decl), s, w);
         HIPCHK(hipGetLastError());
     }
