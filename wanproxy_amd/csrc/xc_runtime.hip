@@ -775,7 +775,12 @@ static int launch_scan(xc_plan *p, const Layer &L, const DevSet &set, uint32_t c
     if (p->timing) p->ktimes.scan_bytes += p->chunk_bytes[ck_hi] - p->chunk_bytes[ck_lo];
     uint32_t need = (ck_hi - ck_lo + SCAN_WAVES - 1) / SCAN_WAVES;
     uint32_t grid = std::min<uint32_t>(need, (uint32_t)ctx->n_cu);
-    hipLaunchKernelGGL(k_scan<0>, dim3(grid), dim3(64 * SCAN_WAVES), 0, ctx->stream, a);
+    // XC_SCAN_ABLATION=m (timing experiments only: results are wrong) runs k_scan<m> in the pipeline
+    static const int abl = getenv("XC_SCAN_ABLATION") ? atoi(getenv("XC_SCAN_ABLATION")) : 0;
+    auto kern = abl == 1 ? k_scan<1> : abl == 2 ? k_scan<2> : abl == 3 ? k_scan<3> : abl == 4 ? k_scan<4>
+              : abl == 5 ? k_scan<5> : k_scan<0>;
+    if (abl) a.mode = (uint32_t)abl;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * SCAN_WAVES), 0, ctx->stream, a);
     HIPCHK(hipGetLastError());
     return XC_OK;
 }
