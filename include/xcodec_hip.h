@@ -138,6 +138,38 @@ typedef struct {
 } xc_run_stats;
 int xc_plan_stats(xc_plan *p, xc_run_stats *st);
 
+/* ---- stateful streams: XCodecEncoder across calls (xcodec/xcodec_encoder.h:43-63) ----
+ *
+ * Stream state of a batch item (xc_plan_set_streams): buffer i is an encoder's pending source_
+ * (the reference's Buffer source_, xcodec/xcodec_encoder.h:47) followed by new input.
+ * start[i] = bytes of source_ (their window ends were looked up by earlier calls), cand[i] =
+ * the pending candidate_start_ (-1 = none), flags[i] & 1 = encode() only (no flush: the
+ * candidate and the trailing literals stay pending).  All three NULL = fresh encode + flush per
+ * buffer (the default).  After a run, xc_plan_stream_results gives the new source_ start
+ * base[i] (buffer offset; == length after a flush) and candidate cand[i] (buffer offset, -1). */
+int xc_plan_set_streams(xc_plan *p, const uint64_t *start, const int64_t *cand, const uint32_t *flags);
+int xc_plan_stream_results(xc_plan *p, uint64_t *base, int64_t *cand);
+
+typedef struct xc_encoder xc_encoder; /* XCodecEncoder: one per connection (xcodec_filter.h:43-48) */
+/* new XCodecEncoder(cache) (xcodec/xcodec_encoder.cc:43-49). */
+int xc_encoder_create(xc_cache *c, xc_encoder **out);
+int xc_encoder_destroy(xc_encoder *e);
+/* Bytes of source_ not yet emitted (an output of 2 * (pending + n) + 16 bytes always suffices). */
+int xc_encoder_pending(xc_encoder *e, uint64_t *bytes);
+/* XCodecEncoder::encode(out, in) (xcodec/xcodec_encoder.cc:60-173): out receives exactly the
+ * bytes the reference appends during this call. */
+int xc_encode(xc_encoder *e, const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len);
+/* XCodecEncoder::flush(out) (xcodec/xcodec_encoder.cc:175-201); *emitted = its bool result. */
+int xc_flush(xc_encoder *e, uint8_t *out, uint64_t cap, uint64_t *out_len, int *emitted);
+/* Cross-connection batch of calls, in the reference's single-thread order: call k is
+ * enc[k]->encode(in[k]) and, with flags[k] & XC_STREAM_FLUSH, enc[k]->flush() (EncodeFilter::consume
+ * without TO_BE_CONTINUED, xcodec/xcodec_filter.cc:146-160).  An encoder may appear in several
+ * calls.  Call k's output goes to out + out_off[k] (capacity out_cap[k]). */
+#define XC_STREAM_FLUSH 1
+int xc_encode_streams(xc_encoder *const *enc, const uint8_t *const *in, const uint64_t *in_len,
+                      const uint32_t *flags, uint64_t n, uint8_t *out, const uint64_t *out_off,
+                      const uint64_t *out_cap, uint64_t *out_len);
+
 /* ---- batch decode: XCodecDecoder::decode (xcodec/xcodec_decoder.cc:76-176) ----
  * status[i] = 1 (decode returned true) or 0 (false); consumed[i] = input bytes the
  * reference removes from its Buffer; has_unknown[i]/unknown[i] = the REF hash the

@@ -21,6 +21,10 @@ _u8p = np.ctypeslib.ndpointer(np.uint8, flags="C")
 _i32p = np.ctypeslib.ndpointer(np.int32, flags="C")
 
 
+class XoBytes(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("len", C.c_size_t), ("cap", C.c_size_t)]
+
+
 def build() -> None:
     subprocess.run(["make", "-s", "-C", HERE], check=True)
 
@@ -43,6 +47,13 @@ def _load() -> C.CDLL:
                                     _u64p, _u64p]
     lib.xo_decode_batch.argtypes = [C.c_void_p, _u8p, _u64p, _u64p, C.c_size_t, _u8p, _u64p,
                                     _u64p, _u64p, _u64p, _i32p, _u64p, _i32p]
+    lib.xo_encoder_new.restype = C.c_void_p
+    lib.xo_encoder_new.argtypes = [C.c_void_p]
+    lib.xo_encoder_free.argtypes = [C.c_void_p]
+    lib.xo_encode.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(XoBytes)]
+    lib.xo_flush.argtypes = [C.c_void_p, C.POINTER(XoBytes)]
+    lib.xo_flush.restype = C.c_int
+    lib.xo_bytes_free.argtypes = [C.POINTER(XoBytes)]
     lib.xo_encode_sharded_timed.restype = C.c_double
     lib.xo_encode_sharded_timed.argtypes = [C.c_void_p, _u8p, _u64p, _u64p, C.c_size_t, C.c_int,
                                             C.POINTER(C.c_uint64)]
@@ -156,6 +167,37 @@ class Cache:
 
 
 # -- the reference's own XCodecHash, compiled from its header (oracle/Makefile `ref`) --
+class Encoder:
+    """Stateful XCodecEncoder restatement (xcodec/xcodec_encoder.cc:43-201): encode() returns the
+    bytes one reference encode(out, in) call appends, flush() -> (bool, bytes)."""
+
+    def __init__(self, cache: Cache):
+        self.cache = cache  # keeps the cache alive
+        self.h = lib().xo_encoder_new(cache.h)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().xo_encoder_free(self.h)
+            self.h = None
+
+    @staticmethod
+    def _take(b: XoBytes) -> bytes:
+        out = C.string_at(b.data, b.len) if b.len else b""
+        lib().xo_bytes_free(C.byref(b))
+        return out
+
+    def encode(self, data) -> bytes:
+        d = np.ascontiguousarray(_as_u8(data))
+        b = XoBytes()
+        lib().xo_encode(self.h, d.ctypes.data if d.size else None, d.size, C.byref(b))
+        return self._take(b)
+
+    def flush(self) -> tuple[bool, bytes]:
+        b = XoBytes()
+        v = lib().xo_flush(self.h, C.byref(b))
+        return bool(v), self._take(b)
+
+
 def ref_hash_lib():
     if not os.path.exists(REF_HASH_PATH):
         return None

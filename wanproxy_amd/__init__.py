@@ -6,7 +6,9 @@ reference expansion) runs as hand-written gfx950 HIP kernels in
 """
 from . import workloads  # noqa: F401
 from .xcodec import (Context, EncodePlan, HostBuffer, XCodecCache, XCodecDecoder,  # noqa: F401
-                     XCodecEncoder, XCodecError, device_count, load_library)
+                     XCodecEncoder, XCodecError, XCodecStreamEncoder, device_count,
+                     encode_streams, load_library)
 
 __all__ = ["Context", "EncodePlan", "HostBuffer", "XCodecCache", "XCodecDecoder", "XCodecEncoder",
-           "XCodecError", "device_count", "load_library", "workloads"]
+           "XCodecError", "XCodecStreamEncoder", "device_count", "encode_streams", "load_library",
+           "workloads"]

@@ -635,6 +635,15 @@ __global__ __launch_bounds__(64) void k_walk(WalkArgs a)
     uint32_t cand_known = 0;
     uint32_t p = XC_SEG - 1u;
     bool cross = false;
+    bool noflush = false;
+    if (P.stream_st) {
+        // a stream's pending source_: window ends below start were looked up by earlier calls
+        // (xcodec_encoder.cc:72-118), a pending candidate carries over (its hash: k_declhash)
+        const uint4 st = P.stream_st[b];
+        p = max(p, uniform(st.x));
+        if (uniform(st.y) != NONE) cand = (int)uniform(st.y);
+        noflush = (uniform(st.z) & SF_NOFLUSH) != 0u;
+    }
 
     if (a.shadow)
         for (uint32_t i = l; i < a.max_decl / 32u + 1u; i += 64u) ref_done[i] = 0u;
@@ -693,6 +702,11 @@ __global__ __launch_bounds__(64) void k_walk(WalkArgs a)
         return R_MISS;
     };
 
+    if (cand >= 0) {  // the carried candidate's hash, when a resolved event supplies it
+        const uint32_t q = (uint32_t)cand + XC_SEG - 1u;
+        const EvInfo d = decl_info(q, event_at(P, P.S, cs, ck1, q, 2, b, base));
+        if (d.st == ST_MATCH) { cand_known = 1; cand_h = d.h; }
+    }
     while (p < len) {
         if (cand < 0) {
             uint64_t h = 0;
@@ -745,12 +759,19 @@ __global__ __launch_bounds__(64) void k_walk(WalkArgs a)
         cand = -1;
         p = dp;
     }
-    // flush (xcodec_encoder.cc:175-201)
-    if (cand >= 0) {
-        emit(OP_EXTRACT, basep, (uint32_t)cand, (uint32_t)cand, DPOS_FLUSH, cand_h, cand_known);
-        basep = (uint32_t)cand + XC_SEG;
+    if (noflush) {
+        // encode() returns here: the candidate and the bytes from basep stay in source_
+        if (l == 0) P.stream_res[b] = make_uint2(basep, cand >= 0 ? (uint32_t)cand : NONE);
+        emit(OP_END, basep, basep, 0, 0, 0, 0);
+    } else {
+        // flush (xcodec_encoder.cc:175-201)
+        if (cand >= 0) {
+            emit(OP_EXTRACT, basep, (uint32_t)cand, (uint32_t)cand, DPOS_FLUSH, cand_h, cand_known);
+            basep = (uint32_t)cand + XC_SEG;
+        }
+        emit(OP_END, basep, len, 0, 0, 0, 0);
+        if (P.stream_res && l == 0) P.stream_res[b] = make_uint2(len, NONE);
     }
-    emit(OP_END, basep, len, 0, 0, 0, 0);
     if (a.shadow) {
         // every predicted REF whose following block the scan skipped must have been emitted
         __syncthreads();
@@ -796,6 +817,10 @@ __global__ __launch_bounds__(64) void k_walk_blocks(WalkArgs a)
     const uint32_t nblk = len / XC_SEG;
     const uint32_t ck0 = P.buf_chunk0[b], ck1 = P.buf_chunk0[b + 1];
     const uint32_t tb = P.tok_base[b];
+    if (!stream_plain(P, b)) {  // carried state or no flush: the sequential walk
+        if (l == 0) P.walk_slow[b] = 1u;
+        return;
+    }
     bool ok = true, cross = false;
     uint32_t n_ext = 0, n_ref = 0;
     for (uint32_t c = ck0; c < ck1 && ballot(!ok) == 0; c++) {
@@ -858,6 +883,7 @@ __global__ __launch_bounds__(64) void k_walk_blocks(WalkArgs a)
         P.buf_next[b] = n_ext;
         P.buf_nref[b] = n_ref;
         P.walk_slow[b] = 0u;
+        if (P.stream_res) P.stream_res[b] = make_uint2(len, NONE);  // flushed: source_ empty
         if (any_cross) atomicMin(&P.ctl[CTL_FIRST_CROSS], b);
     }
 }
@@ -920,6 +946,10 @@ __global__ __launch_bounds__(64) void k_blockpredict(DeclArgs a)
     const uint32_t b = a.j0 + blockIdx.x;
     if (b >= a.j1) return;
     const uint32_t nblk = P.buf_len[b] / XC_SEG, bb = P.blk_base[b];
+    if (stream_carried(P, b)) {  // blocks relative to a carried source_: no predictions
+        for (uint32_t k = lane_id(); k < nblk; k += 64u) P.blk_pref[bb + k] = 0u;
+        return;
+    }
     for (uint32_t k = lane_id(); k < nblk; k += 64u) {
         const uint64_t h = P.blk_h[bb + k];
         uint64_t v;

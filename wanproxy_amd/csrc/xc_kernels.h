@@ -89,7 +89,30 @@ struct PlanDev {
     uint32_t *blk_pref;
     const uint32_t *chunk_blk;  // [nchunks] global index of the chunk's buffer's block 0
     uint32_t *walk_slow;        // [nb] k_walk_blocks left this buffer to the sequential walk
+    // Stateful streams (xc_encode / xc_flush, xcodec_encoder.cc:60-201 across calls), or null
+    // when every buffer is a fresh encoder's encode + flush.  stream_st[b] = {start, cand0,
+    // flags, 0}: the buffer is the encoder's pending source_ (start bytes, whose window ends
+    // were looked up by earlier calls, pending candidate cand0 or NONE) followed by the new
+    // input; flags & SF_NOFLUSH: encode() only, the trailing candidate and literals stay
+    // pending.  stream_res[b] = {base, cand}: the new source_ starts at base, the candidate.
+    const uint4 *stream_st;
+    uint2 *stream_res;
 };
+constexpr uint32_t SF_NOFLUSH = 1u;
+// A buffer with carried-over state (earlier positions already looked up, or a pending
+// candidate): the aligned-block predictions and REF shadows do not apply to it.
+__device__ __forceinline__ bool stream_carried(const PlanDev &P, uint32_t b)
+{
+    if (!P.stream_st) return false;
+    const uint4 st = P.stream_st[b];
+    return st.x != 0u || st.y != NONE;
+}
+__device__ __forceinline__ bool stream_plain(const PlanDev &P, uint32_t b)
+{
+    if (!P.stream_st) return true;
+    const uint4 st = P.stream_st[b];
+    return st.x == 0u && st.y == NONE && !(st.z & SF_NOFLUSH);
+}
 
 // kernel argument blocks (shared by xc_encode.hip and xc_runtime.hip)
 // Pipeline kernels exit at once when the async sub-batch pipeline has been stopped.

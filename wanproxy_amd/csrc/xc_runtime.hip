@@ -451,6 +451,8 @@ struct xc_plan {
     int shadow = 1;          // REF shadows in the async pass (XC_NO_SHADOW=1 disables)
     uint32_t max_decl = 2;   // longest buffer / 2048 + 2 (k_walk's LDS)
     uint32_t *d_chunk_blk = nullptr;
+    uint4 *d_stream_st = nullptr;  // stateful streams (xc_plan_set_streams), else null
+    uint2 *d_stream_res = nullptr;
 };
 
 static hipEvent_t ev_get(xc_plan *p)
@@ -692,6 +694,8 @@ extern "C" int xc_plan_destroy(xc_plan *p)
     hipFree(p->P.buf_nref);
     hipFree(p->P.buf_slot);
     hipFree(p->P.ctl);
+    hipFree(p->d_stream_st);
+    hipFree(p->d_stream_res);
     for (auto &x : p->ev_live) { hipEventDestroy(x.second.first); hipEventDestroy(x.second.second); }
     for (auto e : p->ev_pool) hipEventDestroy(e);
     if (p->hs) {
@@ -748,6 +752,54 @@ extern "C" int xc_plan_stats(xc_plan *p, xc_run_stats *st)
 {
     if (!p || !st) return fail(XC_EINVAL, "null");
     *st = p->stats;
+    return XC_OK;
+}
+
+extern "C" int xc_plan_set_streams(xc_plan *p, const uint64_t *start, const int64_t *cand, const uint32_t *flags)
+{
+    if (!p) return fail(XC_EINVAL, "null");
+    int rc = set_dev(p->cache->ctx);
+    if (rc) return rc;
+    hipStream_t s = p->cache->ctx->stream;
+    if (!start && !cand && !flags) {  // back to fresh encode + flush per buffer
+        p->P.stream_st = nullptr;
+        p->P.stream_res = nullptr;
+        return XC_OK;
+    }
+    std::vector<uint4> st(p->nb);
+    for (uint32_t i = 0; i < p->nb; i++) {
+        const uint64_t n = p->len[i], a = start ? start[i] : 0;
+        const int64_t c = cand ? cand[i] : -1;
+        // the reference's invariants between calls: the carried candidate's window is complete
+        // (c + 2048 <= start) and was not yet due for declaration (c + 4095 >= start)
+        if (a > n || (c >= 0 && ((uint64_t)c + XC_SEG > a || (uint64_t)c + 2 * XC_SEG - 1 < a)) || c < -1)
+            return fail(XC_EINVAL, "invalid stream state for buffer " + std::to_string(i));
+        st[i] = make_uint4((uint32_t)a, c < 0 ? NONE : (uint32_t)c, flags ? flags[i] & SF_NOFLUSH : 0u, 0u);
+    }
+    const size_t nb1 = std::max<uint32_t>(p->nb, 1);
+    if (!p->d_stream_st) {
+        HIPCHK(hipMalloc(&p->d_stream_st, nb1 * sizeof(uint4)));
+        HIPCHK(hipMalloc(&p->d_stream_res, nb1 * sizeof(uint2)));
+    }
+    if (p->nb) HIPCHK(hipMemcpyAsync(p->d_stream_st, st.data(), p->nb * sizeof(uint4), hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+    p->P.stream_st = p->d_stream_st;
+    p->P.stream_res = p->d_stream_res;
+    return XC_OK;
+}
+
+extern "C" int xc_plan_stream_results(xc_plan *p, uint64_t *base, int64_t *cand)
+{
+    if (!p || (p->nb && (!base || !cand))) return fail(XC_EINVAL, "null");
+    if (!p->P.stream_res) return fail(XC_EINVAL, "plan has no stream state (xc_plan_set_streams)");
+    int rc = set_dev(p->cache->ctx);
+    if (rc) return rc;
+    std::vector<uint2> r(p->nb);
+    if (p->nb) HIPCHK(hipMemcpy(r.data(), p->d_stream_res, p->nb * sizeof(uint2), hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < p->nb; i++) {
+        base[i] = r[i].x;
+        cand[i] = r[i].y == NONE ? -1 : (int64_t)r[i].y;
+    }
     return XC_OK;
 }
 
@@ -1051,15 +1103,24 @@ extern "C" int xc_encode_run_host(xc_plan *p, const uint8_t *h_in, uint8_t *h_ou
     return XC_OK;
 }
 
-extern "C" int xc_encode_batch_host(xc_cache *c, const uint8_t *in, const uint64_t *in_off, const uint64_t *in_len,
-                                    uint64_t nbuf, uint8_t *out, const uint64_t *out_off, const uint64_t *out_cap,
-                                    uint64_t *out_len)
+// Host-to-host batch, optionally with stream state (xc_stream.hip): start / cand / flags as in
+// xc_plan_set_streams, the resulting source_ base / candidate to rbase / rcand.
+extern "C" int xc__encode_batch_host_ex(xc_cache *c, const uint8_t *in, const uint64_t *in_off,
+                                        const uint64_t *in_len, uint64_t nbuf, uint8_t *out,
+                                        const uint64_t *out_off, const uint64_t *out_cap, uint64_t *out_len,
+                                        const uint64_t *start, const int64_t *cand, const uint32_t *flags,
+                                        uint64_t *rbase, int64_t *rcand)
 {
     if (!c || (nbuf && (!in || !in_off || !in_len || !out || !out_off || !out_cap || !out_len)))
         return fail(XC_EINVAL, "null");
     xc_plan *p = nullptr;
     int rc = xc_encode_plan_create(c, in_len, nbuf, &p);
     if (rc) return rc;
+    const bool streams = start || cand || flags;
+    if (streams && (rc = xc_plan_set_streams(p, start, cand, flags))) {
+        xc_plan_destroy(p);
+        return rc;
+    }
     hipStream_t s = c->ctx->stream;
     uint8_t *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
     uint64_t *d_len = nullptr;
@@ -1082,6 +1143,7 @@ extern "C" int xc_encode_batch_host(xc_cache *c, const uint8_t *in, const uint64
             if (lens[i] > out_cap[i]) { rc = fail(XC_EINVAL, "output capacity too small"); continue; }
             memcpy(out + out_off[i], h_out + p->out_off[i], lens[i]);
         }
+        if (!rc && streams && rbase && rcand) rc = xc_plan_stream_results(p, rbase, rcand);
     }
     hipHostFree(h_in);
     hipHostFree(h_out);
@@ -1090,6 +1152,14 @@ extern "C" int xc_encode_batch_host(xc_cache *c, const uint8_t *in, const uint64
     hipFree(d_len);
     xc_plan_destroy(p);
     return rc;
+}
+
+extern "C" int xc_encode_batch_host(xc_cache *c, const uint8_t *in, const uint64_t *in_off, const uint64_t *in_len,
+                                    uint64_t nbuf, uint8_t *out, const uint64_t *out_off, const uint64_t *out_cap,
+                                    uint64_t *out_len)
+{
+    return xc__encode_batch_host_ex(c, in, in_off, in_len, nbuf, out, out_off, out_cap, out_len, nullptr, nullptr,
+                                    nullptr, nullptr, nullptr);
 }
 
 // Internal accessors for xc_decode.hip (not part of the public header).

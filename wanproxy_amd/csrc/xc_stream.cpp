@@ -1,0 +1,179 @@
+// xc_stream.cpp — stateful XCodec stream encoders over the batch encoder (host side).
+//
+// Reference: XCodecEncoder (xcodec/xcodec_encoder.h:43-63, xcodec/xcodec_encoder.cc:43-201) as
+// EncodeFilter drives it (xcodec/xcodec_filter.cc:122-164): one encoder per connection, called
+// once per received buffer, flushed unless the caller marks the data TO_BE_CONTINUED.  Between
+// calls an encoder holds exactly its pending `source_` bytes and its candidate
+// (candidate_start_; candidate_symbol_ is the hash of the candidate's bytes), so that is the
+// state kept here.  A call becomes one buffer of a device batch: source_ followed by the new
+// input, with the window ends of source_ marked as already looked up (xc_plan_set_streams).
+//
+// Cross-connection batching: xc_encode_streams runs the calls of many encoders as one batch,
+// with the reference's single-threaded order (call k sees the cache after calls < k).  A batch
+// round holds each encoder at most once; a later call of the same encoder starts a new round.
+#include <algorithm>
+#include <new>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/xcodec_hip.h"
+
+extern "C" int xc__set_error(int code, const char *msg);
+extern "C" int xc__encode_batch_host_ex(xc_cache *c, const uint8_t *in, const uint64_t *in_off,
+                                        const uint64_t *in_len, uint64_t nbuf, uint8_t *out,
+                                        const uint64_t *out_off, const uint64_t *out_cap, uint64_t *out_len,
+                                        const uint64_t *start, const int64_t *cand, const uint32_t *flags,
+                                        uint64_t *rbase, int64_t *rcand);
+
+namespace {
+constexpr uint64_t MAX_BUFFER = 1u << 20;  // longest device batch item (xc_kernels.h MAX_BUF)
+constexpr uint32_t SF_NOFLUSH = 1u;        // xc_kernels.h
+}  // namespace
+
+struct xc_encoder {
+    xc_cache *cache;
+    std::vector<uint8_t> source;  // source_ (bytes not yet emitted)
+    int64_t cand = -1;            // candidate_start_, relative to source[0]
+};
+
+extern "C" int xc_encoder_create(xc_cache *c, xc_encoder **out)
+{
+    if (!c || !out) return xc__set_error(XC_EINVAL, "null");
+    *out = new xc_encoder{c, {}, -1};
+    return XC_OK;
+}
+
+extern "C" int xc_encoder_destroy(xc_encoder *e)
+{
+    delete e;
+    return XC_OK;
+}
+
+extern "C" int xc_encoder_pending(xc_encoder *e, uint64_t *bytes)
+{
+    if (!e || !bytes) return xc__set_error(XC_EINVAL, "null");
+    *bytes = e->source.size();
+    return XC_OK;
+}
+
+namespace {
+// One round: calls [i, j) of the request, each encoder once; the last call may be a prefix of
+// its input (`take` bytes from `done`), which then keeps its flush for a later round.
+struct Item {
+    uint64_t call, from, take;
+    bool flush;
+};
+}  // namespace
+
+static int encode_streams(xc_encoder *const *enc, const uint8_t *const *in, const uint64_t *in_len,
+                          const uint32_t *flags, uint64_t n, uint8_t *out, const uint64_t *out_off,
+                          const uint64_t *out_cap, uint64_t *out_len)
+{
+    if (n && (!enc || !in_len || !out || !out_off || !out_cap || !out_len)) return xc__set_error(XC_EINVAL, "null");
+    xc_cache *cache = n ? enc[0]->cache : nullptr;
+    for (uint64_t k = 0; k < n; k++) {
+        if (!enc[k]) return xc__set_error(XC_EINVAL, "null encoder");
+        if (enc[k]->cache != cache) return xc__set_error(XC_EINVAL, "encoders of one call must share a cache");
+        if (in_len[k] && (!in || !in[k])) return xc__set_error(XC_EINVAL, "null input");
+        out_len[k] = 0;
+    }
+    std::vector<uint64_t> done(n, 0);  // input bytes of call k consumed so far
+    uint64_t k0 = 0;
+    while (k0 < n) {
+        // build the round
+        std::vector<Item> items;
+        std::vector<const xc_encoder *> used;
+        for (uint64_t k = k0; k < n; k++) {
+            xc_encoder *e = enc[k];
+            if (std::find(used.begin(), used.end(), e) != used.end()) break;
+            const uint64_t pend = e->source.size();
+            if (pend >= MAX_BUFFER) return xc__set_error(XC_ENOSPC, "stream pending bytes exceed 1 MiB");
+            const uint64_t rest = in_len[k] - done[k];
+            const uint64_t take = std::min<uint64_t>(rest, MAX_BUFFER - pend);
+            const bool whole = take == rest;
+            items.push_back({k, done[k], take, whole && flags && (flags[k] & XC_STREAM_FLUSH)});
+            used.push_back(e);
+            if (!whole) break;  // the rest of this input is the next round's
+        }
+        const uint64_t m = items.size();
+        std::vector<uint64_t> ioff(m), ilen(m), ooff(m), ocap(m), olen(m), start(m), rbase(m);
+        std::vector<int64_t> cand(m), rcand(m);
+        std::vector<uint32_t> fl(m);
+        uint64_t isz = 0, osz = 0;
+        for (uint64_t i = 0; i < m; i++) {
+            const xc_encoder *e = enc[items[i].call];
+            ioff[i] = isz;
+            ilen[i] = e->source.size() + items[i].take;
+            isz += ilen[i];
+            ooff[i] = osz;
+            ocap[i] = 2 * ilen[i] + 16;
+            osz += ocap[i];
+            start[i] = e->source.size();
+            cand[i] = e->cand;
+            fl[i] = items[i].flush ? 0u : SF_NOFLUSH;
+        }
+        std::vector<uint8_t> arena(std::max<uint64_t>(isz, 1)), obuf(std::max<uint64_t>(osz, 1));
+        for (uint64_t i = 0; i < m; i++) {
+            const xc_encoder *e = enc[items[i].call];
+            std::copy(e->source.begin(), e->source.end(), arena.begin() + ioff[i]);
+            if (items[i].take)
+                std::copy(in[items[i].call] + items[i].from, in[items[i].call] + items[i].from + items[i].take,
+                          arena.begin() + ioff[i] + e->source.size());
+        }
+        int rc = xc__encode_batch_host_ex(cache, arena.data(), ioff.data(), ilen.data(), m, obuf.data(), ooff.data(),
+                                          ocap.data(), olen.data(), start.data(), cand.data(), fl.data(),
+                                          rbase.data(), rcand.data());
+        if (rc) return rc;
+        for (uint64_t i = 0; i < m; i++)
+            if (rbase[i] > ilen[i] || (rcand[i] >= 0 && ((uint64_t)rcand[i] < rbase[i] || (uint64_t)rcand[i] >= ilen[i])))
+                return xc__set_error(XC_EDEVICE, "inconsistent stream state from the device");
+        for (uint64_t i = 0; i < m; i++) {
+            const uint64_t k = items[i].call;
+            xc_encoder *e = enc[k];
+            if (out_len[k] + olen[i] > out_cap[k]) return xc__set_error(XC_EINVAL, "output capacity too small");
+            std::copy(obuf.begin() + ooff[i], obuf.begin() + ooff[i] + olen[i], out + out_off[k] + out_len[k]);
+            out_len[k] += olen[i];
+            // the new source_: the buffer from rbase on (empty after a flush)
+            std::vector<uint8_t> src(arena.begin() + ioff[i] + rbase[i], arena.begin() + ioff[i] + ilen[i]);
+            e->source.swap(src);
+            e->cand = rcand[i] < 0 ? -1 : rcand[i] - (int64_t)rbase[i];
+            done[k] += items[i].take;
+        }
+        // calls fully done advance the start of the next round
+        k0 = items.back().call + (done[items.back().call] == in_len[items.back().call] ? 1 : 0);
+    }
+    return XC_OK;
+}
+
+extern "C" int xc_encode_streams(xc_encoder *const *enc, const uint8_t *const *in, const uint64_t *in_len,
+                                 const uint32_t *flags, uint64_t n, uint8_t *out, const uint64_t *out_off,
+                                 const uint64_t *out_cap, uint64_t *out_len)
+{
+    try {  // no exception crosses the C ABI
+        return encode_streams(enc, in, in_len, flags, n, out, out_off, out_cap, out_len);
+    } catch (const std::bad_alloc &) {
+        return xc__set_error(XC_ENOMEM, "host allocation failed");
+    } catch (const std::exception &x) {
+        return xc__set_error(XC_EINVAL, x.what());
+    }
+}
+
+extern "C" int xc_encode(xc_encoder *e, const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap,
+                         uint64_t *out_len)
+{
+    const uint32_t fl = 0;
+    const uint64_t off = 0;
+    return xc_encode_streams(&e, &in, &n, &fl, 1, out, &off, &cap, out_len);
+}
+
+extern "C" int xc_flush(xc_encoder *e, uint8_t *out, uint64_t cap, uint64_t *out_len, int *emitted)
+{
+    if (!e) return xc__set_error(XC_EINVAL, "null");
+    const uint32_t fl = XC_STREAM_FLUSH;
+    const uint64_t zero = 0, off = 0;
+    const uint8_t *none = nullptr;
+    int rc = xc_encode_streams(&e, &none, &zero, &fl, 1, out, &off, &cap, out_len);
+    if (!rc && emitted) *emitted = *out_len > 0 ? 1 : 0;
+    return rc;
+}

@@ -30,7 +30,10 @@ SYMBOLS = [
     "xc_encode_run", "xc_encode_batch_host", "xc_plan_stats", "xc_decode_batch_host",
     "xc_selftest", "xc_last_error", "xc_cache_restore_async", "xc_plan_set_timing",
     "xc_plan_kernel_times", "xc_host_alloc", "xc_host_free", "xc_encode_run_host",
+    "xc_plan_set_streams", "xc_plan_stream_results", "xc_encoder_create", "xc_encoder_destroy",
+    "xc_encoder_pending", "xc_encode", "xc_flush", "xc_encode_streams",
 ]
+STREAM_FLUSH = 1  # XC_STREAM_FLUSH
 
 KERNELS = ["scan", "resolve", "walk", "declhash", "emit", "blockhash"]
 
@@ -107,6 +110,17 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.xc_host_alloc.argtypes = [_vp, C.c_uint64, C.POINTER(_vp)]
     lib.xc_host_free.argtypes = [_vp]
     lib.xc_encode_run_host.argtypes = [_vp, _vp, _vp, C.c_uint64, _u64p, _u64p]
+    _i64p = np.ctypeslib.ndpointer(np.int64, flags="C")
+    _u32p = np.ctypeslib.ndpointer(np.uint32, flags="C")
+    lib.xc_plan_set_streams.argtypes = [_vp, _u64p, _i64p, _u32p]
+    lib.xc_plan_stream_results.argtypes = [_vp, _u64p, _i64p]
+    lib.xc_encoder_create.argtypes = [_vp, C.POINTER(_vp)]
+    lib.xc_encoder_destroy.argtypes = [_vp]
+    lib.xc_encoder_pending.argtypes = [_vp, C.POINTER(C.c_uint64)]
+    lib.xc_encode.argtypes = [_vp, _u8p, C.c_uint64, _u8p, C.c_uint64, C.POINTER(C.c_uint64)]
+    lib.xc_flush.argtypes = [_vp, _u8p, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_int)]
+    lib.xc_encode_streams.argtypes = [C.POINTER(_vp), C.POINTER(C.c_void_p), _u64p, _u32p, C.c_uint64,
+                                      _u8p, _u64p, _u64p, _u64p]
     _LIB = lib
     return lib
 
@@ -266,6 +280,80 @@ class XCodecEncoder:
         _check(load_library().xc_encode_batch_host(self.cache.h, arena, offs, lens, len(bufs),
                                                    out, ooff, cap, olen))
         return [out[int(o):int(o) + int(n)].tobytes() for o, n in zip(ooff, olen)]
+
+
+class XCodecStreamEncoder:
+    """XCodecEncoder across calls (xcodec/xcodec_encoder.h:43-63): one per connection, holding
+    the reference's state between calls (pending source_ bytes and the candidate).
+
+    ``encode(data)`` returns exactly the bytes the reference's ``encode(out, in)`` appends;
+    ``flush()`` returns ``(bool, bytes)`` like ``flush(out)``.  :func:`encode_streams` runs the
+    calls of many encoders as one device batch."""
+
+    def __init__(self, cache: XCodecCache):
+        self.cache = cache
+        self.h = _vp()
+        _check(load_library().xc_encoder_create(cache.h, C.byref(self.h)))
+        _LIVE["plan"].add(self)
+
+    def _ctx(self):
+        return self.cache.ctx
+
+    @property
+    def pending(self) -> int:
+        n = C.c_uint64()
+        _check(load_library().xc_encoder_pending(self.h, C.byref(n)))
+        return n.value
+
+    def encode(self, data) -> bytes:
+        return encode_streams([(self, data, False)])[0]
+
+    def flush(self) -> tuple[bool, bytes]:
+        cap = 2 * self.pending + 16
+        out = np.zeros(cap, np.uint8)
+        n, em = C.c_uint64(), C.c_int()
+        _check(load_library().xc_flush(self.h, out, cap, C.byref(n), C.byref(em)))
+        return bool(em.value), out[:n.value].tobytes()
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            load_library().xc_encoder_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def encode_streams(calls) -> list[bytes]:
+    """Cross-connection batch (xc_encode_streams): ``calls`` is a sequence of
+    ``(encoder, data, flush)``, run in order as ``encoder.encode(data)`` then, when ``flush``,
+    ``encoder.flush()`` (EncodeFilter::consume, xcodec/xcodec_filter.cc:122-164).  Returns each
+    call's output bytes."""
+    calls = list(calls)
+    n = len(calls)
+    if n == 0:
+        return []
+    datas = [_as_u8(d) for _, d, _ in calls]
+    lens = np.array([d.size for d in datas], np.uint64)
+    flags = np.array([STREAM_FLUSH if f else 0 for _, _, f in calls], np.uint32)
+    # output bound: pending bytes at the call (at most all earlier input of that encoder)
+    pend = {}
+    cap = np.zeros(n, np.uint64)
+    for k, (e, _, _) in enumerate(calls):
+        p = pend.get(id(e), e.pending) + int(lens[k])
+        cap[k] = 2 * p + 16
+        pend[id(e)] = p
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(cap)[:-1]
+    out = np.zeros(int(cap.sum()), np.uint8)
+    olen = np.zeros(n, np.uint64)
+    encs = (_vp * n)(*[e.h for e, _, _ in calls])
+    ptrs = (C.c_void_p * n)(*[d.ctypes.data if d.size else None for d in datas])
+    _check(load_library().xc_encode_streams(encs, ptrs, lens, flags, n, out, off, cap, olen))
+    return [out[int(o):int(o) + int(m)].tobytes() for o, m in zip(off, olen)]
 
 
 class XCodecDecoder:
