@@ -180,6 +180,28 @@ int xc_decode_batch_host(xc_cache *c, const uint8_t *in, const uint64_t *in_off,
                          uint64_t *consumed, int32_t *status, uint64_t *unknown,
                          int32_t *has_unknown);
 
+/* Device-resident decode: a plan fixes the stream lengths and output capacities of a batch and
+ * owns the device workspace.  Input arena: stream j at in_off[j]; output arena: stream j's bytes
+ * at out_off[j] (capacity out_cap[j]).  xc_decode_run takes device arenas in that layout and
+ * device arrays of nbuf results (same meaning as xc_decode_batch_host's); it returns once the
+ * batch is decoded (one host round trip decides the provider rounds). */
+typedef struct xc_dplan xc_dplan;
+typedef struct {
+    uint64_t in_bytes;   /* encoded bytes of the batch */
+    uint64_t n_extract;  /* EXTRACT tokens executed */
+    uint64_t n_ref;      /* REF tokens executed */
+    uint64_t n_entered;  /* segments entered into the cache (xcodec_decoder.cc:133-135) */
+    uint32_t rounds;     /* provider resolution rounds */
+} xc_decode_stats;
+int xc_decode_plan_create(xc_cache *c, const uint64_t *in_len, const uint64_t *out_cap, uint64_t nbuf,
+                          xc_dplan **out);
+int xc_dplan_destroy(xc_dplan *p);
+int xc_dplan_layout(xc_dplan *p, uint64_t *in_off, uint64_t *out_off, uint64_t *in_bytes,
+                    uint64_t *out_bytes);
+int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_out_len,
+                  uint64_t *d_consumed, int32_t *d_status, uint64_t *d_unknown, int32_t *d_has_unknown);
+int xc_dplan_stats(xc_dplan *p, xc_decode_stats *st);
+
 /* Library self-test of the wave primitives on device (returns XC_OK or a negative code). */
 int xc_selftest(xc_ctx *ctx);
 

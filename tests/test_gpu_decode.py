@@ -116,3 +116,53 @@ def test_gpu_encode_gpu_decode_roundtrip(gpu_ctx):
     assert [g[1] for g in got] == [b.tobytes() for b in bufs]
     assert all(g[0] == 1 and g[3] is None for g in got)
     assert len(ec) == len(dc)
+
+
+def test_device_resident_decode_plan(gpu_ctx, oracle_mod):
+    """xc_decode_plan_create + xc_decode_run on HBM arenas, run twice over a restored cache
+    snapshot (the bench's step): same results as the oracle both times."""
+    import torch
+    import wanproxy_amd as w
+    pool = W.pool(256)
+    warm = [pool[i:i + 65536] for i in range(0, len(pool), 65536)]
+    bufs = W.repeat_buffers(96, 0x77, 50, np_segments=256, pool_bytes=pool)
+    eo = oracle_mod.Cache()
+    warm_streams = eo.encode_batch(warm)
+    streams = eo.encode_batch(bufs)
+    streams.append(streams[3][:1000] + b"\xf1\x02" + bytes(8))  # unknown REF (stops the stream)
+    streams.append(b"")
+    oc = oracle_mod.Cache()
+    oc.decode_batch(warm_streams)
+    want = oc.decode_batch(streams)
+    gc = w.XCodecCache(gpu_ctx, 1 << 14)
+    w.XCodecDecoder(gc).decode_batch(warm_streams)
+    gc.snapshot()
+    lens = np.array([len(s) for s in streams], np.uint64)
+    caps = lens * 205 + 16
+    plan = w.DecodePlan(gc, lens, caps)
+    arena = np.zeros(plan.in_bytes, np.uint8)
+    for i, s in enumerate(streams):
+        arena[int(plan.in_off[i]):int(plan.in_off[i]) + len(s)] = np.frombuffer(s, np.uint8)
+    n = len(streams)
+    d_in = torch.from_numpy(arena).cuda()
+    d_out = torch.zeros(plan.out_bytes, dtype=torch.uint8, device="cuda")
+    u64 = torch.zeros(3 * n, dtype=torch.int64, device="cuda")
+    i32 = torch.zeros(2 * n, dtype=torch.int32, device="cuda")
+    for rep in range(2):
+        gc.restore()
+        torch.cuda.synchronize()
+        plan.run(d_in.data_ptr(), d_out.data_ptr(), u64.data_ptr(), u64.data_ptr() + 8 * n,
+                 i32.data_ptr(), u64.data_ptr() + 16 * n, i32.data_ptr() + 4 * n)
+        torch.cuda.synchronize()
+        out = d_out.cpu().numpy()
+        r64 = u64.cpu().numpy().astype(np.uint64)
+        r32 = i32.cpu().numpy()
+        for i, (st, data, cons, unk) in enumerate(want):
+            o = int(plan.out_off[i])
+            assert int(r32[i]) == st, (rep, i, "status")
+            assert int(r64[n + i]) == cons, (rep, i, "consumed")
+            assert (int(r64[2 * n + i]) if r32[n + i] else None) == unk, (rep, i, "unknown")
+            assert out[o:o + int(r64[i])].tobytes() == data, (rep, i, "bytes")
+        assert len(gc) == len(oc)
+    st = plan.stats()
+    assert st.n_entered > 0 and st.n_ref > 0 and st.rounds >= 1

@@ -57,9 +57,10 @@ struct DecDev {
     uint2 *undo;
     DevSet dset;
     uint32_t *ctl;
+    int count;                 // k_dstop: count executed REF / EXTRACT tokens into ctl
 };
 
-enum : uint32_t { DCTL_FIX = 0, DCTL_ERR = 1, DCTL_NENTER = 2 };
+enum : uint32_t { DCTL_FIX = 0, DCTL_ERR = 1, DCTL_NENTER = 2, DCTL_NREF = 3, DCTL_NEXTRACT = 4, DCTL_WORDS = 8 };
 
 // First F1 at or after p in [p, n), or n.
 __device__ __forceinline__ uint32_t find_magic(const uint8_t *s, uint32_t p, uint32_t n)
@@ -227,6 +228,16 @@ __global__ __launch_bounds__(64) void k_dstop(DecDev D)
     }
     // t = stopping token (terminal, unknown REF or colliding EXTRACT); its literal is output
     D.s_stop[j] = t + 1u;
+    if (D.count) {  // executed REF / EXTRACT tokens (decode statistics)
+        uint32_t nr = 0, ne = 0;
+        for (uint32_t k = 0; k < t; k++) {
+            const uint32_t o = D.t_op[tb + k];
+            nr += o == T_REF ? 1u : 0u;
+            ne += o == T_EXTRACT ? 1u : 0u;
+        }
+        if (nr) atomicAdd(&D.ctl[DCTL_NREF], nr);  // (lanes past ns have returned: no wave sums)
+        if (ne) atomicAdd(&D.ctl[DCTL_NEXTRACT], ne);
+    }
     const uint32_t op = D.t_op[tb + t], st = D.t_stat[tb + t], le = D.t_le[tb + t];
     int32_t status = 1, hu = 0;
     uint64_t cons = le, unk = 0;
@@ -429,21 +440,226 @@ __global__ __launch_bounds__(64) void k_dcommit(DecDev D)
 using namespace xc;
 
 // ------------------------------------------------------------------ host side ----------
+// A decode plan (xc_dplan) fixes the stream lengths and output capacities of a batch and owns
+// every device array, so xc_decode_run is device resident: one host round trip to decide the
+// provider rounds (normally a single round), none for allocation.
+//
+// Token capacity: every EXTRACT / REF token consumes >= 10 input bytes and a stream ends in one
+// terminal token (END / WAIT / bad op), so a stream of n bytes has <= n/10 + 1 tokens; the
+// tokenizer writes them straight into per-stream slices (no counting pass).  Only EXTRACTs
+// (>= 2050 bytes each) enter the batch provider table, which is sized by that bound.
+
 // The cache object is defined in xc_runtime.hip; these accessors expose what we need.
 extern "C" int xc__cache_devset(xc_cache *c, void *devset, uint8_t **segs, uint32_t **count, uint32_t *cap,
                                 uint2 **undo, void **stream, int *dev);
 extern "C" int xc__set_error(int code, const char *msg);
 
-#define DCHK(x)                                                                        \
-    do {                                                                               \
-        hipError_t e_ = (x);                                                           \
-        if (e_ != hipSuccess) { rc = xc__set_error(XC_EDEVICE, hipGetErrorString(e_)); goto done; } \
+#define DHIP(x)                                                                          \
+    do {                                                                                 \
+        hipError_t e_ = (x);                                                             \
+        if (e_ != hipSuccess) return xc__set_error(XC_EDEVICE, hipGetErrorString(e_));   \
     } while (0)
 
 template <class T>
 static hipError_t dalloc(T **p, size_t n)
 {
     return hipMalloc((void **)p, std::max<size_t>(n, 1) * sizeof(T));
+}
+
+struct xc_dplan {
+    xc_cache *cache = nullptr;
+    hipStream_t s = nullptr;
+    int dev = 0;
+    uint32_t ns = 0;
+    std::vector<uint64_t> ioff, ooff;
+    uint64_t in_bytes = 0, out_bytes = 0, in_total = 0, ntok = 0;
+    uint32_t n_full = 0, n_lo = 0;
+    DecDev D{};
+    xc_decode_stats stats{};
+    std::vector<void *> owned;
+    template <class T>
+    int alloc(T **p, size_t n)
+    {
+        if (dalloc(p, n) != hipSuccess) return xc__set_error(XC_ENOMEM, "device allocation failed");
+        owned.push_back((void *)*p);
+        return XC_OK;
+    }
+};
+
+extern "C" int xc_dplan_destroy(xc_dplan *p)
+{
+    if (!p) return XC_OK;
+    hipSetDevice(p->dev);
+    hipStreamSynchronize(p->s);
+    for (void *x : p->owned) hipFree(x);
+    delete p;
+    return XC_OK;
+}
+
+extern "C" int xc_decode_plan_create(xc_cache *c, const uint64_t *in_len, const uint64_t *out_cap, uint64_t nbuf,
+                                     xc_dplan **out)
+{
+    if (!c || !out || (nbuf && (!in_len || !out_cap))) return xc__set_error(XC_EINVAL, "null");
+    if (nbuf > (1u << 24)) return xc__set_error(XC_EINVAL, "too many streams");
+    xc_dplan *p = new xc_dplan();
+    DecDev &D = p->D;
+    void *streamv = nullptr;
+    uint32_t cap = 0;
+    int rc = xc__cache_devset(c, &D.cache, &D.segs, &D.seg_count, &cap, &D.undo, &streamv, &p->dev);
+    if (rc) { delete p; return rc; }
+    p->cache = c;
+    p->s = (hipStream_t)streamv;
+    D.seg_cap = cap;
+    const uint32_t ns = (uint32_t)nbuf;
+    p->ns = D.ns = ns;
+    p->ioff.resize(ns);
+    p->ooff.resize(ns);
+    std::vector<uint32_t> ilen(ns), tbase(ns);
+    uint64_t itot = 0, otot = 0, ntok = 0, nprov = 0;
+    for (uint32_t j = 0; j < ns; j++) {
+        if (in_len[j] > 0xFFFFFF00ull) { xc_dplan_destroy(p); return xc__set_error(XC_EINVAL, "stream too long"); }
+        p->ioff[j] = itot;
+        itot += (in_len[j] + 255) / 256 * 256;
+        p->in_total += in_len[j];
+        ilen[j] = (uint32_t)in_len[j];
+        p->ooff[j] = otot;
+        otot += (out_cap[j] + 255) / 256 * 256;
+        tbase[j] = (uint32_t)ntok;
+        ntok += in_len[j] / 10 + 2;
+        nprov += in_len[j] / (XC_SEG + 2) + 1;
+    }
+    if (ntok > 0xFFFFFFF0ull) { xc_dplan_destroy(p); return xc__set_error(XC_EINVAL, "batch too large"); }
+    p->in_bytes = itot + 4096;  // the tokenizer's 256-byte windows read past a stream's end
+    p->out_bytes = otot + 256;
+    p->ntok = ntok;
+    p->n_full = 1024;
+    while (p->n_full < 2 * nprov + 2) p->n_full <<= 1;
+    p->n_lo = 1024;
+    while (p->n_lo < 4 * nprov + 4) p->n_lo <<= 1;
+    uint64_t *d_ioff, *d_ooff, *d_ocap;
+    uint32_t *d_ilen, *d_tbase;
+#define DA(ptr, n) if ((rc = p->alloc(ptr, n))) { xc_dplan_destroy(p); return rc; }
+    if (hipSetDevice(p->dev) != hipSuccess) { xc_dplan_destroy(p); return xc__set_error(XC_EDEVICE, "hipSetDevice"); }
+    DA(&d_ioff, ns); DA(&d_ooff, ns); DA(&d_ocap, ns); DA(&d_ilen, ns); DA(&d_tbase, ns);
+    DA(&D.tok_cnt, ns); DA(&D.s_stop, ns); DA(&D.s_slot, ns); DA(&D.s_lim, ns); DA(&D.ctl, DCTL_WORDS);
+    DA(&D.t_lb, ntok); DA(&D.t_le, ntok); DA(&D.t_op, ntok); DA(&D.t_stat, ntok); DA(&D.t_h, ntok);
+    DA(&D.t_src, ntok);
+    DevSet &ds = D.dset;
+    DA(&ds.filt, XC_FILT_WORDS); DA(&ds.l2, 2 * (size_t)XC_L2_WORDS); DA(&ds.lo_keys, p->n_lo);
+    DA(&ds.lo_zero, 1); DA(&ds.keys, p->n_full); DA(&ds.vals, p->n_full);
+#undef DA
+    ds.mask = p->n_full - 1;
+    ds.lo_mask = p->n_lo - 1;
+    const hipStream_t s = p->s;
+    if (ns) {
+        DHIP(hipMemcpyAsync(d_ioff, p->ioff.data(), ns * 8, hipMemcpyHostToDevice, s));
+        DHIP(hipMemcpyAsync(d_ooff, p->ooff.data(), ns * 8, hipMemcpyHostToDevice, s));
+        DHIP(hipMemcpyAsync(d_ocap, out_cap, ns * 8, hipMemcpyHostToDevice, s));
+        DHIP(hipMemcpyAsync(d_ilen, ilen.data(), ns * 4, hipMemcpyHostToDevice, s));
+        DHIP(hipMemcpyAsync(d_tbase, tbase.data(), ns * 4, hipMemcpyHostToDevice, s));
+    }
+    DHIP(hipStreamSynchronize(s));
+    D.in_off = d_ioff;
+    D.in_len = d_ilen;
+    D.tok_base = d_tbase;
+    D.out_off = d_ooff;
+    D.out_cap = d_ocap;
+    D.count = 1;
+    *out = p;
+    return XC_OK;
+}
+
+extern "C" int xc_dplan_layout(xc_dplan *p, uint64_t *in_off, uint64_t *out_off, uint64_t *in_bytes,
+                               uint64_t *out_bytes)
+{
+    if (!p) return xc__set_error(XC_EINVAL, "null");
+    if (in_off) std::copy(p->ioff.begin(), p->ioff.end(), in_off);
+    if (out_off) std::copy(p->ooff.begin(), p->ooff.end(), out_off);
+    if (in_bytes) *in_bytes = p->in_bytes;
+    if (out_bytes) *out_bytes = p->out_bytes;
+    return XC_OK;
+}
+
+extern "C" int xc_dplan_stats(xc_dplan *p, xc_decode_stats *st)
+{
+    if (!p || !st) return xc__set_error(XC_EINVAL, "null");
+    *st = p->stats;
+    return XC_OK;
+}
+
+extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_out_len,
+                             uint64_t *d_consumed, int32_t *d_status, uint64_t *d_unknown, int32_t *d_has_unknown)
+{
+    if (!p) return xc__set_error(XC_EINVAL, "null");
+    const uint32_t ns = p->ns;
+    if (ns == 0) return XC_OK;
+    if (!d_in || !d_out || !d_out_len || !d_consumed || !d_status || !d_unknown || !d_has_unknown)
+        return xc__set_error(XC_EINVAL, "null");
+    DHIP(hipSetDevice(p->dev));
+    DecDev D = p->D;
+    D.in = d_in;
+    D.out = d_out;
+    D.out_len = d_out_len;
+    D.consumed = d_consumed;
+    D.status = d_status;
+    D.unknown = d_unknown;
+    D.has_unknown = d_has_unknown;
+    const hipStream_t s = p->s;
+    DevSet &ds = D.dset;
+    uint32_t ctl[DCTL_WORDS] = {};
+    int rounds = 0;
+    DHIP(hipMemsetAsync(D.ctl, 0, DCTL_WORDS * 4, s));
+    hipLaunchKernelGGL(k_dtok, dim3(ns), dim3(64), 0, s, D, 1);
+    DHIP(hipGetLastError());
+    hipLaunchKernelGGL(k_dhash, dim3(ns, 8), dim3(64), 0, s, D);
+    DHIP(hipGetLastError());
+    hipLaunchKernelGGL(k_dlim, dim3((ns + 255) / 256), dim3(256), 0, s, D, 1);
+    DHIP(hipGetLastError());
+    for (;;) {
+        DHIP(hipMemsetAsync(ds.filt, 0, XC_FILT_WORDS * 4, s));
+        DHIP(hipMemsetAsync(ds.l2, 0, (size_t)XC_L2_WORDS * 8, s));
+        DHIP(hipMemsetAsync(ds.lo_keys, 0, (size_t)p->n_lo * 4, s));
+        DHIP(hipMemsetAsync(ds.lo_zero, 0, 4, s));
+        DHIP(hipMemsetAsync(ds.keys, 0xFF, (size_t)p->n_full * 8, s));
+        DHIP(hipMemsetAsync(ds.vals, 0xFF, (size_t)p->n_full * 8, s));
+        DHIP(hipMemsetAsync(D.ctl, 0, 4, s));                                    // DCTL_FIX
+        DHIP(hipMemsetAsync(D.ctl + DCTL_NREF, 0, 8, s));                        // counters
+        hipLaunchKernelGGL(k_dres1, dim3(ns, 8), dim3(64), 0, s, D);
+        DHIP(hipGetLastError());
+        hipLaunchKernelGGL(k_dres2, dim3(ns, 8), dim3(64), 0, s, D);
+        DHIP(hipGetLastError());
+        hipLaunchKernelGGL(k_dstop, dim3((ns + 63) / 64), dim3(64), 0, s, D);
+        DHIP(hipGetLastError());
+        hipLaunchKernelGGL(k_dcheck, dim3(ns), dim3(64), 0, s, D, rounds);
+        DHIP(hipGetLastError());
+        DHIP(hipMemcpyAsync(ctl, D.ctl, DCTL_WORDS * 4, hipMemcpyDeviceToHost, s));
+        DHIP(hipStreamSynchronize(s));
+        if (!ctl[DCTL_FIX]) break;
+        hipLaunchKernelGGL(k_dlim, dim3((ns + 255) / 256), dim3(256), 0, s, D, 0);
+        DHIP(hipGetLastError());
+        if (++rounds > 64) return xc__set_error(XC_EDEVICE, "decode provider resolution did not converge");
+    }
+    hipLaunchKernelGGL(k_demit, dim3(ns), dim3(256), 0, s, D);
+    DHIP(hipGetLastError());
+    hipLaunchKernelGGL(k_dalloc, dim3(1), dim3(1024), 0, s, D);
+    DHIP(hipGetLastError());
+    hipLaunchKernelGGL(k_dcommit, dim3(ns), dim3(64), 0, s, D);
+    DHIP(hipGetLastError());
+    DHIP(hipMemcpyAsync(ctl, D.ctl, DCTL_WORDS * 4, hipMemcpyDeviceToHost, s));
+    DHIP(hipStreamSynchronize(s));
+    p->stats.in_bytes = p->in_total;
+    p->stats.n_ref = ctl[DCTL_NREF];
+    p->stats.n_extract = ctl[DCTL_NEXTRACT];
+    p->stats.n_entered = ctl[DCTL_NENTER];
+    p->stats.rounds = (uint32_t)rounds + 1u;
+    if (ctl[DCTL_ERR] & 2u) {
+        const uint32_t c = D.seg_cap;  // the committed prefix stays; the count is clamped
+        hipMemcpyAsync(D.seg_count, &c, 4, hipMemcpyHostToDevice, s);
+        hipStreamSynchronize(s);
+        return xc__set_error(XC_ENOSPC, "device cache capacity exhausted");
+    }
+    if (ctl[DCTL_ERR] & 1u) return xc__set_error(XC_EINVAL, "output capacity too small");
+    return XC_OK;
 }
 
 extern "C" int xc_decode_batch_host(xc_cache *c, const uint8_t *in, const uint64_t *in_off, const uint64_t *in_len,
@@ -455,203 +671,50 @@ extern "C" int xc_decode_batch_host(xc_cache *c, const uint8_t *in, const uint64
                         !status || !unknown || !has_unknown)))
         return xc__set_error(XC_EINVAL, "null");
     if (nbuf == 0) return XC_OK;
-    if (nbuf > (1u << 24)) return xc__set_error(XC_EINVAL, "too many streams");
-    DecDev D{};
-    void *streamv = nullptr;
-    int dev = 0;
-    uint32_t cap = 0;
-    int rc = xc__cache_devset(c, &D.cache, &D.segs, &D.seg_count, &cap, &D.undo, &streamv, &dev);
+    xc_dplan *p = nullptr;
+    int rc = xc_decode_plan_create(c, in_len, out_cap, nbuf, &p);
     if (rc) return rc;
-    D.seg_cap = cap;
-    hipStream_t s = (hipStream_t)streamv;
-    const uint32_t ns = (uint32_t)nbuf;
-    D.ns = ns;
-    std::vector<uint64_t> ioff(ns), ooff(ns);
-    std::vector<uint32_t> ilen(ns), tcnt(ns), tbase(ns);
-    uint64_t itot = 0, otot = 0, ntok = 0;
-    for (uint32_t j = 0; j < ns; j++) {
-        if (in_len[j] > 0xFFFFFFF0ull) return xc__set_error(XC_EINVAL, "stream too long");
-        ioff[j] = itot;
-        itot += (in_len[j] + 255) / 256 * 256;
-        ilen[j] = (uint32_t)in_len[j];
-        ooff[j] = otot;
-        otot += (out_cap[j] + 255) / 256 * 256;
-    }
-    uint8_t *d_in = nullptr, *h_in = nullptr, *d_out = nullptr, *h_out = nullptr;
-    uint64_t *d_ioff = nullptr, *d_ooff = nullptr, *d_ocap = nullptr, *d_olen = nullptr, *d_cons = nullptr,
-             *d_unk = nullptr;
-    uint32_t *d_ilen = nullptr, *d_tbase = nullptr, *d_tcnt = nullptr, *d_stop = nullptr, *d_slot = nullptr,
-             *d_ctl = nullptr, *d_lim = nullptr;
-    int32_t *d_st = nullptr, *d_hu = nullptr;
-    DevSet &ds = D.dset;
-    uint32_t n_full = 0, n_lo = 0;
-    uint32_t ctl[4] = {0, 0, 0, 0};
-    std::vector<uint64_t> olen(ns), cons(ns), unk(ns);
-    std::vector<int32_t> st(ns), hu(ns);
-    int rounds = 0;
-
-    DCHK(hipSetDevice(dev));
-    DCHK(hipHostMalloc((void **)&h_in, itot + 4096));
-    DCHK(dalloc(&d_in, itot + 4096));
-    memset(h_in, 0, itot + 4096);
-    for (uint32_t j = 0; j < ns; j++) memcpy(h_in + ioff[j], in + in_off[j], in_len[j]);
-    DCHK(hipMemcpyAsync(d_in, h_in, itot + 4096, hipMemcpyHostToDevice, s));
-    DCHK(dalloc(&d_ioff, ns));
-    DCHK(dalloc(&d_ilen, ns));
-    DCHK(dalloc(&d_tcnt, ns));
-    DCHK(dalloc(&d_tbase, ns));
-    DCHK(dalloc(&d_stop, ns));
-    DCHK(dalloc(&d_slot, ns));
-    DCHK(dalloc(&d_lim, ns));
-    DCHK(dalloc(&d_ooff, ns));
-    DCHK(dalloc(&d_ocap, ns));
-    DCHK(dalloc(&d_olen, ns));
-    DCHK(dalloc(&d_cons, ns));
-    DCHK(dalloc(&d_unk, ns));
-    DCHK(dalloc(&d_st, ns));
-    DCHK(dalloc(&d_hu, ns));
-    DCHK(dalloc(&d_ctl, 4));
-    DCHK(dalloc(&d_out, otot + 256));
-    DCHK(hipMemcpyAsync(d_ioff, ioff.data(), ns * 8, hipMemcpyHostToDevice, s));
-    DCHK(hipMemcpyAsync(d_ilen, ilen.data(), ns * 4, hipMemcpyHostToDevice, s));
-    DCHK(hipMemcpyAsync(d_ooff, ooff.data(), ns * 8, hipMemcpyHostToDevice, s));
-    DCHK(hipMemcpyAsync(d_ocap, out_cap, ns * 8, hipMemcpyHostToDevice, s));
-    DCHK(hipMemsetAsync(d_ctl, 0, 16, s));
-    D.in = d_in;
-    D.in_off = d_ioff;
-    D.in_len = d_ilen;
-    D.tok_cnt = d_tcnt;
-    D.tok_base = d_tbase;
-    D.s_stop = d_stop;
-    D.s_slot = d_slot;
-    D.s_lim = d_lim;
-    D.out = d_out;
-    D.out_off = d_ooff;
-    D.out_cap = d_ocap;
-    D.out_len = d_olen;
-    D.consumed = d_cons;
-    D.unknown = d_unk;
-    D.status = d_st;
-    D.has_unknown = d_hu;
-    D.ctl = d_ctl;
-
-    // tokens: count, prefix, fill
-    hipLaunchKernelGGL(k_dtok, dim3(ns), dim3(64), 0, s, D, 0);
-    DCHK(hipGetLastError());
-    DCHK(hipMemcpyAsync(tcnt.data(), d_tcnt, ns * 4, hipMemcpyDeviceToHost, s));
-    DCHK(hipStreamSynchronize(s));
-    for (uint32_t j = 0; j < ns; j++) {
-        tbase[j] = (uint32_t)ntok;
-        ntok += tcnt[j];
-    }
-    if (ntok > 0xFFFFFFF0ull) { rc = xc__set_error(XC_EINVAL, "too many tokens"); goto done; }
-    DCHK(hipMemcpyAsync(d_tbase, tbase.data(), ns * 4, hipMemcpyHostToDevice, s));
-    DCHK(dalloc(&D.t_lb, ntok));
-    DCHK(dalloc(&D.t_le, ntok));
-    DCHK(dalloc(&D.t_op, ntok));
-    DCHK(dalloc(&D.t_stat, ntok));
-    DCHK(dalloc(&D.t_h, ntok));
-    DCHK(dalloc(&D.t_src, ntok));
-    hipLaunchKernelGGL(k_dtok, dim3(ns), dim3(64), 0, s, D, 1);
-    DCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_dhash, dim3(ns, 8), dim3(64), 0, s, D);
-    DCHK(hipGetLastError());
-    // batch provider table
-    n_full = 1024;
-    while (n_full < 2 * ntok + 2) n_full <<= 1;
-    n_lo = 1024;
-    while (n_lo < 4 * ntok + 4) n_lo <<= 1;
-    DCHK(dalloc(&ds.filt, XC_FILT_WORDS));
-    DCHK(dalloc(&ds.l2, 2 * (size_t)XC_L2_WORDS));
-    DCHK(dalloc(&ds.lo_keys, n_lo));
-    DCHK(dalloc(&ds.lo_zero, 1));
-    DCHK(dalloc(&ds.keys, n_full));
-    DCHK(dalloc(&ds.vals, n_full));
-    ds.mask = n_full - 1;
-    ds.lo_mask = n_lo - 1;
-    hipLaunchKernelGGL(k_dlim, dim3((ns + 255) / 256), dim3(256), 0, s, D, 1);
-    DCHK(hipGetLastError());
-    for (;;) {
-        DCHK(hipMemsetAsync(ds.filt, 0, XC_FILT_WORDS * 4, s));
-        DCHK(hipMemsetAsync(ds.l2, 0, (size_t)XC_L2_WORDS * 8, s));
-        DCHK(hipMemsetAsync(ds.lo_keys, 0, (size_t)n_lo * 4, s));
-        DCHK(hipMemsetAsync(ds.lo_zero, 0, 4, s));
-        DCHK(hipMemsetAsync(ds.keys, 0xFF, (size_t)n_full * 8, s));
-        DCHK(hipMemsetAsync(ds.vals, 0xFF, (size_t)n_full * 8, s));
-        DCHK(hipMemsetAsync(d_ctl, 0, 4, s));
-        hipLaunchKernelGGL(k_dres1, dim3(ns, 8), dim3(64), 0, s, D);
-        DCHK(hipGetLastError());
-        hipLaunchKernelGGL(k_dres2, dim3(ns, 8), dim3(64), 0, s, D);
-        DCHK(hipGetLastError());
-        hipLaunchKernelGGL(k_dstop, dim3((ns + 63) / 64), dim3(64), 0, s, D);
-        DCHK(hipGetLastError());
-        hipLaunchKernelGGL(k_dcheck, dim3(ns), dim3(64), 0, s, D, rounds);
-        DCHK(hipGetLastError());
-        DCHK(hipMemcpyAsync(ctl, d_ctl, 16, hipMemcpyDeviceToHost, s));
-        DCHK(hipStreamSynchronize(s));
-        if (!ctl[DCTL_FIX]) break;
-        hipLaunchKernelGGL(k_dlim, dim3((ns + 255) / 256), dim3(256), 0, s, D, 0);
-        DCHK(hipGetLastError());
-        if (++rounds > 64) { rc = xc__set_error(XC_EDEVICE, "decode provider resolution did not converge"); goto done; }
-    }
-    hipLaunchKernelGGL(k_demit, dim3(ns), dim3(256), 0, s, D);
-    DCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_dalloc, dim3(1), dim3(1024), 0, s, D);
-    DCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_dcommit, dim3(ns), dim3(64), 0, s, D);
-    DCHK(hipGetLastError());
-    DCHK(hipMemcpyAsync(ctl, d_ctl, 16, hipMemcpyDeviceToHost, s));
-    DCHK(hipMemcpyAsync(olen.data(), d_olen, ns * 8, hipMemcpyDeviceToHost, s));
-    DCHK(hipMemcpyAsync(cons.data(), d_cons, ns * 8, hipMemcpyDeviceToHost, s));
-    DCHK(hipMemcpyAsync(unk.data(), d_unk, ns * 8, hipMemcpyDeviceToHost, s));
-    DCHK(hipMemcpyAsync(st.data(), d_st, ns * 4, hipMemcpyDeviceToHost, s));
-    DCHK(hipMemcpyAsync(hu.data(), d_hu, ns * 4, hipMemcpyDeviceToHost, s));
-    DCHK(hipHostMalloc((void **)&h_out, otot + 256));
-    DCHK(hipMemcpyAsync(h_out, d_out, otot + 256, hipMemcpyDeviceToHost, s));
-    DCHK(hipStreamSynchronize(s));
-    if (ctl[DCTL_ERR] & 2u) { rc = xc__set_error(XC_ENOSPC, "device cache capacity exhausted"); goto done; }
-    if (ctl[DCTL_ERR] & 1u) { rc = xc__set_error(XC_EINVAL, "output capacity too small"); goto done; }
-    for (uint32_t j = 0; j < ns; j++) {
-        out_len[j] = olen[j];
-        consumed[j] = cons[j];
-        unknown[j] = unk[j];
-        status[j] = st[j];
-        has_unknown[j] = hu[j];
-        memcpy(out + out_off[j], h_out + ooff[j], olen[j]);
-    }
-    rc = XC_OK;
-done:
+    const uint32_t ns = p->ns;
+    const hipStream_t s = p->s;
+    uint8_t *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
+    uint64_t *d_u64 = nullptr;  // out_len | consumed | unknown
+    int32_t *d_i32 = nullptr;   // status | has_unknown
+    std::vector<uint64_t> u64(3 * (size_t)ns);
+    std::vector<int32_t> i32(2 * (size_t)ns);
+    auto run = [&]() -> int {
+        DHIP(hipHostMalloc((void **)&h_in, p->in_bytes));
+        DHIP(hipHostMalloc((void **)&h_out, p->out_bytes));
+        DHIP(dalloc(&d_in, p->in_bytes));
+        DHIP(dalloc(&d_out, p->out_bytes));
+        DHIP(dalloc(&d_u64, 3 * (size_t)ns));
+        DHIP(dalloc(&d_i32, 2 * (size_t)ns));
+        memset(h_in, 0, p->in_bytes);
+        for (uint32_t j = 0; j < ns; j++) memcpy(h_in + p->ioff[j], in + in_off[j], in_len[j]);
+        DHIP(hipMemcpyAsync(d_in, h_in, p->in_bytes, hipMemcpyHostToDevice, s));
+        int r = xc_decode_run(p, d_in, d_out, d_u64, d_u64 + ns, d_i32, d_u64 + 2 * ns, d_i32 + ns);
+        if (r) return r;
+        DHIP(hipMemcpyAsync(h_out, d_out, p->out_bytes, hipMemcpyDeviceToHost, s));
+        DHIP(hipMemcpyAsync(u64.data(), d_u64, 3 * (size_t)ns * 8, hipMemcpyDeviceToHost, s));
+        DHIP(hipMemcpyAsync(i32.data(), d_i32, 2 * (size_t)ns * 4, hipMemcpyDeviceToHost, s));
+        DHIP(hipStreamSynchronize(s));
+        for (uint32_t j = 0; j < ns; j++) {
+            out_len[j] = u64[j];
+            consumed[j] = u64[ns + j];
+            unknown[j] = u64[2 * ns + j];
+            status[j] = i32[j];
+            has_unknown[j] = i32[ns + j];
+            memcpy(out + out_off[j], h_out + p->ooff[j], out_len[j]);
+        }
+        return XC_OK;
+    };
+    rc = run();
     hipStreamSynchronize(s);
     hipHostFree(h_in);
     hipHostFree(h_out);
     hipFree(d_in);
     hipFree(d_out);
-    hipFree(d_ioff);
-    hipFree(d_ilen);
-    hipFree(d_tcnt);
-    hipFree(d_tbase);
-    hipFree(d_stop);
-    hipFree(d_slot);
-    hipFree(d_lim);
-    hipFree(d_ooff);
-    hipFree(d_ocap);
-    hipFree(d_olen);
-    hipFree(d_cons);
-    hipFree(d_unk);
-    hipFree(d_st);
-    hipFree(d_hu);
-    hipFree(d_ctl);
-    hipFree(D.t_lb);
-    hipFree(D.t_le);
-    hipFree(D.t_op);
-    hipFree(D.t_stat);
-    hipFree(D.t_h);
-    hipFree(D.t_src);
-    hipFree(ds.filt);
-    hipFree(ds.l2);
-    hipFree(ds.lo_keys);
-    hipFree(ds.lo_zero);
-    hipFree(ds.keys);
-    hipFree(ds.vals);
+    hipFree(d_u64);
+    hipFree(d_i32);
+    xc_dplan_destroy(p);
     return rc;
 }

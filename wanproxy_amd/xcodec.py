@@ -32,6 +32,7 @@ SYMBOLS = [
     "xc_plan_kernel_times", "xc_host_alloc", "xc_host_free", "xc_encode_run_host",
     "xc_plan_set_streams", "xc_plan_stream_results", "xc_encoder_create", "xc_encoder_destroy",
     "xc_encoder_pending", "xc_encode", "xc_flush", "xc_encode_streams",
+    "xc_decode_plan_create", "xc_dplan_destroy", "xc_dplan_layout", "xc_decode_run", "xc_dplan_stats",
 ]
 STREAM_FLUSH = 1  # XC_STREAM_FLUSH
 
@@ -53,6 +54,11 @@ class RunStats(C.Structure):
                 ("walk_rounds", C.c_uint32), ("outer_rounds", C.c_uint32),
                 ("dense_chunks", C.c_uint32), ("redone", C.c_uint32),
                 ("shadow_misses", C.c_uint32)]
+
+
+class DecodeStats(C.Structure):
+    _fields_ = [("in_bytes", C.c_uint64), ("n_extract", C.c_uint64), ("n_ref", C.c_uint64),
+                ("n_entered", C.c_uint64), ("rounds", C.c_uint32)]
 
 
 _LIB = None
@@ -121,6 +127,11 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.xc_flush.argtypes = [_vp, _u8p, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_int)]
     lib.xc_encode_streams.argtypes = [C.POINTER(_vp), C.POINTER(C.c_void_p), _u64p, _u32p, C.c_uint64,
                                       _u8p, _u64p, _u64p, _u64p]
+    lib.xc_decode_plan_create.argtypes = [_vp, _u64p, _u64p, C.c_uint64, C.POINTER(_vp)]
+    lib.xc_dplan_destroy.argtypes = [_vp]
+    lib.xc_dplan_layout.argtypes = [_vp, _u64p, _u64p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+    lib.xc_decode_run.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
+    lib.xc_dplan_stats.argtypes = [_vp, C.POINTER(DecodeStats)]
     _LIB = lib
     return lib
 
@@ -435,6 +446,51 @@ class EncodePlan:
     def close(self) -> None:
         if getattr(self, "h", None):
             load_library().xc_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DecodePlan:
+    """A device-resident decode batch (xc_decode_plan_create / xc_decode_run): fixed stream
+    lengths and output capacities, arenas in HBM.  ``run`` takes raw device pointers: the input
+    and output arenas, then nbuf-long arrays out_len, consumed (u64), status (i32), unknown
+    (u64), has_unknown (i32)."""
+
+    def __init__(self, cache: XCodecCache, lengths, out_caps):
+        self.cache = cache
+        lens = np.ascontiguousarray(lengths, dtype=np.uint64)
+        caps = np.ascontiguousarray(out_caps, dtype=np.uint64)
+        self.nbuf = len(lens)
+        self.h = _vp()
+        _check(load_library().xc_decode_plan_create(cache.h, lens, caps, self.nbuf, C.byref(self.h)))
+        self.in_off = np.zeros(self.nbuf, np.uint64)
+        self.out_off = np.zeros(self.nbuf, np.uint64)
+        ib, ob = C.c_uint64(), C.c_uint64()
+        _check(load_library().xc_dplan_layout(self.h, self.in_off, self.out_off, C.byref(ib), C.byref(ob)))
+        self.in_bytes, self.out_bytes = ib.value, ob.value
+        _LIVE["plan"].add(self)
+
+    def _ctx(self):
+        return self.cache.ctx
+
+    def run(self, d_in: int, d_out: int, d_out_len: int, d_consumed: int, d_status: int,
+            d_unknown: int, d_has_unknown: int) -> None:
+        _check(load_library().xc_decode_run(self.h, d_in, d_out, d_out_len, d_consumed, d_status,
+                                            d_unknown, d_has_unknown))
+
+    def stats(self) -> DecodeStats:
+        st = DecodeStats()
+        _check(load_library().xc_dplan_stats(self.h, C.byref(st)))
+        return st
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            load_library().xc_dplan_destroy(self.h)
             self.h = None
 
     def __del__(self):
