@@ -124,7 +124,9 @@ typedef struct {
     uint64_t launches[XC_K_COUNT];
     uint64_t scan_bytes;          /* input bytes covered by the scan launches */
 } xc_kernel_times;
-int xc_plan_set_timing(xc_plan *p, int enable);
+#define XC_TIMING_ALL 1   /* every kernel (each event pair adds a few us between launches) */
+#define XC_TIMING_SCAN 2  /* the scan launches only */
+int xc_plan_set_timing(xc_plan *p, int mode);
 int xc_plan_kernel_times(xc_plan *p, xc_kernel_times *out, int reset);
 
 /* Counters of the last run (for benchmarks / profiling). */

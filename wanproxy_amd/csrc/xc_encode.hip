@@ -209,20 +209,29 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
     }
     __syncthreads();
 
-    // each wave scans a contiguous run of chunks, so consecutive chunks of one buffer continue
-    // the block stream (and its prefetch) without a restart
-    const uint32_t nwaves = gridDim.x * SCAN_WAVES, nck = a.ck_hi - a.ck_lo;
-    const uint32_t per = (nck + nwaves - 1u) / nwaves;
-    uint32_t c = a.ck_lo + (blockIdx.x * SCAN_WAVES + wave) * per;
-    const uint32_t c_end = min(c + per, a.ck_hi);
-    if (c >= c_end) return;
+    // Work distribution: waves take runs of SCAN_UNIT consecutive chunks from a counter (chunks
+    // of one buffer continue the block stream and its prefetch without a restart), the next run
+    // always claimed one run ahead.  Dynamic, because the cost of a chunk varies (REF shadows,
+    // filter positives) and other kernels may hold some CUs when the scan starts.
+    // The first run of every wave is static (wave g: run g), so only the look-ahead claims
+    // contend on the counter.
+    const uint32_t nwaves = gridDim.x * SCAN_WAVES;
+    auto claim = [&]() -> uint32_t {
+        uint32_t t = 0;
+        if (l == 0) t = atomicAdd(&a.P.ctl[CTL_SCAN_NEXT], SCAN_UNIT);
+        return a.ck_lo + nwaves * SCAN_UNIT + uniform(t);
+    };
+    uint32_t c = a.ck_lo + (blockIdx.x * SCAN_WAVES + wave) * SCAN_UNIT;
+    if (c >= a.ck_hi) return;
+    uint32_t c_end = min(c + SCAN_UNIT, a.ck_hi);
+    uint32_t c_nxt = claim();
 
     // chunk descriptors: {c0, c1, arena offset lo, hi}; the next one is always in flight
     uint4 dsc = a.P.chunk_desc[c];
     uint32_t gblk = a.shadow ? uniform(a.P.chunk_blk[c]) : 0u;
     uint32_t pw[8], w[8], wn[8];
     first_blocks(desc_base(a, dsc), uniform(dsc.x), l, pw, w, wn);
-    uint4 dn = a.P.chunk_desc[min(c + 1u, c_end - 1u)];
+    uint4 dn = a.P.chunk_desc[c + 1u < c_end ? c + 1u : min(c_nxt, a.ck_hi - 1u)];
 
     Pending pd;
     pd.n = 0;
@@ -233,9 +242,10 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
     for (;;) {
         const uint32_t c0 = uniform(dsc.x), c1 = uniform(dsc.y) & 0x3FFFFFFFu;
         const uint8_t *base = desc_base(a, dsc);
-        const bool has_next = c + 1u < c_end;
-        // the next chunk continues this one (same buffer, starts at c1): keep streaming
-        const bool contig = has_next && (uniform(dsc.y) >> 31) != 0u;
+        const bool in_run = c + 1u < c_end;
+        const bool has_next = in_run || c_nxt < a.ck_hi;
+        // the next chunk continues this one (same run and buffer, starts at c1): keep streaming
+        const bool contig = in_run && (uniform(dsc.y) >> 31) != 0u;
         uint32_t ev_n = 0, qn = 0;
         bool dense = false;
 
@@ -367,11 +377,17 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
             if (l == 0 && dense) atomicAdd(&a.P.ctl[CTL_DENSE], 1u);
         }
         if (!has_next) break;
-        c += 1u;
+        if (in_run) {
+            c += 1u;
+        } else {
+            c = c_nxt;
+            c_end = min(c + SCAN_UNIT, a.ck_hi);
+            c_nxt = claim();
+        }
         dsc = dn;
         if (a.shadow) gblk = uniform(a.P.chunk_blk[c]);
         if (!contig) first_blocks(desc_base(a, dsc), uniform(dsc.x), l, pw, w, wn);
-        dn = a.P.chunk_desc[min(c + 1u, c_end - 1u)];
+        dn = a.P.chunk_desc[c + 1u < c_end ? c + 1u : min(c_nxt, a.ck_hi - 1u)];
     }
     if (MODE >= 2 && sink == 0x7FFFFFF0u - a.ck_hi) a.P.ctl[CTL_ERROR] = sink;  // never true; keeps ablations honest
     if (pd.n) {
@@ -427,6 +443,9 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t x, int l)
 
 __global__ __launch_bounds__(256) void k_resolve(ResolveArgs a)
 {
+    // the scan that ran before has handed out all its work: reset its counter for the next
+    // scan (before the abort check, so a redone sub-batch starts from a clean counter)
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.P.ctl[CTL_SCAN_NEXT] = 0u;
     if (aborted(a.P)) return;
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // the walk that follows reports afresh
         a.P.ctl[CTL_GREW] = 0u;

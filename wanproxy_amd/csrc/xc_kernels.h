@@ -10,6 +10,7 @@ constexpr uint32_t EV_CAP = 64;          // sparse events per scan chunk before 
 constexpr uint32_t EV_DENSE = 0x80000000u;
 constexpr uint32_t Q_CAP = 128;          // per-wave LDS queue of level-1 filter positives
 constexpr uint32_t SCAN_WAVES = 16;      // waves per scan workgroup (1024 threads)
+constexpr uint32_t SCAN_UNIT = 4;        // chunks a scan wave takes from the work counter at a time
 constexpr uint32_t SCAN_LDS = XC_FILT_WORDS * 4u + SCAN_WAVES * Q_CAP * 8u;
 constexpr uint32_t MAX_BUF = 1u << 20;   // longest single buffer accepted (1 MiB)
 constexpr uint32_t MAX_DECL = MAX_BUF / XC_SEG + 2u;
@@ -37,6 +38,7 @@ enum : uint32_t {
     CTL_ABORT = 7,     // set by k_gate: a sub-batch needs the host (growth, cross-buffer, error)
     CTL_ABORT_SB = 8,  // ... and which one; every later pipeline kernel exits at once
     CTL_SHADOW = 9,    // a walk did not emit a predicted REF whose shadow the scan skipped
+    CTL_SCAN_NEXT = 10,  // k_scan work counter (chunks handed out); k_resolve resets it
     CTL_WORDS = 16
 };
 constexpr uint32_t ERR_CAPACITY = 1, ERR_TOKENS = 2, ERR_DECLS = 4;  // (ERR_PACK_CAP = 8 below)

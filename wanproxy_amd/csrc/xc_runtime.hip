@@ -427,8 +427,9 @@ struct xc_plan {
     uint32_t *d_blk_base;
     uint32_t *d_l2mix;  // level-2 filter of cache | declaration set for the combined scan
     xc_run_stats stats{};
-    // per-kernel HIP-event timing
-    bool timing = false;
+    // per-kernel HIP-event timing: 0 off, XC_TIMING_ALL every kernel, XC_TIMING_SCAN the scans only
+    // (each recorded event pair costs the stream a few microseconds between dependent launches)
+    int timing = 0;
     std::vector<hipEvent_t> ev_pool;
     std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev_live;
     xc_kernel_times ktimes{};
@@ -474,7 +475,7 @@ struct KSpan {
     hipStream_t st;
     KSpan(xc_plan *p_, int k_, hipStream_t s_ = nullptr) : p(p_), k(k_), st(s_ ? s_ : p_->cache->ctx->stream)
     {
-        if (!p->timing) return;
+        if (!p->timing || (p->timing == XC_TIMING_SCAN && k != XC_K_SCAN)) return;
         a = ev_get(p);
         b = ev_get(p);
         if (a) hipEventRecord(a, st);
@@ -736,7 +737,7 @@ extern "C" int xc_plan_layout(xc_plan *p, uint64_t *in_off, uint64_t *out_off, u
 extern "C" int xc_plan_set_timing(xc_plan *p, int enable)
 {
     if (!p) return fail(XC_EINVAL, "null");
-    p->timing = enable != 0;
+    p->timing = enable == XC_TIMING_SCAN ? XC_TIMING_SCAN : enable ? XC_TIMING_ALL : 0;
     return XC_OK;
 }
 
@@ -825,7 +826,7 @@ static int launch_scan(xc_plan *p, const Layer &L, const DevSet &set, uint32_t c
     }
     KSpan span(p, XC_K_SCAN);
     if (p->timing) p->ktimes.scan_bytes += p->chunk_bytes[ck_hi] - p->chunk_bytes[ck_lo];
-    uint32_t need = (ck_hi - ck_lo + SCAN_WAVES - 1) / SCAN_WAVES;
+    uint32_t need = (ck_hi - ck_lo + SCAN_WAVES * SCAN_UNIT - 1) / (SCAN_WAVES * SCAN_UNIT);
     uint32_t grid = std::min<uint32_t>(need, (uint32_t)ctx->n_cu);
     // XC_SCAN_ABLATION=m (timing experiments only: results are wrong) runs k_scan<m> in the pipeline
     static const int abl = getenv("XC_SCAN_ABLATION") ? atoi(getenv("XC_SCAN_ABLATION")) : 0;
@@ -1187,16 +1188,19 @@ extern "C" double xc__scan_ablation(xc_plan *p, const uint8_t *d_in, int mode, i
     hipSetDevice(ctx->dev);
     p->P.in = d_in;
     ScanArgs a{p->P, p->P.S, p->P.cache, 0, p->nchunks, (uint32_t)mode, DevSet{}, 0, (const uint2 *)p->P.cache.l2};
-    uint32_t need = (p->nchunks + SCAN_WAVES - 1) / SCAN_WAVES;
+    uint32_t need = (p->nchunks + SCAN_WAVES * SCAN_UNIT - 1) / (SCAN_WAVES * SCAN_UNIT);
     uint32_t grid = std::min<uint32_t>(need, (uint32_t)ctx->n_cu);
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
     auto kern = mode == 0 ? k_scan<0> : mode == 1 ? k_scan<1> : mode == 2 ? k_scan<2> : mode == 3 ? k_scan<3> : mode == 4 ? k_scan<4> : k_scan<5>;
+    hipMemsetAsync(p->P.ctl + CTL_SCAN_NEXT, 0, 4, ctx->stream);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * SCAN_WAVES), 0, ctx->stream, a);
     hipEventRecord(e0, ctx->stream);
-    for (int i = 0; i < iters; i++)
+    for (int i = 0; i < iters; i++) {
+        hipMemsetAsync(p->P.ctl + CTL_SCAN_NEXT, 0, 4, ctx->stream);
         hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * SCAN_WAVES), 0, ctx->stream, a);
+    }
     hipEventRecord(e1, ctx->stream);
     hipEventSynchronize(e1);
     float ms = 0;

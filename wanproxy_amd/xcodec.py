@@ -428,8 +428,11 @@ class EncodePlan:
         _check(load_library().xc_encode_run_host(self.h, h_in.ptr, h_out.ptr, h_out.nbytes, lens, pos))
         return lens[:self.nbuf], pos[:self.nbuf]
 
-    def set_timing(self, enable: bool) -> None:
-        _check(load_library().xc_plan_set_timing(self.h, 1 if enable else 0))
+    def set_timing(self, mode) -> None:
+        """HIP-event kernel timing: False (off), True (every kernel) or "scan" (the scan
+        launches only: each event pair adds a few microseconds between dependent launches)."""
+        m = 2 if mode == "scan" else (1 if mode else 0)
+        _check(load_library().xc_plan_set_timing(self.h, m))
 
     def kernel_times(self, reset: bool = False) -> dict:
         kt = KernelTimes()
