@@ -1007,13 +1007,16 @@ extern "C" int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, ui
     p->next_hash = 0;
     const size_t nsub = p->sub.size() - 1;
     size_t si = 0;
+    bool fresh = false;  // ctl was read after the last launch
     while (si < nsub) {
         // Async pass: enqueue every remaining sub-batch with no host round trip.  k_gate
         // stops the device pipeline at the first sub-batch that needs the host.
         for (size_t k = si; k < nsub; k++)
             if ((rc = encode_sub_async(p, (uint32_t)k))) return rc;
         if ((rc = read_ctl(p, ctl))) return rc;
+        fresh = true;
         if (!ctl[CTL_ABORT]) break;
+        fresh = false;
         si = ctl[CTL_ABORT_SB];
         HIPCHK(hipMemsetAsync(p->P.ctl + CTL_ABORT, 0, 4, s));
         if (ctl[CTL_ERROR]) break;
@@ -1025,7 +1028,7 @@ extern "C" int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, ui
         if ((rc = launch_pack(p, p->sub[si], p->sub[si + 1]))) return rc;
         si++;
     }
-    if ((rc = read_ctl(p, ctl))) return rc;
+    if (!fresh && (rc = read_ctl(p, ctl))) return rc;
     for (uint64_t i = 0; i < p->nb; i++) p->stats.in_bytes += p->len[i];
     p->stats.n_extract = ctl[CTL_NEXTRACT];
     p->stats.n_ref = ctl[CTL_NREF];
