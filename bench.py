@@ -307,6 +307,14 @@ def main():
             "sample": f"first {len(sample)} cfg5 buffers ({len(sample) * W.BUF >> 20} MiB), "
                       f"round-robin over {nthreads} threads, each with a private clone of the warm cache",
             "seconds": round(secs, 3)}
+        # the same port on one host thread (1 thread and all threads)
+        one = sample[:min(len(sample), 4096)]
+        oc1 = oracle.Cache()
+        oc1.encode_batch(warm)
+        secs1, _ = oc1.encode_sharded_timed(one, 1)
+        result["cpu_baseline"]["single_thread"] = {
+            "value": round(len(one) * W.BUF / secs1 / 2**30, 4), "unit": "GiB/s", "cores": 1,
+            "sample": f"first {len(one)} cfg5 buffers ({len(one) * W.BUF >> 20} MiB)", "seconds": round(secs1, 3)}
 
     if rank == 0:
         print(json.dumps(result))

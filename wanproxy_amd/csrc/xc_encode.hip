@@ -908,30 +908,33 @@ __global__ __launch_bounds__(64) void k_walk_blocks(WalkArgs a)
 }
 
 // ------------------------------------------------------------ k_declhash ----------------
-// grid (buffers, 8): wave y of buffer b hashes EXTRACT tokens y, y+8, ... and enters them
-// into the declaration set (value = b<<32 | declaration position, min-merged).
-
-__global__ __launch_bounds__(64) void k_declhash(DeclArgs a)
+// One wave per buffer (4 per workgroup): the EXTRACT tokens whose hash no resolved event
+// supplied are hashed and entered into the declaration set (value = b<<32 | declaration
+// position, min-merged); any such entry means the scan missed it: another round.
+__global__ __launch_bounds__(256) void k_declhash(DeclArgs a)
 {
     if (aborted(a.P)) return;
     const PlanDev &P = a.P;
-    const uint32_t b = a.j0 + blockIdx.x;
+    const uint32_t b = a.j0 + blockIdx.x * 4u + (threadIdx.x >> 6);
     if (b >= a.j1) return;
+    const uint32_t l = lane_id();
     const uint8_t *base = P.in + P.buf_off[b];
     const uint32_t tb = P.tok_base[b], n = P.tok_cnt[b];
-    for (uint32_t t = blockIdx.y; t < n; t += gridDim.y) {
-        if (uniform(P.tok_op[tb + t]) != OP_EXTRACT) continue;
-        // a known hash came from a resolved match against the scanned declaration set
-        if (uniform(P.tok_known[tb + t])) continue;
-        const uint32_t seg = uniform(P.tok_seg[tb + t]);
-        const uint64_t h = wave_window_hash(base + seg);
-        if (lane_id() == 0) {
-            P.tok_h[tb + t] = h;
-            const uint64_t v = ((uint64_t)b << 32) | P.tok_dpos[tb + t];
-            set_insert(P.dset, h, v, true, nullptr, nullptr);
-            // not in the set the positions were scanned against: another round is needed
-            if (__hip_atomic_load(&P.ctl[CTL_GREW], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
-                atomicOr(&P.ctl[CTL_GREW], 1u);
+    for (uint32_t t0 = 0; t0 < n; t0 += 64u) {
+        const uint32_t t = t0 + l;
+        const bool unknown = t < n && P.tok_op[tb + t] == OP_EXTRACT && !P.tok_known[tb + t];
+        for (uint64_t m = ballot(unknown); m; m &= m - 1) {
+            const uint32_t tt = tb + t0 + (uint32_t)(__ffsll((unsigned long long)m) - 1);
+            const uint32_t seg = uniform(P.tok_seg[tt]);
+            const uint64_t h = wave_window_hash(base + seg);
+            if (l == 0) {
+                P.tok_h[tt] = h;
+                const uint64_t v = ((uint64_t)b << 32) | P.tok_dpos[tt];
+                set_insert(P.dset, h, v, true, nullptr, nullptr);
+                // not in the set the positions were scanned against: another round is needed
+                if (__hip_atomic_load(&P.ctl[CTL_GREW], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+                    atomicOr(&P.ctl[CTL_GREW], 1u);
+            }
         }
     }
 }
@@ -955,31 +958,29 @@ __global__ __launch_bounds__(64) void k_blockhash(DeclArgs a)
     }
 }
 
-// One wave per buffer, one lane per aligned block: blocks absent from the cache are the
-// predicted declarations (hit-free data declares exactly these, xcodec_encoder.cc:77-82);
-// they enter the declaration set and the combined level-2 filter before the scan.
-__global__ __launch_bounds__(64) void k_blockpredict(DeclArgs a)
+// One lane per aligned block of buffers [j0, j1) (P.blk_buf maps a block to its buffer):
+// blocks absent from the cache are the predicted declarations (hit-free data declares exactly
+// these, xcodec_encoder.cc:77-82); they enter the declaration set and the combined level-2
+// filter before the scan.  Cached blocks are predicted REFs (REF shadows).
+__global__ __launch_bounds__(256) void k_blockpredict(DeclArgs a)
 {
     if (aborted(a.P)) return;
     const PlanDev &P = a.P;
-    const uint32_t b = a.j0 + blockIdx.x;
-    if (b >= a.j1) return;
-    const uint32_t nblk = P.buf_len[b] / XC_SEG, bb = P.blk_base[b];
+    const uint32_t g = P.blk_base[a.j0] + blockIdx.x * 256u + threadIdx.x;
+    if (g >= P.blk_base[a.j1]) return;
+    const uint32_t b = P.blk_buf[g], k = g - P.blk_base[b];
     if (stream_carried(P, b)) {  // blocks relative to a carried source_: no predictions
-        for (uint32_t k = lane_id(); k < nblk; k += 64u) P.blk_pref[bb + k] = 0u;
+        P.blk_pref[g] = 0u;
         return;
     }
-    for (uint32_t k = lane_id(); k < nblk; k += 64u) {
-        const uint64_t h = P.blk_h[bb + k];
-        uint64_t v;
-        const bool cached = set_find(P.cache, h, &v);
-        P.blk_pref[bb + k] = cached ? 1u : 0u;  // a predicted REF (REF shadows, k_scan / k_walk)
-        if (!cached &&
-            set_insert(P.dset, h, ((uint64_t)b << 32) | (k * XC_SEG + 2u * XC_SEG - 1u), true, nullptr, nullptr)) {
-            const uint32_t g = l2_mix((uint32_t)h), gi = (g >> 14) * 2u;
-            atomicOr(&P.l2mix[gi], 1u << (g & 31u));
-            atomicOr(&P.l2mix[gi + 1u], 1u << ((g >> 5) & 31u));
-        }
+    const uint64_t h = P.blk_h[g];
+    uint64_t v;
+    const bool cached = set_find(P.cache, h, &v);
+    P.blk_pref[g] = cached ? 1u : 0u;
+    if (!cached && set_insert(P.dset, h, ((uint64_t)b << 32) | (k * XC_SEG + 2u * XC_SEG - 1u), true, nullptr, nullptr)) {
+        const uint32_t gm = l2_mix((uint32_t)h), gi = (gm >> 14) * 2u;
+        atomicOr(&P.l2mix[gi], 1u << (gm & 31u));
+        atomicOr(&P.l2mix[gi + 1u], 1u << ((gm >> 5) & 31u));
     }
 }
 

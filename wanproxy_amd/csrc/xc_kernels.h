@@ -73,7 +73,8 @@ struct PlanDev {
     uint32_t *tok_cnt;
     uint32_t *tok_lb, *tok_le, *tok_seg, *tok_op, *tok_dpos;
     uint32_t *tok_known;       // EXTRACT hash known from a resolved event (no rehash needed)
-    const uint32_t *blk_base;  // [nb] first aligned-block index of the buffer
+    const uint32_t *blk_base;  // [nb + 1] first aligned-block index of the buffer
+    const uint32_t *blk_buf;   // [blocks] buffer of every aligned block
     uint64_t *blk_h;           // hash of every aligned 2048-byte block (k_blockhash)
     uint64_t *tok_h;
     uint32_t *buf_next;   // [nb] EXTRACT tokens of the buffer (walk)

@@ -424,7 +424,8 @@ struct xc_plan {
     uint32_t *d_buf_len, *d_chunk0, *d_tok_base;
     uint2 *d_chunks;
     uint4 *d_desc;
-    uint32_t *d_blk_base;
+    uint32_t *d_blk_base, *d_blk_buf = nullptr;
+    std::vector<uint32_t> blk_base;  // host copy [nb + 1]
     uint32_t *d_l2mix;  // level-2 filter of cache | declaration set for the combined scan
     xc_run_stats stats{};
     // per-kernel HIP-event timing: 0 off, XC_TIMING_ALL every kernel, XC_TIMING_SCAN the scans only
@@ -547,6 +548,7 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
         toks += 2 * (n / XC_SEG) + 3;
     }
     chunk0[nbuf] = (uint32_t)chunks.size();
+    blk_base[nbuf] = (uint32_t)nblk;
     if (toks > 0xFFFFFFF0ull) return fail(XC_EINVAL, "batch too large");
     p->in_bytes = io + 8192;  // slack: the scan prefetches up to two blocks past a buffer
     p->out_bytes = oo + 256;
@@ -639,7 +641,16 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
         const char *e = getenv("XC_NO_SHADOW");
         p->shadow = (e && atoi(e)) ? 0 : 1;
     }
-    HIPCHK(hipMalloc(&p->d_blk_base, nb1 * 4));
+    HIPCHK(hipMalloc(&p->d_blk_base, (nbuf + 1) * 4));
+    {
+        std::vector<uint32_t> bb(std::max<uint64_t>(nblk, 1), 0);
+        for (uint64_t i = 0; i < nbuf; i++)
+            for (uint32_t g = blk_base[i]; g < blk_base[i + 1]; g++) bb[g] = (uint32_t)i;
+        HIPCHK(hipMalloc(&p->d_blk_buf, bb.size() * 4));
+        HIPCHK(hipMemcpyAsync(p->d_blk_buf, bb.data(), bb.size() * 4, hipMemcpyHostToDevice, s));
+        P.blk_buf = p->d_blk_buf;
+        p->blk_base = blk_base;
+    }
     HIPCHK(hipMalloc(&p->d_l2mix, (size_t)XC_L2_WORDS * 8));
     P.l2mix = p->d_l2mix;
     HIPCHK(hipStreamCreateWithFlags(&p->hs, hipStreamNonBlocking));
@@ -648,7 +659,7 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     p->ev_go.assign(p->sub.size(), nullptr);
     for (auto &e : p->ev_hash) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (auto &e : p->ev_go) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    if (nbuf) HIPCHK(hipMemcpyAsync(p->d_blk_base, blk_base.data(), nbuf * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(p->d_blk_base, blk_base.data(), (nbuf + 1) * 4, hipMemcpyHostToDevice, s));
     P.blk_base = p->d_blk_base;
     HIPCHK(hipMalloc(&P.walk_slow, nb1 * 4));
     HIPCHK(hipMalloc(&P.buf_next, nb1 * 4));
@@ -689,6 +700,7 @@ extern "C" int xc_plan_destroy(xc_plan *p)
     hipFree(p->P.blk_pref);
     hipFree(p->d_chunk_blk);
     hipFree(p->d_blk_base);
+    hipFree(p->d_blk_buf);
     hipFree(p->d_l2mix);
     hipFree(p->P.walk_slow);
     hipFree(p->P.buf_next);
@@ -867,7 +879,7 @@ static int launch_walk_round(xc_plan *p, uint32_t j0, uint32_t j1, int use_d, in
     DeclArgs d{p->P, j0, j1};
     {
         KSpan span(p, XC_K_DECLHASH);
-        hipLaunchKernelGGL(k_declhash, dim3(j1 - j0, 8), dim3(64), 0, s, d);
+        hipLaunchKernelGGL(k_declhash, dim3((j1 - j0 + 3) / 4), dim3(256), 0, s, d);
         HIPCHK(hipGetLastError());
     }
     p->stats.walk_rounds++;
@@ -924,7 +936,8 @@ static int launch_first_round(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t s1,
     {
         DeclArgs d{p->P, j0, s1};
         KSpan span(p, XC_K_DECLHASH);
-        hipLaunchKernelGGL(k_blockpredict, dim3(s1 - j0), dim3(64), 0, s, d);
+        const uint32_t nblk = p->blk_base[s1] - p->blk_base[j0];
+        hipLaunchKernelGGL(k_blockpredict, dim3(std::max<uint32_t>(1u, (nblk + 255) / 256)), dim3(256), 0, s, d);
         HIPCHK(hipGetLastError());
     }
     // the next sub-batch's block hashes run beside this scan (memory-bound beside LDS/L2-bound)
