@@ -3,7 +3,7 @@
 // Reference: XCodecDecoder::decode (xcodec/xcodec_decoder.cc:76-176), one call per stream,
 // streams in index order, one shared XCodecMemoryCache.  Pipeline:
 //
-//   k_dtok     one wave per stream: F1 search by ballot over 256-byte windows -> tokens
+//   k_dtok     one wave per stream: F1 search in 1 KiB register windows -> tokens
 //              (literal run [lb, le) with F1 00 escapes, then the op at le)
 //   k_dhash    H of every EXTRACT payload (xcodec_hash.h:166-174)
 //   k_dres1    EXTRACT vs the cache: equal -> ok, different -> collision (decode returns
@@ -11,9 +11,9 @@
 //              by (stream, token) into the batch table
 //   k_dres2    every token against cache + earlier providers: REF data source or unknown
 //              (xcodec_decoder.cc:142-166); later duplicate EXTRACTs compared with the first
-//   k_dstop    per stream: first token that stops the decode
+//   k_dstop    per stream: first token that stops the decode, ENTER ordinals
 //   (host)     re-resolve if a provider lies past its own stream's stop (rare)
-//   k_dsize    per stream: output offsets of the executed tokens
+//   k_dalloc   cache slots of the ENTER tokens (prefix over streams)
 //   k_demit    unescape literals, copy EXTRACT payloads, gather REF segments
 //   k_dcommit  enter first-seen EXTRACT segments in the cache
 #include <hip/hip_runtime.h>
@@ -62,28 +62,54 @@ struct DecDev {
 
 enum : uint32_t { DCTL_FIX = 0, DCTL_ERR = 1, DCTL_NENTER = 2, DCTL_NREF = 3, DCTL_NEXTRACT = 4, DCTL_WORDS = 8 };
 
-// First F1 at or after p in [p, n), or n.
-__device__ __forceinline__ uint32_t find_magic(const uint8_t *s, uint32_t p, uint32_t n)
+// Tokenizer window: 1 KiB of the stream in registers (lane l: bytes w0 + 16 l .. + 15) and the
+// lane's mask of F1 bytes at positions in [from, n).
+struct DWin {
+    uint32_t w0;
+    uint4 v;
+    uint32_t m;
+};
+
+__device__ __forceinline__ uint32_t magic_mask16(const uint4 &v)
 {
-    const uint32_t l = lane_id();
-    for (uint32_t w0 = p & ~255u; w0 < n; w0 += 256u) {
-        const uint32_t o = w0 + 4u * l;
-        uint32_t m = 0;
+    uint32_t m = 0;
+    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (uint32_t k = 0; k < 4; k++) {
-            const uint32_t i = o + k;
-            if (i >= p && i < n && s[i] == XC_MAGIC) m |= 1u << k;
-        }
-        const uint64_t b = ballot(m != 0u);
-        if (b) {
-            const int f = __ffsll((unsigned long long)b) - 1;
-            return w0 + 4u * (uint32_t)f + (uint32_t)__builtin_ctz(readlane(m, f));
-        }
-    }
-    return n;
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+        for (int b = 0; b < 4; b++)
+            m |= ((d[k] >> (8 * b)) & 0xffu) == XC_MAGIC ? 1u << (4 * k + b) : 0u;
+    return m;
 }
 
-// Tokenizer (xcodec_decoder.cc:85-173).  fill = false only counts tokens.
+// Keep only mask bits of positions in [from, n).
+__device__ __forceinline__ uint32_t clip16(uint32_t m, uint32_t base, uint32_t from, uint32_t n)
+{
+    if (from > base) m = from - base >= 16u ? 0u : m & (0xFFFFu << (from - base));
+    if (n < base + 16u) m = n <= base ? 0u : m & ((1u << (n - base)) - 1u);
+    return m;
+}
+
+__device__ __forceinline__ void dwin_load(DWin &w, const uint8_t *s, uint32_t p, uint32_t n)
+{
+    // the stream arena is padded past every stream, so a whole window is always readable
+    w.w0 = p & ~15u;
+    const uint32_t base = w.w0 + 16u * lane_id();
+    w.v = *(const uint4 *)(s + base);
+    w.m = clip16(magic_mask16(w.v), base, p, n);
+}
+
+// Byte x of the stream, w0 <= x < w0 + 1024 (x uniform): from the window registers.
+__device__ __forceinline__ uint32_t dwin_byte(const DWin &w, uint32_t x)
+{
+    const uint32_t r = x - w.w0, k = (r >> 2) & 3u;
+    const uint32_t d = k == 0 ? w.v.x : k == 1 ? w.v.y : k == 2 ? w.v.z : w.v.w;
+    return (readlane(d, (int)(r >> 4)) >> (8 * (r & 3u))) & 0xffu;
+}
+
+// Tokenizer (xcodec_decoder.cc:85-173), one wave per stream: tokens are found inside 1 KiB
+// register windows (ESC and REF tokens, and the REF hash bytes, without another load); only an
+// EXTRACT, whose 2048-byte payload is skipped, or the window's end, loads a new window.
 __global__ __launch_bounds__(64) void k_dtok(DecDev D, int fill)
 {
     const uint32_t j = blockIdx.x;
@@ -101,24 +127,43 @@ __global__ __launch_bounds__(64) void k_dtok(DecDev D, int fill)
         }
         nt++;
     };
+    DWin w;
+    dwin_load(w, s, 0u, n);
     for (;;) {
-        const uint32_t q = find_magic(s, p, n);
-        if (q >= n) { put(T_END, n, 0); break; }
+        const uint64_t b = ballot(w.m != 0u);
+        if (!b) {
+            p = max(p, w.w0 + 1024u);  // (an ESC / REF may end past the window)
+            if (p >= n) { put(T_END, n, 0); break; }
+            dwin_load(w, s, p, n);
+            continue;
+        }
+        const int f = __ffsll((unsigned long long)b) - 1;
+        const uint32_t q = w.w0 + 16u * (uint32_t)f + (uint32_t)__builtin_ctz(readlane(w.m, f));
         if (q + 1u >= n) { put(T_WAIT, q, 0); break; }
-        const uint32_t op = s[q + 1];
-        if (op == 0x00u) { p = q + 2u; continue; }  // escape stays inside the literal run
+        const uint32_t op = q + 1u < w.w0 + 1024u ? dwin_byte(w, q + 1u) : s[q + 1u];
+        if (op == 0x00u) {  // escape: stays inside the literal run
+            p = q + 2u;
+            w.m = clip16(w.m, w.w0 + 16u * lane_id(), p, n);
+            continue;
+        }
         if (op == 0x01u) {
             if (n - q < 2u + XC_SEG) { put(T_WAIT, q, 0); break; }
             put(T_EXTRACT, q, 0);
             lb = p = q + 2u + XC_SEG;
+            dwin_load(w, s, p, n);
             continue;
         }
         if (op == 0x02u) {
             if (n - q < 10u) { put(T_WAIT, q, 0); break; }
             uint64_t h = 0;
-            for (uint32_t k = 0; k < 8; k++) h = (h << 8) | s[q + 2 + k];
+            if (q + 10u <= w.w0 + 1024u) {
+                for (uint32_t k = 0; k < 8; k++) h = (h << 8) | dwin_byte(w, q + 2u + k);
+            } else {
+                for (uint32_t k = 0; k < 8; k++) h = (h << 8) | s[q + 2u + k];
+            }
             put(T_REF, q, h);
             lb = p = q + 10u;
+            w.m = clip16(w.m, w.w0 + 16u * lane_id(), p, n);
             continue;
         }
         put(T_BADOP, q, 0);
@@ -214,37 +259,36 @@ __global__ __launch_bounds__(64) void k_dres2(DecDev D)
     }
 }
 
-// Per stream: executed token count and the decode's status / consumed bytes.
+// Per stream (one lane each): executed token count, the decode's status / consumed bytes, and
+// the ordinal of every first-seen EXTRACT (ENTER) among the stream's executed tokens, kept in
+// t_src (unused for ENTER tokens); s_slot[j] = the stream's ENTER count (k_dalloc prefixes it).
 __global__ __launch_bounds__(64) void k_dstop(DecDev D)
 {
     const uint32_t j = blockIdx.x * 64u + lane_id();
     if (j >= D.ns) return;
     const uint32_t tb = D.tok_base[j], n = D.tok_cnt[j];
-    uint32_t t = 0;
+    uint32_t t = 0, nr = 0, ne = 0, nent = 0;
     for (; t < n; t++) {
         const uint32_t op = D.t_op[tb + t], st = D.t_stat[tb + t];
         if (op != T_EXTRACT && op != T_REF) break;
         if (st == R_UNKNOWN || st == R_COLL) break;
+        nr += op == T_REF ? 1u : 0u;
+        ne += op == T_EXTRACT ? 1u : 0u;
+        if (st == R_ENTER) D.t_src[tb + t] = nent++;
     }
     // t = stopping token (terminal, unknown REF or colliding EXTRACT); its literal is output
     D.s_stop[j] = t + 1u;
+    D.s_slot[j] = nent;
     if (D.count) {  // executed REF / EXTRACT tokens (decode statistics)
-        uint32_t nr = 0, ne = 0;
-        for (uint32_t k = 0; k < t; k++) {
-            const uint32_t o = D.t_op[tb + k];
-            nr += o == T_REF ? 1u : 0u;
-            ne += o == T_EXTRACT ? 1u : 0u;
-        }
         if (nr) atomicAdd(&D.ctl[DCTL_NREF], nr);  // (lanes past ns have returned: no wave sums)
         if (ne) atomicAdd(&D.ctl[DCTL_NEXTRACT], ne);
     }
-    const uint32_t op = D.t_op[tb + t], st = D.t_stat[tb + t], le = D.t_le[tb + t];
+    const uint32_t op = D.t_op[tb + t], le = D.t_le[tb + t];
     int32_t status = 1, hu = 0;
     uint64_t cons = le, unk = 0;
     if (op == T_BADOP) status = 0;
     else if (op == T_REF) { hu = 1; unk = D.t_h[tb + t]; }              // unknown REF
     else if (op == T_EXTRACT) { status = 0; cons = le + 2u; }           // collision
-    (void)st;
     D.status[j] = status;
     D.consumed[j] = cons;
     D.has_unknown[j] = hu;
@@ -310,10 +354,18 @@ __device__ __forceinline__ void write_unescaped(uint8_t *dst, const uint8_t *p, 
 }
 
 constexpr uint32_t DMAX_TOK = 2048;
+constexpr uint32_t DEMIT_WAVES = 8;
 
-// Output offsets (executed tokens only), then the bytes.  One workgroup (4 waves) per
-// stream, tokens in blocks of DMAX_TOK.
-__global__ __launch_bounds__(256) void k_demit(DecDev D)
+__device__ __forceinline__ uint64_t dreadlane64(uint64_t x, int l)
+{
+    return ((uint64_t)readlane((uint32_t)(x >> 32), l) << 32) | readlane((uint32_t)x, l);
+}
+
+// Output offsets (executed tokens only), then the bytes.  One workgroup (8 waves) per stream,
+// tokens in blocks of DMAX_TOK: sizes lane-parallel (one token per lane; escapes counted only
+// in non-empty literal runs), a prefix, then each wave writes a contiguous token group with
+// two 2048-byte copies in flight.
+__global__ __launch_bounds__(64 * DEMIT_WAVES) void k_demit(DecDev D)
 {
     __shared__ uint64_t off[DMAX_TOK + 1];
     __shared__ uint64_t base_off;
@@ -328,12 +380,19 @@ __global__ __launch_bounds__(256) void k_demit(DecDev D)
     for (uint32_t t0 = 0; t0 < lim; t0 += DMAX_TOK) {
         const uint32_t nb = min(DMAX_TOK, lim - t0);
         __syncthreads();
-        for (uint32_t i = wave; i < nb; i += 4u) {
-            const uint32_t t = t0 + i;
-            const uint32_t lb = D.t_lb[tb + t], le = D.t_le[tb + t], op = D.t_op[tb + t];
-            uint32_t sz = (le - lb) - count_magic_d(s + lb, le - lb);
+        for (uint32_t i0 = wave * 64u; i0 < nb; i0 += 64u * DEMIT_WAVES) {
+            const uint32_t i = i0 + l, t = t0 + i;
+            uint32_t lb = 0, le = 0, op = T_END;
+            if (i < nb) { lb = D.t_lb[tb + t]; le = D.t_le[tb + t]; op = D.t_op[tb + t]; }
+            uint32_t sz = le - lb;
+            for (uint64_t m = ballot(le > lb); m; m &= m - 1) {
+                const int f = __ffsll((unsigned long long)m) - 1;
+                const uint32_t flb = readlane(lb, f), fle = readlane(le, f);
+                const uint32_t c = count_magic_d(s + flb, fle - flb);
+                if ((int)l == f) sz -= c;
+            }
             if (t + 1u != lim && (op == T_EXTRACT || op == T_REF)) sz += XC_SEG;
-            if (l == 0) off[i] = sz;
+            if (i < nb) off[i] = sz;
         }
         __syncthreads();
         if (wave == 0) {
@@ -352,24 +411,50 @@ __global__ __launch_bounds__(256) void k_demit(DecDev D)
             if (threadIdx.x == 0) atomicOr(&D.ctl[DCTL_ERR], 1u);
             return;
         }
-        for (uint32_t i = wave; i < nb; i += 4u) {
-            const uint32_t t = t0 + i;
-            const uint32_t lb = D.t_lb[tb + t], le = D.t_le[tb + t], op = D.t_op[tb + t];
-            write_unescaped(out + off[i], s + lb, le - lb);
-            if (t + 1u == lim) continue;  // the stop token contributes its literal only
-            uint8_t *o = out + off[i + 1] - XC_SEG;
-            if (op == T_EXTRACT) {
-                wave_copy(o, s + le + 2u, XC_SEG);
-            } else if (op == T_REF) {
-                const uint64_t src = D.t_src[tb + t];
-                const uint8_t *from;
-                if (src & SRC_PROV) {
-                    const uint32_t pj = (uint32_t)((src >> 32) & 0x7FFFFFFFu), pt = (uint32_t)src;
-                    from = D.in + D.in_off[pj] + D.t_le[D.tok_base[pj] + pt] + 2u;
-                } else {
-                    from = D.segs + src * XC_SEG;
+        // wave w: tokens [w G, (w+1) G) of the block, one per lane
+        const uint32_t G = (nb + DEMIT_WAVES - 1u) / DEMIT_WAVES;
+        const uint32_t g_end = min(nb, (wave + 1u) * G);
+        for (uint32_t g0 = wave * G; g0 < g_end; g0 += 64u) {
+            const uint32_t i = g0 + l, t = t0 + i;
+            const bool live = i < g_end;
+            uint32_t lb = 0, le = 0, op = T_END;
+            uint64_t from = 0;  // source of the token's 2048 bytes
+            if (live) {
+                lb = D.t_lb[tb + t];
+                le = D.t_le[tb + t];
+                op = t + 1u == lim ? T_END : D.t_op[tb + t];  // the stop token: its literal only
+                if (op == T_EXTRACT) {
+                    from = (uint64_t)(uintptr_t)(s + le + 2u);
+                } else if (op == T_REF) {
+                    const uint64_t src = D.t_src[tb + t];
+                    if (src & SRC_PROV) {
+                        const uint32_t pj = (uint32_t)((src >> 32) & 0x7FFFFFFFu), pt = (uint32_t)src;
+                        from = (uint64_t)(uintptr_t)(D.in + D.in_off[pj] + D.t_le[D.tok_base[pj] + pt] + 2u);
+                    } else {
+                        from = (uint64_t)(uintptr_t)(D.segs + src * XC_SEG);
+                    }
                 }
-                wave_copy(o, from, XC_SEG);
+            }
+            for (uint64_t m = ballot(live && le > lb); m; m &= m - 1) {
+                const int f = __ffsll((unsigned long long)m) - 1;
+                const uint32_t flb = readlane(lb, f);
+                write_unescaped(out + off[readlane(i, f)], s + flb, readlane(le, f) - flb);
+            }
+            for (uint64_t m = ballot(from != 0); m;) {
+                const int f0 = __ffsll((unsigned long long)m) - 1;
+                m &= m - 1;
+                const int f1 = m ? __ffsll((unsigned long long)m) - 1 : -1;
+                if (m) m &= m - 1;
+                uint8_t *d0 = out + off[readlane(i, f0) + 1u] - XC_SEG;
+                PayloadRegs r0, r1;
+                payload_load((const uint8_t *)(uintptr_t)dreadlane64(from, f0), d0, r0);
+                uint8_t *d1 = nullptr;
+                if (f1 >= 0) {
+                    d1 = out + off[readlane(i, f1) + 1u] - XC_SEG;
+                    payload_load((const uint8_t *)(uintptr_t)dreadlane64(from, f1), d1, r1);
+                }
+                payload_store(d0, nullptr, r0);
+                if (f1 >= 0) payload_store(d1, nullptr, r1);
             }
         }
     }
@@ -377,7 +462,8 @@ __global__ __launch_bounds__(256) void k_demit(DecDev D)
     if (threadIdx.x == 0) D.out_len[j] = base_off;
 }
 
-// Count ENTER tokens per stream (executed only) -> s_slot via one-workgroup prefix.
+// Cache slots of the streams' ENTER tokens: exclusive prefix of the per-stream counts k_dstop
+// left in s_slot, on top of the current segment count (one workgroup).
 __global__ __launch_bounds__(1024) void k_dalloc(DecDev D)
 {
     __shared__ uint32_t wsum[16];
@@ -388,11 +474,7 @@ __global__ __launch_bounds__(1024) void k_dalloc(DecDev D)
     const uint32_t start = carry;
     for (uint32_t j0 = 0; j0 < D.ns; j0 += 1024u) {
         const uint32_t j = j0 + threadIdx.x;
-        uint32_t v = 0;
-        if (j < D.ns) {
-            const uint32_t tb = D.tok_base[j], lim = min(D.tok_cnt[j], D.s_stop[j] - 1u);
-            for (uint32_t t = 0; t < lim; t++) v += D.t_stat[tb + t] == R_ENTER ? 1u : 0u;
-        }
+        const uint32_t v = j < D.ns ? D.s_slot[j] : 0u;
         const uint32_t inc = wave_incl_scan(v);
         if (l == 63) wsum[wave] = inc;
         __syncthreads();
@@ -415,16 +497,16 @@ __global__ __launch_bounds__(1024) void k_dalloc(DecDev D)
 }
 
 // XCodecMemoryCache::enter for first-seen EXTRACT payloads (xcodec_decoder.cc:133-135).
+// grid (streams, 8): wave y takes the stream's executed tokens y, y + 8, ...
 __global__ __launch_bounds__(64) void k_dcommit(DecDev D)
 {
     const uint32_t j = blockIdx.x;
     if (j >= D.ns) return;
     const uint8_t *s = D.in + D.in_off[j];
     const uint32_t tb = D.tok_base[j], lim = min(D.tok_cnt[j], D.s_stop[j] - 1u);
-    uint32_t k = 0;
-    for (uint32_t t = 0; t < lim; t++) {
+    for (uint32_t t = blockIdx.y; t < lim; t += gridDim.y) {
         if (uniform(D.t_stat[tb + t]) != R_ENTER) continue;
-        const uint32_t idx = D.s_slot[j] + k++;
+        const uint32_t idx = D.s_slot[j] + uniform((uint32_t)D.t_src[tb + t]);
         if (idx >= D.seg_cap) continue;
         wave_copy(D.segs + (size_t)idx * XC_SEG, s + D.t_le[tb + t] + 2u, XC_SEG);
         if (lane_id() == 0) {
@@ -639,11 +721,11 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
         DHIP(hipGetLastError());
         if (++rounds > 64) return xc__set_error(XC_EDEVICE, "decode provider resolution did not converge");
     }
-    hipLaunchKernelGGL(k_demit, dim3(ns), dim3(256), 0, s, D);
+    hipLaunchKernelGGL(k_demit, dim3(ns), dim3(64 * DEMIT_WAVES), 0, s, D);
     DHIP(hipGetLastError());
     hipLaunchKernelGGL(k_dalloc, dim3(1), dim3(1024), 0, s, D);
     DHIP(hipGetLastError());
-    hipLaunchKernelGGL(k_dcommit, dim3(ns), dim3(64), 0, s, D);
+    hipLaunchKernelGGL(k_dcommit, dim3(ns, 8), dim3(64), 0, s, D);
     DHIP(hipGetLastError());
     DHIP(hipMemcpyAsync(ctl, D.ctl, DCTL_WORDS * 4, hipMemcpyDeviceToHost, s));
     DHIP(hipStreamSynchronize(s));
