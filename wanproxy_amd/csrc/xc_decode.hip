@@ -313,6 +313,34 @@ __global__ __launch_bounds__(64) void k_dcheck(DecDev D, int round)
     }
 }
 
+// A resolution round's fresh batch provider table, its FIX flag and the token counters.
+__global__ void k_dclear(DecDev D, uint32_t n_lo, uint32_t n_full)
+{
+    const DevSet &s = D.dset;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint4 z = make_uint4(0, 0, 0, 0), ones = make_uint4(~0u, ~0u, ~0u, ~0u);
+    for (uint32_t i = i0; i < XC_FILT_WORDS / 4; i += stride) ((uint4 *)s.filt)[i] = z;
+    for (uint32_t i = i0; i < XC_L2_WORDS / 2; i += stride) ((uint4 *)s.l2)[i] = z;
+    for (uint32_t i = i0; i < n_lo / 4; i += stride) ((uint4 *)s.lo_keys)[i] = z;
+    for (uint32_t i = i0; i < n_full / 2; i += stride) {
+        ((uint4 *)s.keys)[i] = ones;
+        ((uint4 *)s.vals)[i] = ones;
+    }
+    if (i0 == 0) {
+        *s.lo_zero = 0u;
+        D.ctl[DCTL_FIX] = 0u;
+        D.ctl[DCTL_NREF] = 0u;
+        D.ctl[DCTL_NEXTRACT] = 0u;
+    }
+}
+
+// Emit kernels stand down while a resolution round asks for another one.
+__device__ __forceinline__ bool fix_pending(const DecDev &D)
+{
+    return __builtin_amdgcn_readfirstlane((int)*(volatile const uint32_t *)&D.ctl[DCTL_FIX]) != 0;
+}
+
 __global__ void k_dlim(DecDev D, int init)
 {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -367,6 +395,7 @@ __device__ __forceinline__ uint64_t dreadlane64(uint64_t x, int l)
 // two 2048-byte copies in flight.
 __global__ __launch_bounds__(64 * DEMIT_WAVES) void k_demit(DecDev D)
 {
+    if (fix_pending(D)) return;
     __shared__ uint64_t off[DMAX_TOK + 1];
     __shared__ uint64_t base_off;
     const uint32_t j = blockIdx.x;
@@ -466,6 +495,7 @@ __global__ __launch_bounds__(64 * DEMIT_WAVES) void k_demit(DecDev D)
 // left in s_slot, on top of the current segment count (one workgroup).
 __global__ __launch_bounds__(1024) void k_dalloc(DecDev D)
 {
+    if (fix_pending(D)) return;
     __shared__ uint32_t wsum[16];
     __shared__ uint32_t carry;
     const uint32_t wave = threadIdx.x >> 6, l = lane_id();
@@ -500,6 +530,7 @@ __global__ __launch_bounds__(1024) void k_dalloc(DecDev D)
 // grid (streams, 8): wave y takes the stream's executed tokens y, y + 8, ...
 __global__ __launch_bounds__(64) void k_dcommit(DecDev D)
 {
+    if (fix_pending(D)) return;
     const uint32_t j = blockIdx.x;
     if (j >= D.ns) return;
     const uint8_t *s = D.in + D.in_off[j];
@@ -687,7 +718,6 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
     D.unknown = d_unknown;
     D.has_unknown = d_has_unknown;
     const hipStream_t s = p->s;
-    DevSet &ds = D.dset;
     uint32_t ctl[DCTL_WORDS] = {};
     int rounds = 0;
     DHIP(hipMemsetAsync(D.ctl, 0, DCTL_WORDS * 4, s));
@@ -697,38 +727,43 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
     DHIP(hipGetLastError());
     hipLaunchKernelGGL(k_dlim, dim3((ns + 255) / 256), dim3(256), 0, s, D, 1);
     DHIP(hipGetLastError());
-    for (;;) {
-        DHIP(hipMemsetAsync(ds.filt, 0, XC_FILT_WORDS * 4, s));
-        DHIP(hipMemsetAsync(ds.l2, 0, (size_t)XC_L2_WORDS * 8, s));
-        DHIP(hipMemsetAsync(ds.lo_keys, 0, (size_t)p->n_lo * 4, s));
-        DHIP(hipMemsetAsync(ds.lo_zero, 0, 4, s));
-        DHIP(hipMemsetAsync(ds.keys, 0xFF, (size_t)p->n_full * 8, s));
-        DHIP(hipMemsetAsync(ds.vals, 0xFF, (size_t)p->n_full * 8, s));
-        DHIP(hipMemsetAsync(D.ctl, 0, 4, s));                                    // DCTL_FIX
-        DHIP(hipMemsetAsync(D.ctl + DCTL_NREF, 0, 8, s));                        // counters
+    // one provider-resolution round (a fresh batch table each time)
+    auto resolve_round = [&](int r) -> int {
+        hipLaunchKernelGGL(k_dclear, dim3(512), dim3(256), 0, s, D, p->n_lo, p->n_full);
+        DHIP(hipGetLastError());
         hipLaunchKernelGGL(k_dres1, dim3(ns, 8), dim3(64), 0, s, D);
         DHIP(hipGetLastError());
         hipLaunchKernelGGL(k_dres2, dim3(ns, 8), dim3(64), 0, s, D);
         DHIP(hipGetLastError());
         hipLaunchKernelGGL(k_dstop, dim3((ns + 63) / 64), dim3(64), 0, s, D);
         DHIP(hipGetLastError());
-        hipLaunchKernelGGL(k_dcheck, dim3(ns), dim3(64), 0, s, D, rounds);
+        hipLaunchKernelGGL(k_dcheck, dim3(ns), dim3(64), 0, s, D, r);
+        DHIP(hipGetLastError());
+        return XC_OK;
+    };
+    // output and cache commit: these kernels return at once while DCTL_FIX is set, so round 0
+    // and the emit are enqueued together and the host waits once in the common case
+    auto emit = [&]() -> int {
+        hipLaunchKernelGGL(k_demit, dim3(ns), dim3(64 * DEMIT_WAVES), 0, s, D);
+        DHIP(hipGetLastError());
+        hipLaunchKernelGGL(k_dalloc, dim3(1), dim3(1024), 0, s, D);
+        DHIP(hipGetLastError());
+        hipLaunchKernelGGL(k_dcommit, dim3(ns, 8), dim3(64), 0, s, D);
         DHIP(hipGetLastError());
         DHIP(hipMemcpyAsync(ctl, D.ctl, DCTL_WORDS * 4, hipMemcpyDeviceToHost, s));
         DHIP(hipStreamSynchronize(s));
-        if (!ctl[DCTL_FIX]) break;
+        return XC_OK;
+    };
+    int rc;
+    if ((rc = resolve_round(0)) || (rc = emit())) return rc;
+    while (ctl[DCTL_FIX]) {
+        // a provider lies past its own stream's stop: re-resolve with the executed prefixes
+        // as the only eligible providers, until the executed sets agree
+        if (++rounds > 64) return xc__set_error(XC_EDEVICE, "decode provider resolution did not converge");
         hipLaunchKernelGGL(k_dlim, dim3((ns + 255) / 256), dim3(256), 0, s, D, 0);
         DHIP(hipGetLastError());
-        if (++rounds > 64) return xc__set_error(XC_EDEVICE, "decode provider resolution did not converge");
+        if ((rc = resolve_round(rounds)) || (rc = emit())) return rc;
     }
-    hipLaunchKernelGGL(k_demit, dim3(ns), dim3(64 * DEMIT_WAVES), 0, s, D);
-    DHIP(hipGetLastError());
-    hipLaunchKernelGGL(k_dalloc, dim3(1), dim3(1024), 0, s, D);
-    DHIP(hipGetLastError());
-    hipLaunchKernelGGL(k_dcommit, dim3(ns, 8), dim3(64), 0, s, D);
-    DHIP(hipGetLastError());
-    DHIP(hipMemcpyAsync(ctl, D.ctl, DCTL_WORDS * 4, hipMemcpyDeviceToHost, s));
-    DHIP(hipStreamSynchronize(s));
     p->stats.in_bytes = p->in_total;
     p->stats.n_ref = ctl[DCTL_NREF];
     p->stats.n_extract = ctl[DCTL_NEXTRACT];
