@@ -14,8 +14,9 @@
 //   k_dstop    per stream: first token that stops the decode, ENTER ordinals
 //   (host)     re-resolve if a provider lies past its own stream's stop (rare)
 //   k_dalloc   cache slots of the ENTER tokens (prefix over streams)
-//   k_demit    unescape literals, copy EXTRACT payloads, gather REF segments
-//   k_dcommit  enter first-seen EXTRACT segments in the cache
+//   k_demit    unescape literals, copy EXTRACT payloads (first-seen ones into their cache
+//              slots too), gather REF segments
+//   k_dcommit  enter the first-seen EXTRACT hashes in the cache
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -448,12 +449,17 @@ __global__ __launch_bounds__(64 * DEMIT_WAVES) void k_demit(DecDev D)
             const bool live = i < g_end;
             uint32_t lb = 0, le = 0, op = T_END;
             uint64_t from = 0;  // source of the token's 2048 bytes
+            uint64_t seg = 0;   // first-seen EXTRACT: its cache slot (k_dalloc), written here too
             if (live) {
                 lb = D.t_lb[tb + t];
                 le = D.t_le[tb + t];
                 op = t + 1u == lim ? T_END : D.t_op[tb + t];  // the stop token: its literal only
                 if (op == T_EXTRACT) {
                     from = (uint64_t)(uintptr_t)(s + le + 2u);
+                    if (D.t_stat[tb + t] == R_ENTER) {
+                        const uint32_t idx = D.s_slot[j] + (uint32_t)D.t_src[tb + t];
+                        if (idx < D.seg_cap) seg = (uint64_t)(uintptr_t)(D.segs + (size_t)idx * XC_SEG);
+                    }
                 } else if (op == T_REF) {
                     const uint64_t src = D.t_src[tb + t];
                     if (src & SRC_PROV) {
@@ -482,8 +488,8 @@ __global__ __launch_bounds__(64 * DEMIT_WAVES) void k_demit(DecDev D)
                     d1 = out + off[readlane(i, f1) + 1u] - XC_SEG;
                     payload_load((const uint8_t *)(uintptr_t)dreadlane64(from, f1), d1, r1);
                 }
-                payload_store(d0, nullptr, r0);
-                if (f1 >= 0) payload_store(d1, nullptr, r1);
+                payload_store(d0, (uint8_t *)(uintptr_t)dreadlane64(seg, f0), r0);
+                if (f1 >= 0) payload_store(d1, (uint8_t *)(uintptr_t)dreadlane64(seg, f1), r1);
             }
         }
     }
@@ -528,23 +534,21 @@ __global__ __launch_bounds__(1024) void k_dalloc(DecDev D)
 
 // XCodecMemoryCache::enter for first-seen EXTRACT payloads (xcodec_decoder.cc:133-135).
 // grid (streams, 8): wave y takes the stream's executed tokens y, y + 8, ...
-__global__ __launch_bounds__(64) void k_dcommit(DecDev D)
+__global__ __launch_bounds__(256) void k_dcommit(DecDev D)
 {
     if (fix_pending(D)) return;
-    const uint32_t j = blockIdx.x;
+    // one wave per stream (4 per workgroup), one lane per token; k_demit already wrote the
+    // payloads into their slots
+    const uint32_t j = blockIdx.x * 4u + (threadIdx.x >> 6);
     if (j >= D.ns) return;
-    const uint8_t *s = D.in + D.in_off[j];
     const uint32_t tb = D.tok_base[j], lim = min(D.tok_cnt[j], D.s_stop[j] - 1u);
-    for (uint32_t t = blockIdx.y; t < lim; t += gridDim.y) {
-        if (uniform(D.t_stat[tb + t]) != R_ENTER) continue;
-        const uint32_t idx = D.s_slot[j] + uniform((uint32_t)D.t_src[tb + t]);
+    for (uint32_t t = lane_id(); t < lim; t += 64u) {
+        if (D.t_stat[tb + t] != R_ENTER) continue;
+        const uint32_t idx = D.s_slot[j] + (uint32_t)D.t_src[tb + t];
         if (idx >= D.seg_cap) continue;
-        wave_copy(D.segs + (size_t)idx * XC_SEG, s + D.t_le[tb + t] + 2u, XC_SEG);
-        if (lane_id() == 0) {
-            uint32_t s1, s2;
-            set_insert(D.cache, D.t_h[tb + t], idx, false, &s1, &s2);
-            D.undo[idx] = make_uint2(s1, s2);
-        }
+        uint32_t s1, s2;
+        set_insert(D.cache, D.t_h[tb + t], idx, false, &s1, &s2);
+        D.undo[idx] = make_uint2(s1, s2);
     }
 }
 
@@ -744,11 +748,11 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
     // output and cache commit: these kernels return at once while DCTL_FIX is set, so round 0
     // and the emit are enqueued together and the host waits once in the common case
     auto emit = [&]() -> int {
+        hipLaunchKernelGGL(k_dalloc, dim3(1), dim3(1024), 0, s, D);  // slots first: k_demit fills them
+        DHIP(hipGetLastError());
         hipLaunchKernelGGL(k_demit, dim3(ns), dim3(64 * DEMIT_WAVES), 0, s, D);
         DHIP(hipGetLastError());
-        hipLaunchKernelGGL(k_dalloc, dim3(1), dim3(1024), 0, s, D);
-        DHIP(hipGetLastError());
-        hipLaunchKernelGGL(k_dcommit, dim3(ns, 8), dim3(64), 0, s, D);
+        hipLaunchKernelGGL(k_dcommit, dim3((ns + 3) / 4), dim3(256), 0, s, D);
         DHIP(hipGetLastError());
         DHIP(hipMemcpyAsync(ctl, D.ctl, DCTL_WORDS * 4, hipMemcpyDeviceToHost, s));
         DHIP(hipStreamSynchronize(s));

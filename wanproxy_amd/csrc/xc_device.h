@@ -103,6 +103,19 @@ __device__ __forceinline__ uint32_t ffbl_byte(uint32_t x)
     return r;
 }
 
+// ffs of the four bytes of x, packed as bytes: each byte's ffbl is written into its own byte of
+// the result (SDWA dst_sel, the other bytes preserved), giving ffs - 1 with 0xFF for a zero
+// byte; a carry-free per-byte +1 (0xFF + 1 wraps to 0 = ffs(0)) finishes ffs.
+__device__ __forceinline__ uint32_t ffs_bytes(uint32_t x)
+{
+    uint32_t p;
+    asm("v_ffbl_b32_sdwa %0, %1 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:BYTE_0" : "=v"(p) : "v"(x));
+    asm("v_ffbl_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_1" : "+v"(p) : "v"(x));
+    asm("v_ffbl_b32_sdwa %0, %1 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2" : "+v"(p) : "v"(x));
+    asm("v_ffbl_b32_sdwa %0, %1 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_3" : "+v"(p) : "v"(x));
+    return ((p & 0x7F7F7F7Fu) + 0x01010101u) ^ (p & 0x80808080u);
+}
+
 __device__ __forceinline__ Sums4 chunk_sums32(const uint32_t w[8])
 {
     Sums4 s = {0, 0, 0, 0};
@@ -113,18 +126,15 @@ __device__ __forceinline__ Sums4 chunk_sums32(const uint32_t w[8])
         const uint32_t wt = (uint32_t)(4 * d) * 0x01010101u + 0x03020100u;
         sb = __builtin_amdgcn_udot4(w[d], 0x01010101u, sb, false);
         jb = __builtin_amdgcn_udot4(w[d], wt, jb, false);
-        // f - 1 per byte (ffbl): sum and j-weighted sum; the +1s are added back below
-        const uint32_t f0 = ffbl_byte<0>(w[d]), f1 = ffbl_byte<1>(w[d]);
-        const uint32_t f2 = ffbl_byte<2>(w[d]), f3 = ffbl_byte<3>(w[d]);
-        sf += f0 + f1 + f2 + f3;
-        // signed 24-bit multiplies (v_mad_i32_i24): ffbl(0) = -1 stays -1 in 24 bits
-        jf += (uint32_t)(__mul24((int)f0, 4 * d) + __mul24((int)f1, 4 * d + 1) + __mul24((int)f2, 4 * d + 2) +
-                         __mul24((int)f3, 4 * d + 3));
+        // f = ffs per byte (0..8), packed: plain and j-weighted byte dot products
+        const uint32_t f = ffs_bytes(w[d]);
+        sf = __builtin_amdgcn_udot4(f, 0x01010101u, sf, false);
+        jf = __builtin_amdgcn_udot4(f, wt, jf, false);
     }
     s.aw = sb + 32u;         // sum (b+1)
     s.bw = jb + 496u;        // sum j*(b+1), sum j = 496
-    s.af = sf + 32u;         // sum ffs(b) = sum (ffbl(b) + 1)
-    s.bf = jf + 496u;        // sum j*ffs(b)
+    s.af = sf;               // sum ffs(b)
+    s.bf = jf;               // sum j*ffs(b)
     return s;
 }
 
