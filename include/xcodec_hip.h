@@ -115,7 +115,7 @@ int xc_cache_restore_async(xc_cache *c);
 #define XC_K_SCAN 0
 #define XC_K_RESOLVE 1
 #define XC_K_WALK 2
-#define XC_K_DECLHASH 3   /* declaration prediction (k_blockpredict) and unknown declarations */
+#define XC_K_DECLHASH 3   /* declaration prediction (k_blockpredict); k_walk hashes the unknown ones */
 #define XC_K_EMIT 4
 #define XC_K_BLOCKHASH 5
 #define XC_K_COUNT 6

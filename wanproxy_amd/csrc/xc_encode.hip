@@ -9,8 +9,10 @@
 //   k_resolve(S)  per event: full 64-bit H, cache probe, 2048-byte compare -> EQUAL / COLL
 //   k_walk        per buffer: the sequential candidate/declare/reference state machine
 //                 (xcodec_encoder.cc:77-170) over the sparse events -> tokens
-//   k_declhash    per EXTRACT: H(segment) (xcodec_hash.h:166-174); declaration set D
-//   k_scan(D), k_resolve(D), k_walk, k_declhash  until D stops growing (self references)
+//                 (block-parallel when no event between aligned windows decides anything),
+//                 then H(segment) of declarations no event supplied (xcodec_hash.h:166-174)
+//                 into the declaration set D
+//   k_scan(D), k_resolve(D), k_walk  until D stops growing (self references)
 //   k_emit        tokens -> F1-escaped wire bytes; EXTRACT payloads entered in the cache
 //
 // Buffers are processed as if in index order against one cache: a buffer whose lookups
@@ -625,20 +627,16 @@ __device__ __forceinline__ EvInfo event_at(const PlanDev &P, const Layer &L, Cur
 
 constexpr uint32_t R_MISS = 0, R_HIT = 1, R_COLL = 2;
 
-__global__ __launch_bounds__(64) void k_walk(WalkArgs a)
+// The sequential walk of buffer b (one wave).
+__device__ __forceinline__ void walk_seq(const WalkArgs &a, uint32_t b, uint64_t *walk_lds)
 {
-    if (aborted(a.P)) return;
     // declarations of this buffer (sized by the plan's longest buffer, so short buffers leave
     // room for many walk waves per CU) and the aligned REFs emitted, one bit per block
-    extern __shared__ uint64_t walk_lds[];
     uint64_t *d_hash = walk_lds;
     uint32_t *d_cand = (uint32_t *)(walk_lds + a.max_decl);
     uint32_t *d_known = d_cand + a.max_decl;
     uint32_t *ref_done = d_known + a.max_decl;
     const PlanDev &P = a.P;
-    const uint32_t b = a.j0 + blockIdx.x;
-    if (b >= a.j1) return;
-    if (a.only_slow && !P.walk_slow[b]) return;  // k_walk_blocks walked it
     const uint32_t l = lane_id();
     const uint32_t len = P.buf_len[b];
     const uint8_t *base = P.in + P.buf_off[b];
@@ -657,7 +655,7 @@ __global__ __launch_bounds__(64) void k_walk(WalkArgs a)
     bool noflush = false;
     if (P.stream_st) {
         // a stream's pending source_: window ends below start were looked up by earlier calls
-        // (xcodec_encoder.cc:72-118), a pending candidate carries over (its hash: k_declhash)
+        // (xcodec_encoder.cc:72-118), a pending candidate carries over (its hash: decl_hash)
         const uint4 st = P.stream_st[b];
         p = max(p, uniform(st.x));
         if (uniform(st.y) != NONE) cand = (int)uniform(st.y);
@@ -810,7 +808,7 @@ __global__ __launch_bounds__(64) void k_walk(WalkArgs a)
     }
 }
 
-// ----------------------------------------------------------- k_walk_blocks --------------
+// ------------------------------------------------------------ walk_blocks ----------------
 // The first-round walk of a buffer whose events decide nothing between its aligned windows
 // (hit-free data and block-aligned repeats: every cfg workload), lane-parallel.  In k_walk's
 // state machine (xcodec_encoder.cc:77-170) a lookup with no candidate pending happens only at
@@ -824,22 +822,18 @@ __global__ __launch_bounds__(64) void k_walk(WalkArgs a)
 // reduction fails on a collision (the next candidate becomes unaligned), an unaligned event
 // that is a hit / collision / declaration match, a dense chunk, or a block repeating an earlier
 // new block of the same buffer (a self-REF that needs a byte compare; the declaration set's
-// min-merged value tells).  Such buffers are flagged in P.walk_slow for the sequential k_walk.
-__global__ __launch_bounds__(64) void k_walk_blocks(WalkArgs a)
+// min-merged value tells).  Such buffers take the sequential walk.
+// Returns false (nothing written that the sequential walk would not rewrite) when the
+// reduction does not apply to buffer b.
+__device__ __forceinline__ bool walk_blocks(const WalkArgs &a, uint32_t b)
 {
-    if (aborted(a.P)) return;
     const PlanDev &P = a.P;
-    const uint32_t b = a.j0 + blockIdx.x;
-    if (b >= a.j1) return;
     const uint32_t l = lane_id();
     const uint32_t len = P.buf_len[b];
     const uint32_t nblk = len / XC_SEG;
     const uint32_t ck0 = P.buf_chunk0[b], ck1 = P.buf_chunk0[b + 1];
     const uint32_t tb = P.tok_base[b];
-    if (!stream_plain(P, b)) {  // carried state or no flush: the sequential walk
-        if (l == 0) P.walk_slow[b] = 1u;
-        return;
-    }
+    if (!stream_plain(P, b)) return false;  // carried state or no flush: the sequential walk
     bool ok = true, cross = false;
     uint32_t n_ext = 0, n_ref = 0;
     for (uint32_t c = ck0; c < ck1 && ballot(!ok) == 0; c++) {
@@ -882,10 +876,7 @@ __global__ __launch_bounds__(64) void k_walk_blocks(WalkArgs a)
         }
         if ((uint32_t)__popcll(ballot(aligned)) != want) ok = false;  // each aligned end, once
     }
-    if (ballot(!ok)) {
-        if (l == 0) P.walk_slow[b] = 1u;
-        return;
-    }
+    if (ballot(!ok)) return false;
     n_ext = wave_sum(n_ext);
     n_ref = wave_sum(n_ref);
     const bool any_cross = ballot(cross) != 0;
@@ -901,22 +892,18 @@ __global__ __launch_bounds__(64) void k_walk_blocks(WalkArgs a)
         P.tok_cnt[b] = nblk + 1u;
         P.buf_next[b] = n_ext;
         P.buf_nref[b] = n_ref;
-        P.walk_slow[b] = 0u;
         if (P.stream_res) P.stream_res[b] = make_uint2(len, NONE);  // flushed: source_ empty
         if (any_cross) atomicMin(&P.ctl[CTL_FIRST_CROSS], b);
     }
+    return true;
 }
 
-// ------------------------------------------------------------ k_declhash ----------------
-// One wave per buffer (4 per workgroup): the EXTRACT tokens whose hash no resolved event
-// supplied are hashed and entered into the declaration set (value = b<<32 | declaration
-// position, min-merged); any such entry means the scan missed it: another round.
-__global__ __launch_bounds__(256) void k_declhash(DeclArgs a)
+// ------------------------------------------------------------ k_walk ---------------------
+// The EXTRACT tokens of buffer b whose hash no resolved event supplied are hashed and entered
+// into the declaration set (value = b<<32 | declaration position, min-merged); any such entry
+// means the scan missed it: another round.
+__device__ __forceinline__ void decl_hash(const PlanDev &P, uint32_t b)
 {
-    if (aborted(a.P)) return;
-    const PlanDev &P = a.P;
-    const uint32_t b = a.j0 + blockIdx.x * 4u + (threadIdx.x >> 6);
-    if (b >= a.j1) return;
     const uint32_t l = lane_id();
     const uint8_t *base = P.in + P.buf_off[b];
     const uint32_t tb = P.tok_base[b], n = P.tok_cnt[b];
@@ -939,23 +926,35 @@ __global__ __launch_bounds__(256) void k_declhash(DeclArgs a)
     }
 }
 
-// grid (buffers, 4): hash of every aligned 2048-byte block (a wave hashes 8 blocks with all
-// loads in flight together).  Depends on the input only, so it runs ahead on a side stream.
-constexpr uint32_t BLK_GROUP = 8;
-
-__global__ __launch_bounds__(64) void k_blockhash(DeclArgs a)
+// One wave per buffer: the first round tries the block-parallel walk, else (and in later rounds)
+// the sequential walk; then the declarations whose hash is still unknown are hashed.
+__global__ __launch_bounds__(64) void k_walk(WalkArgs a)
 {
-    const PlanDev &P = a.P;
+    if (aborted(a.P)) return;
+    extern __shared__ uint64_t walk_lds[];
     const uint32_t b = a.j0 + blockIdx.x;
     if (b >= a.j1) return;
+    if (a.use_d || !walk_blocks(a, b)) walk_seq(a, b, walk_lds);
+    decl_hash(a.P, b);
+}
+
+// Hash of every aligned 2048-byte block, one wave per group of <= BLK_GROUP consecutive blocks
+// of one buffer (P.blk_grp; [a.j0, a.j1) is a range of groups), four waves per workgroup: a
+// wave has all its loads in flight together.  Depends on the input only, so it runs ahead on a
+// side stream.  (One-wave workgroups made this kernel dispatch-bound.)
+constexpr uint32_t BLK_GROUP = 8;
+
+__global__ __launch_bounds__(256) void k_blockhash(DeclArgs a)
+{
+    const PlanDev &P = a.P;
+    const uint32_t g = a.j0 + blockIdx.x * 4u + (threadIdx.x >> 6);
+    if (g >= a.j1) return;
+    const uint2 gr = P.blk_grp[g];
+    const uint32_t b = gr.x, k0 = gr.y;
     const uint8_t *base = P.in + P.buf_off[b];
-    const uint32_t nblk = P.buf_len[b] / XC_SEG, bb = P.blk_base[b];
-    const uint32_t l = lane_id();
-    for (uint32_t k0 = blockIdx.y * BLK_GROUP; k0 < nblk; k0 += gridDim.y * BLK_GROUP) {
-        const uint32_t n = min(BLK_GROUP, nblk - k0);
-        const uint64_t h = wave_block_hashes<BLK_GROUP>(base + (size_t)k0 * XC_SEG, n);
-        if (l < n) P.blk_h[bb + k0 + l] = h;
-    }
+    const uint32_t n = min(BLK_GROUP, P.buf_len[b] / XC_SEG - k0);
+    const uint64_t h = wave_block_hashes<BLK_GROUP>(base + (size_t)k0 * XC_SEG, n);
+    if (lane_id() < n) P.blk_h[P.blk_base[b] + k0 + lane_id()] = h;
 }
 
 // One lane per aligned block of buffers [j0, j1) (P.blk_buf maps a block to its buffer):

@@ -75,6 +75,7 @@ struct PlanDev {
     uint32_t *tok_known;       // EXTRACT hash known from a resolved event (no rehash needed)
     const uint32_t *blk_base;  // [nb + 1] first aligned-block index of the buffer
     const uint32_t *blk_buf;   // [blocks] buffer of every aligned block
+    const uint2 *blk_grp;      // [groups] (buffer, first block) of every k_blockhash group
     uint64_t *blk_h;           // hash of every aligned 2048-byte block (k_blockhash)
     uint64_t *tok_h;
     uint32_t *buf_next;   // [nb] EXTRACT tokens of the buffer (walk)
@@ -91,7 +92,6 @@ struct PlanDev {
     // skip the next block's windows and the walk verifies that the REF happened.
     uint32_t *blk_pref;
     const uint32_t *chunk_blk;  // [nchunks] global index of the chunk's buffer's block 0
-    uint32_t *walk_slow;        // [nb] k_walk_blocks left this buffer to the sequential walk
     // Stateful streams (xc_encode / xc_flush, xcodec_encoder.cc:60-201 across calls), or null
     // when every buffer is a fresh encoder's encode + flush.  stream_st[b] = {start, cand0,
     // flags, 0}: the buffer is the encoder's pending source_ (start bytes, whose window ends
@@ -147,7 +147,6 @@ struct WalkArgs {
     int use_d;  // 0 on the first round (no declaration layer yet)
     int shadow; // the scan skipped predicted-REF shadows: verify every such REF was emitted
     uint32_t max_decl;  // >= declarations of any buffer (longest buffer / 2048 + 2)
-    int only_slow;      // k_walk: only the buffers k_walk_blocks flagged in P.walk_slow
 };
 // dynamic LDS of k_walk
 __host__ __device__ constexpr uint32_t walk_lds_bytes(uint32_t max_decl) { return max_decl * 16u + 8u * (max_decl / 32u + 1u); }
@@ -178,8 +177,6 @@ __global__ void k_pack_offsets(PackArgs a);
 __global__ void k_pack_copy(PackArgs a);
 __global__ void k_resolve(ResolveArgs a);
 __global__ void k_walk(WalkArgs a);
-__global__ void k_walk_blocks(WalkArgs a);
-__global__ void k_declhash(DeclArgs a);
 __global__ void k_blockhash(DeclArgs a);
 __global__ void k_blockpredict(DeclArgs a);
 __global__ void k_or_words(uint4 *dst, const uint4 *a, const uint4 *b, uint32_t n);

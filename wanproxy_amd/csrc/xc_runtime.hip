@@ -426,6 +426,8 @@ struct xc_plan {
     uint4 *d_desc;
     uint32_t *d_blk_base, *d_blk_buf = nullptr;
     std::vector<uint32_t> blk_base;  // host copy [nb + 1]
+    uint2 *d_blk_grp = nullptr;      // k_blockhash groups
+    std::vector<uint32_t> grp_base;  // [nb + 1] first group of every buffer
     uint32_t *d_l2mix;  // level-2 filter of cache | declaration set for the combined scan
     xc_run_stats stats{};
     // per-kernel HIP-event timing: 0 off, XC_TIMING_ALL every kernel, XC_TIMING_SCAN the scans only
@@ -650,6 +652,18 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
         HIPCHK(hipMemcpyAsync(p->d_blk_buf, bb.data(), bb.size() * 4, hipMemcpyHostToDevice, s));
         P.blk_buf = p->d_blk_buf;
         p->blk_base = blk_base;
+        // block-hash groups: up to 8 consecutive blocks of one buffer
+        std::vector<uint2> grp;
+        p->grp_base.assign(nbuf + 1, 0);
+        for (uint64_t i = 0; i < nbuf; i++) {
+            p->grp_base[i] = (uint32_t)grp.size();
+            for (uint32_t k0 = 0; k0 < blk_base[i + 1] - blk_base[i]; k0 += 8) grp.push_back(make_uint2((uint32_t)i, k0));
+        }
+        p->grp_base[nbuf] = (uint32_t)grp.size();
+        HIPCHK(hipMalloc(&p->d_blk_grp, std::max<size_t>(grp.size(), 1) * sizeof(uint2)));
+        if (!grp.empty())
+            HIPCHK(hipMemcpyAsync(p->d_blk_grp, grp.data(), grp.size() * sizeof(uint2), hipMemcpyHostToDevice, s));
+        P.blk_grp = p->d_blk_grp;
     }
     HIPCHK(hipMalloc(&p->d_l2mix, (size_t)XC_L2_WORDS * 8));
     P.l2mix = p->d_l2mix;
@@ -661,7 +675,6 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     for (auto &e : p->ev_go) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHK(hipMemcpyAsync(p->d_blk_base, blk_base.data(), (nbuf + 1) * 4, hipMemcpyHostToDevice, s));
     P.blk_base = p->d_blk_base;
-    HIPCHK(hipMalloc(&P.walk_slow, nb1 * 4));
     HIPCHK(hipMalloc(&P.buf_next, nb1 * 4));
     HIPCHK(hipMalloc(&P.buf_nref, nb1 * 4));
     HIPCHK(hipMalloc(&P.buf_slot, nb1 * 4));
@@ -701,8 +714,8 @@ extern "C" int xc_plan_destroy(xc_plan *p)
     hipFree(p->d_chunk_blk);
     hipFree(p->d_blk_base);
     hipFree(p->d_blk_buf);
+    hipFree(p->d_blk_grp);
     hipFree(p->d_l2mix);
-    hipFree(p->P.walk_slow);
     hipFree(p->P.buf_next);
     hipFree(p->P.buf_nref);
     hipFree(p->P.buf_slot);
@@ -864,22 +877,13 @@ static int launch_walk_round(xc_plan *p, uint32_t j0, uint32_t j1, int use_d, in
 {
     hipStream_t s = p->cache->ctx->stream;
     // (k_resolve, always launched just before, reset GREW / FIRST_CROSS / SHADOW)
-    // first round: the block-parallel walk (k_walk_blocks), then the sequential walk for the
-    // buffers it flagged; later rounds (declaration layer) walk every buffer sequentially
-    WalkArgs w{p->P, j0, j1, use_d, shadow, p->max_decl, use_d ? 0 : 1};
+    // one wave per buffer: the block-parallel walk on the first round where it applies, else
+    // the sequential walk (every buffer on the declaration-layer rounds), then the hashes of
+    // declarations no event supplied
+    WalkArgs w{p->P, j0, j1, use_d, shadow, p->max_decl};
     {
         KSpan span(p, XC_K_WALK);
-        if (!use_d) {
-            hipLaunchKernelGGL(k_walk_blocks, dim3(j1 - j0), dim3(64), 0, s, w);
-            HIPCHK(hipGetLastError());
-        }
         hipLaunchKernelGGL(k_walk, dim3(j1 - j0), dim3(64), walk_lds_bytes(p->max_decl), s, w);
-        HIPCHK(hipGetLastError());
-    }
-    DeclArgs d{p->P, j0, j1};
-    {
-        KSpan span(p, XC_K_DECLHASH);
-        hipLaunchKernelGGL(k_declhash, dim3((j1 - j0 + 3) / 4), dim3(256), 0, s, d);
         HIPCHK(hipGetLastError());
     }
     p->stats.walk_rounds++;
@@ -906,10 +910,11 @@ static int enqueue_block_hash(xc_plan *p, uint32_t k, hipEvent_t after)
 {
     HIPCHK(hipStreamWaitEvent(p->hs, after, 0));
     if (p->host_path) HIPCHK(hipStreamWaitEvent(p->hs, p->ev_h2d[k], 0));  // its input has landed
-    DeclArgs d{p->P, p->sub[k], p->sub[k + 1]};
-    {
+    const uint32_t g0 = p->grp_base[p->sub[k]], g1 = p->grp_base[p->sub[k + 1]];
+    DeclArgs d{p->P, g0, g1};  // a range of block groups
+    if (g1 > g0) {
         KSpan span(p, XC_K_BLOCKHASH, p->hs);
-        hipLaunchKernelGGL(k_blockhash, dim3(p->sub[k + 1] - p->sub[k], 4), dim3(64), 0, p->hs, d);
+        hipLaunchKernelGGL(k_blockhash, dim3((g1 - g0 + 3) / 4), dim3(256), 0, p->hs, d);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(p->ev_hash[k], p->hs));
