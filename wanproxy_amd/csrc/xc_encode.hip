@@ -976,11 +976,8 @@ __global__ __launch_bounds__(256) void k_blockpredict(DeclArgs a)
     uint64_t v;
     const bool cached = set_find(P.cache, h, &v);
     P.blk_pref[g] = cached ? 1u : 0u;
-    if (!cached && set_insert(P.dset, h, ((uint64_t)b << 32) | (k * XC_SEG + 2u * XC_SEG - 1u), true, nullptr, nullptr)) {
-        const uint32_t gm = l2_mix((uint32_t)h), gi = (gm >> 14) * 2u;
-        atomicOr(&P.l2mix[gi], 1u << (gm & 31u));
-        atomicOr(&P.l2mix[gi + 1u], 1u << ((gm >> 5) & 31u));
-    }
+    // (the set's level-2 filter is P.l2mix, the combined filter the scan reads)
+    if (!cached) set_insert(P.dset, h, ((uint64_t)b << 32) | (k * XC_SEG + 2u * XC_SEG - 1u), true, nullptr, nullptr);
 }
 
 // -------------------------------------------------------------- k_emit ------------------
@@ -1328,8 +1325,9 @@ __global__ void k_clear_set(DevSet s, uint32_t n_lo, uint32_t n_full, uint4 *l2m
     const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
     const uint4 z = make_uint4(0, 0, 0, 0), ones = make_uint4(~0u, ~0u, ~0u, ~0u);
     for (uint32_t i = i0; i < XC_FILT_WORDS / 4; i += stride) ((uint4 *)s.filt)[i] = z;
+    const bool own_l2 = (const void *)s.l2 != (const void *)l2mix;  // (plans alias the two)
     for (uint32_t i = i0; i < XC_L2_WORDS / 2; i += stride) {
-        ((uint4 *)s.l2)[i] = z;
+        if (own_l2) ((uint4 *)s.l2)[i] = z;
         l2mix[i] = cache_l2[i];
     }
     for (uint32_t i = i0; i < n_lo / 4; i += stride) ((uint4 *)s.lo_keys)[i] = z;

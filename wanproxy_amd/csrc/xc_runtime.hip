@@ -667,6 +667,9 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     }
     HIPCHK(hipMalloc(&p->d_l2mix, (size_t)XC_L2_WORDS * 8));
     P.l2mix = p->d_l2mix;
+    // the declaration set's level-2 filter is the combined one (cache | declarations): every
+    // declaration insert lands there directly, and the declaration-layer scans test a superset
+    P.dset.l2 = p->d_l2mix;
     HIPCHK(hipStreamCreateWithFlags(&p->hs, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&p->ev_start, hipEventDisableTiming));
     p->ev_hash.assign(p->sub.size(), nullptr);
