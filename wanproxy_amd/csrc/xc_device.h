@@ -162,15 +162,60 @@ __device__ __forceinline__ uint64_t wave_window_hash(const uint8_t *p)
     return wave_hash_regs(w);
 }
 
-// Hashes of n <= G consecutive 16-byte-aligned blocks at p: all loads are issued first, then
-// lane i (< n) receives block i's hash.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_perm(uint32_t x)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, false);
+}
+
+// Butterfly step: each lane keeps half of its values, the partner (an involution differing in
+// `bit` of the lane id) sends the other half.  After it, lane l holds half as many sums.
+template <int H, int CTRL>
+__device__ __forceinline__ void bfly_dpp(uint32_t v[], uint32_t bit)
+{
+#pragma unroll
+    for (int i = 0; i < H; i++) {
+        const uint32_t send = bit ? v[i] : v[i + H], keep = bit ? v[i + H] : v[i];
+        v[i] = keep + dpp_perm<CTRL>(send);
+    }
+}
+
+// Transposed wave reduction of 32 values per lane: lane l returns the 64-lane sum of value
+// (l >> 1) & 31.  Butterflies over the lane bits 5, 4 (v_permlane32/16_swap: no selects), 3, 2
+// (row_mirror, row_half_mirror: partners differ in that bit, and in lower ones, which the later
+// steps cover), 1, 0 (quad_perm): 70 VALU instead of 32 separate 6-step scans.
+__device__ __forceinline__ uint32_t wave_sums32(uint32_t v[32])
+{
+    const uint32_t l = lane_id();
+#pragma unroll
+    for (int i = 0; i < 16; i++) {  // lanes < 32 keep value i, lanes >= 32 value i + 16
+        const auto r = __builtin_amdgcn_permlane32_swap(v[i], v[i + 16], false, false);
+        v[i] = r[0] + r[1];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) {   // even rows keep value i, odd rows value i + 8
+        const auto r = __builtin_amdgcn_permlane16_swap(v[i], v[i + 8], false, false);
+        v[i] = r[0] + r[1];
+    }
+    bfly_dpp<4, 0x140>(v, (l >> 3) & 1u);  // row_mirror: lane j <-> 15 - j
+    bfly_dpp<2, 0x141>(v, (l >> 2) & 1u);  // row_half_mirror: lane j <-> 7 - j
+    bfly_dpp<1, 0x4E>(v, (l >> 1) & 1u);   // quad_perm [2,3,0,1]
+    return v[0] + dpp_perm<0xB1>(v[0]);    // quad_perm [1,0,3,2]
+}
+
+// Hashes of n <= 8 consecutive 16-byte-aligned blocks at p: all loads are issued first, then
+// lane i (< n) receives block i's hash.  The 4 window sums of the 8 blocks are reduced together
+// (wave_sums32): value 4 i + c lands in lanes 8 i + 2 c (and + 1).
 template <int G>
 __device__ __forceinline__ uint64_t wave_block_hashes(const uint8_t *p, uint32_t n)
 {
+    static_assert(G == 8, "8 blocks x 4 sums fill the 32-value transposed reduction");
     const uint32_t l = lane_id();
     uint32_t w[G][8];
 #pragma unroll
     for (int i = 0; i < G; i++) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) w[i][k] = 0u;
         if ((uint32_t)i < n) {
             const uint4 *q = (const uint4 *)(p + (size_t)i * XC_SEG + 32u * l);
             const uint4 x = q[0], y = q[1];
@@ -178,15 +223,22 @@ __device__ __forceinline__ uint64_t wave_block_hashes(const uint8_t *p, uint32_t
             w[i][4] = y.x; w[i][5] = y.y; w[i][6] = y.z; w[i][7] = y.w;
         }
     }
-    uint64_t mine = 0;
+    uint32_t v[32];
+    const uint32_t k = XC_SEG - 32u * l;  // weight of this lane's byte 0 is (2048 - 32l)
 #pragma unroll
     for (int i = 0; i < G; i++) {
-        if ((uint32_t)i < n) {
-            const uint64_t h = wave_hash_regs(w[i]);
-            if (l == (uint32_t)i) mine = h;
-        }
+        const Sums4 s = chunk_sums32(w[i]);
+        v[4 * i + 0] = s.aw;
+        v[4 * i + 1] = k * s.aw - s.bw;
+        v[4 * i + 2] = s.af;
+        v[4 * i + 3] = k * s.af - s.bf;
     }
-    return mine;
+    const uint32_t sum = wave_sums32(v);
+    const int src = (int)(8u * (l & 7u));
+    const uint32_t s1w = (uint32_t)__shfl((int)sum, src), s2w = (uint32_t)__shfl((int)sum, src + 2);
+    const uint32_t s1f = (uint32_t)__shfl((int)sum, src + 4), s2f = (uint32_t)__shfl((int)sum, src + 6);
+    const uint32_t bytes_hash = (s1w << 20) + s2w, bits_hash = (s1f << 16) + s2f;
+    return ((uint64_t)bits_hash << 36) + (uint64_t)bytes_hash;
 }
 
 // 2048-byte equality of two windows (any alignment); wave-uniform result.
