@@ -88,21 +88,10 @@ struct Sums4 {
     uint32_t aw, bw, af, bf;
 };
 
-// ffbl of byte K of x, minus... exactly: v_ffbl_b32 on the zero-extended byte, which the
-// hardware defines as 0xFFFFFFFF for a zero byte, so ffbl + 1 == ffs(byte) with ffs(0) == 0
-// (xcodec/xcodec_hash.h:95-96) and no compare/select.  Inline asm: the compiler's cttz would
-// add the zero test back.
-template <int K>
-__device__ __forceinline__ uint32_t ffbl_byte(uint32_t x)
-{
-    uint32_t r;
-    if (K == 0) asm("v_ffbl_b32_sdwa %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0" : "=v"(r) : "v"(x));
-    if (K == 1) asm("v_ffbl_b32_sdwa %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1" : "=v"(r) : "v"(x));
-    if (K == 2) asm("v_ffbl_b32_sdwa %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2" : "=v"(r) : "v"(x));
-    if (K == 3) asm("v_ffbl_b32_sdwa %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3" : "=v"(r) : "v"(x));
-    return r;
-}
-
+// ffs per byte uses v_ffbl_b32 on the zero-extended byte (SDWA src0_sel), which the hardware
+// defines as 0xFFFFFFFF for a zero byte: ffbl + 1 == ffs(byte) with ffs(0) == 0
+// (xcodec/xcodec_hash.h:95-96) and no compare/select.  Inline asm: the compiler's cttz would add
+// the zero test back.
 // ffs of the four bytes of x, packed as bytes: each byte's ffbl is written into its own byte of
 // the result (SDWA dst_sel, the other bytes preserved), giving ffs - 1 with 0xFF for a zero
 // byte; a carry-free per-byte +1 (0xFF + 1 wraps to 0 = ffs(0)) finishes ffs.
@@ -138,6 +127,13 @@ __device__ __forceinline__ Sums4 chunk_sums32(const uint32_t w[8])
     return s;
 }
 
+// Lane permutation by a DPP control (quad_perm, row_mirror, row_half_mirror, ...).
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_perm(uint32_t x)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, false);
+}
+
 // Full hash of a 2048-byte window held as 32 bytes per lane (lane l: bytes 32l..32l+31);
 // every lane returns the result.
 __device__ __forceinline__ uint64_t wave_hash_regs(const uint32_t w[8])
@@ -145,10 +141,23 @@ __device__ __forceinline__ uint64_t wave_hash_regs(const uint32_t w[8])
     const uint32_t l = lane_id();
     Sums4 s = chunk_sums32(w);
     const uint32_t k = XC_SEG - 32u * l;  // weight of this lane's byte 0 is (2048 - 32l)
-    uint32_t s1w = wave_sum(s.aw);
-    uint32_t s2w = wave_sum(k * s.aw - s.bw);
-    uint32_t s1f = wave_sum(s.af);
-    uint32_t s2f = wave_sum(k * s.af - s.bf);
+    // transposed reduction of the 4 sums: permlane swaps over lane bits 5 and 4 leave value
+    // 2 bit5 + bit4 in each 16-lane row, then a row sum
+    uint32_t v0 = s.aw, v1 = k * s.aw - s.bw, v2 = s.af, v3 = k * s.af - s.bf;
+    {
+        const auto r = __builtin_amdgcn_permlane32_swap(v0, v2, false, false);
+        const auto q = __builtin_amdgcn_permlane32_swap(v1, v3, false, false);
+        v0 = r[0] + r[1];  // lanes < 32: value 0, lanes >= 32: value 2
+        v1 = q[0] + q[1];  // lanes < 32: value 1, lanes >= 32: value 3
+        const auto t = __builtin_amdgcn_permlane16_swap(v0, v1, false, false);
+        v0 = t[0] + t[1];  // row r holds value r
+    }
+    v0 += dpp_perm<0x140>(v0);  // row_mirror
+    v0 += dpp_perm<0x141>(v0);  // row_half_mirror
+    v0 += dpp_perm<0x4E>(v0);   // quad_perm [2,3,0,1]
+    v0 += dpp_perm<0xB1>(v0);   // quad_perm [1,0,3,2]: every lane of row r: the sum of value r
+    const uint32_t s1w = readlane(v0, 0), s2w = readlane(v0, 16);
+    const uint32_t s1f = readlane(v0, 32), s2f = readlane(v0, 48);
     uint32_t bytes_hash = (s1w << 20) + s2w;
     uint32_t bits_hash = (s1f << 16) + s2f;
     return ((uint64_t)bits_hash << 36) + (uint64_t)bytes_hash;
@@ -160,12 +169,6 @@ __device__ __forceinline__ uint64_t wave_window_hash(const uint8_t *p)
     uint32_t w[8];
     load32_unaligned(p + 32u * lane_id(), w);
     return wave_hash_regs(w);
-}
-
-template <int CTRL>
-__device__ __forceinline__ uint32_t dpp_perm(uint32_t x)
-{
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, false);
 }
 
 // Butterfly step: each lane keeps half of its values, the partner (an involution differing in
