@@ -1022,7 +1022,6 @@ __device__ __forceinline__ uint32_t write_escaped(uint8_t *dst, const uint8_t *p
     return o;
 }
 
-constexpr uint32_t EMIT_WAVES = 8;
 
 __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
 {

@@ -900,7 +900,7 @@ static int launch_emit(xc_plan *p, uint32_t j0, uint32_t jc, uint32_t gate_sb = 
     hipLaunchKernelGGL(k_alloc, dim3(1), dim3(1024), 0, s, e);
     HIPCHK(hipGetLastError());
     KSpan span(p, XC_K_EMIT);
-    hipLaunchKernelGGL(k_emit, dim3(jc - j0), dim3(512), 0, s, e);
+    hipLaunchKernelGGL(k_emit, dim3(jc - j0), dim3(64 * EMIT_WAVES), 0, s, e);
     HIPCHK(hipGetLastError());
     return XC_OK;
 }
