@@ -191,7 +191,7 @@ __device__ __forceinline__ const uint8_t *desc_base(const ScanArgs &a, const uin
 }
 
 template <int MODE>
-__global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
+__global__ __launch_bounds__(64 * SCAN_WAVES) void k_scan(ScanArgs a)
 {
     if (aborted(a.P)) return;
     __shared__ uint32_t filt[XC_FILT_WORDS];
@@ -200,8 +200,8 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a)
     uint2 *queue = queues[wave];
     const uint32_t l = lane_id();
 
-    static_assert(XC_FILT_WORDS % 4096u == 0u, "filter load loop");
-    for (uint32_t i = threadIdx.x * 4u; i < XC_FILT_WORDS; i += 4096u) {
+    static_assert(XC_FILT_WORDS % (256u * SCAN_WAVES) == 0u, "filter load loop");
+    for (uint32_t i = threadIdx.x * 4u; i < XC_FILT_WORDS; i += 256u * SCAN_WAVES) {
         uint4 f = *(const uint4 *)(a.set.filt + i);
         if (a.has2) {
             const uint4 g = *(const uint4 *)(a.set2.filt + i);
