@@ -250,6 +250,13 @@ __global__ __launch_bounds__(64 * SCAN_WAVES) void k_scan(ScanArgs a)
         const bool contig = in_run && (uniform(dsc.y) >> 31) != 0u;
         uint32_t ev_n = 0, qn = 0;
         bool dense = false;
+        // REF-shadow flags of the chunk's iterations, one load per chunk (lane j: the block before
+        // s = c0 + 2048 j), instead of a dependent load at every iteration
+        uint32_t sflag = 0;
+        if (a.shadow) {
+            const uint32_t sj = c0 + XC_SEG * l;
+            if (l < CHUNK_BLOCKS && sj >= XC_SEG && sj < c1) sflag = a.P.blk_pref[gblk + (sj >> 11) - 1u];
+        }
 
         BlockSums ps = block_sums(pw, l);
         uint32_t s = c0;
@@ -271,7 +278,7 @@ __global__ __launch_bounds__(64 * SCAN_WAVES) void k_scan(ScanArgs a)
             const BlockSums cs = block_sums(w, l);
             // REF shadow: the block before s is a predicted REF, after which the reference looks
             // nothing up until s + 2047 (recorded below); k_walk verifies the REF happened
-            const bool shadowed = a.shadow && uniform(a.P.blk_pref[gblk + (s >> 11) - 1u]) != 0u;
+            const bool shadowed = a.shadow && ((ballot(sflag != 0u) >> ((s - c0) >> 11)) & 1u) != 0u;
             // window ending just before this lane's first position q = s + 32 l:
             // out-chunks of lanes >= l (previous block) + in-chunks of lanes < l.
             const uint32_t sufA = ps.totA - ps.preA, sufC = ps.totC - ps.preC;

@@ -10,6 +10,7 @@ constexpr uint32_t EV_CAP = 64;          // sparse events per scan chunk before 
 constexpr uint32_t EV_DENSE = 0x80000000u;
 constexpr uint32_t Q_CAP = 128;          // per-wave LDS queue of level-1 filter positives
 constexpr uint32_t SCAN_WAVES = 16;      // waves per scan workgroup (one per CU: all of its LDS and VGPRs)
+constexpr uint32_t CHUNK_BLOCKS = 8;     // 2048-byte blocks per scan chunk (16 KiB)
 constexpr uint32_t SCAN_UNIT = 4;        // chunks a scan wave takes from the work counter at a time
 constexpr uint32_t EMIT_WAVES = 4;       // k_emit waves per buffer (workgroup)
 constexpr uint32_t SCAN_LDS = XC_FILT_WORDS * 4u + SCAN_WAVES * Q_CAP * 8u;

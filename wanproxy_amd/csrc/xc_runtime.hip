@@ -372,6 +372,7 @@ extern "C" int xc_window_hashes(xc_ctx *ctx, const uint8_t *d_in, uint64_t n, ui
 
 // ------------------------------------------------------------------ plan ----------
 static const uint32_t CHUNK_LEN = 16384;
+static_assert(CHUNK_LEN == CHUNK_BLOCKS * XC_SEG, "k_scan loads a chunk's shadow flags in one wave load");
 static const uint64_t SUB_BYTES_DEFAULT = 512ull << 20;  // sub-batch: bound on input bytes (tuned on cfg5)
 static const uint32_t SUB_BUFS = 32768;                  // sub-batch: bound on buffers
 
