@@ -139,3 +139,24 @@ def test_collision_semantics(oracle_mod):
     assert len(out) > 0
     st, dec, cons, unk = c.clone().decode_batch([b"\xf1\x01" + y.tobytes()])[0]
     assert st == 0
+
+
+def test_stateful_encoder_split_invariance(oracle_mod):
+    """The stateful oracle encoder (the checker of the stream API): splitting encode() calls
+    never changes the concatenated output, and encode + flush per buffer equals
+    the batch form; outputs appear only when a declaration or a REF completes."""
+    pool = W.pool(32)
+    data = np.concatenate([W.gen(5, 10000), pool[:20000], W.gen(6, 30000), pool[4096:12288]])
+    want = oracle_mod.Cache().encode_batch([data])[0]
+    rng = np.random.default_rng(3)
+    for trial in range(4):
+        e = oracle_mod.Encoder(oracle_mod.Cache())
+        cuts = sorted(rng.integers(0, len(data), 1 + trial * 5))
+        outs = [e.encode(p) for p in np.split(data, cuts)]
+        emitted, tail = e.flush()
+        assert emitted and b"".join(outs) + tail == want
+    # under 2048 bytes nothing is emitted before flush; flush of nothing returns False
+    e = oracle_mod.Encoder(oracle_mod.Cache())
+    assert e.encode(W.gen(7, 2047)) == b""
+    assert e.flush()[0] is True
+    assert e.flush() == (False, b"")
