@@ -570,6 +570,9 @@ using namespace xc;
 extern "C" int xc__cache_devset(xc_cache *c, void *devset, uint8_t **segs, uint32_t **count, uint32_t *cap,
                                 uint2 **undo, void **stream, int *dev);
 extern "C" int xc__set_error(int code, const char *msg);
+extern "C" int xc__dalloc(void **p, uint64_t bytes);
+extern "C" int xc__halloc(void **p, uint64_t bytes);
+extern "C" void xc__pfree(void *p);
 
 #define DHIP(x)                                                                          \
     do {                                                                                 \
@@ -580,7 +583,8 @@ extern "C" int xc__set_error(int code, const char *msg);
 template <class T>
 static hipError_t dalloc(T **p, size_t n)
 {
-    return hipMalloc((void **)p, std::max<size_t>(n, 1) * sizeof(T));
+    // the runtime's caching pool (xc_runtime.hip): no hipMalloc per call
+    return xc__dalloc((void **)p, std::max<size_t>(n, 1) * sizeof(T)) == XC_OK ? hipSuccess : hipErrorOutOfMemory;
 }
 
 struct xc_dplan {
@@ -608,7 +612,7 @@ extern "C" int xc_dplan_destroy(xc_dplan *p)
     if (!p) return XC_OK;
     hipSetDevice(p->dev);
     hipStreamSynchronize(p->s);
-    for (void *x : p->owned) hipFree(x);
+    for (void *x : p->owned) xc__pfree(x);
     delete p;
     return XC_OK;
 }
@@ -803,8 +807,8 @@ extern "C" int xc_decode_batch_host(xc_cache *c, const uint8_t *in, const uint64
     std::vector<uint64_t> u64(3 * (size_t)ns);
     std::vector<int32_t> i32(2 * (size_t)ns);
     auto run = [&]() -> int {
-        DHIP(hipHostMalloc((void **)&h_in, p->in_bytes));
-        DHIP(hipHostMalloc((void **)&h_out, p->out_bytes));
+        if (xc__halloc((void **)&h_in, p->in_bytes) || xc__halloc((void **)&h_out, p->out_bytes))
+            return XC_ENOMEM;
         DHIP(dalloc(&d_in, p->in_bytes));
         DHIP(dalloc(&d_out, p->out_bytes));
         DHIP(dalloc(&d_u64, 3 * (size_t)ns));
@@ -830,12 +834,12 @@ extern "C" int xc_decode_batch_host(xc_cache *c, const uint8_t *in, const uint64
     };
     rc = run();
     hipStreamSynchronize(s);
-    hipHostFree(h_in);
-    hipHostFree(h_out);
-    hipFree(d_in);
-    hipFree(d_out);
-    hipFree(d_u64);
-    hipFree(d_i32);
+    xc__pfree(h_in);
+    xc__pfree(h_out);
+    xc__pfree(d_in);
+    xc__pfree(d_out);
+    xc__pfree(d_u64);
+    xc__pfree(d_i32);
     xc_dplan_destroy(p);
     return rc;
 }

@@ -11,7 +11,10 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/xcodec_hip.h"
@@ -37,11 +40,120 @@ static int fail(int code, const std::string &msg)
 
 extern "C" const char *xc_last_error(void) { return g_err.c_str(); }
 
+// ------------------------------------------------------------------ allocation ----------
+// Caching allocator for device and pinned host memory.  Plans, declaration sets and the
+// host-to-host entry points allocate and free dozens of arrays per call; hipMalloc/hipFree (and
+// hipHostMalloc for staging) cost far more than the work of a small call.  Freed blocks are kept
+// per (device, kind) in a best-fit pool (a block serves requests down to half its size) and
+// reused; they go back to HIP only at process exit.
+namespace {
+struct Pool {
+    std::mutex mu;
+    std::multimap<std::pair<int, size_t>, void *> free_;  // (device | host flag, size) -> block
+    std::unordered_map<void *, std::pair<int, size_t>> size_;
+};
+Pool &pool()
+{
+    static Pool *p = new Pool();  // never destroyed: blocks may be released after static teardown
+    return *p;
+}
+size_t size_class(size_t n)
+{
+    if (n <= 4096) return 4096;
+    if (n <= (64u << 20)) {
+        size_t c = 4096;
+        while (c < n) c <<= 1;
+        return c;
+    }
+    return (n + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+}
+constexpr int HOST_KIND = 1 << 20;  // pinned host blocks share the pool under this key
+}  // namespace
+
+static hipError_t pool_alloc(void **out, size_t n, bool host)
+{
+    int dev = 0;
+    if (!host && hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
+    const int kind = host ? HOST_KIND : dev;
+    const size_t c = size_class(std::max<size_t>(n, 1));
+    Pool &P = pool();
+    {
+        std::lock_guard<std::mutex> g(P.mu);
+        auto it = P.free_.lower_bound({kind, c});
+        if (it != P.free_.end() && it->first.first == kind && it->first.second <= 2 * c) {
+            *out = it->second;
+            P.free_.erase(it);
+            return hipSuccess;
+        }
+    }
+    void *ptr = nullptr;
+    hipError_t e = host ? hipHostMalloc(&ptr, c, 0) : hipMalloc(&ptr, c);
+    if (e != hipSuccess) {
+        // release cached blocks of this kind and retry once
+        std::vector<void *> drop;
+        {
+            std::lock_guard<std::mutex> g(P.mu);
+            for (auto it = P.free_.begin(); it != P.free_.end();) {
+                if (it->first.first == kind) {
+                    drop.push_back(it->second);
+                    P.size_.erase(it->second);
+                    it = P.free_.erase(it);
+                } else {
+                    ++it;
+                }
+            }
+        }
+        for (void *q : drop) host ? (void)hipHostFree(q) : (void)hipFree(q);
+        e = host ? hipHostMalloc(&ptr, c, 0) : hipMalloc(&ptr, c);
+        if (e != hipSuccess) return e;
+    }
+    std::lock_guard<std::mutex> g(P.mu);
+    P.size_[ptr] = {kind, c};
+    *out = ptr;
+    return hipSuccess;
+}
+
+static void pool_free(void *ptr)
+{
+    if (!ptr) return;
+    Pool &P = pool();
+    std::lock_guard<std::mutex> g(P.mu);
+    auto it = P.size_.find(ptr);
+    if (it == P.size_.end()) return;  // not from the pool
+    P.free_.insert({it->second, ptr});
+}
+
+// Device / pinned-host arrays of T (the pool's hipMalloc / hipFree).
+template <class T>
+static hipError_t dmalloc(T **p, size_t bytes)
+{
+    return pool_alloc((void **)p, bytes, false);
+}
+static hipError_t dfree(void *p)
+{
+    pool_free(p);
+    return hipSuccess;
+}
+static hipError_t hmalloc(void **p, size_t bytes) { return pool_alloc(p, bytes, true); }
+
+// For xc_decode.hip.
+extern "C" int xc__dalloc(void **p, uint64_t bytes)
+{
+    return pool_alloc(p, bytes, false) == hipSuccess ? XC_OK : fail(XC_ENOMEM, "device allocation failed");
+}
+extern "C" int xc__halloc(void **p, uint64_t bytes)
+{
+    return pool_alloc(p, bytes, true) == hipSuccess ? XC_OK : fail(XC_ENOMEM, "pinned allocation failed");
+}
+extern "C" void xc__pfree(void *p) { pool_free(p); }
+
 
 // ------------------------------------------------------------------ context ----------
 struct xc_ctx {
     int dev;
     hipStream_t stream;
+    hipStream_t side = nullptr;  // block hashing ahead of the scans (shared by the plans)
+    hipStream_t copy = nullptr;  // host-path input copies
     int n_cu;
     uint32_t *d_scratch;  // small device scratch (flags)
     uint8_t *d_seg;       // one segment of device scratch
@@ -73,8 +185,8 @@ extern "C" int xc_ctx_create(int dev, xc_ctx **out)
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, dev));
     c->n_cu = prop.multiProcessorCount;
-    HIPCHK(hipMalloc(&c->d_scratch, 4096));
-    HIPCHK(hipMalloc(&c->d_seg, 4096));
+    HIPCHK(dmalloc(&c->d_scratch, 4096));
+    HIPCHK(dmalloc(&c->d_seg, 4096));
     *out = c;
     return XC_OK;
 }
@@ -84,8 +196,10 @@ extern "C" int xc_ctx_destroy(xc_ctx *ctx)
     if (!ctx) return XC_OK;
     hipSetDevice(ctx->dev);
     hipStreamSynchronize(ctx->stream);
-    hipFree(ctx->d_scratch);
-    hipFree(ctx->d_seg);
+    dfree(ctx->d_scratch);
+    dfree(ctx->d_seg);
+    if (ctx->side) { hipStreamSynchronize(ctx->side); hipStreamDestroy(ctx->side); }
+    if (ctx->copy) { hipStreamSynchronize(ctx->copy); hipStreamDestroy(ctx->copy); }
     hipStreamDestroy(ctx->stream);
     delete ctx;
     return XC_OK;
@@ -117,12 +231,12 @@ struct HostSet {
         n_full = pow2_at_least(entries * 2, 1024);
         n_lo = pow2_at_least(entries * 4, 1024);
         if (n_full > (1u << 27) || n_lo > (1u << 25)) return fail(XC_EINVAL, "set too large");
-        HIPCHK(hipMalloc(&d.filt, XC_FILT_WORDS * 4));
-        HIPCHK(hipMalloc(&d.l2, (size_t)XC_L2_WORDS * 8));
-        HIPCHK(hipMalloc(&d.lo_keys, (size_t)n_lo * 4));
-        HIPCHK(hipMalloc(&d.lo_zero, 4));
-        HIPCHK(hipMalloc(&d.keys, (size_t)n_full * 8));
-        HIPCHK(hipMalloc(&d.vals, (size_t)n_full * 8));
+        HIPCHK(dmalloc(&d.filt, XC_FILT_WORDS * 4));
+        HIPCHK(dmalloc(&d.l2, (size_t)XC_L2_WORDS * 8));
+        HIPCHK(dmalloc(&d.lo_keys, (size_t)n_lo * 4));
+        HIPCHK(dmalloc(&d.lo_zero, 4));
+        HIPCHK(dmalloc(&d.keys, (size_t)n_full * 8));
+        HIPCHK(dmalloc(&d.vals, (size_t)n_full * 8));
         d.lo_mask = n_lo - 1;
         d.mask = n_full - 1;
         return XC_OK;
@@ -139,12 +253,12 @@ struct HostSet {
     }
     void release()
     {
-        hipFree(d.filt);
-        hipFree(d.l2);
-        hipFree(d.lo_keys);
-        hipFree(d.lo_zero);
-        hipFree(d.keys);
-        hipFree(d.vals);
+        dfree(d.filt);
+        dfree(d.l2);
+        dfree(d.lo_keys);
+        dfree(d.lo_zero);
+        dfree(d.keys);
+        dfree(d.vals);
         d = DevSet{};
     }
 };
@@ -188,14 +302,14 @@ extern "C" int xc_cache_create(xc_ctx *ctx, uint64_t cap, xc_cache **out)
     c->ctx = ctx;
     c->cap = cap;
     if ((rc = c->set.alloc(cap))) return rc;
-    HIPCHK(hipMalloc(&c->segs, (size_t)cap * XC_SEG + 4096));
-    HIPCHK(hipMalloc(&c->count, 4));
-    HIPCHK(hipMalloc(&c->undo, (size_t)cap * sizeof(uint2)));
-    HIPCHK(hipMalloc(&c->ctl, CTL_WORDS * 4));
-    HIPCHK(hipMalloc(&c->snap_filt, XC_FILT_WORDS * 4));
-    HIPCHK(hipMalloc(&c->snap_lo_zero, 4));
-    HIPCHK(hipMalloc(&c->snap_count_dev, 4));
-    HIPCHK(hipMalloc(&c->snap_l2, (size_t)XC_L2_WORDS * 8));
+    HIPCHK(dmalloc(&c->segs, (size_t)cap * XC_SEG + 4096));
+    HIPCHK(dmalloc(&c->count, 4));
+    HIPCHK(dmalloc(&c->undo, (size_t)cap * sizeof(uint2)));
+    HIPCHK(dmalloc(&c->ctl, CTL_WORDS * 4));
+    HIPCHK(dmalloc(&c->snap_filt, XC_FILT_WORDS * 4));
+    HIPCHK(dmalloc(&c->snap_lo_zero, 4));
+    HIPCHK(dmalloc(&c->snap_count_dev, 4));
+    HIPCHK(dmalloc(&c->snap_l2, (size_t)XC_L2_WORDS * 8));
     if ((rc = c->set.clear(ctx->stream))) return rc;
     HIPCHK(hipMemsetAsync(c->count, 0, 4, ctx->stream));
     HIPCHK(hipMemsetAsync(c->ctl, 0, CTL_WORDS * 4, ctx->stream));
@@ -208,16 +322,16 @@ extern "C" int xc_cache_destroy(xc_cache *c)
 {
     if (!c) return XC_OK;
     hipSetDevice(c->ctx->dev);
-    hipStreamSynchronize(c->ctx->stream);
+    hipDeviceSynchronize();  // pooled memory is reused at once: every stream must be done with it
     c->set.release();
-    hipFree(c->segs);
-    hipFree(c->count);
-    hipFree(c->undo);
-    hipFree(c->ctl);
-    hipFree(c->snap_filt);
-    hipFree(c->snap_lo_zero);
-    hipFree(c->snap_count_dev);
-    hipFree(c->snap_l2);
+    dfree(c->segs);
+    dfree(c->count);
+    dfree(c->undo);
+    dfree(c->ctl);
+    dfree(c->snap_filt);
+    dfree(c->snap_lo_zero);
+    dfree(c->snap_count_dev);
+    dfree(c->snap_l2);
     delete c;
     return XC_OK;
 }
@@ -390,22 +504,22 @@ struct HostLayer {
     int alloc(uint32_t nchunks, uint32_t chunk_len)
     {
         size_t n = std::max<uint32_t>(nchunks, 1);
-        HIPCHK(hipMalloc(&d.cnt, n * 4));
-        HIPCHK(hipMalloc(&d.pos, n * EV_CAP * 4));
-        HIPCHK(hipMalloc(&d.stat, n * EV_CAP * 4));
-        HIPCHK(hipMalloc(&d.h, n * EV_CAP * 8));
-        HIPCHK(hipMalloc(&d.val, n * EV_CAP * 8));
-        HIPCHK(hipMalloc(&d.bits, n * (chunk_len / 32) * 4));
+        HIPCHK(dmalloc(&d.cnt, n * 4));
+        HIPCHK(dmalloc(&d.pos, n * EV_CAP * 4));
+        HIPCHK(dmalloc(&d.stat, n * EV_CAP * 4));
+        HIPCHK(dmalloc(&d.h, n * EV_CAP * 8));
+        HIPCHK(dmalloc(&d.val, n * EV_CAP * 8));
+        HIPCHK(dmalloc(&d.bits, n * (chunk_len / 32) * 4));
         return XC_OK;
     }
     void release()
     {
-        hipFree(d.cnt);
-        hipFree(d.pos);
-        hipFree(d.stat);
-        hipFree(d.h);
-        hipFree(d.val);
-        hipFree(d.bits);
+        dfree(d.cnt);
+        dfree(d.pos);
+        dfree(d.stat);
+        dfree(d.h);
+        dfree(d.val);
+        dfree(d.bits);
     }
 };
 
@@ -590,13 +704,13 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     if ((rc = p->D.alloc(p->nchunks, CHUNK_LEN))) return rc;
 
     size_t nb1 = std::max<uint64_t>(nbuf, 1);
-    HIPCHK(hipMalloc(&p->d_buf_off, nb1 * 8));
-    HIPCHK(hipMalloc(&p->d_out_off, nb1 * 8));
-    HIPCHK(hipMalloc(&p->d_buf_len, nb1 * 4));
-    HIPCHK(hipMalloc(&p->d_chunk0, (nbuf + 1) * 4));
-    HIPCHK(hipMalloc(&p->d_tok_base, (nbuf + 1) * 4));
-    HIPCHK(hipMalloc(&p->d_chunks, std::max<size_t>(chunks.size(), 1) * sizeof(uint2)));
-    HIPCHK(hipMalloc(&p->d_desc, std::max<size_t>(chunks.size(), 1) * sizeof(uint4)));
+    HIPCHK(dmalloc(&p->d_buf_off, nb1 * 8));
+    HIPCHK(dmalloc(&p->d_out_off, nb1 * 8));
+    HIPCHK(dmalloc(&p->d_buf_len, nb1 * 4));
+    HIPCHK(dmalloc(&p->d_chunk0, (nbuf + 1) * 4));
+    HIPCHK(dmalloc(&p->d_tok_base, (nbuf + 1) * 4));
+    HIPCHK(dmalloc(&p->d_chunks, std::max<size_t>(chunks.size(), 1) * sizeof(uint2)));
+    HIPCHK(dmalloc(&p->d_desc, std::max<size_t>(chunks.size(), 1) * sizeof(uint4)));
     hipStream_t s = c->ctx->stream;
     if (nbuf) {
         HIPCHK(hipMemcpyAsync(p->d_buf_off, p->in_off.data(), nbuf * 8, hipMemcpyHostToDevice, s));
@@ -624,32 +738,32 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     P.dset = p->dset.d;
     P.tok_base = p->d_tok_base;
     size_t nt = std::max<uint64_t>(toks, 1);
-    HIPCHK(hipMalloc(&P.tok_cnt, nb1 * 4));
-    HIPCHK(hipMalloc(&P.tok_lb, nt * 4));
-    HIPCHK(hipMalloc(&P.tok_le, nt * 4));
-    HIPCHK(hipMalloc(&P.tok_seg, nt * 4));
-    HIPCHK(hipMalloc(&P.tok_op, nt * 4));
-    HIPCHK(hipMalloc(&P.tok_dpos, nt * 4));
-    HIPCHK(hipMalloc(&P.tok_h, nt * 8));
-    HIPCHK(hipMalloc(&P.tok_known, nt * 4));
-    HIPCHK(hipMalloc(&P.blk_h, std::max<uint64_t>(nblk, 1) * 8));
-    HIPCHK(hipMalloc(&P.blk_pref, std::max<uint64_t>(nblk, 1) * 4));
+    HIPCHK(dmalloc(&P.tok_cnt, nb1 * 4));
+    HIPCHK(dmalloc(&P.tok_lb, nt * 4));
+    HIPCHK(dmalloc(&P.tok_le, nt * 4));
+    HIPCHK(dmalloc(&P.tok_seg, nt * 4));
+    HIPCHK(dmalloc(&P.tok_op, nt * 4));
+    HIPCHK(dmalloc(&P.tok_dpos, nt * 4));
+    HIPCHK(dmalloc(&P.tok_h, nt * 8));
+    HIPCHK(dmalloc(&P.tok_known, nt * 4));
+    HIPCHK(dmalloc(&P.blk_h, std::max<uint64_t>(nblk, 1) * 8));
+    HIPCHK(dmalloc(&P.blk_pref, std::max<uint64_t>(nblk, 1) * 4));
     HIPCHK(hipMemsetAsync(P.blk_pref, 0, std::max<uint64_t>(nblk, 1) * 4, s));
     {
         std::vector<uint32_t> cb(std::max<size_t>(chunks.size(), 1), 0);
         for (size_t k = 0; k < chunks.size(); k++) cb[k] = blk_base[chunks[k].x];
-        HIPCHK(hipMalloc(&p->d_chunk_blk, cb.size() * 4));
+        HIPCHK(dmalloc(&p->d_chunk_blk, cb.size() * 4));
         HIPCHK(hipMemcpyAsync(p->d_chunk_blk, cb.data(), cb.size() * 4, hipMemcpyHostToDevice, s));
         P.chunk_blk = p->d_chunk_blk;
         const char *e = getenv("XC_NO_SHADOW");
         p->shadow = (e && atoi(e)) ? 0 : 1;
     }
-    HIPCHK(hipMalloc(&p->d_blk_base, (nbuf + 1) * 4));
+    HIPCHK(dmalloc(&p->d_blk_base, (nbuf + 1) * 4));
     {
         std::vector<uint32_t> bb(std::max<uint64_t>(nblk, 1), 0);
         for (uint64_t i = 0; i < nbuf; i++)
             for (uint32_t g = blk_base[i]; g < blk_base[i + 1]; g++) bb[g] = (uint32_t)i;
-        HIPCHK(hipMalloc(&p->d_blk_buf, bb.size() * 4));
+        HIPCHK(dmalloc(&p->d_blk_buf, bb.size() * 4));
         HIPCHK(hipMemcpyAsync(p->d_blk_buf, bb.data(), bb.size() * 4, hipMemcpyHostToDevice, s));
         P.blk_buf = p->d_blk_buf;
         p->blk_base = blk_base;
@@ -661,17 +775,18 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
             for (uint32_t k0 = 0; k0 < blk_base[i + 1] - blk_base[i]; k0 += 8) grp.push_back(make_uint2((uint32_t)i, k0));
         }
         p->grp_base[nbuf] = (uint32_t)grp.size();
-        HIPCHK(hipMalloc(&p->d_blk_grp, std::max<size_t>(grp.size(), 1) * sizeof(uint2)));
+        HIPCHK(dmalloc(&p->d_blk_grp, std::max<size_t>(grp.size(), 1) * sizeof(uint2)));
         if (!grp.empty())
             HIPCHK(hipMemcpyAsync(p->d_blk_grp, grp.data(), grp.size() * sizeof(uint2), hipMemcpyHostToDevice, s));
         P.blk_grp = p->d_blk_grp;
     }
-    HIPCHK(hipMalloc(&p->d_l2mix, (size_t)XC_L2_WORDS * 8));
+    HIPCHK(dmalloc(&p->d_l2mix, (size_t)XC_L2_WORDS * 8));
     P.l2mix = p->d_l2mix;
     // the declaration set's level-2 filter is the combined one (cache | declarations): every
     // declaration insert lands there directly, and the declaration-layer scans test a superset
     P.dset.l2 = p->d_l2mix;
-    HIPCHK(hipStreamCreateWithFlags(&p->hs, hipStreamNonBlocking));
+    if (!c->ctx->side) HIPCHK(hipStreamCreateWithFlags(&c->ctx->side, hipStreamNonBlocking));
+    p->hs = c->ctx->side;
     HIPCHK(hipEventCreateWithFlags(&p->ev_start, hipEventDisableTiming));
     p->ev_hash.assign(p->sub.size(), nullptr);
     p->ev_go.assign(p->sub.size(), nullptr);
@@ -679,10 +794,10 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     for (auto &e : p->ev_go) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHK(hipMemcpyAsync(p->d_blk_base, blk_base.data(), (nbuf + 1) * 4, hipMemcpyHostToDevice, s));
     P.blk_base = p->d_blk_base;
-    HIPCHK(hipMalloc(&P.buf_next, nb1 * 4));
-    HIPCHK(hipMalloc(&P.buf_nref, nb1 * 4));
-    HIPCHK(hipMalloc(&P.buf_slot, nb1 * 4));
-    HIPCHK(hipMalloc(&P.ctl, CTL_WORDS * 4));
+    HIPCHK(dmalloc(&P.buf_next, nb1 * 4));
+    HIPCHK(dmalloc(&P.buf_nref, nb1 * 4));
+    HIPCHK(dmalloc(&P.buf_slot, nb1 * 4));
+    HIPCHK(dmalloc(&P.ctl, CTL_WORDS * 4));
     HIPCHK(hipMemsetAsync(P.ctl, 0, CTL_WORDS * 4, s));
     P.out_off = p->d_out_off;
     HIPCHK(hipStreamSynchronize(s));
@@ -694,56 +809,57 @@ extern "C" int xc_plan_destroy(xc_plan *p)
 {
     if (!p) return XC_OK;
     hipSetDevice(p->cache->ctx->dev);
+    // pooled memory goes back for reuse at once: nothing may still read or write it
     hipStreamSynchronize(p->cache->ctx->stream);
+    if (p->hs) hipStreamSynchronize(p->hs);
+    if (p->cs) hipStreamSynchronize(p->cs);
     p->S.release();
     p->D.release();
     p->dset.release();
-    hipFree(p->d_buf_off);
-    hipFree(p->d_out_off);
-    hipFree(p->d_buf_len);
-    hipFree(p->d_chunk0);
-    hipFree(p->d_tok_base);
-    hipFree(p->d_chunks);
-    hipFree(p->d_desc);
-    hipFree(p->P.tok_cnt);
-    hipFree(p->P.tok_lb);
-    hipFree(p->P.tok_le);
-    hipFree(p->P.tok_seg);
-    hipFree(p->P.tok_op);
-    hipFree(p->P.tok_dpos);
-    hipFree(p->P.tok_h);
-    hipFree(p->P.tok_known);
-    hipFree(p->P.blk_h);
-    hipFree(p->P.blk_pref);
-    hipFree(p->d_chunk_blk);
-    hipFree(p->d_blk_base);
-    hipFree(p->d_blk_buf);
-    hipFree(p->d_blk_grp);
-    hipFree(p->d_l2mix);
-    hipFree(p->P.buf_next);
-    hipFree(p->P.buf_nref);
-    hipFree(p->P.buf_slot);
-    hipFree(p->P.ctl);
-    hipFree(p->d_stream_st);
-    hipFree(p->d_stream_res);
+    dfree(p->d_buf_off);
+    dfree(p->d_out_off);
+    dfree(p->d_buf_len);
+    dfree(p->d_chunk0);
+    dfree(p->d_tok_base);
+    dfree(p->d_chunks);
+    dfree(p->d_desc);
+    dfree(p->P.tok_cnt);
+    dfree(p->P.tok_lb);
+    dfree(p->P.tok_le);
+    dfree(p->P.tok_seg);
+    dfree(p->P.tok_op);
+    dfree(p->P.tok_dpos);
+    dfree(p->P.tok_h);
+    dfree(p->P.tok_known);
+    dfree(p->P.blk_h);
+    dfree(p->P.blk_pref);
+    dfree(p->d_chunk_blk);
+    dfree(p->d_blk_base);
+    dfree(p->d_blk_buf);
+    dfree(p->d_blk_grp);
+    dfree(p->d_l2mix);
+    dfree(p->P.buf_next);
+    dfree(p->P.buf_nref);
+    dfree(p->P.buf_slot);
+    dfree(p->P.ctl);
+    dfree(p->d_stream_st);
+    dfree(p->d_stream_res);
     for (auto &x : p->ev_live) { hipEventDestroy(x.second.first); hipEventDestroy(x.second.second); }
     for (auto e : p->ev_pool) hipEventDestroy(e);
     if (p->hs) {
-        hipStreamSynchronize(p->hs);
-        hipStreamDestroy(p->hs);
+        hipStreamSynchronize(p->hs);  // (the context's side stream: kept)
     }
     if (p->ev_start) hipEventDestroy(p->ev_start);
     if (p->cs) {
-        hipStreamSynchronize(p->cs);
-        hipStreamDestroy(p->cs);
+        hipStreamSynchronize(p->cs);  // (the context's copy stream: kept)
     }
     for (auto e : p->ev_h2d)
         if (e) hipEventDestroy(e);
-    hipFree(p->e_in);
-    hipFree(p->e_out);
-    hipFree(p->e_len);
-    hipFree(p->e_pos);
-    hipFree(p->e_total);
+    dfree(p->e_in);
+    dfree(p->e_out);
+    dfree(p->e_len);
+    dfree(p->e_pos);
+    dfree(p->e_total);
     for (auto e : p->ev_hash)
         if (e) hipEventDestroy(e);
     for (auto e : p->ev_go)
@@ -808,8 +924,8 @@ extern "C" int xc_plan_set_streams(xc_plan *p, const uint64_t *start, const int6
     }
     const size_t nb1 = std::max<uint32_t>(p->nb, 1);
     if (!p->d_stream_st) {
-        HIPCHK(hipMalloc(&p->d_stream_st, nb1 * sizeof(uint4)));
-        HIPCHK(hipMalloc(&p->d_stream_res, nb1 * sizeof(uint2)));
+        HIPCHK(dmalloc(&p->d_stream_st, nb1 * sizeof(uint4)));
+        HIPCHK(dmalloc(&p->d_stream_res, nb1 * sizeof(uint2)));
     }
     if (p->nb) HIPCHK(hipMemcpyAsync(p->d_stream_st, st.data(), p->nb * sizeof(uint4), hipMemcpyHostToDevice, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -1089,12 +1205,13 @@ extern "C" int xc_encode_run_host(xc_plan *p, const uint8_t *h_in, uint8_t *h_ou
     if (rc) return rc;
     hipStream_t s = p->cache->ctx->stream;
     if (!p->e_in) {  // device arenas and the copy stream, kept for later runs
-        HIPCHK(hipMalloc(&p->e_in, p->in_bytes));
-        HIPCHK(hipMalloc(&p->e_out, p->out_bytes));
-        HIPCHK(hipMalloc(&p->e_len, std::max<uint64_t>(p->nb, 1) * 8));
-        HIPCHK(hipMalloc(&p->e_pos, std::max<uint64_t>(p->nb, 1) * 8));
-        HIPCHK(hipMalloc(&p->e_total, 8));
-        HIPCHK(hipStreamCreateWithFlags(&p->cs, hipStreamNonBlocking));
+        HIPCHK(dmalloc(&p->e_in, p->in_bytes));
+        HIPCHK(dmalloc(&p->e_out, p->out_bytes));
+        HIPCHK(dmalloc(&p->e_len, std::max<uint64_t>(p->nb, 1) * 8));
+        HIPCHK(dmalloc(&p->e_pos, std::max<uint64_t>(p->nb, 1) * 8));
+        HIPCHK(dmalloc(&p->e_total, 8));
+        if (!p->cache->ctx->copy) HIPCHK(hipStreamCreateWithFlags(&p->cache->ctx->copy, hipStreamNonBlocking));
+        p->cs = p->cache->ctx->copy;
         p->ev_h2d.assign(p->sub.size(), nullptr);
         for (auto &e : p->ev_h2d) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
@@ -1151,11 +1268,11 @@ extern "C" int xc__encode_batch_host_ex(xc_cache *c, const uint8_t *in, const ui
     uint8_t *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
     uint64_t *d_len = nullptr;
     std::vector<uint64_t> lens(nbuf);
-    HIPCHK(hipHostMalloc(&h_in, p->in_bytes));
-    HIPCHK(hipHostMalloc(&h_out, p->out_bytes));
-    HIPCHK(hipMalloc(&d_in, p->in_bytes));
-    HIPCHK(hipMalloc(&d_out, p->out_bytes));
-    HIPCHK(hipMalloc(&d_len, std::max<uint64_t>(nbuf, 1) * 8));
+    HIPCHK(hmalloc((void **)&h_in, p->in_bytes));
+    HIPCHK(hmalloc((void **)&h_out, p->out_bytes));
+    HIPCHK(dmalloc(&d_in, p->in_bytes));
+    HIPCHK(dmalloc(&d_out, p->out_bytes));
+    HIPCHK(dmalloc(&d_len, std::max<uint64_t>(nbuf, 1) * 8));
     memset(h_in, 0, p->in_bytes);
     for (uint64_t i = 0; i < nbuf; i++) memcpy(h_in + p->in_off[i], in + in_off[i], in_len[i]);
     HIPCHK(hipMemcpyAsync(d_in, h_in, p->in_bytes, hipMemcpyHostToDevice, s));
@@ -1171,11 +1288,11 @@ extern "C" int xc__encode_batch_host_ex(xc_cache *c, const uint8_t *in, const ui
         }
         if (!rc && streams && rbase && rcand) rc = xc_plan_stream_results(p, rbase, rcand);
     }
-    hipHostFree(h_in);
-    hipHostFree(h_out);
-    hipFree(d_in);
-    hipFree(d_out);
-    hipFree(d_len);
+    pool_free(h_in);
+    pool_free(h_out);
+    dfree(d_in);
+    dfree(d_out);
+    dfree(d_len);
     xc_plan_destroy(p);
     return rc;
 }
