@@ -87,7 +87,7 @@ static hipError_t pool_alloc(void **out, size_t n, bool host)
         }
     }
     void *ptr = nullptr;
-    hipError_t e = host ? hipHostMalloc(&ptr, c, 0) : hipMalloc(&ptr, c);
+    hipError_t e = host ? hipHostMalloc(&ptr, c, hipHostMallocMapped) : hipMalloc(&ptr, c);
     if (e != hipSuccess) {
         // release cached blocks of this kind and retry once
         std::vector<void *> drop;
@@ -104,7 +104,7 @@ static hipError_t pool_alloc(void **out, size_t n, bool host)
             }
         }
         for (void *q : drop) host ? (void)hipHostFree(q) : (void)hipFree(q);
-        e = host ? hipHostMalloc(&ptr, c, 0) : hipMalloc(&ptr, c);
+        e = host ? hipHostMalloc(&ptr, c, hipHostMallocMapped) : hipMalloc(&ptr, c);
         if (e != hipSuccess) return e;
     }
     std::lock_guard<std::mutex> g(P.mu);
@@ -1264,36 +1264,31 @@ extern "C" int xc__encode_batch_host_ex(xc_cache *c, const uint8_t *in, const ui
         xc_plan_destroy(p);
         return rc;
     }
-    hipStream_t s = c->ctx->stream;
-    uint8_t *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
-    uint64_t *d_len = nullptr;
-    std::vector<uint64_t> lens(nbuf);
-    HIPCHK(hmalloc((void **)&h_in, p->in_bytes));
-    HIPCHK(hmalloc((void **)&h_out, p->out_bytes));
-    HIPCHK(dmalloc(&d_in, p->in_bytes));
-    HIPCHK(dmalloc(&d_out, p->out_bytes));
-    HIPCHK(dmalloc(&d_len, std::max<uint64_t>(nbuf, 1) * 8));
-    memset(h_in, 0, p->in_bytes);
+    // the end-to-end path (xc_encode_run_host): per-sub-batch input copies overlapping the
+    // encode, the encoded streams packed into pinned memory by a kernel; the input arena needs no
+    // clearing (bytes past a buffer's end are read but never used)
+    uint8_t *h_in = nullptr, *h_out = nullptr;
+    uint64_t cap_total = 0;
+    for (uint64_t i = 0; i < nbuf; i++) cap_total += 2 * in_len[i] + 16;
+    std::vector<uint64_t> lens(std::max<uint64_t>(nbuf, 1)), pos(std::max<uint64_t>(nbuf, 1));
+    if (hmalloc((void **)&h_in, p->in_bytes) != hipSuccess || hmalloc((void **)&h_out, cap_total + 16) != hipSuccess) {
+        pool_free(h_in);
+        xc_plan_destroy(p);
+        return fail(XC_ENOMEM, "pinned allocation failed");
+    }
     for (uint64_t i = 0; i < nbuf; i++) memcpy(h_in + p->in_off[i], in + in_off[i], in_len[i]);
-    HIPCHK(hipMemcpyAsync(d_in, h_in, p->in_bytes, hipMemcpyHostToDevice, s));
-    rc = xc_encode_run(p, d_in, d_out, d_len);
+    rc = xc_encode_run_host(p, h_in, h_out, cap_total + 16, lens.data(), pos.data());
     if (!rc) {
-        HIPCHK(hipMemcpyAsync(h_out, d_out, p->out_bytes, hipMemcpyDeviceToHost, s));
-        if (nbuf) HIPCHK(hipMemcpyAsync(lens.data(), d_len, nbuf * 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
         for (uint64_t i = 0; i < nbuf; i++) {
             out_len[i] = lens[i];
             if (lens[i] > out_cap[i]) { rc = fail(XC_EINVAL, "output capacity too small"); continue; }
-            memcpy(out + out_off[i], h_out + p->out_off[i], lens[i]);
+            memcpy(out + out_off[i], h_out + pos[i], lens[i]);
         }
         if (!rc && streams && rbase && rcand) rc = xc_plan_stream_results(p, rbase, rcand);
     }
+    xc_plan_destroy(p);  // (synchronizes before the pinned buffers return to the pool)
     pool_free(h_in);
     pool_free(h_out);
-    dfree(d_in);
-    dfree(d_out);
-    dfree(d_len);
-    xc_plan_destroy(p);
     return rc;
 }
 
