@@ -1367,14 +1367,21 @@ __global__ void k_undo(DevSet cache, const uint2 *undo, uint32_t from, uint32_t 
 }
 
 // Same, reading the current count on the device (no host round trip).
-__global__ void k_undo_dev(DevSet cache, const uint2 *undo, uint32_t from, const uint32_t *count, uint32_t cap)
+__global__ void k_undo_dev(DevSet cache, const uint2 *undo, uint32_t from, const uint32_t *count, uint32_t cap,
+                           const uint4 *snap_filt, const uint4 *snap_l2, const uint32_t *snap_lo_zero)
 {
+    // every table slot entered after the snapshot is cleared, the filters are copied back from
+    // the snapshot (one launch for the whole restore; the count is restored after it)
     const uint32_t to = min(*count, cap);
-    for (uint32_t i = from + blockIdx.x * blockDim.x + threadIdx.x; i < to; i += gridDim.x * blockDim.x) {
+    const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+    for (uint32_t i = from + i0; i < to; i += stride) {
         const uint2 u = undo[i];
         cache.keys[u.x] = XC_EMPTY64;
         if (u.y != NONE) cache.lo_keys[u.y] = 0u;
     }
+    for (uint32_t i = i0; i < XC_FILT_WORDS / 4; i += stride) ((uint4 *)cache.filt)[i] = snap_filt[i];
+    for (uint32_t i = i0; i < XC_L2_WORDS / 2; i += stride) ((uint4 *)cache.l2)[i] = snap_l2[i];
+    if (i0 == 0) *cache.lo_zero = *snap_lo_zero;
 }
 
 // Cache enter from the host API (single segment).

@@ -188,7 +188,8 @@ __global__ void k_clear_set(DevSet s, uint32_t n_lo, uint32_t n_full, uint4 *l2m
 __global__ void k_hash_segments(const uint8_t *segs, uint64_t n, uint64_t *out);
 __global__ void k_window_hashes(const uint8_t *in, uint32_t n, uint64_t *out);
 __global__ void k_undo(DevSet cache, const uint2 *undo, uint32_t from, uint32_t to);
-__global__ void k_undo_dev(DevSet cache, const uint2 *undo, uint32_t from, const uint32_t *count, uint32_t cap);
+__global__ void k_undo_dev(DevSet cache, const uint2 *undo, uint32_t from, const uint32_t *count, uint32_t cap,
+                           const uint4 *snap_filt, const uint4 *snap_l2, const uint32_t *snap_lo_zero);
 __global__ void k_enter_one(PlanDev P, uint64_t h, const uint8_t *seg);
 __global__ void k_lookup_one(PlanDev P, uint64_t h, uint8_t *out, uint32_t *found);
 __global__ void k_selftest(uint32_t *err);

@@ -396,17 +396,14 @@ extern "C" int xc_cache_restore_async(xc_cache *c)
     int rc = set_dev(c->ctx);
     if (rc) return rc;
     hipStream_t s = c->ctx->stream;
-    if (c->cap > c->snap_count) {
-        uint32_t n = (uint32_t)(c->cap - c->snap_count);
-        uint32_t blocks = std::min<uint32_t>((n + 255) / 256, 2048);
-        hipLaunchKernelGGL(k_undo_dev, dim3(blocks), dim3(256), 0, s, c->set.d, (const uint2 *)c->undo,
-                           c->snap_count, (const uint32_t *)c->count, (uint32_t)c->cap);
-        HIPCHK(hipGetLastError());
-    }
-    HIPCHK(hipMemcpyAsync(c->set.d.filt, c->snap_filt, XC_FILT_WORDS * 4, hipMemcpyDeviceToDevice, s));
-    HIPCHK(hipMemcpyAsync(c->set.d.lo_zero, c->snap_lo_zero, 4, hipMemcpyDeviceToDevice, s));
+    // one kernel: table slots entered since the snapshot, filters copied back; then the count
+    const uint32_t n = (uint32_t)std::max<uint64_t>(c->cap - c->snap_count, XC_L2_WORDS / 2);
+    const uint32_t blocks = std::min<uint32_t>((n + 255) / 256, 2048);
+    hipLaunchKernelGGL(k_undo_dev, dim3(blocks), dim3(256), 0, s, c->set.d, (const uint2 *)c->undo, c->snap_count,
+                       (const uint32_t *)c->count, (uint32_t)c->cap, (const uint4 *)c->snap_filt,
+                       (const uint4 *)c->snap_l2, (const uint32_t *)c->snap_lo_zero);
+    HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(c->count, c->snap_count_dev, 4, hipMemcpyDeviceToDevice, s));
-    HIPCHK(hipMemcpyAsync(c->set.d.l2, c->snap_l2, (size_t)XC_L2_WORDS * 8, hipMemcpyDeviceToDevice, s));
     return XC_OK;
 }
 
