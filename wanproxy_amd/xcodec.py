@@ -19,7 +19,8 @@ import weakref
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libxcodec_hip.so")
+# XC_LIB_PATH: an alternative build of the same library (A/B timing experiments, tools/ab.sh)
+LIB_PATH = os.environ.get("XC_LIB_PATH") or os.path.join(HERE, "libxcodec_hip.so")
 SEGMENT_LENGTH = 2048
 
 SYMBOLS = [
