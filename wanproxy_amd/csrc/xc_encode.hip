@@ -504,7 +504,9 @@ __global__ __launch_bounds__(256) void k_resolve(ResolveArgs a)
             if (f[g] >= 0) {
                 const uint32_t qf = readlane(q, f[g]);
                 const uint64_t vf = readlane64(v, f[g]);
-                load32_unaligned(base + qf - (XC_SEG - 1u) + 32u * l, x[g]);
+                const uint8_t *wp = base + qf - (XC_SEG - 1u) + 32u * l;
+                if (((qf + 1u) & (XC_SEG - 1u)) == 0u) load32_aligned(wp, x[g]);  // a block: 2 x 16 B
+                else load32_unaligned(wp, x[g]);
                 const uint4 *sp = (const uint4 *)(P.segs + vf * XC_SEG + 32u * l);
                 const uint4 s0 = sp[0], s1 = sp[1];
                 y[g][0] = s0.x; y[g][1] = s0.y; y[g][2] = s0.z; y[g][3] = s0.w;
