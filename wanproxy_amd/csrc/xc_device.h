@@ -310,8 +310,13 @@ __device__ __forceinline__ void payload_load(const uint8_t *src, const uint8_t *
     const uint32_t l = lane_id();
     const uint32_t head = (uint32_t)((16u - ((uintptr_t)out & 15u)) & 15u);
     const uint32_t nbody = (XC_SEG - head) >> 4;
-    r.a0 = load16_unaligned(src + 16u * l);
-    r.a1 = load16_unaligned(src + 1024u + 16u * l);
+    if (((uintptr_t)src & 15u) == 0u) {  // (aligned blocks, segment-store slots): one load each
+        r.a0 = *(const uint4 *)(src + 16u * l);
+        r.a1 = *(const uint4 *)(src + 1024u + 16u * l);
+    } else {
+        r.a0 = load16_unaligned(src + 16u * l);
+        r.a1 = load16_unaligned(src + 1024u + 16u * l);
+    }
     r.b0 = r.a0;
     r.b1 = r.a1;
     if (head) {
