@@ -7,7 +7,7 @@ for r in $(seq 1 ${2:-3}); do
   for v in a b; do
     lib=$PWD/wanproxy_amd/libxcodec_hip.so
     [ $v = b ] && lib=$PWD/wanproxy_amd/libxcodec_hip_b.so
-    XC_LIB_PATH=$lib timeout -k 10 200 python bench.py --no-cpu --no-e2e --no-decode --verify 4 --steps 20 > $out/$v$r.log 2>&1 || exit 1
+    XC_LIB_PATH=$lib timeout -k 10 200 python bench.py --no-cpu --no-e2e --no-decode --verify ${AB_VERIFY:-4} --steps 20 > $out/$v$r.log 2>&1 || exit 1
     python -c "import json; d=json.loads(open('$out/$v$r.log').read().strip().splitlines()[-1]); print('$v', $r, d['value'], d['kernel_ms_per_step'])"
   done
 done

@@ -1,0 +1,17 @@
+# Builds an alternative library wanproxy_amd/libxcodec_hip_b.so (for tools/ab.sh) from the current
+# sources with extra compiler flags, in a scratch directory (the in-tree objects stay untouched).
+# usage (here, on the CPU): bash tools/build_variant.sh [-DFLAG ...]
+set -e
+root=$(cd "$(dirname "$0")/.." && pwd)
+out=$(mktemp -d /tmp/xcvar.XXXXXX)
+mkdir -p "$out"/include "$out"/w/csrc
+cp "$root"/include/*.h "$out"/include/
+cp "$root"/wanproxy_amd/csrc/*.hip "$root"/wanproxy_amd/csrc/*.h "$root"/wanproxy_amd/csrc/*.cpp "$out"/w/csrc/
+cd "$out"/w/csrc
+FL="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -Wno-unused-value $*"
+for f in xc_encode xc_decode xc_runtime; do /opt/rocm/bin/hipcc $FL -c $f.hip -o $f.o & done
+g++ -O2 -std=c++17 -fPIC -Wall -c xc_stream.cpp -o xc_stream.o
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$root"/wanproxy_amd/libxcodec_hip_b.so *.o
+rm -rf "$out"
+echo "built wanproxy_amd/libxcodec_hip_b.so with: $*"
