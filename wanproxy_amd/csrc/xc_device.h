@@ -206,26 +206,14 @@ __device__ __forceinline__ uint32_t wave_sums32(uint32_t v[32])
     return v[0] + dpp_perm<0xB1>(v[0]);    // quad_perm [1,0,3,2]
 }
 
-// Hashes of n <= 8 consecutive 16-byte-aligned blocks at p: all loads are issued first, then
-// lane i (< n) receives block i's hash.  The 4 window sums of the 8 blocks are reduced together
-// (wave_sums32): value 4 i + c lands in lanes 8 i + 2 c (and + 1).
+// Hashes of G = 8 blocks held as 32 bytes per lane (w[i]: block i): lane i (< 8) receives block
+// i's hash.  The 4 window sums of the 8 blocks are reduced together (wave_sums32): value 4 i + c
+// lands in lanes 8 i + 2 c (and + 1).
 template <int G>
-__device__ __forceinline__ uint64_t wave_block_hashes(const uint8_t *p, uint32_t n)
+__device__ __forceinline__ uint64_t block_group_hash(const uint32_t w[G][8])
 {
     static_assert(G == 8, "8 blocks x 4 sums fill the 32-value transposed reduction");
     const uint32_t l = lane_id();
-    uint32_t w[G][8];
-#pragma unroll
-    for (int i = 0; i < G; i++) {
-#pragma unroll
-        for (int k = 0; k < 8; k++) w[i][k] = 0u;
-        if ((uint32_t)i < n) {
-            const uint4 *q = (const uint4 *)(p + (size_t)i * XC_SEG + 32u * l);
-            const uint4 x = q[0], y = q[1];
-            w[i][0] = x.x; w[i][1] = x.y; w[i][2] = x.z; w[i][3] = x.w;
-            w[i][4] = y.x; w[i][5] = y.y; w[i][6] = y.z; w[i][7] = y.w;
-        }
-    }
     uint32_t v[32];
     const uint32_t k = XC_SEG - 32u * l;  // weight of this lane's byte 0 is (2048 - 32l)
 #pragma unroll
@@ -242,6 +230,27 @@ __device__ __forceinline__ uint64_t wave_block_hashes(const uint8_t *p, uint32_t
     const uint32_t s1f = (uint32_t)__shfl((int)sum, src + 4), s2f = (uint32_t)__shfl((int)sum, src + 6);
     const uint32_t bytes_hash = (s1w << 20) + s2w, bits_hash = (s1f << 16) + s2f;
     return ((uint64_t)bits_hash << 36) + (uint64_t)bytes_hash;
+}
+
+// Hashes of n <= 8 consecutive 16-byte-aligned blocks at p: all loads are issued first, then
+// lane i (< n) receives block i's hash.
+template <int G>
+__device__ __forceinline__ uint64_t wave_block_hashes(const uint8_t *p, uint32_t n)
+{
+    const uint32_t l = lane_id();
+    uint32_t w[G][8];
+#pragma unroll
+    for (int i = 0; i < G; i++) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) w[i][k] = 0u;
+        if ((uint32_t)i < n) {
+            const uint4 *q = (const uint4 *)(p + (size_t)i * XC_SEG + 32u * l);
+            const uint4 x = q[0], y = q[1];
+            w[i][0] = x.x; w[i][1] = x.y; w[i][2] = x.z; w[i][3] = x.w;
+            w[i][4] = y.x; w[i][5] = y.y; w[i][6] = y.z; w[i][7] = y.w;
+        }
+    }
+    return block_group_hash<G>(w);
 }
 
 // 2048-byte equality of two windows (any alignment); wave-uniform result.
