@@ -278,7 +278,7 @@ __global__ __launch_bounds__(64 * SCAN_WAVES) void k_scan(ScanArgs a)
             const BlockSums cs = block_sums(w, l);
             // REF shadow: the block before s is a predicted REF, after which the reference looks
             // nothing up until s + 2047 (recorded below); k_walk verifies the REF happened
-            const bool shadowed = a.shadow && ((ballot(sflag != 0u) >> ((s - c0) >> 11)) & 1u) != 0u;
+            const bool shadowed = a.shadow && ((ballot(blk_cached(sflag)) >> ((s - c0) >> 11)) & 1u) != 0u;
             // window ending just before this lane's first position q = s + 32 l:
             // out-chunks of lanes >= l (previous block) + in-chunks of lanes < l.
             const uint32_t sufA = ps.totA - ps.preA, sufC = ps.totC - ps.preC;
@@ -475,10 +475,19 @@ __global__ __launch_bounds__(256) void k_resolve(ResolveArgs a)
     uint32_t rank = 0;
     for (uint32_t k = 0; k < cnt; k++) rank += readlane(p0, (int)k) < p0 ? 1u : 0u;
     const uint32_t q = (uint32_t)__builtin_amdgcn_ds_permute((int)(4u * (live ? rank : l)), (int)p0);
-    // full hashes: aligned windows from the block table (lane-parallel), the rest per wave
+    // full hashes: aligned windows from the block table (lane-parallel), the rest per wave.  On
+    // the first round (dmode 2) k_blockpredict already probed the cache for every aligned block
+    // of a buffer without carried state and entered the others in D: their slots come from
+    // blk_pref (the cache does not change between k_blockpredict and this kernel).
     const bool aligned = live && ((q + 1u) & (XC_SEG - 1u)) == 0u && P.blk_h;
+    const bool pref_ok = a.dmode == 2 && !stream_carried(P, ck.x);
     uint64_t h = 0;
-    if (aligned) h = P.blk_h[P.blk_base[ck.x] + (q + 1u) / XC_SEG - 1u];
+    uint32_t pref = 0;
+    if (aligned) {
+        const uint32_t gi = P.chunk_blk[c] + (q + 1u) / XC_SEG - 1u;
+        h = P.blk_h[gi];
+        if (pref_ok) pref = P.blk_pref[gi];
+    }
     for (uint64_t m = ballot(live && !aligned); m; m &= m - 1) {
         const int f = __ffsll((unsigned long long)m) - 1;
         const uint32_t qf = readlane(q, f);
@@ -488,8 +497,18 @@ __global__ __launch_bounds__(256) void k_resolve(ResolveArgs a)
     // cache then declaration-set probes, lane-parallel
     uint64_t v = 0;
     uint32_t st = ST_MISS;
-    if (live && a.dmode != 1 && set_find(P.cache, h, &v)) st = ST_EQUAL;
-    if (live && st == ST_MISS && a.dmode != 0) {
+    const bool known = pref != 0u;  // (aligned and pref_ok)
+    if (known) {
+        if (blk_cached(pref)) {
+            st = ST_EQUAL;  // (until the comparison below)
+            v = pref - 1u;
+        } else {
+            st = ST_MATCH;
+            v = P.dset.vals[pref & ~BP_DECL];
+        }
+    }
+    if (live && !known && a.dmode != 1 && set_find(P.cache, h, &v)) st = ST_EQUAL;
+    if (live && !known && st == ST_MISS && a.dmode != 0) {
         if (set_find(P.dset, h, &v)) st = ST_MATCH;
         else v = 0;
     }
@@ -804,7 +823,7 @@ __device__ __forceinline__ void walk_seq(const WalkArgs &a, uint32_t b, uint64_t
         const uint32_t nblk = len / XC_SEG, bb = P.blk_base[b];
         bool miss = false;
         for (uint32_t k = l; k < nblk; k += 64u)
-            if ((k + 1u) * XC_SEG < len && P.blk_pref[bb + k] && !((ref_done[k >> 5] >> (k & 31u)) & 1u))
+            if ((k + 1u) * XC_SEG < len && blk_cached(P.blk_pref[bb + k]) && !((ref_done[k >> 5] >> (k & 31u)) & 1u))
                 miss = true;
         if (ballot(miss) && l == 0) atomicOr(&P.ctl[CTL_SHADOW], 1u);
     }
@@ -983,10 +1002,14 @@ __global__ __launch_bounds__(256) void k_blockpredict(DeclArgs a)
     }
     const uint64_t h = P.blk_h[g];
     uint64_t v;
-    const bool cached = set_find(P.cache, h, &v);
-    P.blk_pref[g] = cached ? 1u : 0u;
-    // (the set's level-2 filter is P.l2mix, the combined filter the scan reads)
-    if (!cached) set_insert(P.dset, h, ((uint64_t)b << 32) | (k * XC_SEG + 2u * XC_SEG - 1u), true, nullptr, nullptr);
+    if (set_find(P.cache, h, &v)) {
+        P.blk_pref[g] = (uint32_t)v + 1u;  // (cache capacity <= 2^23)
+    } else {
+        // (the set's level-2 filter is P.l2mix, the combined filter the scan reads)
+        uint32_t slot;
+        set_insert(P.dset, h, ((uint64_t)b << 32) | (k * XC_SEG + 2u * XC_SEG - 1u), true, &slot, nullptr);
+        P.blk_pref[g] = BP_DECL | slot;
+    }
 }
 
 // -------------------------------------------------------------- k_emit ------------------

@@ -88,10 +88,14 @@ struct PlanDev {
     uint64_t *out_len;
     uint32_t *ctl;
     uint32_t *l2mix;  // level-2 filter of cache | predicted declarations (combined scan)
-    // REF shadows: blk_pref[g] = 1 when aligned block g (global index) is in the cache, so the
-    // window ending at its last byte is a predicted REF; the reference looks nothing up in the
-    // 2047 positions after a REF (xcodec_encoder.cc:111-118 resets the hash), so the scan may
-    // skip the next block's windows and the walk verifies that the REF happened.
+    // k_blockpredict's verdict on aligned block g (global index), see blk_cached():
+    //   cached slot + 1 (positive as int32): the block is in the cache, so the window ending at
+    //     its last byte is a predicted REF.  REF shadows: the reference looks nothing up in the
+    //     2047 positions after a REF (xcodec_encoder.cc:111-118 resets the hash), so the scan may
+    //     skip the next block's windows and the walk verifies that the REF happened;
+    //   0x80000000 | D slot: a predicted declaration, entered in D at that slot;
+    //   0: no prediction (carried stream state).
+    // k_resolve's first round takes the aligned windows' cache and D slots from here.
     uint32_t *blk_pref;
     const uint32_t *chunk_blk;  // [nchunks] global index of the chunk's buffer's block 0
     // Stateful streams (xc_encode / xc_flush, xcodec_encoder.cc:60-201 across calls), or null
@@ -104,6 +108,8 @@ struct PlanDev {
     uint2 *stream_res;
 };
 constexpr uint32_t SF_NOFLUSH = 1u;
+constexpr uint32_t BP_DECL = 0x80000000u;  // blk_pref: predicted declaration | D slot
+__device__ __forceinline__ bool blk_cached(uint32_t pref) { return (int32_t)pref > 0; }
 // A buffer with carried-over state (earlier positions already looked up, or a pending
 // candidate): the aligned-block predictions and REF shadows do not apply to it.
 __device__ __forceinline__ bool stream_carried(const PlanDev &P, uint32_t b)
