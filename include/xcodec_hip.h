@@ -66,6 +66,9 @@ int xc_cache_enter(xc_cache *c, uint64_t hash, const uint8_t *seg);
 /* XCodecHash::hash (xcodec/xcodec_hash.h:166-174) of n device-resident, 2048-byte-strided
  * segments -> n hashes (device).  stream may be NULL. */
 int xc_hash_segments(xc_ctx *ctx, const uint8_t *d_segs, uint64_t n, uint64_t *d_out, void *stream);
+/* The same from host memory (n segments at segs, hashes to out; synchronous): the hash of a
+ * <LEARN>ed segment, DecodeFilter::consume (xcodec/xcodec_filter.cc:320-322). */
+int xc_hash_segments_host(xc_ctx *ctx, const uint8_t *segs, uint64_t n, uint64_t *out);
 
 /* The encoder's rolling hash (xcodec/xcodec_hash.h:93-164 as driven by
  * xcodec/xcodec_encoder.cc:72-84) at every window end of one device buffer:

@@ -43,6 +43,9 @@ def _load() -> C.CDLL:
     lib.xo_cache_count.restype = C.c_size_t
     lib.xo_cache_count.argtypes = [C.c_void_p]
     lib.xo_cache_entry.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_uint64), C.c_void_p]
+    lib.xo_cache_lookup.restype = C.c_int
+    lib.xo_cache_lookup.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]
+    lib.xo_cache_enter.argtypes = [C.c_void_p, C.c_uint64, _u8p]
     lib.xo_encode_batch.argtypes = [C.c_void_p, _u8p, _u64p, _u64p, C.c_size_t, _u8p, _u64p,
                                     _u64p, _u64p]
     lib.xo_decode_batch.argtypes = [C.c_void_p, _u8p, _u64p, _u64p, C.c_size_t, _u8p, _u64p,
@@ -125,6 +128,19 @@ class Cache:
             lib().xo_cache_entry(self.h, i, C.byref(h), seg.ctypes.data_as(C.c_void_p))
             out.append((h.value, seg.tobytes()))
         return out
+
+    def lookup(self, h: int) -> bytes | None:
+        """XCodecMemoryCache::lookup (xcodec/xcodec_cache.h:190-210)."""
+        p = C.c_void_p()
+        if not lib().xo_cache_lookup(self.h, h, C.byref(p)):
+            return None
+        return C.string_at(p, 2048)
+
+    def enter(self, h: int, seg) -> None:
+        """XCodecMemoryCache::enter (xcodec/xcodec_cache.h:182-188)."""
+        seg = np.ascontiguousarray(_as_u8(seg))
+        assert seg.size == 2048
+        lib().xo_cache_enter(self.h, h, seg)
 
     def encode_batch(self, bufs) -> list[bytes]:
         arena, offs, lens = _packed(bufs)

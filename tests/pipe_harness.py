@@ -1,0 +1,126 @@
+"""Test harness for wanproxy_amd.pipe: a duplex pair of XCodec pipes (one EncodeFilter and one
+DecodeFilter per side, each side with its own cache registry, as two proxies would have),
+connected by queued "wires" so that <ASK>/<LEARN> round trips happen between consume calls as
+they do over sockets (xcodec/xcodec_filter.cc, proxy/proxy_connector.cc:154-189).
+
+OracleBackend runs the filters over the oracle restatement (test infrastructure only): the CPU
+tests use it to check the framing state machine, the GPU tests as the expected wire bytes."""
+import numpy as np
+
+from wanproxy_amd import pipe as P
+
+UUID_A = "0f1e2d3c-4b5a-6978-8796-a5b4c3d2e1f0"
+UUID_B = "12345678-9abc-def0-1234-56789abcdef0"
+
+
+class OracleBackend:
+    def __init__(self, oracle_mod):
+        self.o = oracle_mod
+
+    def new_store(self):
+        return self.o.Cache()
+
+    def new_encoder(self, store):
+        return self.o.Encoder(store)
+
+    def encode(self, encoder, data, flush):
+        out = encoder.encode(data)
+        if flush:
+            out += encoder.flush()[1]
+        return out
+
+    def flush(self, encoder):
+        return encoder.flush()
+
+    def decode(self, store, data):
+        st, out, consumed, unknown = store.decode_batch([data])[0]
+        return bool(st), out, consumed, unknown
+
+    def hash_segment(self, seg):
+        return int(self.o.hash_segment(np.frombuffer(seg, np.uint8)))
+
+
+class Wire(P.Filter):
+    """A socket: bytes queue up until pump() delivers them."""
+
+    def __init__(self):
+        super().__init__()
+        self.q = bytearray()
+        self.log = bytearray()  # everything ever sent
+        self.flushes = []
+
+    def consume(self, buf, flg=0):
+        self.q += buf
+        self.log += buf
+        return True
+
+    def flush(self, flg):
+        self.flushes.append(flg)
+
+
+class Side:
+    def __init__(self, backend, uuid, warm=None, waiting=False, size=64):
+        self.registry = P.CacheRegistry(backend)
+        store = backend.new_store()
+        if warm is not None:
+            warm(store)
+        self.cache = self.registry.register(P.CodecCache(store, uuid, size))
+        self.codec = P.Codec(backend, self.cache, self.registry)
+        self.enc = P.EncodeFilter(self.codec, 1 if waiting else 0)
+        self.dec = P.DecodeFilter(self.codec)
+        self.sink = P.Sink()
+        self.wire = Wire()
+        self.enc.chain(self.wire)
+        self.dec.chain(self.sink)
+        self.dec.set_upstream(self.enc)
+
+
+def pump(a: Side, b: Side, chunk=None, max_rounds=10**7):
+    """Deliver queued wire bytes (a -> b.dec, b -> a.dec) until both wires are idle; every
+    consume must succeed.  ``chunk``: deliver at most that many bytes per consume call."""
+    for _ in range(max_rounds):
+        moved = False
+        for src, dst in ((a, b), (b, a)):
+            if src.wire.q:
+                n = len(src.wire.q) if chunk is None else min(chunk, len(src.wire.q))
+                data = bytes(src.wire.q[:n])
+                del src.wire.q[:n]
+                assert dst.dec.consume(data), "decode filter failed"
+                moved = True
+        if not moved:
+            return
+    raise AssertionError("pipes did not settle")
+
+
+def parse(stream: bytes):
+    """Split a pipe stream into (op, payload) messages."""
+    out, i = [], 0
+    while i < len(stream):
+        op = stream[i]
+        if op == P.OP_HELLO:
+            n = stream[i + 1]
+            out.append((op, stream[i + 2:i + 2 + n]))
+            i += 2 + n
+        elif op == P.OP_FRAME:
+            n = int.from_bytes(stream[i + 1:i + 3], "big")
+            out.append((op, stream[i + 3:i + 3 + n]))
+            i += 3 + n
+        elif op == P.OP_ASK:
+            out.append((op, stream[i + 1:i + 9]))
+            i += 9
+        elif op == P.OP_LEARN:
+            out.append((op, stream[i + 1:i + 1 + 2048]))
+            i += 1 + 2048
+        elif op in (P.OP_EOS, P.OP_EOS_ACK):
+            out.append((op, b""))
+            i += 1
+        else:
+            raise AssertionError(f"bad op {op:#x} at {i}")
+    return out
+
+
+def esc_buffer(n, seed, frac=0.05):
+    rng = np.random.default_rng(seed)
+    b = rng.integers(0, 256, n, dtype=np.uint8)
+    b[rng.random(n) < frac] = 0xF1
+    return b

@@ -467,6 +467,26 @@ extern "C" int xc_hash_segments(xc_ctx *ctx, const uint8_t *d_segs, uint64_t n, 
     return XC_OK;
 }
 
+extern "C" int xc_hash_segments_host(xc_ctx *ctx, const uint8_t *segs, uint64_t n, uint64_t *out)
+{
+    if (!ctx || (n && (!segs || !out))) return fail(XC_EINVAL, "null");
+    if (n == 0) return XC_OK;
+    int rc = set_dev(ctx);
+    if (rc) return rc;
+    hipStream_t s = ctx->stream;
+    uint8_t *d_segs = nullptr;
+    uint64_t *d_out = nullptr;
+    if ((rc = xc__dalloc((void **)&d_segs, n * XC_SEG))) return rc;
+    if ((rc = xc__dalloc((void **)&d_out, n * 8))) return rc;
+    HIPCHK(hipMemcpyAsync(d_segs, segs, n * XC_SEG, hipMemcpyHostToDevice, s));
+    if ((rc = xc_hash_segments(ctx, d_segs, n, d_out, s))) return rc;
+    HIPCHK(hipMemcpyAsync(out, d_out, n * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    xc__pfree(d_segs);
+    xc__pfree(d_out);
+    return XC_OK;
+}
+
 extern "C" int xc_window_hashes(xc_ctx *ctx, const uint8_t *d_in, uint64_t n, uint64_t *d_out, void *stream)
 {
     if (!ctx) return fail(XC_EINVAL, "null");

@@ -34,6 +34,7 @@ SYMBOLS = [
     "xc_plan_set_streams", "xc_plan_stream_results", "xc_encoder_create", "xc_encoder_destroy",
     "xc_encoder_pending", "xc_encode", "xc_flush", "xc_encode_streams",
     "xc_decode_plan_create", "xc_dplan_destroy", "xc_dplan_layout", "xc_decode_run", "xc_dplan_stats",
+    "xc_hash_segments_host",
 ]
 STREAM_FLUSH = 1  # XC_STREAM_FLUSH
 
@@ -100,6 +101,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.xc_cache_lookup.argtypes = [_vp, C.c_uint64, _u8p, C.POINTER(C.c_int)]
     lib.xc_cache_enter.argtypes = [_vp, C.c_uint64, _u8p]
     lib.xc_hash_segments.argtypes = [_vp, _vp, C.c_uint64, _vp, _vp]
+    lib.xc_hash_segments_host.argtypes = [_vp, _u8p, C.c_uint64, _u64p]
     lib.xc_window_hashes.argtypes = [_vp, _vp, C.c_uint64, _vp, _vp]
     lib.xc_encode_plan_create.argtypes = [_vp, _u64p, C.c_uint64, C.POINTER(_vp)]
     lib.xc_plan_destroy.argtypes = [_vp]
@@ -538,6 +540,18 @@ class HostBuffer:
 
 def hash_segments(ctx: Context, d_segs: int, n: int, d_out: int, stream: int | None = None) -> None:
     _check(load_library().xc_hash_segments(ctx.h, d_segs, n, d_out, stream))
+
+
+def hash_segments_host(ctx: Context, segs) -> np.ndarray:
+    """XCodecHash::hash (xcodec/xcodec_hash.h:166-174) of the consecutive 2048-byte segments in
+    host memory ``segs``, computed on the device."""
+    segs = np.ascontiguousarray(_as_u8(segs))
+    if segs.size % SEGMENT_LENGTH:
+        raise ValueError("segments must be whole 2048-byte blocks")
+    n = segs.size // SEGMENT_LENGTH
+    out = np.zeros(max(n, 1), np.uint64)
+    _check(load_library().xc_hash_segments_host(ctx.h, segs, n, out))
+    return out[:n]
 
 
 def window_hashes(ctx: Context, d_in: int, n: int, d_out: int, stream: int | None = None) -> None:
