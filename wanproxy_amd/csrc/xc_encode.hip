@@ -92,18 +92,16 @@ __device__ __forceinline__ void pend_issue(const ScanArgs &a, Pending &pd, const
     pd.n = qn;
     pd.c = c;
     pd.c0 = c0;
+    // every lane loads (empty slots: word 0), so the count of outstanding loads is static and
+    // the compiler can keep these in flight across the next iteration
 #pragma unroll
     for (int s = 0; s < 2; s++) {
         const uint32_t i = lane_id() + 64u * s;
-        pd.pos[s] = 0;
-        pd.lo[s] = 0;
-        pd.w[s] = make_uint2(0, 0);
-        if (i < qn) {
-            const uint2 e = queue[i];
-            pd.pos[s] = e.x;
-            pd.lo[s] = e.y;
-            pd.w[s] = a.l2[l2_mix(e.y) >> 14];
-        }
+        const uint2 e = queue[i];
+        const bool v = i < qn;
+        pd.pos[s] = v ? e.x : 0u;
+        pd.lo[s] = v ? e.y : 0u;
+        pd.w[s] = a.l2[v ? l2_mix(e.y) >> 14 : 0u];
     }
 }
 
@@ -355,10 +353,8 @@ __global__ __launch_bounds__(64 * SCAN_WAVES) void k_scan(ScanArgs a)
                 }
             }
             if (MODE == 4) { sink = sink * 31u + qn + queue[l & 63u].y; qn = 0; }
-            if (qn) {
-                pend_issue(a, pd, queue, qn, c, c0);
-                qn = 0;
-            }
+            pend_issue(a, pd, queue, qn, c, c0);  // (also when empty: a static load count)
+            qn = 0;
 #pragma unroll
             for (int d = 0; d < 8; d++) { pw[d] = w[d]; w[d] = wn[d]; wn[d] = wn2[d]; }
             ps = cs;
