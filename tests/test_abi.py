@@ -51,3 +51,15 @@ def test_no_oracle_in_product_path():
             if f.endswith((".py", ".hip", ".h", ".cpp")):
                 s = open(os.path.join(dp, f)).read()
                 assert "oracle" not in s.lower() or f == "__init__.py" and False, f
+
+
+def test_cpp_host_layer_compiles_and_links():
+    """include/xcodec_hip.hpp (the C++ host layer) compiles warning-free as C++17, and its check
+    program links against the library (no GPU needed for either)."""
+    hpp = os.path.join(ROOT, "include", "xcodec_hip.hpp")
+    subprocess.run(["g++", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-fsyntax-only", "-x", "c++", "-"],
+                   input=f'#include "{hpp}"\n', text=True, check=True)
+    prog = os.path.join(ROOT, "tests", "cpp", "xchip_roundtrip")
+    assert os.access(prog, os.X_OK), "built by wanproxy_amd/csrc/Makefile (__graft_entry__.build())"
+    out = subprocess.run(["ldd", prog], capture_output=True, text=True, check=True).stdout
+    assert "libxcodec_hip.so" in out and "not found" not in out
