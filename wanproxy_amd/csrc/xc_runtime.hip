@@ -1045,7 +1045,7 @@ static int launch_emit(xc_plan *p, uint32_t j0, uint32_t jc, uint32_t gate_sb = 
 // stream) has passed; ev_hash[k] marks completion.
 static int enqueue_block_hash(xc_plan *p, uint32_t k, hipEvent_t after)
 {
-    HIPCHK(hipStreamWaitEvent(p->hs, after, 0));
+    if (after) HIPCHK(hipStreamWaitEvent(p->hs, after, 0));
     if (p->host_path) HIPCHK(hipStreamWaitEvent(p->hs, p->ev_h2d[k], 0));  // its input has landed
     const uint32_t g0 = p->grp_base[p->sub[k]], g1 = p->grp_base[p->sub[k + 1]];
     DeclArgs d{p->P, g0, g1};  // a range of block groups
@@ -1068,8 +1068,15 @@ static int launch_first_round(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t s1,
     const uint32_t ck_lo = p->chunk0[j0], ck_hi = p->chunk0[s1];
     p->stats.outer_rounds++;
     if (p->next_hash <= sb) {  // first sub-batch of the run: nothing to overlap with
-        HIPCHK(hipEventRecord(p->ev_start, s));
-        if ((rc = enqueue_block_hash(p, sb, p->ev_start))) return rc;
+        // Block hashes depend on the input only (ready when the run is called, or after the
+        // host path's copy), so the first ones need not wait for the main stream: they overlap
+        // whatever was enqueued there before the run (a cache restore).
+        hipEvent_t after = nullptr;
+        if (sb != 0) {
+            HIPCHK(hipEventRecord(p->ev_start, s));
+            after = p->ev_start;
+        }
+        if ((rc = enqueue_block_hash(p, sb, after))) return rc;
     }
     HIPCHK(hipStreamWaitEvent(s, p->ev_hash[sb], 0));
     hipLaunchKernelGGL(k_clear_set, dim3(1024), dim3(256), 0, s, p->P.dset, p->dset.n_lo, p->dset.n_full,
