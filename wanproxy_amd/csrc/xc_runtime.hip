@@ -573,6 +573,8 @@ struct xc_plan {
     // scans; sub-batch k's prediction step waits for ev_hash[k]
     hipStream_t hs = nullptr;
     hipEvent_t ev_start = nullptr;
+    uint32_t *h_ctl = nullptr;  // pinned copy of the control words (read_ctl)
+    hipEvent_t ev_ctl = nullptr;
     std::vector<hipEvent_t> ev_hash, ev_go;
     uint32_t next_hash = 0;  // first sub-batch not yet enqueued for hashing in this run
     // end-to-end host path (xc_encode_run_host): per-sub-batch H2D on a copy stream, packing
@@ -867,6 +869,8 @@ extern "C" int xc_plan_destroy(xc_plan *p)
         hipStreamSynchronize(p->hs);  // (the context's side stream: kept)
     }
     if (p->ev_start) hipEventDestroy(p->ev_start);
+    if (p->ev_ctl) hipEventDestroy(p->ev_ctl);
+    if (p->h_ctl) pool_free(p->h_ctl);
     if (p->cs) {
         hipStreamSynchronize(p->cs);  // (the context's copy stream: kept)
     }
@@ -966,11 +970,21 @@ extern "C" int xc_plan_stream_results(xc_plan *p, uint64_t *base, int64_t *cand)
     return XC_OK;
 }
 
+// The run's one host wait: the control words through a pinned buffer, then a spin on an event
+// (returns within a few us of the copy; a blocking stream synchronize wakes up later).
 static int read_ctl(xc_plan *p, uint32_t *ctl)
 {
     hipStream_t s = p->cache->ctx->stream;
-    HIPCHK(hipMemcpyAsync(ctl, p->P.ctl, CTL_WORDS * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    if (!p->h_ctl) {
+        if (hmalloc((void **)&p->h_ctl, CTL_WORDS * 4) != hipSuccess) return fail(XC_ENOMEM, "pinned allocation failed");
+        HIPCHK(hipEventCreateWithFlags(&p->ev_ctl, hipEventDisableTiming));
+    }
+    HIPCHK(hipMemcpyAsync(p->h_ctl, p->P.ctl, CTL_WORDS * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipEventRecord(p->ev_ctl, s));
+    hipError_t e;
+    while ((e = hipEventQuery(p->ev_ctl)) == hipErrorNotReady) { }
+    HIPCHK(e);
+    memcpy(ctl, p->h_ctl, CTL_WORDS * 4);
     ev_collect(p);
     return XC_OK;
 }
