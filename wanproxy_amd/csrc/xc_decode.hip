@@ -598,6 +598,8 @@ struct xc_dplan {
     DecDev D{};
     xc_decode_stats stats{};
     std::vector<void *> owned;
+    uint32_t *h_ctl = nullptr;    // pinned copy of the control words (the run's host wait)
+    hipEvent_t ev_ctl = nullptr;
     template <class T>
     int alloc(T **p, size_t n)
     {
@@ -613,6 +615,8 @@ extern "C" int xc_dplan_destroy(xc_dplan *p)
     hipSetDevice(p->dev);
     hipStreamSynchronize(p->s);
     for (void *x : p->owned) xc__pfree(x);
+    if (p->h_ctl) xc__pfree(p->h_ctl);
+    if (p->ev_ctl) hipEventDestroy(p->ev_ctl);
     delete p;
     return XC_OK;
 }
@@ -751,6 +755,7 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
     };
     // output and cache commit: these kernels return at once while DCTL_FIX is set, so round 0
     // and the emit are enqueued together and the host waits once in the common case
+    int rc0 = XC_OK;
     auto emit = [&]() -> int {
         hipLaunchKernelGGL(k_dalloc, dim3(1), dim3(1024), 0, s, D);  // slots first: k_demit fills them
         DHIP(hipGetLastError());
@@ -758,8 +763,17 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
         DHIP(hipGetLastError());
         hipLaunchKernelGGL(k_dcommit, dim3((ns + 3) / 4), dim3(256), 0, s, D);
         DHIP(hipGetLastError());
-        DHIP(hipMemcpyAsync(ctl, D.ctl, DCTL_WORDS * 4, hipMemcpyDeviceToHost, s));
-        DHIP(hipStreamSynchronize(s));
+        // through a pinned buffer, then a spin on an event: back within a few us of the copy
+        if (!p->h_ctl) {
+            if ((rc0 = xc__halloc((void **)&p->h_ctl, DCTL_WORDS * 4))) return rc0;
+            DHIP(hipEventCreateWithFlags(&p->ev_ctl, hipEventDisableTiming));
+        }
+        DHIP(hipMemcpyAsync(p->h_ctl, D.ctl, DCTL_WORDS * 4, hipMemcpyDeviceToHost, s));
+        DHIP(hipEventRecord(p->ev_ctl, s));
+        hipError_t e;
+        while ((e = hipEventQuery(p->ev_ctl)) == hipErrorNotReady) { }
+        DHIP(e);
+        memcpy(ctl, p->h_ctl, DCTL_WORDS * 4);
         return XC_OK;
     };
     int rc;
