@@ -43,8 +43,61 @@ def parse():
     ap.add_argument("--verify", type=int, default=16, help="buffers checked against the oracle (rank 0)")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-decode", action="store_true")
+    ap.add_argument("--no-legs", action="store_true", help="skip the cfg2 / cfg3 encode lines")
     ap.add_argument("--decode-streams", type=int, default=4096, help="cfg4: streams decoded per step")
     return ap.parse_args()
+
+
+def bench_encode_leg(ctx, warm, bufs, steps, verify):
+    """One more encode configuration of BASELINE.json (device resident, one GPU): every step
+    restores the cache snapshot (the warm pool, or empty for a cold cache) and encodes bufs."""
+    import torch
+    import wanproxy_amd as w
+    from wanproxy_amd import workloads as W
+    n = len(bufs)
+    cache = w.XCodecCache(ctx, W.POOL_SEGMENTS + n * (W.BUF // SEG + 1) + 1024)
+    if warm is not None:
+        w.XCodecEncoder(cache).encode_batch(warm)
+    cache.snapshot()
+    lens = np.array([b.size for b in bufs], np.uint64)
+    plan = w.EncodePlan(cache, lens)
+    arena = np.zeros(plan.in_bytes, np.uint8)
+    for i, b in enumerate(bufs):
+        arena[int(plan.in_off[i]):int(plan.in_off[i]) + b.size] = b
+    d_in = torch.from_numpy(arena).cuda()
+    d_out = torch.zeros(plan.out_bytes, dtype=torch.uint8, device="cuda")
+    d_len = torch.zeros(n, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+
+    def step():
+        cache.restore_async()
+        plan.run(d_in.data_ptr(), d_out.data_ptr(), d_len.data_ptr())
+
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / steps
+    olen = d_len.cpu().numpy()
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # checker only
+    oc = oracle.Cache()
+    if warm is not None:
+        oc.encode_batch(warm)
+    want = oc.encode_batch([bufs[i] for i in range(min(verify, n))])
+    out = d_out.cpu().numpy()
+    for i, x in enumerate(want):
+        o = int(plan.out_off[i])
+        if out[o:o + int(olen[i])].tobytes() != x:
+            raise SystemExit("bench: GPU output differs from the oracle (extra configuration)")
+    plan.close()
+    cache.close()
+    return {"value": round(int(lens.sum()) / el / 2**30, 3), "unit": "GiB/s", "ms_per_step": round(el * 1e3, 3),
+            "buffers": n, "out_over_in": round(float(olen.sum()) / float(lens.sum()), 4),
+            "verified_buffers": len(want)}
 
 
 def bench_decode(args, ctx, warm):
@@ -292,6 +345,15 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_decode:
         result["decode"] = bench_decode(args, ctx, warm)
+
+    if rank == 0 and world == 1 and not args.no_legs:
+        # BASELINE.json configs[1] and [2] (parity-test cases; value stays cfg5)
+        result["other_configs"] = {
+            "cfg2": dict(bench_encode_leg(ctx, None, W.random_buffers(256), 20, 8),
+                         workload="256 x 64 KiB, 0% repeats, cold (empty) cache"),
+            "cfg3": dict(bench_encode_leg(ctx, warm, list(W.repeat_shard(4096, 0x77)), 20, 8),
+                         workload="4096 x 64 KiB, 50% repeats, seed 0x77, warm pool cache"),
+        }
 
     if rank == 0 and world == 1 and not args.no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
