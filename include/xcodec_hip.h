@@ -88,7 +88,10 @@ int xc_plan_layout(xc_plan *p, uint64_t *in_off, uint64_t *out_off, uint64_t *in
                    uint64_t *out_bytes);
 /* Device-resident encode: d_in / d_out are device arenas in the plan's layout, d_out_len
  * receives nbuf uint64 lengths (device).  Blocks the host until the batch is decided
- * (the codec's sequential-order fix-ups need a host decision), results are on the device. */
+ * (the codec's sequential-order fix-ups need a host decision), results are on the device.
+ * Ordering: the run starts after everything enqueued on the context stream (xc_ctx_stream)
+ * before the call, e.g. an async copy into d_in or xc_cache_restore_async; input written on any
+ * other stream must be complete (or ordered before the context stream by the caller). */
 int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_out_len);
 /* Host-to-host convenience: pinned H2D, xc_encode_run, D2H.  out_len receives nbuf lengths. */
 int xc_encode_batch_host(xc_cache *c, const uint8_t *in, const uint64_t *in_off,

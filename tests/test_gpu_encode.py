@@ -343,3 +343,38 @@ def test_host_path_capacity(gpu_ctx, oracle_mod):
     import wanproxy_amd as w
     with pytest.raises(w.XCodecError):
         _host_path(gpu_ctx, oracle_mod, [W.gen(9, 65536)], [], cap=1000)
+
+
+def test_input_written_on_context_stream(gpu_ctx, oracle_mod):
+    """xc_encode_run is ordered after the context stream (xcodec_hip.h): an input arena filled by
+    an asynchronous copy enqueued on xc_ctx_stream just before restore_async + run is the input
+    that gets encoded — block hashing on the side stream included."""
+    import torch
+    import wanproxy_amd as w
+    n = 256
+    warm = W.pool_warmup_buffers()
+    cache = w.XCodecCache(gpu_ctx, W.POOL_SEGMENTS + n * 33 + 1024)
+    w.XCodecEncoder(cache).encode_batch(warm)
+    cache.snapshot()
+    plan = w.EncodePlan(cache, np.full(n, W.BUF, np.uint64))
+    d_in = torch.zeros(plan.in_bytes, dtype=torch.uint8, device="cuda")
+    d_out = torch.zeros(plan.out_bytes, dtype=torch.uint8, device="cuda")
+    d_len = torch.zeros(n, dtype=torch.int64, device="cuda")
+    for seed in (0x5555, 0x77):
+        bufs = W.repeat_shard(n, seed)
+        src = torch.from_numpy(bufs.reshape(-1)).cuda()
+        torch.cuda.synchronize()
+        with torch.cuda.stream(torch.cuda.ExternalStream(gpu_ctx.stream)):
+            d_in.zero_()  # a kernel ahead of the copy: the copy lands late
+            d_in[:n * W.BUF].copy_(src, non_blocking=True)
+        cache.restore_async()
+        plan.run(d_in.data_ptr(), d_out.data_ptr(), d_len.data_ptr())
+        torch.cuda.synchronize()
+        ref = oracle_mod.Cache()
+        ref.encode_batch(warm)
+        want = ref.encode_batch([bufs[i] for i in range(n)])
+        lens = d_len.cpu().numpy()
+        out = d_out.cpu().numpy()
+        for i in range(n):
+            o = int(plan.out_off[i])
+            assert out[o:o + int(lens[i])].tobytes() == want[i], (seed, i)

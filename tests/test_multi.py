@@ -92,7 +92,7 @@ def test_bench_small_gpu():
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--total", "256", "--steps", "2",
-                          "--warmup", "1", "--cpu-sample", "32"], capture_output=True, text=True, timeout=600)
+                          "--warmup", "1", "--cpu-threads", "4"], capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stderr[-2000:]
     line = [x for x in out.stdout.splitlines() if x.startswith("{")][-1]
     r = json.loads(line)

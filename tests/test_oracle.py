@@ -160,3 +160,21 @@ def test_stateful_encoder_split_invariance(oracle_mod):
     assert e.encode(W.gen(7, 2047)) == b""
     assert e.flush()[0] is True
     assert e.flush() == (False, b"")
+
+
+def test_fullsize_digest_fixture(oracle_mod):
+    """tests/golden/fullsize_digests.npz (made by tests/golden/make_fullsize.py) against a fresh
+    oracle run: all of cfg2, the first buffers of cfg3, of cfg5 at N = 1 and of an N = 8 shard."""
+    z = np.load(os.path.join(GOLD, "fullsize_digests.npz"))
+    warm = W.pool_warmup_buffers()
+    cases = [("cfg2", np.stack(W.random_buffers(256)), False, 256),
+             ("cfg3", W.repeat_shard(4096, 0x77)[:128], True, 128),
+             ("cfg5_g1_r0", W.repeat_shard(1024, 0x5555)[:128], True, 128),
+             ("cfg5_g8_r3", W.repeat_shard(32768, 0x5555, 3, 8)[:64], True, 64)]
+    for name, bufs, warmed, n in cases:
+        c = oracle_mod.Cache()
+        if warmed:
+            c.encode_batch(warm)
+        outs = c.encode_batch([bufs[i] for i in range(n)])
+        assert [len(o) for o in outs] == [int(x) for x in z[name + "_len"][:n]], name
+        assert [W.stream_digest(o) for o in outs] == [int(x) for x in z[name + "_dig"][:n]], name

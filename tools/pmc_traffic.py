@@ -1,42 +1,62 @@
-"""HBM traffic per launch of the dominant kernel from rocprofv3 PMC passes (tools/pmc_kernels.sh).
+"""HBM traffic of one cfg5 encode step, every kernel, from rocprofv3 PMC passes (tools/pmc_kernels.sh).
 
-FETCH_SIZE and WRITE_SIZE are in KiB.  Per MI355X_MICROARCH.md (HBM section), on gfx950 FETCH_SIZE
-reports half the bytes of wide coalesced streaming reads (16 B per lane), so it is doubled;
-WRITE_SIZE is exact for 16-B-per-lane streaming stores.  The scan's other reads (8-B gathers into
-the L2-resident filter and the lo32 sets) are not calibrated; they are a small share at cfg5.
+A step is a cache restore (k_undo_dev) followed by the encode's kernels; the PMC runs are
+`bench.py --steps 1 --warmup 0 --no-cpu --no-e2e --no-decode --no-legs`, whose last 3 steps are the
+diagnostic steps after the timed one.  Each of those steps spans the dispatches from its
+k_undo_dev to the next one (the last to the end); only the library's kernels (xc::) count.
 
-usage: python tools/pmc_traffic.py PMC_DIR OUT_JSON SUB_BATCHES [kernel_regex]
+FETCH_SIZE and WRITE_SIZE are in KiB.  Per MI355X_MICROARCH.md (HBM section), on gfx950
+FETCH_SIZE reports half the bytes of wide coalesced streaming reads (16 B per lane), so it is
+doubled; WRITE_SIZE is exact for 16-B-per-lane streaming stores.  Narrow gathers (the scan's filter
+and set probes, the tables' random reads) are not calibrated: doubling them overstates them, so the
+figure is an upper bound on the bytes the step moves.
+
+usage: python tools/pmc_traffic.py PMC_DIR OUT_JSON SUB_BATCHES ALG_BYTES_PER_STEP
 """
+import collections
 import csv
 import json
-import re
 import sys
 
 
-def per_dispatch(path, counter, kernel):
+def dispatches(path, counter):
     out = {}
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] == counter and re.search(kernel, r["Kernel_Name"]):
-            out[int(r["Dispatch_Id"])] = (int(r["Grid_Size"]), float(r["Counter_Value"]))
+        if r["Counter_Name"] == counter:
+            out[int(r["Dispatch_Id"])] = (r["Kernel_Name"].split("(")[0], float(r["Counter_Value"]))
     return out
+
+
+def steps(disp, n=3):
+    ids = sorted(disp)
+    starts = [i for i in ids if "k_undo_dev" in disp[i][0]][-n:]
+    bounds = starts + [ids[-1] + 1]
+    return [[i for i in ids if bounds[k] <= i < bounds[k + 1] and disp[i][0].startswith(("xc::", "void xc::"))]
+            for k in range(len(starts))]
 
 
 def main():
     d, out_path = sys.argv[1], sys.argv[2]
-    sub_batches = int(sys.argv[3])
-    kernel = sys.argv[4] if len(sys.argv) > 4 else r"k_scan<0>"
-    fetch = per_dispatch(f"{d}/p3/run_counter_collection.csv", "FETCH_SIZE", kernel)
-    write = per_dispatch(f"{d}/p4/run_counter_collection.csv", "WRITE_SIZE", kernel)
-    grid = max(g for g, _ in fetch.values())  # the cfg5 step launches (the warm-up encode is smaller)
-    f = [v for g, v in fetch.values() if g == grid]
-    w = [v for g, v in write.values() if g == grid]
-    fetch_kib, write_kib = sum(f) / len(f), sum(w) / len(w)
-    rec = {"kernel": kernel, "launches": len(f), "grid": grid, "sub_batches": sub_batches,
-           "fetch_size_kib_raw": round(fetch_kib, 1), "write_size_kib": round(write_kib, 1),
-           "traffic_bytes_per_launch": int((2 * fetch_kib + write_kib) * 1024),
+    sub_batches, alg = int(sys.argv[3]), int(sys.argv[4])
+    fetch = dispatches(f"{d}/p3/run_counter_collection.csv", "FETCH_SIZE")
+    write = dispatches(f"{d}/p4/run_counter_collection.csv", "WRITE_SIZE")
+    per_kernel = collections.defaultdict(lambda: [0.0, 0.0])
+    fs, ws = steps(fetch), steps(write)
+    for st in fs:
+        for i in st:
+            per_kernel[fetch[i][0]][0] += fetch[i][1] / len(fs)
+    for st in ws:
+        for i in st:
+            per_kernel[write[i][0]][1] += write[i][1] / len(ws)
+    kib = sum(2 * f + w for f, w in per_kernel.values())
+    rec = {"steps_averaged": len(fs), "sub_batches": sub_batches,
+           "traffic_bytes_per_step": int(kib * 1024), "alg_bytes_per_step": alg,
+           "traffic_over_alg": round(kib * 1024 / alg, 3),
+           "per_kernel_bytes": {k: {"fetch_x2": int(2 * f * 1024), "write": int(w * 1024)}
+                                for k, (f, w) in sorted(per_kernel.items(), key=lambda x: -(2 * x[1][0] + x[1][1]))},
            "correction": "FETCH_SIZE x2 (gfx950 wide streaming reads), WRITE_SIZE x1; KiB -> bytes"}
     json.dump(rec, open(out_path, "w"), indent=1)
-    print(json.dumps(rec))
+    print(json.dumps(rec, indent=1))
 
 
 if __name__ == "__main__":

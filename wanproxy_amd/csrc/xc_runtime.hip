@@ -1082,15 +1082,10 @@ static int launch_first_round(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t s1,
     const uint32_t ck_lo = p->chunk0[j0], ck_hi = p->chunk0[s1];
     p->stats.outer_rounds++;
     if (p->next_hash <= sb) {  // first sub-batch of the run: nothing to overlap with
-        // Block hashes depend on the input only (ready when the run is called, or after the
-        // host path's copy), so the first ones need not wait for the main stream: they overlap
-        // whatever was enqueued there before the run (a cache restore).
-        hipEvent_t after = nullptr;
-        if (sb != 0) {
-            HIPCHK(hipEventRecord(p->ev_start, s));
-            after = p->ev_start;
-        }
-        if ((rc = enqueue_block_hash(p, sb, after))) return rc;
+        // Block hashes read the input, which the caller may have written with work enqueued on
+        // the context stream (xc_ctx_stream) before the run: the side stream starts after it.
+        HIPCHK(hipEventRecord(p->ev_start, s));
+        if ((rc = enqueue_block_hash(p, sb, p->ev_start))) return rc;
     }
     HIPCHK(hipStreamWaitEvent(s, p->ev_hash[sb], 0));
     hipLaunchKernelGGL(k_clear_set, dim3(1024), dim3(256), 0, s, p->P.dset, p->dset.n_lo, p->dset.n_full,

@@ -14,6 +14,8 @@ of a generator whose state starts at ``seed``.  The configs:
 """
 from __future__ import annotations
 
+import hashlib
+
 import numpy as np
 
 GAMMA = np.uint64(0x9E3779B97F4A7C15)
@@ -128,6 +130,18 @@ def repeat_shard(total: int, seed: int, rank: int = 0, world: int = 1, repeat_pc
     fresh = ~rep
     out[fresh] = gen_segments(draws[fresh])
     return out.reshape(draws.shape[0], slots * SEG)
+
+
+def stream_digest(b) -> int:
+    """First 8 bytes of sha256(b) as a little-endian uint64 (the per-buffer digest of
+    tests/golden/fullsize_digests.npz)."""
+    return int.from_bytes(hashlib.sha256(b).digest()[:8], "little")
+
+
+def arena_digests(arena: np.ndarray, offs, lens) -> np.ndarray:
+    """Per-buffer digests (:func:`stream_digest`) of the streams arena[offs[i]:offs[i]+lens[i]]."""
+    mv = memoryview(np.ascontiguousarray(arena))
+    return np.array([stream_digest(mv[int(o):int(o) + int(n)]) for o, n in zip(offs, lens)], np.uint64)
 
 
 def pack(buffers: list[np.ndarray], align: int = 256) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
