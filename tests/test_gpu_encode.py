@@ -219,6 +219,21 @@ def test_many_subbatches_async_pipeline(gpu_ctx, oracle_mod, monkeypatch):
     buffer's new declaration in the same sub-batch, self-referencing char runs, collisions); the
     host then redoes that sub-batch step by step and restarts the pass after it."""
     monkeypatch.setenv("XC_SUB_MB", "1")
+    bufs, warm = _mixed_batch()
+    _check(gpu_ctx, oracle_mod, bufs, warm=warm)
+
+
+@pytest.mark.parametrize("blocks", ["1", "3", "8"])
+def test_scan_chunk_lengths(gpu_ctx, oracle_mod, monkeypatch, blocks):
+    """The scan's chunk length and work unit are chosen per plan from the batch size (2 KiB
+    chunks for a few buffers, 16 KiB for big batches); forced here, the bytes do not change."""
+    monkeypatch.setenv("XC_CHUNK_BLOCKS", blocks)
+    bufs, warm = _mixed_batch()
+    _check(gpu_ctx, oracle_mod, bufs, warm=warm)
+    _check(gpu_ctx, oracle_mod, W.random_buffers(24) + [W.gen(9, 1 << 20), W.gen(5, 2049)])
+
+
+def _mixed_batch():
     x, y = _collision_pair(7)
     a = W.gen(51, 65536)
     pool = W.pool(64)
@@ -241,7 +256,7 @@ def test_many_subbatches_async_pipeline(gpu_ctx, oracle_mod, monkeypatch):
             bufs.append(_esc(40000, k))
         else:
             bufs.append(a.copy())
-    _check(gpu_ctx, oracle_mod, bufs, warm=[[pool[i:i + 65536] for i in range(0, 8 * 65536, 65536)]])
+    return bufs, [[pool[i:i + 65536] for i in range(0, 8 * 65536, 65536)]]
 
 
 def test_ref_shadow_misses(gpu_ctx, oracle_mod, monkeypatch):
@@ -378,3 +393,46 @@ def test_input_written_on_context_stream(gpu_ctx, oracle_mod):
         for i in range(n):
             o = int(plan.out_off[i])
             assert out[o:o + int(lens[i])].tobytes() == want[i], (seed, i)
+
+
+@pytest.mark.parametrize("no_graph", ["0", "1"])
+def test_graph_replay_and_recapture(gpu_ctx, oracle_mod, monkeypatch, no_graph):
+    """xc_encode_run replays its asynchronous pass as a HIP graph captured on the first run with
+    the given arenas; a run with other arenas captures again, and a sub-batch the gate hands back
+    to the host (cross-buffer duplicates, self references) still takes the step-by-step path after
+    the graph.  Every run equals the oracle; XC_NO_GRAPH=1 (direct enqueue) gives the same bytes."""
+    import torch
+    import wanproxy_amd as w
+    monkeypatch.setenv("XC_SUB_MB", "1")
+    monkeypatch.setenv("XC_NO_GRAPH", no_graph)
+    bufs, warm = _mixed_batch()
+    oc = oracle_mod.Cache()
+    for batch in warm:
+        oc.encode_batch(batch)
+    want = oc.encode_batch(bufs)
+    cache = w.XCodecCache(gpu_ctx, 1 << 14)
+    for batch in warm:
+        w.XCodecEncoder(cache).encode_batch(batch)
+    cache.snapshot()
+    plan = w.EncodePlan(cache, [len(b) for b in bufs])
+    arena = np.zeros(plan.in_bytes, np.uint8)
+    for i, b in enumerate(bufs):
+        arena[int(plan.in_off[i]):int(plan.in_off[i]) + len(b)] = b
+    d_in = torch.from_numpy(arena).cuda()
+    outs = [torch.zeros(plan.out_bytes, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    d_len = torch.zeros(len(bufs), dtype=torch.int64, device="cuda")
+    stats = []
+    for it in range(5):
+        d_out = outs[it % 2] if it < 4 else outs[0]
+        d_out.zero_()
+        torch.cuda.synchronize()
+        cache.restore_async()
+        plan.run(d_in.data_ptr(), d_out.data_ptr(), d_len.data_ptr())
+        torch.cuda.synchronize()
+        out, lens = d_out.cpu().numpy(), d_len.cpu().numpy()
+        for i in range(len(bufs)):
+            o = int(plan.out_off[i])
+            assert out[o:o + int(lens[i])].tobytes() == want[i], (it, i)
+        st = plan.stats()
+        stats.append((st.sub_batches, st.redone, st.n_extract, st.n_ref))
+    assert len(set(stats)) == 1 and stats[0][1] > 0, stats  # same pass every run, some redone

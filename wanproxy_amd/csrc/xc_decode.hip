@@ -567,6 +567,7 @@ using namespace xc;
 // (>= 2050 bytes each) enter the batch provider table, which is sized by that bound.
 
 // The cache object is defined in xc_runtime.hip; these accessors expose what we need.
+extern "C" void xc__cache_count_unknown(xc_cache *c);
 extern "C" int xc__cache_devset(xc_cache *c, void *devset, uint8_t **segs, uint32_t **count, uint32_t *cap,
                                 uint2 **undo, void **stream, int *dev);
 extern "C" int xc__set_error(int code, const char *msg);
@@ -732,6 +733,7 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
     const hipStream_t s = p->s;
     uint32_t ctl[DCTL_WORDS] = {};
     int rounds = 0;
+    xc__cache_count_unknown(p->cache);  // the run enters segments: the host's copy of the count is stale
     DHIP(hipMemsetAsync(D.ctl, 0, DCTL_WORDS * 4, s));
     hipLaunchKernelGGL(k_dtok, dim3(ns), dim3(64), 0, s, D, 1);
     DHIP(hipGetLastError());

@@ -444,6 +444,15 @@ __device__ __forceinline__ bool set_find(const DevSet &s, uint64_t h, uint64_t *
 __device__ __forceinline__ int set_insert(const DevSet &s, uint64_t h, uint64_t val, bool min_merge,
                                           uint32_t *slot_out, uint32_t *lo_slot_out)
 {
+    // filter bits first: their atomics return nothing, so none waits, and setting them again
+    // for a key already present changes nothing
+    {
+        const uint32_t lo = (uint32_t)h;
+        atomicOr(&s.filt[filt_word(lo)], (1u << (lo & 31u)) | (1u << ((lo >> 5) & 31u)));
+        const uint32_t g = l2_mix(lo), gi = (g >> 14) * 2u;
+        atomicOr(&s.l2[gi], 1u << (g & 31u));
+        atomicOr(&s.l2[gi + 1u], 1u << ((g >> 5) & 31u));
+    }
     uint32_t i = key_slot(h, s.mask);
     int fresh = 0;
     for (;;) {
@@ -469,10 +478,6 @@ __device__ __forceinline__ int set_insert(const DevSet &s, uint64_t h, uint64_t 
                 j = (j + 1u) & s.lo_mask;
             }
         }
-        atomicOr(&s.filt[filt_word(lo)], (1u << (lo & 31u)) | (1u << ((lo >> 5) & 31u)));
-        const uint32_t g = l2_mix(lo), gi = (g >> 14) * 2u;
-        atomicOr(&s.l2[gi], 1u << (g & 31u));
-        atomicOr(&s.l2[gi + 1u], 1u << ((g >> 5) & 31u));
     }
     if (lo_slot_out) *lo_slot_out = los;
     return fresh;

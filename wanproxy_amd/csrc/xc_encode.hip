@@ -209,21 +209,25 @@ __global__ __launch_bounds__(64 * SCAN_WAVES) void k_scan(ScanArgs a)
     }
     __syncthreads();
 
-    // Work distribution: waves take runs of SCAN_UNIT consecutive chunks from a counter (chunks
+    // Work distribution: waves take runs of a.unit consecutive chunks from a counter (chunks
     // of one buffer continue the block stream and its prefetch without a restart), the next run
     // always claimed one run ahead.  Dynamic, because the cost of a chunk varies (REF shadows,
     // filter positives) and other kernels may hold some CUs when the scan starts.
     // The first run of every wave is static (wave g: run g), so only the look-ahead claims
     // contend on the counter.
+    // When the static first runs cover every chunk (small batches) no wave claims: claims from
+    // thousands of waves at once serialize on the counter's one address.
     const uint32_t nwaves = gridDim.x * SCAN_WAVES;
+    const bool dynamic = nwaves * a.unit < a.ck_hi - a.ck_lo;
     auto claim = [&]() -> uint32_t {
+        if (!dynamic) return a.ck_hi;
         uint32_t t = 0;
-        if (l == 0) t = atomicAdd(&a.P.ctl[CTL_SCAN_NEXT], SCAN_UNIT);
-        return a.ck_lo + nwaves * SCAN_UNIT + uniform(t);
+        if (l == 0) t = atomicAdd(&a.P.ctl[CTL_SCAN_NEXT], a.unit);
+        return a.ck_lo + nwaves * a.unit + uniform(t);
     };
-    uint32_t c = a.ck_lo + (blockIdx.x * SCAN_WAVES + wave) * SCAN_UNIT;
+    uint32_t c = a.ck_lo + (blockIdx.x * SCAN_WAVES + wave) * a.unit;
     if (c >= a.ck_hi) return;
-    uint32_t c_end = min(c + SCAN_UNIT, a.ck_hi);
+    uint32_t c_end = min(c + a.unit, a.ck_hi);
     uint32_t c_nxt = claim();
 
     // chunk descriptors: {c0, c1, arena offset lo, hi}; the next one is always in flight
@@ -386,7 +390,7 @@ __global__ __launch_bounds__(64 * SCAN_WAVES) void k_scan(ScanArgs a)
             c += 1u;
         } else {
             c = c_nxt;
-            c_end = min(c + SCAN_UNIT, a.ck_hi);
+            c_end = min(c + a.unit, a.ck_hi);
             c_nxt = claim();
         }
         dsc = dn;
@@ -860,45 +864,66 @@ __device__ __forceinline__ bool walk_blocks(const WalkArgs &a, uint32_t b)
     if (!stream_plain(P, b)) return false;  // carried state or no flush: the sequential walk
     bool ok = true, cross = false;
     uint32_t n_ext = 0, n_ref = 0;
-    for (uint32_t c = ck0; c < ck1 && ballot(!ok) == 0; c++) {
-        const uint32_t cnt = uniform(P.S.cnt[c]);
-        const uint32_t c0 = (c - ck0) * P.chunk_len;
-        const uint32_t want = min(c0 + P.chunk_len, len) / XC_SEG - c0 / XC_SEG;  // aligned ends
-        if (cnt & EV_DENSE) { ok = false; break; }
-        bool aligned = false;
-        if (l < cnt) {
-            const uint32_t e = c * EV_CAP + l;
-            const uint32_t q = P.S.pos[e], st = P.S.stat[e];
-            aligned = ((q + 1u) & (XC_SEG - 1u)) == 0u;
-            if (!aligned) {
-                if (st != ST_MISS) ok = false;
-            } else {
-                const uint32_t k = q / XC_SEG;
-                const uint64_t h = P.S.h[e], v = P.S.val[e];
-                const uint32_t dpos = q + XC_SEG;  // declaration point cand + 4095
-                if (st == ST_COLL) ok = false;
-                if (st == ST_MATCH && (uint32_t)(v >> 32) == b && (uint32_t)v < dpos) ok = false;  // self-REF
-                if (st == ST_MATCH && (uint32_t)(v >> 32) < b) cross = true;
-                const uint32_t t = tb + k;
-                if (st == ST_EQUAL) {
-                    P.tok_op[t] = OP_REF;
-                    P.tok_known[t] = 1u;
-                    P.tok_dpos[t] = 0u;
-                    P.tok_h[t] = h;
-                    n_ref++;
-                } else {
-                    P.tok_op[t] = OP_EXTRACT;
-                    P.tok_known[t] = st == ST_MATCH ? 1u : 0u;
-                    P.tok_dpos[t] = dpos < len ? dpos : DPOS_FLUSH;
-                    P.tok_h[t] = st == ST_MATCH ? h : 0u;
-                    n_ext++;
-                }
-                P.tok_lb[t] = k * XC_SEG;
-                P.tok_le[t] = k * XC_SEG;
-                P.tok_seg[t] = k * XC_SEG;
+    // chunks in groups of WB_GROUP: every load of a group is issued before any is used (a buffer
+    // of short chunks would otherwise pay one memory round trip per chunk)
+    constexpr uint32_t WB_GROUP = 4;
+    for (uint32_t cg = ck0; cg < ck1 && ballot(!ok) == 0; cg += WB_GROUP) {
+        uint32_t cnt[WB_GROUP], q[WB_GROUP], st[WB_GROUP];
+        uint64_t hh[WB_GROUP], vv[WB_GROUP];
+#pragma unroll
+        for (uint32_t i = 0; i < WB_GROUP; i++) {
+            cnt[i] = 0u;
+            q[i] = st[i] = 0u;
+            hh[i] = vv[i] = 0u;
+            if (cg + i < ck1) {  // (uniform) entries past the count are loaded but never used
+                const uint32_t e = (cg + i) * EV_CAP + l;
+                cnt[i] = uniform(P.S.cnt[cg + i]);
+                q[i] = P.S.pos[e];
+                st[i] = P.S.stat[e];
+                hh[i] = P.S.h[e];
+                vv[i] = P.S.val[e];
             }
         }
-        if ((uint32_t)__popcll(ballot(aligned)) != want) ok = false;  // each aligned end, once
+#pragma unroll
+        for (uint32_t i = 0; i < WB_GROUP; i++) {
+            const uint32_t c = cg + i;
+            if (c >= ck1) break;
+            const uint32_t c0 = (c - ck0) * P.chunk_len;
+            const uint32_t want = min(c0 + P.chunk_len, len) / XC_SEG - c0 / XC_SEG;  // aligned ends
+            if (cnt[i] & EV_DENSE) { ok = false; break; }
+            bool aligned = false;
+            if (l < cnt[i]) {
+                aligned = ((q[i] + 1u) & (XC_SEG - 1u)) == 0u;
+                if (!aligned) {
+                    if (st[i] != ST_MISS) ok = false;
+                } else {
+                    const uint32_t k = q[i] / XC_SEG;
+                    const uint64_t h = hh[i], v = vv[i];
+                    const uint32_t dpos = q[i] + XC_SEG;  // declaration point cand + 4095
+                    if (st[i] == ST_COLL) ok = false;
+                    if (st[i] == ST_MATCH && (uint32_t)(v >> 32) == b && (uint32_t)v < dpos) ok = false;  // self-REF
+                    if (st[i] == ST_MATCH && (uint32_t)(v >> 32) < b) cross = true;
+                    const uint32_t t = tb + k;
+                    if (st[i] == ST_EQUAL) {
+                        P.tok_op[t] = OP_REF;
+                        P.tok_known[t] = 1u;
+                        P.tok_dpos[t] = 0u;
+                        P.tok_h[t] = h;
+                        n_ref++;
+                    } else {
+                        P.tok_op[t] = OP_EXTRACT;
+                        P.tok_known[t] = st[i] == ST_MATCH ? 1u : 0u;
+                        P.tok_dpos[t] = dpos < len ? dpos : DPOS_FLUSH;
+                        P.tok_h[t] = st[i] == ST_MATCH ? h : 0u;
+                        n_ext++;
+                    }
+                    P.tok_lb[t] = k * XC_SEG;
+                    P.tok_le[t] = k * XC_SEG;
+                    P.tok_seg[t] = k * XC_SEG;
+                }
+            }
+            if ((uint32_t)__popcll(ballot(aligned)) != want) ok = false;  // each aligned end, once
+        }
     }
     if (ballot(!ok)) return false;
     n_ext = wave_sum(n_ext);
@@ -1051,6 +1076,7 @@ __device__ __forceinline__ uint32_t write_escaped(uint8_t *dst, const uint8_t *p
 }
 
 
+template <uint32_t EMIT_WAVES>
 __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
 {
     if (aborted(a.P)) return;
@@ -1172,6 +1198,9 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
     }
 }
 
+template __global__ void k_emit<4>(EmitArgs);
+template __global__ void k_emit<16>(EmitArgs);
+
 // One workgroup: cache slots for the declarations of buffers [j0, j1) in buffer order
 // (exclusive prefix of buf_next on top of the current segment count), plus run totals.
 __global__ __launch_bounds__(1024) void k_alloc(EmitArgs a)
@@ -1223,6 +1252,7 @@ __global__ __launch_bounds__(1024) void k_alloc(EmitArgs a)
     (void)nref_tot;
     if (threadIdx.x == 0) {
         *P.seg_count = carry[0];
+        P.ctl[CTL_COUNT] = carry[0];
         P.ctl[CTL_NEXTRACT] += carry[0] - start;
         P.ctl[CTL_NREF] += carry[1];
         if (carry[0] > P.seg_cap) P.ctl[CTL_ERROR] |= ERR_CAPACITY;
@@ -1346,10 +1376,14 @@ __global__ __launch_bounds__(64) void k_window_hashes(const uint8_t *in, uint32_
 
 // Clear a declaration set (all of its tables) and seed the combined level-2 filter with the
 // cache's: one launch instead of a memset per table.
-__global__ void k_clear_set(DevSet s, uint32_t n_lo, uint32_t n_full, uint4 *l2mix, const uint4 *cache_l2)
+__global__ void k_clear_set(DevSet s, uint32_t n_lo, uint32_t n_full, uint4 *l2mix, const uint4 *cache_l2,
+                            uint32_t *ctl_zero)
 {
     const uint32_t stride = gridDim.x * blockDim.x;
     const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
+    // a run's first sub-batch also clears the run's control words (nothing reads them before the
+    // kernels after this one)
+    if (ctl_zero && i0 < CTL_WORDS) ctl_zero[i0] = 0u;
     const uint4 z = make_uint4(0, 0, 0, 0), ones = make_uint4(~0u, ~0u, ~0u, ~0u);
     for (uint32_t i = i0; i < XC_FILT_WORDS / 4; i += stride) ((uint4 *)s.filt)[i] = z;
     const bool own_l2 = (const void *)s.l2 != (const void *)l2mix;  // (plans alias the two)
@@ -1403,6 +1437,25 @@ __global__ void k_undo_dev(DevSet cache, const uint2 *undo, uint32_t from, const
     for (uint32_t i = i0; i < XC_FILT_WORDS / 4; i += stride) ((uint4 *)cache.filt)[i] = snap_filt[i];
     for (uint32_t i = i0; i < XC_L2_WORDS / 2; i += stride) ((uint4 *)cache.l2)[i] = snap_l2[i];
     if (i0 == 0) *cache.lo_zero = *snap_lo_zero;
+}
+
+// The same with the current count known on the host (to): nothing reads the count, so the
+// restore writes the snapshot's count itself (one launch, no device-to-device copy).
+__global__ void k_undo_known(DevSet cache, const uint2 *undo, uint32_t from, uint32_t to, uint32_t *count,
+                             const uint4 *snap_filt, const uint4 *snap_l2, const uint32_t *snap_lo_zero)
+{
+    const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+    for (uint32_t i = from + i0; i < to; i += stride) {
+        const uint2 u = undo[i];
+        cache.keys[u.x] = XC_EMPTY64;
+        if (u.y != NONE) cache.lo_keys[u.y] = 0u;
+    }
+    for (uint32_t i = i0; i < XC_FILT_WORDS / 4; i += stride) ((uint4 *)cache.filt)[i] = snap_filt[i];
+    for (uint32_t i = i0; i < XC_L2_WORDS / 2; i += stride) ((uint4 *)cache.l2)[i] = snap_l2[i];
+    if (i0 == 0) {
+        *cache.lo_zero = *snap_lo_zero;
+        *count = from;
+    }
 }
 
 // Cache enter from the host API (single segment).

@@ -10,8 +10,8 @@ constexpr uint32_t EV_CAP = 64;          // sparse events per scan chunk before 
 constexpr uint32_t EV_DENSE = 0x80000000u;
 constexpr uint32_t Q_CAP = 128;          // per-wave LDS queue of level-1 filter positives
 constexpr uint32_t SCAN_WAVES = 16;      // waves per scan workgroup (one per CU: all of its LDS and VGPRs)
-constexpr uint32_t CHUNK_BLOCKS = 8;     // 2048-byte blocks per scan chunk (16 KiB)
-constexpr uint32_t SCAN_UNIT = 4;        // chunks a scan wave takes from the work counter at a time
+constexpr uint32_t CHUNK_BLOCKS = 8;     // most 2048-byte blocks per scan chunk (16 KiB; small plans use fewer)
+constexpr uint32_t SCAN_UNIT = 4;        // most chunks a scan wave takes from the work counter at a time
 constexpr uint32_t EMIT_WAVES = 4;       // k_emit waves per buffer (workgroup)
 constexpr uint32_t SCAN_LDS = XC_FILT_WORDS * 4u + SCAN_WAVES * Q_CAP * 8u;
 constexpr uint32_t MAX_BUF = 1u << 20;   // longest single buffer accepted (1 MiB)
@@ -41,6 +41,7 @@ enum : uint32_t {
     CTL_ABORT_SB = 8,  // ... and which one; every later pipeline kernel exits at once
     CTL_SHADOW = 9,    // a walk did not emit a predicted REF whose shadow the scan skipped
     CTL_SCAN_NEXT = 10,  // k_scan work counter (chunks handed out); k_resolve resets it
+    CTL_COUNT = 11,      // the cache's segment count after the last k_alloc (for the host)
     CTL_WORDS = 16
 };
 constexpr uint32_t ERR_CAPACITY = 1, ERR_TOKENS = 2, ERR_DECLS = 4;  // (ERR_PACK_CAP = 8 below)
@@ -142,6 +143,7 @@ struct ScanArgs {
     int has2;
     const uint2 *l2;  // level-2 filter of set (| set2): one 8-byte L2 read per level-1 positive
     int shadow;       // skip the windows in the shadow of predicted REFs (P.blk_pref)
+    uint32_t unit;    // chunks per work unit (the plan's scan granularity, <= SCAN_UNIT)
 };
 struct ResolveArgs {
     PlanDev P;
@@ -181,6 +183,7 @@ struct PackArgs {
 constexpr uint32_t ERR_PACK_CAP = 8;
 
 template <int MODE> __global__ void k_scan(ScanArgs a);
+template <uint32_t NW> __global__ void k_emit(EmitArgs a);
 __global__ void k_pack_offsets(PackArgs a);
 __global__ void k_pack_copy(PackArgs a);
 __global__ void k_resolve(ResolveArgs a);
@@ -188,14 +191,16 @@ __global__ void k_walk(WalkArgs a);
 __global__ void k_blockhash(DeclArgs a);
 __global__ void k_blockpredict(DeclArgs a);
 __global__ void k_or_words(uint4 *dst, const uint4 *a, const uint4 *b, uint32_t n);
-__global__ void k_emit(EmitArgs a);
 __global__ void k_alloc(EmitArgs a);
-__global__ void k_clear_set(DevSet s, uint32_t n_lo, uint32_t n_full, uint4 *l2mix, const uint4 *cache_l2);
+__global__ void k_clear_set(DevSet s, uint32_t n_lo, uint32_t n_full, uint4 *l2mix, const uint4 *cache_l2,
+                            uint32_t *ctl_zero);
 __global__ void k_hash_segments(const uint8_t *segs, uint64_t n, uint64_t *out);
 __global__ void k_window_hashes(const uint8_t *in, uint32_t n, uint64_t *out);
 __global__ void k_undo(DevSet cache, const uint2 *undo, uint32_t from, uint32_t to);
 __global__ void k_undo_dev(DevSet cache, const uint2 *undo, uint32_t from, const uint32_t *count, uint32_t cap,
                            const uint4 *snap_filt, const uint4 *snap_l2, const uint32_t *snap_lo_zero);
+__global__ void k_undo_known(DevSet cache, const uint2 *undo, uint32_t from, uint32_t to, uint32_t *count,
+                             const uint4 *snap_filt, const uint4 *snap_l2, const uint32_t *snap_lo_zero);
 __global__ void k_enter_one(PlanDev P, uint64_t h, const uint8_t *seg);
 __global__ void k_lookup_one(PlanDev P, uint64_t h, uint8_t *out, uint32_t *found);
 __global__ void k_selftest(uint32_t *err);

@@ -279,7 +279,15 @@ struct xc_cache {
     uint32_t *snap_lo_zero = nullptr;
     uint32_t *snap_count_dev = nullptr;
     uint32_t *snap_l2 = nullptr;
+    // the device's segment count as the host last learned it (a run's control words), or -1:
+    // lets a restore write the count itself instead of copying it on the device
+    int64_t host_count = -1;
 };
+
+extern "C" void xc__cache_count_unknown(xc_cache *c)
+{
+    if (c) c->host_count = -1;
+}
 
 static PlanDev cache_plandev(xc_cache *c)
 {
@@ -360,6 +368,7 @@ extern "C" int xc_cache_snapshot(xc_cache *c)
     int rc = set_dev(c->ctx);
     if (rc) return rc;
     if ((rc = cache_count_host(c, &c->snap_count))) return rc;
+    c->host_count = c->snap_count;
     hipStream_t s = c->ctx->stream;
     HIPCHK(hipMemcpyAsync(c->snap_filt, c->set.d.filt, XC_FILT_WORDS * 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(c->snap_lo_zero, c->set.d.lo_zero, 4, hipMemcpyDeviceToDevice, s));
@@ -396,6 +405,18 @@ extern "C" int xc_cache_restore_async(xc_cache *c)
     int rc = set_dev(c->ctx);
     if (rc) return rc;
     hipStream_t s = c->ctx->stream;
+    if (c->host_count >= 0) {
+        // one kernel: table slots entered since the snapshot, filters and count from the snapshot
+        const uint32_t to = (uint32_t)std::min<int64_t>(c->host_count, (int64_t)c->cap);
+        const uint32_t n = std::max<uint32_t>(to > c->snap_count ? to - c->snap_count : 0u, XC_L2_WORDS / 2);
+        const uint32_t blocks = std::min<uint32_t>((n + 255) / 256, 2048);
+        hipLaunchKernelGGL(k_undo_known, dim3(blocks), dim3(256), 0, s, c->set.d, (const uint2 *)c->undo,
+                           c->snap_count, to, c->count, (const uint4 *)c->snap_filt, (const uint4 *)c->snap_l2,
+                           (const uint32_t *)c->snap_lo_zero);
+        HIPCHK(hipGetLastError());
+        c->host_count = c->snap_count;
+        return XC_OK;
+    }
     // one kernel: table slots entered since the snapshot, filters copied back; then the count
     const uint32_t n = (uint32_t)std::max<uint64_t>(c->cap - c->snap_count, XC_L2_WORDS / 2);
     const uint32_t blocks = std::min<uint32_t>((n + 255) / 256, 2048);
@@ -404,6 +425,7 @@ extern "C" int xc_cache_restore_async(xc_cache *c)
                        (const uint4 *)c->snap_l2, (const uint32_t *)c->snap_lo_zero);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(c->count, c->snap_count_dev, 4, hipMemcpyDeviceToDevice, s));
+    c->host_count = c->snap_count;
     return XC_OK;
 }
 
@@ -417,6 +439,7 @@ extern "C" int xc_cache_restore(xc_cache *c)
     if ((rc = cache_count_host(c, &cur))) return rc;
     if ((rc = cache_restore_async(c, cur))) return rc;
     HIPCHK(hipStreamSynchronize(c->ctx->stream));
+    c->host_count = c->snap_count;
     return XC_OK;
 }
 
@@ -443,6 +466,7 @@ extern "C" int xc_cache_enter(xc_cache *c, uint64_t h, const uint8_t *seg)
     int rc = set_dev(c->ctx);
     if (rc) return rc;
     hipStream_t s = c->ctx->stream;
+    c->host_count = -1;
     HIPCHK(hipMemcpyAsync(c->ctx->d_seg, seg, XC_SEG, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemsetAsync(c->ctl, 0, CTL_WORDS * 4, s));
     hipLaunchKernelGGL(k_enter_one, dim3(1), dim3(64), 0, s, cache_plandev(c), h, (const uint8_t *)c->ctx->d_seg);
@@ -502,7 +526,7 @@ extern "C" int xc_window_hashes(xc_ctx *ctx, const uint8_t *d_in, uint64_t n, ui
 }
 
 // ------------------------------------------------------------------ plan ----------
-static const uint32_t CHUNK_LEN = 16384;
+static const uint32_t CHUNK_LEN = 16384;  // the longest scan chunk (plans of small batches use shorter ones)
 static_assert(CHUNK_LEN == CHUNK_BLOCKS * XC_SEG, "k_scan loads a chunk's shadow flags in one wave load");
 static const uint64_t SUB_BYTES_DEFAULT = 512ull << 20;  // sub-batch: bound on input bytes (tuned on cfg5)
 static const uint32_t SUB_BUFS = 32768;                  // sub-batch: bound on buffers
@@ -589,8 +613,21 @@ struct xc_plan {
     int shadow = 1;          // REF shadows in the async pass (XC_NO_SHADOW=1 disables)
     uint32_t max_decl = 2;   // longest buffer / 2048 + 2 (k_walk's LDS)
     uint32_t *d_chunk_blk = nullptr;
+    // scan granularity: chunk length (a multiple of 2048 up to CHUNK_LEN) and chunks per work
+    // unit, chosen so that the largest sub-batch gives every SIMD of the chip a unit
+    uint32_t chunk_len = CHUNK_LEN, scan_unit = SCAN_UNIT;
     uint4 *d_stream_st = nullptr;  // stateful streams (xc_plan_set_streams), else null
     uint2 *d_stream_res = nullptr;
+    // The asynchronous pass of a run (every sub-batch's kernels and the control-word readback) as
+    // a HIP graph: one launch instead of ~10 host launches per sub-batch, which bound small batches
+    // (the host enqueues slower than the device runs their kernels).  Captured on the first run
+    // with given arenas, replayed while they stay the same.
+    hipGraphExec_t gexec = nullptr;
+    const void *g_in = nullptr, *g_out = nullptr, *g_len = nullptr;
+    const void *g_stream = nullptr;  // P.stream_st the graph was captured with
+    xc_run_stats g_stats{};          // host-side counters of the captured pass
+    bool g_off = false;              // capture failed (or XC_NO_GRAPH): enqueue directly
+    bool zero_ctl = false;           // the next k_clear_set also clears the run's control words
 };
 
 static hipEvent_t ev_get(xc_plan *p)
@@ -652,6 +689,52 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     p->len.assign(lengths, lengths + nbuf);
     p->in_off.resize(nbuf);
     p->out_off.resize(nbuf);
+    // sub-batches (bounded input bytes and buffers, in index order)
+    p->sub.push_back(0);
+    uint64_t max_sub_blocks = 0;
+    {
+        uint64_t bytes = 0, blocks = 0;
+        uint32_t cnt = 0;
+        uint64_t decl = 0, maxdecl = 0;
+        const uint64_t sub_max = sub_bytes();
+        for (uint32_t i = 0; i < nbuf; i++) {
+            if (lengths[i] > MAX_BUF) return fail(XC_EINVAL, "buffer longer than 1 MiB");
+            if (cnt && (bytes + lengths[i] > sub_max || cnt >= SUB_BUFS)) {
+                p->sub.push_back(i);
+                maxdecl = std::max(maxdecl, decl);
+                max_sub_blocks = std::max(max_sub_blocks, blocks);
+                bytes = 0;
+                cnt = 0;
+                decl = 0;
+                blocks = 0;
+            }
+            bytes += lengths[i];
+            blocks += lengths[i] >= XC_SEG ? (lengths[i] + XC_SEG - 1) / XC_SEG : 0;
+            cnt++;
+            decl += lengths[i] / XC_SEG + 1;
+        }
+        maxdecl = std::max(maxdecl, decl);
+        max_sub_blocks = std::max(max_sub_blocks, blocks);
+        if (p->sub.back() != nbuf) p->sub.push_back((uint32_t)nbuf);
+        if ((rc = p->dset.alloc(std::max<uint64_t>(maxdecl, 64)))) return rc;
+    }
+    // scan granularity: the longest chunks and units that still give every SIMD of the chip a
+    // work unit in the largest sub-batch (a 16 MiB batch would otherwise keep 16 of 256 CUs busy)
+    {
+        const uint64_t waves = (uint64_t)c->ctx->n_cu * SCAN_WAVES;
+        static const uint32_t opts[][2] = {{8, 4}, {8, 2}, {8, 1}, {4, 1}, {2, 1}, {1, 1}};  // blocks, unit
+        for (const auto &o : opts) {
+            p->chunk_len = o[0] * XC_SEG;
+            p->scan_unit = o[1];
+            if (max_sub_blocks / ((uint64_t)o[0] * o[1]) >= waves) break;
+        }
+        const char *e = getenv("XC_CHUNK_BLOCKS");  // (tuning experiments: force a chunk length, unit 1)
+        if (e && atoi(e) >= 1 && atoi(e) <= (int)CHUNK_BLOCKS) {
+            p->chunk_len = (uint32_t)atoi(e) * XC_SEG;
+            p->scan_unit = 1;
+        }
+    }
+    const uint32_t chunk_len = p->chunk_len;
     std::vector<uint32_t> blen(nbuf), chunk0(nbuf + 1), tok_base(nbuf + 1), blk_base(nbuf + 1);
     uint64_t nblk = 0;
     std::vector<uint2> chunks;
@@ -660,7 +743,6 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     uint64_t toks = 0;
     for (uint64_t i = 0; i < nbuf; i++) {
         uint64_t n = lengths[i];
-        if (n > MAX_BUF) return fail(XC_EINVAL, "buffer longer than 1 MiB");
         blen[i] = (uint32_t)n;
         p->in_off[i] = io;
         io += (n + 255) / 256 * 256;
@@ -668,13 +750,13 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
         oo += (2 * n + 16 + 255) / 256 * 256;
         chunk0[i] = (uint32_t)chunks.size();
         if (n >= XC_SEG)
-            for (uint32_t s = 0; s < n; s += CHUNK_LEN) {
+            for (uint32_t s = 0; s < n; s += chunk_len) {
                 chunks.push_back(make_uint2((uint32_t)i, s));
                 // bit 31 of the end position: the next chunk continues this buffer; bit 30: and
                 // it reaches past its first block (the scan's 2-deep prefetch ring needs to know)
-                const uint32_t more = (s + CHUNK_LEN < n ? 0x80000000u : 0u) |
-                                      (s + CHUNK_LEN + XC_SEG < n ? 0x40000000u : 0u);
-                descs.push_back(make_uint4(s, (uint32_t)std::min<uint64_t>(s + CHUNK_LEN, n) | more,
+                const uint32_t more = (s + chunk_len < n ? 0x80000000u : 0u) |
+                                      (s + chunk_len + XC_SEG < n ? 0x40000000u : 0u);
+                descs.push_back(make_uint4(s, (uint32_t)std::min<uint64_t>(s + chunk_len, n) | more,
                                            (uint32_t)p->in_off[i], (uint32_t)(p->in_off[i] >> 32)));
             }
         p->max_decl = std::max<uint32_t>(p->max_decl, (uint32_t)(n / XC_SEG) + 2u);
@@ -693,34 +775,11 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     p->chunk_bytes.assign(chunks.size() + 1, 0);
     for (size_t k = 0; k < chunks.size(); k++) {
         uint64_t n = lengths[chunks[k].x];
-        uint64_t e = std::min<uint64_t>(chunks[k].y + CHUNK_LEN, n);
+        uint64_t e = std::min<uint64_t>(chunks[k].y + chunk_len, n);
         p->chunk_bytes[k + 1] = p->chunk_bytes[k] + (e - chunks[k].y);
     }
-    // sub-batches
-    p->sub.push_back(0);
-    {
-        uint64_t bytes = 0;
-        uint32_t cnt = 0;
-        uint64_t decl = 0, maxdecl = 0;
-        const uint64_t sub_max = sub_bytes();
-        for (uint32_t i = 0; i < nbuf; i++) {
-            if (cnt && (bytes + lengths[i] > sub_max || cnt >= SUB_BUFS)) {
-                p->sub.push_back(i);
-                maxdecl = std::max(maxdecl, decl);
-                bytes = 0;
-                cnt = 0;
-                decl = 0;
-            }
-            bytes += lengths[i];
-            cnt++;
-            decl += lengths[i] / XC_SEG + 1;
-        }
-        maxdecl = std::max(maxdecl, decl);
-        if (p->sub.back() != nbuf) p->sub.push_back((uint32_t)nbuf);
-        if ((rc = p->dset.alloc(std::max<uint64_t>(maxdecl, 64)))) return rc;
-    }
-    if ((rc = p->S.alloc(p->nchunks, CHUNK_LEN))) return rc;
-    if ((rc = p->D.alloc(p->nchunks, CHUNK_LEN))) return rc;
+    if ((rc = p->S.alloc(p->nchunks, chunk_len))) return rc;
+    if ((rc = p->D.alloc(p->nchunks, chunk_len))) return rc;
 
     size_t nb1 = std::max<uint64_t>(nbuf, 1);
     HIPCHK(dmalloc(&p->d_buf_off, nb1 * 8));
@@ -751,7 +810,7 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     P.chunks = p->d_chunks;
     P.chunk_desc = p->d_desc;
     P.buf_chunk0 = p->d_chunk0;
-    P.chunk_len = CHUNK_LEN;
+    P.chunk_len = chunk_len;
     P.S = p->S.d;
     P.D = p->D.d;
     P.dset = p->dset.d;
@@ -868,6 +927,7 @@ extern "C" int xc_plan_destroy(xc_plan *p)
     if (p->hs) {
         hipStreamSynchronize(p->hs);  // (the context's side stream: kept)
     }
+    if (p->gexec) hipGraphExecDestroy(p->gexec);
     if (p->ev_start) hipEventDestroy(p->ev_start);
     if (p->ev_ctl) hipEventDestroy(p->ev_ctl);
     if (p->h_ctl) pool_free(p->h_ctl);
@@ -972,14 +1032,30 @@ extern "C" int xc_plan_stream_results(xc_plan *p, uint64_t *base, int64_t *cand)
 
 // The run's one host wait: the control words through a pinned buffer, then a spin on an event
 // (returns within a few us of the copy; a blocking stream synchronize wakes up later).
-static int read_ctl(xc_plan *p, uint32_t *ctl)
+static int ctl_buffers(xc_plan *p)
 {
-    hipStream_t s = p->cache->ctx->stream;
     if (!p->h_ctl) {
         if (hmalloc((void **)&p->h_ctl, CTL_WORDS * 4) != hipSuccess) return fail(XC_ENOMEM, "pinned allocation failed");
         HIPCHK(hipEventCreateWithFlags(&p->ev_ctl, hipEventDisableTiming));
     }
+    return XC_OK;
+}
+
+// Wait for the copy of the control words enqueued before ev_ctl.
+static int wait_ctl(xc_plan *p, uint32_t *ctl);
+
+static int read_ctl(xc_plan *p, uint32_t *ctl)
+{
+    hipStream_t s = p->cache->ctx->stream;
+    int rc = ctl_buffers(p);
+    if (rc) return rc;
     HIPCHK(hipMemcpyAsync(p->h_ctl, p->P.ctl, CTL_WORDS * 4, hipMemcpyDeviceToHost, s));
+    return wait_ctl(p, ctl);
+}
+
+static int wait_ctl(xc_plan *p, uint32_t *ctl)
+{
+    hipStream_t s = p->cache->ctx->stream;
     HIPCHK(hipEventRecord(p->ev_ctl, s));
     hipError_t e;
     while ((e = hipEventQuery(p->ev_ctl)) == hipErrorNotReady) { }
@@ -994,7 +1070,7 @@ static int launch_scan(xc_plan *p, const Layer &L, const DevSet &set, uint32_t c
 {
     if (ck_hi <= ck_lo) return XC_OK;
     xc_ctx *ctx = p->cache->ctx;
-    ScanArgs a{p->P, L, set, ck_lo, ck_hi, 0, DevSet{}, 0, (const uint2 *)set.l2, shadow};
+    ScanArgs a{p->P, L, set, ck_lo, ck_hi, 0, DevSet{}, 0, (const uint2 *)set.l2, shadow, p->scan_unit};
     if (set2) {
         a.set2 = *set2;
         a.has2 = 1;
@@ -1002,7 +1078,7 @@ static int launch_scan(xc_plan *p, const Layer &L, const DevSet &set, uint32_t c
     }
     KSpan span(p, XC_K_SCAN);
     if (p->timing) p->ktimes.scan_bytes += p->chunk_bytes[ck_hi] - p->chunk_bytes[ck_lo];
-    uint32_t need = (ck_hi - ck_lo + SCAN_WAVES * SCAN_UNIT - 1) / (SCAN_WAVES * SCAN_UNIT);
+    uint32_t need = (ck_hi - ck_lo + SCAN_WAVES * p->scan_unit - 1) / (SCAN_WAVES * p->scan_unit);
     uint32_t grid = std::min<uint32_t>(need, (uint32_t)ctx->n_cu);
     // XC_SCAN_ABLATION=m (timing experiments only: results are wrong) runs k_scan<m> in the pipeline
     static const int abl = getenv("XC_SCAN_ABLATION") ? atoi(getenv("XC_SCAN_ABLATION")) : 0;
@@ -1048,7 +1124,11 @@ static int launch_emit(xc_plan *p, uint32_t j0, uint32_t jc, uint32_t gate_sb = 
     hipLaunchKernelGGL(k_alloc, dim3(1), dim3(1024), 0, s, e);
     HIPCHK(hipGetLastError());
     KSpan span(p, XC_K_EMIT);
-    hipLaunchKernelGGL(k_emit, dim3(jc - j0), dim3(64 * EMIT_WAVES), 0, s, e);
+    // one workgroup per buffer: 4 waves when the buffers alone fill the chip, 16 for few buffers
+    if ((uint64_t)(jc - j0) * EMIT_WAVES >= (uint64_t)p->cache->ctx->n_cu * 16u)
+        hipLaunchKernelGGL(k_emit<EMIT_WAVES>, dim3(jc - j0), dim3(64 * EMIT_WAVES), 0, s, e);
+    else
+        hipLaunchKernelGGL(k_emit<16>, dim3(jc - j0), dim3(64 * 16), 0, s, e);
     HIPCHK(hipGetLastError());
     return XC_OK;
 }
@@ -1057,18 +1137,21 @@ static int launch_emit(xc_plan *p, uint32_t j0, uint32_t jc, uint32_t gate_sb = 
 // position of buffers [j0, s1) against cache + predictions, resolve, first walk round.
 // Hash sub-batch k's aligned blocks on the side stream once `after` (an event of the main
 // stream) has passed; ev_hash[k] marks completion.
-static int enqueue_block_hash(xc_plan *p, uint32_t k, hipEvent_t after)
+// On the main stream (st == nullptr: the run's first sub-batch, nothing to overlap with) no
+// events are needed.
+static int enqueue_block_hash(xc_plan *p, uint32_t k, hipEvent_t after, hipStream_t st)
 {
-    if (after) HIPCHK(hipStreamWaitEvent(p->hs, after, 0));
-    if (p->host_path) HIPCHK(hipStreamWaitEvent(p->hs, p->ev_h2d[k], 0));  // its input has landed
+    const bool side = st == p->hs;
+    if (after) HIPCHK(hipStreamWaitEvent(st, after, 0));
+    if (p->host_path) HIPCHK(hipStreamWaitEvent(st, p->ev_h2d[k], 0));  // its input has landed
     const uint32_t g0 = p->grp_base[p->sub[k]], g1 = p->grp_base[p->sub[k + 1]];
     DeclArgs d{p->P, g0, g1};  // a range of block groups
     if (g1 > g0) {
-        KSpan span(p, XC_K_BLOCKHASH, p->hs);
-        hipLaunchKernelGGL(k_blockhash, dim3((g1 - g0 + 3) / 4), dim3(256), 0, p->hs, d);
+        KSpan span(p, XC_K_BLOCKHASH, st);
+        hipLaunchKernelGGL(k_blockhash, dim3((g1 - g0 + 3) / 4), dim3(256), 0, st, d);
         HIPCHK(hipGetLastError());
     }
-    HIPCHK(hipEventRecord(p->ev_hash[k], p->hs));
+    if (side) HIPCHK(hipEventRecord(p->ev_hash[k], st));
     p->next_hash = k + 1;
     return XC_OK;
 }
@@ -1081,16 +1164,18 @@ static int launch_first_round(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t s1,
     int rc;
     const uint32_t ck_lo = p->chunk0[j0], ck_hi = p->chunk0[s1];
     p->stats.outer_rounds++;
-    if (p->next_hash <= sb) {  // first sub-batch of the run: nothing to overlap with
-        // Block hashes read the input, which the caller may have written with work enqueued on
-        // the context stream (xc_ctx_stream) before the run: the side stream starts after it.
-        HIPCHK(hipEventRecord(p->ev_start, s));
-        if ((rc = enqueue_block_hash(p, sb, p->ev_start))) return rc;
-    }
-    HIPCHK(hipStreamWaitEvent(s, p->ev_hash[sb], 0));
+    // the set's clear (and, first in a run, the control words' clear)
     hipLaunchKernelGGL(k_clear_set, dim3(1024), dim3(256), 0, s, p->P.dset, p->dset.n_lo, p->dset.n_full,
-                       (uint4 *)p->d_l2mix, (const uint4 *)p->P.cache.l2);
+                       (uint4 *)p->d_l2mix, (const uint4 *)p->P.cache.l2, p->zero_ctl ? p->P.ctl : nullptr);
     HIPCHK(hipGetLastError());
+    p->zero_ctl = false;
+    if (p->next_hash <= sb) {
+        // first sub-batch of the run: nothing to overlap with, its blocks are hashed in line
+        // (after whatever the caller enqueued on the context stream to fill the input)
+        if ((rc = enqueue_block_hash(p, sb, nullptr, s))) return rc;
+    } else {
+        HIPCHK(hipStreamWaitEvent(s, p->ev_hash[sb], 0));  // hashed ahead on the side stream
+    }
     {
         DeclArgs d{p->P, j0, s1};
         KSpan span(p, XC_K_DECLHASH);
@@ -1101,7 +1186,7 @@ static int launch_first_round(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t s1,
     // the next sub-batch's block hashes run beside this scan (memory-bound beside LDS/L2-bound)
     if (p->next_hash == sb + 1 && sb + 2 < p->sub.size()) {
         HIPCHK(hipEventRecord(p->ev_go[sb], s));
-        if ((rc = enqueue_block_hash(p, sb + 1, p->ev_go[sb]))) return rc;
+        if ((rc = enqueue_block_hash(p, sb + 1, p->ev_go[sb], p->hs))) return rc;
     }
     if ((rc = launch_scan(p, p->P.S, p->P.cache, ck_lo, ck_hi, &p->P.dset, shadow))) return rc;
     if ((rc = launch_resolve(p, p->P.S, 2, ck_lo, ck_hi))) return rc;
@@ -1163,6 +1248,66 @@ static int encode_sub_sync(xc_plan *p, uint32_t sb, uint32_t *ctl)
     return XC_OK;
 }
 
+// The graph path applies to device-resident runs without per-kernel timing events.
+static bool use_graph(xc_plan *p)
+{
+    const char *e = getenv("XC_NO_GRAPH");
+    return !(e && atoi(e)) && !p->g_off && !p->timing && !p->host_path && p->sub.size() > 1;
+}
+
+// The first asynchronous pass of a run (the ctl words were cleared before it) as a graph launch,
+// then the control-word wait.  (Re)captured when the arenas differ from the captured ones.
+static int run_graph(xc_plan *p, uint32_t *ctl)
+{
+    hipStream_t s = p->cache->ctx->stream;
+    int rc = ctl_buffers(p);
+    if (rc) return rc;
+    const size_t nsub = p->sub.size() - 1;
+    if (!p->gexec || p->g_in != p->P.in || p->g_out != p->P.out || p->g_len != p->P.out_len ||
+        p->g_stream != p->P.stream_st) {
+        if (p->gexec) {
+            HIPCHK(hipGraphExecDestroy(p->gexec));
+            p->gexec = nullptr;
+        }
+        // capture on the context stream (work the caller enqueued before it stays outside)
+        HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
+        const xc_run_stats st0 = p->stats;
+        for (size_t k = 0; k < nsub && !rc; k++) rc = encode_sub_async(p, (uint32_t)k);
+        if (!rc && hipMemcpyAsync(p->h_ctl, p->P.ctl, CTL_WORDS * 4, hipMemcpyDeviceToHost, s) != hipSuccess)
+            rc = fail(XC_EDEVICE, "graph capture: control-word copy");
+        hipGraph_t g = nullptr;
+        const hipError_t ce = hipStreamEndCapture(s, &g);
+        if (!rc && ce == hipSuccess && g && hipGraphInstantiate(&p->gexec, g, nullptr, nullptr, 0) == hipSuccess) {
+            p->g_stats = p->stats;
+            p->g_stats.sub_batches -= st0.sub_batches;
+            p->g_stats.outer_rounds -= st0.outer_rounds;
+            p->g_stats.walk_rounds -= st0.walk_rounds;
+            p->g_in = p->P.in;
+            p->g_out = p->P.out;
+            p->g_len = p->P.out_len;
+            p->g_stream = p->P.stream_st;
+        } else {
+            p->gexec = nullptr;
+        }
+        if (g) hipGraphDestroy(g);
+        (void)hipGetLastError();
+        p->stats = st0;
+        if (!p->gexec) {  // not capturable here: enqueue directly from now on
+            p->g_off = true;
+            p->next_hash = 0;
+            for (size_t k = 0; k < nsub; k++)
+                if ((rc = encode_sub_async(p, (uint32_t)k))) return rc;
+            return read_ctl(p, ctl);
+        }
+    }
+    HIPCHK(hipGraphLaunch(p->gexec, s));
+    p->stats.sub_batches += p->g_stats.sub_batches;
+    p->stats.outer_rounds += p->g_stats.outer_rounds;
+    p->stats.walk_rounds += p->g_stats.walk_rounds;
+    p->next_hash = (uint32_t)nsub;  // (the graph hashed every sub-batch's blocks)
+    return wait_ctl(p, ctl);
+}
+
 extern "C" int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_out_len)
 {
     if (!p || (!d_in && p->nb) || (!d_out && p->nb) || (!d_out_len && p->nb)) return fail(XC_EINVAL, "null");
@@ -1173,18 +1318,26 @@ extern "C" int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, ui
     p->P.out = d_out;
     p->P.out_len = d_out_len;
     p->stats = xc_run_stats{};
-    HIPCHK(hipMemsetAsync(p->P.ctl, 0, CTL_WORDS * 4, s));
+    p->cache->host_count = -1;
+    if (p->sub.size() > 1) p->zero_ctl = true;  // (the first k_clear_set clears the control words)
+    else HIPCHK(hipMemsetAsync(p->P.ctl, 0, CTL_WORDS * 4, s));
     uint32_t ctl[CTL_WORDS];
     p->next_hash = 0;
     const size_t nsub = p->sub.size() - 1;
     size_t si = 0;
     bool fresh = false;  // ctl was read after the last launch
+    bool first = true;   // the run's first asynchronous pass (the graph's part)
     while (si < nsub) {
         // Async pass: enqueue every remaining sub-batch with no host round trip.  k_gate
         // stops the device pipeline at the first sub-batch that needs the host.
-        for (size_t k = si; k < nsub; k++)
-            if ((rc = encode_sub_async(p, (uint32_t)k))) return rc;
-        if ((rc = read_ctl(p, ctl))) return rc;
+        if (first && use_graph(p)) {
+            if ((rc = run_graph(p, ctl))) return rc;
+        } else {
+            for (size_t k = si; k < nsub; k++)
+                if ((rc = encode_sub_async(p, (uint32_t)k))) return rc;
+            if ((rc = read_ctl(p, ctl))) return rc;
+        }
+        first = false;
         fresh = true;
         if (!ctl[CTL_ABORT]) break;
         fresh = false;
@@ -1204,6 +1357,7 @@ extern "C" int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, ui
     p->stats.n_extract = ctl[CTL_NEXTRACT];
     p->stats.n_ref = ctl[CTL_NREF];
     p->stats.dense_chunks = ctl[CTL_DENSE];
+    if (!ctl[CTL_ERROR] && p->sub.size() > 1) p->cache->host_count = ctl[CTL_COUNT];
     if (ctl[CTL_ERROR] & ERR_CAPACITY) {
         uint32_t cap = (uint32_t)p->cache->cap;
         hipMemcpyAsync(p->cache->count, &cap, 4, hipMemcpyHostToDevice, s);
@@ -1357,8 +1511,9 @@ extern "C" double xc__scan_ablation(xc_plan *p, const uint8_t *d_in, int mode, i
     xc_ctx *ctx = p->cache->ctx;
     hipSetDevice(ctx->dev);
     p->P.in = d_in;
-    ScanArgs a{p->P, p->P.S, p->P.cache, 0, p->nchunks, (uint32_t)mode, DevSet{}, 0, (const uint2 *)p->P.cache.l2};
-    uint32_t need = (p->nchunks + SCAN_WAVES * SCAN_UNIT - 1) / (SCAN_WAVES * SCAN_UNIT);
+    ScanArgs a{p->P, p->P.S, p->P.cache, 0, p->nchunks, (uint32_t)mode, DevSet{}, 0, (const uint2 *)p->P.cache.l2, 0,
+               p->scan_unit};
+    uint32_t need = (p->nchunks + SCAN_WAVES * p->scan_unit - 1) / (SCAN_WAVES * p->scan_unit);
     uint32_t grid = std::min<uint32_t>(need, (uint32_t)ctx->n_cu);
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
