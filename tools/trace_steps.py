@@ -5,7 +5,7 @@ import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 k = int(sys.argv[2]) if len(sys.argv) > 2 else 2
-idx = [i for i, r in enumerate(rows) if "k_undo_dev" in r["Kernel_Name"]]
+idx = [i for i, r in enumerate(rows) if "k_undo_" in r["Kernel_Name"]]
 i0, i1 = idx[-k - 1], idx[-k]
 t0 = int(rows[i0]["Start_Timestamp"])
 for r in rows[i0:i1 + 1]:

@@ -993,6 +993,15 @@ __global__ __launch_bounds__(64) void k_walk(WalkArgs a)
 // side stream.  (One-wave workgroups made this kernel dispatch-bound.)
 constexpr uint32_t BLK_GROUP = 8;
 
+// Block g (global index; block k of buffer b) with hash h: blocks absent from the cache are the
+// predicted declarations (hit-free data declares exactly these, xcodec_encoder.cc:77-82); they
+// enter the declaration set and the combined level-2 filter before the scan.  Cached blocks are
+// predicted REFs (REF shadows).
+__device__ __forceinline__ void block_predict(const PlanDev &P, uint32_t g, uint32_t b, uint32_t k, uint64_t h);
+
+// predict: also the predictions of these blocks (the run's first sub-batch, hashed in line after
+// the declaration set's clear: one kernel instead of two)
+template <bool PREDICT>
 __global__ __launch_bounds__(256) void k_blockhash(DeclArgs a)
 {
     const PlanDev &P = a.P;
@@ -1003,13 +1012,17 @@ __global__ __launch_bounds__(256) void k_blockhash(DeclArgs a)
     const uint8_t *base = P.in + P.buf_off[b];
     const uint32_t n = min(BLK_GROUP, P.buf_len[b] / XC_SEG - k0);
     const uint64_t h = wave_block_hashes<BLK_GROUP>(base + (size_t)k0 * XC_SEG, n);
-    if (lane_id() < n) P.blk_h[P.blk_base[b] + k0 + lane_id()] = h;
+    const uint32_t l = lane_id();
+    if (l < n) {
+        const uint32_t gi = P.blk_base[b] + k0 + l;
+        P.blk_h[gi] = h;
+        if (PREDICT) block_predict(P, gi, b, k0 + l, h);
+    }
 }
+template __global__ void k_blockhash<false>(DeclArgs);
+template __global__ void k_blockhash<true>(DeclArgs);
 
-// One lane per aligned block of buffers [j0, j1) (P.blk_buf maps a block to its buffer):
-// blocks absent from the cache are the predicted declarations (hit-free data declares exactly
-// these, xcodec_encoder.cc:77-82); they enter the declaration set and the combined level-2
-// filter before the scan.  Cached blocks are predicted REFs (REF shadows).
+// One lane per aligned block of buffers [j0, j1) (P.blk_buf maps a block to its buffer).
 __global__ __launch_bounds__(256) void k_blockpredict(DeclArgs a)
 {
     if (aborted(a.P)) return;
@@ -1017,11 +1030,15 @@ __global__ __launch_bounds__(256) void k_blockpredict(DeclArgs a)
     const uint32_t g = P.blk_base[a.j0] + blockIdx.x * 256u + threadIdx.x;
     if (g >= P.blk_base[a.j1]) return;
     const uint32_t b = P.blk_buf[g], k = g - P.blk_base[b];
+    block_predict(P, g, b, k, P.blk_h[g]);
+}
+
+__device__ __forceinline__ void block_predict(const PlanDev &P, uint32_t g, uint32_t b, uint32_t k, uint64_t h)
+{
     if (stream_carried(P, b)) {  // blocks relative to a carried source_: no predictions
         P.blk_pref[g] = 0u;
         return;
     }
-    const uint64_t h = P.blk_h[g];
     uint64_t v;
     if (set_find(P.cache, h, &v)) {
         P.blk_pref[g] = (uint32_t)v + 1u;  // (cache capacity <= 2^23)

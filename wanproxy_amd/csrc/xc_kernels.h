@@ -188,7 +188,7 @@ __global__ void k_pack_offsets(PackArgs a);
 __global__ void k_pack_copy(PackArgs a);
 __global__ void k_resolve(ResolveArgs a);
 __global__ void k_walk(WalkArgs a);
-__global__ void k_blockhash(DeclArgs a);
+template <bool PREDICT> __global__ void k_blockhash(DeclArgs a);
 __global__ void k_blockpredict(DeclArgs a);
 __global__ void k_or_words(uint4 *dst, const uint4 *a, const uint4 *b, uint32_t n);
 __global__ void k_alloc(EmitArgs a);

@@ -1139,7 +1139,7 @@ static int launch_emit(xc_plan *p, uint32_t j0, uint32_t jc, uint32_t gate_sb = 
 // stream) has passed; ev_hash[k] marks completion.
 // On the main stream (st == nullptr: the run's first sub-batch, nothing to overlap with) no
 // events are needed.
-static int enqueue_block_hash(xc_plan *p, uint32_t k, hipEvent_t after, hipStream_t st)
+static int enqueue_block_hash(xc_plan *p, uint32_t k, hipEvent_t after, hipStream_t st, bool predict = false)
 {
     const bool side = st == p->hs;
     if (after) HIPCHK(hipStreamWaitEvent(st, after, 0));
@@ -1148,7 +1148,10 @@ static int enqueue_block_hash(xc_plan *p, uint32_t k, hipEvent_t after, hipStrea
     DeclArgs d{p->P, g0, g1};  // a range of block groups
     if (g1 > g0) {
         KSpan span(p, XC_K_BLOCKHASH, st);
-        hipLaunchKernelGGL(k_blockhash, dim3((g1 - g0 + 3) / 4), dim3(256), 0, st, d);
+        if (predict)
+            hipLaunchKernelGGL(k_blockhash<true>, dim3((g1 - g0 + 3) / 4), dim3(256), 0, st, d);
+        else
+            hipLaunchKernelGGL(k_blockhash<false>, dim3((g1 - g0 + 3) / 4), dim3(256), 0, st, d);
         HIPCHK(hipGetLastError());
     }
     if (side) HIPCHK(hipEventRecord(p->ev_hash[k], st));
@@ -1169,14 +1172,16 @@ static int launch_first_round(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t s1,
                        (uint4 *)p->d_l2mix, (const uint4 *)p->P.cache.l2, p->zero_ctl ? p->P.ctl : nullptr);
     HIPCHK(hipGetLastError());
     p->zero_ctl = false;
-    if (p->next_hash <= sb) {
+    const bool inline_hash = p->next_hash <= sb;
+    if (inline_hash) {
         // first sub-batch of the run: nothing to overlap with, its blocks are hashed in line
-        // (after whatever the caller enqueued on the context stream to fill the input)
-        if ((rc = enqueue_block_hash(p, sb, nullptr, s))) return rc;
+        // (after whatever the caller enqueued on the context stream to fill the input), and
+        // predicted by the same kernel
+        if ((rc = enqueue_block_hash(p, sb, nullptr, s, true))) return rc;
     } else {
         HIPCHK(hipStreamWaitEvent(s, p->ev_hash[sb], 0));  // hashed ahead on the side stream
     }
-    {
+    if (!inline_hash || j0 != p->sub[sb]) {
         DeclArgs d{p->P, j0, s1};
         KSpan span(p, XC_K_DECLHASH);
         const uint32_t nblk = p->blk_base[s1] - p->blk_base[j0];
