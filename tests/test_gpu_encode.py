@@ -397,13 +397,13 @@ def test_input_written_on_context_stream(gpu_ctx, oracle_mod):
 
 @pytest.mark.parametrize("no_graph", ["0", "1"])
 def test_graph_replay_and_recapture(gpu_ctx, oracle_mod, monkeypatch, no_graph):
-    """xc_encode_run replays its asynchronous pass as a HIP graph captured on the first run with
-    the given arenas; a run with other arenas captures again, and a sub-batch the gate hands back
-    to the host (cross-buffer duplicates, self references) still takes the step-by-step path after
-    the graph.  Every run equals the oracle; XC_NO_GRAPH=1 (direct enqueue) gives the same bytes."""
+    """xc_encode_run replays the asynchronous pass of a single-sub-batch plan as a HIP graph
+    captured on the first run with the given arenas; a run with other arenas captures again, and a
+    sub-batch the gate hands back to the host (cross-buffer duplicates, self references) still
+    takes the step-by-step path after the graph.  Every run equals the oracle; XC_NO_GRAPH=1 (direct enqueue) gives the same bytes."""
     import torch
     import wanproxy_amd as w
-    monkeypatch.setenv("XC_SUB_MB", "1")
+    monkeypatch.setenv("XC_SUB_MB", "64")  # one sub-batch: the graph path
     monkeypatch.setenv("XC_NO_GRAPH", no_graph)
     bufs, warm = _mixed_batch()
     oc = oracle_mod.Cache()

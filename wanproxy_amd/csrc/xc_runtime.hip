@@ -1253,11 +1253,14 @@ static int encode_sub_sync(xc_plan *p, uint32_t sb, uint32_t *ctl)
     return XC_OK;
 }
 
-// The graph path applies to device-resident runs without per-kernel timing events.
+// The graph path applies to device-resident single-sub-batch runs without per-kernel timing
+// events.  (With several sub-batches the graph loses the side stream's block hashing beside the
+// scans: cfg5 A/B on one box, graph 489-507 GiB/s against 515-525 enqueued directly; the host's
+// launches are hidden behind the long kernels there anyway.)
 static bool use_graph(xc_plan *p)
 {
     const char *e = getenv("XC_NO_GRAPH");
-    return !(e && atoi(e)) && !p->g_off && !p->timing && !p->host_path && p->sub.size() > 1;
+    return !(e && atoi(e)) && !p->g_off && !p->timing && !p->host_path && p->sub.size() == 2;
 }
 
 // The first asynchronous pass of a run (the ctl words were cleared before it) as a graph launch,
