@@ -50,9 +50,13 @@ void *xc_ctx_stream(xc_ctx *ctx);
 int xc_ctx_sync(xc_ctx *ctx);
 
 /* XCodecMemoryCache(UUID, size) (xcodec/xcodec_cache.h:169-172), device resident.
- * cap_segments bounds the segments the cache can hold (the reference map is unbounded;
- * exceeding cap fails the batch with XC_ENOSPC instead of evicting). */
+ * cap_segments is the initial capacity.  Like the reference's map, which is unbounded
+ * (xcodec/xcodec_cache.h:164,182-188), the cache grows before any call that could fill it (its
+ * tables are rebuilt into larger arrays; snapshots stay valid), up to 2^25 segments (64 GiB of
+ * segment store) or the device's memory; only past that does a call fail with XC_ENOSPC. */
 int xc_cache_create(xc_ctx *ctx, uint64_t cap_segments, xc_cache **out);
+/* Current capacity in segments (grows on demand). */
+int xc_cache_capacity(xc_cache *c, uint64_t *cap);
 int xc_cache_destroy(xc_cache *c);
 int xc_cache_count(xc_cache *c, uint64_t *n);
 /* Remember the current contents; xc_cache_restore() rolls every later enter() back. */

@@ -39,6 +39,13 @@ class OracleBackend:
     def hash_segment(self, seg):
         return int(self.o.hash_segment(np.frombuffer(seg, np.uint8)))
 
+    # the Batcher's entry points: sequential, as the reference runs them
+    def encode_many(self, calls):
+        return [self.encode(e, d, f) for e, d, f in calls]
+
+    def decode_many(self, store, datas):
+        return [self.decode(store, d) for d in datas]
+
 
 class Wire(P.Filter):
     """A socket: bytes queue up until pump() delivers them."""
@@ -124,3 +131,92 @@ def esc_buffer(n, seed, frac=0.05):
     b = rng.integers(0, 256, n, dtype=np.uint8)
     b[rng.random(n) < frac] = 0xF1
     return b
+
+
+class Proxy:
+    """One WANProxy process's codec side: a local cache (its UUID) shared by every connection's
+    EncodeFilter, a registry holding the peers' caches shared by every DecodeFilter, and an
+    optional Batcher for the codec calls of each event-loop turn."""
+
+    def __init__(self, backend, uuid, warm=None, batched=False, waiting=False):
+        self.registry = P.CacheRegistry(backend)
+        store = backend.new_store()
+        if warm is not None:
+            warm(store)
+        self.cache = self.registry.register(P.CodecCache(store, uuid, 64))
+        self.batcher = P.Batcher(backend) if batched else None
+        self.codec = P.Codec(backend, self.cache, self.registry, self.batcher)
+        self.waiting = waiting
+
+    def end_turn(self):
+        if self.batcher is not None:
+            failed = self.batcher.run()
+            assert not failed, "a deferred consume failed"
+
+
+class Conn:
+    """A connection between two proxies: a pipe each way (EncodeFilter -> wire -> DecodeFilter)."""
+
+    def __init__(self, a: Proxy, b: Proxy):
+        self.a, self.b = a, b
+        self.a_enc = P.EncodeFilter(a.codec, 1 if a.waiting else 0)
+        self.a_dec = P.DecodeFilter(a.codec)
+        self.b_enc = P.EncodeFilter(b.codec, 1 if b.waiting else 0)
+        self.b_dec = P.DecodeFilter(b.codec)
+        self.ab, self.ba = Wire(), Wire()
+        self.a_sink, self.b_sink = P.Sink(), P.Sink()
+        self.a_enc.chain(self.ab)
+        self.b_enc.chain(self.ba)
+        self.a_dec.chain(self.a_sink)
+        self.b_dec.chain(self.b_sink)
+        self.a_dec.set_upstream(self.a_enc)
+        self.b_dec.set_upstream(self.b_enc)
+
+
+def pump_turns(a: Proxy, b: Proxy, conns, chunk=None, max_turns=10**6):
+    """Deliver queued wire bytes turn by turn: in a turn every connection's queued bytes (as they
+    stood when the turn began, at most ``chunk`` per wire) reach the other side's DecodeFilter,
+    then both proxies end the turn (the batchers run).  Until every wire is idle."""
+    for _ in range(max_turns):
+        work = []
+        for c in conns:
+            for w, dec in ((c.ab, c.b_dec), (c.ba, c.a_dec)):
+                if w.q:
+                    n = len(w.q) if chunk is None else min(chunk, len(w.q))
+                    work.append((dec, bytes(w.q[:n])))
+                    del w.q[:n]
+        if not work:
+            return
+        for dec, data in work:
+            assert dec.consume(data), "decode filter failed"
+        a.end_turn()
+        b.end_turn()
+    raise AssertionError("pipes did not settle")
+
+
+def run_connections(backend, warm_a, inputs, batched, chunk=None, order_seed=5, waiting=False):
+    """Proxies A (warm cache) and B; connection i sends inputs[i][0], inputs[i][1], ... from A,
+    one consume per connection per turn in a seeded shuffled order, pumping between turns; then
+    EOS both ways.  Returns (a, b, conns)."""
+    a = Proxy(backend, UUID_A, warm=warm_a, batched=batched, waiting=waiting)
+    b = Proxy(backend, UUID_B, batched=batched)
+    conns = [Conn(a, b) for _ in inputs]
+    rng = np.random.default_rng(order_seed)
+    turns = max(len(x) for x in inputs)
+    for t in range(turns):
+        for i in rng.permutation(len(conns)):
+            if t < len(inputs[i]):
+                assert conns[i].a_enc.consume(inputs[i][t].tobytes())
+        a.end_turn()
+        b.end_turn()
+        if waiting:
+            for c in conns:
+                c.a_enc.on_read_timeout()
+        pump_turns(a, b, conns, chunk)
+    for c in conns:
+        c.a_enc.flush(0)
+    pump_turns(a, b, conns, chunk)
+    for c in conns:
+        c.b_enc.flush(0)
+    pump_turns(a, b, conns, chunk)
+    return a, b, conns

@@ -436,3 +436,38 @@ def test_graph_replay_and_recapture(gpu_ctx, oracle_mod, monkeypatch, no_graph):
         st = plan.stats()
         stats.append((st.sub_batches, st.redone, st.n_extract, st.n_ref))
     assert len(set(stats)) == 1 and stats[0][1] > 0, stats  # same pass every run, some redone
+
+
+def test_cache_grows_like_the_reference_map(gpu_ctx, oracle_mod):
+    """The reference's memory cache never fills (xcodec/xcodec_cache.h:164,182-188).  A device
+    cache created for 1024 segments takes ten times that through several batches, a snapshot taken
+    before it grew still restores, and every output equals the oracle's."""
+    import wanproxy_amd as w
+    cache = w.XCodecCache(gpu_ctx, 1024)
+    oc = oracle_mod.Cache()
+    enc = w.XCodecEncoder(cache)
+    first = W.random_buffers(16, seed0=0x9000)           # 512 segments
+    assert enc.encode_batch(first) == oc.encode_batch(first)
+    cache.snapshot()
+    snap_oracle = oc.clone()
+    for k in range(4):                                     # 4 x 2560 = 10240 more segments
+        bufs = W.random_buffers(80, seed0=0xA000 + 100 * k)
+        assert enc.encode_batch(bufs) == oc.encode_batch(bufs), k
+    assert len(cache) == len(oc) == 512 + 10240
+    assert cache.capacity >= len(cache) > 1024
+    # the pre-growth snapshot: the grown cache returns to it exactly
+    cache.restore()
+    assert len(cache) == 512
+    again = W.random_buffers(8, seed0=0xA000) + first[:4]
+    assert enc.encode_batch(again) == snap_oracle.encode_batch(again)
+    # enter() and the decoder grow a cache too
+    small = w.XCodecCache(gpu_ctx, 4)
+    for i in range(12):
+        seg = W.gen(700 + i, 2048)
+        small.enter(oracle_mod.hash_segment(seg), seg)
+    assert len(small) == 12 and small.lookup(oracle_mod.hash_segment(W.gen(705, 2048))) == W.gen(705, 2048).tobytes()
+    streams = oracle_mod.Cache().encode_batch(W.random_buffers(40, seed0=0xB000))
+    dc = w.XCodecCache(gpu_ctx, 16)
+    got = w.XCodecDecoder(dc).decode_batch(streams)
+    want = oracle_mod.Cache().decode_batch(streams)
+    assert got == want and len(dc) == 40 * 32

@@ -1,0 +1,42 @@
+"""Multi-process GPU rehearsal of bench.py's N-GPU path on one MI355X.
+
+bench.py --gpus N runs one process per GPU (torch.distributed.run), shards buffer i to rank i mod N
+with a cache per rank and no data-path collective, and reduces only timings and
+counts over gloo.  Here N ranks share the box's one GPU (bench.py maps local rank r to device
+r mod device_count): every rank's shard of the full cfg5 job is encoded by the HIP path and checked
+buffer by buffer against the oracle's independent run of that shard (the committed digests of
+tests/golden/fullsize_digests.npz), and rank 0 prints the job's line."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_sharded_ranks_on_one_gpu(world):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--steps", "2", "--warmup", "1", "--no-cpu"]
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = [x for x in out.stdout.splitlines() if x.startswith("{")][-1]
+    r = json.loads(line)
+    assert r["n_gpus"] == world and r["config"]["buffers_per_gpu"] == 32768 // world
+    assert r["verified_buffers"] == 32768, r["verified_against"]
+    assert "cfg5_g%d" % world in r["verified_against"]
+    assert r["roofline"]["peak"] == 8000.0 * world and r["value"] > 0

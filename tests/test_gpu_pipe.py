@@ -75,3 +75,20 @@ def test_hash_segments_host(gpu_ctx, oracle_mod):
     want = [oracle_mod.hash_segment(segs[i:i + 2048]) for i in range(0, segs.size, 2048)]
     assert [int(x) for x in got] == [int(x) for x in want]
     assert X.hash_segments_host(gpu_ctx, np.zeros(0, np.uint8)).size == 0
+
+
+def test_batched_device_pipes_64_connections(gpu_ctx, oracle_mod):
+    """64 interleaved connections between two proxies, each proxy's codec calls batched per
+    event-loop turn (wanproxy_amd.pipe.Batcher: one xc_encode_streams call for every EncodeFilter
+    consume of the turn, one device decode call per peer cache): every wire byte in both
+    directions and every decoded byte equal the unbatched filters over the oracle."""
+    from pipe_harness import run_connections
+    from test_pipe import _conn_inputs
+    inputs = _conn_inputs(64, 3, seed=0x2718)
+    da, db, dc = run_connections(P.DeviceBackend(gpu_ctx, 1 << 14), _warm_device, inputs, batched=True)
+    oa, ob, oc = run_connections(OracleBackend(oracle_mod), _warm_oracle, inputs, batched=False)
+    for i, (d, o) in enumerate(zip(dc, oc)):
+        assert bytes(d.b_sink.data) == b"".join(x.tobytes() for x in inputs[i]), i
+        assert bytes(d.ab.log) == bytes(o.ab.log), i
+        assert bytes(d.ba.log) == bytes(o.ba.log), i
+    assert da.batcher.device_calls <= 16  # 3 encode turns + a few decode turns, not 192 calls

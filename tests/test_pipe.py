@@ -10,7 +10,7 @@ import pytest
 from wanproxy_amd import pipe as P
 from wanproxy_amd import workloads as W
 
-from pipe_harness import UUID_A, UUID_B, OracleBackend, Side, esc_buffer, parse, pump
+from pipe_harness import UUID_A, UUID_B, OracleBackend, Side, esc_buffer, parse, pump, run_connections
 
 POOL_SEGS = 256  # a small pool keeps the CPU cases fast
 
@@ -153,3 +153,47 @@ def test_encoder_needs_a_valid_uuid(oracle_mod):
     e.chain(P.Sink())
     assert not e.consume(b"abc")
     assert not P.DecodeFilter(P.Codec(be, None, reg)).consume(b"\xfc")  # no upstream
+
+
+def _conn_inputs(n_conn, turns, seed=0x3141):
+    """Per connection, per turn: 64 KiB buffers with repeats of a small pool, of other
+    connections' earlier buffers (cross-connection duplicates) and F1-heavy literals."""
+    p = W.pool(POOL_SEGS)
+    rng = np.random.default_rng(seed)
+    shared = [W.gen(1000 + k, 8192) for k in range(8)]
+    out = []
+    for i in range(n_conn):
+        row = []
+        for t in range(turns):
+            kind = (i + t) % 4
+            if kind == 0:
+                b = W.repeat_buffers(1, 0x500 + 31 * i + t, np_segments=POOL_SEGS, pool_bytes=p)[0]
+            elif kind == 1:
+                b = np.concatenate([shared[(i * 3 + t) % 8], esc_buffer(3000 + i, i * 7 + t), shared[t % 8]])
+            elif kind == 2:
+                b = W.gen(2000 + 97 * i + t, 20000 + int(rng.integers(0, 30000)))
+            else:
+                b = np.concatenate([p[2048 * (i % 50):2048 * (i % 50) + 6000], esc_buffer(900, t)])
+            row.append(b)
+        out.append(row)
+    return out
+
+
+@pytest.mark.parametrize("chunk", [None, 5000])
+def test_batched_turns_equal_sequential_calls(oracle_mod, chunk):
+    """The Batcher (one codec call per kind and cache per event-loop turn) gives exactly the wire
+    bytes of the unbatched filters called one by one in the same order (oracle backend)."""
+    be = OracleBackend(oracle_mod)
+    inputs = _conn_inputs(12, 3)
+    warm = _pool_warm(oracle_mod)
+    sa, sb, sc = run_connections(be, warm, inputs, batched=False, chunk=chunk)
+    ba, bb, bc = run_connections(be, warm, inputs, batched=True, chunk=chunk)
+    asked = False
+    for i, (s, b) in enumerate(zip(sc, bc)):
+        assert bytes(b.b_sink.data) == b"".join(x.tobytes() for x in inputs[i])
+        assert bytes(b.ab.log) == bytes(s.ab.log), i
+        assert bytes(b.ba.log) == bytes(s.ba.log), i
+        asked = asked or b"\xfd" in bytes(b.ba.log)
+        assert b.a_enc.eos_ack and b.b_enc.eos_ack
+    assert asked  # the peer cache started empty: <ASK>/<LEARN> ran, through the sync path
+    assert ba.batcher.device_calls < sum(len(r) for r in inputs)

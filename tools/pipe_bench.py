@@ -1,0 +1,63 @@
+"""Filter-path throughput: N connections of one proxy, each EncodeFilter
+consuming one 64 KiB socket read per event-loop turn (cfg5 data: 50 % repeats of the warm pool),
+with and without the cross-connection Batcher; then the peer's DecodeFilters decoding those
+pipes per turn.  Prints one JSON line.  usage: python tools/pipe_bench.py [N] [TURNS]"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import numpy as np  # noqa: E402
+
+import wanproxy_amd as w  # noqa: E402
+from wanproxy_amd import pipe as P  # noqa: E402
+from wanproxy_amd import workloads as W  # noqa: E402
+from pipe_harness import UUID_A, UUID_B, Proxy, Conn  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+turns = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+ctx = w.Context(0)
+be = P.DeviceBackend(ctx, 1 << 20)
+warm = W.pool_warmup_buffers()
+data = W.repeat_shard(n * turns, 0x5555).reshape(turns, n, -1)
+
+
+def warm_store(store):
+    w.XCodecEncoder(store).encode_batch(warm)
+
+
+res = {"connections": n, "turns": turns, "read_bytes": W.BUF}
+for batched in (True, False):
+    a = Proxy(be, UUID_A, warm=warm_store, batched=batched)
+    b = Proxy(be, UUID_B, batched=batched)
+    # the peer's copy of A's cache holds the pool too (steady state: no <ASK>/<LEARN>)
+    peer = be.new_store()
+    warm_store(peer)
+    b.registry.register(P.CodecCache(peer, UUID_A, 64))
+    conns = [Conn(a, b) for _ in range(n)]
+    t0 = time.perf_counter()
+    for t in range(turns):
+        for i in range(n):
+            assert conns[i].a_enc.consume(data[t, i].tobytes())
+        a.end_turn()
+    enc_s = time.perf_counter() - t0
+    # the peer decodes every pipe (frames only: one device decode call per turn)
+    t0 = time.perf_counter()
+    for c in conns:
+        q = bytes(c.ab.q)
+        c.ab.q.clear()
+        assert c.b_dec.consume(q)
+    b.end_turn()
+    dec_s = time.perf_counter() - t0
+    ok = all(bytes(c.b_sink.data) == data[:, i].tobytes() for i, c in enumerate(conns))
+    key = "batched" if batched else "unbatched"
+    res[key] = {"encode_GiBs": round(n * turns * W.BUF / enc_s / 2**30, 3),
+                "encode_ms_per_turn": round(enc_s / turns * 1e3, 3),
+                "decode_GiBs": round(n * turns * W.BUF / dec_s / 2**30, 3),
+                "device_calls": a.batcher.device_calls if batched else n * turns, "round_trip_ok": ok}
+    for c in conns:
+        c.a_enc.flush(0)
+print(json.dumps(res))

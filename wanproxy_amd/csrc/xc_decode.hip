@@ -568,6 +568,8 @@ using namespace xc;
 
 // The cache object is defined in xc_runtime.hip; these accessors expose what we need.
 extern "C" void xc__cache_count_unknown(xc_cache *c);
+extern "C" int xc__cache_reserve(xc_cache *c, uint64_t extra);
+extern "C" uint32_t xc__cache_gen(xc_cache *c);
 extern "C" int xc__cache_devset(xc_cache *c, void *devset, uint8_t **segs, uint32_t **count, uint32_t *cap,
                                 uint2 **undo, void **stream, int *dev);
 extern "C" int xc__set_error(int code, const char *msg);
@@ -601,6 +603,7 @@ struct xc_dplan {
     std::vector<void *> owned;
     uint32_t *h_ctl = nullptr;    // pinned copy of the control words (the run's host wait)
     hipEvent_t ev_ctl = nullptr;
+    uint32_t cache_gen = 0;       // the cache arrays D holds (they move when the cache grows)
     template <class T>
     int alloc(T **p, size_t n)
     {
@@ -634,6 +637,7 @@ extern "C" int xc_decode_plan_create(xc_cache *c, const uint64_t *in_len, const 
     int rc = xc__cache_devset(c, &D.cache, &D.segs, &D.seg_count, &cap, &D.undo, &streamv, &p->dev);
     if (rc) { delete p; return rc; }
     p->cache = c;
+    p->cache_gen = xc__cache_gen(c);
     p->s = (hipStream_t)streamv;
     D.seg_cap = cap;
     const uint32_t ns = (uint32_t)nbuf;
@@ -733,6 +737,23 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
     const hipStream_t s = p->s;
     uint32_t ctl[DCTL_WORDS] = {};
     int rounds = 0;
+    // room for every EXTRACT of the batch (>= 2050 input bytes each): the cache grows, never fills
+    int rcr = xc__cache_reserve(p->cache, p->in_total / (XC_SEG + 2) + 1);
+    if (rcr) return rcr;
+    if (p->cache_gen != xc__cache_gen(p->cache)) {  // it grew: its arrays moved
+        void *streamv = nullptr;
+        int dev = 0;
+        DecDev &PD = p->D;
+        if ((rcr = xc__cache_devset(p->cache, &PD.cache, &PD.segs, &PD.seg_count, &PD.seg_cap, &PD.undo, &streamv,
+                                    &dev)))
+            return rcr;
+        D.cache = PD.cache;
+        D.segs = PD.segs;
+        D.seg_count = PD.seg_count;
+        D.seg_cap = PD.seg_cap;
+        D.undo = PD.undo;
+        p->cache_gen = xc__cache_gen(p->cache);
+    }
     xc__cache_count_unknown(p->cache);  // the run enters segments: the host's copy of the count is stale
     DHIP(hipMemsetAsync(D.ctl, 0, DCTL_WORDS * 4, s));
     hipLaunchKernelGGL(k_dtok, dim3(ns), dim3(64), 0, s, D, 1);

@@ -406,7 +406,7 @@ __device__ __forceinline__ uint32_t filt_test(const uint32_t *f, uint32_t lo)
     const uint32_t w = f[filt_word(lo)];
     return (w >> (lo & 31u)) & (w >> ((lo >> 5) & 31u)) & 1u;
 }
-__device__ __forceinline__ uint32_t lo_slot(uint32_t lo, uint32_t mask) { return (lo * 0x9E3779B1u) >> 7 & mask; }
+__device__ __forceinline__ uint32_t lo_slot(uint32_t lo, uint32_t mask) { return (lo * 0x9E3779B1u) >> 5 & mask; }
 __device__ __forceinline__ uint32_t key_slot(uint64_t h, uint32_t mask)
 {
     uint32_t lo = (uint32_t)h, hi = (uint32_t)(h >> 32);

@@ -1433,7 +1433,7 @@ __global__ void k_undo(DevSet cache, const uint2 *undo, uint32_t from, uint32_t 
 {
     for (uint32_t i = from + blockIdx.x * blockDim.x + threadIdx.x; i < to; i += gridDim.x * blockDim.x) {
         const uint2 u = undo[i];
-        cache.keys[u.x] = XC_EMPTY64;
+        if (u.x != NONE) cache.keys[u.x] = XC_EMPTY64;
         if (u.y != NONE) cache.lo_keys[u.y] = 0u;
     }
 }
@@ -1448,7 +1448,7 @@ __global__ void k_undo_dev(DevSet cache, const uint2 *undo, uint32_t from, const
     const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
     for (uint32_t i = from + i0; i < to; i += stride) {
         const uint2 u = undo[i];
-        cache.keys[u.x] = XC_EMPTY64;
+        if (u.x != NONE) cache.keys[u.x] = XC_EMPTY64;
         if (u.y != NONE) cache.lo_keys[u.y] = 0u;
     }
     for (uint32_t i = i0; i < XC_FILT_WORDS / 4; i += stride) ((uint4 *)cache.filt)[i] = snap_filt[i];
@@ -1464,7 +1464,7 @@ __global__ void k_undo_known(DevSet cache, const uint2 *undo, uint32_t from, uin
     const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
     for (uint32_t i = from + i0; i < to; i += stride) {
         const uint2 u = undo[i];
-        cache.keys[u.x] = XC_EMPTY64;
+        if (u.x != NONE) cache.keys[u.x] = XC_EMPTY64;
         if (u.y != NONE) cache.lo_keys[u.y] = 0u;
     }
     for (uint32_t i = i0; i < XC_FILT_WORDS / 4; i += stride) ((uint4 *)cache.filt)[i] = snap_filt[i];
@@ -1472,6 +1472,46 @@ __global__ void k_undo_known(DevSet cache, const uint2 *undo, uint32_t from, uin
     if (i0 == 0) {
         *cache.lo_zero = *snap_lo_zero;
         *count = from;
+    }
+}
+
+// Cache growth (xc_runtime.hip cache_grow): every entry of the old full table into the larger
+// tables of `to`, its slots into the undo log at its segment index (the restore's record).  A lo32
+// key shared by several entries belongs, in the undo log, to the oldest (smallest index) entry, as
+// when they were entered in index order: lo_owner[slot] = that index (k_rehash_owner applies it).
+// The filters depend on the keys only and are copied as they are.
+__global__ void k_rehash(DevSet from, DevSet to, uint2 *undo, uint32_t *lo_owner)
+{
+    const uint32_t n = from.mask + 1u;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint64_t h = from.keys[i];
+        if (h == XC_EMPTY64) continue;
+        const uint32_t v = (uint32_t)from.vals[i];
+        uint32_t j = key_slot(h, to.mask);
+        while (atomicCAS((unsigned long long *)&to.keys[j], (unsigned long long)XC_EMPTY64, (unsigned long long)h) !=
+               XC_EMPTY64)
+            j = (j + 1u) & to.mask;  // (keys are unique: every other key found here is another's)
+        to.vals[j] = v;
+        const uint32_t lo = (uint32_t)h;
+        uint32_t ls = NONE;
+        if (lo != 0u) {
+            ls = lo_slot(lo, to.lo_mask);
+            for (;;) {
+                const uint32_t prev = atomicCAS(&to.lo_keys[ls], 0u, lo);
+                if (prev == 0u || prev == lo) break;
+                ls = (ls + 1u) & to.lo_mask;
+            }
+            atomicMin(&lo_owner[ls], v);
+        }
+        undo[v] = make_uint2(j, ls);
+    }
+}
+
+__global__ void k_rehash_owner(uint2 *undo, uint32_t n, const uint32_t *lo_owner)
+{
+    for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += gridDim.x * blockDim.x) {
+        const uint2 u = undo[v];
+        if (u.y != NONE && lo_owner[u.y] != v) undo[v].y = NONE;
     }
 }
 

@@ -201,6 +201,8 @@ __global__ void k_undo_dev(DevSet cache, const uint2 *undo, uint32_t from, const
                            const uint4 *snap_filt, const uint4 *snap_l2, const uint32_t *snap_lo_zero);
 __global__ void k_undo_known(DevSet cache, const uint2 *undo, uint32_t from, uint32_t to, uint32_t *count,
                              const uint4 *snap_filt, const uint4 *snap_l2, const uint32_t *snap_lo_zero);
+__global__ void k_rehash(DevSet from, DevSet to, uint2 *undo, uint32_t *lo_owner);
+__global__ void k_rehash_owner(uint2 *undo, uint32_t n, const uint32_t *lo_owner);
 __global__ void k_enter_one(PlanDev P, uint64_t h, const uint8_t *seg);
 __global__ void k_lookup_one(PlanDev P, uint64_t h, uint8_t *out, uint32_t *found);
 __global__ void k_selftest(uint32_t *err);

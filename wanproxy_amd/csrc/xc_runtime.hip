@@ -230,7 +230,8 @@ struct HostSet {
     {
         n_full = pow2_at_least(entries * 2, 1024);
         n_lo = pow2_at_least(entries * 4, 1024);
-        if (n_full > (1u << 27) || n_lo > (1u << 25)) return fail(XC_EINVAL, "set too large");
+        // (slot hashes use 27 bits: lo_slot / key_slot in xc_device.h)
+        if (n_full > (1u << 27) || n_lo > (1u << 27)) return fail(XC_EINVAL, "set too large");
         HIPCHK(dmalloc(&d.filt, XC_FILT_WORDS * 4));
         HIPCHK(dmalloc(&d.l2, (size_t)XC_L2_WORDS * 8));
         HIPCHK(dmalloc(&d.lo_keys, (size_t)n_lo * 4));
@@ -282,7 +283,13 @@ struct xc_cache {
     // the device's segment count as the host last learned it (a run's control words), or -1:
     // lets a restore write the count itself instead of copying it on the device
     int64_t host_count = -1;
+    uint32_t gen = 0;  // bumped when the cache grows (its arrays move): plans refresh their copies
 };
+
+// The reference's memory cache is unbounded (xcodec/xcodec_cache.h:164,182-188).  The device cache
+// starts at the capacity it was created with and grows (cache_reserve) before any run that could
+// exceed it, up to CAP_MAX segments (64 GiB of segment store) or device memory.
+static const uint64_t CAP_MAX = 1ull << 25;
 
 extern "C" void xc__cache_count_unknown(xc_cache *c)
 {
@@ -303,7 +310,7 @@ static PlanDev cache_plandev(xc_cache *c)
 
 extern "C" int xc_cache_create(xc_ctx *ctx, uint64_t cap, xc_cache **out)
 {
-    if (!ctx || !out || cap == 0 || cap > (1ull << 23)) return fail(XC_EINVAL, "bad cache capacity");
+    if (!ctx || !out || cap == 0 || cap > CAP_MAX) return fail(XC_EINVAL, "bad cache capacity");
     int rc = set_dev(ctx);
     if (rc) return rc;
     xc_cache *c = new xc_cache();
@@ -348,6 +355,89 @@ static int cache_count_host(xc_cache *c, uint32_t *n)
 {
     HIPCHK(hipMemcpyAsync(n, c->count, 4, hipMemcpyDeviceToHost, c->ctx->stream));
     HIPCHK(hipStreamSynchronize(c->ctx->stream));
+    return XC_OK;
+}
+
+// Move the cache into arrays for `need` segments (or twice the capacity): the segment store and
+// the undo log are copied, the tables rebuilt by k_rehash (slots move; the filters depend on the
+// keys only and are copied).  Snapshots stay valid: the rebuilt undo log records the new slots.
+static int cache_grow(xc_cache *c, uint64_t need)
+{
+    if (need > CAP_MAX) return fail(XC_ENOSPC, "device cache capacity exhausted (2^25 segments)");
+    const uint64_t ncap = std::min<uint64_t>(CAP_MAX, std::max<uint64_t>(need + need / 4, 2 * c->cap));
+    hipStream_t s = c->ctx->stream;
+    HIPCHK(hipDeviceSynchronize());  // (plans' side streams too: nothing may use the old arrays)
+    uint32_t count = 0;
+    int rc = cache_count_host(c, &count);
+    if (rc) return rc;
+    count = std::min<uint32_t>(count, (uint32_t)c->cap);
+    HostSet ns;
+    uint8_t *segs = nullptr;
+    uint2 *undo = nullptr;
+    uint32_t *owner = nullptr;
+    if ((rc = ns.alloc(ncap))) return rc;
+    if (dmalloc(&segs, (size_t)ncap * XC_SEG + 4096) != hipSuccess || dmalloc(&undo, (size_t)ncap * sizeof(uint2)) ||
+        dmalloc(&owner, (size_t)ns.n_lo * 4) != hipSuccess) {
+        ns.release();
+        dfree(segs);
+        dfree(undo);
+        return fail(XC_ENOSPC, "device cache capacity exhausted (device memory)");
+    }
+    HIPCHK(hipMemcpyAsync(ns.d.filt, c->set.d.filt, XC_FILT_WORDS * 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(ns.d.l2, c->set.d.l2, (size_t)XC_L2_WORDS * 8, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(ns.d.lo_zero, c->set.d.lo_zero, 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemsetAsync(ns.d.lo_keys, 0, (size_t)ns.n_lo * 4, s));
+    HIPCHK(hipMemsetAsync(ns.d.keys, 0xFF, (size_t)ns.n_full * 8, s));
+    HIPCHK(hipMemsetAsync(ns.d.vals, 0xFF, (size_t)ns.n_full * 8, s));
+    HIPCHK(hipMemsetAsync(undo, 0xFF, (size_t)ncap * sizeof(uint2), s));
+    HIPCHK(hipMemsetAsync(owner, 0xFF, (size_t)ns.n_lo * 4, s));
+    if (count) HIPCHK(hipMemcpyAsync(segs, c->segs, (size_t)count * XC_SEG, hipMemcpyDeviceToDevice, s));
+    const uint32_t blocks = std::min<uint32_t>((c->set.n_full + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_rehash, dim3(blocks), dim3(256), 0, s, c->set.d, ns.d, undo, owner);
+    HIPCHK(hipGetLastError());
+    if (count) {
+        hipLaunchKernelGGL(k_rehash_owner, dim3(std::min<uint32_t>((count + 255) / 256, 8192)), dim3(256), 0, s,
+                           undo, count, (const uint32_t *)owner);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    c->set.release();
+    dfree(c->segs);
+    dfree(c->undo);
+    dfree(owner);
+    c->set = ns;
+    c->segs = segs;
+    c->undo = undo;
+    c->cap = ncap;
+    c->host_count = count;
+    c->gen++;
+    return XC_OK;
+}
+
+// Room for `extra` more segments: grow first when the count could pass the capacity.
+static int cache_reserve(xc_cache *c, uint64_t extra)
+{
+    if (c->host_count < 0) {
+        uint32_t v = 0;
+        int rc = cache_count_host(c, &v);
+        if (rc) return rc;
+        c->host_count = v;
+    }
+    if ((uint64_t)c->host_count + extra <= c->cap) return XC_OK;
+    return cache_grow(c, (uint64_t)c->host_count + extra);
+}
+
+extern "C" int xc__cache_reserve(xc_cache *c, uint64_t extra)
+{
+    int rc = set_dev(c->ctx);
+    return rc ? rc : cache_reserve(c, extra);
+}
+extern "C" uint32_t xc__cache_gen(xc_cache *c) { return c->gen; }
+
+extern "C" int xc_cache_capacity(xc_cache *c, uint64_t *cap)
+{
+    if (!c || !cap) return fail(XC_EINVAL, "null");
+    *cap = c->cap;
     return XC_OK;
 }
 
@@ -466,6 +556,7 @@ extern "C" int xc_cache_enter(xc_cache *c, uint64_t h, const uint8_t *seg)
     int rc = set_dev(c->ctx);
     if (rc) return rc;
     hipStream_t s = c->ctx->stream;
+    if ((rc = cache_reserve(c, 1))) return rc;
     c->host_count = -1;
     HIPCHK(hipMemcpyAsync(c->ctx->d_seg, seg, XC_SEG, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemsetAsync(c->ctl, 0, CTL_WORDS * 4, s));
@@ -628,6 +719,8 @@ struct xc_plan {
     xc_run_stats g_stats{};          // host-side counters of the captured pass
     bool g_off = false;              // capture failed (or XC_NO_GRAPH): enqueue directly
     bool zero_ctl = false;           // the next k_clear_set also clears the run's control words
+    uint32_t cache_gen = 0;          // the cache arrays P holds (xc_cache::gen)
+    uint64_t max_new = 0;            // most segments a run can enter (sum of len / 2048 + 1)
 };
 
 static hipEvent_t ev_get(xc_plan *p)
@@ -804,6 +897,8 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
 
     PlanDev &P = p->P;
     P = cache_plandev(c);
+    p->cache_gen = c->gen;
+    for (uint64_t i = 0; i < nbuf; i++) p->max_new += lengths[i] / XC_SEG + 1;
     P.buf_off = p->d_buf_off;
     P.buf_len = p->d_buf_len;
     P.nb = (uint32_t)nbuf;
@@ -1322,6 +1417,22 @@ extern "C" int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, ui
     int rc = set_dev(p->cache->ctx);
     if (rc) return rc;
     hipStream_t s = p->cache->ctx->stream;
+    // room for every segment this run can declare (the reference's cache never fills)
+    xc_cache *c = p->cache;
+    if ((rc = cache_reserve(c, p->max_new))) return rc;
+    if (p->cache_gen != c->gen) {  // the cache grew: its arrays moved
+        const PlanDev cp = cache_plandev(c);
+        p->P.cache = cp.cache;
+        p->P.segs = cp.segs;
+        p->P.seg_count = cp.seg_count;
+        p->P.seg_cap = cp.seg_cap;
+        p->P.undo = cp.undo;
+        p->cache_gen = c->gen;
+        if (p->gexec) {
+            HIPCHK(hipGraphExecDestroy(p->gexec));
+            p->gexec = nullptr;
+        }
+    }
     p->P.in = d_in;
     p->P.out = d_out;
     p->P.out_len = d_out_len;

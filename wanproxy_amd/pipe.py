@@ -18,6 +18,15 @@ The codec is the device library (``wanproxy_amd.xcodec``) through :class:`Device
 filters hold no codec logic of their own.  There is no CPU fallback: a backend is always given
 explicitly (the CPU tests pass their CPU restatement of the codec, to check the framing state
 machine).
+
+Cross-connection batching: the reference calls the codec once per ``consume``
+on its one event thread (``event/event_system.cc:45-56``), one connection at a time.  A
+:class:`Batcher` attached to the :class:`Codec` defers the codec calls of one event-loop turn:
+every ``EncodeFilter.consume`` becomes one call of a single device batch (``xc_encode_streams``),
+every frames-only ``DecodeFilter.consume`` one stream of a device decode batch per cache, and the
+framing and ``produce`` of each deferred consume then run in call order.  The device batches keep
+the reference's single-thread order exactly (one cache shared by the calls in call order), so the
+wire bytes are those of the unbatched filters.
 """
 from __future__ import annotations
 
@@ -107,6 +116,15 @@ class DeviceBackend:
         st, out, consumed, unknown = self._x.XCodecDecoder(store).decode_batch([data])[0]
         return bool(st), out, consumed, unknown
 
+    def encode_many(self, calls) -> list[bytes]:
+        """One device call for ``(encoder, data, flush)`` calls in order (xc_encode_streams)."""
+        return self._x.encode_streams(calls)
+
+    def decode_many(self, store, datas) -> list[tuple[bool, bytes, int, int | None]]:
+        """One device call: XCodecDecoder::decode of each input in order, one cache."""
+        res = self._x.XCodecDecoder(store).decode_batch(list(datas))
+        return [(bool(st), out, consumed, unknown) for st, out, consumed, unknown in res]
+
     def hash_segment(self, seg: bytes) -> int:
         return int(self._x.hash_segments_host(self.ctx, seg)[0])
 
@@ -157,12 +175,80 @@ class CacheRegistry:
 
 class Codec:
     """``WANProxyCodec`` (``proxy/wanproxy_codec.h:43-71``): the local cache (``xcache_``), the
-    backend that makes caches and codecs, and the registry peer caches are found in."""
+    backend that makes caches and codecs, and the registry peer caches are found in; ``batcher``
+    (optional) defers the filters' codec calls to the end of the event-loop turn."""
 
-    def __init__(self, backend, cache: CodecCache | None, registry: CacheRegistry):
+    def __init__(self, backend, cache: CodecCache | None, registry: CacheRegistry,
+                 batcher: "Batcher | None" = None):
         self.backend = backend
         self.cache = cache
         self.registry = registry
+        self.batcher = batcher
+
+
+class Batcher:
+    """The codec calls of one event-loop turn, for every connection, as few device calls.
+
+    Filters submit jobs in call order: an encode job is ``(encoder, data, flush)`` plus a
+    completion that frames and produces the output; a decode job is a DecodeFilter whose frame
+    buffer is decoded when the job runs.  :meth:`run` (end of the turn; also whenever a filter
+    needs every earlier call finished) cuts the job list into rounds, each the longest prefix of the
+    remaining jobs in which no filter repeats and no cache is both encoded and decoded, and runs a
+    round as one ``backend.encode_many`` call plus one ``backend.decode_many`` call per decoder
+    cache, then the completions in call order.  Calls in a round share their caches exactly as the
+    reference's sequential calls do (the device batches process their items in order against one
+    cache), and every call of a round precedes every call of the next in call order, so the
+    results are the unbatched ones.  Returns the filters whose deferred consume failed."""
+
+    def __init__(self, backend):
+        self.backend = backend
+        self.jobs: list = []
+        self.device_calls = 0
+
+    def submit_encode(self, owner, encoder, store, data: bytes, flush: bool, done) -> None:
+        self.jobs.append(("e", owner, store, (encoder, data, flush), done))
+
+    def submit_decode(self, owner, store, done) -> None:
+        self.jobs.append(("d", owner, store, None, done))
+
+    def pending(self, owner) -> bool:
+        return any(j[1] is owner for j in self.jobs)
+
+    def run(self) -> list:
+        failed = []
+        while self.jobs:
+            rnd, owners, enc_stores, dec_stores = [], set(), set(), set()
+            for j in self.jobs:
+                kind, owner, store = j[0], j[1], j[2]
+                if id(owner) in owners:
+                    break
+                if (kind == "e" and id(store) in dec_stores) or (kind == "d" and id(store) in enc_stores):
+                    break
+                owners.add(id(owner))
+                (enc_stores if kind == "e" else dec_stores).add(id(store))
+                rnd.append(j)
+            del self.jobs[:len(rnd)]
+            results = [None] * len(rnd)
+            enc = [k for k, j in enumerate(rnd) if j[0] == "e"]
+            if enc:
+                outs = self.backend.encode_many([rnd[k][3] for k in enc])
+                self.device_calls += 1
+                for k, o in zip(enc, outs):
+                    results[k] = o
+            by_store: dict = {}
+            for k, j in enumerate(rnd):
+                if j[0] == "d":
+                    by_store.setdefault(id(j[2]), []).append(k)
+            for ks in by_store.values():
+                store = rnd[ks[0]][2]
+                outs = self.backend.decode_many(store, [bytes(rnd[k][1].frame_buffer) for k in ks])
+                self.device_calls += 1
+                for k, o in zip(ks, outs):
+                    results[k] = o
+            for j, r in zip(rnd, results):
+                if not j[4](r):
+                    failed.append(j[1])
+        return failed
 
 
 def _frame(src: bytearray, trg: bytearray) -> None:
@@ -173,6 +259,16 @@ def _frame(src: bytearray, trg: bytearray) -> None:
     trg += struct.pack(">H", n)
     trg += src[:n]
     del src[:n]
+
+
+def _frames(enc: bytes, trg: bytearray) -> None:
+    """Every frame of ``enc`` (``encode_frame`` until the encoded bytes are used up)."""
+    mv = memoryview(enc)
+    for o in range(0, len(enc), MAX_FRAME):
+        n = min(len(enc) - o, MAX_FRAME)
+        trg.append(OP_FRAME)
+        trg += struct.pack(">H", n)
+        trg += mv[o:o + n]
 
 
 class EncodeFilter(Filter):
@@ -204,12 +300,23 @@ class EncodeFilter(Filter):
         flush_now = not (flg & TO_BE_CONTINUED) and not self.waiting
         if not (flg & TO_BE_CONTINUED) and self.waiting:
             self.wait_armed = True  # (re)start the timer; on_read_timeout() flushes
-        enc = bytearray(self.codec.backend.encode(self.encoder, bytes(buf), flush_now))
-        while enc:
-            _frame(enc, output)
-        return self.produce(output, flg) if output else True
+
+        def done(enc: bytes) -> bool:
+            _frames(enc, output)
+            return self.produce(output, flg) if output else True
+        b = self.codec.batcher
+        if b is not None:  # deferred to the end of the turn: one device call for every connection
+            b.submit_encode(self, self.encoder, self.cache.store, bytes(buf), flush_now, done)
+            return True
+        return done(self.codec.backend.encode(self.encoder, bytes(buf), flush_now))
+
+    def _drain(self) -> None:
+        # a direct codec call must follow every deferred one (the reference's order)
+        if self.codec is not None and self.codec.batcher is not None:
+            self.codec.batcher.run()
 
     def flush(self, flg: int) -> None:
+        self._drain()
         if flg == OP_EOS_ACK:
             self.eos_ack = True
         else:
@@ -231,6 +338,7 @@ class EncodeFilter(Filter):
         """``EncodeFilter::on_read_timeout`` (``xcodec_filter.cc:205-216``): the waiting-mode
         flush, when the caller's 150 ms timer fires."""
         self.wait_armed = False
+        self._drain()
         if not self.flushing and self.encoder is not None:
             emitted, enc = self.codec.backend.flush(self.encoder)
             if emitted:
@@ -264,11 +372,64 @@ class DecodeFilter(Filter):
     def set_upstream(self, f: Filter) -> None:
         self.upstream = f
 
+    def _frames_only(self, data: bytes) -> bool:
+        """Whether ``data`` (pending bytes) holds only <HELLO> (first) and <FRAME> messages, the
+        last one possibly incomplete: such a consume changes nothing but the frame buffer before
+        its decode, which can then be deferred."""
+        i, n = 0, len(data)
+        while i < n:
+            op = data[i]
+            if op == OP_FRAME:
+                if n - i < 3:
+                    return True
+                i += 3 + struct.unpack(">H", data[i + 1:i + 3])[0]
+            elif op == OP_HELLO and i == 0 and self.decoder_cache is None:
+                if n - i < 2:
+                    return True
+                i += 2 + data[i + 1]
+            else:
+                return False
+        return True
+
+    def _decoded(self, res, flg: int) -> bool:
+        """The part of the frame loop after ``XCodecDecoder::decode`` (xcodec_filter.cc:414-455)."""
+        ok, output, consumed, unknown = res
+        if not ok:
+            return False  # "Decoder exiting with error."
+        del self.frame_buffer[:consumed]
+        if unknown is not None:
+            self.unknown_hashes.add(unknown)
+        if output:
+            assert not self.flushing
+            if not self.produce(output, flg):
+                return False
+        ask = b"".join(bytes([OP_ASK]) + struct.pack(">Q", h) for h in sorted(self.unknown_hashes))
+        if ask and not self.upstream.produce(ask):
+            return False
+        return True
+
     def consume(self, buf: bytes, flg: int = 0) -> bool:
         if self.upstream is None:
             return False  # "Decoder not configured"
-        backend = self.codec.backend
+        b = self.codec.batcher if self.codec is not None else None
+        if b is not None:
+            if (not self.received_eos and not self.unknown_hashes and not b.pending(self)
+                    and self._frames_only(bytes(self.pending) + bytes(buf))):
+                # frames only: parse now, decode at the end of the turn in the device batch (the
+                # frames of one consume decode in one call as they do one by one: the decoder
+                # keeps a token that straddles frames, and stops at the first unknown REF)
+                self.pending += buf
+                if not self._parse(flg, defer=True):
+                    return False
+                if self.frame_buffer and not self.unknown_hashes:
+                    b.submit_decode(self, self.decoder_cache.store, lambda r: self._decoded(r, flg))
+                return True
+            b.run()  # anything else runs now, after every earlier deferred call
         self.pending += buf
+        return self._parse(flg, defer=False)
+
+    def _parse(self, flg: int, defer: bool) -> bool:
+        backend = self.codec.backend
         while self.pending:
             op = self.pending[0]
             if op == OP_HELLO:
@@ -349,18 +510,9 @@ class DecodeFilter(Filter):
                 continue
             if self.unknown_hashes:
                 continue  # waiting for <LEARN>s
-            ok, output, consumed, unknown = backend.decode(self.decoder_cache.store, bytes(self.frame_buffer))
-            if not ok:
-                return False  # "Decoder exiting with error."
-            del self.frame_buffer[:consumed]
-            if unknown is not None:
-                self.unknown_hashes.add(unknown)
-            if output:
-                assert not self.flushing
-                if not self.produce(output, flg):
-                    return False
-            ask = b"".join(bytes([OP_ASK]) + struct.pack(">Q", h) for h in sorted(self.unknown_hashes))
-            if ask and not self.upstream.produce(ask):
+            if defer:
+                continue  # (the batch decodes the frame buffer once every frame is in)
+            if not self._decoded(backend.decode(self.decoder_cache.store, bytes(self.frame_buffer)), flg):
                 return False
 
         if self.received_eos and not self.sent_eos_ack and not self.frame_buffer:
@@ -381,6 +533,8 @@ class DecodeFilter(Filter):
         return True
 
     def flush(self, flg: int) -> None:
+        if self.codec is not None and self.codec.batcher is not None:
+            self.codec.batcher.run()
         self.flushing = True
         self.flush_flags |= flg
         if not self.upflushed and self.upstream is not None:

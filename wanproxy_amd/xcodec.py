@@ -34,7 +34,7 @@ SYMBOLS = [
     "xc_plan_set_streams", "xc_plan_stream_results", "xc_encoder_create", "xc_encoder_destroy",
     "xc_encoder_pending", "xc_encode", "xc_flush", "xc_encode_streams",
     "xc_decode_plan_create", "xc_dplan_destroy", "xc_dplan_layout", "xc_decode_run", "xc_dplan_stats",
-    "xc_hash_segments_host",
+    "xc_hash_segments_host", "xc_cache_capacity",
 ]
 STREAM_FLUSH = 1  # XC_STREAM_FLUSH
 
@@ -96,6 +96,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.xc_cache_create.argtypes = [_vp, C.c_uint64, C.POINTER(_vp)]
     lib.xc_cache_destroy.argtypes = [_vp]
     lib.xc_cache_count.argtypes = [_vp, C.POINTER(C.c_uint64)]
+    lib.xc_cache_capacity.argtypes = [_vp, C.POINTER(C.c_uint64)]
     lib.xc_cache_snapshot.argtypes = [_vp]
     lib.xc_cache_restore.argtypes = [_vp]
     lib.xc_cache_lookup.argtypes = [_vp, C.c_uint64, _u8p, C.POINTER(C.c_int)]
@@ -222,14 +223,13 @@ def _pack(bufs):
 class XCodecCache:
     """XCodecMemoryCache (xcodec/xcodec_cache.h:162-211) held in HBM.
 
-    ``capacity`` bounds the number of 2048-byte segments (the reference map grows without
-    bound; here an overflow raises instead of evicting)."""
+    ``capacity`` is the initial number of 2048-byte segments; like the reference's map, which
+    grows without bound, the cache grows before any call that could fill it (xc_cache_create)."""
 
     def __init__(self, ctx: Context, capacity: int = 1 << 16):
         self.ctx = ctx
         self.h = _vp()
         _check(load_library().xc_cache_create(ctx.h, capacity, C.byref(self.h)))
-        self.capacity = capacity
         _LIVE["cache"].add(self)
 
     def _ctx(self):
@@ -238,6 +238,13 @@ class XCodecCache:
     def __len__(self) -> int:
         n = C.c_uint64()
         _check(load_library().xc_cache_count(self.h, C.byref(n)))
+        return n.value
+
+    @property
+    def capacity(self) -> int:
+        """Segments the cache holds before it grows again (it grows on demand)."""
+        n = C.c_uint64()
+        _check(load_library().xc_cache_capacity(self.h, C.byref(n)))
         return n.value
 
     def lookup(self, h: int) -> bytes | None:
