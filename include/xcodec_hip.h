@@ -176,7 +176,10 @@ int xc_flush(xc_encoder *e, uint8_t *out, uint64_t cap, uint64_t *out_len, int *
 /* Cross-connection batch of calls, in the reference's single-thread order: call k is
  * enc[k]->encode(in[k]) and, with flags[k] & XC_STREAM_FLUSH, enc[k]->flush() (EncodeFilter::consume
  * without TO_BE_CONTINUED, xcodec/xcodec_filter.cc:146-160).  An encoder may appear in several
- * calls.  Call k's output goes to out + out_off[k] (capacity out_cap[k]). */
+ * calls.  Call k's output goes to out + out_off[k] (capacity out_cap[k], at least twice the
+ * encoder's pending bytes plus its inputs up to and including call k, else XC_EINVAL before
+ * anything runs).  After a device error (XC_EDEVICE / XC_ENOMEM / XC_ENOSPC) the encoders and the
+ * cache may hold part of the batch: destroy them. */
 #define XC_STREAM_FLUSH 1
 int xc_encode_streams(xc_encoder *const *enc, const uint8_t *const *in, const uint64_t *in_len,
                       const uint32_t *flags, uint64_t n, uint8_t *out, const uint64_t *out_off,

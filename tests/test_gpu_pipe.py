@@ -92,3 +92,11 @@ def test_batched_device_pipes_64_connections(gpu_ctx, oracle_mod):
         assert bytes(d.ab.log) == bytes(o.ab.log), i
         assert bytes(d.ba.log) == bytes(o.ba.log), i
     assert da.batcher.device_calls <= 16  # 3 encode turns + a few decode turns, not 192 calls
+
+
+def test_device_chain_with_deflate_stage(gpu_ctx, oracle_mod):
+    """The proxy chain with the zlib stage (EncodeFilter -> DeflateFilter -> wire -> InflateFilter
+    -> DecodeFilter, proxy/proxy_connector.cc:146-150,177-189) over the device codec: the compressed
+    wire bytes equal the same chain over the oracle, and the peer gets every byte back."""
+    from test_zlib import chain_round_trip
+    assert chain_round_trip(P.DeviceBackend(gpu_ctx, 1 << 12)) == chain_round_trip(OracleBackend(oracle_mod))

@@ -573,6 +573,7 @@ extern "C" uint32_t xc__cache_gen(xc_cache *c);
 extern "C" int xc__cache_devset(xc_cache *c, void *devset, uint8_t **segs, uint32_t **count, uint32_t *cap,
                                 uint2 **undo, void **stream, int *dev);
 extern "C" int xc__set_error(int code, const char *msg);
+extern "C" hipError_t xc__spin_wait(hipEvent_t ev);
 extern "C" int xc__dalloc(void **p, uint64_t bytes);
 extern "C" int xc__halloc(void **p, uint64_t bytes);
 extern "C" void xc__pfree(void *p);
@@ -793,9 +794,7 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
         }
         DHIP(hipMemcpyAsync(p->h_ctl, D.ctl, DCTL_WORDS * 4, hipMemcpyDeviceToHost, s));
         DHIP(hipEventRecord(p->ev_ctl, s));
-        hipError_t e;
-        while ((e = hipEventQuery(p->ev_ctl)) == hipErrorNotReady) { }
-        DHIP(e);
+        DHIP(xc__spin_wait(p->ev_ctl));  // (polls, yielding the core after ~20 us)
         memcpy(ctl, p->h_ctl, DCTL_WORDS * 4);
         return XC_OK;
     };

@@ -9,7 +9,10 @@ namespace xc {
 constexpr uint32_t EV_CAP = 64;          // sparse events per scan chunk before it turns dense
 constexpr uint32_t EV_DENSE = 0x80000000u;
 constexpr uint32_t Q_CAP = 128;          // per-wave LDS queue of level-1 filter positives
-constexpr uint32_t SCAN_WAVES = 16;      // waves per scan workgroup (one per CU: all of its LDS and VGPRs)
+#ifndef XC_SCAN_WAVES
+#define XC_SCAN_WAVES 16
+#endif
+constexpr uint32_t SCAN_WAVES = XC_SCAN_WAVES;  // waves per scan workgroup (one per CU: all of its LDS)
 constexpr uint32_t CHUNK_BLOCKS = 8;     // most 2048-byte blocks per scan chunk (16 KiB; small plans use fewer)
 constexpr uint32_t SCAN_UNIT = 4;        // most chunks a scan wave takes from the work counter at a time
 constexpr uint32_t EMIT_WAVES = 4;       // k_emit waves per buffer (workgroup)

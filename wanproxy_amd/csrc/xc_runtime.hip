@@ -8,6 +8,8 @@
 // declarations (see DESIGN.md "Sequential semantics").
 #include <hip/hip_runtime.h>
 
+#include <sched.h>
+
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
@@ -1127,6 +1129,17 @@ extern "C" int xc_plan_stream_results(xc_plan *p, uint64_t *base, int64_t *cand)
 
 // The run's one host wait: the control words through a pinned buffer, then a spin on an event
 // (returns within a few us of the copy; a blocking stream synchronize wakes up later).
+// Wait for an event: poll it (a blocking wait wakes up tens of microseconds late), yielding the
+// core to other threads of the process (a proxy's event loop) after the first ~20 us.
+static hipError_t spin_wait(hipEvent_t ev)
+{
+    hipError_t e;
+    for (int i = 0; (e = hipEventQuery(ev)) == hipErrorNotReady; i++)
+        if (i >= 64) sched_yield();
+    return e;
+}
+extern "C" hipError_t xc__spin_wait(hipEvent_t ev) { return spin_wait(ev); }
+
 static int ctl_buffers(xc_plan *p)
 {
     if (!p->h_ctl) {
@@ -1152,9 +1165,7 @@ static int wait_ctl(xc_plan *p, uint32_t *ctl)
 {
     hipStream_t s = p->cache->ctx->stream;
     HIPCHK(hipEventRecord(p->ev_ctl, s));
-    hipError_t e;
-    while ((e = hipEventQuery(p->ev_ctl)) == hipErrorNotReady) { }
-    HIPCHK(e);
+    HIPCHK(spin_wait(p->ev_ctl));
     memcpy(ctl, p->h_ctl, CTL_WORDS * 4);
     ev_collect(p);
     return XC_OK;

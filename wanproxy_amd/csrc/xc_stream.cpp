@@ -78,6 +78,19 @@ static int encode_streams(xc_encoder *const *enc, const uint8_t *const *in, cons
         if (in_len[k] && (!in || !in[k])) return xc__set_error(XC_EINVAL, "null input");
         out_len[k] = 0;
     }
+    // Every output capacity is checked before anything runs, so that an argument error leaves the
+    // encoders and the cache as they were.  A call emits at most 2 bytes per byte it takes from
+    // source_ and its input (escaped F1 literals; EXTRACT 2050 per 2048, REF 10), and source_ at
+    // the call holds at most the encoder's pending bytes plus its earlier inputs of this request.
+    {
+        std::vector<std::pair<const xc_encoder *, uint64_t>> pend;
+        for (uint64_t k = 0; k < n; k++) {
+            auto it = std::find_if(pend.begin(), pend.end(), [&](const auto &x) { return x.first == enc[k]; });
+            if (it == pend.end()) it = pend.insert(pend.end(), {enc[k], enc[k]->source.size()});
+            it->second += in_len[k];
+            if (out_cap[k] < 2 * it->second) return xc__set_error(XC_EINVAL, "output capacity too small");
+        }
+    }
     std::vector<uint64_t> done(n, 0);  // input bytes of call k consumed so far
     uint64_t k0 = 0;
     while (k0 < n) {
