@@ -217,6 +217,40 @@ int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_
                   uint64_t *d_consumed, int32_t *d_status, uint64_t *d_unknown, int32_t *d_has_unknown);
 int xc_dplan_stats(xc_dplan *p, xc_decode_stats *st);
 
+/* ---- persistent COSS cache: XCodecCacheCOSS (xcodec/cache/coss/xcodec_cache_coss.{h,cc}) ----
+ *
+ * XCodecCacheCOSS(uuid, cache_dir, size) (xcodec_cache_coss.cc:31-80): the stripe file
+ * <dir>/<uuid>.wpc (uuid: the 36-character UUID string), size_mb 0 = 1024, read back if valid.
+ * The segments a lookup can find are mirrored in a device cache on ctx; encode and decode batches
+ * run on the device and advance the COSS state (stripes, freshness, use flags, the recent window,
+ * purges, the file) exactly as the reference's codec calls would (wanproxy_amd/csrc/xc_coss.cpp).
+ * ctx NULL: the host store alone (lookup / enter only). */
+typedef struct xc_coss xc_coss;
+int xc_coss_open(xc_ctx *ctx, const char *dir, const char *uuid, uint64_t size_mb, xc_coss **out);
+/* ~XCodecCacheCOSS (:82-105): the loaded stripes are stored. */
+int xc_coss_close(xc_coss *c);
+/* The device mirror (NULL for a host-only store): for device-resident plans on a COSS cache only
+ * while nothing is purged (use the batch calls below to keep the COSS state). */
+xc_cache *xc_coss_cache(xc_coss *c);
+int xc_coss_count(xc_coss *c, uint64_t *n);
+/* {lookups (hits only: misses are not counted here), found in the recent window, found in the
+ * stripes, index size, stripe limit, serial number} (COSSStats, xcodec_cache_coss.h:179-187). */
+int xc_coss_stats(xc_coss *c, uint64_t *out6);
+/* XCodecCacheCOSS::lookup / enter (:188-228, :163-186); the device mirror follows. */
+int xc_coss_lookup(xc_coss *c, uint64_t hash, uint8_t *out, int *found);
+int xc_coss_enter(xc_coss *c, uint64_t hash, const uint8_t *seg);
+/* xc_encode_batch_host / xc_decode_batch_host over the COSS cache. */
+int xc_coss_encode_batch_host(xc_coss *c, const uint8_t *in, const uint64_t *in_off, const uint64_t *in_len,
+                              uint64_t nbuf, uint8_t *out, const uint64_t *out_off, const uint64_t *out_cap,
+                              uint64_t *out_len);
+int xc_coss_decode_batch_host(xc_coss *c, const uint8_t *in, const uint64_t *in_off, const uint64_t *in_len,
+                              uint64_t nbuf, uint8_t *out, const uint64_t *out_off, const uint64_t *out_cap,
+                              uint64_t *out_len, uint64_t *consumed, int32_t *status, uint64_t *unknown,
+                              int32_t *has_unknown);
+/* The host store's own lookup / enter, without the device mirror (tests of the store). */
+int xc_coss_store_lookup(xc_coss *c, uint64_t hash, uint8_t *out, int *found);
+int xc_coss_store_enter(xc_coss *c, uint64_t hash, const uint8_t *seg);
+
 /* Library self-test of the wave primitives on device (returns XC_OK or a negative code). */
 int xc_selftest(xc_ctx *ctx);
 

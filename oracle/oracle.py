@@ -57,6 +57,8 @@ def _load() -> C.CDLL:
     lib.xo_flush.argtypes = [C.c_void_p, C.POINTER(XoBytes)]
     lib.xo_flush.restype = C.c_int
     lib.xo_bytes_free.argtypes = [C.POINTER(XoBytes)]
+    lib.xo_cache_new_coss.restype = C.c_void_p
+    lib.xo_cache_new_coss.argtypes = [C.c_char_p, C.c_char_p, C.c_uint64]
     lib.xo_encode_sharded_timed.restype = C.c_double
     lib.xo_encode_sharded_timed.argtypes = [C.c_void_p, _u8p, _u64p, _u64p, C.c_size_t, C.c_int,
                                             C.POINTER(C.c_uint64)]
@@ -110,6 +112,17 @@ class Cache:
         self.h = handle if handle is not None else lib().xo_cache_new()
 
     def __del__(self):
+        if getattr(self, "h", None):
+            lib().xo_cache_free(self.h)
+            self.h = None
+
+    @classmethod
+    def coss(cls, directory: str, uuid: str, size_mb: int = 0) -> "Cache":
+        """XCodecCacheCOSS (oracle/xc_coss.c) behind the same cache interface; closing it (del)
+        runs the destructor's stores."""
+        return cls(lib().xo_cache_new_coss(directory.encode(), uuid.encode(), size_mb))
+
+    def close(self) -> None:
         if getattr(self, "h", None):
             lib().xo_cache_free(self.h)
             self.h = None

@@ -112,6 +112,7 @@ struct xo_cache {
         size_t slot; /* segment index the pointer refers to (stable across realloc) */
     } window[XO_WINDOW_COUNT];
     unsigned cursor;
+    xo_coss *coss; /* non-null: XCodecCacheCOSS instead of the memory cache */
 };
 
 static size_t slot_of(uint64_t h, size_t mask) { return (size_t)((h * 0x9E3779B97F4A7C15ull) >> 17) & mask; }
@@ -164,9 +165,17 @@ xo_cache *xo_cache_clone(const xo_cache *s)
     return c;
 }
 
+xo_cache *xo_cache_new_coss(const char *dir, const char *uuid, uint64_t size_mb)
+{
+    xo_cache *c = xo_cache_new();
+    c->coss = xo_coss_open(dir, uuid, size_mb);
+    return c;
+}
+
 void xo_cache_free(xo_cache *c)
 {
     if (!c) return;
+    if (c->coss) xo_coss_close(c->coss);
     free(c->keys);
     free(c->idx);
     free(c->seg_hash);
@@ -174,7 +183,7 @@ void xo_cache_free(xo_cache *c)
     free(c);
 }
 
-size_t xo_cache_count(const xo_cache *c) { return c->count; }
+size_t xo_cache_count(const xo_cache *c) { return c->coss ? xo_coss_count(c->coss) : c->count; }
 
 static long cache_find(const xo_cache *c, uint64_t h)
 {
@@ -188,6 +197,7 @@ static long cache_find(const xo_cache *c, uint64_t h)
 
 int xo_cache_lookup(xo_cache *c, uint64_t h, const uint8_t **data)
 { /* xcodec_cache.h:190-210 */
+    if (c->coss) return xo_coss_lookup(c->coss, h, data);
     for (int i = 0; i < XO_WINDOW_COUNT; i++) { /* find_recent, :137-147 */
         if (c->window[i].hash == h && c->window[i].data) {
             *data = c->window[i].data;
@@ -208,6 +218,10 @@ int xo_cache_lookup(xo_cache *c, uint64_t h, const uint8_t **data)
 void xo_cache_enter(xo_cache *c, uint64_t h, const uint8_t *seg)
 { /* xcodec_cache.h:182-188.  A duplicate enter is an assert in the reference; release
    * builds overwrite the map value, which is what we do. */
+    if (c->coss) {
+        xo_coss_enter(c->coss, h, seg);
+        return;
+    }
     long k = cache_find(c, h);
     if (c->count == c->seg_cap) {
         size_t nc = c->seg_cap ? c->seg_cap * 2 : 1024;

@@ -52,6 +52,20 @@ void xo_cache_enter(xo_cache *c, uint64_t h, const uint8_t *seg);
 /* i-th entered (hash, segment) pair, insertion order. */
 int xo_cache_entry(const xo_cache *c, size_t i, uint64_t *h, uint8_t *seg);
 
+/* XCodecCacheCOSS (xcodec/cache/coss/xcodec_cache_coss.{h,cc}): oracle/xc_coss.c.  The file is
+ * <dir>/<uuid>.wpc; size_mb 0 = 1024. */
+typedef struct xo_coss xo_coss;
+xo_coss *xo_coss_open(const char *dir, const char *uuid, uint64_t size_mb);
+void xo_coss_close(xo_coss *c);
+void xo_coss_enter(xo_coss *c, uint64_t h, const uint8_t *seg);
+int xo_coss_lookup(xo_coss *c, uint64_t h, const uint8_t **data);
+size_t xo_coss_count(const xo_coss *c);
+void xo_coss_stats(const xo_coss *c, uint64_t *out);
+size_t xo_coss_hashes(const xo_coss *c, uint64_t *out, size_t cap);
+/* An xo_cache whose lookup / enter are the COSS cache's (the encoder and decoder take it like
+ * the memory cache).  xo_cache_free closes the COSS cache (its destructor's stores). */
+xo_cache *xo_cache_new_coss(const char *dir, const char *uuid, uint64_t size_mb);
+
 /* XCodecEncoder (xcodec/xcodec_encoder.{h,cc}). Output is appended to a growable byte vector. */
 typedef struct {
     uint8_t *data;

@@ -82,6 +82,22 @@ __device__ __forceinline__ void load32_unaligned(const uint8_t *p, uint32_t out[
     for (int k = 0; k < 8; k++) out[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
 }
 
+// The same for a lane's part of a 2048-byte window that may end where its allocation ends: the
+// ninth word only when p is unaligned (it then holds the part's last bytes; an aligned part ends
+// on a word boundary).
+__device__ __forceinline__ void load32_window(const uint8_t *p, uint32_t out[8])
+{
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    uint32_t d[9];
+#pragma unroll
+    for (int k = 0; k < 8; k++) d[k] = w[k];
+    d[8] = sh ? w[8] : 0u;
+#pragma unroll
+    for (int k = 0; k < 8; k++) out[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+}
+
 // Per-lane partial sums of 32 bytes at local offsets 0..31:
 //   A = sum w, B = sum j*w for w = byte+1   (and the same with f = ffs(byte))
 struct Sums4 {
@@ -167,7 +183,7 @@ __device__ __forceinline__ uint64_t wave_hash_regs(const uint32_t w[8])
 __device__ __forceinline__ uint64_t wave_window_hash(const uint8_t *p)
 {
     uint32_t w[8];
-    load32_unaligned(p + 32u * lane_id(), w);
+    load32_window(p + 32u * lane_id(), w);
     return wave_hash_regs(w);
 }
 
@@ -258,8 +274,8 @@ __device__ __forceinline__ bool wave_equal2048(const uint8_t *a, const uint8_t *
 {
     const uint32_t l = lane_id();
     uint32_t x[8], y[8];
-    load32_unaligned(a + 32u * l, x);
-    load32_unaligned(b + 32u * l, y);
+    load32_window(a + 32u * l, x);
+    load32_window(b + 32u * l, y);
     uint32_t diff = 0;
 #pragma unroll
     for (int k = 0; k < 8; k++) diff |= x[k] ^ y[k];
@@ -425,13 +441,25 @@ __device__ __forceinline__ bool set_has_lo(const DevSet &s, uint32_t lo)
     }
 }
 
-// Returns true and *val if present.
+// A cache entry evicted by the COSS tier (xc_coss.cpp) keeps its key with this bit in its value:
+// absent to every lookup, revived by the next insert of the key.
+#define XC_DEAD (1ull << 63)
+// The undo record's lo slot of an insert that revived an evicted key: undoing it evicts the key
+// again (clearing the key would cut the probe chains of keys inserted after it).
+#define XC_REVIVED 0xFFFFFFFEu
+
+// Returns true and *val if present (and not evicted).
 __device__ __forceinline__ bool set_find(const DevSet &s, uint64_t h, uint64_t *val)
 {
     uint32_t i = key_slot(h, s.mask);
     for (;;) {
         uint64_t k = s.keys[i];
-        if (k == h) { *val = s.vals[i]; return true; }
+        if (k == h) {
+            const uint64_t v = s.vals[i];
+            if (v & XC_DEAD) return false;
+            *val = v;
+            return true;
+        }
         if (k == XC_EMPTY64) return false;
         i = (i + 1u) & s.mask;
     }
@@ -462,10 +490,15 @@ __device__ __forceinline__ int set_insert(const DevSet &s, uint64_t h, uint64_t 
         if (prev == h) break;
         i = (i + 1u) & s.mask;
     }
-    if (min_merge) atomicMin((unsigned long long *)&s.vals[i], (unsigned long long)val);
-    else if (fresh) s.vals[i] = val;
+    bool revived = false;
+    if (min_merge) {
+        atomicMin((unsigned long long *)&s.vals[i], (unsigned long long)val);
+    } else if (fresh || (s.vals[i] & XC_DEAD)) {
+        revived = !fresh;  // an evicted key comes back: its undo record restores the eviction
+        s.vals[i] = val;
+    }
     if (slot_out) *slot_out = i;
-    uint32_t los = 0xFFFFFFFFu;
+    uint32_t los = revived ? XC_REVIVED : 0xFFFFFFFFu;
     if (fresh) {
         uint32_t lo = (uint32_t)h;
         if (lo == 0u) atomicOr(s.lo_zero, 1u);

@@ -732,16 +732,26 @@ __device__ __forceinline__ void walk_seq(const WalkArgs &a, uint32_t b, uint64_t
         if (!a.use_d) return s;
         return event_at(P, P.D, cd, ck1, q, 1, b, base);
     };
+    uint32_t n_coll = 0;
+    // a lookup hit with other bytes: record it, with the candidate pending then (NONE: none)
+    auto coll = [&](uint32_t q, uint64_t h) {
+        if (P.coll && n_coll < COLL_CAP && l == 0)
+            P.coll[b * COLL_CAP + n_coll] =
+                make_uint4(q, (uint32_t)h, (uint32_t)(h >> 32), cand >= 0 ? (uint32_t)cand : NONE);
+        n_coll++;
+    };
     auto lookup = [&](uint32_t q, uint64_t *hout) -> uint32_t {
         EvInfo s = event_at(P, P.S, cs, ck1, q, 2, b, base);
         if (s.st == ST_EQUAL) { *hout = s.h; return R_HIT; }
-        if (s.st == ST_COLL) return R_COLL;
+        if (s.st == ST_COLL) { coll(q, s.h); return R_COLL; }
         EvInfo d = decl_info(q, s);
         if (d.st != ST_MATCH) return R_MISS;
         const uint32_t i = own_decl(d.h);
         if (i != NONE) {
             *hout = d.h;
-            return wave_equal2048(base + q - (XC_SEG - 1u), base + d_cand[i]) ? R_HIT : R_COLL;
+            if (wave_equal2048(base + q - (XC_SEG - 1u), base + d_cand[i])) return R_HIT;
+            coll(q, d.h);
+            return R_COLL;
         }
         if ((uint32_t)(d.v >> 32) < b) cross = true;  // an earlier buffer declared it
         return R_MISS;
@@ -831,6 +841,7 @@ __device__ __forceinline__ void walk_seq(const WalkArgs &a, uint32_t b, uint64_t
         P.tok_cnt[b] = ntok;
         P.buf_next[b] = n_ext;
         P.buf_nref[b] = n_ref;
+        if (P.coll_cnt) P.coll_cnt[b] = n_coll;
         if (ntok > tcap) atomicOr(&P.ctl[CTL_ERROR], ERR_TOKENS);
         if (cross) atomicMin(&P.ctl[CTL_FIRST_CROSS], b);
     }
@@ -941,6 +952,7 @@ __device__ __forceinline__ bool walk_blocks(const WalkArgs &a, uint32_t b)
         P.tok_cnt[b] = nblk + 1u;
         P.buf_next[b] = n_ext;
         P.buf_nref[b] = n_ref;
+        if (P.coll_cnt) P.coll_cnt[b] = 0u;  // (a collision makes the walk sequential)
         if (P.stream_res) P.stream_res[b] = make_uint2(len, NONE);  // flushed: source_ empty
         if (any_cross) atomicMin(&P.ctl[CTL_FIRST_CROSS], b);
     }
@@ -1433,6 +1445,10 @@ __global__ void k_undo(DevSet cache, const uint2 *undo, uint32_t from, uint32_t 
 {
     for (uint32_t i = from + blockIdx.x * blockDim.x + threadIdx.x; i < to; i += gridDim.x * blockDim.x) {
         const uint2 u = undo[i];
+        if (u.y == XC_REVIVED) {
+            cache.vals[u.x] |= XC_DEAD;
+            continue;
+        }
         if (u.x != NONE) cache.keys[u.x] = XC_EMPTY64;
         if (u.y != NONE) cache.lo_keys[u.y] = 0u;
     }
@@ -1448,6 +1464,10 @@ __global__ void k_undo_dev(DevSet cache, const uint2 *undo, uint32_t from, const
     const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
     for (uint32_t i = from + i0; i < to; i += stride) {
         const uint2 u = undo[i];
+        if (u.y == XC_REVIVED) {
+            cache.vals[u.x] |= XC_DEAD;
+            continue;
+        }
         if (u.x != NONE) cache.keys[u.x] = XC_EMPTY64;
         if (u.y != NONE) cache.lo_keys[u.y] = 0u;
     }
@@ -1464,6 +1484,10 @@ __global__ void k_undo_known(DevSet cache, const uint2 *undo, uint32_t from, uin
     const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
     for (uint32_t i = from + i0; i < to; i += stride) {
         const uint2 u = undo[i];
+        if (u.y == XC_REVIVED) {
+            cache.vals[u.x] |= XC_DEAD;
+            continue;
+        }
         if (u.x != NONE) cache.keys[u.x] = XC_EMPTY64;
         if (u.y != NONE) cache.lo_keys[u.y] = 0u;
     }
@@ -1475,23 +1499,24 @@ __global__ void k_undo_known(DevSet cache, const uint2 *undo, uint32_t from, uin
     }
 }
 
-// Cache growth (xc_runtime.hip cache_grow): every entry of the old full table into the larger
-// tables of `to`, its slots into the undo log at its segment index (the restore's record).  A lo32
+// Cache growth and truncation (xc_runtime.hip cache_rebuild): every entry of the old full table
+// with a segment index below `keep` (live, with drop_dead) into the tables of `to`, its slots into the undo log at its segment index (the restore's record).  A lo32
 // key shared by several entries belongs, in the undo log, to the oldest (smallest index) entry, as
 // when they were entered in index order: lo_owner[slot] = that index (k_rehash_owner applies it).
 // The filters depend on the keys only and are copied as they are.
-__global__ void k_rehash(DevSet from, DevSet to, uint2 *undo, uint32_t *lo_owner)
+__global__ void k_rehash(DevSet from, DevSet to, uint2 *undo, uint32_t *lo_owner, uint32_t keep, int drop_dead)
 {
     const uint32_t n = from.mask + 1u;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint64_t h = from.keys[i];
         if (h == XC_EMPTY64) continue;
         const uint32_t v = (uint32_t)from.vals[i];
+        if (v >= keep || (drop_dead && (from.vals[i] & XC_DEAD))) continue;
         uint32_t j = key_slot(h, to.mask);
         while (atomicCAS((unsigned long long *)&to.keys[j], (unsigned long long)XC_EMPTY64, (unsigned long long)h) !=
                XC_EMPTY64)
             j = (j + 1u) & to.mask;  // (keys are unique: every other key found here is another's)
-        to.vals[j] = v;
+        to.vals[j] = from.vals[i];   // (an evicted entry stays evicted)
         const uint32_t lo = (uint32_t)h;
         uint32_t ls = NONE;
         if (lo != 0u) {
@@ -1534,6 +1559,40 @@ __global__ void k_enter_one(PlanDev P, uint64_t h, const uint8_t *seg)
         set_insert(P.cache, h, idx, false, &s1, &s2);
         P.undo[idx] = make_uint2(s1, s2);
         P.seg_count[0] = idx + 1u;
+    }
+}
+
+// Many host-API enters at once (the COSS tier's load of its index at open): one wave per segment,
+// into slots first, first + 1, ... (the host has checked capacity and that the hashes are new).
+__global__ void k_enter_bulk(PlanDev P, const uint64_t *h, const uint8_t *segs, uint32_t n, uint32_t first)
+{
+    const uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6);
+    if (i >= n) return;
+    const uint32_t idx = first + i;
+    wave_copy(P.segs + (size_t)idx * XC_SEG, segs + (size_t)i * XC_SEG, XC_SEG);
+    if (lane_id() == 0) {
+        uint32_t s1, s2;
+        set_insert(P.cache, h[i], idx, false, &s1, &s2);
+        P.undo[idx] = make_uint2(s1, s2);
+    }
+}
+
+// Segments the COSS tier evicted (purge_stripe, xcodec_cache_coss.cc:347-377): absent to every
+// later lookup until entered again.
+__global__ void k_kill(DevSet cache, const uint64_t *h, uint32_t n)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t k = h[i];
+    uint32_t j = key_slot(k, cache.mask);
+    for (;;) {
+        const uint64_t x = cache.keys[j];
+        if (x == k) {
+            cache.vals[j] |= XC_DEAD;
+            return;
+        }
+        if (x == XC_EMPTY64) return;
+        j = (j + 1u) & cache.mask;
     }
 }
 

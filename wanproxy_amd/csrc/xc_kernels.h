@@ -110,7 +110,14 @@ struct PlanDev {
     // pending.  stream_res[b] = {base, cand}: the new source_ starts at base, the candidate.
     const uint4 *stream_st;
     uint2 *stream_res;
+    // Lookups that hit the cache with different bytes (collisions, xcodec_encoder.cc:129-137), per
+    // buffer, for the COSS tier's replay of lookup side effects (xc_coss.cpp), or null:
+    // coll[b * COLL_CAP + i] = {window end, hash lo, hash hi, 0}, coll_cnt[b] = count (may exceed
+    // COLL_CAP: then the host cannot replay the buffer).
+    uint4 *coll;
+    uint32_t *coll_cnt;
 };
+constexpr uint32_t COLL_CAP = 16;
 constexpr uint32_t SF_NOFLUSH = 1u;
 constexpr uint32_t BP_DECL = 0x80000000u;  // blk_pref: predicted declaration | D slot
 __device__ __forceinline__ bool blk_cached(uint32_t pref) { return (int32_t)pref > 0; }
@@ -204,9 +211,11 @@ __global__ void k_undo_dev(DevSet cache, const uint2 *undo, uint32_t from, const
                            const uint4 *snap_filt, const uint4 *snap_l2, const uint32_t *snap_lo_zero);
 __global__ void k_undo_known(DevSet cache, const uint2 *undo, uint32_t from, uint32_t to, uint32_t *count,
                              const uint4 *snap_filt, const uint4 *snap_l2, const uint32_t *snap_lo_zero);
-__global__ void k_rehash(DevSet from, DevSet to, uint2 *undo, uint32_t *lo_owner);
+__global__ void k_rehash(DevSet from, DevSet to, uint2 *undo, uint32_t *lo_owner, uint32_t keep, int drop_dead);
 __global__ void k_rehash_owner(uint2 *undo, uint32_t n, const uint32_t *lo_owner);
 __global__ void k_enter_one(PlanDev P, uint64_t h, const uint8_t *seg);
+__global__ void k_enter_bulk(PlanDev P, const uint64_t *h, const uint8_t *segs, uint32_t n, uint32_t first);
+__global__ void k_kill(DevSet cache, const uint64_t *h, uint32_t n);
 __global__ void k_lookup_one(PlanDev P, uint64_t h, uint8_t *out, uint32_t *found);
 __global__ void k_selftest(uint32_t *err);
 

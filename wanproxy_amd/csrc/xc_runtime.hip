@@ -360,26 +360,27 @@ static int cache_count_host(xc_cache *c, uint32_t *n)
     return XC_OK;
 }
 
-// Move the cache into arrays for `need` segments (or twice the capacity): the segment store and
-// the undo log are copied, the tables rebuilt by k_rehash (slots move; the filters depend on the
-// keys only and are copied).  Snapshots stay valid: the rebuilt undo log records the new slots.
-static int cache_grow(xc_cache *c, uint64_t need)
+// Rebuild the cache's tables for `ncap` segments, keeping the entries with a segment index below
+// `keep` (and, with drop_dead, only the live ones): the undo log is rewritten for the new slots and
+// the segment store copied when the capacity changes; the filters depend on the keys only and are
+// copied.  Snapshots stay valid: the rebuilt undo log records the new slots.
+static int cache_rebuild(xc_cache *c, uint64_t ncap, uint32_t keep, bool drop_dead)
 {
-    if (need > CAP_MAX) return fail(XC_ENOSPC, "device cache capacity exhausted (2^25 segments)");
-    const uint64_t ncap = std::min<uint64_t>(CAP_MAX, std::max<uint64_t>(need + need / 4, 2 * c->cap));
     hipStream_t s = c->ctx->stream;
     HIPCHK(hipDeviceSynchronize());  // (plans' side streams too: nothing may use the old arrays)
     uint32_t count = 0;
     int rc = cache_count_host(c, &count);
     if (rc) return rc;
     count = std::min<uint32_t>(count, (uint32_t)c->cap);
+    const uint32_t kept = std::min(count, keep);
+    const bool move_segs = ncap != c->cap;
     HostSet ns;
     uint8_t *segs = nullptr;
     uint2 *undo = nullptr;
     uint32_t *owner = nullptr;
     if ((rc = ns.alloc(ncap))) return rc;
-    if (dmalloc(&segs, (size_t)ncap * XC_SEG + 4096) != hipSuccess || dmalloc(&undo, (size_t)ncap * sizeof(uint2)) ||
-        dmalloc(&owner, (size_t)ns.n_lo * 4) != hipSuccess) {
+    if ((move_segs && dmalloc(&segs, (size_t)ncap * XC_SEG + 4096) != hipSuccess) ||
+        dmalloc(&undo, (size_t)ncap * sizeof(uint2)) != hipSuccess || dmalloc(&owner, (size_t)ns.n_lo * 4) != hipSuccess) {
         ns.release();
         dfree(segs);
         dfree(undo);
@@ -393,27 +394,38 @@ static int cache_grow(xc_cache *c, uint64_t need)
     HIPCHK(hipMemsetAsync(ns.d.vals, 0xFF, (size_t)ns.n_full * 8, s));
     HIPCHK(hipMemsetAsync(undo, 0xFF, (size_t)ncap * sizeof(uint2), s));
     HIPCHK(hipMemsetAsync(owner, 0xFF, (size_t)ns.n_lo * 4, s));
-    if (count) HIPCHK(hipMemcpyAsync(segs, c->segs, (size_t)count * XC_SEG, hipMemcpyDeviceToDevice, s));
+    if (move_segs && kept) HIPCHK(hipMemcpyAsync(segs, c->segs, (size_t)kept * XC_SEG, hipMemcpyDeviceToDevice, s));
     const uint32_t blocks = std::min<uint32_t>((c->set.n_full + 255) / 256, 8192);
-    hipLaunchKernelGGL(k_rehash, dim3(blocks), dim3(256), 0, s, c->set.d, ns.d, undo, owner);
+    hipLaunchKernelGGL(k_rehash, dim3(blocks), dim3(256), 0, s, c->set.d, ns.d, undo, owner, keep, (int)drop_dead);
     HIPCHK(hipGetLastError());
-    if (count) {
-        hipLaunchKernelGGL(k_rehash_owner, dim3(std::min<uint32_t>((count + 255) / 256, 8192)), dim3(256), 0, s,
-                           undo, count, (const uint32_t *)owner);
+    if (kept) {
+        hipLaunchKernelGGL(k_rehash_owner, dim3(std::min<uint32_t>((kept + 255) / 256, 8192)), dim3(256), 0, s,
+                           undo, kept, (const uint32_t *)owner);
         HIPCHK(hipGetLastError());
     }
+    if (kept != count) HIPCHK(hipMemcpyAsync(c->count, &kept, 4, hipMemcpyHostToDevice, s));
     HIPCHK(hipStreamSynchronize(s));
     c->set.release();
-    dfree(c->segs);
+    if (move_segs) {
+        dfree(c->segs);
+        c->segs = segs;
+    }
     dfree(c->undo);
     dfree(owner);
     c->set = ns;
-    c->segs = segs;
     c->undo = undo;
     c->cap = ncap;
-    c->host_count = count;
+    c->host_count = kept;
     c->gen++;
     return XC_OK;
+}
+
+// Move the cache into arrays for `need` segments (or twice the capacity).
+static int cache_grow(xc_cache *c, uint64_t need)
+{
+    if (need > CAP_MAX) return fail(XC_ENOSPC, "device cache capacity exhausted (2^25 segments)");
+    const uint64_t ncap = std::min<uint64_t>(CAP_MAX, std::max<uint64_t>(need + need / 4, 2 * c->cap));
+    return cache_rebuild(c, ncap, 0xFFFFFFFFu, false);
 }
 
 // Room for `extra` more segments: grow first when the count could pass the capacity.
@@ -427,6 +439,61 @@ static int cache_reserve(xc_cache *c, uint64_t extra)
     }
     if ((uint64_t)c->host_count + extra <= c->cap) return XC_OK;
     return cache_grow(c, (uint64_t)c->host_count + extra);
+}
+
+// For the COSS tier (xc_coss.cpp): the segments entered after the first `keep` are taken out again,
+// evicted ones too.  The tables are rebuilt rather than the later slots cleared: a batch's inserts
+// run in parallel, so an entry kept can sit past one taken out on its probe chain.
+extern "C" int xc__cache_truncate(xc_cache *c, uint64_t keep)
+{
+    int rc = set_dev(c->ctx);
+    if (rc) return rc;
+    return cache_rebuild(c, c->cap, (uint32_t)std::min<uint64_t>(keep, 0xFFFFFFFFu), true);
+}
+
+// Evicted segments (host hashes): absent to every lookup until entered again.
+extern "C" int xc__cache_kill(xc_cache *c, const uint64_t *h, uint64_t n)
+{
+    if (!n) return XC_OK;
+    int rc = set_dev(c->ctx);
+    if (rc) return rc;
+    hipStream_t s = c->ctx->stream;
+    uint64_t *d = nullptr;
+    HIPCHK(dmalloc(&d, n * 8));
+    HIPCHK(hipMemcpyAsync(d, h, n * 8, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_kill, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, c->set.d, (const uint64_t *)d,
+                       (uint32_t)n);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));
+    dfree(d);
+    return XC_OK;
+}
+
+// n new (hash, segment) pairs from host memory at once (the hashes absent from the cache).
+extern "C" int xc__cache_enter_bulk(xc_cache *c, const uint64_t *h, const uint8_t *segs, uint64_t n)
+{
+    if (!n) return XC_OK;
+    int rc = set_dev(c->ctx);
+    if (rc) return rc;
+    if ((rc = cache_reserve(c, n))) return rc;
+    hipStream_t s = c->ctx->stream;
+    const uint32_t first = (uint32_t)c->host_count;
+    uint64_t *dh = nullptr;
+    uint8_t *ds = nullptr;
+    HIPCHK(dmalloc(&dh, n * 8));
+    HIPCHK(dmalloc(&ds, n * XC_SEG));
+    HIPCHK(hipMemcpyAsync(dh, h, n * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(ds, segs, n * XC_SEG, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_enter_bulk, dim3((uint32_t)((n + 3) / 4)), dim3(256), 0, s, cache_plandev(c),
+                       (const uint64_t *)dh, (const uint8_t *)ds, (uint32_t)n, first);
+    HIPCHK(hipGetLastError());
+    const uint32_t cnt = first + (uint32_t)n;
+    HIPCHK(hipMemcpyAsync(c->count, &cnt, 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+    c->host_count = cnt;
+    dfree(dh);
+    dfree(ds);
+    return XC_OK;
 }
 
 extern "C" int xc__cache_reserve(xc_cache *c, uint64_t extra)
@@ -722,6 +789,8 @@ struct xc_plan {
     bool g_off = false;              // capture failed (or XC_NO_GRAPH): enqueue directly
     bool zero_ctl = false;           // the next k_clear_set also clears the run's control words
     uint32_t cache_gen = 0;          // the cache arrays P holds (xc_cache::gen)
+    uint4 *d_coll = nullptr;         // collision records (xc__plan_collisions), else null
+    uint32_t *d_coll_cnt = nullptr;
     uint64_t max_new = 0;            // most segments a run can enter (sum of len / 2048 + 1)
 };
 
@@ -1019,6 +1088,8 @@ extern "C" int xc_plan_destroy(xc_plan *p)
     dfree(p->P.ctl);
     dfree(p->d_stream_st);
     dfree(p->d_stream_res);
+    dfree(p->d_coll);
+    dfree(p->d_coll_cnt);
     for (auto &x : p->ev_live) { hipEventDestroy(x.second.first); hipEventDestroy(x.second.second); }
     for (auto e : p->ev_pool) hipEventDestroy(e);
     if (p->hs) {
@@ -1565,11 +1636,14 @@ extern "C" int xc_encode_run_host(xc_plan *p, const uint8_t *h_in, uint8_t *h_ou
 
 // Host-to-host batch, optionally with stream state (xc_stream.hip): start / cand / flags as in
 // xc_plan_set_streams, the resulting source_ base / candidate to rbase / rcand.
-extern "C" int xc__encode_batch_host_ex(xc_cache *c, const uint8_t *in, const uint64_t *in_off,
-                                        const uint64_t *in_len, uint64_t nbuf, uint8_t *out,
-                                        const uint64_t *out_off, const uint64_t *out_cap, uint64_t *out_len,
-                                        const uint64_t *start, const int64_t *cand, const uint32_t *flags,
-                                        uint64_t *rbase, int64_t *rcand)
+// Host-to-host batch with stream state (xc_stream.cpp) and, when coll_cnt is given, every buffer's
+// collision lookups (the COSS tier's replay, xc_coss.cpp): coll_cnt[i] records in
+// coll[i * COLL_CAP * 4 ..] as {window end, hash lo, hash hi, 0} (at most COLL_CAP kept).
+extern "C" int xc__encode_batch_host_coll(xc_cache *c, const uint8_t *in, const uint64_t *in_off,
+                                          const uint64_t *in_len, uint64_t nbuf, uint8_t *out,
+                                          const uint64_t *out_off, const uint64_t *out_cap, uint64_t *out_len,
+                                          const uint64_t *start, const int64_t *cand, const uint32_t *flags,
+                                          uint64_t *rbase, int64_t *rcand, uint32_t *coll_cnt, uint32_t *coll)
 {
     if (!c || (nbuf && (!in || !in_off || !in_len || !out || !out_off || !out_cap || !out_len)))
         return fail(XC_EINVAL, "null");
@@ -1580,6 +1654,15 @@ extern "C" int xc__encode_batch_host_ex(xc_cache *c, const uint8_t *in, const ui
     if (streams && (rc = xc_plan_set_streams(p, start, cand, flags))) {
         xc_plan_destroy(p);
         return rc;
+    }
+    if (coll_cnt && nbuf) {
+        if (dmalloc(&p->d_coll, (size_t)nbuf * COLL_CAP * sizeof(uint4)) != hipSuccess ||
+            dmalloc(&p->d_coll_cnt, (size_t)nbuf * 4) != hipSuccess) {
+            xc_plan_destroy(p);
+            return fail(XC_ENOMEM, "device allocation failed");
+        }
+        p->P.coll = p->d_coll;
+        p->P.coll_cnt = p->d_coll_cnt;
     }
     // the end-to-end path (xc_encode_run_host): per-sub-batch input copies overlapping the
     // encode, the encoded streams packed into pinned memory by a kernel; the input arena needs no
@@ -1602,11 +1685,26 @@ extern "C" int xc__encode_batch_host_ex(xc_cache *c, const uint8_t *in, const ui
             memcpy(out + out_off[i], h_out + pos[i], lens[i]);
         }
         if (!rc && streams && rbase && rcand) rc = xc_plan_stream_results(p, rbase, rcand);
+        if (!rc && coll_cnt && nbuf) {
+            if (hipMemcpy(coll_cnt, p->d_coll_cnt, nbuf * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(coll, p->d_coll, (size_t)nbuf * COLL_CAP * sizeof(uint4), hipMemcpyDeviceToHost) != hipSuccess)
+                rc = fail(XC_EDEVICE, "collision records copy");
+        }
     }
     xc_plan_destroy(p);  // (synchronizes before the pinned buffers return to the pool)
     pool_free(h_in);
     pool_free(h_out);
     return rc;
+}
+
+extern "C" int xc__encode_batch_host_ex(xc_cache *c, const uint8_t *in, const uint64_t *in_off,
+                                        const uint64_t *in_len, uint64_t nbuf, uint8_t *out,
+                                        const uint64_t *out_off, const uint64_t *out_cap, uint64_t *out_len,
+                                        const uint64_t *start, const int64_t *cand, const uint32_t *flags,
+                                        uint64_t *rbase, int64_t *rcand)
+{
+    return xc__encode_batch_host_coll(c, in, in_off, in_len, nbuf, out, out_off, out_cap, out_len, start, cand, flags,
+                                      rbase, rcand, nullptr, nullptr);
 }
 
 extern "C" int xc_encode_batch_host(xc_cache *c, const uint8_t *in, const uint64_t *in_off, const uint64_t *in_len,

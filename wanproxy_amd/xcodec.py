@@ -35,6 +35,9 @@ SYMBOLS = [
     "xc_encoder_pending", "xc_encode", "xc_flush", "xc_encode_streams",
     "xc_decode_plan_create", "xc_dplan_destroy", "xc_dplan_layout", "xc_decode_run", "xc_dplan_stats",
     "xc_hash_segments_host", "xc_cache_capacity",
+    "xc_coss_open", "xc_coss_close", "xc_coss_cache", "xc_coss_count", "xc_coss_stats", "xc_coss_lookup",
+    "xc_coss_enter", "xc_coss_encode_batch_host", "xc_coss_decode_batch_host", "xc_coss_store_lookup",
+    "xc_coss_store_enter",
 ]
 STREAM_FLUSH = 1  # XC_STREAM_FLUSH
 
@@ -136,18 +139,30 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.xc_dplan_layout.argtypes = [_vp, _u64p, _u64p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     lib.xc_decode_run.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
     lib.xc_dplan_stats.argtypes = [_vp, C.POINTER(DecodeStats)]
+    lib.xc_coss_open.argtypes = [_vp, C.c_char_p, C.c_char_p, C.c_uint64, C.POINTER(_vp)]
+    lib.xc_coss_close.argtypes = [_vp]
+    lib.xc_coss_cache.restype = _vp
+    lib.xc_coss_cache.argtypes = [_vp]
+    lib.xc_coss_count.argtypes = [_vp, C.POINTER(C.c_uint64)]
+    lib.xc_coss_stats.argtypes = [_vp, _u64p]
+    for name in ("xc_coss_lookup", "xc_coss_store_lookup"):
+        getattr(lib, name).argtypes = [_vp, C.c_uint64, _u8p, C.POINTER(C.c_int)]
+    for name in ("xc_coss_enter", "xc_coss_store_enter"):
+        getattr(lib, name).argtypes = [_vp, C.c_uint64, _u8p]
+    lib.xc_coss_encode_batch_host.argtypes = lib.xc_encode_batch_host.argtypes
+    lib.xc_coss_decode_batch_host.argtypes = lib.xc_decode_batch_host.argtypes
     _LIB = lib
     return lib
 
 
 # Native objects must be destroyed before the context they live on and before the HIP runtime
 # tears itself down at process exit: keep weak references and release them in order at exit.
-_LIVE = {"plan": weakref.WeakSet(), "cache": weakref.WeakSet(), "ctx": weakref.WeakSet()}
+_LIVE = {"plan": weakref.WeakSet(), "coss": weakref.WeakSet(), "cache": weakref.WeakSet(), "ctx": weakref.WeakSet()}
 
 
 @atexit.register
 def _teardown() -> None:
-    for kind in ("plan", "cache", "ctx"):
+    for kind in ("plan", "coss", "cache", "ctx"):
         for obj in list(_LIVE[kind]):
             try:
                 obj.close()
@@ -189,7 +204,7 @@ class Context:
     def close(self) -> None:
         """Destroy the context; every cache / plan created on it is released first."""
         if getattr(self, "h", None):
-            for kind in ("plan", "cache"):
+            for kind in ("plan", "coss", "cache"):
                 for obj in list(_LIVE[kind]):
                     if obj._ctx() is self:
                         obj.close()
@@ -283,6 +298,57 @@ class XCodecCache:
             pass
 
 
+class CossCache:
+    """XCodecCacheCOSS (xcodec/cache/coss/xcodec_cache_coss.{h,cc}): the persistent stripe file
+    ``<directory>/<uuid>.wpc`` with a device mirror on ``ctx`` (``ctx=None``: the host store alone,
+    lookup / enter only).  ``XCodecEncoder`` / ``XCodecDecoder`` take it like an XCodecCache."""
+
+    def __init__(self, ctx: Context | None, directory: str, uuid: str, size_mb: int = 0):
+        self.ctx = ctx
+        self.h = _vp()
+        _check(load_library().xc_coss_open(ctx.h if ctx else None, directory.encode(), uuid.encode(), size_mb,
+                                           C.byref(self.h)))
+        _LIVE["coss"].add(self)
+
+    def _ctx(self):
+        return self.ctx
+
+    def __len__(self) -> int:
+        n = C.c_uint64()
+        _check(load_library().xc_coss_count(self.h, C.byref(n)))
+        return n.value
+
+    def stats(self) -> dict:
+        o = np.zeros(6, np.uint64)
+        _check(load_library().xc_coss_stats(self.h, o))
+        return dict(zip(["hits", "found_1", "found_2", "index", "stripe_limit", "serial"], (int(x) for x in o)))
+
+    def lookup(self, h: int, store_only: bool = False) -> bytes | None:
+        """XCodecCacheCOSS::lookup (side effects included); ``store_only``: the host store alone."""
+        out = np.zeros(SEGMENT_LENGTH, np.uint8)
+        f = C.c_int()
+        fn = load_library().xc_coss_store_lookup if store_only else load_library().xc_coss_lookup
+        _check(fn(self.h, h, out, C.byref(f)))
+        return out.tobytes() if f.value else None
+
+    def enter(self, h: int, seg, store_only: bool = False) -> None:
+        seg = np.ascontiguousarray(_as_u8(seg))
+        fn = load_library().xc_coss_store_enter if store_only else load_library().xc_coss_enter
+        _check(fn(self.h, h, seg))
+
+    def close(self) -> None:
+        """~XCodecCacheCOSS: the loaded stripes are written back."""
+        if getattr(self, "h", None):
+            load_library().xc_coss_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class XCodecEncoder:
     """Batch form of XCodecEncoder: each buffer is ``encode(out, buf); flush(out)`` on a fresh
     encoder, buffers in index order, one shared cache (xcodec/xcodec_encoder.cc:60-201)."""
@@ -298,8 +364,9 @@ class XCodecEncoder:
             ooff[1:] = np.cumsum(cap)[:-1]
         out = np.zeros(max(1, int(cap.sum())), np.uint8)
         olen = np.zeros(len(bufs), np.uint64)
-        _check(load_library().xc_encode_batch_host(self.cache.h, arena, offs, lens, len(bufs),
-                                                   out, ooff, cap, olen))
+        fn = (load_library().xc_coss_encode_batch_host if isinstance(self.cache, CossCache)
+              else load_library().xc_encode_batch_host)
+        _check(fn(self.cache.h, arena, offs, lens, len(bufs), out, ooff, cap, olen))
         return [out[int(o):int(o) + int(n)].tobytes() for o, n in zip(ooff, olen)]
 
 
@@ -387,7 +454,14 @@ class XCodecDecoder:
 
     def decode_batch(self, streams, out_cap: int | None = None):
         arena, offs, lens = _pack(streams)
-        cap = (lens * 205 + 16) if out_cap is None else np.full(len(streams), out_cap, np.uint64)
+        if out_cap is None:
+            # a stream decodes to at most its length plus 2038 bytes per F1 byte in it (only a
+            # <F1 02 hash> REF grows, 10 -> 2048 bytes; an EXTRACT keeps 2048 of 2050, an escape
+            # shrinks): a tight bound, where 205 x the length would size gigabytes of staging
+            f1 = np.array([np.count_nonzero(_as_u8(x) == 0xF1) for x in streams], np.uint64)
+            cap = lens + f1 * np.uint64(2038) + np.uint64(16)
+        else:
+            cap = np.full(len(streams), out_cap, np.uint64)
         ooff = np.zeros(len(streams), dtype=np.uint64)
         if len(streams) > 1:
             ooff[1:] = np.cumsum(cap)[:-1]
@@ -397,8 +471,9 @@ class XCodecDecoder:
         st = np.zeros(len(streams), np.int32)
         unk = np.zeros(len(streams), np.uint64)
         hu = np.zeros(len(streams), np.int32)
-        _check(load_library().xc_decode_batch_host(self.cache.h, arena, offs, lens, len(streams),
-                                                   out, ooff, cap, olen, cons, st, unk, hu))
+        fn = (load_library().xc_coss_decode_batch_host if isinstance(self.cache, CossCache)
+              else load_library().xc_decode_batch_host)
+        _check(fn(self.cache.h, arena, offs, lens, len(streams), out, ooff, cap, olen, cons, st, unk, hu))
         return [(int(st[i]), out[int(ooff[i]):int(ooff[i]) + int(olen[i])].tobytes(),
                  int(cons[i]), int(unk[i]) if hu[i] else None) for i in range(len(streams))]
 
