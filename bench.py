@@ -236,7 +236,9 @@ def cpu_baseline(args, shard, warm, world) -> dict:
     import oracle  # CPU baseline: the C restatement (port) of the reference encoder
     nthreads = args.cpu_threads or host_cores()
     n_local = shard.shape[0]
-    n = min(n_local, max(4096, 256 * nthreads))
+    # the whole shard on T threads (cfg5 at N=1: 2 GiB, about 26 CPU-seconds at 16 threads), and
+    # 8192 buffers (512 MiB, about 6 s) on one
+    n = n_local
     sample = [shard[i] for i in range(n)]
     oc = oracle.Cache()
     oc.encode_batch(warm)
@@ -247,7 +249,7 @@ def cpu_baseline(args, shard, warm, world) -> dict:
                      f"{nthreads} threads, each with a private clone of the pool-warmed cache",
            "seconds": round(secs, 3), "host_cpus_visible": os.cpu_count(),
            "cores_allowed": host_cores(), "cores_note": "affinity capped by the cgroup CPU quota (cpu.max)"}
-    one = sample[:min(n, 2048)]
+    one = sample[:min(n, 8192)]
     oc1 = oracle.Cache()
     oc1.encode_batch(warm)
     secs1, _ = oc1.encode_sharded_timed(one, 1)

@@ -1,9 +1,9 @@
 """HBM traffic of one cfg5 encode step, every kernel, from rocprofv3 PMC passes (tools/pmc_kernels.sh).
 
-A step is a cache restore (k_undo_dev) followed by the encode's kernels; the PMC runs are
+A step is a cache restore (k_undo_known, or k_undo_dev) followed by the encode's kernels; the PMC runs are
 `bench.py --steps 1 --warmup 0 --no-cpu --no-e2e --no-decode --no-legs`, whose last 3 steps are the
 diagnostic steps after the timed one.  Each of those steps spans the dispatches from its
-k_undo_dev to the next one (the last to the end); only the library's kernels (xc::) count.
+restore kernel to the next one (the last to the end); only the library's kernels (xc::) count.
 
 FETCH_SIZE and WRITE_SIZE are in KiB.  Per MI355X_MICROARCH.md (HBM section), on gfx950
 FETCH_SIZE reports half the bytes of wide coalesced streaming reads (16 B per lane), so it is
@@ -29,7 +29,7 @@ def dispatches(path, counter):
 
 def steps(disp, n=3):
     ids = sorted(disp)
-    starts = [i for i in ids if "k_undo_dev" in disp[i][0]][-n:]
+    starts = [i for i in ids if "k_undo_dev" in disp[i][0] or "k_undo_known" in disp[i][0]][-n:]
     bounds = starts + [ids[-1] + 1]
     return [[i for i in ids if bounds[k] <= i < bounds[k + 1] and disp[i][0].startswith(("xc::", "void xc::"))]
             for k in range(len(starts))]
