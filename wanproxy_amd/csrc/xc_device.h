@@ -417,6 +417,16 @@ __device__ __forceinline__ uint32_t filt_word(uint32_t lo)
 {
     return (uint32_t)(((uint64_t)(lo >> 8) * (uint64_t)(XC_FILT_WORDS << 8)) >> 32);
 }
+// The same word for a filter of `words` words (XC_FILT_WORDS >> fold: the folded image)
+__device__ __forceinline__ uint32_t filt_word_n(uint32_t lo, uint32_t words)
+{
+    return (uint32_t)(((uint64_t)(lo >> 8) * (uint64_t)(words << 8)) >> 32);
+}
+__device__ __forceinline__ uint32_t filt_test_n(const uint32_t *f, uint32_t lo, uint32_t words)
+{
+    const uint32_t w = f[filt_word_n(lo, words)];
+    return (w >> (lo & 31u)) & (w >> ((lo >> 5) & 31u)) & 1u;
+}
 __device__ __forceinline__ uint32_t filt_test(const uint32_t *f, uint32_t lo)
 {
     const uint32_t w = f[filt_word(lo)];

@@ -198,15 +198,11 @@ __global__ __launch_bounds__(64 * SCAN_WAVES) void k_scan(ScanArgs a)
     uint2 *queue = queues[wave];
     const uint32_t l = lane_id();
 
-    static_assert(XC_FILT_WORDS % (256u * SCAN_WAVES) == 0u, "filter load loop");
-    for (uint32_t i = threadIdx.x * 4u; i < XC_FILT_WORDS; i += 256u * SCAN_WAVES) {
-        uint4 f = *(const uint4 *)(a.set.filt + i);
-        if (a.has2) {
-            const uint4 g = *(const uint4 *)(a.set2.filt + i);
-            f.x |= g.x; f.y |= g.y; f.z |= g.z; f.w |= g.w;
-        }
-        *(uint4 *)(filt + i) = f;
-    }
+    // the level-1 image (the first round's is cache | predicted declarations, folded for small
+    // key counts: a multiple of 4 words)
+    const uint32_t fw = a.filt_words;
+    for (uint32_t i = threadIdx.x * 4u; i < fw; i += 256u * SCAN_WAVES)
+        *(uint4 *)(filt + i) = *(const uint4 *)(a.filt + i);
     __syncthreads();
 
     // Work distribution: waves take runs of a.unit consecutive chunks from a counter (chunks
@@ -306,7 +302,7 @@ __global__ __launch_bounds__(64 * SCAN_WAVES) void k_scan(ScanArgs a)
                         V += U + (uint32_t)__mul24((int)ob, -2048);
                         const uint32_t x = (U << 20) + V;
                         lo[d * 4 + k] = x;
-                        if (MODE == 0 || MODE >= 3) hit |= filt_test(filt, x) << (d * 4 + k);
+                        if (MODE == 0 || MODE >= 3) hit |= filt_test_n(filt, x, fw) << (d * 4 + k);
                         else hit |= (x == 0x12345678u) ? 1u << (d * 4 + k) : 0u;
                     }
                 }
@@ -829,7 +825,10 @@ __device__ __forceinline__ void walk_seq(const WalkArgs &a, uint32_t b, uint64_t
     }
     if (a.shadow) {
         // every predicted REF whose following block the scan skipped must have been emitted
-        __syncthreads();
+        // (ref_done was written by this wave's lane 0: a wave-level barrier orders it)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const uint32_t nblk = len / XC_SEG, bb = P.blk_base[b];
         bool miss = false;
         for (uint32_t k = l; k < nblk; k += 64u)
@@ -863,22 +862,30 @@ __device__ __forceinline__ void walk_seq(const WalkArgs &a, uint32_t b, uint64_t
 // new block of the same buffer (a self-REF that needs a byte compare; the declaration set's
 // min-merged value tells).  Such buffers take the sequential walk.
 // Returns false (nothing written that the sequential walk would not rewrite) when the
-// reduction does not apply to buffer b.
-__device__ __forceinline__ bool walk_blocks(const WalkArgs &a, uint32_t b)
+// reduction does not apply to buffer b.  The buffer's chunks are shared by the workgroup's
+// a.waves waves (groups of WB_GROUP chunks round-robin), combined through LDS.
+struct WalkShared {
+    uint32_t fail, cross, n_ext, n_ref;
+};
+
+__device__ __forceinline__ bool walk_blocks(const WalkArgs &a, uint32_t b, WalkShared &sh)
 {
     const PlanDev &P = a.P;
-    const uint32_t l = lane_id();
+    const uint32_t l = lane_id(), wave = threadIdx.x >> 6;
     const uint32_t len = P.buf_len[b];
     const uint32_t nblk = len / XC_SEG;
     const uint32_t ck0 = P.buf_chunk0[b], ck1 = P.buf_chunk0[b + 1];
     const uint32_t tb = P.tok_base[b];
     if (!stream_plain(P, b)) return false;  // carried state or no flush: the sequential walk
+    if (threadIdx.x == 0) sh = WalkShared{0u, 0u, 0u, 0u};
+    __syncthreads();
     bool ok = true, cross = false;
     uint32_t n_ext = 0, n_ref = 0;
     // chunks in groups of WB_GROUP: every load of a group is issued before any is used (a buffer
     // of short chunks would otherwise pay one memory round trip per chunk)
     constexpr uint32_t WB_GROUP = 4;
-    for (uint32_t cg = ck0; cg < ck1 && ballot(!ok) == 0; cg += WB_GROUP) {
+    for (uint32_t cg = ck0 + wave * WB_GROUP; cg < ck1 && ballot(!ok) == 0; cg += a.waves * WB_GROUP) {
+        if (a.waves > 1 && *(volatile uint32_t *)&sh.fail) break;  // another wave gave up
         uint32_t cnt[WB_GROUP], q[WB_GROUP], st[WB_GROUP];
         uint64_t hh[WB_GROUP], vv[WB_GROUP];
 #pragma unroll
@@ -936,11 +943,18 @@ __device__ __forceinline__ bool walk_blocks(const WalkArgs &a, uint32_t b)
             if ((uint32_t)__popcll(ballot(aligned)) != want) ok = false;  // each aligned end, once
         }
     }
-    if (ballot(!ok)) return false;
     n_ext = wave_sum(n_ext);
     n_ref = wave_sum(n_ref);
     const bool any_cross = ballot(cross) != 0;
     if (l == 0) {
+        if (ballot(!ok)) atomicOr(&sh.fail, 1u);
+        if (any_cross) atomicOr(&sh.cross, 1u);
+        atomicAdd(&sh.n_ext, n_ext);
+        atomicAdd(&sh.n_ref, n_ref);
+    }
+    __syncthreads();
+    if (sh.fail) return false;
+    if (threadIdx.x == 0) {
         const uint32_t t = tb + nblk;  // END: the tail after the last block, escaped by flush()
         P.tok_op[t] = OP_END;
         P.tok_known[t] = 0u;
@@ -950,11 +964,11 @@ __device__ __forceinline__ bool walk_blocks(const WalkArgs &a, uint32_t b)
         P.tok_dpos[t] = 0u;
         P.tok_h[t] = 0u;
         P.tok_cnt[b] = nblk + 1u;
-        P.buf_next[b] = n_ext;
-        P.buf_nref[b] = n_ref;
+        P.buf_next[b] = sh.n_ext;
+        P.buf_nref[b] = sh.n_ref;
         if (P.coll_cnt) P.coll_cnt[b] = 0u;  // (a collision makes the walk sequential)
         if (P.stream_res) P.stream_res[b] = make_uint2(len, NONE);  // flushed: source_ empty
-        if (any_cross) atomicMin(&P.ctl[CTL_FIRST_CROSS], b);
+        if (sh.cross) atomicMin(&P.ctl[CTL_FIRST_CROSS], b);
     }
     return true;
 }
@@ -989,13 +1003,16 @@ __device__ __forceinline__ void decl_hash(const PlanDev &P, uint32_t b)
 
 // One wave per buffer: the first round tries the block-parallel walk, else (and in later rounds)
 // the sequential walk; then the declarations whose hash is still unknown are hashed.
-__global__ __launch_bounds__(64) void k_walk(WalkArgs a)
+__global__ __launch_bounds__(64 * WALK_WAVES_MAX) void k_walk(WalkArgs a)
 {
     if (aborted(a.P)) return;
     extern __shared__ uint64_t walk_lds[];
+    __shared__ WalkShared sh;
     const uint32_t b = a.j0 + blockIdx.x;
     if (b >= a.j1) return;
-    if (a.use_d || !walk_blocks(a, b)) walk_seq(a, b, walk_lds);
+    const bool blocks = !a.use_d && walk_blocks(a, b, sh);  // (every wave, or none: uniform per block)
+    if (threadIdx.x >= 64u) return;  // the sequential walk and the declaration hashes: wave 0
+    if (!blocks) walk_seq(a, b, walk_lds);
     decl_hash(a.P, b);
 }
 
@@ -1058,6 +1075,8 @@ __device__ __forceinline__ void block_predict(const PlanDev &P, uint32_t g, uint
         // (the set's level-2 filter is P.l2mix, the combined filter the scan reads)
         uint32_t slot;
         set_insert(P.dset, h, ((uint64_t)b << 32) | (k * XC_SEG + 2u * XC_SEG - 1u), true, &slot, nullptr);
+        const uint32_t lo = (uint32_t)h;  // (the combined level-1 image the first scan loads)
+        atomicOr(&P.fmix[filt_word_n(lo, XC_FILT_WORDS >> P.fmix_fold)], (1u << (lo & 31u)) | (1u << ((lo >> 5) & 31u)));
         P.blk_pref[g] = BP_DECL | slot;
     }
 }
@@ -1406,10 +1425,17 @@ __global__ __launch_bounds__(64) void k_window_hashes(const uint8_t *in, uint32_
 // Clear a declaration set (all of its tables) and seed the combined level-2 filter with the
 // cache's: one launch instead of a memset per table.
 __global__ void k_clear_set(DevSet s, uint32_t n_lo, uint32_t n_full, uint4 *l2mix, const uint4 *cache_l2,
-                            uint32_t *ctl_zero)
+                            uint32_t *fmix, const uint32_t *cache_filt, uint32_t fold, uint32_t *ctl_zero)
 {
     const uint32_t stride = gridDim.x * blockDim.x;
     const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
+    // the first scan's level-1 image starts as the cache's, folded
+    if (fmix)
+        for (uint32_t i = i0; i < (XC_FILT_WORDS >> fold); i += stride) {
+            uint32_t v = 0;
+            for (uint32_t j = 0; j < (1u << fold); j++) v |= cache_filt[(i << fold) + j];
+            fmix[i] = v;
+        }
     // a run's first sub-batch also clears the run's control words (nothing reads them before the
     // kernels after this one)
     if (ctl_zero && i0 < CTL_WORDS) ctl_zero[i0] = 0u;

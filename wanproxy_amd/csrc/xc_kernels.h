@@ -92,6 +92,12 @@ struct PlanDev {
     uint64_t *out_len;
     uint32_t *ctl;
     uint32_t *l2mix;  // level-2 filter of cache | predicted declarations (combined scan)
+    // level-1 filter of cache | predicted declarations for the first round's scan, folded
+    // (XC_FILT_WORDS >> fmix_fold words: word w is the OR of words w << fold .. (w + 1) << fold - 1
+    // of the full filter, which is the word filt_word_n gives for the folded count) so that
+    // small batches load a small image (k_clear_set builds it from the cache, block_predict adds)
+    uint32_t *fmix;
+    uint32_t fmix_fold;
     // k_blockpredict's verdict on aligned block g (global index), see blk_cached():
     //   cached slot + 1 (positive as int32): the block is in the cache, so the window ending at
     //     its last byte is a predicted REF.  REF shadows: the reference looks nothing up in the
@@ -154,6 +160,8 @@ struct ScanArgs {
     const uint2 *l2;  // level-2 filter of set (| set2): one 8-byte L2 read per level-1 positive
     int shadow;       // skip the windows in the shadow of predicted REFs (P.blk_pref)
     uint32_t unit;    // chunks per work unit (the plan's scan granularity, <= SCAN_UNIT)
+    const uint32_t *filt;  // level-1 image (set's filter, or P.fmix for set | set2), filt_words words
+    uint32_t filt_words;
 };
 struct ResolveArgs {
     PlanDev P;
@@ -167,7 +175,10 @@ struct WalkArgs {
     int use_d;  // 0 on the first round (no declaration layer yet)
     int shadow; // the scan skipped predicted-REF shadows: verify every such REF was emitted
     uint32_t max_decl;  // >= declarations of any buffer (longest buffer / 2048 + 2)
+    uint32_t waves;     // waves per buffer (workgroup) sharing the block-parallel walk's chunks
 };
+constexpr uint32_t WALK_WAVES_MAX = 4;
+constexpr uint32_t MIX_FOLD_MAX = 4;  // (XC_FILT_WORDS >> 4 = 2304 words: still a multiple of 4)
 // dynamic LDS of k_walk
 __host__ __device__ constexpr uint32_t walk_lds_bytes(uint32_t max_decl) { return max_decl * 16u + 8u * (max_decl / 32u + 1u); }
 struct DeclArgs {
@@ -203,6 +214,7 @@ __global__ void k_blockpredict(DeclArgs a);
 __global__ void k_or_words(uint4 *dst, const uint4 *a, const uint4 *b, uint32_t n);
 __global__ void k_alloc(EmitArgs a);
 __global__ void k_clear_set(DevSet s, uint32_t n_lo, uint32_t n_full, uint4 *l2mix, const uint4 *cache_l2,
+                            uint32_t *fmix, const uint32_t *cache_filt, uint32_t fold,
                             uint32_t *ctl_zero);
 __global__ void k_hash_segments(const uint8_t *segs, uint64_t n, uint64_t *out);
 __global__ void k_window_hashes(const uint8_t *in, uint32_t n, uint64_t *out);

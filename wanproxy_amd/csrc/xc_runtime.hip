@@ -745,6 +745,7 @@ struct xc_plan {
     uint2 *d_blk_grp = nullptr;      // k_blockhash groups
     std::vector<uint32_t> grp_base;  // [nb + 1] first group of every buffer
     uint32_t *d_l2mix;  // level-2 filter of cache | declaration set for the combined scan
+    uint32_t *d_fmix;   // level-1 image of cache | declaration set for the first scan (folded)
     xc_run_stats stats{};
     // per-kernel HIP-event timing: 0 off, XC_TIMING_ALL every kernel, XC_TIMING_SCAN the scans only
     // (each recorded event pair costs the stream a few microseconds between dependent launches)
@@ -772,6 +773,7 @@ struct xc_plan {
     uint64_t pack_cap = 0;
     int shadow = 1;          // REF shadows in the async pass (XC_NO_SHADOW=1 disables)
     uint32_t max_decl = 2;   // longest buffer / 2048 + 2 (k_walk's LDS)
+    uint32_t walk_waves = 1; // waves per buffer in k_walk (the block-parallel walk's chunk groups)
     uint32_t *d_chunk_blk = nullptr;
     // scan granularity: chunk length (a multiple of 2048 up to CHUNK_LEN) and chunks per work
     // unit, chosen so that the largest sub-batch gives every SIMD of the chip a unit
@@ -931,6 +933,12 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     }
     chunk0[nbuf] = (uint32_t)chunks.size();
     blk_base[nbuf] = (uint32_t)nblk;
+    {   // a wave per 4 chunks of the longest buffer, up to WALK_WAVES_MAX: short chunks (small
+        // batches) would leave the block walk one memory round trip per 4 chunks on one wave
+        uint32_t maxc = 0;
+        for (uint64_t i = 0; i < nbuf; i++) maxc = std::max(maxc, chunk0[i + 1] - chunk0[i]);
+        p->walk_waves = std::min<uint32_t>(WALK_WAVES_MAX, std::max<uint32_t>(1u, (maxc + 3u) / 4u));
+    }
     if (toks > 0xFFFFFFF0ull) return fail(XC_EINVAL, "batch too large");
     p->in_bytes = io + 8192;  // slack: the scan prefetches up to two blocks past a buffer
     p->out_bytes = oo + 256;
@@ -1026,6 +1034,9 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     }
     HIPCHK(dmalloc(&p->d_l2mix, (size_t)XC_L2_WORDS * 8));
     P.l2mix = p->d_l2mix;
+    HIPCHK(dmalloc(&p->d_fmix, (size_t)XC_FILT_WORDS * 4));
+    P.fmix = p->d_fmix;
+    P.fmix_fold = 0;
     // the declaration set's level-2 filter is the combined one (cache | declarations): every
     // declaration insert lands there directly, and the declaration-layer scans test a superset
     P.dset.l2 = p->d_l2mix;
@@ -1082,6 +1093,7 @@ extern "C" int xc_plan_destroy(xc_plan *p)
     dfree(p->d_blk_buf);
     dfree(p->d_blk_grp);
     dfree(p->d_l2mix);
+    dfree(p->d_fmix);
     dfree(p->P.buf_next);
     dfree(p->P.buf_nref);
     dfree(p->P.buf_slot);
@@ -1247,11 +1259,14 @@ static int launch_scan(xc_plan *p, const Layer &L, const DevSet &set, uint32_t c
 {
     if (ck_hi <= ck_lo) return XC_OK;
     xc_ctx *ctx = p->cache->ctx;
-    ScanArgs a{p->P, L, set, ck_lo, ck_hi, 0, DevSet{}, 0, (const uint2 *)set.l2, shadow, p->scan_unit};
+    ScanArgs a{p->P, L, set, ck_lo, ck_hi, 0, DevSet{}, 0, (const uint2 *)set.l2, shadow, p->scan_unit,
+               set.filt, XC_FILT_WORDS};
     if (set2) {
         a.set2 = *set2;
         a.has2 = 1;
         a.l2 = (const uint2 *)p->d_l2mix;  // cache | set2, built by k_clear_set + k_blockhash
+        a.filt = p->d_fmix;               // the same for level 1, folded
+        a.filt_words = XC_FILT_WORDS >> p->P.fmix_fold;
     }
     KSpan span(p, XC_K_SCAN);
     if (p->timing) p->ktimes.scan_bytes += p->chunk_bytes[ck_hi] - p->chunk_bytes[ck_lo];
@@ -1284,10 +1299,11 @@ static int launch_walk_round(xc_plan *p, uint32_t j0, uint32_t j1, int use_d, in
     // one wave per buffer: the block-parallel walk on the first round where it applies, else
     // the sequential walk (every buffer on the declaration-layer rounds), then the hashes of
     // declarations no event supplied
-    WalkArgs w{p->P, j0, j1, use_d, shadow, p->max_decl};
+    const uint32_t nw = use_d ? 1u : p->walk_waves;  // (later rounds walk sequentially: one wave)
+    WalkArgs w{p->P, j0, j1, use_d, shadow, p->max_decl, nw};
     {
         KSpan span(p, XC_K_WALK);
-        hipLaunchKernelGGL(k_walk, dim3(j1 - j0), dim3(64), walk_lds_bytes(p->max_decl), s, w);
+        hipLaunchKernelGGL(k_walk, dim3(j1 - j0), dim3(64 * nw), walk_lds_bytes(p->max_decl), s, w);
         HIPCHK(hipGetLastError());
     }
     p->stats.walk_rounds++;
@@ -1346,7 +1362,8 @@ static int launch_first_round(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t s1,
     p->stats.outer_rounds++;
     // the set's clear (and, first in a run, the control words' clear)
     hipLaunchKernelGGL(k_clear_set, dim3(1024), dim3(256), 0, s, p->P.dset, p->dset.n_lo, p->dset.n_full,
-                       (uint4 *)p->d_l2mix, (const uint4 *)p->P.cache.l2, p->zero_ctl ? p->P.ctl : nullptr);
+                       (uint4 *)p->d_l2mix, (const uint4 *)p->P.cache.l2, p->d_fmix, (const uint32_t *)p->P.cache.filt,
+                       p->P.fmix_fold, p->zero_ctl ? p->P.ctl : nullptr);
     HIPCHK(hipGetLastError());
     p->zero_ctl = false;
     const bool inline_hash = p->next_hash <= sb;
@@ -1519,6 +1536,13 @@ extern "C" int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, ui
     p->P.out = d_out;
     p->P.out_len = d_out_len;
     p->stats = xc_run_stats{};
+    {   // the first scans' level-1 image: folded while it keeps >= 16 bits per key (the keys of
+        // the cache at the start, when known, and every segment this run can enter)
+        const uint64_t keys = (p->cache->host_count >= 0 ? (uint64_t)p->cache->host_count : p->cache->cap) + p->max_new;
+        uint32_t f = 0;
+        while (f < MIX_FOLD_MAX && ((uint64_t)XC_FILT_WORDS * 32u >> (f + 1)) >= 16u * keys) f++;
+        p->P.fmix_fold = f;
+    }
     p->cache->host_count = -1;
     if (p->sub.size() > 1) p->zero_ctl = true;  // (the first k_clear_set clears the control words)
     else HIPCHK(hipMemsetAsync(p->P.ctl, 0, CTL_WORDS * 4, s));
@@ -1740,7 +1764,7 @@ extern "C" double xc__scan_ablation(xc_plan *p, const uint8_t *d_in, int mode, i
     hipSetDevice(ctx->dev);
     p->P.in = d_in;
     ScanArgs a{p->P, p->P.S, p->P.cache, 0, p->nchunks, (uint32_t)mode, DevSet{}, 0, (const uint2 *)p->P.cache.l2, 0,
-               p->scan_unit};
+               p->scan_unit, p->P.cache.filt, XC_FILT_WORDS};
     uint32_t need = (p->nchunks + SCAN_WAVES * p->scan_unit - 1) / (SCAN_WAVES * p->scan_unit);
     uint32_t grid = std::min<uint32_t>(need, (uint32_t)ctx->n_cu);
     hipEvent_t e0, e1;
