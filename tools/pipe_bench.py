@@ -70,8 +70,10 @@ def warm_store(store):
     w.XCodecEncoder(store).encode_batch(warm)
 
 
-res = {"connections": n, "turns": turns, "read_bytes": W.BUF}
-for batched in (True, False):
+res = {"connections": n, "turns": turns, "read_bytes": W.BUF,
+       "note": "each mode run twice, the second measured (the first pays one-time pinned/device "
+               "allocations of the library's pool and page faults)"}
+for batched in (True, True, False, False):
     a = Proxy(be, UUID_A, warm=warm_store, batched=batched)
     b = Proxy(be, UUID_B, batched=batched)
     # the peer's copy of A's cache holds the pool too (steady state: no <ASK>/<LEARN>)

@@ -849,7 +849,8 @@ extern "C" int xc_decode_batch_host(xc_cache *c, const uint8_t *in, const uint64
         DHIP(dalloc(&d_out, p->out_bytes));
         DHIP(dalloc(&d_u64, 3 * (size_t)ns));
         DHIP(dalloc(&d_i32, 2 * (size_t)ns));
-        memset(h_in, 0, p->in_bytes);
+        // (the padding between streams needs no clearing: the tokenizer clips every window to its
+        // stream's length)
         for (uint32_t j = 0; j < ns; j++) memcpy(h_in + p->ioff[j], in + in_off[j], in_len[j]);
         DHIP(hipMemcpyAsync(d_in, h_in, p->in_bytes, hipMemcpyHostToDevice, s));
         int r = xc_decode_run(p, d_in, d_out, d_u64, d_u64 + ns, d_i32, d_u64 + 2 * ns, d_i32 + ns);

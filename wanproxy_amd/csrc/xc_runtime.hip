@@ -1721,6 +1721,52 @@ extern "C" int xc__encode_batch_host_coll(xc_cache *c, const uint8_t *in, const 
     return rc;
 }
 
+// Internal (xc_stream.cpp): the host batch with each item gathered from two host pieces (an
+// encoder's pending source_ and its new input) straight into the pinned input arena, and each
+// item's encoded bytes handed to `take` from pinned memory together with the item's input (from
+// which the caller keeps the new source_), after the stream results are in rbase / rcand: no
+// intermediate host arenas.
+extern "C" int xc__encode_gather(xc_cache *c, uint64_t nbuf, const uint8_t *const *head, const uint64_t *head_len,
+                                 const uint8_t *const *tail, const uint64_t *tail_len, const uint64_t *start,
+                                 const int64_t *cand, const uint32_t *flags, uint64_t *rbase, int64_t *rcand,
+                                 int (*take)(void *ctx, uint64_t i, const uint8_t *out, uint64_t out_len,
+                                             const uint8_t *in),
+                                 void *ctx)
+{
+    if (!c || (nbuf && (!head || !head_len || !tail || !tail_len || !rbase || !rcand || !take)))
+        return fail(XC_EINVAL, "null");
+    if (nbuf == 0) return XC_OK;
+    std::vector<uint64_t> len(nbuf);
+    for (uint64_t i = 0; i < nbuf; i++) len[i] = head_len[i] + tail_len[i];
+    xc_plan *p = nullptr;
+    int rc = xc_encode_plan_create(c, len.data(), nbuf, &p);
+    if (rc) return rc;
+    if ((rc = xc_plan_set_streams(p, start, cand, flags))) {
+        xc_plan_destroy(p);
+        return rc;
+    }
+    uint8_t *h_in = nullptr, *h_out = nullptr;
+    uint64_t cap_total = 0;
+    for (uint64_t i = 0; i < nbuf; i++) cap_total += 2 * len[i] + 16;
+    std::vector<uint64_t> lens(nbuf), pos(nbuf);
+    if (hmalloc((void **)&h_in, p->in_bytes) != hipSuccess || hmalloc((void **)&h_out, cap_total + 16) != hipSuccess) {
+        pool_free(h_in);
+        xc_plan_destroy(p);
+        return fail(XC_ENOMEM, "pinned allocation failed");
+    }
+    for (uint64_t i = 0; i < nbuf; i++) {
+        if (head_len[i]) memcpy(h_in + p->in_off[i], head[i], head_len[i]);
+        if (tail_len[i]) memcpy(h_in + p->in_off[i] + head_len[i], tail[i], tail_len[i]);
+    }
+    rc = xc_encode_run_host(p, h_in, h_out, cap_total + 16, lens.data(), pos.data());
+    if (!rc) rc = xc_plan_stream_results(p, rbase, rcand);
+    for (uint64_t i = 0; i < nbuf && !rc; i++) rc = take(ctx, i, h_out + pos[i], lens[i], h_in + p->in_off[i]);
+    xc_plan_destroy(p);  // (synchronizes before the pinned buffers return to the pool)
+    pool_free(h_in);
+    pool_free(h_out);
+    return rc;
+}
+
 extern "C" int xc__encode_batch_host_ex(xc_cache *c, const uint8_t *in, const uint64_t *in_off,
                                         const uint64_t *in_len, uint64_t nbuf, uint8_t *out,
                                         const uint64_t *out_off, const uint64_t *out_cap, uint64_t *out_len,

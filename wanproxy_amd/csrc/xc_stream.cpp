@@ -12,6 +12,7 @@
 // with the reference's single-threaded order (call k sees the cache after calls < k).  A batch
 // round holds each encoder at most once; a later call of the same encoder starts a new round.
 #include <algorithm>
+#include <cstring>
 #include <new>
 #include <stdexcept>
 #include <string>
@@ -20,11 +21,12 @@
 #include "../../include/xcodec_hip.h"
 
 extern "C" int xc__set_error(int code, const char *msg);
-extern "C" int xc__encode_batch_host_ex(xc_cache *c, const uint8_t *in, const uint64_t *in_off,
-                                        const uint64_t *in_len, uint64_t nbuf, uint8_t *out,
-                                        const uint64_t *out_off, const uint64_t *out_cap, uint64_t *out_len,
-                                        const uint64_t *start, const int64_t *cand, const uint32_t *flags,
-                                        uint64_t *rbase, int64_t *rcand);
+extern "C" int xc__encode_gather(xc_cache *c, uint64_t nbuf, const uint8_t *const *head, const uint64_t *head_len,
+                                 const uint8_t *const *tail, const uint64_t *tail_len, const uint64_t *start,
+                                 const int64_t *cand, const uint32_t *flags, uint64_t *rbase, int64_t *rcand,
+                                 int (*take)(void *ctx, uint64_t i, const uint8_t *out, uint64_t out_len,
+                                             const uint8_t *in),
+                                 void *ctx);
 
 namespace {
 constexpr uint64_t MAX_BUFFER = 1u << 20;  // longest device batch item (xc_kernels.h MAX_BUF)
@@ -110,49 +112,48 @@ static int encode_streams(xc_encoder *const *enc, const uint8_t *const *in, cons
             if (!whole) break;  // the rest of this input is the next round's
         }
         const uint64_t m = items.size();
-        std::vector<uint64_t> ioff(m), ilen(m), ooff(m), ocap(m), olen(m), start(m), rbase(m);
+        std::vector<const uint8_t *> head(m), tail(m);
+        std::vector<uint64_t> hlen(m), tlen(m), start(m), rbase(m);
         std::vector<int64_t> cand(m), rcand(m);
         std::vector<uint32_t> fl(m);
-        uint64_t isz = 0, osz = 0;
         for (uint64_t i = 0; i < m; i++) {
             const xc_encoder *e = enc[items[i].call];
-            ioff[i] = isz;
-            ilen[i] = e->source.size() + items[i].take;
-            isz += ilen[i];
-            ooff[i] = osz;
-            ocap[i] = 2 * ilen[i] + 16;
-            osz += ocap[i];
+            head[i] = e->source.data();
+            hlen[i] = e->source.size();
+            tail[i] = items[i].take ? in[items[i].call] + items[i].from : nullptr;
+            tlen[i] = items[i].take;
             start[i] = e->source.size();
             cand[i] = e->cand;
             fl[i] = items[i].flush ? 0u : SF_NOFLUSH;
         }
-        std::vector<uint8_t> arena(std::max<uint64_t>(isz, 1)), obuf(std::max<uint64_t>(osz, 1));
-        for (uint64_t i = 0; i < m; i++) {
-            const xc_encoder *e = enc[items[i].call];
-            std::copy(e->source.begin(), e->source.end(), arena.begin() + ioff[i]);
-            if (items[i].take)
-                std::copy(in[items[i].call] + items[i].from, in[items[i].call] + items[i].from + items[i].take,
-                          arena.begin() + ioff[i] + e->source.size());
-        }
-        int rc = xc__encode_batch_host_ex(cache, arena.data(), ioff.data(), ilen.data(), m, obuf.data(), ooff.data(),
-                                          ocap.data(), olen.data(), start.data(), cand.data(), fl.data(),
-                                          rbase.data(), rcand.data());
-        if (rc) return rc;
-        for (uint64_t i = 0; i < m; i++)
-            if (rbase[i] > ilen[i] || (rcand[i] >= 0 && ((uint64_t)rcand[i] < rbase[i] || (uint64_t)rcand[i] >= ilen[i])))
+        // each item's output goes straight to its call's output, its new source_ (the input from
+        // rbase on: empty after a flush) straight from the pinned arena
+        struct Take {
+            const std::vector<Item> *items;
+            xc_encoder *const *enc;
+            uint8_t *out;
+            const uint64_t *out_off, *out_cap;
+            uint64_t *out_len, *done;
+            const uint64_t *hlen, *tlen, *rbase;
+            const int64_t *rcand;
+        } tk{&items, enc, out, out_off, out_cap, out_len, done.data(), hlen.data(), tlen.data(), rbase.data(), rcand.data()};
+        auto take = [](void *vp, uint64_t i, const uint8_t *o, uint64_t olen, const uint8_t *inp) -> int {
+            Take &t = *(Take *)vp;
+            const uint64_t k = (*t.items)[i].call, ilen = t.hlen[i] + t.tlen[i];
+            if (t.rbase[i] > ilen || (t.rcand[i] >= 0 && ((uint64_t)t.rcand[i] < t.rbase[i] || (uint64_t)t.rcand[i] >= ilen)))
                 return xc__set_error(XC_EDEVICE, "inconsistent stream state from the device");
-        for (uint64_t i = 0; i < m; i++) {
-            const uint64_t k = items[i].call;
-            xc_encoder *e = enc[k];
-            if (out_len[k] + olen[i] > out_cap[k]) return xc__set_error(XC_EINVAL, "output capacity too small");
-            std::copy(obuf.begin() + ooff[i], obuf.begin() + ooff[i] + olen[i], out + out_off[k] + out_len[k]);
-            out_len[k] += olen[i];
-            // the new source_: the buffer from rbase on (empty after a flush)
-            std::vector<uint8_t> src(arena.begin() + ioff[i] + rbase[i], arena.begin() + ioff[i] + ilen[i]);
-            e->source.swap(src);
-            e->cand = rcand[i] < 0 ? -1 : rcand[i] - (int64_t)rbase[i];
-            done[k] += items[i].take;
-        }
+            if (t.out_len[k] + olen > t.out_cap[k]) return xc__set_error(XC_EINVAL, "output capacity too small");
+            std::copy(o, o + olen, t.out + t.out_off[k] + t.out_len[k]);
+            t.out_len[k] += olen;
+            xc_encoder *e = t.enc[k];
+            e->source.assign(inp + t.rbase[i], inp + ilen);
+            e->cand = t.rcand[i] < 0 ? -1 : t.rcand[i] - (int64_t)t.rbase[i];
+            t.done[k] += (*t.items)[i].take;
+            return XC_OK;
+        };
+        int rc = xc__encode_gather(cache, m, head.data(), hlen.data(), tail.data(), tlen.data(), start.data(),
+                                   cand.data(), fl.data(), rbase.data(), rcand.data(), take, &tk);
+        if (rc) return rc;
         // calls fully done advance the start of the next round
         k0 = items.back().call + (done[items.back().call] == in_len[items.back().call] ? 1 : 0);
     }
@@ -189,4 +190,23 @@ extern "C" int xc_flush(xc_encoder *e, uint8_t *out, uint64_t cap, uint64_t *out
     int rc = xc_encode_streams(&e, &none, &zero, &fl, 1, out, &off, &cap, out_len);
     if (!rc && emitted) *emitted = *out_len > 0 ? 1 : 0;
     return rc;
+}
+
+// Internal (the Python mirror's decode_batch): an output bound per stream, its length plus 2038 bytes
+// per F1 byte in it (only a REF, F1 02 + 8 bytes, grows: 10 -> 2048 bytes; an EXTRACT keeps 2048
+// of 2050, an escape shrinks), plus 16.
+extern "C" int xc__decode_bound(const uint8_t *in, const uint64_t *off, const uint64_t *len, uint64_t n,
+                                uint64_t *cap)
+{
+    if (n && (!in || !off || !len || !cap)) return xc__set_error(XC_EINVAL, "null");
+    for (uint64_t j = 0; j < n; j++) {
+        const uint8_t *p = in + off[j], *e = p + len[j];
+        uint64_t c = 0;
+        while ((p = (const uint8_t *)std::memchr(p, 0xF1, (size_t)(e - p))) != nullptr) {
+            c++;
+            p++;
+        }
+        cap[j] = len[j] + 2038u * c + 16u;
+    }
+    return XC_OK;
 }

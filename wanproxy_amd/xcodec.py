@@ -14,6 +14,7 @@ from __future__ import annotations
 import atexit
 import ctypes as C
 import os
+import threading
 import weakref
 
 import numpy as np
@@ -116,6 +117,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
                                          _u64p]
     lib.xc_decode_batch_host.argtypes = [_vp, _u8p, _u64p, _u64p, C.c_uint64, _u8p, _u64p, _u64p,
                                          _u64p, _u64p, _i32p, _u64p, _i32p]
+    lib.xc__decode_bound.argtypes = [_u8p, _u64p, _u64p, C.c_uint64, _u64p]
     lib.xc_selftest.argtypes = [_vp]
     lib.xc_cache_restore_async.argtypes = [_vp]
     lib.xc_plan_set_timing.argtypes = [_vp, C.c_int]
@@ -362,7 +364,7 @@ class XCodecEncoder:
         ooff = np.zeros(len(bufs), dtype=np.uint64)
         if len(bufs) > 1:
             ooff[1:] = np.cumsum(cap)[:-1]
-        out = np.zeros(max(1, int(cap.sum())), np.uint8)
+        out = _scratch("encode", int(cap.sum()))
         olen = np.zeros(len(bufs), np.uint64)
         fn = (load_library().xc_coss_encode_batch_host if isinstance(self.cache, CossCache)
               else load_library().xc_encode_batch_host)
@@ -415,6 +417,21 @@ class XCodecStreamEncoder:
             pass
 
 
+_TLS = threading.local()
+
+
+def _scratch(name: str, n: int) -> np.ndarray:
+    """A per-thread output staging array of at least n bytes, kept between calls: a fresh array
+    per call pays a page fault per 4 KiB when the library first writes it.  (Results are copied
+    out with ``tobytes`` before the next call.)"""
+    d = _TLS.__dict__.setdefault("bufs", {})
+    a = d.get(name)
+    if a is None or a.size < n:
+        a = np.empty(max(n, 1), np.uint8)
+        d[name] = a
+    return a[:max(n, 1)]
+
+
 def encode_streams(calls) -> list[bytes]:
     """Cross-connection batch (xc_encode_streams): ``calls`` is a sequence of
     ``(encoder, data, flush)``, run in order as ``encoder.encode(data)`` then, when ``flush``,
@@ -436,7 +453,7 @@ def encode_streams(calls) -> list[bytes]:
         pend[id(e)] = p
     off = np.zeros(n, np.uint64)
     off[1:] = np.cumsum(cap)[:-1]
-    out = np.zeros(int(cap.sum()), np.uint8)
+    out = _scratch("streams", int(cap.sum()))
     olen = np.zeros(n, np.uint64)
     encs = (_vp * n)(*[e.h for e, _, _ in calls])
     ptrs = (C.c_void_p * n)(*[d.ctypes.data if d.size else None for d in datas])
@@ -458,14 +475,14 @@ class XCodecDecoder:
             # a stream decodes to at most its length plus 2038 bytes per F1 byte in it (only a
             # <F1 02 hash> REF grows, 10 -> 2048 bytes; an EXTRACT keeps 2048 of 2050, an escape
             # shrinks): a tight bound, where 205 x the length would size gigabytes of staging
-            f1 = np.array([np.count_nonzero(_as_u8(x) == 0xF1) for x in streams], np.uint64)
-            cap = lens + f1 * np.uint64(2038) + np.uint64(16)
+            cap = np.zeros(len(streams), np.uint64)
+            _check(load_library().xc__decode_bound(arena, offs, lens, len(streams), cap))
         else:
             cap = np.full(len(streams), out_cap, np.uint64)
         ooff = np.zeros(len(streams), dtype=np.uint64)
         if len(streams) > 1:
             ooff[1:] = np.cumsum(cap)[:-1]
-        out = np.zeros(max(1, int(cap.sum())), np.uint8)
+        out = _scratch("decode", int(cap.sum()))
         olen = np.zeros(len(streams), np.uint64)
         cons = np.zeros(len(streams), np.uint64)
         st = np.zeros(len(streams), np.int32)
