@@ -247,6 +247,13 @@ int xc_coss_decode_batch_host(xc_coss *c, const uint8_t *in, const uint64_t *in_
                               uint64_t nbuf, uint8_t *out, const uint64_t *out_off, const uint64_t *out_cap,
                               uint64_t *out_len, uint64_t *consumed, int32_t *status, uint64_t *unknown,
                               int32_t *has_unknown);
+/* xc_encode_streams over the COSS cache: stateful encoders (xcodec_encoder.h:45-50) created with
+ * xc_encoder_create(xc_coss_cache(c), ...), their calls run in call order as one batch each round,
+ * the COSS state advanced as the reference's sequential calls would (the server side's waiting
+ * mode, encode() without flush, included). */
+int xc_coss_encode_streams(xc_coss *c, xc_encoder *const *enc, const uint8_t *const *in, const uint64_t *in_len,
+                           const uint32_t *flags, uint64_t n, uint8_t *out, const uint64_t *out_off,
+                           const uint64_t *out_cap, uint64_t *out_len);
 /* The host store's own lookup / enter, without the device mirror (tests of the store). */
 int xc_coss_store_lookup(xc_coss *c, uint64_t hash, uint8_t *out, int *found);
 int xc_coss_store_enter(xc_coss *c, uint64_t hash, const uint8_t *seg);

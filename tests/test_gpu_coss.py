@@ -74,3 +74,48 @@ def test_coss_encode_decode_equal_the_oracle(gpu_ctx, oracle_mod, tmp_path, size
     oc.close()
     pc.close()
     assert (do / (UUID_B + ".wpc")).read_bytes() == (dp / (UUID_B + ".wpc")).read_bytes()
+
+
+@pytest.mark.parametrize("size_mb", [3, 20])
+def test_coss_stream_encoders_equal_the_oracle(gpu_ctx, oracle_mod, tmp_path, size_mb):
+    """Stateful encoders over COSS (the server side's waiting mode: encode() without flush, the
+    candidate and pending bytes carried between calls), many connections batched per round
+    (xc_coss_encode_streams): every call's bytes, the final flushes and the file equal the oracle's
+    stateful encoders over the oracle's COSS cache."""
+    import wanproxy_amd as w
+    do, dp = tmp_path / "o", tmp_path / "p"
+    do.mkdir()
+    dp.mkdir()
+    oc = oracle_mod.Cache.coss(str(do), UUID_A, size_mb)
+    pc = w.CossCache(gpu_ctx, str(dp), UUID_A, size_mb)
+    rng = np.random.default_rng(size_mb)
+    nconn = 24
+    oenc = [oracle_mod.Encoder(oc) for _ in range(nconn)]
+    genc = [w.XCodecStreamEncoder(pc) for _ in range(nconn)]
+    # each connection's data: pool repeats and fresh data (64 KiB reads), cut at random points
+    conns = []
+    for k, bufs in enumerate(_batches(4 if size_mb == 3 else 10, nconn, 0x900 + size_mb)):
+        for c in range(nconn):
+            conns.append((c, bufs[c]))
+    for turn in range(0, len(conns), nconn):
+        calls = []
+        for c, buf in conns[turn:turn + nconn]:
+            cuts = sorted(rng.integers(0, len(buf), 2))
+            for piece in np.split(buf, cuts):
+                calls.append((c, piece, bool(rng.random() < 0.3)))
+        rng.shuffle(calls)
+        want = []
+        for c, d, f in calls:
+            o = oenc[c].encode(d)
+            if f:
+                o += oenc[c].flush()[1]
+            want.append(o)
+        got = w.encode_streams([(genc[c], d, f) for c, d, f in calls])
+        bad = [i for i, (a, b) in enumerate(zip(want, got)) if a != b]
+        assert not bad, (turn, bad[:5])
+    for c in range(nconn):
+        assert genc[c].flush() == oenc[c].flush(), c
+    assert len(oc) == len(pc)
+    oc.close()
+    pc.close()
+    assert (do / (UUID_A + ".wpc")).read_bytes() == (dp / (UUID_A + ".wpc")).read_bytes()

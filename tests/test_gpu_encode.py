@@ -471,3 +471,21 @@ def test_cache_grows_like_the_reference_map(gpu_ctx, oracle_mod):
     got = w.XCodecDecoder(dc).decode_batch(streams)
     want = oracle_mod.Cache().decode_batch(streams)
     assert got == want and len(dc) == 40 * 32
+
+
+@pytest.mark.parametrize("blocks", ["1", "2", "8"])
+def test_block_walk_falls_back_on_any_event(gpu_ctx, oracle_mod, monkeypatch, blocks):
+    """The block-parallel walk applies only when no event between aligned windows decides
+    anything; an unaligned hit behind an aligned REF of the same chunk (a later lane of the chunk's
+    event list) must send the buffer to the sequential walk."""
+    monkeypatch.setenv("XC_CHUNK_BLOCKS", blocks)
+    pool = W.pool(64)
+    blk = lambda i: pool[(i % 64) * 2048:(i % 64) * 2048 + 2048]
+    bufs = []
+    for j in range(32):
+        parts = []
+        for k in range(6):
+            parts.append(blk(j + k))                           # aligned: a cached block (REF)
+            parts.append(W.gen(7000 + 16 * j + k, 37 + 211 * ((j + k) % 9)))  # shifts the next copy
+        bufs.append(np.concatenate(parts))
+    _check(gpu_ctx, oracle_mod, bufs, warm=[[pool[i:i + 65536] for i in range(0, len(pool), 65536)]])

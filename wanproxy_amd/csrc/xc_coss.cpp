@@ -683,27 +683,28 @@ extern "C" int xc_coss_enter(xc_coss *c, uint64_t h, const uint8_t *seg)
     }
 }
 
-// Encoder batch over the COSS cache: buffer i is one encode()+flush() on a fresh encoder, buffers
-// in index order (xc_encode_batch_host's semantics), the COSS state advanced exactly as the
-// reference's would be.
-extern "C" int xc_coss_encode_batch_host(xc_coss *c, const uint8_t *in, const uint64_t *in_off,
-                                         const uint64_t *in_len, uint64_t nbuf, uint8_t *out,
-                                         const uint64_t *out_off, const uint64_t *out_cap, uint64_t *out_len)
+namespace {
+// An encoder batch item over the COSS cache: `data` (len bytes) is an encoder's pending source_
+// followed by its new input, window ends below `start` already looked up, candidate `cand` (or -1),
+// encode() only when `noflush`.  `off`: where data lies in the caller's item (restarts move it).
+struct CItem {
+    uint64_t buf;
+    const uint8_t *data;
+    uint64_t len, start;
+    int64_t cand;
+    uint64_t off;
+    bool noflush;
+};
+
+// The batch on the device, its cache events replayed into the Store in the reference's order
+// (items in order), restarting the rest after a change a later event depends on.  Outputs append
+// at out + out_off[buf]; res_base / res_cand: the new source_ start and candidate of each buffer,
+// relative to its first item's data.
+int coss_encode(xc_coss *c, std::vector<CItem> items, uint8_t *out, const uint64_t *out_off, const uint64_t *out_cap,
+                uint64_t *out_len, uint64_t *res_base, int64_t *res_cand)
 {
-    if (!c || !c->cache || (nbuf && (!in || !in_off || !in_len || !out || !out_off || !out_cap || !out_len)))
-        return xc__set_error(XC_EINVAL, "null (or a host-only COSS store)");
-    try {
-        struct Item {
-            uint64_t buf;
-            const uint8_t *data;
-            uint64_t len, start;
-            int64_t cand;
-        };
-        std::vector<Item> items;
-        for (uint64_t i = 0; i < nbuf; i++) {
-            items.push_back({i, in + in_off[i], in_len[i], 0, -1});
-            out_len[i] = 0;
-        }
+    {
+        {
         while (!items.empty()) {
             const uint64_t m = items.size();
             uint64_t count0 = 0;
@@ -713,6 +714,7 @@ extern "C" int xc_coss_encode_batch_host(xc_coss *c, const uint8_t *in, const ui
             std::vector<uint64_t> ioff(m), ilen(m), start(m), ooff(m), ocap(m), olen(m), rbase(m);
             std::vector<int64_t> cand(m), rcand(m);
             std::vector<uint32_t> fl(m, 0u), ccnt(m);
+            for (uint64_t k = 0; k < m; k++) fl[k] = items[k].noflush ? 1u : 0u;  // (SF_NOFLUSH)
             std::vector<uint32_t> coll(m * coss::COLL_CAP * 4);
             uint64_t isz = 0, osz = 0;
             for (uint64_t k = 0; k < m; k++) {
@@ -796,10 +798,10 @@ extern "C" int xc_coss_encode_batch_host(xc_coss *c, const uint8_t *in, const ui
             if ((rc = unmirrorable(c))) return rc;
             uint64_t entered = 0;
             bool redo = false;
-            std::vector<Item> next;
+            std::vector<CItem> next;
             std::vector<Change> held;  // changes nothing later in the pass saw: mirrored at its end
             for (uint64_t k = 0; k < m && !redo; k++) {
-                const Item &it = items[k];
+                const CItem &it = items[k];
                 for (size_t e = 0; e < ev[k].size(); e++) {
                     const EncEvent &E = ev[k][e];
                     Touch t;
@@ -831,15 +833,17 @@ extern "C" int xc_coss_encode_batch_host(xc_coss *c, const uint8_t *in, const ui
                         if ((rc = mirror(c, h))) return rc;
                     held.clear();
                     if ((rc = mirror(c, ch))) return rc;
-                    const uint64_t keep = E.out_end;
+                    // (after flush()'s declaration only the escaped tail follows: no lookups)
+                    const uint64_t keep = E.pos == ~0ull ? olen[k] : E.out_end;
                     if (out_len[it.buf] + keep > out_cap[it.buf])
                         return xc__set_error(XC_EINVAL, "output capacity too small");
                     std::memcpy(out + out_off[it.buf] + out_len[it.buf], &obuf[ooff[k]], keep);
                     out_len[it.buf] += keep;
                     if (E.pos != ~0ull) {
-                        Item r = it;
+                        CItem r = it;
                         r.data = it.data + E.base;
                         r.len = it.len - E.base;
+                        r.off = it.off + E.base;
                         if (E.kind == 0) {  // after a declaration: its lookup at the same position is next
                             r.start = 2 * SEG - 1 - SEG;  // window end 2047 of the rest: not looked up yet
                             r.cand = -1;
@@ -851,6 +855,9 @@ extern "C" int xc_coss_encode_batch_host(xc_coss *c, const uint8_t *in, const ui
                             r.cand = E.cand >= 0 ? E.cand - (int64_t)E.base : -1;
                         }
                         next.push_back(r);
+                    } else {  // flush()'s declaration ended the item: source_ is empty
+                        res_base[it.buf] = it.off + it.len;
+                        res_cand[it.buf] = -1;
                     }
                     for (uint64_t k2 = k + 1; k2 < m; k2++) next.push_back(items[k2]);
                     redo = true;
@@ -861,13 +868,78 @@ extern "C" int xc_coss_encode_batch_host(xc_coss *c, const uint8_t *in, const ui
                         return xc__set_error(XC_EINVAL, "output capacity too small");
                     std::memcpy(out + out_off[it.buf] + out_len[it.buf], &obuf[ooff[k]], olen[k]);
                     out_len[it.buf] += olen[k];
+                    res_base[it.buf] = it.off + rbase[k];
+                    res_cand[it.buf] = rcand[k] >= 0 ? (int64_t)it.off + rcand[k] : -1;
                 }
             }
             for (const Change &h : held)
                 if ((rc = mirror(c, h))) return rc;
             items.swap(next);
         }
-        return XC_OK;
+        }
+    }
+    return XC_OK;
+}
+}  // namespace
+
+// Encoder batch over the COSS cache: buffer i is one encode()+flush() on a fresh encoder, buffers
+// in index order (xc_encode_batch_host's semantics), the COSS state advanced exactly as the
+// reference's would be.
+extern "C" int xc_coss_encode_batch_host(xc_coss *c, const uint8_t *in, const uint64_t *in_off,
+                                         const uint64_t *in_len, uint64_t nbuf, uint8_t *out,
+                                         const uint64_t *out_off, const uint64_t *out_cap, uint64_t *out_len)
+{
+    if (!c || !c->cache || (nbuf && (!in || !in_off || !in_len || !out || !out_off || !out_cap || !out_len)))
+        return xc__set_error(XC_EINVAL, "null (or a host-only COSS store)");
+    try {
+        std::vector<CItem> items;
+        for (uint64_t i = 0; i < nbuf; i++) {
+            items.push_back({i, in + in_off[i], in_len[i], 0, -1, 0, false});
+            out_len[i] = 0;
+        }
+        std::vector<uint64_t> rb(nbuf);
+        std::vector<int64_t> rc(nbuf);
+        return coss_encode(c, std::move(items), out, out_off, out_cap, out_len, rb.data(), rc.data());
+    } catch (const std::bad_alloc &) {
+        return xc__set_error(XC_ENOMEM, "host allocation failed");
+    }
+}
+
+// Internal (xc_stream.cpp, xc_coss_encode_streams): xc__encode_gather's contract over the COSS
+// cache: item i is head[i] (an encoder's source_) then tail[i] (its new input), with stream state
+// start / cand / flags (SF_NOFLUSH: encode() only); `take` receives each item's output and input
+// after rbase / rcand are set.
+extern "C" int xc__coss_encode_gather(xc_coss *c, uint64_t nbuf, const uint8_t *const *head, const uint64_t *head_len,
+                                      const uint8_t *const *tail, const uint64_t *tail_len, const uint64_t *start,
+                                      const int64_t *cand, const uint32_t *flags, uint64_t *rbase, int64_t *rcand,
+                                      int (*take)(void *ctx, uint64_t i, const uint8_t *out, uint64_t out_len,
+                                                  const uint8_t *in),
+                                      void *ctx)
+{
+    if (!c || !c->cache || (nbuf && (!head || !head_len || !tail || !tail_len || !start || !cand || !flags || !rbase ||
+                                     !rcand || !take)))
+        return xc__set_error(XC_EINVAL, "null (or a host-only COSS store)");
+    try {
+        std::vector<std::vector<uint8_t>> data(nbuf);
+        std::vector<uint64_t> ooff(nbuf), ocap(nbuf), olen(nbuf, 0);
+        std::vector<CItem> items;
+        uint64_t osz = 0;
+        for (uint64_t i = 0; i < nbuf; i++) {
+            data[i].resize(head_len[i] + tail_len[i]);
+            if (head_len[i]) std::memcpy(data[i].data(), head[i], head_len[i]);
+            if (tail_len[i]) std::memcpy(data[i].data() + head_len[i], tail[i], tail_len[i]);
+            ooff[i] = osz;
+            ocap[i] = 2 * data[i].size() + 16;
+            osz += ocap[i];
+            if (start[i] > data[i].size() || cand[i] < -1 ||
+                (cand[i] >= 0 && ((uint64_t)cand[i] + SEG > start[i] || (uint64_t)cand[i] + 2 * SEG - 1 < start[i])))
+                return xc__set_error(XC_EINVAL, "invalid stream state");
+            items.push_back({i, data[i].data(), data[i].size(), start[i], cand[i], 0, (flags[i] & 1u) != 0});
+        }
+        std::vector<uint8_t> obuf(std::max<uint64_t>(osz, 1));
+        int rc = coss_encode(c, std::move(items), obuf.data(), ooff.data(), ocap.data(), olen.data(), rbase, rcand);
+        for (uint64_t i = 0; i < nbuf && !rc; i++) rc = take(ctx, i, obuf.data() + ooff[i], olen[i], data[i].data());
+        return rc;
     } catch (const std::bad_alloc &) {
         return xc__set_error(XC_ENOMEM, "host allocation failed");
     }

@@ -943,11 +943,12 @@ __device__ __forceinline__ bool walk_blocks(const WalkArgs &a, uint32_t b, WalkS
             if ((uint32_t)__popcll(ballot(aligned)) != want) ok = false;  // each aligned end, once
         }
     }
+    const bool wave_fail = ballot(!ok) != 0;  // (every lane's verdict: ballots run on all lanes)
     n_ext = wave_sum(n_ext);
     n_ref = wave_sum(n_ref);
     const bool any_cross = ballot(cross) != 0;
     if (l == 0) {
-        if (ballot(!ok)) atomicOr(&sh.fail, 1u);
+        if (wave_fail) atomicOr(&sh.fail, 1u);
         if (any_cross) atomicOr(&sh.cross, 1u);
         atomicAdd(&sh.n_ext, n_ext);
         atomicAdd(&sh.n_ref, n_ref);

@@ -28,6 +28,14 @@ extern "C" int xc__encode_gather(xc_cache *c, uint64_t nbuf, const uint8_t *cons
                                              const uint8_t *in),
                                  void *ctx);
 
+extern "C" int xc__coss_encode_gather(xc_coss *c, uint64_t nbuf, const uint8_t *const *head,
+                                      const uint64_t *head_len, const uint8_t *const *tail, const uint64_t *tail_len,
+                                      const uint64_t *start, const int64_t *cand, const uint32_t *flags,
+                                      uint64_t *rbase, int64_t *rcand,
+                                      int (*take)(void *ctx, uint64_t i, const uint8_t *out, uint64_t out_len,
+                                                  const uint8_t *in),
+                                      void *ctx);
+
 namespace {
 constexpr uint64_t MAX_BUFFER = 1u << 20;  // longest device batch item (xc_kernels.h MAX_BUF)
 constexpr uint32_t SF_NOFLUSH = 1u;        // xc_kernels.h
@@ -68,15 +76,19 @@ struct Item {
 };
 }  // namespace
 
-static int encode_streams(xc_encoder *const *enc, const uint8_t *const *in, const uint64_t *in_len,
+// coss: the encoders' cache is that COSS cache's device mirror, and the batches run through the
+// COSS replay (xc__coss_encode_gather); else the memory cache (xc__encode_gather).
+static int encode_streams(xc_coss *coss, xc_encoder *const *enc, const uint8_t *const *in, const uint64_t *in_len,
                           const uint32_t *flags, uint64_t n, uint8_t *out, const uint64_t *out_off,
                           const uint64_t *out_cap, uint64_t *out_len)
 {
     if (n && (!enc || !in_len || !out || !out_off || !out_cap || !out_len)) return xc__set_error(XC_EINVAL, "null");
-    xc_cache *cache = n ? enc[0]->cache : nullptr;
+    xc_cache *cache = coss ? xc_coss_cache(coss) : n ? enc[0]->cache : nullptr;
     for (uint64_t k = 0; k < n; k++) {
         if (!enc[k]) return xc__set_error(XC_EINVAL, "null encoder");
-        if (enc[k]->cache != cache) return xc__set_error(XC_EINVAL, "encoders of one call must share a cache");
+        if (enc[k]->cache != cache)
+            return xc__set_error(XC_EINVAL, coss ? "encoder not created on this COSS cache (xc_coss_cache)"
+                                                 : "encoders of one call must share a cache");
         if (in_len[k] && (!in || !in[k])) return xc__set_error(XC_EINVAL, "null input");
         out_len[k] = 0;
     }
@@ -151,8 +163,11 @@ static int encode_streams(xc_encoder *const *enc, const uint8_t *const *in, cons
             t.done[k] += (*t.items)[i].take;
             return XC_OK;
         };
-        int rc = xc__encode_gather(cache, m, head.data(), hlen.data(), tail.data(), tlen.data(), start.data(),
-                                   cand.data(), fl.data(), rbase.data(), rcand.data(), take, &tk);
+        int rc = coss ? xc__coss_encode_gather(coss, m, head.data(), hlen.data(), tail.data(), tlen.data(),
+                                               start.data(), cand.data(), fl.data(), rbase.data(), rcand.data(), take,
+                                               &tk)
+                      : xc__encode_gather(cache, m, head.data(), hlen.data(), tail.data(), tlen.data(), start.data(),
+                                          cand.data(), fl.data(), rbase.data(), rcand.data(), take, &tk);
         if (rc) return rc;
         // calls fully done advance the start of the next round
         k0 = items.back().call + (done[items.back().call] == in_len[items.back().call] ? 1 : 0);
@@ -165,7 +180,21 @@ extern "C" int xc_encode_streams(xc_encoder *const *enc, const uint8_t *const *i
                                  const uint64_t *out_cap, uint64_t *out_len)
 {
     try {  // no exception crosses the C ABI
-        return encode_streams(enc, in, in_len, flags, n, out, out_off, out_cap, out_len);
+        return encode_streams(nullptr, enc, in, in_len, flags, n, out, out_off, out_cap, out_len);
+    } catch (const std::bad_alloc &) {
+        return xc__set_error(XC_ENOMEM, "host allocation failed");
+    } catch (const std::exception &x) {
+        return xc__set_error(XC_EINVAL, x.what());
+    }
+}
+
+extern "C" int xc_coss_encode_streams(xc_coss *c, xc_encoder *const *enc, const uint8_t *const *in,
+                                      const uint64_t *in_len, const uint32_t *flags, uint64_t n, uint8_t *out,
+                                      const uint64_t *out_off, const uint64_t *out_cap, uint64_t *out_len)
+{
+    if (!c || !xc_coss_cache(c)) return xc__set_error(XC_EINVAL, "null (or a host-only COSS store)");
+    try {
+        return encode_streams(c, enc, in, in_len, flags, n, out, out_off, out_cap, out_len);
     } catch (const std::bad_alloc &) {
         return xc__set_error(XC_ENOMEM, "host allocation failed");
     } catch (const std::exception &x) {

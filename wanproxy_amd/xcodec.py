@@ -38,7 +38,7 @@ SYMBOLS = [
     "xc_hash_segments_host", "xc_cache_capacity",
     "xc_coss_open", "xc_coss_close", "xc_coss_cache", "xc_coss_count", "xc_coss_stats", "xc_coss_lookup",
     "xc_coss_enter", "xc_coss_encode_batch_host", "xc_coss_decode_batch_host", "xc_coss_store_lookup",
-    "xc_coss_store_enter",
+    "xc_coss_store_enter", "xc_coss_encode_streams",
 ]
 STREAM_FLUSH = 1  # XC_STREAM_FLUSH
 
@@ -152,6 +152,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     for name in ("xc_coss_enter", "xc_coss_store_enter"):
         getattr(lib, name).argtypes = [_vp, C.c_uint64, _u8p]
     lib.xc_coss_encode_batch_host.argtypes = lib.xc_encode_batch_host.argtypes
+    lib.xc_coss_encode_streams.argtypes = [_vp] + list(lib.xc_encode_streams.argtypes)
     lib.xc_coss_decode_batch_host.argtypes = lib.xc_decode_batch_host.argtypes
     _LIB = lib
     return lib
@@ -380,10 +381,12 @@ class XCodecStreamEncoder:
     ``flush()`` returns ``(bool, bytes)`` like ``flush(out)``.  :func:`encode_streams` runs the
     calls of many encoders as one device batch."""
 
-    def __init__(self, cache: XCodecCache):
+    def __init__(self, cache):
         self.cache = cache
         self.h = _vp()
-        _check(load_library().xc_encoder_create(cache.h, C.byref(self.h)))
+        # over a COSS cache: the encoder works on its device mirror, encode_streams on the COSS cache
+        ch = _vp(load_library().xc_coss_cache(cache.h)) if isinstance(cache, CossCache) else cache.h
+        _check(load_library().xc_encoder_create(ch, C.byref(self.h)))
         _LIVE["plan"].add(self)
 
     def _ctx(self):
@@ -399,6 +402,9 @@ class XCodecStreamEncoder:
         return encode_streams([(self, data, False)])[0]
 
     def flush(self) -> tuple[bool, bytes]:
+        if isinstance(self.cache, CossCache):  # (the COSS state follows the flush's events)
+            out = encode_streams([(self, b"", True)])[0]
+            return len(out) > 0, out
         cap = 2 * self.pending + 16
         out = np.zeros(cap, np.uint8)
         n, em = C.c_uint64(), C.c_int()
@@ -457,7 +463,13 @@ def encode_streams(calls) -> list[bytes]:
     olen = np.zeros(n, np.uint64)
     encs = (_vp * n)(*[e.h for e, _, _ in calls])
     ptrs = (C.c_void_p * n)(*[d.ctypes.data if d.size else None for d in datas])
-    _check(load_library().xc_encode_streams(encs, ptrs, lens, flags, n, out, off, cap, olen))
+    c0 = calls[0][0].cache
+    if isinstance(c0, CossCache):
+        if any(e.cache is not c0 for e, _, _ in calls):
+            raise XCodecError("encode_streams: the encoders of one call share one cache")
+        _check(load_library().xc_coss_encode_streams(c0.h, encs, ptrs, lens, flags, n, out, off, cap, olen))
+    else:
+        _check(load_library().xc_encode_streams(encs, ptrs, lens, flags, n, out, off, cap, olen))
     return [out[int(o):int(o) + int(m)].tobytes() for o, m in zip(off, olen)]
 
 
