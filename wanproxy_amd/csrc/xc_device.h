@@ -387,8 +387,9 @@ __device__ __forceinline__ void wave_copy_payload(uint8_t *out, uint8_t *seg, co
 #define XC_FILT_WORDS 36864u  // in 32-bit words (a multiple of 4096)
 #define XC_EMPTY64 0xFFFFFFFFFFFFFFFFull           // H never has bits 32..35 set
 
-// Level-2 filter: a blocked k=2 Bloom filter of 2^18 64-bit words (2 MB, sized to stay in an
-// XCD's L2) keyed by a remix of lo32, independent of the level-1 bits.
+// Level-2 filter: a blocked k=2 Bloom filter of 2^19 32-bit words (2 MB, sized to stay in an
+// XCD's L2) keyed by a remix g of lo32, independent of the level-1 bits: word g >> 13, bits g[4:0]
+// and g[9:5] (one 4-byte read per test).  XC_L2_WORDS counts 8-byte units of its storage.
 #define XC_L2_WORDS (1u << 18)
 
 __device__ __forceinline__ uint32_t l2_mix(uint32_t lo)
@@ -397,9 +398,10 @@ __device__ __forceinline__ uint32_t l2_mix(uint32_t lo)
     return g ^ (g >> 12);
 }
 
-__device__ __forceinline__ bool l2_test(uint2 w, uint32_t g)
+__device__ __forceinline__ uint32_t l2_word(uint32_t g) { return g >> 13; }
+__device__ __forceinline__ bool l2_test(uint32_t w, uint32_t g)
 {
-    return ((w.x >> (g & 31u)) & (w.y >> ((g >> 5) & 31u)) & 1u) != 0u;
+    return ((w >> (g & 31u)) & (w >> ((g >> 5) & 31u)) & 1u) != 0u;
 }
 
 struct DevSet {
@@ -487,9 +489,8 @@ __device__ __forceinline__ int set_insert(const DevSet &s, uint64_t h, uint64_t 
     {
         const uint32_t lo = (uint32_t)h;
         atomicOr(&s.filt[filt_word(lo)], (1u << (lo & 31u)) | (1u << ((lo >> 5) & 31u)));
-        const uint32_t g = l2_mix(lo), gi = (g >> 14) * 2u;
-        atomicOr(&s.l2[gi], 1u << (g & 31u));
-        atomicOr(&s.l2[gi + 1u], 1u << ((g >> 5) & 31u));
+        const uint32_t g = l2_mix(lo);
+        atomicOr(&s.l2[l2_word(g)], (1u << (g & 31u)) | (1u << ((g >> 5) & 31u)));
     }
     uint32_t i = key_slot(h, s.mask);
     int fresh = 0;

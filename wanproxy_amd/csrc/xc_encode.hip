@@ -83,7 +83,7 @@ struct Pending {
     uint32_t n;          // entries (uniform); 0 = nothing pending
     uint32_t c, c0;      // chunk the entries belong to
     uint32_t pos[2], lo[2];
-    uint2 w[2];
+    uint32_t w[2];
 };
 
 __device__ __forceinline__ void pend_issue(const ScanArgs &a, Pending &pd, const uint2 *queue, uint32_t qn,
@@ -101,7 +101,7 @@ __device__ __forceinline__ void pend_issue(const ScanArgs &a, Pending &pd, const
         const bool v = i < qn;
         pd.pos[s] = v ? e.x : 0u;
         pd.lo[s] = v ? e.y : 0u;
-        pd.w[s] = a.l2[v ? l2_mix(e.y) >> 14 : 0u];
+        pd.w[s] = a.l2[v ? l2_word(l2_mix(e.y)) : 0u];
     }
 }
 
@@ -187,6 +187,12 @@ __device__ __forceinline__ const uint8_t *desc_base(const ScanArgs &a, const uin
 {
     return a.P.in + (((uint64_t)uniform(d.w) << 32) | uniform(d.z));
 }
+
+// A half-iteration with more level-1 positives than this probes the level-2 filter directly from
+// every lane (one round trip) instead of queueing them for the next iteration's batch.
+#ifndef XC_DIRECT_MIN
+#define XC_DIRECT_MIN Q_CAP
+#endif
 
 template <int MODE>
 __global__ __launch_bounds__(64 * SCAN_WAVES) void k_scan(ScanArgs a)
@@ -312,8 +318,7 @@ __global__ __launch_bounds__(64 * SCAN_WAVES) void k_scan(ScanArgs a)
                 const uint32_t cnt = (uint32_t)__popc(hit);
                 const uint32_t incl = wave_incl_scan(cnt);
                 const uint32_t tot = readlane(incl, 63);
-                if (tot && qn + tot > Q_CAP) scan_flush<MODE>(a, queue, qn, c, c0, ev_n, dense);
-                if (tot && tot <= Q_CAP) {
+                if (tot && qn + tot <= Q_CAP && tot <= XC_DIRECT_MIN) {
                     // lane-parallel append: this lane's hits go to [qn + excl, qn + excl + cnt);
                     // (offsets j unrolled: lo[j] stays a static register)
                     uint32_t slot = qn + incl - cnt;
@@ -326,14 +331,29 @@ __global__ __launch_bounds__(64 * SCAN_WAVES) void k_scan(ScanArgs a)
                     }
                     qn += tot;
                 } else if (tot) {
-#pragma unroll 1
-                    for (uint32_t j = 0; j < 16u; j++) {
-                        const bool t = (hit >> j) & 1u;
-                        const uint64_t m = ballot(t);
-                        if (m) {
-                            if (t) queue[qn + mbcnt(m)] = make_uint2(q + 16u * half + j, lo[j]);
-                            qn = uniform(qn + (uint32_t)__popcll(m));
-                            if (qn > Q_CAP - 64u) scan_flush<MODE>(a, queue, qn, c, c0, ev_n, dense);
+                    // more positives than the queue holds (a dense filter late in a run): every
+                    // lane probes its own level-2 words directly, all loads in flight before the
+                    // first test (one round trip for the half instead of a flush per 128)
+                    if (MODE == 4) {
+                        sink = sink * 31u + hit;
+                    } else {
+#pragma unroll
+                        for (int g0 = 0; g0 < 16; g0 += 8) {  // (two groups of 8: registers)
+                            uint32_t w2[8];
+#pragma unroll
+                            for (int j = 0; j < 8; j++) {
+                                w2[j] = 0u;
+                                if ((hit >> (g0 + j)) & 1u) w2[j] = a.l2[l2_word(l2_mix(lo[g0 + j]))];
+                            }
+#pragma unroll
+                            for (int j = 0; j < 8; j++) {
+                                const bool pass = ((hit >> (g0 + j)) & 1u) && l2_test(w2[j], l2_mix(lo[g0 + j]));
+                                if (ballot(pass)) {  // (rare: level-2 survivors)
+                                    const bool match =
+                                        pass && (MODE == 5 ? lo[g0 + j] == 0x12345u : scan_has_lo(a, lo[g0 + j]));
+                                    scan_record(a, c, c0, match, q + 16u * half + (uint32_t)(g0 + j), ev_n, dense);
+                                }
+                            }
                         }
                     }
                 }

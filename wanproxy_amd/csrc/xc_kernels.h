@@ -157,7 +157,7 @@ struct ScanArgs {
     uint32_t mode;  // ablation (timing only): 0 full, 1 no filter test, 2 loads + block sums only
     DevSet set2;    // optional second set tested in the same pass (predicted declarations)
     int has2;
-    const uint2 *l2;  // level-2 filter of set (| set2): one 8-byte L2 read per level-1 positive
+    const uint32_t *l2;  // level-2 filter of set (| set2): one 4-byte L2 read per level-1 positive
     int shadow;       // skip the windows in the shadow of predicted REFs (P.blk_pref)
     uint32_t unit;    // chunks per work unit (the plan's scan granularity, <= SCAN_UNIT)
     const uint32_t *filt;  // level-1 image (set's filter, or P.fmix for set | set2), filt_words words

@@ -1260,12 +1260,12 @@ static int launch_scan(xc_plan *p, const Layer &L, const DevSet &set, uint32_t c
 {
     if (ck_hi <= ck_lo) return XC_OK;
     xc_ctx *ctx = p->cache->ctx;
-    ScanArgs a{p->P, L, set, ck_lo, ck_hi, 0, DevSet{}, 0, (const uint2 *)set.l2, shadow, p->scan_unit,
+    ScanArgs a{p->P, L, set, ck_lo, ck_hi, 0, DevSet{}, 0, (const uint32_t *)set.l2, shadow, p->scan_unit,
                set.filt, XC_FILT_WORDS};
     if (set2) {
         a.set2 = *set2;
         a.has2 = 1;
-        a.l2 = (const uint2 *)p->d_l2mix;  // cache | set2, built by k_clear_set + k_blockhash
+        a.l2 = (const uint32_t *)p->d_l2mix;  // cache | set2, built by k_clear_set + k_blockhash
         a.filt = p->d_fmix;               // the same for level 1, folded
         a.filt_words = XC_FILT_WORDS >> p->P.fmix_fold;
     }
@@ -1814,7 +1814,7 @@ extern "C" double xc__scan_ablation(xc_plan *p, const uint8_t *d_in, int mode, i
     xc_ctx *ctx = p->cache->ctx;
     hipSetDevice(ctx->dev);
     p->P.in = d_in;
-    ScanArgs a{p->P, p->P.S, p->P.cache, 0, p->nchunks, (uint32_t)mode, DevSet{}, 0, (const uint2 *)p->P.cache.l2, 0,
+    ScanArgs a{p->P, p->P.S, p->P.cache, 0, p->nchunks, (uint32_t)mode, DevSet{}, 0, (const uint32_t *)p->P.cache.l2, 0,
                p->scan_unit, p->P.cache.filt, XC_FILT_WORDS};
     uint32_t need = (p->nchunks + SCAN_WAVES * p->scan_unit - 1) / (SCAN_WAVES * p->scan_unit);
     uint32_t grid = std::min<uint32_t>(need, (uint32_t)ctx->n_cu);
