@@ -748,6 +748,11 @@ __device__ __forceinline__ void walk_seq(const WalkArgs &a, uint32_t b, uint64_t
         if (!a.use_d) return s;
         return event_at(P, P.D, cd, ck1, q, 1, b, base);
     };
+    // A candidate whose hash a declaration-set match supplies: 1, or 2 when the entry is a later
+    // buffer's (its predicted declaration of the same bytes): this buffer declares them first, so
+    // the set must hold this buffer's declaration (decl_hash enters it and asks for another round,
+    // in which that later buffer sees it as an earlier buffer's declaration: a cross-buffer case).
+    auto known_of = [&](const EvInfo &d) -> uint32_t { return (uint32_t)(d.v >> 32) > b ? 2u : 1u; };
     uint32_t n_coll = 0;
     // a lookup hit with other bytes: record it, with the candidate pending then (NONE: none)
     auto coll = [&](uint32_t q, uint64_t h) {
@@ -776,7 +781,7 @@ __device__ __forceinline__ void walk_seq(const WalkArgs &a, uint32_t b, uint64_t
     if (cand >= 0) {  // the carried candidate's hash, when a resolved event supplies it
         const uint32_t q = (uint32_t)cand + XC_SEG - 1u;
         const EvInfo d = decl_info(q, event_at(P, P.S, cs, ck1, q, 2, b, base));
-        if (d.st == ST_MATCH) { cand_known = 1; cand_h = d.h; }
+        if (d.st == ST_MATCH) { cand_known = known_of(d); cand_h = d.h; }
     }
     while (p < len) {
         if (cand < 0) {
@@ -794,7 +799,7 @@ __device__ __forceinline__ void walk_seq(const WalkArgs &a, uint32_t b, uint64_t
             cand_h = 0;
             {
                 const EvInfo d = decl_info(p, event_at(P, P.S, cs, ck1, p, 2, b, base));
-                if (d.st == ST_MATCH) { cand_known = 1; cand_h = d.h; }
+                if (d.st == ST_MATCH) { cand_known = known_of(d); cand_h = d.h; }
             }
             p++;
             continue;
@@ -997,7 +1002,8 @@ __device__ __forceinline__ bool walk_blocks(const WalkArgs &a, uint32_t b, WalkS
 // ------------------------------------------------------------ k_walk ---------------------
 // The EXTRACT tokens of buffer b whose hash no resolved event supplied are hashed and entered
 // into the declaration set (value = b<<32 | declaration position, min-merged); any such entry
-// means the scan missed it: another round.
+// means the scan missed it: another round.  So are the declarations whose hash came from a later
+// buffer's entry (tok_known 2): their min-merged value moves to this buffer.
 __device__ __forceinline__ void decl_hash(const PlanDev &P, uint32_t b)
 {
     const uint32_t l = lane_id();
@@ -1005,11 +1011,14 @@ __device__ __forceinline__ void decl_hash(const PlanDev &P, uint32_t b)
     const uint32_t tb = P.tok_base[b], n = P.tok_cnt[b];
     for (uint32_t t0 = 0; t0 < n; t0 += 64u) {
         const uint32_t t = t0 + l;
-        const bool unknown = t < n && P.tok_op[tb + t] == OP_EXTRACT && !P.tok_known[tb + t];
+        const bool unknown = t < n && P.tok_op[tb + t] == OP_EXTRACT && P.tok_known[tb + t] != 1u;
         for (uint64_t m = ballot(unknown); m; m &= m - 1) {
             const uint32_t tt = tb + t0 + (uint32_t)(__ffsll((unsigned long long)m) - 1);
             const uint32_t seg = uniform(P.tok_seg[tt]);
-            const uint64_t h = wave_window_hash(base + seg);
+            const bool known = uniform(P.tok_known[tt]) != 0u;
+            const uint64_t h = known ? ((uint64_t)uniform((uint32_t)(P.tok_h[tt] >> 32)) << 32) |
+                                           uniform((uint32_t)P.tok_h[tt])
+                                     : wave_window_hash(base + seg);
             if (l == 0) {
                 P.tok_h[tt] = h;
                 const uint64_t v = ((uint64_t)b << 32) | P.tok_dpos[tt];
