@@ -21,8 +21,12 @@ def _collision_pair(seed):
     return x, y
 
 
-def _batch(rng, pool):
+def _batch(rng, pool, pair=True):
+    """pair=False: only one half of the collision pair (stateful streams: see DESIGN.md §8 on a
+    declaration of a hash another connection entered with other bytes since the lookup)."""
     x, y = _collision_pair(int(rng.integers(1 << 30)))
+    if not pair:
+        y = x
     pieces = []
     bufs = []
     for _ in range(int(rng.integers(8, 48))):
