@@ -498,11 +498,14 @@ __global__ __launch_bounds__(256) void k_resolve(ResolveArgs a)
     const bool aligned = live && ((q + 1u) & (XC_SEG - 1u)) == 0u && P.blk_h;
     const bool pref_ok = a.dmode == 2 && !stream_carried(P, ck.x);
     uint64_t h = 0;
-    uint32_t pref = 0;
+    uint32_t pref = 0, bcmp = 0;
     if (aligned) {
         const uint32_t gi = P.chunk_blk[c] + (q + 1u) / XC_SEG - 1u;
         h = P.blk_h[gi];
-        if (pref_ok) pref = P.blk_pref[gi];
+        if (pref_ok) {
+            pref = P.blk_pref[gi];
+            bcmp = P.blk_cmp[gi];
+        }
     }
     for (uint64_t m = ballot(live && !aligned); m; m &= m - 1) {
         const int f = __ffsll((unsigned long long)m) - 1;
@@ -514,9 +517,11 @@ __global__ __launch_bounds__(256) void k_resolve(ResolveArgs a)
     uint64_t v = 0;
     uint32_t st = ST_MISS;
     const bool known = pref != 0u;  // (aligned and pref_ok)
+    bool compared = false;  // k_blockhash compared the block with the same cached segment
     if (known) {
         if (blk_cached(pref)) {
-            st = ST_EQUAL;  // (until the comparison below)
+            compared = bcmp != 0u && (bcmp & ~BC_DIFF) == pref;
+            st = compared && (bcmp & BC_DIFF) ? ST_COLL : ST_EQUAL;  // (else until the comparison below)
             v = pref - 1u;
         } else {
             st = ST_MATCH;
@@ -529,7 +534,7 @@ __global__ __launch_bounds__(256) void k_resolve(ResolveArgs a)
         else v = 0;
     }
     // 2048-byte comparisons against the cached segments: up to 4 per pass, all loads in flight
-    for (uint64_t m = ballot(st == ST_EQUAL); m;) {
+    for (uint64_t m = ballot(st == ST_EQUAL && !compared); m;) {
         int f[4];
         uint32_t x[4][8], y[4][8];
 #pragma unroll
@@ -1056,7 +1061,8 @@ constexpr uint32_t BLK_GROUP = 8;
 // predicted declarations (hit-free data declares exactly these, xcodec_encoder.cc:77-82); they
 // enter the declaration set and the combined level-2 filter before the scan.  Cached blocks are
 // predicted REFs (REF shadows).
-__device__ __forceinline__ void block_predict(const PlanDev &P, uint32_t g, uint32_t b, uint32_t k, uint64_t h);
+// Returns the prediction (blk_pref).
+__device__ __forceinline__ uint32_t block_predict(const PlanDev &P, uint32_t g, uint32_t b, uint32_t k, uint64_t h);
 
 // predict: also the predictions of these blocks (the run's first sub-batch, hashed in line after
 // the declaration set's clear: one kernel instead of two)
@@ -1072,11 +1078,47 @@ __global__ __launch_bounds__(256) void k_blockhash(DeclArgs a)
     const uint32_t n = min(BLK_GROUP, P.buf_len[b] / XC_SEG - k0);
     const uint64_t h = wave_block_hashes<BLK_GROUP>(base + (size_t)k0 * XC_SEG, n);
     const uint32_t l = lane_id();
+    const uint32_t gi = P.blk_base[b] + k0 + l;
+    uint32_t cmp = 0;  // the cached slot + 1 to compare the block with (blk_cmp)
     if (l < n) {
-        const uint32_t gi = P.blk_base[b] + k0 + l;
         P.blk_h[gi] = h;
-        if (PREDICT) block_predict(P, gi, b, k0 + l, h);
+        if (PREDICT) {
+            const uint32_t pref = block_predict(P, gi, b, k0 + l, h);
+            if (blk_cached(pref)) cmp = pref;
+        } else if (a.limit && !stream_carried(P, b)) {
+            // (a concurrent k_alloc may be entering keys: only complete entries are compared)
+            uint64_t v;
+            if (set_find(P.cache, h, &v) && (uint32_t)v < *a.limit) cmp = (uint32_t)v + 1u;
+        }
     }
+    // the compares of a predicted REF's bytes, off k_resolve's critical path: four blocks per
+    // pass, all loads in flight (both sides 16-byte aligned)
+    uint32_t verdict = cmp;
+    for (uint64_t m = ballot(cmp != 0u); m;) {
+        int f[4];
+        uint4 x[4][2], y[4][2];
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            f[g] = m ? __ffsll((unsigned long long)m) - 1 : -1;
+            if (m) m &= m - 1;
+            if (f[g] >= 0) {
+                const uint32_t slot = readlane(cmp, f[g]) - 1u;
+                const uint4 *xp = (const uint4 *)(base + (size_t)(k0 + f[g]) * XC_SEG + 32u * l);
+                const uint4 *yp = (const uint4 *)(P.segs + (size_t)slot * XC_SEG + 32u * l);
+                x[g][0] = xp[0]; x[g][1] = xp[1];
+                y[g][0] = yp[0]; y[g][1] = yp[1];
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            if (f[g] < 0) continue;
+            const uint32_t diff = (x[g][0].x ^ y[g][0].x) | (x[g][0].y ^ y[g][0].y) | (x[g][0].z ^ y[g][0].z) |
+                                  (x[g][0].w ^ y[g][0].w) | (x[g][1].x ^ y[g][1].x) | (x[g][1].y ^ y[g][1].y) |
+                                  (x[g][1].z ^ y[g][1].z) | (x[g][1].w ^ y[g][1].w);
+            if (ballot(diff != 0u) && (int)l == f[g]) verdict |= BC_DIFF;
+        }
+    }
+    if (l < n) P.blk_cmp[gi] = verdict;
 }
 template __global__ void k_blockhash<false>(DeclArgs);
 template __global__ void k_blockhash<true>(DeclArgs);
@@ -1092,23 +1134,23 @@ __global__ __launch_bounds__(256) void k_blockpredict(DeclArgs a)
     block_predict(P, g, b, k, P.blk_h[g]);
 }
 
-__device__ __forceinline__ void block_predict(const PlanDev &P, uint32_t g, uint32_t b, uint32_t k, uint64_t h)
+__device__ __forceinline__ uint32_t block_predict(const PlanDev &P, uint32_t g, uint32_t b, uint32_t k, uint64_t h)
 {
-    if (stream_carried(P, b)) {  // blocks relative to a carried source_: no predictions
-        P.blk_pref[g] = 0u;
-        return;
-    }
+    uint32_t pref = 0u;  // blocks relative to a carried source_: no predictions
     uint64_t v;
-    if (set_find(P.cache, h, &v)) {
-        P.blk_pref[g] = (uint32_t)v + 1u;  // (cache capacity <= 2^23)
+    if (stream_carried(P, b)) {
+    } else if (set_find(P.cache, h, &v)) {
+        pref = (uint32_t)v + 1u;  // (cache capacity <= 2^23)
     } else {
         // (the set's level-2 filter is P.l2mix, the combined filter the scan reads)
         uint32_t slot;
         set_insert(P.dset, h, ((uint64_t)b << 32) | (k * XC_SEG + 2u * XC_SEG - 1u), true, &slot, nullptr);
         const uint32_t lo = (uint32_t)h;  // (the combined level-1 image the first scan loads)
         atomicOr(&P.fmix[filt_word_n(lo, XC_FILT_WORDS >> P.fmix_fold)], (1u << (lo & 31u)) | (1u << ((lo >> 5) & 31u)));
-        P.blk_pref[g] = BP_DECL | slot;
+        pref = BP_DECL | slot;
     }
+    P.blk_pref[g] = pref;
+    return pref;
 }
 
 // -------------------------------------------------------------- k_emit ------------------
@@ -1455,10 +1497,12 @@ __global__ __launch_bounds__(64) void k_window_hashes(const uint8_t *in, uint32_
 // Clear a declaration set (all of its tables) and seed the combined level-2 filter with the
 // cache's: one launch instead of a memset per table.
 __global__ void k_clear_set(DevSet s, uint32_t n_lo, uint32_t n_full, uint4 *l2mix, const uint4 *cache_l2,
-                            uint32_t *fmix, const uint32_t *cache_filt, uint32_t fold, uint32_t *ctl_zero)
+                            uint32_t *fmix, const uint32_t *cache_filt, uint32_t fold, const uint32_t *count,
+                            uint32_t *count_out, uint32_t *ctl_zero)
 {
     const uint32_t stride = gridDim.x * blockDim.x;
     const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
+    if (count_out && i0 == 0) *count_out = *count;  // (the sub-batch's start count: P.sb_count)
     // the first scan's level-1 image starts as the cache's, folded
     if (fmix)
         for (uint32_t i = i0; i < (XC_FILT_WORDS >> fold); i += stride) {

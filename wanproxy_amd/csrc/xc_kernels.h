@@ -107,6 +107,12 @@ struct PlanDev {
     //   0: no prediction (carried stream state).
     // k_resolve's first round takes the aligned windows' cache and D slots from here.
     uint32_t *blk_pref;
+    // The block hashing's verdict on aligned block g against the cache of the time (entries below
+    // the sub-batch's start count only: complete, and unchanged during the run): 0 none, else
+    // (cached slot + 1) | (0x80000000 when the bytes differ).  k_resolve skips the 2048-byte
+    // compare of a predicted REF whose slot it names.
+    uint32_t *blk_cmp;
+    uint32_t *sb_count;         // [sub-batches] the cache's count when the sub-batch started
     const uint32_t *chunk_blk;  // [nchunks] global index of the chunk's buffer's block 0
     // Stateful streams (xc_encode / xc_flush, xcodec_encoder.cc:60-201 across calls), or null
     // when every buffer is a fresh encoder's encode + flush.  stream_st[b] = {start, cand0,
@@ -126,6 +132,7 @@ struct PlanDev {
 constexpr uint32_t COLL_CAP = 16;
 constexpr uint32_t SF_NOFLUSH = 1u;
 constexpr uint32_t BP_DECL = 0x80000000u;  // blk_pref: predicted declaration | D slot
+constexpr uint32_t BC_DIFF = 0x80000000u;  // blk_cmp: the block differs from the cached segment
 __device__ __forceinline__ bool blk_cached(uint32_t pref) { return (int32_t)pref > 0; }
 // A buffer with carried-over state (earlier positions already looked up, or a pending
 // candidate): the aligned-block predictions and REF shadows do not apply to it.
@@ -184,6 +191,9 @@ __host__ __device__ constexpr uint32_t walk_lds_bytes(uint32_t max_decl) { retur
 struct DeclArgs {
     PlanDev P;
     uint32_t j0, j1;
+    // k_blockhash on the side stream: the cache count below which entries are complete while it
+    // runs (P.sb_count of the sub-batch the main stream is in); null: no block compares
+    const uint32_t *limit;
 };
 struct EmitArgs {
     PlanDev P;
@@ -214,8 +224,8 @@ __global__ void k_blockpredict(DeclArgs a);
 __global__ void k_or_words(uint4 *dst, const uint4 *a, const uint4 *b, uint32_t n);
 __global__ void k_alloc(EmitArgs a);
 __global__ void k_clear_set(DevSet s, uint32_t n_lo, uint32_t n_full, uint4 *l2mix, const uint4 *cache_l2,
-                            uint32_t *fmix, const uint32_t *cache_filt, uint32_t fold,
-                            uint32_t *ctl_zero);
+                            uint32_t *fmix, const uint32_t *cache_filt, uint32_t fold, const uint32_t *count,
+                            uint32_t *count_out, uint32_t *ctl_zero);
 __global__ void k_hash_segments(const uint8_t *segs, uint64_t n, uint64_t *out);
 __global__ void k_window_hashes(const uint8_t *in, uint32_t n, uint64_t *out);
 __global__ void k_undo(DevSet cache, const uint2 *undo, uint32_t from, uint32_t to);

@@ -1002,6 +1002,10 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     HIPCHK(dmalloc(&P.blk_h, std::max<uint64_t>(nblk, 1) * 8));
     HIPCHK(dmalloc(&P.blk_pref, std::max<uint64_t>(nblk, 1) * 4));
     HIPCHK(hipMemsetAsync(P.blk_pref, 0, std::max<uint64_t>(nblk, 1) * 4, s));
+    HIPCHK(dmalloc(&P.blk_cmp, std::max<uint64_t>(nblk, 1) * 4));
+    HIPCHK(hipMemsetAsync(P.blk_cmp, 0, std::max<uint64_t>(nblk, 1) * 4, s));
+    HIPCHK(dmalloc(&P.sb_count, p->sub.size() * 4));
+    HIPCHK(hipMemsetAsync(P.sb_count, 0, p->sub.size() * 4, s));
     {
         std::vector<uint32_t> cb(std::max<size_t>(chunks.size(), 1), 0);
         for (size_t k = 0; k < chunks.size(); k++) cb[k] = blk_base[chunks[k].x];
@@ -1089,6 +1093,8 @@ extern "C" int xc_plan_destroy(xc_plan *p)
     dfree(p->P.tok_known);
     dfree(p->P.blk_h);
     dfree(p->P.blk_pref);
+    dfree(p->P.blk_cmp);
+    dfree(p->P.sb_count);
     dfree(p->d_chunk_blk);
     dfree(p->d_blk_base);
     dfree(p->d_blk_buf);
@@ -1339,7 +1345,9 @@ static int enqueue_block_hash(xc_plan *p, uint32_t k, hipEvent_t after, hipStrea
     if (after) HIPCHK(hipStreamWaitEvent(st, after, 0));
     if (p->host_path) HIPCHK(hipStreamWaitEvent(st, p->ev_h2d[k], 0));  // its input has landed
     const uint32_t g0 = p->grp_base[p->sub[k]], g1 = p->grp_base[p->sub[k + 1]];
-    DeclArgs d{p->P, g0, g1};  // a range of block groups
+    // a range of block groups; on the side stream (sub-batch k - 1 on the main stream) the block
+    // compares against the entries complete when k - 1 started
+    DeclArgs d{p->P, g0, g1, side && k > 0 ? p->P.sb_count + (k - 1) : nullptr};
     // XC_ABL_SKIP_BLOCKHASH=1 (timing experiments only, valid when every run reads the same input):
     // the side stream's block hashing after the plan's first run is skipped
     static const bool skip = getenv("XC_ABL_SKIP_BLOCKHASH") && atoi(getenv("XC_ABL_SKIP_BLOCKHASH"));
@@ -1367,7 +1375,7 @@ static int launch_first_round(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t s1,
     // the set's clear (and, first in a run, the control words' clear)
     hipLaunchKernelGGL(k_clear_set, dim3(1024), dim3(256), 0, s, p->P.dset, p->dset.n_lo, p->dset.n_full,
                        (uint4 *)p->d_l2mix, (const uint4 *)p->P.cache.l2, p->d_fmix, (const uint32_t *)p->P.cache.filt,
-                       p->P.fmix_fold, p->zero_ctl ? p->P.ctl : nullptr);
+                       p->P.fmix_fold, p->P.seg_count, p->P.sb_count + sb, p->zero_ctl ? p->P.ctl : nullptr);
     HIPCHK(hipGetLastError());
     p->zero_ctl = false;
     const bool inline_hash = p->next_hash <= sb;
