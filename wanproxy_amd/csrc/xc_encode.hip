@@ -1196,6 +1196,8 @@ __device__ __forceinline__ uint32_t write_escaped(uint8_t *dst, const uint8_t *p
 }
 
 
+constexpr int EMIT_PAY = 2;  // payloads a wave has in flight
+
 template <uint32_t EMIT_WAVES>
 __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
 {
@@ -1295,25 +1297,25 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
             o[0] = (uint8_t)XC_MAGIC;
             o[1] = (uint8_t)OP_EXTRACT;
         }
-        // payloads to the wire and into the slots k_alloc reserved, two at a time
+        // payloads to the wire and into the slots k_alloc reserved, EMIT_PAY at a time
         for (uint64_t m = ballot(live && op == OP_EXTRACT); m;) {
-            const int f0 = __ffsll((unsigned long long)m) - 1;
-            m &= m - 1;
-            const int f1 = m ? __ffsll((unsigned long long)m) - 1 : -1;
-            if (m) m &= m - 1;
-            const uint32_t i0 = slot0 + ord[g0 + (uint32_t)f0];
-            uint8_t *d0 = out + readlane(off, f0) + 2u;
-            PayloadRegs r0, r1;
-            payload_load(base + readlane(seg, f0), d0, r0);
-            uint8_t *d1 = nullptr;
-            uint32_t i1 = 0;
-            if (f1 >= 0) {
-                i1 = slot0 + ord[g0 + (uint32_t)f1];
-                d1 = out + readlane(off, f1) + 2u;
-                payload_load(base + readlane(seg, f1), d1, r1);
+            int f[EMIT_PAY];
+            uint32_t ii[EMIT_PAY];
+            uint8_t *d[EMIT_PAY];
+            PayloadRegs r[EMIT_PAY];
+#pragma unroll
+            for (int g = 0; g < EMIT_PAY; g++) {
+                f[g] = m ? __ffsll((unsigned long long)m) - 1 : -1;
+                if (m) m &= m - 1;
+                if (f[g] >= 0) {
+                    ii[g] = slot0 + ord[g0 + (uint32_t)f[g]];
+                    d[g] = out + readlane(off, f[g]) + 2u;
+                    payload_load(base + readlane(seg, f[g]), d[g], r[g]);
+                }
             }
-            payload_store(d0, i0 < P.seg_cap ? P.segs + (size_t)i0 * XC_SEG : nullptr, r0);
-            if (f1 >= 0) payload_store(d1, i1 < P.seg_cap ? P.segs + (size_t)i1 * XC_SEG : nullptr, r1);
+#pragma unroll
+            for (int g = 0; g < EMIT_PAY; g++)
+                if (f[g] >= 0) payload_store(d[g], ii[g] < P.seg_cap ? P.segs + (size_t)ii[g] * XC_SEG : nullptr, r[g]);
         }
     }
 }
