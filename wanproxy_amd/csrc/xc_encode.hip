@@ -1198,16 +1198,57 @@ __device__ __forceinline__ uint32_t write_escaped(uint8_t *dst, const uint8_t *p
 
 constexpr int EMIT_PAY = 2;  // payloads a wave has in flight
 
-template <uint32_t EMIT_WAVES>
+// k_alloc's gate (a sub-batch that needs the host stops the device pipeline here).
+__device__ __forceinline__ bool gate_stop(const EmitArgs &a)
+{
+    const uint32_t *ctl = a.P.ctl;
+    return a.gate_sb != NONE && (ctl[CTL_GREW] || ctl[CTL_SHADOW] || ctl[CTL_FIRST_CROSS] < a.j1 || ctl[CTL_ERROR]);
+}
+
+__device__ __forceinline__ void gate_abort(const EmitArgs &a)
+{
+    a.P.ctl[CTL_ABORT_SB] = a.gate_sb;
+    a.P.ctl[CTL_ABORT] = 1u;
+}
+
+// The control words to the caller's mapped host buffer (one thread).
+__device__ __forceinline__ void ctl_publish(const EmitArgs &a)
+{
+    if (!a.ctl_host) return;
+    __threadfence();
+    for (uint32_t i = 0; i < CTL_WORDS; i++) a.ctl_host[i] = __atomic_load_n(&a.P.ctl[i], __ATOMIC_RELAXED);
+    __threadfence_system();
+}
+
+// SLOTS: k_alloc's work too (sub-batches of <= EMIT_SLOTS_MAX buffers), with no extra round trip
+// on a workgroup's path: the gate words, the sub-batch's start count (P.sb_count, written by
+// k_clear_set: the cache count does not change before this kernel) and every buffer's buf_next /
+// buf_nref are loaded with the token metadata; this buffer's first slot is the start count plus
+// the buf_next of the buffers before it, and workgroup 0 publishes the totals.
+template <uint32_t EMIT_WAVES, bool SLOTS>
 __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
 {
     if (aborted(a.P)) return;
     __shared__ uint32_t sz[MAX_TOK];
     __shared__ uint32_t ord[MAX_TOK];
+    __shared__ uint4 red[EMIT_WAVES];
     const PlanDev &P = a.P;
     const uint32_t b = a.j0 + blockIdx.x;
     if (b >= a.j1) return;
     const uint32_t wave = threadIdx.x >> 6, l = lane_id();
+    uint32_t s_pre = 0, s_tot = 0, s_ref = 0, s_stop = 0, s_base = 0;
+    if (SLOTS) {
+        for (uint32_t i = a.j0 + threadIdx.x; i < a.j1; i += 64u * EMIT_WAVES) {
+            const uint32_t v = P.buf_next[i];
+            s_tot += v;
+            s_ref += P.buf_nref[i];
+            if (i < b) s_pre += v;
+        }
+        if (threadIdx.x == 0) {
+            s_stop = gate_stop(a) ? 1u : 0u;
+            s_base = *a.base;
+        }
+    }
     const uint8_t *base = P.in + P.buf_off[b];
     uint8_t *out = P.out + P.out_off[b];
     const uint32_t tb = P.tok_base[b], n = min(P.tok_cnt[b], MAX_TOK);
@@ -1233,7 +1274,37 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
             ord[t] = op == OP_EXTRACT ? 1u : 0u;
         }
     }
+    if (SLOTS) {
+        const uint32_t x = wave_sum(s_pre), y = wave_sum(s_tot), z = wave_sum(s_ref);
+        if (l == 0) red[wave] = make_uint4(x, y, z, wave == 0 ? (s_stop | (s_base << 1)) : 0u);
+    }
     __syncthreads();
+    if (SLOTS) {
+        uint4 t = make_uint4(0, 0, 0, 0);
+        for (uint32_t k = 0; k < EMIT_WAVES; k++) {
+            t.x += red[k].x;
+            t.y += red[k].y;
+            t.z += red[k].z;
+        }
+        if (red[0].w & 1u) {  // the gate: every workgroup decides the same
+            if (blockIdx.x == 0 && threadIdx.x == 0) {
+                gate_abort(a);
+                ctl_publish(a);
+            }
+            return;
+        }
+        s_base = red[0].w >> 1;
+        s_pre = t.x;
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            const uint32_t count = s_base + t.y;
+            *P.seg_count = count;
+            P.ctl[CTL_COUNT] = count;
+            P.ctl[CTL_NEXTRACT] += t.y;
+            P.ctl[CTL_NREF] += t.z;
+            if (count > P.seg_cap) P.ctl[CTL_ERROR] |= ERR_CAPACITY;
+            ctl_publish(a);
+        }
+    }
     if (wave == 0) {
         uint32_t carry = 0, ocarry = 0;
         for (uint32_t t0 = 0; t0 < n; t0 += 64u) {
@@ -1247,7 +1318,7 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
         if (l == 0) P.out_len[b] = carry;
     }
     __syncthreads();
-    const uint32_t slot0 = P.buf_slot[b];
+    const uint32_t slot0 = SLOTS ? s_base + s_pre : P.buf_slot[b];
     if (wave == EMIT_WAVES - 1u) {  // the wave with the smallest token group (wave 0 did the prefix)
         // XCodecMemoryCache::enter (xcodec_cache.h:182-188) of this buffer's declarations,
         // one lane per EXTRACT token, into the slots k_alloc reserved
@@ -1320,8 +1391,10 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
     }
 }
 
-template __global__ void k_emit<4>(EmitArgs);
-template __global__ void k_emit<16>(EmitArgs);
+template __global__ void k_emit<4, false>(EmitArgs);
+template __global__ void k_emit<16, false>(EmitArgs);
+template __global__ void k_emit<4, true>(EmitArgs);
+template __global__ void k_emit<16, true>(EmitArgs);
 
 // One workgroup: cache slots for the declarations of buffers [j0, j1) in buffer order
 // (exclusive prefix of buf_next on top of the current segment count), plus run totals.
@@ -1333,12 +1406,8 @@ __global__ __launch_bounds__(1024) void k_alloc(EmitArgs a)
         // the host: declaration growth, a missed REF shadow, a cross-buffer conflict or an error
         __shared__ uint32_t stop;
         if (threadIdx.x == 0) {
-            const uint32_t *ctl = a.P.ctl;
-            stop = (ctl[CTL_GREW] || ctl[CTL_SHADOW] || ctl[CTL_FIRST_CROSS] < a.j1 || ctl[CTL_ERROR]) ? 1u : 0u;
-            if (stop) {
-                a.P.ctl[CTL_ABORT_SB] = a.gate_sb;
-                a.P.ctl[CTL_ABORT] = 1u;
-            }
+            stop = gate_stop(a) ? 1u : 0u;
+            if (stop) gate_abort(a);
         }
         __syncthreads();
         if (stop) return;

@@ -199,7 +199,14 @@ struct EmitArgs {
     PlanDev P;
     uint32_t j0, j1;
     uint32_t gate_sb;  // k_alloc: async-pipeline gate for sub-batch gate_sb (NONE: no gate)
+    // k_emit<.., true>: the control words' final state also goes here (mapped pinned host
+    // memory; null: not wanted)
+    uint32_t *ctl_host;
+    const uint32_t *base;  // k_emit<.., true>: the cache count at the sub-batch's start (P.sb_count)
 };
+// Sub-batches of at most this many buffers take k_alloc's work inside k_emit (every workgroup
+// sums the buf_next of the buffers before it): one launch less on small batches.
+constexpr uint32_t EMIT_SLOTS_MAX = 1024;
 
 // Packing a sub-batch's encoded streams, in buffer order, into one caller buffer (pinned host
 // memory written over PCIe by the kernel, or device memory): the end-to-end host path.
@@ -214,7 +221,7 @@ struct PackArgs {
 constexpr uint32_t ERR_PACK_CAP = 8;
 
 template <int MODE> __global__ void k_scan(ScanArgs a);
-template <uint32_t NW> __global__ void k_emit(EmitArgs a);
+template <uint32_t NW, bool SLOTS> __global__ void k_emit(EmitArgs a);
 __global__ void k_pack_offsets(PackArgs a);
 __global__ void k_pack_copy(PackArgs a);
 __global__ void k_resolve(ResolveArgs a);

@@ -759,6 +759,9 @@ struct xc_plan {
     hipStream_t hs = nullptr;
     hipEvent_t ev_start = nullptr;
     uint32_t *h_ctl = nullptr;  // pinned copy of the control words (read_ctl)
+    uint32_t *d_hctl = nullptr;  // its device address (k_emit<.., true> publishes the words there)
+    uint32_t *emit_ctl_host = nullptr;  // set while a graph whose last emit publishes is captured
+    bool g_publish = false;      // the captured graph's emit publishes the control words
     hipEvent_t ev_ctl = nullptr;
     std::vector<hipEvent_t> ev_hash, ev_go;
     uint32_t next_hash = 0;  // first sub-batch not yet enqueued for hashing in this run
@@ -1234,6 +1237,9 @@ static int ctl_buffers(xc_plan *p)
 {
     if (!p->h_ctl) {
         if (hmalloc((void **)&p->h_ctl, CTL_WORDS * 4) != hipSuccess) return fail(XC_ENOMEM, "pinned allocation failed");
+        void *dp = nullptr;
+        HIPCHK(hipHostGetDevicePointer(&dp, p->h_ctl, 0));
+        p->d_hctl = (uint32_t *)dp;
         HIPCHK(hipEventCreateWithFlags(&p->ev_ctl, hipEventDisableTiming));
     }
     return XC_OK;
@@ -1317,18 +1323,23 @@ static int launch_walk_round(xc_plan *p, uint32_t j0, uint32_t j1, int use_d, in
     return XC_OK;
 }
 
-static int launch_emit(xc_plan *p, uint32_t j0, uint32_t jc, uint32_t gate_sb = NONE)
+static int launch_emit(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t jc, uint32_t gate_sb = NONE)
 {
     hipStream_t s = p->cache->ctx->stream;
-    EmitArgs e{p->P, j0, jc, gate_sb};
-    hipLaunchKernelGGL(k_alloc, dim3(1), dim3(1024), 0, s, e);
-    HIPCHK(hipGetLastError());
+    // few buffers: the slots inside the emit (one launch less)
+    const bool slots = jc > j0 && jc - j0 <= EMIT_SLOTS_MAX;
+    EmitArgs e{p->P, j0, jc, gate_sb, slots ? p->emit_ctl_host : nullptr, p->P.sb_count + sb};
+    if (!slots) {
+        hipLaunchKernelGGL(k_alloc, dim3(1), dim3(1024), 0, s, e);
+        HIPCHK(hipGetLastError());
+    }
+    if (jc <= j0) return XC_OK;
     KSpan span(p, XC_K_EMIT);
     // one workgroup per buffer: 4 waves when the buffers alone fill the chip, 16 for few buffers
-    if ((uint64_t)(jc - j0) * EMIT_WAVES >= (uint64_t)p->cache->ctx->n_cu * 16u)
-        hipLaunchKernelGGL(k_emit<EMIT_WAVES>, dim3(jc - j0), dim3(64 * EMIT_WAVES), 0, s, e);
-    else
-        hipLaunchKernelGGL(k_emit<16>, dim3(jc - j0), dim3(64 * 16), 0, s, e);
+    const bool wide = (uint64_t)(jc - j0) * EMIT_WAVES < (uint64_t)p->cache->ctx->n_cu * 16u;
+    auto kern = wide ? (slots ? k_emit<16, true> : k_emit<16, false>)
+                     : (slots ? k_emit<EMIT_WAVES, true> : k_emit<EMIT_WAVES, false>);
+    hipLaunchKernelGGL(kern, dim3(jc - j0), dim3(64 * (wide ? 16 : EMIT_WAVES)), 0, s, e);
     HIPCHK(hipGetLastError());
     return XC_OK;
 }
@@ -1424,7 +1435,7 @@ static int encode_sub_async(xc_plan *p, uint32_t sb)
     int rc;
     p->stats.sub_batches++;
     if ((rc = launch_first_round(p, sb, j0, s1, p->shadow))) return rc;
-    if ((rc = launch_emit(p, j0, s1, sb))) return rc;
+    if ((rc = launch_emit(p, sb, j0, s1, sb))) return rc;
     return launch_pack(p, j0, s1);
 }
 
@@ -1453,7 +1464,7 @@ static int encode_sub_sync(xc_plan *p, uint32_t sb, uint32_t *ctl)
         if (ctl[CTL_ERROR]) return XC_OK;
         uint32_t jc = std::min<uint32_t>(ctl[CTL_FIRST_CROSS], s1);
         if (jc <= j0) jc = j0 + 1;  // cannot happen (buffer j0 has no earlier buffer); progress guard
-        if ((rc = launch_emit(p, j0, jc))) return rc;
+        if ((rc = launch_emit(p, sb, j0, jc))) return rc;
         j0 = jc;
     }
     return XC_OK;
@@ -1484,10 +1495,16 @@ static int run_graph(xc_plan *p, uint32_t *ctl)
             p->gexec = nullptr;
         }
         // capture on the context stream (work the caller enqueued before it stays outside)
+        // a one-sub-batch graph whose emit takes the slots also publishes the control words
+        // (no copy launch after it)
+        const uint32_t nlast = p->sub[nsub] - p->sub[nsub - 1];
+        const bool publish = nsub == 1 && nlast > 0 && nlast <= EMIT_SLOTS_MAX && !p->host_path;
         HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
         const xc_run_stats st0 = p->stats;
+        p->emit_ctl_host = publish ? p->d_hctl : nullptr;
         for (size_t k = 0; k < nsub && !rc; k++) rc = encode_sub_async(p, (uint32_t)k);
-        if (!rc && hipMemcpyAsync(p->h_ctl, p->P.ctl, CTL_WORDS * 4, hipMemcpyDeviceToHost, s) != hipSuccess)
+        p->emit_ctl_host = nullptr;
+        if (!rc && !publish && hipMemcpyAsync(p->h_ctl, p->P.ctl, CTL_WORDS * 4, hipMemcpyDeviceToHost, s) != hipSuccess)
             rc = fail(XC_EDEVICE, "graph capture: control-word copy");
         hipGraph_t g = nullptr;
         const hipError_t ce = hipStreamEndCapture(s, &g);
@@ -1500,6 +1517,7 @@ static int run_graph(xc_plan *p, uint32_t *ctl)
             p->g_out = p->P.out;
             p->g_len = p->P.out_len;
             p->g_stream = p->P.stream_st;
+            p->g_publish = publish;
         } else {
             p->gexec = nullptr;
         }
@@ -1514,12 +1532,16 @@ static int run_graph(xc_plan *p, uint32_t *ctl)
             return read_ctl(p, ctl);
         }
     }
+    // (a sentinel in the unused last word: the emit's publication clears it)
+    if (p->g_publish) p->h_ctl[CTL_WORDS - 1] = 0xFFFFFFFFu;
     HIPCHK(hipGraphLaunch(p->gexec, s));
     p->stats.sub_batches += p->g_stats.sub_batches;
     p->stats.outer_rounds += p->g_stats.outer_rounds;
     p->stats.walk_rounds += p->g_stats.walk_rounds;
     p->next_hash = (uint32_t)nsub;  // (the graph hashed every sub-batch's blocks)
-    return wait_ctl(p, ctl);
+    if ((rc = wait_ctl(p, ctl))) return rc;
+    if (p->g_publish && ctl[CTL_WORDS - 1] != 0u) return read_ctl(p, ctl);  // (not published)
+    return XC_OK;
 }
 
 extern "C" int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_out_len)
