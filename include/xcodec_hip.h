@@ -33,6 +33,7 @@ extern "C" {
 #define XC_ENOSPC (-28)  /* device cache capacity exhausted */
 #define XC_EDEVICE (-5)  /* HIP runtime error */
 #define XC_ENOENT (-2)
+#define XC_EBUSY (-16)   /* a run of this plan is in flight (xc_encode_submit) */
 
 typedef struct xc_ctx xc_ctx;     /* one per GPU; use from one host thread at a time */
 typedef struct xc_cache xc_cache; /* replaces XCodecMemoryCache (xcodec/xcodec_cache.h:162-211) */
@@ -97,6 +98,16 @@ int xc_plan_layout(xc_plan *p, uint64_t *in_off, uint64_t *out_off, uint64_t *in
  * before the call, e.g. an async copy into d_in or xc_cache_restore_async; input written on any
  * other stream must be complete (or ordered before the context stream by the caller). */
 int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_out_len);
+/* xc_encode_run for an event loop: xc_encode_submit enqueues the run and returns at once;
+ * xc_encode_poll never blocks while the device works (*done = 0) and finishes the run once it
+ * has (*done = 1, returning the run's status, as xc_encode_run would); xc_encode_wait blocks
+ * (yielding the CPU) until then.  Until the run is finished the plan, its cache and the arenas
+ * belong to it (another submit on the plan fails with XC_EBUSY).  A run whose sub-batches need
+ * the host (declaration growth, cross-buffer conflicts: rare) completes those inside the poll
+ * or wait that finishes it.  xc_encode_run = submit + wait. */
+int xc_encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_out_len);
+int xc_encode_poll(xc_plan *p, int *done);
+int xc_encode_wait(xc_plan *p);
 /* Host-to-host convenience: pinned H2D, xc_encode_run, D2H.  out_len receives nbuf lengths. */
 int xc_encode_batch_host(xc_cache *c, const uint8_t *in, const uint64_t *in_off,
                          const uint64_t *in_len, uint64_t nbuf, uint8_t *out,

@@ -438,6 +438,60 @@ def test_graph_replay_and_recapture(gpu_ctx, oracle_mod, monkeypatch, no_graph):
     assert len(set(stats)) == 1 and stats[0][1] > 0, stats  # same pass every run, some redone
 
 
+@pytest.mark.parametrize("sub_mb", ["64", "1"])
+def test_submit_poll_wait(gpu_ctx, oracle_mod, monkeypatch, sub_mb):
+    """xc_encode_submit returns before the device has finished; xc_encode_poll reports the run
+    unfinished without blocking, then finishes it (including the sub-batches the gate hands back
+    to the host: cross-buffer duplicates, self references); xc_encode_wait does the same blocking.
+    A second submit while a run is in flight fails with XC_EBUSY, a poll with no run in flight
+    fails.  One sub-batch (the graph path) and many.  Every run equals the oracle."""
+    import time
+    import torch
+    import wanproxy_amd as w
+    monkeypatch.setenv("XC_SUB_MB", sub_mb)
+    bufs, warm = _mixed_batch()
+    oc = oracle_mod.Cache()
+    for batch in warm:
+        oc.encode_batch(batch)
+    want = oc.encode_batch(bufs)
+    cache = w.XCodecCache(gpu_ctx, 1 << 14)
+    for batch in warm:
+        w.XCodecEncoder(cache).encode_batch(batch)
+    cache.snapshot()
+    plan = w.EncodePlan(cache, [len(b) for b in bufs])
+    arena = np.zeros(plan.in_bytes, np.uint8)
+    for i, b in enumerate(bufs):
+        arena[int(plan.in_off[i]):int(plan.in_off[i]) + len(b)] = b
+    d_in = torch.from_numpy(arena).cuda()
+    d_out = torch.zeros(plan.out_bytes, dtype=torch.uint8, device="cuda")
+    d_len = torch.zeros(len(bufs), dtype=torch.int64, device="cuda")
+    with pytest.raises(w.XCodecError):
+        plan.poll()  # nothing in flight
+    stats = []
+    for it in range(4):
+        d_out.zero_()
+        torch.cuda.synchronize()
+        cache.restore_async()
+        plan.submit(d_in.data_ptr(), d_out.data_ptr(), d_len.data_ptr())
+        if it == 0:
+            with pytest.raises(w.XCodecError):
+                plan.submit(d_in.data_ptr(), d_out.data_ptr(), d_len.data_ptr())
+        if it % 2:
+            plan.wait()
+        else:
+            t0 = time.time()
+            while not plan.poll():
+                assert time.time() - t0 < 60
+        torch.cuda.synchronize()
+        out, lens = d_out.cpu().numpy(), d_len.cpu().numpy()
+        for i in range(len(bufs)):
+            o = int(plan.out_off[i])
+            assert out[o:o + int(lens[i])].tobytes() == want[i], (it, i)
+        st = plan.stats()
+        stats.append((st.sub_batches, st.redone, st.n_extract, st.n_ref))
+    assert len(set(stats)) == 1 and stats[0][1] > 0, stats
+
+
 def test_cache_grows_like_the_reference_map(gpu_ctx, oracle_mod):
     """The reference's memory cache never fills (xcodec/xcodec_cache.h:164,182-188).  A device
     cache created for 1024 segments takes ten times that through several batches, a snapshot taken

@@ -762,6 +762,8 @@ struct xc_plan {
     uint32_t *d_hctl = nullptr;  // its device address (k_emit<.., true> publishes the words there)
     uint32_t *emit_ctl_host = nullptr;  // set while a graph whose last emit publishes is captured
     bool g_publish = false;      // the captured graph's emit publishes the control words
+    bool pass_published = false;  // the in-flight first pass publishes them (else a copy)
+    bool inflight = false;        // xc_encode_submit enqueued a run not finished yet
     hipEvent_t ev_ctl = nullptr;
     std::vector<hipEvent_t> ev_hash, ev_go;
     uint32_t next_hash = 0;  // first sub-batch not yet enqueued for hashing in this run
@@ -1480,9 +1482,17 @@ static bool use_graph(xc_plan *p)
     return !(e && atoi(e)) && !p->g_off && !p->timing && !p->host_path && p->sub.size() == 2;
 }
 
+// Record ev_ctl after the control words' copy to h_ctl (enqueued by the caller or published by
+// the emit): the host reads them once it has passed.
+static int record_ctl(xc_plan *p)
+{
+    HIPCHK(hipEventRecord(p->ev_ctl, p->cache->ctx->stream));
+    return XC_OK;
+}
+
 // The first asynchronous pass of a run (the ctl words were cleared before it) as a graph launch,
-// then the control-word wait.  (Re)captured when the arenas differ from the captured ones.
-static int run_graph(xc_plan *p, uint32_t *ctl)
+// then ev_ctl; nothing waits.  (Re)captured when the arenas differ from the captured ones.
+static int graph_launch(xc_plan *p)
 {
     hipStream_t s = p->cache->ctx->stream;
     int rc = ctl_buffers(p);
@@ -1527,9 +1537,11 @@ static int run_graph(xc_plan *p, uint32_t *ctl)
         if (!p->gexec) {  // not capturable here: enqueue directly from now on
             p->g_off = true;
             p->next_hash = 0;
+            p->pass_published = false;
             for (size_t k = 0; k < nsub; k++)
                 if ((rc = encode_sub_async(p, (uint32_t)k))) return rc;
-            return read_ctl(p, ctl);
+            HIPCHK(hipMemcpyAsync(p->h_ctl, p->P.ctl, CTL_WORDS * 4, hipMemcpyDeviceToHost, s));
+            return record_ctl(p);
         }
     }
     // (a sentinel in the unused last word: the emit's publication clears it)
@@ -1539,13 +1551,14 @@ static int run_graph(xc_plan *p, uint32_t *ctl)
     p->stats.outer_rounds += p->g_stats.outer_rounds;
     p->stats.walk_rounds += p->g_stats.walk_rounds;
     p->next_hash = (uint32_t)nsub;  // (the graph hashed every sub-batch's blocks)
-    if ((rc = wait_ctl(p, ctl))) return rc;
-    if (p->g_publish && ctl[CTL_WORDS - 1] != 0u) return read_ctl(p, ctl);  // (not published)
-    return XC_OK;
+    p->pass_published = p->g_publish;
+    return record_ctl(p);
 }
 
-extern "C" int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_out_len)
+// Everything of a run up to its first asynchronous pass, which is enqueued with ev_ctl after it.
+extern "C" int xc_encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_out_len)
 {
+    if (p && p->inflight) return fail(XC_EBUSY, "a run of this plan is in flight (xc_encode_poll / xc_encode_wait)");
     if (!p || (!d_in && p->nb) || (!d_out && p->nb) || (!d_out_len && p->nb)) return fail(XC_EINVAL, "null");
     int rc = set_dev(p->cache->ctx);
     if (rc) return rc;
@@ -1580,27 +1593,38 @@ extern "C" int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, ui
     p->cache->host_count = -1;
     if (p->sub.size() > 1) p->zero_ctl = true;  // (the first k_clear_set clears the control words)
     else HIPCHK(hipMemsetAsync(p->P.ctl, 0, CTL_WORDS * 4, s));
-    uint32_t ctl[CTL_WORDS];
     p->next_hash = 0;
     const size_t nsub = p->sub.size() - 1;
-    size_t si = 0;
-    bool fresh = false;  // ctl was read after the last launch
-    bool first = true;   // the run's first asynchronous pass (the graph's part)
-    while (si < nsub) {
-        // Async pass: enqueue every remaining sub-batch with no host round trip.  k_gate
-        // stops the device pipeline at the first sub-batch that needs the host.
-        if (first && use_graph(p)) {
-            if ((rc = run_graph(p, ctl))) return rc;
-        } else {
-            for (size_t k = si; k < nsub; k++)
-                if ((rc = encode_sub_async(p, (uint32_t)k))) return rc;
-            if ((rc = read_ctl(p, ctl))) return rc;
-        }
-        first = false;
-        fresh = true;
-        if (!ctl[CTL_ABORT]) break;
+    if ((rc = ctl_buffers(p))) return rc;
+    if (use_graph(p)) {
+        if ((rc = graph_launch(p))) return rc;
+    } else {
+        p->pass_published = false;
+        for (size_t k = 0; k < nsub; k++)
+            if ((rc = encode_sub_async(p, (uint32_t)k))) return rc;
+        HIPCHK(hipMemcpyAsync(p->h_ctl, p->P.ctl, CTL_WORDS * 4, hipMemcpyDeviceToHost, s));
+        if ((rc = record_ctl(p))) return rc;
+    }
+    p->inflight = true;
+    return XC_OK;
+}
+
+// After the first pass's ev_ctl: its control words, then the sub-batches that need the host
+// (step by step) and further asynchronous passes, then the run's totals.
+static int encode_finish(xc_plan *p)
+{
+    p->inflight = false;
+    int rc = XC_OK;
+    hipStream_t s = p->cache->ctx->stream;
+    uint32_t ctl[CTL_WORDS];
+    memcpy(ctl, p->h_ctl, CTL_WORDS * 4);
+    ev_collect(p);
+    if (p->pass_published && ctl[CTL_WORDS - 1] != 0u && (rc = read_ctl(p, ctl))) return rc;  // (not published)
+    const size_t nsub = p->sub.size() - 1;
+    bool fresh = true;  // ctl was read after the last launch
+    while (ctl[CTL_ABORT]) {
         fresh = false;
-        si = ctl[CTL_ABORT_SB];
+        size_t si = ctl[CTL_ABORT_SB];
         HIPCHK(hipMemsetAsync(p->P.ctl + CTL_ABORT, 0, 4, s));
         if (ctl[CTL_ERROR]) break;
         p->stats.redone++;
@@ -1609,7 +1633,12 @@ extern "C" int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, ui
         if ((rc = encode_sub_sync(p, (uint32_t)si, ctl))) return rc;
         if (ctl[CTL_ERROR]) break;
         if ((rc = launch_pack(p, p->sub[si], p->sub[si + 1]))) return rc;
-        si++;
+        if (++si >= nsub) break;
+        // the rest asynchronously again: k_alloc's gate stops at the next sub-batch needing the host
+        for (size_t k = si; k < nsub; k++)
+            if ((rc = encode_sub_async(p, (uint32_t)k))) return rc;
+        if ((rc = read_ctl(p, ctl))) return rc;
+        fresh = true;
     }
     if (!fresh && (rc = read_ctl(p, ctl))) return rc;
     for (uint64_t i = 0; i < p->nb; i++) p->stats.in_bytes += p->len[i];
@@ -1627,6 +1656,46 @@ extern "C" int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, ui
     if (ctl[CTL_ERROR] & ERR_PACK_CAP) return fail(XC_EINVAL, "packed output capacity too small");
     if (ctl[CTL_ERROR]) return fail(XC_EDEVICE, "internal encode error " + std::to_string(ctl[CTL_ERROR]));
     return XC_OK;
+}
+
+extern "C" int xc_encode_poll(xc_plan *p, int *done)
+{
+    if (!p || !done) return fail(XC_EINVAL, "null");
+    if (!p->inflight) return fail(XC_EINVAL, "no run in flight");
+    int rc = set_dev(p->cache->ctx);
+    if (rc) return rc;
+    const hipError_t e = hipEventQuery(p->ev_ctl);
+    if (e == hipErrorNotReady) {
+        *done = 0;
+        return XC_OK;
+    }
+    *done = 1;
+    if (e != hipSuccess) {
+        p->inflight = false;
+        return fail(XC_EDEVICE, std::string("run: ") + hipGetErrorString(e));
+    }
+    return encode_finish(p);
+}
+
+extern "C" int xc_encode_wait(xc_plan *p)
+{
+    if (!p) return fail(XC_EINVAL, "null");
+    if (!p->inflight) return fail(XC_EINVAL, "no run in flight");
+    int rc = set_dev(p->cache->ctx);
+    if (rc) return rc;
+    const hipError_t e = spin_wait(p->ev_ctl);
+    if (e != hipSuccess) {
+        p->inflight = false;
+        return fail(XC_EDEVICE, std::string("run: ") + hipGetErrorString(e));
+    }
+    return encode_finish(p);
+}
+
+extern "C" int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_out_len)
+{
+    int rc = xc_encode_submit(p, d_in, d_out, d_out_len);
+    if (rc) return rc;
+    return xc_encode_wait(p);
 }
 
 extern "C" int xc_host_alloc(xc_ctx *ctx, uint64_t bytes, void **out)

@@ -38,7 +38,7 @@ SYMBOLS = [
     "xc_hash_segments_host", "xc_cache_capacity",
     "xc_coss_open", "xc_coss_close", "xc_coss_cache", "xc_coss_count", "xc_coss_stats", "xc_coss_lookup",
     "xc_coss_enter", "xc_coss_encode_batch_host", "xc_coss_decode_batch_host", "xc_coss_store_lookup",
-    "xc_coss_store_enter", "xc_coss_encode_streams",
+    "xc_coss_store_enter", "xc_coss_encode_streams", "xc_encode_submit", "xc_encode_poll", "xc_encode_wait",
 ]
 STREAM_FLUSH = 1  # XC_STREAM_FLUSH
 
@@ -112,6 +112,9 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.xc_plan_destroy.argtypes = [_vp]
     lib.xc_plan_layout.argtypes = [_vp, _u64p, _u64p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     lib.xc_encode_run.argtypes = [_vp, _vp, _vp, _vp]
+    lib.xc_encode_submit.argtypes = [_vp, _vp, _vp, _vp]
+    lib.xc_encode_poll.argtypes = [_vp, C.POINTER(C.c_int)]
+    lib.xc_encode_wait.argtypes = [_vp]
     lib.xc_plan_stats.argtypes = [_vp, C.POINTER(RunStats)]
     lib.xc_encode_batch_host.argtypes = [_vp, _u8p, _u64p, _u64p, C.c_uint64, _u8p, _u64p, _u64p,
                                          _u64p]
@@ -532,6 +535,21 @@ class EncodePlan:
 
     def run(self, d_in: int, d_out: int, d_len: int) -> None:
         _check(load_library().xc_encode_run(self.h, d_in, d_out, d_len))
+
+    def submit(self, d_in: int, d_out: int, d_len: int) -> None:
+        """Enqueue a run and return at once (xc_encode_submit); finish it with poll() / wait()."""
+        _check(load_library().xc_encode_submit(self.h, d_in, d_out, d_len))
+
+    def poll(self) -> bool:
+        """True once the submitted run has finished (raising if it failed); never blocks while
+        the device works (xc_encode_poll)."""
+        done = C.c_int(0)
+        _check(load_library().xc_encode_poll(self.h, C.byref(done)))
+        return bool(done.value)
+
+    def wait(self) -> None:
+        """Block until the submitted run has finished (xc_encode_wait)."""
+        _check(load_library().xc_encode_wait(self.h))
 
     def run_host(self, h_in: "HostBuffer", h_out: "HostBuffer"):
         """End-to-end from host memory (xc_encode_run_host): ``h_in`` holds the input arena in
