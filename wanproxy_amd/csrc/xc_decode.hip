@@ -4,9 +4,10 @@
 // streams in index order, one shared XCodecMemoryCache.  Pipeline:
 //
 //   k_dtok     one wave per stream: F1 search in 1 KiB register windows -> tokens
-//              (literal run [lb, le) with F1 00 escapes, then the op at le)
-//   k_dhash    H of every EXTRACT payload (xcodec_hash.h:166-174)
-//   k_dres1    EXTRACT vs the cache: equal -> ok, different -> collision (decode returns
+//              (literal run [lb, le) with F1 00 escapes, then the op at le); also the run's
+//              prologue (control words, provider limits, round 0's provider table)
+//   k_dres1    (round 0: H of every EXTRACT payload first, xcodec_hash.h:166-174)
+//              EXTRACT vs the cache: equal -> ok, different -> collision (decode returns
 //              false, xcodec_decoder.cc:120-132); absent -> candidate provider, min-merged
 //              by (stream, token) into the batch table
 //   k_dres2    every token against cache + earlier providers: REF data source or unknown
@@ -111,9 +112,19 @@ __device__ __forceinline__ uint32_t dwin_byte(const DWin &w, uint32_t x)
 // Tokenizer (xcodec_decoder.cc:85-173), one wave per stream: tokens are found inside 1 KiB
 // register windows (ESC and REF tokens, and the REF hash bytes, without another load); only an
 // EXTRACT, whose 2048-byte payload is skipped, or the window's end, loads a new window.
-__global__ __launch_bounds__(64) void k_dtok(DecDev D, int fill)
+__device__ __forceinline__ void dclear_range(const DecDev &D, uint32_t n_lo, uint32_t n_full, uint32_t i0,
+                                             uint32_t stride);
+
+// first: also the run's prologue, spread over the tokenizer's threads (the control words, every
+// stream's provider limit, the round-0 batch provider table): three launches less.
+__global__ __launch_bounds__(64) void k_dtok(DecDev D, int fill, int first, uint32_t n_lo, uint32_t n_full)
 {
     const uint32_t j = blockIdx.x;
+    if (first) {
+        if (j == 0 && threadIdx.x < DCTL_WORDS) D.ctl[threadIdx.x] = 0u;
+        if (j < D.ns && threadIdx.x == 0) D.s_lim[j] = 0xFFFFFFFFu;
+        dclear_range(D, n_lo, n_full, j * 64u + threadIdx.x, gridDim.x * 64u);
+    }
     if (j >= D.ns) return;
     const uint8_t *s = D.in + D.in_off[j];
     const uint32_t n = D.in_len[j];
@@ -173,20 +184,9 @@ __global__ __launch_bounds__(64) void k_dtok(DecDev D, int fill)
     if (lane_id() == 0) D.tok_cnt[j] = nt;
 }
 
-__global__ __launch_bounds__(64) void k_dhash(DecDev D)
-{
-    const uint32_t j = blockIdx.x;
-    if (j >= D.ns) return;
-    const uint8_t *s = D.in + D.in_off[j];
-    const uint32_t tb = D.tok_base[j], n = D.tok_cnt[j];
-    for (uint32_t t = blockIdx.y; t < n; t += gridDim.y) {
-        if (uniform(D.t_op[tb + t]) != T_EXTRACT) continue;
-        const uint64_t h = wave_window_hash(s + D.t_le[tb + t] + 2u);
-        if (lane_id() == 0) D.t_h[tb + t] = h;
-    }
-}
-
 // EXTRACTs against the cache; absent ones become provider candidates in the batch table.
+// HASH (round 0): the payloads' hashes H first (xcodec_hash.h:166-174), kept in t_h.
+template <bool HASH>
 __global__ __launch_bounds__(64) void k_dres1(DecDev D)
 {
     const uint32_t j = blockIdx.x;
@@ -196,8 +196,14 @@ __global__ __launch_bounds__(64) void k_dres1(DecDev D)
     const uint32_t lim = D.s_lim[j];
     for (uint32_t t = blockIdx.y; t < n; t += gridDim.y) {
         if (uniform(D.t_op[tb + t]) != T_EXTRACT) continue;
-        const uint64_t h = D.t_h[tb + t];
         const uint8_t *pay = s + D.t_le[tb + t] + 2u;
+        uint64_t h;
+        if (HASH) {
+            h = wave_window_hash(pay);
+            if (lane_id() == 0) D.t_h[tb + t] = h;
+        } else {
+            h = D.t_h[tb + t];
+        }
         uint64_t v;
         uint32_t st;
         if (set_find(D.cache, h, &v)) {
@@ -314,12 +320,10 @@ __global__ __launch_bounds__(64) void k_dcheck(DecDev D, int round)
     }
 }
 
-// A resolution round's fresh batch provider table, its FIX flag and the token counters.
-__global__ void k_dclear(DecDev D, uint32_t n_lo, uint32_t n_full)
+__device__ __forceinline__ void dclear_range(const DecDev &D, uint32_t n_lo, uint32_t n_full, uint32_t i0,
+                                             uint32_t stride)
 {
     const DevSet &s = D.dset;
-    const uint32_t stride = gridDim.x * blockDim.x;
-    const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
     const uint4 z = make_uint4(0, 0, 0, 0), ones = make_uint4(~0u, ~0u, ~0u, ~0u);
     for (uint32_t i = i0; i < XC_FILT_WORDS / 4; i += stride) ((uint4 *)s.filt)[i] = z;
     for (uint32_t i = i0; i < XC_L2_WORDS / 2; i += stride) ((uint4 *)s.l2)[i] = z;
@@ -328,8 +332,15 @@ __global__ void k_dclear(DecDev D, uint32_t n_lo, uint32_t n_full)
         ((uint4 *)s.keys)[i] = ones;
         ((uint4 *)s.vals)[i] = ones;
     }
+    if (i0 == 0) *s.lo_zero = 0u;
+}
+
+// A resolution round's fresh batch provider table, its FIX flag and the token counters.
+__global__ void k_dclear(DecDev D, uint32_t n_lo, uint32_t n_full)
+{
+    const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
+    dclear_range(D, n_lo, n_full, i0, gridDim.x * blockDim.x);
     if (i0 == 0) {
-        *s.lo_zero = 0u;
         D.ctl[DCTL_FIX] = 0u;
         D.ctl[DCTL_NREF] = 0u;
         D.ctl[DCTL_NEXTRACT] = 0u;
@@ -568,6 +579,8 @@ using namespace xc;
 
 // The cache object is defined in xc_runtime.hip; these accessors expose what we need.
 extern "C" void xc__cache_count_unknown(xc_cache *c);
+extern "C" int64_t xc__cache_host_count(xc_cache *c);
+extern "C" void xc__cache_set_host_count(xc_cache *c, int64_t n);
 extern "C" int xc__cache_reserve(xc_cache *c, uint64_t extra);
 extern "C" uint32_t xc__cache_gen(xc_cache *c);
 extern "C" int xc__cache_devset(xc_cache *c, void *devset, uint8_t **segs, uint32_t **count, uint32_t *cap,
@@ -755,19 +768,21 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
         D.undo = PD.undo;
         p->cache_gen = xc__cache_gen(p->cache);
     }
-    xc__cache_count_unknown(p->cache);  // the run enters segments: the host's copy of the count is stale
-    DHIP(hipMemsetAsync(D.ctl, 0, DCTL_WORDS * 4, s));
-    hipLaunchKernelGGL(k_dtok, dim3(ns), dim3(64), 0, s, D, 1);
+    // the run enters segments: the host's copy of the count is stale until the run's totals
+    const int64_t count0 = xc__cache_host_count(p->cache);
+    xc__cache_count_unknown(p->cache);
+    // tokens, with the prologue (control words, provider limits, round 0's provider table)
+    hipLaunchKernelGGL(k_dtok, dim3(std::max<uint32_t>(ns, 256u)), dim3(64), 0, s, D, 1, 1, p->n_lo, p->n_full);
     DHIP(hipGetLastError());
-    hipLaunchKernelGGL(k_dhash, dim3(ns, 8), dim3(64), 0, s, D);
-    DHIP(hipGetLastError());
-    hipLaunchKernelGGL(k_dlim, dim3((ns + 255) / 256), dim3(256), 0, s, D, 1);
-    DHIP(hipGetLastError());
-    // one provider-resolution round (a fresh batch table each time)
+    // one provider-resolution round (a fresh batch table each time; round 0's came with k_dtok)
     auto resolve_round = [&](int r) -> int {
-        hipLaunchKernelGGL(k_dclear, dim3(512), dim3(256), 0, s, D, p->n_lo, p->n_full);
-        DHIP(hipGetLastError());
-        hipLaunchKernelGGL(k_dres1, dim3(ns, 8), dim3(64), 0, s, D);
+        if (r > 0) {
+            hipLaunchKernelGGL(k_dclear, dim3(512), dim3(256), 0, s, D, p->n_lo, p->n_full);
+            DHIP(hipGetLastError());
+            hipLaunchKernelGGL(k_dres1<false>, dim3(ns, 8), dim3(64), 0, s, D);
+        } else {
+            hipLaunchKernelGGL(k_dres1<true>, dim3(ns, 8), dim3(64), 0, s, D);
+        }
         DHIP(hipGetLastError());
         hipLaunchKernelGGL(k_dres2, dim3(ns, 8), dim3(64), 0, s, D);
         DHIP(hipGetLastError());
@@ -820,6 +835,9 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
         return xc__set_error(XC_ENOSPC, "device cache capacity exhausted");
     }
     if (ctl[DCTL_ERR] & 1u) return xc__set_error(XC_EINVAL, "output capacity too small");
+    // (k_dalloc advanced the count by exactly the entered segments: a later restore or reserve
+    // needs no device read)
+    if (count0 >= 0) xc__cache_set_host_count(p->cache, count0 + ctl[DCTL_NENTER]);
     return XC_OK;
 }
 

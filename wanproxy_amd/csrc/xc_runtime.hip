@@ -297,6 +297,12 @@ extern "C" void xc__cache_count_unknown(xc_cache *c)
 {
     if (c) c->host_count = -1;
 }
+// The host's copy of the count (-1: unknown), and setting it after a run that knows it.
+extern "C" int64_t xc__cache_host_count(xc_cache *c) { return c ? c->host_count : -1; }
+extern "C" void xc__cache_set_host_count(xc_cache *c, int64_t n)
+{
+    if (c) c->host_count = n;
+}
 
 static PlanDev cache_plandev(xc_cache *c)
 {
