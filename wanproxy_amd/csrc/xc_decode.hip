@@ -46,7 +46,7 @@ struct DecDev {
     uint32_t *s_stop;          // executed tokens per stream (the stop token included: its literal runs)
     uint32_t *s_lim;           // tokens eligible as EXTRACT providers this round
     uint32_t *s_slot;          // first cache slot of the stream's entered segments
-    uint64_t *s_outoff;        // unused placeholder
+    uint2 *s_cnt;              // executed (REF, EXTRACT) tokens of the stream (k_dalloc sums them)
     uint8_t *out;
     const uint64_t *out_off;
     const uint64_t *out_cap;
@@ -266,30 +266,42 @@ __global__ __launch_bounds__(64) void k_dres2(DecDev D)
     }
 }
 
-// Per stream (one lane each): executed token count, the decode's status / consumed bytes, and
-// the ordinal of every first-seen EXTRACT (ENTER) among the stream's executed tokens, kept in
-// t_src (unused for ENTER tokens); s_slot[j] = the stream's ENTER count (k_dalloc prefixes it).
-__global__ __launch_bounds__(64) void k_dstop(DecDev D)
+// Per stream (one wave each, 64 tokens per step): executed token count, the decode's status /
+// consumed bytes, and the ordinal of every first-seen EXTRACT (ENTER) among the stream's executed
+// tokens, kept in t_src (unused for ENTER tokens); s_slot[j] = the stream's ENTER count (k_dalloc
+// prefixes it).
+__global__ __launch_bounds__(256) void k_dstop(DecDev D)
 {
-    const uint32_t j = blockIdx.x * 64u + lane_id();
+    const uint32_t j = blockIdx.x * 4u + (threadIdx.x >> 6), l = lane_id();
     if (j >= D.ns) return;
     const uint32_t tb = D.tok_base[j], n = D.tok_cnt[j];
-    uint32_t t = 0, nr = 0, ne = 0, nent = 0;
-    for (; t < n; t++) {
-        const uint32_t op = D.t_op[tb + t], st = D.t_stat[tb + t];
-        if (op != T_EXTRACT && op != T_REF) break;
-        if (st == R_UNKNOWN || st == R_COLL) break;
-        nr += op == T_REF ? 1u : 0u;
-        ne += op == T_EXTRACT ? 1u : 0u;
-        if (st == R_ENTER) D.t_src[tb + t] = nent++;
+    uint32_t t = n, nr = 0, ne = 0, nent = 0;
+    for (uint32_t t0 = 0; t0 < n; t0 += 64u) {
+        const uint32_t i = t0 + l;
+        uint32_t op = T_END, st = 0;
+        if (i < n) {
+            op = D.t_op[tb + i];
+            st = D.t_stat[tb + i];
+        }
+        // the first token that stops the decode: terminal, unknown REF or colliding EXTRACT
+        const uint64_t brk = ballot(i < n && ((op != T_EXTRACT && op != T_REF) || st == R_UNKNOWN || st == R_COLL));
+        const uint32_t k = brk ? (uint32_t)__ffsll((unsigned long long)brk) - 1u : 64u;
+        const bool ex = l < k && i < n;
+        nr += (uint32_t)__popcll(ballot(ex && op == T_REF));
+        ne += (uint32_t)__popcll(ballot(ex && op == T_EXTRACT));
+        const uint64_t em = ballot(ex && st == R_ENTER);
+        if (ex && st == R_ENTER) D.t_src[tb + i] = nent + mbcnt(em);
+        nent += (uint32_t)__popcll(em);
+        if (brk) {
+            t = t0 + k;
+            break;
+        }
     }
-    // t = stopping token (terminal, unknown REF or colliding EXTRACT); its literal is output
+    if (l != 0) return;
+    // t = stopping token; its literal is output
     D.s_stop[j] = t + 1u;
     D.s_slot[j] = nent;
-    if (D.count) {  // executed REF / EXTRACT tokens (decode statistics)
-        if (nr) atomicAdd(&D.ctl[DCTL_NREF], nr);  // (lanes past ns have returned: no wave sums)
-        if (ne) atomicAdd(&D.ctl[DCTL_NEXTRACT], ne);
-    }
+    D.s_cnt[j] = make_uint2(nr, ne);  // (one device-wide atomic per stream serializes: k_dalloc sums)
     const uint32_t op = D.t_op[tb + t], le = D.t_le[tb + t];
     int32_t status = 1, hu = 0;
     uint64_t cons = le, unk = 0;
@@ -514,14 +526,21 @@ __global__ __launch_bounds__(1024) void k_dalloc(DecDev D)
 {
     if (fix_pending(D)) return;
     __shared__ uint32_t wsum[16];
+    __shared__ uint2 csum[16];
     __shared__ uint32_t carry;
     const uint32_t wave = threadIdx.x >> 6, l = lane_id();
     if (threadIdx.x == 0) carry = *D.seg_count;
     __syncthreads();
     const uint32_t start = carry;
+    uint32_t nr = 0, ne = 0;  // executed REF / EXTRACT tokens (decode statistics)
     for (uint32_t j0 = 0; j0 < D.ns; j0 += 1024u) {
         const uint32_t j = j0 + threadIdx.x;
         const uint32_t v = j < D.ns ? D.s_slot[j] : 0u;
+        if (j < D.ns) {
+            const uint2 c = D.s_cnt[j];
+            nr += c.x;
+            ne += c.y;
+        }
         const uint32_t inc = wave_incl_scan(v);
         if (l == 63) wsum[wave] = inc;
         __syncthreads();
@@ -536,7 +555,20 @@ __global__ __launch_bounds__(1024) void k_dalloc(DecDev D)
         }
         __syncthreads();
     }
+    nr = wave_sum(nr);
+    ne = wave_sum(ne);
+    if (l == 0) csum[wave] = make_uint2(nr, ne);
+    __syncthreads();
     if (threadIdx.x == 0) {
+        if (D.count) {
+            uint2 t = make_uint2(0, 0);
+            for (uint32_t k = 0; k < 16; k++) {
+                t.x += csum[k].x;
+                t.y += csum[k].y;
+            }
+            D.ctl[DCTL_NREF] = t.x;
+            D.ctl[DCTL_NEXTRACT] = t.y;
+        }
         *D.seg_count = carry;
         D.ctl[DCTL_NENTER] = carry - start;
         if (carry > D.seg_cap) D.ctl[DCTL_ERR] |= 2u;
@@ -685,7 +717,7 @@ extern "C" int xc_decode_plan_create(xc_cache *c, const uint64_t *in_len, const 
 #define DA(ptr, n) if ((rc = p->alloc(ptr, n))) { xc_dplan_destroy(p); return rc; }
     if (hipSetDevice(p->dev) != hipSuccess) { xc_dplan_destroy(p); return xc__set_error(XC_EDEVICE, "hipSetDevice"); }
     DA(&d_ioff, ns); DA(&d_ooff, ns); DA(&d_ocap, ns); DA(&d_ilen, ns); DA(&d_tbase, ns);
-    DA(&D.tok_cnt, ns); DA(&D.s_stop, ns); DA(&D.s_slot, ns); DA(&D.s_lim, ns); DA(&D.ctl, DCTL_WORDS);
+    DA(&D.tok_cnt, ns); DA(&D.s_stop, ns); DA(&D.s_slot, ns); DA(&D.s_cnt, ns); DA(&D.s_lim, ns); DA(&D.ctl, DCTL_WORDS);
     DA(&D.t_lb, ntok); DA(&D.t_le, ntok); DA(&D.t_op, ntok); DA(&D.t_stat, ntok); DA(&D.t_h, ntok);
     DA(&D.t_src, ntok);
     DevSet &ds = D.dset;
@@ -786,7 +818,7 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
         DHIP(hipGetLastError());
         hipLaunchKernelGGL(k_dres2, dim3(ns, 8), dim3(64), 0, s, D);
         DHIP(hipGetLastError());
-        hipLaunchKernelGGL(k_dstop, dim3((ns + 63) / 64), dim3(64), 0, s, D);
+        hipLaunchKernelGGL(k_dstop, dim3((ns + 3) / 4), dim3(256), 0, s, D);
         DHIP(hipGetLastError());
         hipLaunchKernelGGL(k_dcheck, dim3(ns), dim3(64), 0, s, D, r);
         DHIP(hipGetLastError());
