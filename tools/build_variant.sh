@@ -8,7 +8,7 @@ mkdir -p "$out"/include "$out"/w/csrc
 cp "$root"/include/*.h "$out"/include/
 cp "$root"/wanproxy_amd/csrc/*.hip "$root"/wanproxy_amd/csrc/*.h "$root"/wanproxy_amd/csrc/*.cpp "$out"/w/csrc/
 cd "$out"/w/csrc
-if [ -n "$XC_VARIANT_SED" ]; then sed -i "$XC_VARIANT_SED" xc_encode.hip; fi  # (a source edit for the variant)
+if [ -n "$XC_VARIANT_SED" ]; then sed -i "$XC_VARIANT_SED" ${XC_VARIANT_FILE:-xc_encode.hip}; fi  # (a source edit for the variant)
 FL="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -Wno-unused-value $*"
 for f in xc_encode xc_decode xc_runtime; do /opt/rocm/bin/hipcc $FL -c $f.hip -o $f.o & done
 for f in *.cpp; do g++ -O2 -std=c++17 -fPIC -Wall -c $f -o ${f%.cpp}.o; done

@@ -184,6 +184,9 @@ __global__ __launch_bounds__(64) void k_dtok(DecDev D, int fill, int first, uint
     if (lane_id() == 0) D.tok_cnt[j] = nt;
 }
 
+// k_dres1 / k_dres2 grids: (streams, DRES_WAVES), wave y taking tokens y, y + DRES_WAVES, ...
+constexpr uint32_t DRES_WAVES = 8;
+
 // EXTRACTs against the cache; absent ones become provider candidates in the batch table.
 // HASH (round 0): the payloads' hashes H first (xcodec_hash.h:166-174), kept in t_h.
 template <bool HASH>
@@ -811,12 +814,12 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
         if (r > 0) {
             hipLaunchKernelGGL(k_dclear, dim3(512), dim3(256), 0, s, D, p->n_lo, p->n_full);
             DHIP(hipGetLastError());
-            hipLaunchKernelGGL(k_dres1<false>, dim3(ns, 8), dim3(64), 0, s, D);
+            hipLaunchKernelGGL(k_dres1<false>, dim3(ns, DRES_WAVES), dim3(64), 0, s, D);
         } else {
-            hipLaunchKernelGGL(k_dres1<true>, dim3(ns, 8), dim3(64), 0, s, D);
+            hipLaunchKernelGGL(k_dres1<true>, dim3(ns, DRES_WAVES), dim3(64), 0, s, D);
         }
         DHIP(hipGetLastError());
-        hipLaunchKernelGGL(k_dres2, dim3(ns, 8), dim3(64), 0, s, D);
+        hipLaunchKernelGGL(k_dres2, dim3(ns, DRES_WAVES), dim3(64), 0, s, D);
         DHIP(hipGetLastError());
         hipLaunchKernelGGL(k_dstop, dim3((ns + 3) / 4), dim3(256), 0, s, D);
         DHIP(hipGetLastError());
