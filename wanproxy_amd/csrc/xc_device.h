@@ -248,13 +248,12 @@ __device__ __forceinline__ uint64_t block_group_hash(const uint32_t w[G][8])
     return ((uint64_t)bits_hash << 36) + (uint64_t)bytes_hash;
 }
 
-// Hashes of n <= 8 consecutive 16-byte-aligned blocks at p: all loads are issued first, then
-// lane i (< n) receives block i's hash.
+// The words of n <= G consecutive 16-byte-aligned blocks at p (lane l: bytes 32 l .. 32 l + 31 of
+// each; zeros past n), all loads issued together.
 template <int G>
-__device__ __forceinline__ uint64_t wave_block_hashes(const uint8_t *p, uint32_t n)
+__device__ __forceinline__ void wave_load_blocks(const uint8_t *p, uint32_t n, uint32_t (&w)[G][8])
 {
     const uint32_t l = lane_id();
-    uint32_t w[G][8];
 #pragma unroll
     for (int i = 0; i < G; i++) {
 #pragma unroll
@@ -266,6 +265,14 @@ __device__ __forceinline__ uint64_t wave_block_hashes(const uint8_t *p, uint32_t
             w[i][4] = y.x; w[i][5] = y.y; w[i][6] = y.z; w[i][7] = y.w;
         }
     }
+}
+
+// Hashes of n <= 8 consecutive 16-byte-aligned blocks at p: lane i (< n) receives block i's hash.
+template <int G>
+__device__ __forceinline__ uint64_t wave_block_hashes(const uint8_t *p, uint32_t n)
+{
+    uint32_t w[G][8];
+    wave_load_blocks<G>(p, n, w);
     return block_group_hash<G>(w);
 }
 

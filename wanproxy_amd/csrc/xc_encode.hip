@@ -1076,7 +1076,9 @@ __global__ __launch_bounds__(256) void k_blockhash(DeclArgs a)
     const uint32_t b = gr.x, k0 = gr.y;
     const uint8_t *base = P.in + P.buf_off[b];
     const uint32_t n = min(BLK_GROUP, P.buf_len[b] / XC_SEG - k0);
-    const uint64_t h = wave_block_hashes<BLK_GROUP>(base + (size_t)k0 * XC_SEG, n);
+    uint32_t w[BLK_GROUP][8];  // (kept for the compares below)
+    wave_load_blocks<BLK_GROUP>(base + (size_t)k0 * XC_SEG, n, w);
+    const uint64_t h = block_group_hash<BLK_GROUP>(w);
     const uint32_t l = lane_id();
     const uint32_t gi = P.blk_base[b] + k0 + l;
     uint32_t cmp = 0;  // the cached slot + 1 to compare the block with (blk_cmp)
@@ -1091,31 +1093,31 @@ __global__ __launch_bounds__(256) void k_blockhash(DeclArgs a)
             if (set_find(P.cache, h, &v) && (uint32_t)v < *a.limit) cmp = (uint32_t)v + 1u;
         }
     }
-    // the compares of a predicted REF's bytes, off k_resolve's critical path: four blocks per
-    // pass, all loads in flight (both sides 16-byte aligned)
+    // the compares of a predicted REF's bytes, off k_resolve's critical path, against the block
+    // words still in registers: four blocks per pass, their segments' loads all in flight
     uint32_t verdict = cmp;
-    for (uint64_t m = ballot(cmp != 0u); m;) {
-        int f[4];
-        uint4 x[4][2], y[4][2];
+    if (ballot(cmp != 0u)) {
 #pragma unroll
-        for (int g = 0; g < 4; g++) {
-            f[g] = m ? __ffsll((unsigned long long)m) - 1 : -1;
-            if (m) m &= m - 1;
-            if (f[g] >= 0) {
-                const uint32_t slot = readlane(cmp, f[g]) - 1u;
-                const uint4 *xp = (const uint4 *)(base + (size_t)(k0 + f[g]) * XC_SEG + 32u * l);
-                const uint4 *yp = (const uint4 *)(P.segs + (size_t)slot * XC_SEG + 32u * l);
-                x[g][0] = xp[0]; x[g][1] = xp[1];
-                y[g][0] = yp[0]; y[g][1] = yp[1];
+        for (int g0 = 0; g0 < (int)BLK_GROUP; g0 += 4) {
+            uint4 y[4][2];
+            uint32_t slot[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                slot[i] = readlane(cmp, g0 + i);
+                if (slot[i]) {
+                    const uint4 *yp = (const uint4 *)(P.segs + (size_t)(slot[i] - 1u) * XC_SEG + 32u * l);
+                    y[i][0] = yp[0];
+                    y[i][1] = yp[1];
+                }
             }
-        }
 #pragma unroll
-        for (int g = 0; g < 4; g++) {
-            if (f[g] < 0) continue;
-            const uint32_t diff = (x[g][0].x ^ y[g][0].x) | (x[g][0].y ^ y[g][0].y) | (x[g][0].z ^ y[g][0].z) |
-                                  (x[g][0].w ^ y[g][0].w) | (x[g][1].x ^ y[g][1].x) | (x[g][1].y ^ y[g][1].y) |
-                                  (x[g][1].z ^ y[g][1].z) | (x[g][1].w ^ y[g][1].w);
-            if (ballot(diff != 0u) && (int)l == f[g]) verdict |= BC_DIFF;
+            for (int i = 0; i < 4; i++) {
+                if (!slot[i]) continue;
+                const uint32_t *x = w[g0 + i];
+                const uint32_t diff = (x[0] ^ y[i][0].x) | (x[1] ^ y[i][0].y) | (x[2] ^ y[i][0].z) | (x[3] ^ y[i][0].w) |
+                                      (x[4] ^ y[i][1].x) | (x[5] ^ y[i][1].y) | (x[6] ^ y[i][1].z) | (x[7] ^ y[i][1].w);
+                if (ballot(diff != 0u) && (int)l == g0 + i) verdict |= BC_DIFF;
+            }
         }
     }
     if (l < n) P.blk_cmp[gi] = verdict;
