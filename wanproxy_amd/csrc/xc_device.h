@@ -422,25 +422,23 @@ struct DevSet {
     uint64_t *vals;
 };
 
-__device__ __forceinline__ uint32_t filt_word(uint32_t lo)
-{
-    return (uint32_t)(((uint64_t)(lo >> 8) * (uint64_t)(XC_FILT_WORDS << 8)) >> 32);
-}
-// The same word for a filter of `words` words (XC_FILT_WORDS >> fold: the folded image)
+// Word of a filter of `words` words (XC_FILT_WORDS >> fold: the folded image, whose word w is the
+// OR of the full image's words w << fold ..): floor(lo[23:0] * words / 2^24), one full-rate
+// v_mul_hi_u32_u24 on lo itself (the unit ignores lo[31:24]; both operands must be provably
+// 24-bit, or the compiler emits the quarter-rate 32-bit v_mul_hi_u32).
 __device__ __forceinline__ uint32_t filt_word_n(uint32_t lo, uint32_t words)
 {
-    return (uint32_t)(((uint64_t)(lo >> 8) * (uint64_t)(words << 8)) >> 32);
+    return (uint32_t)(((uint64_t)(lo & 0xFFFFFFu) * (uint64_t)((words << 8) & 0xFFFFFFu)) >> 32);
 }
+__device__ __forceinline__ uint32_t filt_word(uint32_t lo) { return filt_word_n(lo, XC_FILT_WORDS); }
+// The key's two bits in its word: lo[4:0] and lo[31:27] (outside the bits that pick the word).
+__device__ __forceinline__ uint32_t filt_mask(uint32_t lo) { return (1u << (lo & 31u)) | (1u << (lo >> 27)); }
 __device__ __forceinline__ uint32_t filt_test_n(const uint32_t *f, uint32_t lo, uint32_t words)
 {
     const uint32_t w = f[filt_word_n(lo, words)];
-    return (w >> (lo & 31u)) & (w >> ((lo >> 5) & 31u)) & 1u;
+    return (w >> (lo & 31u)) & (w >> (lo >> 27)) & 1u;
 }
-__device__ __forceinline__ uint32_t filt_test(const uint32_t *f, uint32_t lo)
-{
-    const uint32_t w = f[filt_word(lo)];
-    return (w >> (lo & 31u)) & (w >> ((lo >> 5) & 31u)) & 1u;
-}
+__device__ __forceinline__ uint32_t filt_test(const uint32_t *f, uint32_t lo) { return filt_test_n(f, lo, XC_FILT_WORDS); }
 __device__ __forceinline__ uint32_t lo_slot(uint32_t lo, uint32_t mask) { return (lo * 0x9E3779B1u) >> 5 & mask; }
 __device__ __forceinline__ uint32_t key_slot(uint64_t h, uint32_t mask)
 {
@@ -495,7 +493,7 @@ __device__ __forceinline__ int set_insert(const DevSet &s, uint64_t h, uint64_t 
     // for a key already present changes nothing
     {
         const uint32_t lo = (uint32_t)h;
-        atomicOr(&s.filt[filt_word(lo)], (1u << (lo & 31u)) | (1u << ((lo >> 5) & 31u)));
+        atomicOr(&s.filt[filt_word(lo)], filt_mask(lo));
         const uint32_t g = l2_mix(lo);
         atomicOr(&s.l2[l2_word(g)], (1u << (g & 31u)) | (1u << ((g >> 5) & 31u)));
     }

@@ -1148,7 +1148,7 @@ __device__ __forceinline__ uint32_t block_predict(const PlanDev &P, uint32_t g, 
         uint32_t slot;
         set_insert(P.dset, h, ((uint64_t)b << 32) | (k * XC_SEG + 2u * XC_SEG - 1u), true, &slot, nullptr);
         const uint32_t lo = (uint32_t)h;  // (the combined level-1 image the first scan loads)
-        atomicOr(&P.fmix[filt_word_n(lo, XC_FILT_WORDS >> P.fmix_fold)], (1u << (lo & 31u)) | (1u << ((lo >> 5) & 31u)));
+        atomicOr(&P.fmix[filt_word_n(lo, XC_FILT_WORDS >> P.fmix_fold)], filt_mask(lo));
         pref = BP_DECL | slot;
     }
     P.blk_pref[g] = pref;
