@@ -405,6 +405,14 @@ __device__ __forceinline__ uint32_t l2_mix(uint32_t lo)
     return g ^ (g >> 12);
 }
 
+// lo from l2_mix(lo) (both steps invert: an xorshift, and a multiply by an odd constant)
+__device__ __forceinline__ uint32_t l2_unmix(uint32_t g)
+{
+    g ^= (g >> 12) ^ (g >> 24);
+    g *= 0x64EA2D65u;  // 0x2C1B3C6D^-1 mod 2^32
+    return g ^ (g >> 15) ^ (g >> 30);
+}
+
 __device__ __forceinline__ uint32_t l2_word(uint32_t g) { return g >> 13; }
 __device__ __forceinline__ bool l2_test(uint32_t w, uint32_t g)
 {

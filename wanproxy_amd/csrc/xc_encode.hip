@@ -82,7 +82,7 @@ __device__ __forceinline__ bool scan_has_lo(const ScanArgs &a, uint32_t lo)
 struct Pending {
     uint32_t n;          // entries (uniform); 0 = nothing pending
     uint32_t c, c0;      // chunk the entries belong to
-    uint32_t pos[2], lo[2];
+    uint32_t pos[2], lo[2];  // lo: l2_mix of the window's lo32
     uint32_t w[2];
 };
 
@@ -100,8 +100,8 @@ __device__ __forceinline__ void pend_issue(const ScanArgs &a, Pending &pd, const
         const uint2 e = queue[i];
         const bool v = i < qn;
         pd.pos[s] = v ? e.x : 0u;
-        pd.lo[s] = v ? e.y : 0u;
-        pd.w[s] = a.l2[v ? l2_word(l2_mix(e.y)) : 0u];
+        pd.lo[s] = l2_mix(e.y);  // (kept mixed: the exact probe unmixes its few survivors)
+        pd.w[s] = a.l2[v ? l2_word(pd.lo[s]) : 0u];
     }
 }
 
@@ -113,8 +113,9 @@ __device__ __forceinline__ void pend_complete(const ScanArgs &a, Pending &pd, ui
         if (64u * s >= pd.n) break;
         const uint32_t i = lane_id() + 64u * s;
         bool match = false;
-        if (i < pd.n && l2_test(pd.w[s], l2_mix(pd.lo[s]))) {
-            match = MODE == 5 ? pd.lo[s] == 0x12345u : scan_has_lo(a, pd.lo[s]);
+        if (i < pd.n && l2_test(pd.w[s], pd.lo[s])) {
+            const uint32_t x = l2_unmix(pd.lo[s]);
+            match = MODE == 5 ? x == 0x12345u : scan_has_lo(a, x);
         }
         scan_record(a, pd.c, pd.c0, match, pd.pos[s], ev_n, dense);
     }
@@ -192,6 +193,10 @@ __device__ __forceinline__ const uint8_t *desc_base(const ScanArgs &a, const uin
 // every lane (one round trip) instead of queueing them for the next iteration's batch.
 #ifndef XC_DIRECT_MIN
 #define XC_DIRECT_MIN Q_CAP
+#endif
+// Level-2 loads of the direct path in flight at once (16 spills registers).
+#ifndef XC_DIRECT_GROUP
+#define XC_DIRECT_GROUP 8
 #endif
 
 template <int MODE>
@@ -337,23 +342,35 @@ __global__ __launch_bounds__(64 * SCAN_WAVES) void k_scan(ScanArgs a)
                     if (MODE == 4) {
                         sink = sink * 31u + hit;
                     } else {
+                        // lo[j] becomes its level-2 mix in place (inverted for the rare survivors);
+                        // every lane loads (word 0 for non-positives: one coalesced request), so all
+                        // 16 loads are in flight and the tests wait for them in order, branch-free
+                        uint32_t pm = 0;
 #pragma unroll
-                        for (int g0 = 0; g0 < 16; g0 += 8) {  // (two groups of 8: registers)
-                            uint32_t w2[8];
+                        for (int g0 = 0; g0 < 16; g0 += XC_DIRECT_GROUP) {  // (groups: registers)
+                            uint32_t w2[XC_DIRECT_GROUP];
 #pragma unroll
-                            for (int j = 0; j < 8; j++) {
-                                w2[j] = 0u;
-                                if ((hit >> (g0 + j)) & 1u) w2[j] = a.l2[l2_word(l2_mix(lo[g0 + j]))];
+                            for (int j = 0; j < XC_DIRECT_GROUP; j++) {
+                                lo[g0 + j] = l2_mix(lo[g0 + j]);
+                                w2[j] = a.l2[((hit >> (g0 + j)) & 1u) ? l2_word(lo[g0 + j]) : 0u];
                             }
 #pragma unroll
-                            for (int j = 0; j < 8; j++) {
-                                const bool pass = ((hit >> (g0 + j)) & 1u) && l2_test(w2[j], l2_mix(lo[g0 + j]));
-                                if (ballot(pass)) {  // (rare: level-2 survivors)
-                                    const bool match =
-                                        pass && (MODE == 5 ? lo[g0 + j] == 0x12345u : scan_has_lo(a, lo[g0 + j]));
-                                    scan_record(a, c, c0, match, q + 16u * half + (uint32_t)(g0 + j), ev_n, dense);
-                                }
-                            }
+                            for (int j = 0; j < XC_DIRECT_GROUP; j++)
+                                pm |= (uint32_t)l2_test(w2[j], lo[g0 + j]) << (g0 + j);
+                        }
+                        pm &= hit;
+                        // level-2 survivors (few): each lane its lowest one per round, exact lo32 sets
+                        for (;;) {
+                            const bool any = pm != 0u;
+                            if (!ballot(any)) break;
+                            const uint32_t j = any ? (uint32_t)__builtin_ctz(pm) : 0u;
+                            pm &= pm - 1u;
+                            uint32_t g = lo[0];
+#pragma unroll
+                            for (int jj = 1; jj < 16; jj++) g = j == (uint32_t)jj ? lo[jj] : g;
+                            const uint32_t x = l2_unmix(g);
+                            const bool match = any && (MODE == 5 ? x == 0x12345u : scan_has_lo(a, x));
+                            scan_record(a, c, c0, match, q + 16u * half + j, ev_n, dense);
                         }
                     }
                 }
@@ -1791,6 +1808,10 @@ __global__ void k_selftest(uint32_t *err)
     if (inc != ref) atomicOr(err, 1u);
     const uint64_t m = ballot((l & 3) == 1);
     if (mbcnt(m) != (l + 2) / 4) atomicOr(err, 2u);
+    for (uint32_t k = 0; k < 64; k++) {  // the scan's level-2 mix inverts
+        const uint32_t v = (x ^ (k * 0x9E3779B9u)) * (k | 1u);
+        if (l2_unmix(l2_mix(v)) != v) atomicOr(err, 4u);
+    }
 }
 
 }  // namespace xc
