@@ -108,6 +108,7 @@ def bench_encode_leg(ctx, warm, bufs, steps, case):
     cache.snapshot()
     lens = np.array([b.size for b in bufs], np.uint64)
     plan = w.EncodePlan(cache, lens)
+    plan.set_completion(True)  # (stream ordered: every read below follows a device synchronize)
     arena = np.zeros(plan.in_bytes, np.uint8)
     for i, b in enumerate(bufs):
         arena[int(plan.in_off[i]):int(plan.in_off[i]) + b.size] = b
@@ -307,6 +308,7 @@ def main():
 
     lens = np.full(n_local, W.BUF, dtype=np.uint64)
     plan = w.EncodePlan(cache, lens)
+    plan.set_completion(True)  # (stream ordered: every read below follows a device synchronize)
     assert all(int(plan.in_off[i]) == i * W.BUF for i in range(n_local))
     d_in = torch.zeros(plan.in_bytes, dtype=torch.uint8, device="cuda")
     d_in[:n_local * W.BUF] = torch.from_numpy(shard.reshape(-1)).cuda()

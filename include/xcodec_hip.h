@@ -108,6 +108,18 @@ int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_o
 int xc_encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_out_len);
 int xc_encode_poll(xc_plan *p, int *done);
 int xc_encode_wait(xc_plan *p);
+/* When xc_encode_run / xc_encode_wait / xc_encode_poll report a run finished:
+ * XC_COMPLETE_RUN (the default): every device write of the run is complete;
+ * XC_COMPLETE_STREAM: the run is decided (its control words are final, the host has nothing left
+ * to do) and its remaining device work completes in the order of the context stream
+ * (xc_ctx_stream): work enqueued there afterwards (the next run, a restore, a copy of the outputs)
+ * sees the results; other streams and the host must synchronize with that stream first
+ * (xc_ctx_sync).  The host then returns while the last kernel still writes the wire bytes, so the
+ * next call's launches overlap it.  Applies to device-resident one-sub-batch runs (the captured
+ * graph); others complete as with XC_COMPLETE_RUN. */
+#define XC_COMPLETE_RUN 0
+#define XC_COMPLETE_STREAM 1
+int xc_plan_set_completion(xc_plan *p, int mode);
 /* Host-to-host convenience: pinned H2D, xc_encode_run, D2H.  out_len receives nbuf lengths. */
 int xc_encode_batch_host(xc_cache *c, const uint8_t *in, const uint64_t *in_off,
                          const uint64_t *in_len, uint64_t nbuf, uint8_t *out,

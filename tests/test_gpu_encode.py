@@ -492,6 +492,68 @@ def test_submit_poll_wait(gpu_ctx, oracle_mod, monkeypatch, sub_mb):
     assert len(set(stats)) == 1 and stats[0][1] > 0, stats
 
 
+@pytest.mark.parametrize("mixed", [False, True])
+def test_stream_ordered_completion(gpu_ctx, oracle_mod, monkeypatch, mixed):
+    """xc_plan_set_completion(XC_COMPLETE_STREAM): runs return once decided (the graph's emit
+    has published the control words) and the rest completes in context-stream order, so
+    back-to-back restore + run calls with no host synchronisation in between (run, submit + wait,
+    submit + poll) each produce the oracle's bytes; a batch whose sub-batch the gate hands back to
+    the host (mixed: cross-buffer duplicates, self references) and one that never does."""
+    import time
+    import torch
+    import wanproxy_amd as w
+    from wanproxy_amd import workloads as W
+    monkeypatch.setenv("XC_SUB_MB", "64")  # one sub-batch: the graph path
+    if mixed:
+        bufs, warm = _mixed_batch()
+    else:
+        bufs, warm = list(W.repeat_shard(96, 0x77)), [W.pool_warmup_buffers()]
+    oc = oracle_mod.Cache()
+    for batch in warm:
+        oc.encode_batch(batch)
+    want = oc.encode_batch(bufs)
+    cache = w.XCodecCache(gpu_ctx, 1 << 15)
+    for batch in warm:
+        w.XCodecEncoder(cache).encode_batch(batch)
+    cache.snapshot()
+    plan = w.EncodePlan(cache, [len(b) for b in bufs])
+    plan.set_completion(True)
+    arena = np.zeros(plan.in_bytes, np.uint8)
+    for i, b in enumerate(bufs):
+        arena[int(plan.in_off[i]):int(plan.in_off[i]) + len(b)] = b
+    d_in = torch.from_numpy(arena).cuda()
+    outs = [torch.zeros(plan.out_bytes, dtype=torch.uint8, device="cuda") for _ in range(3)]
+    lens = [torch.zeros(len(bufs), dtype=torch.int64, device="cuda") for _ in range(3)]
+    torch.cuda.synchronize()
+    stats = []
+    for it in range(9):
+        d_out, d_len = outs[it % 3], lens[it % 3]
+        cache.restore_async()
+        if it % 3 == 0:
+            plan.run(d_in.data_ptr(), d_out.data_ptr(), d_len.data_ptr())
+        else:
+            plan.submit(d_in.data_ptr(), d_out.data_ptr(), d_len.data_ptr())
+            if it % 3 == 1:
+                plan.wait()
+            else:
+                t0 = time.time()
+                while not plan.poll():
+                    assert time.time() - t0 < 60
+        st = plan.stats()
+        stats.append((st.sub_batches, st.redone, st.n_extract, st.n_ref))
+    gpu_ctx.sync()
+    torch.cuda.synchronize()
+    for k in range(3):
+        out, ln = outs[k].cpu().numpy(), lens[k].cpu().numpy()
+        for i in range(len(bufs)):
+            o = int(plan.out_off[i])
+            assert out[o:o + int(ln[i])].tobytes() == want[i], (k, i)
+    assert len(set(stats)) == 1 and (stats[0][1] > 0) == mixed, stats
+    plan.set_completion(False)
+    plan.close()
+    cache.close()
+
+
 def test_cache_grows_like_the_reference_map(gpu_ctx, oracle_mod):
     """The reference's memory cache never fills (xcodec/xcodec_cache.h:164,182-188).  A device
     cache created for 1024 segments takes ten times that through several batches, a snapshot taken

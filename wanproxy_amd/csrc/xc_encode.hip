@@ -1235,7 +1235,10 @@ __device__ __forceinline__ void ctl_publish(const EmitArgs &a)
 {
     if (!a.ctl_host) return;
     __threadfence();
-    for (uint32_t i = 0; i < CTL_WORDS; i++) a.ctl_host[i] = __atomic_load_n(&a.P.ctl[i], __ATOMIC_RELAXED);
+    for (uint32_t i = 0; i + 1u < CTL_WORDS; i++) a.ctl_host[i] = __atomic_load_n(&a.P.ctl[i], __ATOMIC_RELAXED);
+    // the last word (unused: 0) clears the host's sentinel only after the others are visible
+    __threadfence_system();
+    a.ctl_host[CTL_WORDS - 1] = __atomic_load_n(&a.P.ctl[CTL_WORDS - 1], __ATOMIC_RELAXED);
     __threadfence_system();
 }
 

@@ -769,6 +769,7 @@ struct xc_plan {
     uint32_t *emit_ctl_host = nullptr;  // set while a graph whose last emit publishes is captured
     bool g_publish = false;      // the captured graph's emit publishes the control words
     bool pass_published = false;  // the in-flight first pass publishes them (else a copy)
+    int completion = XC_COMPLETE_RUN;  // xc_plan_set_completion
     bool inflight = false;        // xc_encode_submit enqueued a run not finished yet
     hipEvent_t ev_ctl = nullptr;
     std::vector<hipEvent_t> ev_hash, ev_go;
@@ -1253,6 +1254,34 @@ static int ctl_buffers(xc_plan *p)
     return XC_OK;
 }
 
+// XC_COMPLETE_STREAM: a published first pass is decided once the emit's publication has cleared
+// the sentinel in the last control word (it is written last); the event covers a pass that
+// published nothing (the caller then reads the words).
+static bool published(const xc_plan *p)
+{
+    if (*(volatile const uint32_t *)(p->h_ctl + CTL_WORDS - 1) != 0u) return false;
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    return true;
+}
+
+static bool early_done(const xc_plan *p)
+{
+    return p->completion == XC_COMPLETE_STREAM && p->pass_published;
+}
+
+static hipError_t wait_decided(xc_plan *p)
+{
+    if (!early_done(p)) return spin_wait(p->ev_ctl);
+    for (int i = 0;; i++) {
+        if (published(p)) return hipSuccess;
+        if ((i & 15) == 15) {
+            const hipError_t e = hipEventQuery(p->ev_ctl);
+            if (e != hipErrorNotReady) return e;
+            if (i >= 1024) sched_yield();
+        }
+    }
+}
+
 // Wait for the copy of the control words enqueued before ev_ctl.
 static int wait_ctl(xc_plan *p, uint32_t *ctl);
 
@@ -1670,7 +1699,7 @@ extern "C" int xc_encode_poll(xc_plan *p, int *done)
     if (!p->inflight) return fail(XC_EINVAL, "no run in flight");
     int rc = set_dev(p->cache->ctx);
     if (rc) return rc;
-    const hipError_t e = hipEventQuery(p->ev_ctl);
+    const hipError_t e = early_done(p) && published(p) ? hipSuccess : hipEventQuery(p->ev_ctl);
     if (e == hipErrorNotReady) {
         *done = 0;
         return XC_OK;
@@ -1689,12 +1718,20 @@ extern "C" int xc_encode_wait(xc_plan *p)
     if (!p->inflight) return fail(XC_EINVAL, "no run in flight");
     int rc = set_dev(p->cache->ctx);
     if (rc) return rc;
-    const hipError_t e = spin_wait(p->ev_ctl);
+    const hipError_t e = wait_decided(p);
     if (e != hipSuccess) {
         p->inflight = false;
         return fail(XC_EDEVICE, std::string("run: ") + hipGetErrorString(e));
     }
     return encode_finish(p);
+}
+
+extern "C" int xc_plan_set_completion(xc_plan *p, int mode)
+{
+    if (!p || (mode != XC_COMPLETE_RUN && mode != XC_COMPLETE_STREAM)) return fail(XC_EINVAL, "completion mode");
+    if (p->inflight) return fail(XC_EBUSY, "a run of this plan is in flight");
+    p->completion = mode;
+    return XC_OK;
 }
 
 extern "C" int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_out_len)

@@ -39,6 +39,7 @@ SYMBOLS = [
     "xc_coss_open", "xc_coss_close", "xc_coss_cache", "xc_coss_count", "xc_coss_stats", "xc_coss_lookup",
     "xc_coss_enter", "xc_coss_encode_batch_host", "xc_coss_decode_batch_host", "xc_coss_store_lookup",
     "xc_coss_store_enter", "xc_coss_encode_streams", "xc_encode_submit", "xc_encode_poll", "xc_encode_wait",
+    "xc_plan_set_completion",
 ]
 STREAM_FLUSH = 1  # XC_STREAM_FLUSH
 
@@ -115,6 +116,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.xc_encode_submit.argtypes = [_vp, _vp, _vp, _vp]
     lib.xc_encode_poll.argtypes = [_vp, C.POINTER(C.c_int)]
     lib.xc_encode_wait.argtypes = [_vp]
+    lib.xc_plan_set_completion.argtypes = [_vp, C.c_int]
     lib.xc_plan_stats.argtypes = [_vp, C.POINTER(RunStats)]
     lib.xc_encode_batch_host.argtypes = [_vp, _u8p, _u64p, _u64p, C.c_uint64, _u8p, _u64p, _u64p,
                                          _u64p]
@@ -535,6 +537,12 @@ class EncodePlan:
 
     def run(self, d_in: int, d_out: int, d_len: int) -> None:
         _check(load_library().xc_encode_run(self.h, d_in, d_out, d_len))
+
+    def set_completion(self, stream_ordered: bool) -> None:
+        """xc_plan_set_completion: with ``stream_ordered`` a run returns once it is decided and
+        its last device writes complete in the order of the context stream (synchronize with
+        ``Context.sync()`` or the device before reading the outputs from another stream)."""
+        _check(load_library().xc_plan_set_completion(self.h, 1 if stream_ordered else 0))
 
     def submit(self, d_in: int, d_out: int, d_len: int) -> None:
         """Enqueue a run and return at once (xc_encode_submit); finish it with poll() / wait()."""
