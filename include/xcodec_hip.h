@@ -115,8 +115,8 @@ int xc_encode_wait(xc_plan *p);
  * (xc_ctx_stream): work enqueued there afterwards (the next run, a restore, a copy of the outputs)
  * sees the results; other streams and the host must synchronize with that stream first
  * (xc_ctx_sync).  The host then returns while the last kernel still writes the wire bytes, so the
- * next call's launches overlap it.  Applies to device-resident one-sub-batch runs (the captured
- * graph); others complete as with XC_COMPLETE_RUN. */
+ * next call's launches overlap it.  Applies to device-resident runs without per-kernel timing (a
+ * run whose sub-batch the host redoes returns after the redo). */
 #define XC_COMPLETE_RUN 0
 #define XC_COMPLETE_STREAM 1
 int xc_plan_set_completion(xc_plan *p, int mode);

@@ -1469,6 +1469,7 @@ __global__ __launch_bounds__(1024) void k_alloc(EmitArgs a)
         P.ctl[CTL_NEXTRACT] += carry[0] - start;
         P.ctl[CTL_NREF] += carry[1];
         if (carry[0] > P.seg_cap) P.ctl[CTL_ERROR] |= ERR_CAPACITY;
+        ctl_publish(a);  // (the pass's last sub-batch: its emit changes no control word)
     }
 }
 

@@ -1365,7 +1365,9 @@ static int launch_emit(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t jc, uint32
     hipStream_t s = p->cache->ctx->stream;
     // few buffers: the slots inside the emit (one launch less)
     const bool slots = jc > j0 && jc - j0 <= EMIT_SLOTS_MAX;
-    EmitArgs e{p->P, j0, jc, gate_sb, slots ? p->emit_ctl_host : nullptr, p->P.sb_count + sb};
+    // (the pass's last sub-batch publishes the control words: from the emit when it takes the
+    // slots, else from k_alloc; the non-slot emit never reads ctl_host)
+    EmitArgs e{p->P, j0, jc, gate_sb, p->emit_ctl_host, p->P.sb_count + sb};
     if (!slots) {
         hipLaunchKernelGGL(k_alloc, dim3(1), dim3(1024), 0, s, e);
         HIPCHK(hipGetLastError());
@@ -1543,7 +1545,7 @@ static int graph_launch(xc_plan *p)
         // a one-sub-batch graph whose emit takes the slots also publishes the control words
         // (no copy launch after it)
         const uint32_t nlast = p->sub[nsub] - p->sub[nsub - 1];
-        const bool publish = nsub == 1 && nlast > 0 && nlast <= EMIT_SLOTS_MAX && !p->host_path;
+        const bool publish = nsub == 1 && nlast > 0 && !p->host_path;
         HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
         const xc_run_stats st0 = p->stats;
         p->emit_ctl_host = publish ? p->d_hctl : nullptr;
@@ -1634,10 +1636,20 @@ extern "C" int xc_encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out,
     if (use_graph(p)) {
         if ((rc = graph_launch(p))) return rc;
     } else {
-        p->pass_published = false;
-        for (size_t k = 0; k < nsub; k++)
-            if ((rc = encode_sub_async(p, (uint32_t)k))) return rc;
-        HIPCHK(hipMemcpyAsync(p->h_ctl, p->P.ctl, CTL_WORDS * 4, hipMemcpyDeviceToHost, s));
+        // stream-ordered completion: the last sub-batch's k_alloc (or slot-taking emit) publishes
+        // the control words, so the host returns before the last emit has finished (no copy of
+        // the words after it: a copy landing after the host re-armed the sentinel would clear it)
+        const bool pub = p->completion == XC_COMPLETE_STREAM && !p->timing && !p->host_path && nsub > 0 &&
+                         p->sub[nsub] > p->sub[nsub - 1];
+        if (pub) p->h_ctl[CTL_WORDS - 1] = 0xFFFFFFFFu;
+        p->pass_published = pub;
+        for (size_t k = 0; k < nsub; k++) {
+            p->emit_ctl_host = pub && k + 1 == nsub ? p->d_hctl : nullptr;
+            rc = encode_sub_async(p, (uint32_t)k);
+            p->emit_ctl_host = nullptr;
+            if (rc) return rc;
+        }
+        if (!pub) HIPCHK(hipMemcpyAsync(p->h_ctl, p->P.ctl, CTL_WORDS * 4, hipMemcpyDeviceToHost, s));
         if ((rc = record_ctl(p))) return rc;
     }
     p->inflight = true;
