@@ -492,18 +492,20 @@ def test_submit_poll_wait(gpu_ctx, oracle_mod, monkeypatch, sub_mb):
     assert len(set(stats)) == 1 and stats[0][1] > 0, stats
 
 
+@pytest.mark.parametrize("sub_mb", ["64", "1"])
 @pytest.mark.parametrize("mixed", [False, True])
-def test_stream_ordered_completion(gpu_ctx, oracle_mod, monkeypatch, mixed):
+def test_stream_ordered_completion(gpu_ctx, oracle_mod, monkeypatch, mixed, sub_mb):
     """xc_plan_set_completion(XC_COMPLETE_STREAM): runs return once decided (the graph's emit
     has published the control words) and the rest completes in context-stream order, so
     back-to-back restore + run calls with no host synchronisation in between (run, submit + wait,
     submit + poll) each produce the oracle's bytes; a batch whose sub-batch the gate hands back to
-    the host (mixed: cross-buffer duplicates, self references) and one that never does."""
+    the host (mixed: cross-buffer duplicates, self references) and one that never does; one
+    sub-batch (the graph) and many (published by the last k_alloc, aborts by any gate)."""
     import time
     import torch
     import wanproxy_amd as w
     from wanproxy_amd import workloads as W
-    monkeypatch.setenv("XC_SUB_MB", "64")  # one sub-batch: the graph path
+    monkeypatch.setenv("XC_SUB_MB", sub_mb)  # 64: one sub-batch (the graph path)
     if mixed:
         bufs, warm = _mixed_batch()
     else:

@@ -1324,7 +1324,7 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
             P.ctl[CTL_NEXTRACT] += t.y;
             P.ctl[CTL_NREF] += t.z;
             if (count > P.seg_cap) P.ctl[CTL_ERROR] |= ERR_CAPACITY;
-            ctl_publish(a);
+            if (a.pub_final) ctl_publish(a);
         }
     }
     if (wave == 0) {
@@ -1429,7 +1429,10 @@ __global__ __launch_bounds__(1024) void k_alloc(EmitArgs a)
         __shared__ uint32_t stop;
         if (threadIdx.x == 0) {
             stop = gate_stop(a) ? 1u : 0u;
-            if (stop) gate_abort(a);
+            if (stop) {
+                gate_abort(a);
+                ctl_publish(a);
+            }
         }
         __syncthreads();
         if (stop) return;
@@ -1469,7 +1472,7 @@ __global__ __launch_bounds__(1024) void k_alloc(EmitArgs a)
         P.ctl[CTL_NEXTRACT] += carry[0] - start;
         P.ctl[CTL_NREF] += carry[1];
         if (carry[0] > P.seg_cap) P.ctl[CTL_ERROR] |= ERR_CAPACITY;
-        ctl_publish(a);  // (the pass's last sub-batch: its emit changes no control word)
+        if (a.pub_final) ctl_publish(a);  // (the pass's last sub-batch: its emit changes no word)
     }
 }
 

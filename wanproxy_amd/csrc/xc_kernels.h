@@ -199,10 +199,12 @@ struct EmitArgs {
     PlanDev P;
     uint32_t j0, j1;
     uint32_t gate_sb;  // k_alloc: async-pipeline gate for sub-batch gate_sb (NONE: no gate)
-    // k_emit<.., true>: the control words' final state also goes here (mapped pinned host
-    // memory; null: not wanted)
+    // k_alloc / k_emit<.., true>: the control words also go here (mapped pinned host memory;
+    // null: not wanted) when the gate stops the pass, and, on the pass's last sub-batch
+    // (pub_final), once they are final
     uint32_t *ctl_host;
     const uint32_t *base;  // k_emit<.., true>: the cache count at the sub-batch's start (P.sb_count)
+    uint32_t pub_final;
 };
 // Sub-batches of at most this many buffers take k_alloc's work inside k_emit (every workgroup
 // sums the buf_next of the buffers before it): one launch less on small batches.

@@ -766,7 +766,8 @@ struct xc_plan {
     hipEvent_t ev_start = nullptr;
     uint32_t *h_ctl = nullptr;  // pinned copy of the control words (read_ctl)
     uint32_t *d_hctl = nullptr;  // its device address (k_emit<.., true> publishes the words there)
-    uint32_t *emit_ctl_host = nullptr;  // set while a graph whose last emit publishes is captured
+    uint32_t *emit_ctl_host = nullptr;  // set while a pass that publishes its control words is enqueued
+    uint32_t emit_pub_final = 0;        // ... on its last sub-batch
     bool g_publish = false;      // the captured graph's emit publishes the control words
     bool pass_published = false;  // the in-flight first pass publishes them (else a copy)
     int completion = XC_COMPLETE_RUN;  // xc_plan_set_completion
@@ -1269,15 +1270,22 @@ static bool early_done(const xc_plan *p)
     return p->completion == XC_COMPLETE_STREAM && p->pass_published;
 }
 
+// Not published yet: has the stream drained (the pass ended without publishing: the caller reads
+// the words), or failed?
+static hipError_t pass_state(xc_plan *p)
+{
+    return published(p) ? hipSuccess : hipStreamQuery(p->cache->ctx->stream);
+}
+
 static hipError_t wait_decided(xc_plan *p)
 {
     if (!early_done(p)) return spin_wait(p->ev_ctl);
     for (int i = 0;; i++) {
         if (published(p)) return hipSuccess;
-        if ((i & 15) == 15) {
-            const hipError_t e = hipEventQuery(p->ev_ctl);
+        if ((i & 255) == 255) {
+            const hipError_t e = pass_state(p);
             if (e != hipErrorNotReady) return e;
-            if (i >= 1024) sched_yield();
+            if (i >= 4096) sched_yield();
         }
     }
 }
@@ -1367,7 +1375,7 @@ static int launch_emit(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t jc, uint32
     const bool slots = jc > j0 && jc - j0 <= EMIT_SLOTS_MAX;
     // (the pass's last sub-batch publishes the control words: from the emit when it takes the
     // slots, else from k_alloc; the non-slot emit never reads ctl_host)
-    EmitArgs e{p->P, j0, jc, gate_sb, p->emit_ctl_host, p->P.sb_count + sb};
+    EmitArgs e{p->P, j0, jc, gate_sb, p->emit_ctl_host, p->P.sb_count + sb, p->emit_pub_final};
     if (!slots) {
         hipLaunchKernelGGL(k_alloc, dim3(1), dim3(1024), 0, s, e);
         HIPCHK(hipGetLastError());
@@ -1523,6 +1531,9 @@ static bool use_graph(xc_plan *p)
 // the emit): the host reads them once it has passed.
 static int record_ctl(xc_plan *p)
 {
+    // a stream-ordered published pass needs no event (its marker costs ~4 us between passes):
+    // every outcome of the gate is published, and a stream query covers the rest
+    if (early_done(p)) return XC_OK;
     HIPCHK(hipEventRecord(p->ev_ctl, p->cache->ctx->stream));
     return XC_OK;
 }
@@ -1549,8 +1560,12 @@ static int graph_launch(xc_plan *p)
         HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
         const xc_run_stats st0 = p->stats;
         p->emit_ctl_host = publish ? p->d_hctl : nullptr;
-        for (size_t k = 0; k < nsub && !rc; k++) rc = encode_sub_async(p, (uint32_t)k);
+        for (size_t k = 0; k < nsub && !rc; k++) {
+            p->emit_pub_final = k + 1 == nsub;
+            rc = encode_sub_async(p, (uint32_t)k);
+        }
         p->emit_ctl_host = nullptr;
+        p->emit_pub_final = 0;
         if (!rc && !publish && hipMemcpyAsync(p->h_ctl, p->P.ctl, CTL_WORDS * 4, hipMemcpyDeviceToHost, s) != hipSuccess)
             rc = fail(XC_EDEVICE, "graph capture: control-word copy");
         hipGraph_t g = nullptr;
@@ -1644,9 +1659,11 @@ extern "C" int xc_encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out,
         if (pub) p->h_ctl[CTL_WORDS - 1] = 0xFFFFFFFFu;
         p->pass_published = pub;
         for (size_t k = 0; k < nsub; k++) {
-            p->emit_ctl_host = pub && k + 1 == nsub ? p->d_hctl : nullptr;
+            p->emit_ctl_host = pub ? p->d_hctl : nullptr;
+            p->emit_pub_final = k + 1 == nsub;
             rc = encode_sub_async(p, (uint32_t)k);
             p->emit_ctl_host = nullptr;
+            p->emit_pub_final = 0;
             if (rc) return rc;
         }
         if (!pub) HIPCHK(hipMemcpyAsync(p->h_ctl, p->P.ctl, CTL_WORDS * 4, hipMemcpyDeviceToHost, s));
@@ -1711,7 +1728,7 @@ extern "C" int xc_encode_poll(xc_plan *p, int *done)
     if (!p->inflight) return fail(XC_EINVAL, "no run in flight");
     int rc = set_dev(p->cache->ctx);
     if (rc) return rc;
-    const hipError_t e = early_done(p) && published(p) ? hipSuccess : hipEventQuery(p->ev_ctl);
+    const hipError_t e = early_done(p) ? pass_state(p) : hipEventQuery(p->ev_ctl);
     if (e == hipErrorNotReady) {
         *done = 0;
         return XC_OK;
