@@ -239,6 +239,11 @@ int xc_dplan_layout(xc_dplan *p, uint64_t *in_off, uint64_t *out_off, uint64_t *
 int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_out_len,
                   uint64_t *d_consumed, int32_t *d_status, uint64_t *d_unknown, int32_t *d_has_unknown);
 int xc_dplan_stats(xc_dplan *p, xc_decode_stats *st);
+/* As xc_plan_set_completion: with XC_COMPLETE_STREAM xc_decode_run returns once the batch is
+ * decided (its statistics and errors are final: the streams' stops, the cache slots) and the
+ * output copies and cache inserts complete in the order of the plan's stream (the context
+ * stream); a batch whose outputs may not fit their capacities returns after the whole run. */
+int xc_dplan_set_completion(xc_dplan *p, int mode);
 
 /* ---- persistent COSS cache: XCodecCacheCOSS (xcodec/cache/coss/xcodec_cache_coss.{h,cc}) ----
  *

@@ -118,9 +118,13 @@ def test_gpu_encode_gpu_decode_roundtrip(gpu_ctx):
     assert len(ec) == len(dc)
 
 
-def test_device_resident_decode_plan(gpu_ctx, oracle_mod):
+@pytest.mark.parametrize("stream_ordered", [False, True])
+def test_device_resident_decode_plan(gpu_ctx, oracle_mod, stream_ordered):
     """xc_decode_plan_create + xc_decode_run on HBM arenas, run twice over a restored cache
-    snapshot (the bench's step): same results as the oracle both times."""
+    snapshot (the bench's step): same results as the oracle both times.  Stream ordered
+    (xc_dplan_set_completion): the runs return once decided, back to back with no host
+    synchronisation; a plan whose capacities are too small still fails (k_dstop's bound stops the
+    early return)."""
     import torch
     import wanproxy_amd as w
     pool = W.pool(256)
@@ -145,15 +149,26 @@ def test_device_resident_decode_plan(gpu_ctx, oracle_mod):
         arena[int(plan.in_off[i]):int(plan.in_off[i]) + len(s)] = np.frombuffer(s, np.uint8)
     n = len(streams)
     d_in = torch.from_numpy(arena).cuda()
-    d_out = torch.zeros(plan.out_bytes, dtype=torch.uint8, device="cuda")
-    u64 = torch.zeros(3 * n, dtype=torch.int64, device="cuda")
-    i32 = torch.zeros(2 * n, dtype=torch.int32, device="cuda")
+    sets = [(torch.zeros(plan.out_bytes, dtype=torch.uint8, device="cuda"),
+             torch.zeros(3 * n, dtype=torch.int64, device="cuda"),
+             torch.zeros(2 * n, dtype=torch.int32, device="cuda")) for _ in range(2)]
+    plan.set_completion(stream_ordered)
+    torch.cuda.synchronize()
     for rep in range(2):
-        gc.restore()
-        torch.cuda.synchronize()
+        d_out, u64, i32 = sets[rep]
+        if stream_ordered:
+            gc.restore_async()
+        else:
+            gc.restore()
+            torch.cuda.synchronize()
         plan.run(d_in.data_ptr(), d_out.data_ptr(), u64.data_ptr(), u64.data_ptr() + 8 * n,
                  i32.data_ptr(), u64.data_ptr() + 16 * n, i32.data_ptr() + 4 * n)
-        torch.cuda.synchronize()
+        if not stream_ordered:
+            torch.cuda.synchronize()
+    gpu_ctx.sync()
+    torch.cuda.synchronize()
+    for rep in range(2):
+        d_out, u64, i32 = sets[rep]
         out = d_out.cpu().numpy()
         r64 = u64.cpu().numpy().astype(np.uint64)
         r32 = i32.cpu().numpy()
@@ -163,6 +178,14 @@ def test_device_resident_decode_plan(gpu_ctx, oracle_mod):
             assert int(r64[n + i]) == cons, (rep, i, "consumed")
             assert (int(r64[2 * n + i]) if r32[n + i] else None) == unk, (rep, i, "unknown")
             assert out[o:o + int(r64[i])].tobytes() == data, (rep, i, "bytes")
-        assert len(gc) == len(oc)
+    assert len(gc) == len(oc)
     st = plan.stats()
     assert st.n_entered > 0 and st.n_ref > 0 and st.rounds >= 1
+    small = w.DecodePlan(gc, lens, np.maximum(lens, 1))
+    small.set_completion(stream_ordered)
+    d_out, u64, i32 = sets[0]
+    gc.restore()
+    with pytest.raises(w.XCodecError):
+        small.run(d_in.data_ptr(), d_out.data_ptr(), u64.data_ptr(), u64.data_ptr() + 8 * n,
+                  i32.data_ptr(), u64.data_ptr() + 16 * n, i32.data_ptr() + 4 * n)
+    gpu_ctx.sync()

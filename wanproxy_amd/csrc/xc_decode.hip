@@ -19,6 +19,7 @@
 //              slots too), gather REF segments
 //   k_dcommit  enter the first-seen EXTRACT hashes in the cache
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <cstring>
@@ -60,9 +61,25 @@ struct DecDev {
     DevSet dset;
     uint32_t *ctl;
     int count;                 // k_dstop: count executed REF / EXTRACT tokens into ctl
+    uint32_t *ctl_host;        // k_dalloc: publish the control words here (mapped host memory)
 };
 
 enum : uint32_t { DCTL_FIX = 0, DCTL_ERR = 1, DCTL_NENTER = 2, DCTL_NREF = 3, DCTL_NEXTRACT = 4, DCTL_WORDS = 8 };
+// DCTL_ERR bits: 1 an output capacity is too small (k_demit), 2 the cache is full (k_dalloc),
+// 4 an output may not fit (k_dstop's bound: the words are then final only after k_demit)
+constexpr uint32_t DERR_MAYBE_OUT = 4u;
+
+// The control words to the run's mapped host buffer, the last word (unused: the host's sentinel)
+// cleared only after the others are visible (one thread).
+__device__ __forceinline__ void dctl_publish(const DecDev &D)
+{
+    if (!D.ctl_host) return;
+    __threadfence();
+    for (uint32_t i = 0; i + 1u < DCTL_WORDS; i++) D.ctl_host[i] = __atomic_load_n(&D.ctl[i], __ATOMIC_RELAXED);
+    __threadfence_system();
+    D.ctl_host[DCTL_WORDS - 1] = 0u;
+    __threadfence_system();
+}
 
 // Tokenizer window: 1 KiB of the stream in registers (lane l: bytes w0 + 16 l .. + 15) and the
 // lane's mask of F1 bytes at positions in [from, n).
@@ -279,16 +296,19 @@ __global__ __launch_bounds__(256) void k_dstop(DecDev D)
     if (j >= D.ns) return;
     const uint32_t tb = D.tok_base[j], n = D.tok_cnt[j];
     uint32_t t = n, nr = 0, ne = 0, nent = 0;
+    uint64_t lit = 0;  // literal bytes of the executed tokens and the stop token (escapes counted twice)
     for (uint32_t t0 = 0; t0 < n; t0 += 64u) {
         const uint32_t i = t0 + l;
-        uint32_t op = T_END, st = 0;
+        uint32_t op = T_END, st = 0, ll = 0;
         if (i < n) {
             op = D.t_op[tb + i];
             st = D.t_stat[tb + i];
+            ll = D.t_le[tb + i] - D.t_lb[tb + i];
         }
         // the first token that stops the decode: terminal, unknown REF or colliding EXTRACT
         const uint64_t brk = ballot(i < n && ((op != T_EXTRACT && op != T_REF) || st == R_UNKNOWN || st == R_COLL));
         const uint32_t k = brk ? (uint32_t)__ffsll((unsigned long long)brk) - 1u : 64u;
+        lit += wave_sum(l <= k ? ll : 0u);
         const bool ex = l < k && i < n;
         nr += (uint32_t)__popcll(ballot(ex && op == T_REF));
         ne += (uint32_t)__popcll(ballot(ex && op == T_EXTRACT));
@@ -301,6 +321,9 @@ __global__ __launch_bounds__(256) void k_dstop(DecDev D)
         }
     }
     if (l != 0) return;
+    // the output is at most the literal bytes plus a segment per executed EXTRACT / REF: when
+    // that may exceed the capacity, only k_demit's exact sizes decide (no early publication)
+    if (lit + (uint64_t)XC_SEG * (nr + ne) > D.out_cap[j]) atomicOr(&D.ctl[DCTL_ERR], DERR_MAYBE_OUT);
     // t = stopping token; its literal is output
     D.s_stop[j] = t + 1u;
     D.s_slot[j] = nent;
@@ -527,7 +550,10 @@ __global__ __launch_bounds__(64 * DEMIT_WAVES) void k_demit(DecDev D)
 // left in s_slot, on top of the current segment count (one workgroup).
 __global__ __launch_bounds__(1024) void k_dalloc(DecDev D)
 {
-    if (fix_pending(D)) return;
+    if (fix_pending(D)) {  // another resolution round: the host decides it now
+        if (threadIdx.x == 0) dctl_publish(D);
+        return;
+    }
     __shared__ uint32_t wsum[16];
     __shared__ uint2 csum[16];
     __shared__ uint32_t carry;
@@ -575,6 +601,9 @@ __global__ __launch_bounds__(1024) void k_dalloc(DecDev D)
         *D.seg_count = carry;
         D.ctl[DCTL_NENTER] = carry - start;
         if (carry > D.seg_cap) D.ctl[DCTL_ERR] |= 2u;
+        // final unless an output may overflow (k_demit then sets bit 1): the rest of the run
+        // changes no control word
+        if (!(D.ctl[DCTL_ERR] & DERR_MAYBE_OUT)) dctl_publish(D);
     }
 }
 
@@ -651,7 +680,9 @@ struct xc_dplan {
     xc_decode_stats stats{};
     std::vector<void *> owned;
     uint32_t *h_ctl = nullptr;    // pinned copy of the control words (the run's host wait)
+    uint32_t *d_hctl = nullptr;   // its device address (k_dalloc publishes there)
     hipEvent_t ev_ctl = nullptr;
+    int completion = XC_COMPLETE_RUN;  // xc_dplan_set_completion
     uint32_t cache_gen = 0;       // the cache arrays D holds (they move when the cache grows)
     template <class T>
     int alloc(T **p, size_t n)
@@ -661,6 +692,13 @@ struct xc_dplan {
         return XC_OK;
     }
 };
+
+extern "C" int xc_dplan_set_completion(xc_dplan *p, int mode)
+{
+    if (!p || (mode != XC_COMPLETE_RUN && mode != XC_COMPLETE_STREAM)) return xc__set_error(XC_EINVAL, "completion mode");
+    p->completion = mode;
+    return XC_OK;
+}
 
 extern "C" int xc_dplan_destroy(xc_dplan *p)
 {
@@ -831,17 +869,43 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
     // and the emit are enqueued together and the host waits once in the common case
     int rc0 = XC_OK;
     auto emit = [&]() -> int {
-        hipLaunchKernelGGL(k_dalloc, dim3(1), dim3(1024), 0, s, D);  // slots first: k_demit fills them
+        if (!p->h_ctl) {
+            if ((rc0 = xc__halloc((void **)&p->h_ctl, DCTL_WORDS * 4))) return rc0;
+            void *dp = nullptr;
+            DHIP(hipHostGetDevicePointer(&dp, p->h_ctl, 0));
+            p->d_hctl = (uint32_t *)dp;
+            DHIP(hipEventCreateWithFlags(&p->ev_ctl, hipEventDisableTiming));
+        }
+        // stream-ordered completion: k_dalloc publishes the words when they are final (a sentinel
+        // in the last word, cleared last) and the host returns while k_demit / k_dcommit run
+        const bool pub = p->completion == XC_COMPLETE_STREAM;
+        DecDev Da = D;
+        if (pub) {
+            p->h_ctl[DCTL_WORDS - 1] = 0xFFFFFFFFu;
+            Da.ctl_host = p->d_hctl;
+        }
+        hipLaunchKernelGGL(k_dalloc, dim3(1), dim3(1024), 0, s, Da);  // slots first: k_demit fills them
         DHIP(hipGetLastError());
         hipLaunchKernelGGL(k_demit, dim3(ns), dim3(64 * DEMIT_WAVES), 0, s, D);
         DHIP(hipGetLastError());
         hipLaunchKernelGGL(k_dcommit, dim3((ns + 3) / 4), dim3(256), 0, s, D);
         DHIP(hipGetLastError());
-        // through a pinned buffer, then a spin on an event: back within a few us of the copy
-        if (!p->h_ctl) {
-            if ((rc0 = xc__halloc((void **)&p->h_ctl, DCTL_WORDS * 4))) return rc0;
-            DHIP(hipEventCreateWithFlags(&p->ev_ctl, hipEventDisableTiming));
+        if (pub) {
+            for (int i = 0;; i++) {
+                if (*(volatile const uint32_t *)(p->h_ctl + DCTL_WORDS - 1) == 0u) {
+                    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+                    memcpy(ctl, p->h_ctl, DCTL_WORDS * 4);
+                    return XC_OK;
+                }
+                if ((i & 255) == 255) {
+                    const hipError_t e = hipStreamQuery(s);
+                    if (e == hipSuccess) break;  // drained without a publication: read the words
+                    if (e != hipErrorNotReady) DHIP(e);
+                    if (i >= 4096) sched_yield();
+                }
+            }
         }
+        // through a pinned buffer, then a spin on an event: back within a few us of the copy
         DHIP(hipMemcpyAsync(p->h_ctl, D.ctl, DCTL_WORDS * 4, hipMemcpyDeviceToHost, s));
         DHIP(hipEventRecord(p->ev_ctl, s));
         DHIP(xc__spin_wait(p->ev_ctl));  // (polls, yielding the core after ~20 us)

@@ -39,7 +39,7 @@ SYMBOLS = [
     "xc_coss_open", "xc_coss_close", "xc_coss_cache", "xc_coss_count", "xc_coss_stats", "xc_coss_lookup",
     "xc_coss_enter", "xc_coss_encode_batch_host", "xc_coss_decode_batch_host", "xc_coss_store_lookup",
     "xc_coss_store_enter", "xc_coss_encode_streams", "xc_encode_submit", "xc_encode_poll", "xc_encode_wait",
-    "xc_plan_set_completion",
+    "xc_plan_set_completion", "xc_dplan_set_completion",
 ]
 STREAM_FLUSH = 1  # XC_STREAM_FLUSH
 
@@ -146,6 +146,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.xc_dplan_layout.argtypes = [_vp, _u64p, _u64p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     lib.xc_decode_run.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
     lib.xc_dplan_stats.argtypes = [_vp, C.POINTER(DecodeStats)]
+    lib.xc_dplan_set_completion.argtypes = [_vp, C.c_int]
     lib.xc_coss_open.argtypes = [_vp, C.c_char_p, C.c_char_p, C.c_uint64, C.POINTER(_vp)]
     lib.xc_coss_close.argtypes = [_vp]
     lib.xc_coss_cache.restype = _vp
@@ -625,6 +626,10 @@ class DecodePlan:
             d_unknown: int, d_has_unknown: int) -> None:
         _check(load_library().xc_decode_run(self.h, d_in, d_out, d_out_len, d_consumed, d_status,
                                             d_unknown, d_has_unknown))
+
+    def set_completion(self, stream_ordered: bool) -> None:
+        """xc_dplan_set_completion (see EncodePlan.set_completion)."""
+        _check(load_library().xc_dplan_set_completion(self.h, 1 if stream_ordered else 0))
 
     def stats(self) -> DecodeStats:
         st = DecodeStats()
