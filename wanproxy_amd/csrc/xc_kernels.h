@@ -208,7 +208,10 @@ struct EmitArgs {
 };
 // Sub-batches of at most this many buffers take k_alloc's work inside k_emit (every workgroup
 // sums the buf_next of the buffers before it): one launch less on small batches.
-constexpr uint32_t EMIT_SLOTS_MAX = 1024;
+#ifndef XC_EMIT_SLOTS_MAX
+#define XC_EMIT_SLOTS_MAX 1024
+#endif
+constexpr uint32_t EMIT_SLOTS_MAX = XC_EMIT_SLOTS_MAX;
 
 // Packing a sub-batch's encoded streams, in buffer order, into one caller buffer (pinned host
 // memory written over PCIe by the kernel, or device memory): the end-to-end host path.
