@@ -20,7 +20,7 @@ ctx = w.Context(0)
 pool = W.pool(64)
 t_end = time.time() + budget
 fails = 0
-runs = {"encode": 0, "streams": 0, "decode": 0, "coss": 0}
+runs = {"encode": 0, "streams": 0, "decode": 0, "coss": 0, "plan": 0}
 while time.time() < t_end:
     if seed % 10 == 0:
         print("progress seed", seed, runs, "fails", fails, flush=True)
@@ -77,7 +77,45 @@ while time.time() < t_end:
         gc = w.XCodecCache(ctx, int(rng.choice([1024, 1 << 16])))
         oc.encode_batch(warm)
         w.XCodecEncoder(gc).encode_batch(warm)
-        if kind == "encode":
+        if kind == "plan":
+            # device-resident plan: back-to-back restore + run (run / submit+wait / submit+poll) in
+            # a random completion mode (stream ordered: no host synchronisation between runs)
+            import torch
+            gc.snapshot()
+            bufs = F._batch(rng, pool)
+            want = oc.encode_batch(bufs)
+            plan = w.EncodePlan(gc, [len(b) for b in bufs])
+            plan.set_completion(bool(rng.random() < 0.7))
+            arena = np.zeros(plan.in_bytes, np.uint8)
+            for i, b in enumerate(bufs):
+                arena[int(plan.in_off[i]):int(plan.in_off[i]) + len(b)] = b
+            d_in = torch.from_numpy(arena).cuda()
+            reps = int(rng.integers(2, 5))
+            outs = [(torch.zeros(plan.out_bytes, dtype=torch.uint8, device="cuda"),
+                     torch.zeros(len(bufs), dtype=torch.int64, device="cuda")) for _ in range(reps)]
+            torch.cuda.synchronize()
+            for r in range(reps):
+                gc.restore_async()
+                mode = int(rng.integers(3))
+                if mode == 0:
+                    plan.run(d_in.data_ptr(), outs[r][0].data_ptr(), outs[r][1].data_ptr())
+                else:
+                    plan.submit(d_in.data_ptr(), outs[r][0].data_ptr(), outs[r][1].data_ptr())
+                    if mode == 1:
+                        plan.wait()
+                    else:
+                        while not plan.poll():
+                            pass
+            ctx.sync()
+            torch.cuda.synchronize()
+            for r in range(reps):
+                out, ln = outs[r][0].cpu().numpy(), outs[r][1].cpu().numpy()
+                for i in range(len(bufs)):
+                    o = int(plan.out_off[i])
+                    if out[o:o + int(ln[i])].tobytes() != want[i]:
+                        raise AssertionError(f"plan run {r} buffer {i} differs")
+            plan.close()
+        elif kind == "encode":
             for _ in range(int(rng.integers(1, 4))):
                 bufs = F._batch(rng, pool)
                 if oc.encode_batch(bufs) != w.XCodecEncoder(gc).encode_batch(bufs):
