@@ -206,6 +206,28 @@ constexpr uint32_t DRES_WAVES = 8;
 
 // EXTRACTs against the cache; absent ones become provider candidates in the batch table.
 // HASH (round 0): the payloads' hashes H first (xcodec_hash.h:166-174), kept in t_h.
+// A payload's 2048 bytes as raw dword loads (lane l: bytes 32 l ..), aligned only when used, so
+// that the next payload's loads stay in flight while the current one is hashed and looked up.
+struct RawWin {
+    uint32_t d[9];
+    uint32_t sh;
+};
+
+__device__ __forceinline__ void raw_load(RawWin &r, const uint8_t *p)
+{
+    const uintptr_t a = (uintptr_t)(p + 32u * lane_id());
+    const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
+    r.sh = (uint32_t)(a & 3);
+#pragma unroll
+    for (int k = 0; k < 9; k++) r.d[k] = w[k];  // (the ninth dword: the input arena has slack)
+}
+
+__device__ __forceinline__ void raw_align(const RawWin &r, uint32_t out[8])
+{
+#pragma unroll
+    for (int k = 0; k < 8; k++) out[k] = __builtin_amdgcn_alignbyte(r.d[k + 1], r.d[k], r.sh);
+}
+
 template <bool HASH>
 __global__ __launch_bounds__(64) void k_dres1(DecDev D)
 {
@@ -214,6 +236,51 @@ __global__ __launch_bounds__(64) void k_dres1(DecDev D)
     const uint8_t *s = D.in + D.in_off[j];
     const uint32_t tb = D.tok_base[j], n = D.tok_cnt[j];
     const uint32_t lim = D.s_lim[j];
+    if (HASH) {
+        // round 0: the wave's tokens 64 at a time (lane i: token t0 + i * gridDim.y), their
+        // EXTRACTs in token order with the next payload's loads issued before this one is used
+        const uint32_t l = lane_id();
+        for (uint32_t t0 = blockIdx.y; t0 < n; t0 += 64u * gridDim.y) {
+            const uint32_t tl = t0 + l * gridDim.y;
+            const bool ex = tl < n && D.t_op[tb + tl] == T_EXTRACT;
+            const uint32_t le = ex ? D.t_le[tb + tl] : 0u;
+            uint64_t m = ballot(ex);
+            if (!m) continue;
+            int f = __ffsll((unsigned long long)m) - 1;
+            RawWin cur, nxt;
+            raw_load(cur, s + readlane(le, f) + 2u);
+            for (;;) {
+                m &= m - 1;
+                const int fn = m ? __ffsll((unsigned long long)m) - 1 : -1;
+                if (fn >= 0) raw_load(nxt, s + readlane(le, fn) + 2u);
+                const uint32_t t = t0 + (uint32_t)f * gridDim.y;
+                uint32_t w[8];
+                raw_align(cur, w);
+                const uint64_t h = wave_hash_regs(w);
+                uint64_t v;
+                uint32_t st;
+                if (set_find(D.cache, h, &v)) {
+                    const uint4 *sp = (const uint4 *)(D.segs + v * XC_SEG + 32u * l);
+                    const uint4 y0 = sp[0], y1 = sp[1];
+                    const uint32_t diff = (w[0] ^ y0.x) | (w[1] ^ y0.y) | (w[2] ^ y0.z) | (w[3] ^ y0.w) |
+                                          (w[4] ^ y1.x) | (w[5] ^ y1.y) | (w[6] ^ y1.z) | (w[7] ^ y1.w);
+                    st = ballot(diff != 0u) == 0 ? R_OKCACHE : R_COLL;
+                } else {
+                    st = R_PENDING;
+                    if (l == 0 && t < lim) set_insert(D.dset, h, ((uint64_t)j << 32) | t, true, nullptr, nullptr);
+                }
+                if (l == 0) {
+                    D.t_h[tb + t] = h;
+                    D.t_stat[tb + t] = st;
+                    D.t_src[tb + t] = st == R_OKCACHE ? v : 0;
+                }
+                if (fn < 0) break;
+                cur = nxt;
+                f = fn;
+            }
+        }
+        return;
+    }
     for (uint32_t t = blockIdx.y; t < n; t += gridDim.y) {
         if (uniform(D.t_op[tb + t]) != T_EXTRACT) continue;
         const uint8_t *pay = s + D.t_le[tb + t] + 2u;
