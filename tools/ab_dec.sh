@@ -8,7 +8,7 @@ for r in $(seq 1 ${2:-3}); do
     lib=$PWD/wanproxy_amd/libxcodec_hip.so
     envs=""
     if [ $v = b ]; then
-      if [ -n "$B_ENV" ]; then envs="$B_ENV"; else lib=$PWD/wanproxy_amd/libxcodec_hip_b.so; fi
+      if [ -n "$B_ENV" ]; then envs="$B_ENV"; else lib=$PWD/wanproxy_amd/${B_LIB:-libxcodec_hip_b.so}; fi
     fi
     env $envs XC_LIB_PATH=$lib timeout -k 10 200 python tools/dec_leg.py ${3:-30} > $out/$v$r.log 2>&1 || exit 1
     python -c "import json; d=json.loads(open('$out/$v$r.log').read().strip().splitlines()[-1]); print('$v', $r, d['value'], d['ms_per_step'])"

@@ -202,7 +202,10 @@ __global__ __launch_bounds__(64) void k_dtok(DecDev D, int fill, int first, uint
 }
 
 // k_dres1 / k_dres2 grids: (streams, DRES_WAVES), wave y taking tokens y, y + DRES_WAVES, ...
-constexpr uint32_t DRES_WAVES = 8;
+#ifndef XC_DRES_WAVES
+#define XC_DRES_WAVES 8
+#endif
+constexpr uint32_t DRES_WAVES = XC_DRES_WAVES;
 
 // EXTRACTs against the cache; absent ones become provider candidates in the batch table.
 // HASH (round 0): the payloads' hashes H first (xcodec_hash.h:166-174), kept in t_h.
