@@ -321,36 +321,45 @@ __global__ __launch_bounds__(64) void k_dres1(DecDev D)
     }
 }
 
-// Provider resolution in (stream, token) order.
+__device__ __forceinline__ uint64_t dreadlane64(uint64_t x, int l)
+{
+    return ((uint64_t)readlane((uint32_t)(x >> 32), l) << 32) | readlane((uint32_t)x, l);
+}
+
+// Provider resolution in (stream, token) order: one wave per stream, one lane per token (every
+// probe of 64 tokens in flight together); an EXTRACT with an earlier provider then takes a
+// wave-wide 2048-byte comparison (rare: the same new segment twice in a batch).
 __global__ __launch_bounds__(64) void k_dres2(DecDev D)
 {
     const uint32_t j = blockIdx.x;
     if (j >= D.ns) return;
     const uint8_t *s = D.in + D.in_off[j];
     const uint32_t tb = D.tok_base[j], n = D.tok_cnt[j];
-    for (uint32_t t = blockIdx.y; t < n; t += gridDim.y) {
-        const uint32_t op = uniform(D.t_op[tb + t]);
+    const uint32_t l = lane_id();
+    for (uint32_t t0 = 64u * blockIdx.y; t0 < n; t0 += 64u * gridDim.y) {
+        const uint32_t t = t0 + l;
+        const uint32_t op = t < n ? D.t_op[tb + t] : T_END;
         const uint64_t self = ((uint64_t)j << 32) | t;
-        uint64_t v;
+        uint32_t st = 0;
+        uint64_t src = 0, pv = 0;
+        bool wst = false, wsrc = false, cmp = false;
         if (op == T_EXTRACT) {
-            if (uniform(D.t_stat[tb + t]) != R_PENDING) continue;
-            const uint64_t h = D.t_h[tb + t];
-            uint32_t st = R_ENTER;
-            uint64_t src = 0;
-            if (set_find(D.dset, h, &v) && v < self) {
-                const uint32_t pj = (uint32_t)(v >> 32), pt = (uint32_t)v;
-                const uint8_t *pp = D.in + D.in_off[pj] + D.t_le[D.tok_base[pj] + pt] + 2u;
-                st = wave_equal2048(s + D.t_le[tb + t] + 2u, pp) ? R_OKPROV : R_COLL;
-                src = SRC_PROV | v;
-            }
-            if (lane_id() == 0) {
-                D.t_stat[tb + t] = st;
-                D.t_src[tb + t] = src;
+            if (D.t_stat[tb + t] == R_PENDING) {
+                const uint64_t h = D.t_h[tb + t];
+                uint64_t v;
+                st = R_ENTER;
+                wst = wsrc = true;
+                if (set_find(D.dset, h, &v) && v < self) {
+                    cmp = true;
+                    pv = v;
+                    src = SRC_PROV | v;
+                }
             }
         } else if (op == T_REF) {
             const uint64_t h = D.t_h[tb + t];
-            uint32_t st = R_UNKNOWN;
-            uint64_t src = 0;
+            uint64_t v;
+            st = R_UNKNOWN;
+            wst = wsrc = true;
             if (set_find(D.cache, h, &v)) {
                 st = R_OKCACHE;
                 src = v;
@@ -358,13 +367,20 @@ __global__ __launch_bounds__(64) void k_dres2(DecDev D)
                 st = R_OKPROV;
                 src = SRC_PROV | v;
             }
-            if (lane_id() == 0) {
-                D.t_stat[tb + t] = st;
-                D.t_src[tb + t] = src;
-            }
-        } else if (lane_id() == 0) {
-            D.t_stat[tb + t] = 0;
+        } else if (t < n) {
+            wst = true;
         }
+        for (uint64_t m = ballot(cmp); m; m &= m - 1) {
+            const int f = __ffsll((unsigned long long)m) - 1;
+            const uint64_t v = dreadlane64(pv, f);
+            const uint32_t tf = readlane(t, f);
+            const uint32_t pj = (uint32_t)(v >> 32), pt = (uint32_t)v;
+            const uint8_t *pp = D.in + D.in_off[pj] + D.t_le[D.tok_base[pj] + pt] + 2u;
+            const bool eq = wave_equal2048(s + D.t_le[tb + tf] + 2u, pp);
+            if ((int)l == f) st = eq ? R_OKPROV : R_COLL;
+        }
+        if (wst) D.t_stat[tb + t] = st;
+        if (wsrc) D.t_src[tb + t] = src;
     }
 }
 
@@ -516,10 +532,6 @@ __device__ __forceinline__ void write_unescaped(uint8_t *dst, const uint8_t *p, 
 constexpr uint32_t DMAX_TOK = 2048;
 constexpr uint32_t DEMIT_WAVES = 8;
 
-__device__ __forceinline__ uint64_t dreadlane64(uint64_t x, int l)
-{
-    return ((uint64_t)readlane((uint32_t)(x >> 32), l) << 32) | readlane((uint32_t)x, l);
-}
 
 // Output offsets (executed tokens only), then the bytes.  One workgroup (8 waves) per stream,
 // tokens in blocks of DMAX_TOK: sizes lane-parallel (one token per lane; escapes counted only
@@ -939,7 +951,7 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
             hipLaunchKernelGGL(k_dres1<true>, dim3(ns, DRES_WAVES), dim3(64), 0, s, D);
         }
         DHIP(hipGetLastError());
-        hipLaunchKernelGGL(k_dres2, dim3(ns, DRES_WAVES), dim3(64), 0, s, D);
+        hipLaunchKernelGGL(k_dres2, dim3(ns), dim3(64), 0, s, D);  // (a wave per stream)
         DHIP(hipGetLastError());
         hipLaunchKernelGGL(k_dstop, dim3((ns + 3) / 4), dim3(256), 0, s, D);
         DHIP(hipGetLastError());
