@@ -243,6 +243,11 @@ __device__ __forceinline__ void raw_align(const RawWin &r, uint32_t out[8])
     for (int k = 0; k < 8; k++) out[k] = __builtin_amdgcn_alignbyte(r.d[k + 1], r.d[k], r.sh);
 }
 
+__device__ __forceinline__ uint64_t dreadlane64(uint64_t x, int l)
+{
+    return ((uint64_t)readlane((uint32_t)(x >> 32), l) << 32) | readlane((uint32_t)x, l);
+}
+
 template <bool HASH>
 __global__ __launch_bounds__(64) void k_dres1(DecDev D)
 {
@@ -252,8 +257,9 @@ __global__ __launch_bounds__(64) void k_dres1(DecDev D)
     const uint32_t tb = D.tok_base[j], n = D.tok_cnt[j];
     const uint32_t lim = D.s_lim[j];
     if (HASH) {
-        // round 0: the wave's tokens 64 at a time (lane i: token t0 + i * gridDim.y), their
-        // EXTRACTs in token order with the next payload's loads issued before this one is used
+        // round 0: the wave's tokens 64 at a time (lane i: token t0 + i * gridDim.y): their
+        // EXTRACT payloads hashed in token order with the next payload's loads issued before this
+        // one is used, then every probe and insert at once, one lane per token
         const uint32_t l = lane_id();
         for (uint32_t t0 = blockIdx.y; t0 < n; t0 += 64u * gridDim.y) {
             const uint32_t tl = t0 + l * gridDim.y;
@@ -264,34 +270,38 @@ __global__ __launch_bounds__(64) void k_dres1(DecDev D)
             int f = __ffsll((unsigned long long)m) - 1;
             RawWin cur, nxt;
             raw_load(cur, s + readlane(le, f) + 2u);
-            for (;;) {
-                m &= m - 1;
-                const int fn = m ? __ffsll((unsigned long long)m) - 1 : -1;
+            // the hashes, wave-wide, each kept by its token's lane
+            uint64_t hl = 0;
+            for (uint64_t mm = m;;) {
+                mm &= mm - 1;
+                const int fn = mm ? __ffsll((unsigned long long)mm) - 1 : -1;
                 if (fn >= 0) raw_load(nxt, s + readlane(le, fn) + 2u);
-                const uint32_t t = t0 + (uint32_t)f * gridDim.y;
                 uint32_t w[8];
                 raw_align(cur, w);
                 const uint64_t h = wave_hash_regs(w);
-                uint64_t v;
-                uint32_t st;
-                if (set_find(D.cache, h, &v)) {
-                    const uint4 *sp = (const uint4 *)(D.segs + v * XC_SEG + 32u * l);
-                    const uint4 y0 = sp[0], y1 = sp[1];
-                    const uint32_t diff = (w[0] ^ y0.x) | (w[1] ^ y0.y) | (w[2] ^ y0.z) | (w[3] ^ y0.w) |
-                                          (w[4] ^ y1.x) | (w[5] ^ y1.y) | (w[6] ^ y1.z) | (w[7] ^ y1.w);
-                    st = ballot(diff != 0u) == 0 ? R_OKCACHE : R_COLL;
-                } else {
-                    st = R_PENDING;
-                    if (l == 0 && t < lim) set_insert(D.dset, h, ((uint64_t)j << 32) | t, true, nullptr, nullptr);
-                }
-                if (l == 0) {
-                    D.t_h[tb + t] = h;
-                    D.t_stat[tb + t] = st;
-                    D.t_src[tb + t] = st == R_OKCACHE ? v : 0;
-                }
+                if ((int)l == f) hl = h;
                 if (fn < 0) break;
                 cur = nxt;
                 f = fn;
+            }
+            // the cache probes and the batch table's inserts, lane-parallel
+            uint64_t v = 0;
+            uint32_t st = 0;
+            const bool hit = ex && set_find(D.cache, hl, &v);
+            if (ex && !hit) {
+                st = R_PENDING;
+                if (tl < lim) set_insert(D.dset, hl, ((uint64_t)j << 32) | tl, true, nullptr, nullptr);
+            }
+            // a cached hash: its payload against the cached segment, wave-wide (rare)
+            for (uint64_t mh = ballot(hit); mh; mh &= mh - 1) {
+                const int fh = __ffsll((unsigned long long)mh) - 1;
+                const bool eq = wave_equal2048(s + readlane(le, fh) + 2u, D.segs + dreadlane64(v, fh) * XC_SEG);
+                if ((int)l == fh) st = eq ? R_OKCACHE : R_COLL;
+            }
+            if (ex) {
+                D.t_h[tb + tl] = hl;
+                D.t_stat[tb + tl] = st;
+                D.t_src[tb + tl] = st == R_OKCACHE ? v : 0;
             }
         }
         return;
@@ -321,10 +331,6 @@ __global__ __launch_bounds__(64) void k_dres1(DecDev D)
     }
 }
 
-__device__ __forceinline__ uint64_t dreadlane64(uint64_t x, int l)
-{
-    return ((uint64_t)readlane((uint32_t)(x >> 32), l) << 32) | readlane((uint32_t)x, l);
-}
 
 // Provider resolution in (stream, token) order: one wave per stream, one lane per token (every
 // probe of 64 tokens in flight together); an EXTRACT with an earlier provider then takes a
