@@ -215,7 +215,7 @@ __global__ __launch_bounds__(64) void k_dtok(DecDev D, int fill, int first, uint
 
 // k_dres1 / k_dres2 grids: (streams, DRES_WAVES), wave y taking tokens y, y + DRES_WAVES, ...
 #ifndef XC_DRES_WAVES
-#define XC_DRES_WAVES 8
+#define XC_DRES_WAVES 4
 #endif
 constexpr uint32_t DRES_WAVES = XC_DRES_WAVES;
 
