@@ -536,7 +536,7 @@ __device__ __forceinline__ void write_unescaped(uint8_t *dst, const uint8_t *p, 
 }
 
 constexpr uint32_t DMAX_TOK = 2048;
-constexpr uint32_t DEMIT_WAVES = 8;
+constexpr uint32_t DEMIT_WAVES = 4;
 
 
 // Output offsets (executed tokens only), then the bytes.  One workgroup (8 waves) per stream,
