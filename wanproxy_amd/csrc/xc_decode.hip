@@ -126,6 +126,26 @@ __device__ __forceinline__ uint32_t dwin_byte(const DWin &w, uint32_t x)
     return (readlane(d, (int)(r >> 4)) >> (8 * (r & 3u))) & 0xffu;
 }
 
+// Dword i of the window (uniform i): lane i / 4 holds dwords 4 l .. 4 l + 3.
+__device__ __forceinline__ uint32_t dwin_dword(const DWin &w, uint32_t i)
+{
+    const uint32_t k = i & 3u;
+    const uint32_t d = k == 0 ? w.v.x : k == 1 ? w.v.y : k == 2 ? w.v.z : w.v.w;
+    return readlane(d, (int)(i >> 2));
+}
+
+// The big-endian 64-bit value at bytes x .. x + 7 of the window, w0 <= x, x + 8 <= w0 + 1024 (x
+// uniform): three dwords instead of eight single bytes.
+__device__ __forceinline__ uint64_t dwin_be64(const DWin &w, uint32_t x)
+{
+    const uint32_t r = x - w.w0, i = r >> 2, sh = 8u * (r & 3u);
+    const uint32_t d0 = dwin_dword(w, i), d1 = dwin_dword(w, i + 1u);
+    const uint32_t d2 = (r & 3u) ? dwin_dword(w, i + 2u) : 0u;  // (i + 2 stays inside the window then)
+    const uint32_t lo = sh ? (d0 >> sh) | (d1 << (32u - sh)) : d0;  // bytes x .. x + 3, little endian
+    const uint32_t hi = sh ? (d1 >> sh) | (d2 << (32u - sh)) : d1;
+    return ((uint64_t)__builtin_bswap32(lo) << 32) | __builtin_bswap32(hi);
+}
+
 // Tokenizer (xcodec_decoder.cc:85-173), one wave per stream: tokens are found inside 1 KiB
 // register windows (ESC and REF tokens, and the REF hash bytes, without another load); only an
 // EXTRACT, whose 2048-byte payload is skipped, or the window's end, loads a new window.
@@ -197,7 +217,7 @@ __global__ __launch_bounds__(64) void k_dtok(DecDev D, int fill, int first, uint
             if (n - q < 10u) { put(T_WAIT, q, 0); break; }
             uint64_t h = 0;
             if (q + 10u <= w.w0 + 1024u) {
-                for (uint32_t k = 0; k < 8; k++) h = (h << 8) | dwin_byte(w, q + 2u + k);
+                h = dwin_be64(w, q + 2u);
             } else {
                 for (uint32_t k = 0; k < 8; k++) h = (h << 8) | s[q + 2u + k];
             }
