@@ -483,7 +483,7 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t x, int l)
     return ((uint64_t)readlane((uint32_t)(x >> 32), l) << 32) | readlane((uint32_t)x, l);
 }
 
-__global__ __launch_bounds__(256) void k_resolve(ResolveArgs a)
+__global__ __launch_bounds__(64 * RES_WAVES) void k_resolve(ResolveArgs a)
 {
     // the scan that ran before has handed out all its work: reset its counter for the next
     // scan (before the abort check, so a redone sub-batch starts from a clean counter)
@@ -494,7 +494,7 @@ __global__ __launch_bounds__(256) void k_resolve(ResolveArgs a)
         a.P.ctl[CTL_FIRST_CROSS] = NONE;
         a.P.ctl[CTL_SHADOW] = 0u;
     }
-    const uint32_t c = a.ck_lo + blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint32_t c = a.ck_lo + blockIdx.x * RES_WAVES + (threadIdx.x >> 6);
     if (c >= a.ck_hi) return;
     const uint32_t cnt = a.L.cnt[c];
     if (cnt == 0 || (cnt & EV_DENSE)) return;

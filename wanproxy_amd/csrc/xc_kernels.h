@@ -185,6 +185,10 @@ struct WalkArgs {
     uint32_t waves;     // waves per buffer (workgroup) sharing the block-parallel walk's chunks
 };
 constexpr uint32_t WALK_WAVES_MAX = 4;
+#ifndef XC_RES_WAVES
+#define XC_RES_WAVES 1
+#endif
+constexpr uint32_t RES_WAVES = XC_RES_WAVES;  // k_resolve: chunks (waves) per workgroup
 constexpr uint32_t MIX_FOLD_MAX = 4;  // (XC_FILT_WORDS >> 4 = 2304 words: still a multiple of 4)
 // dynamic LDS of k_walk
 __host__ __device__ constexpr uint32_t walk_lds_bytes(uint32_t max_decl) { return max_decl * 16u + 8u * (max_decl / 32u + 1u); }

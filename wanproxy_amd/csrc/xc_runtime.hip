@@ -1344,7 +1344,8 @@ static int launch_resolve(xc_plan *p, const Layer &L, int dmode, uint32_t ck_lo,
 {
     ResolveArgs a{p->P, L, dmode, ck_lo, ck_hi};
     KSpan span(p, XC_K_RESOLVE);
-    hipLaunchKernelGGL(k_resolve, dim3(std::max<uint32_t>(1u, (ck_hi - ck_lo + 3) / 4)), dim3(256), 0,
+    hipLaunchKernelGGL(k_resolve, dim3(std::max<uint32_t>(1u, (ck_hi - ck_lo + RES_WAVES - 1) / RES_WAVES)),
+                       dim3(64 * RES_WAVES), 0,
                        p->cache->ctx->stream, a);
     HIPCHK(hipGetLastError());
     return XC_OK;
