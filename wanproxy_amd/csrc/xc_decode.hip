@@ -238,6 +238,10 @@ __global__ __launch_bounds__(64) void k_dtok(DecDev D, int fill, int first, uint
 #define XC_DRES_WAVES 4
 #endif
 constexpr uint32_t DRES_WAVES = XC_DRES_WAVES;
+#ifndef XC_DCOMMIT_WAVES
+#define XC_DCOMMIT_WAVES 4
+#endif
+constexpr uint32_t DCOMMIT_WAVES = XC_DCOMMIT_WAVES;  // k_dcommit: streams (waves) per workgroup
 
 // EXTRACTs against the cache; absent ones become provider candidates in the batch table.
 // HASH (round 0): the payloads' hashes H first (xcodec_hash.h:166-174), kept in t_h.
@@ -729,12 +733,12 @@ __global__ __launch_bounds__(1024) void k_dalloc(DecDev D)
 
 // XCodecMemoryCache::enter for first-seen EXTRACT payloads (xcodec_decoder.cc:133-135).
 // grid (streams, 8): wave y takes the stream's executed tokens y, y + 8, ...
-__global__ __launch_bounds__(256) void k_dcommit(DecDev D)
+__global__ __launch_bounds__(64 * DCOMMIT_WAVES) void k_dcommit(DecDev D)
 {
     if (fix_pending(D)) return;
     // one wave per stream (4 per workgroup), one lane per token; k_demit already wrote the
     // payloads into their slots
-    const uint32_t j = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint32_t j = blockIdx.x * DCOMMIT_WAVES + (threadIdx.x >> 6);
     if (j >= D.ns) return;
     const uint32_t tb = D.tok_base[j], lim = min(D.tok_cnt[j], D.s_stop[j] - 1u);
     for (uint32_t t = lane_id(); t < lim; t += 64u) {
@@ -1008,7 +1012,7 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
         DHIP(hipGetLastError());
         hipLaunchKernelGGL(k_demit, dim3(ns), dim3(64 * DEMIT_WAVES), 0, s, D);
         DHIP(hipGetLastError());
-        hipLaunchKernelGGL(k_dcommit, dim3((ns + 3) / 4), dim3(256), 0, s, D);
+        hipLaunchKernelGGL(k_dcommit, dim3((ns + DCOMMIT_WAVES - 1) / DCOMMIT_WAVES), dim3(64 * DCOMMIT_WAVES), 0, s, D);
         DHIP(hipGetLastError());
         if (pub) {
             for (int i = 0;; i++) {
