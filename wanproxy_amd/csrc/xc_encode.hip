@@ -913,6 +913,7 @@ __device__ __forceinline__ void walk_seq(const WalkArgs &a, uint32_t b, uint64_t
 // a.waves waves (groups of WB_GROUP chunks round-robin), combined through LDS.
 struct WalkShared {
     uint32_t fail, cross, n_ext, n_ref;
+    uint32_t n_unk;  // EXTRACTs whose hash no event supplied (decl_hash's work)
 };
 
 __device__ __forceinline__ bool walk_blocks(const WalkArgs &a, uint32_t b, WalkShared &sh)
@@ -924,10 +925,10 @@ __device__ __forceinline__ bool walk_blocks(const WalkArgs &a, uint32_t b, WalkS
     const uint32_t ck0 = P.buf_chunk0[b], ck1 = P.buf_chunk0[b + 1];
     const uint32_t tb = P.tok_base[b];
     if (!stream_plain(P, b)) return false;  // carried state or no flush: the sequential walk
-    if (threadIdx.x == 0) sh = WalkShared{0u, 0u, 0u, 0u};
+    if (threadIdx.x == 0) sh = WalkShared{0u, 0u, 0u, 0u, 0u};
     __syncthreads();
     bool ok = true, cross = false;
-    uint32_t n_ext = 0, n_ref = 0;
+    uint32_t n_ext = 0, n_ref = 0, n_unk = 0;
     // chunks in groups of WB_GROUP: every load of a group is issued before any is used (a buffer
     // of short chunks would otherwise pay one memory round trip per chunk)
     constexpr uint32_t WB_GROUP = 4;
@@ -978,6 +979,7 @@ __device__ __forceinline__ bool walk_blocks(const WalkArgs &a, uint32_t b, WalkS
                     } else {
                         P.tok_op[t] = OP_EXTRACT;
                         P.tok_known[t] = st[i] == ST_MATCH ? 1u : 0u;
+                        n_unk += st[i] == ST_MATCH ? 0u : 1u;
                         P.tok_dpos[t] = dpos < len ? dpos : DPOS_FLUSH;
                         P.tok_h[t] = st[i] == ST_MATCH ? h : 0u;
                         n_ext++;
@@ -993,12 +995,14 @@ __device__ __forceinline__ bool walk_blocks(const WalkArgs &a, uint32_t b, WalkS
     const bool wave_fail = ballot(!ok) != 0;  // (every lane's verdict: ballots run on all lanes)
     n_ext = wave_sum(n_ext);
     n_ref = wave_sum(n_ref);
+    n_unk = wave_sum(n_unk);
     const bool any_cross = ballot(cross) != 0;
     if (l == 0) {
         if (wave_fail) atomicOr(&sh.fail, 1u);
         if (any_cross) atomicOr(&sh.cross, 1u);
         atomicAdd(&sh.n_ext, n_ext);
         atomicAdd(&sh.n_ref, n_ref);
+        atomicAdd(&sh.n_unk, n_unk);
     }
     __syncthreads();
     if (sh.fail) return false;
@@ -1065,7 +1069,8 @@ __global__ __launch_bounds__(64 * WALK_WAVES_MAX) void k_walk(WalkArgs a)
     const bool blocks = !a.use_d && walk_blocks(a, b, sh);  // (every wave, or none: uniform per block)
     if (threadIdx.x >= 64u) return;  // the sequential walk and the declaration hashes: wave 0
     if (!blocks) walk_seq(a, b, walk_lds);
-    decl_hash(a.P, b);
+    // (a block walk whose every EXTRACT hash came from an event leaves decl_hash nothing to do)
+    if (!blocks || sh.n_unk) decl_hash(a.P, b);
 }
 
 // Hash of every aligned 2048-byte block, one wave per group of <= BLK_GROUP consecutive blocks
