@@ -261,7 +261,8 @@ int xc_coss_close(xc_coss *c);
  * while nothing is purged (use the batch calls below to keep the COSS state). */
 xc_cache *xc_coss_cache(xc_coss *c);
 int xc_coss_count(xc_coss *c, uint64_t *n);
-/* {lookups (hits only: misses are not counted here), found in the recent window, found in the
+/* {lookups (every call, misses included, as the reference counts them: the batch paths add the
+ * encoder's and decoder's missed lookups of each replayed item), found in the recent window, found in the
  * stripes, index size, stripe limit, serial number} (COSSStats, xcodec_cache_coss.h:179-187). */
 int xc_coss_stats(xc_coss *c, uint64_t *out6);
 /* XCodecCacheCOSS::lookup / enter (:188-228, :163-186); the device mirror follows. */

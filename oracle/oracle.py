@@ -42,6 +42,8 @@ def _load() -> C.CDLL:
     lib.xo_cache_free.argtypes = [C.c_void_p]
     lib.xo_cache_count.restype = C.c_size_t
     lib.xo_cache_count.argtypes = [C.c_void_p]
+    lib.xo_cache_coss_stats.restype = C.c_int
+    lib.xo_cache_coss_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
     lib.xo_cache_entry.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_uint64), C.c_void_p]
     lib.xo_cache_lookup.restype = C.c_int
     lib.xo_cache_lookup.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]
@@ -132,6 +134,12 @@ class Cache:
 
     def __len__(self) -> int:
         return int(lib().xo_cache_count(self.h))
+
+    def coss_stats(self) -> dict:
+        """COSSStats of a COSS cache (lookups, window / stripe matches, index, stripe limit, serial)."""
+        o = np.zeros(6, np.uint64)
+        assert lib().xo_cache_coss_stats(self.h, o.ctypes.data_as(C.POINTER(C.c_uint64)))
+        return dict(zip(["lookups", "found_1", "found_2", "index", "stripe_limit", "serial"], (int(x) for x in o)))
 
     def entries(self) -> list[tuple[int, bytes]]:
         out = []

@@ -185,6 +185,14 @@ void xo_cache_free(xo_cache *c)
 
 size_t xo_cache_count(const xo_cache *c) { return c->coss ? xo_coss_count(c->coss) : c->count; }
 
+/* COSSStats of a COSS cache (xcodec_cache_coss.h:179-187); 0 for the memory cache. */
+int xo_cache_coss_stats(const xo_cache *c, uint64_t *out6)
+{
+    if (!c->coss) return 0;
+    xo_coss_stats(c->coss, out6);
+    return 1;
+}
+
 static long cache_find(const xo_cache *c, uint64_t h)
 {
     size_t s = slot_of(h, c->mask);

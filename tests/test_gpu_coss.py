@@ -59,6 +59,8 @@ def test_coss_encode_decode_equal_the_oracle(gpu_ctx, oracle_mod, tmp_path, size
             assert not bad, (phase, k, bad[:5])
             streams += want
         assert len(oc) == len(pc)
+        # COSSStats (xcodec_cache_coss.cc:194-233): every lookup call, misses included
+        assert pc.stats() == oc.coss_stats(), phase
         oc.close()
         pc.close()
         assert (do / (UUID_A + ".wpc")).read_bytes() == (dp / (UUID_A + ".wpc")).read_bytes(), phase
@@ -71,6 +73,7 @@ def test_coss_encode_decode_equal_the_oracle(gpu_ctx, oracle_mod, tmp_path, size
         got = w.XCodecDecoder(pc).decode_batch(chunk)
         bad = [i for i, (x, y) in enumerate(zip(want, got)) if x != y]
         assert not bad, (a, bad[:5])
+    assert pc.stats() == oc.coss_stats()
     oc.close()
     pc.close()
     assert (do / (UUID_B + ".wpc")).read_bytes() == (dp / (UUID_B + ".wpc")).read_bytes()
@@ -116,6 +119,7 @@ def test_coss_stream_encoders_equal_the_oracle(gpu_ctx, oracle_mod, tmp_path, si
     for c in range(nconn):
         assert genc[c].flush() == oenc[c].flush(), c
     assert len(oc) == len(pc)
+    assert pc.stats() == oc.coss_stats()
     oc.close()
     pc.close()
     assert (do / (UUID_A + ".wpc")).read_bytes() == (dp / (UUID_A + ".wpc")).read_bytes()

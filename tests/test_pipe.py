@@ -197,3 +197,25 @@ def test_batched_turns_equal_sequential_calls(oracle_mod, chunk):
         assert b.a_enc.eos_ack and b.b_enc.eos_ack
     assert asked  # the peer cache started empty: <ASK>/<LEARN> ran, through the sync path
     assert ba.batcher.device_calls < sum(len(r) for r in inputs)
+
+
+def test_deferred_failure_is_reported_and_tears_the_filter_down(oracle_mod):
+    """A deferred decode that fails (a bad opcode inside a frame, xcodec_decoder.cc:169-171) while
+    a flush drains the batch: the turn's run() still reports the filter, and its next consume
+    returns False, as the reference's consume of that call would have."""
+    be = OracleBackend(oracle_mod)
+    a = P.Batcher(be)
+    reg = P.CacheRegistry(be)
+    codec = P.Codec(be, reg.register(P.CodecCache(be.new_store(), UUID_A, 64)), reg, a)
+    dec = P.DecodeFilter(codec)
+    dec.set_upstream(P.Sink())
+    dec.chain(P.Sink())
+    hello = bytes([P.OP_HELLO, 44]) + UUID_B.encode() + struct.pack("<Q", 64)
+    bad = b"abc\xf1\x07xyz"
+    assert dec.consume(hello + bytes([P.OP_FRAME]) + struct.pack(">H", len(bad)) + bad)
+    assert a.pending(dec)
+    dec.flush(0)                      # drains the batch: the deferred decode fails here
+    assert dec.deferred_failed
+    assert a.run() == [dec]           # reported by the turn's end
+    assert a.run() == []              # once
+    assert not dec.consume(bytes([P.OP_FRAME]) + struct.pack(">H", 1) + b"a")

@@ -252,6 +252,9 @@ public:
     }
 
     size_t size() const { return index_.size(); }
+    // Lookups the device made that missed (a miss outside the one state LOAD_MISS flags has no side
+    // effect but the count): stats_.lookups counts every call (:194).
+    void count_misses(uint64_t n) { lookups_ += n; }
     void stats(uint64_t *o) const
     {
         o[0] = lookups_;
@@ -597,6 +600,24 @@ int64_t get_be64(const uint8_t *p)
     for (int i = 0; i < 8; i++) v = (v << 8) | p[i];
     return (int64_t)v;
 }
+
+// The encoder's lookup calls (xcodec_encoder.cc:111) at window ends [lo, hi) of an item, whose REF
+// events are ev[0..n): every window end once the window is full, except the 2047 after a REF (the
+// hash restarts, :117-127).  Minus its hits (the replay's Store::lookup counted those): its misses.
+uint64_t enc_misses(uint64_t lo, uint64_t hi, const std::vector<EncEvent> &ev, size_t n)
+{
+    uint64_t calls = 0, hits = 0, cur = lo;
+    for (size_t i = 0; i < n; i++) {
+        const EncEvent &e = ev[i];
+        if (e.kind == 0 || e.pos >= hi) continue;
+        hits++;
+        if (e.kind != 1) continue;
+        if (e.pos >= cur) calls += e.pos + 1 - cur;
+        cur = std::max(cur, e.pos + SEG);
+    }
+    if (hi > cur) calls += hi - cur;
+    return calls > hits ? calls - hits : 0;
+}
 }  // namespace
 
 extern "C" int xc_coss_open(xc_ctx *ctx, const char *dir, const char *uuid, uint64_t size_mb, xc_coss **out)
@@ -827,7 +848,14 @@ int coss_encode(xc_coss *c, std::vector<CItem> items, uint8_t *out, const uint64
                         held.push_back(std::move(ch));
                         continue;
                     }
-                    // roll the device cache back to this event, follow the changes, run the rest again
+                    // the lookups up to this event (its own, unless a declaration: the lookup at the
+                    // same position follows it), then roll the device cache back to this event,
+                    // follow the changes, run the rest again
+                    if (E.pos != ~0ull)
+                        c->st.count_misses(enc_misses(std::max<uint64_t>(SEG - 1, it.start),
+                                                      E.kind == 0 ? E.pos : E.pos + 1, ev[k], e + 1));
+                    else
+                        c->st.count_misses(enc_misses(std::max<uint64_t>(SEG - 1, it.start), it.len, ev[k], e + 1));
                     if ((rc = xc__cache_truncate(c->cache, count0 + entered))) return rc;
                     for (const Change &h : held)
                         if ((rc = mirror(c, h))) return rc;
@@ -864,6 +892,7 @@ int coss_encode(xc_coss *c, std::vector<CItem> items, uint8_t *out, const uint64
                     break;
                 }
                 if (!redo) {  // item k is final
+                    c->st.count_misses(enc_misses(std::max<uint64_t>(SEG - 1, it.start), it.len, ev[k], ev[k].size()));
                     if (out_len[it.buf] + olen[k] > out_cap[it.buf])
                         return xc__set_error(XC_EINVAL, "output capacity too small");
                     std::memcpy(out + out_off[it.buf] + out_len[it.buf], &obuf[ooff[k]], olen[k]);
@@ -1076,6 +1105,7 @@ extern "C" int xc_coss_decode_batch_host(xc_coss *c, const uint8_t *in, const ui
                     break;
                 }
                 if (!redo) {
+                    if (hu[k]) c->st.count_misses(1);  // (the unknown REF's lookup, :150)
                     std::memcpy(out + out_off[it.buf] + out_len[it.buf], &obuf[ooff[k]], olen[k]);
                     out_len[it.buf] += olen[k];
                     consumed[it.buf] = it.from + cons[k];

@@ -286,7 +286,18 @@ struct xc_cache {
     // lets a restore write the count itself instead of copying it on the device
     int64_t host_count = -1;
     uint32_t gen = 0;  // bumped when the cache grows (its arrays move): plans refresh their copies
+    const void *busy = nullptr;  // the plan whose submitted run is in flight on this cache
 };
+
+// A run submitted on the cache and not finished (xc_encode_submit without poll/wait): every other
+// operation on the cache would read a partial count, or move the arrays that run's kernels (and
+// its host-side redo) still use.
+static int cache_busy(const xc_cache *c, const void *owner = nullptr)
+{
+    if (c && c->busy && c->busy != owner)
+        return fail(XC_EBUSY, "a run on this cache is in flight (xc_encode_poll / xc_encode_wait first)");
+    return XC_OK;
+}
 
 // The reference's memory cache is unbounded (xcodec/xcodec_cache.h:164,182-188).  The device cache
 // starts at the capacity it was created with and grows (cache_reserve) before any run that could
@@ -437,6 +448,7 @@ static int cache_grow(xc_cache *c, uint64_t need)
 // Room for `extra` more segments: grow first when the count could pass the capacity.
 static int cache_reserve(xc_cache *c, uint64_t extra)
 {
+    if (int rc = cache_busy(c)) return rc;
     if (c->host_count < 0) {
         uint32_t v = 0;
         int rc = cache_count_host(c, &v);
@@ -453,6 +465,7 @@ static int cache_reserve(xc_cache *c, uint64_t extra)
 extern "C" int xc__cache_truncate(xc_cache *c, uint64_t keep)
 {
     int rc = set_dev(c->ctx);
+    if (!rc) rc = cache_busy(c);
     if (rc) return rc;
     return cache_rebuild(c, c->cap, (uint32_t)std::min<uint64_t>(keep, 0xFFFFFFFFu), true);
 }
@@ -462,6 +475,7 @@ extern "C" int xc__cache_kill(xc_cache *c, const uint64_t *h, uint64_t n)
 {
     if (!n) return XC_OK;
     int rc = set_dev(c->ctx);
+    if (!rc) rc = cache_busy(c);
     if (rc) return rc;
     hipStream_t s = c->ctx->stream;
     uint64_t *d = nullptr;
@@ -480,6 +494,7 @@ extern "C" int xc__cache_enter_bulk(xc_cache *c, const uint64_t *h, const uint8_
 {
     if (!n) return XC_OK;
     int rc = set_dev(c->ctx);
+    if (!rc) rc = cache_busy(c);
     if (rc) return rc;
     if ((rc = cache_reserve(c, n))) return rc;
     hipStream_t s = c->ctx->stream;
@@ -531,6 +546,7 @@ extern "C" int xc_cache_snapshot(xc_cache *c)
 {
     if (!c) return fail(XC_EINVAL, "null");
     int rc = set_dev(c->ctx);
+    if (!rc) rc = cache_busy(c);
     if (rc) return rc;
     if ((rc = cache_count_host(c, &c->snap_count))) return rc;
     c->host_count = c->snap_count;
@@ -568,6 +584,7 @@ extern "C" int xc_cache_restore_async(xc_cache *c)
     if (!c) return fail(XC_EINVAL, "null");
     if (!c->has_snap) return fail(XC_EINVAL, "no snapshot");
     int rc = set_dev(c->ctx);
+    if (!rc) rc = cache_busy(c);
     if (rc) return rc;
     hipStream_t s = c->ctx->stream;
     if (c->host_count >= 0) {
@@ -599,6 +616,7 @@ extern "C" int xc_cache_restore(xc_cache *c)
     if (!c) return fail(XC_EINVAL, "null");
     if (!c->has_snap) return fail(XC_EINVAL, "no snapshot");
     int rc = set_dev(c->ctx);
+    if (!rc) rc = cache_busy(c);
     if (rc) return rc;
     uint32_t cur = 0;
     if ((rc = cache_count_host(c, &cur))) return rc;
@@ -612,6 +630,7 @@ extern "C" int xc_cache_lookup(xc_cache *c, uint64_t h, uint8_t *out, int *found
 {
     if (!c || !out || !found) return fail(XC_EINVAL, "null");
     int rc = set_dev(c->ctx);
+    if (!rc) rc = cache_busy(c);
     if (rc) return rc;
     hipStream_t s = c->ctx->stream;
     uint32_t *d_found = c->ctx->d_scratch;
@@ -629,6 +648,7 @@ extern "C" int xc_cache_enter(xc_cache *c, uint64_t h, const uint8_t *seg)
 {
     if (!c || !seg) return fail(XC_EINVAL, "null");
     int rc = set_dev(c->ctx);
+    if (!rc) rc = cache_busy(c);
     if (rc) return rc;
     hipStream_t s = c->ctx->stream;
     if ((rc = cache_reserve(c, 1))) return rc;
@@ -1330,6 +1350,10 @@ static int launch_scan(xc_plan *p, const Layer &L, const DevSet &set, uint32_t c
     if (p->timing) p->ktimes.scan_bytes += p->chunk_bytes[ck_hi] - p->chunk_bytes[ck_lo];
     uint32_t need = (ck_hi - ck_lo + SCAN_WAVES * p->scan_unit - 1) / (SCAN_WAVES * p->scan_unit);
     uint32_t grid = std::min<uint32_t>(need, (uint32_t)ctx->n_cu);
+    // XC_SCAN_GRID=n (tuning experiments): at most n scan workgroups, the other CUs left to the
+    // kernels of other streams
+    static const uint32_t grid_cap = getenv("XC_SCAN_GRID") ? (uint32_t)atoi(getenv("XC_SCAN_GRID")) : 0u;
+    if (grid_cap) grid = std::min(grid, grid_cap);
     // XC_SCAN_ABLATION=m (timing experiments only: results are wrong) runs k_scan<m> in the pipeline
     static const int abl = getenv("XC_SCAN_ABLATION") ? atoi(getenv("XC_SCAN_ABLATION")) : 0;
     auto kern = abl == 1 ? k_scan<1> : abl == 2 ? k_scan<2> : abl == 3 ? k_scan<3> : abl == 4 ? k_scan<4>
@@ -1618,7 +1642,7 @@ extern "C" int xc_encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out,
     hipStream_t s = p->cache->ctx->stream;
     // room for every segment this run can declare (the reference's cache never fills)
     xc_cache *c = p->cache;
-    if ((rc = cache_reserve(c, p->max_new))) return rc;
+    if ((rc = cache_busy(c, p)) || (rc = cache_reserve(c, p->max_new))) return rc;
     if (p->cache_gen != c->gen) {  // the cache grew: its arrays moved
         const PlanDev cp = cache_plandev(c);
         p->P.cache = cp.cache;
@@ -1671,6 +1695,7 @@ extern "C" int xc_encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out,
         if ((rc = record_ctl(p))) return rc;
     }
     p->inflight = true;
+    c->busy = p;
     return XC_OK;
 }
 
@@ -1679,6 +1704,7 @@ extern "C" int xc_encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out,
 static int encode_finish(xc_plan *p)
 {
     p->inflight = false;
+    p->cache->busy = nullptr;
     int rc = XC_OK;
     hipStream_t s = p->cache->ctx->stream;
     uint32_t ctl[CTL_WORDS];
@@ -1737,6 +1763,7 @@ extern "C" int xc_encode_poll(xc_plan *p, int *done)
     *done = 1;
     if (e != hipSuccess) {
         p->inflight = false;
+        p->cache->busy = nullptr;
         return fail(XC_EDEVICE, std::string("run: ") + hipGetErrorString(e));
     }
     return encode_finish(p);
@@ -1751,6 +1778,7 @@ extern "C" int xc_encode_wait(xc_plan *p)
     const hipError_t e = wait_decided(p);
     if (e != hipSuccess) {
         p->inflight = false;
+        p->cache->busy = nullptr;
         return fail(XC_EDEVICE, std::string("run: ") + hipGetErrorString(e));
     }
     return encode_finish(p);

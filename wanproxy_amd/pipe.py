@@ -198,12 +198,20 @@ class Batcher:
     cache, then the completions in call order.  Calls in a round share their caches exactly as the
     reference's sequential calls do (the device batches process their items in order against one
     cache), and every call of a round precedes every call of the next in call order, so the
-    results are the unbatched ones.  Returns the filters whose deferred consume failed."""
+    results are the unbatched ones.
+
+    :meth:`run` returns the filters whose deferred consume failed since the last :meth:`run`,
+    including failures of the runs a filter triggers itself (``flush``, ``on_read_timeout``, a
+    decoder consume that needs the earlier calls finished).  A failed filter is also marked
+    (``deferred_failed``): its next ``consume`` returns False, as the reference's consume of that
+    call would have (``xcodec_filter.cc:146-164,414-418``), and the caller tears the connection
+    down."""
 
     def __init__(self, backend):
         self.backend = backend
         self.jobs: list = []
         self.device_calls = 0
+        self._failed: list = []  # not reported by run() yet
 
     def submit_encode(self, owner, encoder, store, data: bytes, flush: bool, done) -> None:
         self.jobs.append(("e", owner, store, (encoder, data, flush), done))
@@ -215,7 +223,15 @@ class Batcher:
         return any(j[1] is owner for j in self.jobs)
 
     def run(self) -> list:
-        failed = []
+        """End of the event-loop turn: every deferred call; the filters that failed since the last
+        ``run``."""
+        self.drain()
+        failed, self._failed = self._failed, []
+        return failed
+
+    def drain(self) -> None:
+        """Every deferred call now (a filter needs its earlier calls finished); failures are kept
+        for the next :meth:`run` and marked on the filters."""
         while self.jobs:
             rnd, owners, enc_stores, dec_stores = [], set(), set(), set()
             for j in self.jobs:
@@ -247,8 +263,8 @@ class Batcher:
                     results[k] = o
             for j, r in zip(rnd, results):
                 if not j[4](r):
-                    failed.append(j[1])
-        return failed
+                    j[1].deferred_failed = True
+                    self._failed.append(j[1])
 
 
 def _frame(src: bytearray, trg: bytearray) -> None:
@@ -285,8 +301,11 @@ class EncodeFilter(Filter):
         self.eos_ack = False
         self.flushing = False
         self.flush_flags = 0
+        self.deferred_failed = False  # a deferred consume of this filter failed (Batcher)
 
     def consume(self, buf: bytes, flg: int = 0) -> bool:
+        if self.deferred_failed:
+            return False
         assert not self.flushing
         output = bytearray()
         if self.encoder is None:
@@ -313,7 +332,7 @@ class EncodeFilter(Filter):
     def _drain(self) -> None:
         # a direct codec call must follow every deferred one (the reference's order)
         if self.codec is not None and self.codec.batcher is not None:
-            self.codec.batcher.run()
+            self.codec.batcher.drain()
 
     def flush(self, flg: int) -> None:
         self._drain()
@@ -368,6 +387,7 @@ class DecodeFilter(Filter):
         self.flushing = False
         self.flush_flags = 0
         self.upstream: Filter | None = None
+        self.deferred_failed = False  # a deferred decode of this filter failed (Batcher)
 
     def set_upstream(self, f: Filter) -> None:
         self.upstream = f
@@ -411,6 +431,8 @@ class DecodeFilter(Filter):
     def consume(self, buf: bytes, flg: int = 0) -> bool:
         if self.upstream is None:
             return False  # "Decoder not configured"
+        if self.deferred_failed:
+            return False
         b = self.codec.batcher if self.codec is not None else None
         if b is not None:
             if (not self.received_eos and not self.unknown_hashes and not b.pending(self)
@@ -424,7 +446,9 @@ class DecodeFilter(Filter):
                 if self.frame_buffer and not self.unknown_hashes:
                     b.submit_decode(self, self.decoder_cache.store, lambda r: self._decoded(r, flg))
                 return True
-            b.run()  # anything else runs now, after every earlier deferred call
+            b.drain()  # anything else runs now, after every earlier deferred call
+            if self.deferred_failed:
+                return False  # (its own deferred decode failed: this consume is the teardown)
         self.pending += buf
         return self._parse(flg, defer=False)
 
@@ -534,7 +558,7 @@ class DecodeFilter(Filter):
 
     def flush(self, flg: int) -> None:
         if self.codec is not None and self.codec.batcher is not None:
-            self.codec.batcher.run()
+            self.codec.batcher.drain()  # (a failure is reported by the turn's run())
         self.flushing = True
         self.flush_flags |= flg
         if not self.upflushed and self.upstream is not None:

@@ -330,7 +330,7 @@ class CossCache:
     def stats(self) -> dict:
         o = np.zeros(6, np.uint64)
         _check(load_library().xc_coss_stats(self.h, o))
-        return dict(zip(["hits", "found_1", "found_2", "index", "stripe_limit", "serial"], (int(x) for x in o)))
+        return dict(zip(["lookups", "found_1", "found_2", "index", "stripe_limit", "serial"], (int(x) for x in o)))
 
     def lookup(self, h: int, store_only: bool = False) -> bytes | None:
         """XCodecCacheCOSS::lookup (side effects included); ``store_only``: the host store alone."""
