@@ -1,0 +1,39 @@
+/*
+ * facade/xcodec/xcodec_decoder.cc — XCodecDecoder over the device library (replaces
+ * xcodec/xcodec_decoder.cc; see xcodec_decoder.h).
+ */
+#include <vector>
+
+#include <common/buffer.h>
+#include <xcodec/xcodec.h>
+#include <xcodec/xcodec_cache.h>
+#include <xcodec/xcodec_decoder.h>
+
+XCodecDecoder::XCodecDecoder(XCodecCache* cache) : cache_(cache) { }
+
+XCodecDecoder::~XCodecDecoder() { }
+
+bool XCodecDecoder::decode(Buffer& output, Buffer& input, std::set<uint64_t>& unknown_hashes)
+{
+    if (input.empty())
+        return true;
+    const uint64_t n = input.length();
+    std::vector<uint8_t> in(n);
+    input.copyout(&in[0], n);
+    /* a REF (10 bytes) expands to 2048: the output bound of xc__decode_bound, and at least n */
+    uint64_t off = 0, len = n, cap = n * 205 + 16, olen = 0, consumed = 0, unknown = 0;
+    int32_t status = 0, has_unknown = 0;
+    std::vector<uint8_t> out(cap);
+    if (cache_->coss())
+        xchip::check(xc_coss_decode_batch_host(cache_->coss(), &in[0], &off, &len, 1, &out[0], &off, &cap, &olen,
+                                               &consumed, &status, &unknown, &has_unknown));
+    else
+        xchip::check(xc_decode_batch_host(cache_->device(), &in[0], &off, &len, 1, &out[0], &off, &cap, &olen,
+                                          &consumed, &status, &unknown, &has_unknown));
+    if (olen)
+        output.append(&out[0], olen);
+    input.skip(consumed);  /* the reference consumes exactly this much (xcodec_decoder.cc:85-173) */
+    if (has_unknown)
+        unknown_hashes.insert(unknown);
+    return status != 0;
+}

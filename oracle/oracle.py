@@ -42,6 +42,8 @@ def _load() -> C.CDLL:
     lib.xo_cache_free.argtypes = [C.c_void_p]
     lib.xo_cache_count.restype = C.c_size_t
     lib.xo_cache_count.argtypes = [C.c_void_p]
+    lib.xo_cache_segments.restype = C.c_size_t
+    lib.xo_cache_segments.argtypes = [C.c_void_p]
     lib.xo_cache_coss_stats.restype = C.c_int
     lib.xo_cache_coss_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
     lib.xo_cache_entry.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_uint64), C.c_void_p]
@@ -143,7 +145,7 @@ class Cache:
 
     def entries(self) -> list[tuple[int, bytes]]:
         out = []
-        for i in range(len(self)):
+        for i in range(int(lib().xo_cache_segments(self.h))):
             h = C.c_uint64()
             seg = np.zeros(2048, np.uint8)
             lib().xo_cache_entry(self.h, i, C.byref(h), seg.ctypes.data_as(C.c_void_p))

@@ -102,7 +102,8 @@ void xo_window_hashes(const uint8_t *data, size_t n, uint64_t *out)
 struct xo_cache {
     uint64_t *keys;  /* open addressing, EMPTY marked by idx == UINT32_MAX */
     uint32_t *idx;
-    size_t mask, count;
+    size_t mask, count; /* count: segments stored (every enter) */
+    size_t nkeys;       /* the map's size (a hash entered twice counts once) */
     uint64_t *seg_hash; /* insertion order */
     uint8_t *segs;
     size_t seg_cap;
@@ -183,7 +184,9 @@ void xo_cache_free(xo_cache *c)
     free(c);
 }
 
-size_t xo_cache_count(const xo_cache *c) { return c->coss ? xo_coss_count(c->coss) : c->count; }
+/* The map's entries (segment_hash_map_.size(), xcodec_cache.h:164). */
+size_t xo_cache_count(const xo_cache *c) { return c->coss ? xo_coss_count(c->coss) : c->nkeys; }
+size_t xo_cache_segments(const xo_cache *c) { return c->coss ? xo_coss_count(c->coss) : c->count; }
 
 /* COSSStats of a COSS cache (xcodec_cache_coss.h:179-187); 0 for the memory cache. */
 int xo_cache_coss_stats(const xo_cache *c, uint64_t *out6)
@@ -206,8 +209,9 @@ static long cache_find(const xo_cache *c, uint64_t h)
 int xo_cache_lookup(xo_cache *c, uint64_t h, const uint8_t **data)
 { /* xcodec_cache.h:190-210 */
     if (c->coss) return xo_coss_lookup(c->coss, h, data);
-    for (int i = 0; i < XO_WINDOW_COUNT; i++) { /* find_recent, :137-147 */
-        if (c->window[i].hash == h && c->window[i].data) {
+    for (int i = 0; i < XO_WINDOW_COUNT; i++) { /* find_recent, :137-147: the first entry with */
+        if (c->window[i].hash == h) {           /* the hash (an unused slot: hash 0, no data) */
+            if (!c->window[i].data) break;
             *data = c->window[i].data;
             return 1;
         }
@@ -248,6 +252,7 @@ void xo_cache_enter(xo_cache *c, uint64_t h, const uint8_t *seg)
         c->idx[s] = (uint32_t)id;
         return;
     }
+    c->nkeys++;
     if ((c->count) * 2 > c->mask + 1) cache_rehash(c, (c->mask + 1) * 2);
     size_t s = slot_of(h, c->mask);
     while (c->idx[s] != UINT32_MAX) s = (s + 1) & c->mask;
@@ -309,6 +314,9 @@ xo_encoder *xo_encoder_new(xo_cache *c)
     e->cand = -1;
     return e;
 }
+
+/* Bytes pending in source_ (XCodecEncoder's state between calls, xcodec_encoder.h:45-50). */
+size_t xo_encoder_pending(const xo_encoder *e) { return e->src.len - e->src_head; }
 
 void xo_encoder_free(xo_encoder *e)
 {

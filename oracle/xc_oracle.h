@@ -76,6 +76,7 @@ void xo_bytes_free(xo_bytes *b);
 typedef struct xo_encoder xo_encoder;
 xo_encoder *xo_encoder_new(xo_cache *c);
 void xo_encoder_free(xo_encoder *e);
+size_t xo_encoder_pending(const xo_encoder *e);
 void xo_encode(xo_encoder *e, const uint8_t *in, size_t n, xo_bytes *out);
 int xo_flush(xo_encoder *e, xo_bytes *out);
 

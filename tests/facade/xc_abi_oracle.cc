@@ -1,0 +1,86 @@
+/* TEST ONLY (tests/test_facade.py): the subset of include/xcodec_hip.h the facade calls, over the
+ * CPU oracle (oracle/xc_oracle.c), so that the facade linked with the reference's own Buffer
+ * (common/buffer.cc) round-trips a stream on the CPU build.  The product library is the HIP one
+ * (wanproxy_amd/libxcodec_hip.so); this double only exercises the facade's Buffer adaptation. */
+#include <cstring>
+#include <string>
+
+#include "../../include/xcodec_hip.h"
+#include "../../oracle/xc_oracle.h"
+
+struct xc_ctx { int dev; };
+struct xc_cache { xo_cache *c; };
+struct xc_encoder { xo_encoder *e; xc_cache *cache; };
+struct xc_coss { xc_cache cache; };
+
+static std::string g_err;
+
+extern "C" {
+const char *xc_last_error(void) { return g_err.c_str(); }
+int xc_device_count(int *n) { *n = 1; return XC_OK; }
+int xc_ctx_create(int dev, xc_ctx **out) { *out = new xc_ctx{dev}; return XC_OK; }
+int xc_ctx_destroy(xc_ctx *c) { delete c; return XC_OK; }
+int xc_cache_create(xc_ctx *, uint64_t, xc_cache **out) { *out = new xc_cache{xo_cache_new()}; return XC_OK; }
+int xc_cache_destroy(xc_cache *c) { if (c) xo_cache_free(c->c); delete c; return XC_OK; }
+int xc_cache_count(xc_cache *c, uint64_t *n) { *n = xo_cache_count(c->c); return XC_OK; }
+int xc_cache_lookup(xc_cache *c, uint64_t h, uint8_t *out, int *found)
+{
+    const uint8_t *d = nullptr;
+    *found = xo_cache_lookup(c->c, h, &d);
+    if (*found) std::memcpy(out, d, XC_SEGMENT_LENGTH);
+    return XC_OK;
+}
+int xc_cache_enter(xc_cache *c, uint64_t h, const uint8_t *seg) { xo_cache_enter(c->c, h, seg); return XC_OK; }
+int xc_encoder_create(xc_cache *c, xc_encoder **out) { *out = new xc_encoder{xo_encoder_new(c->c), c}; return XC_OK; }
+int xc_encoder_destroy(xc_encoder *e) { if (e) xo_encoder_free(e->e); delete e; return XC_OK; }
+int xc_encoder_pending(xc_encoder *e, uint64_t *n) { *n = xo_encoder_pending(e->e); return XC_OK; }
+int xc_encode_streams(xc_encoder *const *enc, const uint8_t *const *in, const uint64_t *in_len, const uint32_t *flags,
+                      uint64_t n, uint8_t *out, const uint64_t *out_off, const uint64_t *out_cap, uint64_t *out_len)
+{
+    for (uint64_t k = 0; k < n; k++) {
+        xo_bytes b = {nullptr, 0, 0};
+        if (in_len[k]) xo_encode(enc[k]->e, in[k], in_len[k], &b);
+        if (flags && (flags[k] & XC_STREAM_FLUSH)) xo_flush(enc[k]->e, &b);
+        if (b.len > out_cap[k]) { xo_bytes_free(&b); g_err = "output capacity too small"; return XC_EINVAL; }
+        if (b.len) std::memcpy(out + out_off[k], b.data, b.len);
+        out_len[k] = b.len;
+        xo_bytes_free(&b);
+    }
+    return XC_OK;
+}
+int xc_decode_batch_host(xc_cache *c, const uint8_t *in, const uint64_t *in_off, const uint64_t *in_len, uint64_t nbuf,
+                         uint8_t *out, const uint64_t *out_off, const uint64_t *out_cap, uint64_t *out_len,
+                         uint64_t *consumed, int32_t *status, uint64_t *unknown, int32_t *has_unknown)
+{
+    return xo_decode_batch(c->c, in, in_off, in_len, nbuf, out, out_off, out_cap, out_len, consumed, status, unknown,
+                           has_unknown) ? XC_EINVAL : XC_OK;
+}
+int xc_hash_segments_host(xc_ctx *, const uint8_t *segs, uint64_t n, uint64_t *out)
+{
+    for (uint64_t i = 0; i < n; i++) out[i] = xo_hash_segment(segs + i * XC_SEGMENT_LENGTH);
+    return XC_OK;
+}
+int xc_coss_open(xc_ctx *, const char *dir, const char *uuid, uint64_t size_mb, xc_coss **out)
+{
+    *out = new xc_coss{{xo_cache_new_coss(dir, uuid, size_mb)}};
+    return XC_OK;
+}
+int xc_coss_close(xc_coss *c) { if (c) xo_cache_free(c->cache.c); delete c; return XC_OK; }
+xc_cache *xc_coss_cache(xc_coss *c) { return &c->cache; }
+int xc_coss_lookup(xc_coss *c, uint64_t h, uint8_t *out, int *found) { return xc_cache_lookup(&c->cache, h, out, found); }
+int xc_coss_enter(xc_coss *c, uint64_t h, const uint8_t *seg) { return xc_cache_enter(&c->cache, h, seg); }
+int xc_coss_encode_streams(xc_coss *, xc_encoder *const *enc, const uint8_t *const *in, const uint64_t *in_len,
+                           const uint32_t *flags, uint64_t n, uint8_t *out, const uint64_t *out_off,
+                           const uint64_t *out_cap, uint64_t *out_len)
+{
+    return xc_encode_streams(enc, in, in_len, flags, n, out, out_off, out_cap, out_len);
+}
+int xc_coss_decode_batch_host(xc_coss *c, const uint8_t *in, const uint64_t *in_off, const uint64_t *in_len,
+                              uint64_t nbuf, uint8_t *out, const uint64_t *out_off, const uint64_t *out_cap,
+                              uint64_t *out_len, uint64_t *consumed, int32_t *status, uint64_t *unknown,
+                              int32_t *has_unknown)
+{
+    return xc_decode_batch_host(&c->cache, in, in_off, in_len, nbuf, out, out_off, out_cap, out_len, consumed, status,
+                                unknown, has_unknown);
+}
+}

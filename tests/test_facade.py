@@ -1,0 +1,57 @@
+"""The drop-in boundary compiles (CPU, this container only: it needs /root/reference's sources).
+
+facade/xcodec/ replaces the reference's xcodec_cache.h, xcodec_encoder.{h,cc}, xcodec_decoder.{h,cc}
+and cache/coss/xcodec_cache_coss.h.  This test compiles the reference's own,
+unchanged xcodec/xcodec_filter.cc (the EncodeFilter / DecodeFilter that call the codec,
+xcodec_filter.cc:122-512) and proxy/wanproxy_codec.h (WANProxyCodec::xcache_, :43-71) against it,
+then links the facade with the reference's Buffer (common/buffer.cc) and round-trips a stream.
+
+Two test-only pieces make that possible here (tests/facade/): the three libuuid declarations
+common/uuid/uuid.h needs (the image has libuuid.so.1 but not its header), and, for the CPU round
+trip, the part of the C ABI the facade calls over the CPU oracle (the product library needs a GPU).
+This is a check of our headers against the reference's code, not an oracle claim; nothing built
+here goes to the GPU box."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = "/root/reference"
+
+pytestmark = pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "xcodec")), reason="needs the reference sources")
+
+FLAGS = ["-std=gnu++17", "-O1", "-DNDEBUG=1", "-Wno-deprecated", "-include", "common/common.h",
+         "-I" + os.path.join(ROOT, "facade"), "-I" + os.path.join(ROOT, "include"), "-I" + REF,
+         "-I" + os.path.join(ROOT, "tests", "facade", "shim")]
+
+
+def _cc(args, cwd):
+    r = subprocess.run(["g++"] + FLAGS + args, cwd=cwd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-4000:]
+
+
+def test_reference_filter_compiles_against_the_facade(tmp_path):
+    _cc(["-c", os.path.join(REF, "xcodec", "xcodec_filter.cc"), "-o", "filter.o"], tmp_path)
+    (tmp_path / "codec_tu.cc").write_text("#include <proxy/wanproxy_codec.h>\n#include <proxy/wanproxy.h>\n")
+    _cc(["-c", "codec_tu.cc", "-o", "codec.o"], tmp_path)
+    # the filter calls exactly the facade's codec and cache classes
+    nm = subprocess.run(["nm", "-C", "-u", str(tmp_path / "filter.o")], capture_output=True, text=True).stdout
+    for sym in ("XCodecEncoder::XCodecEncoder(XCodecCache*)", "XCodecEncoder::encode(Buffer&, Buffer&)",
+                "XCodecEncoder::flush(Buffer&)", "XCodecDecoder::XCodecDecoder(XCodecCache*)",
+                "XCodecDecoder::decode(Buffer&, Buffer&, std::set<unsigned long"):
+        assert sym in nm, sym
+
+
+def test_facade_round_trip_with_the_reference_buffer(tmp_path):
+    make = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], capture_output=True, text=True)
+    assert make.returncode == 0, make.stderr
+    fac = os.path.join(ROOT, "facade", "xcodec")
+    t = os.path.join(ROOT, "tests", "facade")
+    _cc(["-o", "rt", os.path.join(t, "facade_roundtrip.cc"), os.path.join(fac, "xcodec_encoder.cc"),
+         os.path.join(fac, "xcodec_decoder.cc"), os.path.join(t, "xc_abi_oracle.cc"),
+         os.path.join(REF, "common", "buffer.cc"), os.path.join(REF, "common", "log.cc"),
+         os.path.join(REF, "common", "uuid", "uuid.cc"), "-L" + os.path.join(ROOT, "oracle"), "-loracle",
+         "-Wl,-rpath," + os.path.join(ROOT, "oracle"), "-l:libuuid.so.1"], tmp_path)
+    r = subprocess.run([str(tmp_path / "rt")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "facade ok" in r.stdout, r.stdout + r.stderr

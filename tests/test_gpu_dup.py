@@ -1,0 +1,135 @@
+"""A hash entered twice with different bytes (XCodecMemoryCache::enter, xcodec/xcodec_cache.h:182-188).
+
+The reference asserts that an entered hash is new; a release build overwrites the map value, while
+the 64-entry recent window (:94-98,128-147) keeps returning the bytes it remembered for that hash
+until 64 later remembers push the entry out.  The only way an encoder reaches it: a stateful
+connection's candidate is looked up (a miss) in one call and declared in a later one
+(xcodec/xcodec_encoder.cc:77-82,203-215), after another connection entered a different segment with
+the same 64-bit hash.  The hash is weak enough to build such a pair: odd bytes with +-2 swaps at
+(i, i+1, j, j+1) keep both sums.
+
+Every call's bytes must equal the stateful oracle's (oracle/xc_oracle.c: release semantics with the
+recent window), and the cache's entry count the reference map's size."""
+import numpy as np
+import pytest
+
+from wanproxy_amd import workloads as W
+
+pytestmark = pytest.mark.gpu
+
+POOL = 96
+
+
+def _collision_pair(seed=1):
+    rng = np.random.default_rng(seed)
+    x = (rng.integers(2, 126, 2048, dtype=np.int64) * 2 + 1).astype(np.uint8)
+    y = x.copy()
+    y[100] += 2; y[101] -= 2; y[1500] -= 2; y[1501] += 2
+    return x, y
+
+
+def _cat(*a):
+    return np.concatenate([np.asarray(v, np.uint8) for v in a])
+
+
+def _run(ctx, oracle_mod, nconn, calls, batch):
+    import wanproxy_amd as w
+    warm = W.pool_warmup_buffers(POOL)
+    oc = oracle_mod.Cache()
+    gc = w.XCodecCache(ctx, 1 << 12)
+    oc.encode_batch(warm)
+    w.XCodecEncoder(gc).encode_batch(warm)
+    oenc = [oracle_mod.Encoder(oc) for _ in range(nconn)]
+    genc = [w.XCodecStreamEncoder(gc) for _ in range(nconn)]
+    want = []
+    for k, d, f in calls:
+        o = oenc[k].encode(d)
+        if f:
+            o += oenc[k].flush()[1]
+        want.append(o)
+    if batch:
+        got = w.encode_streams([(genc[k], d, f) for k, d, f in calls])
+    else:
+        got = []
+        for k, d, f in calls:
+            o = genc[k].encode(d)
+            if f:
+                o += genc[k].flush()[1]
+            got.append(o)
+    bad = [i for i, (g, e) in enumerate(zip(got, want)) if g != e]
+    assert not bad, f"calls {bad} differ from the oracle"
+    for k in range(nconn):
+        assert genc[k].flush() == oenc[k].flush(), k
+    assert len(gc) == len(oc)
+    return want, gc, oc
+
+
+def _calls(remembered: bool, evict: int):
+    """Connection 0 carries candidate x across calls; connection 1 enters the twin y first.
+    remembered: a lookup of y (connection 2) puts y's entry in the recent window before x is
+    declared.  evict: REFs of that many distinct pool segments after the declaration (64 push the
+    remembered entry out)."""
+    x, y = _collision_pair()
+    p = W.pool(POOL)
+    calls = [
+        (0, _cat(x, W.gen(11, 100)), False),      # candidate x, carried (encode() only)
+        (1, y, True),                             # y declared by flush(): the hash is in the map
+    ]
+    if remembered:
+        calls.append((2, _cat(y, W.gen(12, 50)), True))  # REF y: remembered in the window
+    calls += [
+        (0, W.gen(13, 4096), False),              # x declared at cand + 4095: the duplicate enter
+        (3, y, True),                             # window: y (REF) / map: x (collision)
+        (4, x, True),                             # window: y (collision) / map: x (REF)
+    ]
+    if evict:
+        segs = [p[2048 * i:2048 * (i + 1)] for i in range(evict)]
+        calls.append((5, _cat(*segs), True))
+    calls += [
+        (6, x, True),
+        (7, y, True),
+        (0, W.gen(14, 300), True),
+    ]
+    return calls
+
+
+def _has_ref(stream: bytes) -> bool:
+    return b"\xf1\x02" in stream
+
+
+@pytest.mark.parametrize("batch", [True, False])
+@pytest.mark.parametrize("remembered,evict", [(True, 0), (True, 70), (False, 0), (True, 40)])
+def test_duplicate_enter_follows_the_release_reference(gpu_ctx, oracle_mod, batch, remembered, evict):
+    calls = _calls(remembered, evict)
+    want, gc, oc = _run(gpu_ctx, oracle_mod, 8, calls, batch)
+    i = 3 if remembered else 2
+    # the scenario does reach both answers of the reference (checked on the oracle's own output)
+    if remembered:
+        assert _has_ref(want[i + 1]) and not _has_ref(want[i + 2]), "window answers y after the overwrite"
+    else:
+        assert not _has_ref(want[i + 1]) and _has_ref(want[i + 2]), "the map answers x at once"
+    last_x, last_y = want[-3], want[-2]
+    if remembered and evict < 64:
+        assert not _has_ref(last_x) and _has_ref(last_y)
+    else:
+        assert _has_ref(last_x) and not _has_ref(last_y)
+
+
+def test_duplicate_enter_then_batches_and_lookups(gpu_ctx, oracle_mod):
+    """After the duplicate enter: fresh-encoder batches (xc_encode_batch_host) and direct lookups
+    (the <ASK> handler's, xcodec_filter.cc:296) see what the reference's cache returns."""
+    import wanproxy_amd as w
+    x, y = _collision_pair()
+    calls = _calls(True, 0)
+    want, gc, oc = _run(gpu_ctx, oracle_mod, 8, calls, True)
+    h = int(oracle_mod.hash_segment(x))
+    assert h == int(oracle_mod.hash_segment(y))
+    p = W.pool(POOL)
+    bufs = [_cat(x, W.gen(20, 99)), _cat(y, W.gen(21, 77)),
+            _cat(*[p[2048 * i:2048 * (i + 1)] for i in range(70)]), _cat(W.gen(22, 33), x), y]
+    o = oc.encode_batch(bufs)
+    g = w.XCodecEncoder(gc).encode_batch(bufs)
+    assert g == o
+    # a direct lookup: the window's bytes or the map's (a remember when the map answers)
+    assert gc.lookup(h) == oc.lookup(h)
+    assert len(gc) == len(oc)

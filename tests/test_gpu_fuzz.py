@@ -21,12 +21,10 @@ def _collision_pair(seed):
     return x, y
 
 
-def _batch(rng, pool, pair=True):
-    """pair=False: only one half of the collision pair (stateful streams: see DESIGN.md §8 on a
-    declaration of a hash another connection entered with other bytes since the lookup)."""
+def _batch(rng, pool):
+    """Buffers of random pieces, both halves of a collision pair among them (with stateful streams
+    the pair reaches the duplicate enter of xcodec_cache.h:182-188, tests/test_gpu_dup.py)."""
     x, y = _collision_pair(int(rng.integers(1 << 30)))
-    if not pair:
-        y = x
     pieces = []
     bufs = []
     for _ in range(int(rng.integers(8, 48))):
@@ -98,3 +96,41 @@ def test_fuzz_encode_decode(gpu_ctx, oracle_mod, monkeypatch, seed):
         for i, (st, out, consumed, unk) in enumerate(res):
             assert st == 1 and unk is None and consumed == len(streams[i]), (seed, i)
             assert out == bufs[i].tobytes(), (seed, i)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_fuzz_streams(gpu_ctx, oracle_mod, monkeypatch, seed):
+    """Stateful connections (encode() without flush, calls cut at random points and shuffled over
+    connections) over one cache against the oracle's stateful encoders, the collision pair included."""
+    import wanproxy_amd as w
+    rng = np.random.default_rng(2000 + seed)
+    monkeypatch.setenv("XC_CHUNK_BLOCKS", str(int(rng.choice([1, 2, 3, 5, 8]))))
+    monkeypatch.setenv("XC_SUB_MB", str(int(rng.choice([1, 2, 512]))))
+    pool = W.pool(64)
+    warm = [pool[i:i + 65536] for i in range(0, int(rng.integers(1, 9)) * 65536, 65536)]
+    oc = oracle_mod.Cache()
+    gc = w.XCodecCache(gpu_ctx, int(rng.choice([1024, 1 << 16])))
+    oc.encode_batch(warm)
+    w.XCodecEncoder(gc).encode_batch(warm)
+    n = int(rng.integers(2, 12))
+    oe = [oracle_mod.Encoder(oc) for _ in range(n)]
+    ge = [w.XCodecStreamEncoder(gc) for _ in range(n)]
+    for _ in range(3):
+        calls = []
+        for buf in _batch(rng, pool):
+            c = int(rng.integers(n))
+            cuts = sorted(rng.integers(0, max(buf.size, 1), int(rng.integers(0, 4))))
+            for piece in np.split(buf, cuts):
+                calls.append((c, piece, bool(rng.random() < 0.4)))
+        want = []
+        for c, d, f in calls:
+            o = oe[c].encode(d)
+            if f:
+                o += oe[c].flush()[1]
+            want.append(o)
+        got = w.encode_streams([(ge[c], d, f) for c, d, f in calls])
+        bad = [i for i, (g, e) in enumerate(zip(got, want)) if g != e]
+        assert not bad, (seed, bad[:5])
+    for c in range(n):
+        assert ge[c].flush() == oe[c].flush(), c
+    assert len(gc) == len(oc)

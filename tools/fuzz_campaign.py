@@ -43,7 +43,7 @@ while time.time() < t_end:
             ge = [w.XCodecStreamEncoder(gc) for _ in range(n)]
             streams = []
             for _ in range(int(rng.integers(2, 6))):
-                bufs = F._batch(rng, pool, pair=False)
+                bufs = F._batch(rng, pool)
                 if rng.random() < 0.5:
                     want = oc.encode_batch(bufs)
                     if w.XCodecEncoder(gc).encode_batch(bufs) != want:
@@ -126,7 +126,7 @@ while time.time() < t_end:
             ge = [w.XCodecStreamEncoder(gc) for _ in range(n)]
             for _ in range(int(rng.integers(1, 4))):
                 calls = []
-                for buf in F._batch(rng, pool, pair=False):
+                for buf in F._batch(rng, pool):
                     c = int(rng.integers(n))
                     cuts = sorted(rng.integers(0, max(buf.size, 1), int(rng.integers(0, 4))))
                     for piece in np.split(buf, cuts):

@@ -39,15 +39,11 @@
 
 #include "../../include/xcodec_hip.h"
 
-extern "C" int xc__set_error(int code, const char *msg);
-extern "C" int xc__encode_batch_host_coll(xc_cache *c, const uint8_t *in, const uint64_t *in_off,
-                                          const uint64_t *in_len, uint64_t nbuf, uint8_t *out,
-                                          const uint64_t *out_off, const uint64_t *out_cap, uint64_t *out_len,
-                                          const uint64_t *start, const int64_t *cand, const uint32_t *flags,
-                                          uint64_t *rbase, int64_t *rcand, uint32_t *coll_cnt, uint32_t *coll);
-extern "C" int xc__cache_truncate(xc_cache *c, uint64_t keep);
-extern "C" int xc__cache_kill(xc_cache *c, const uint64_t *h, uint64_t n);
-extern "C" int xc__cache_enter_bulk(xc_cache *c, const uint64_t *h, const uint8_t *segs, uint64_t n);
+#include "xc_replay.h"
+
+extern "C" void xc__cache_untracked(xc_cache *c);
+extern "C" int xc__cache_find(xc_cache *c, const uint64_t *h, uint64_t n, uint64_t *val);
+extern "C" int xc__cache_read(xc_cache *c, uint64_t h, uint8_t *out, int *found);
 
 namespace coss {
 
@@ -58,7 +54,6 @@ constexpr uint32_t STRIPE_SEGS = 512;        // :85
 constexpr int LOADED = 16;                   // :86
 constexpr uint64_t BASIC_MB = 1024;          // :87
 constexpr int WINDOW = 64;                   // xcodec_cache.h:48
-constexpr uint32_t COLL_CAP = 16;            // xc_kernels.h
 
 struct Meta {  // COSSMetadata (:147-160), on disk as is
     uint32_t signature, version;
@@ -83,17 +78,8 @@ struct Stripe {  // COSSStripe (:170-177)
     uint8_t seg[STRIPE_SEGS][SEG];
 };
 
-struct Loc {
-    uint64_t range;
-    uint32_t pos;
-};
-
-// What a Store operation touched: the hashes and stripe ranges whose lookup result may have
-// changed, and the slots whose bytes were replaced (recent-window entries point into them).
-struct Touch {
-    std::vector<uint64_t> hs, ranges;
-    std::vector<int> slots;
-};
+using replay::Loc;
+using replay::Touch;
 
 class Store {
 public:
@@ -199,7 +185,7 @@ public:
     // What lookup(h) returns now, without its side effects: FOUND (*p: the bytes), IN_FILE (the
     // stripe is loaded from the file first, *l: where the bytes are), ABSENT, or LOAD_MISS (not
     // found, after loading a stripe: a miss with side effects).
-    enum { ABSENT, FOUND, IN_FILE, LOAD_MISS };
+    enum { ABSENT = replay::ABSENT, FOUND = replay::FOUND, IN_FILE = replay::IN_FILE, LOAD_MISS = replay::LOAD_MISS };
     int peek(uint64_t h, const uint8_t **p, Loc *l) const
     {
         for (int i = 0; i < WINDOW; i++)
@@ -471,16 +457,9 @@ private:
     uint64_t lookups_ = 0, found_1_ = 0, found_2_ = 0;
 };
 
-// What a Store operation did to the set of segments a lookup finds (the device mirror's contents).
-struct Change {
-    std::vector<uint64_t> removed;  // no longer found
-    std::vector<uint64_t> added;    // found now, or found with other bytes
-    std::vector<uint8_t> bytes;     // their bytes, SEG each
-    bool any() const { return !removed.empty() || !added.empty(); }
-};
-
 }  // namespace coss
 
+// The COSS cache: the Store, and the device cache as its mirror (xc_replay.h's context).
 struct xc_coss {
     xc_ctx *ctx = nullptr;
     xc_cache *cache = nullptr;  // the device mirror (null for a host-only store)
@@ -489,135 +468,58 @@ struct xc_coss {
     std::unordered_map<uint64_t, uint64_t> known;
     // hashes a lookup misses only after loading a stripe (a miss with side effects)
     std::unordered_set<uint64_t> load_miss;
+
+    // per replay pass: hashes the device held before the pass's batch, and those entered in it
+    std::unordered_set<uint64_t> pre, inpass;
+    int err = XC_OK;
+
+    // the device entered a declared segment: its bytes, unless the hash was there already (the
+    // device keeps a key's first segment: a declaration of a hash another connection entered since
+    // the candidate's lookup, xcodec_memcache.cpp) -- then the mirror holds what it held, or, for two
+    // enters in one batch, whichever the device took
+    void entered(uint64_t h, const uint8_t *seg)
+    {
+        if (pre.count(h)) return;
+        if (inpass.insert(h).second) {
+            known[h] = replay::fingerprint(seg);
+            return;
+        }
+        uint8_t b[replay::SEG];
+        int found = 0;
+        if (!err && (err = xc__cache_read(cache, h, b, &found)) == XC_OK && found) known[h] = replay::fingerprint(b);
+    }
+    int before_mirror(const replay::Change &) { return XC_OK; }
+    void mirrored(const replay::Change &) {}
+    int begin_pass(const std::vector<uint64_t> &hs, uint64_t count0)
+    {
+        pre.clear();
+        inpass.clear();
+        std::vector<uint64_t> q(hs);
+        std::sort(q.begin(), q.end());
+        q.erase(std::unique(q.begin(), q.end()), q.end());
+        if (q.empty()) return XC_OK;
+        std::vector<uint64_t> v(q.size());
+        int rc = xc__cache_find(cache, q.data(), q.size(), v.data());
+        for (size_t i = 0; i < q.size() && !rc; i++)
+            if (v[i] != ~0ull && v[i] < count0) pre.insert(q[i]);
+        return rc;
+    }
+    int end_pass() { return err; }
+    int unmirrorable()
+    {
+        if (err) return err;
+        if (load_miss.empty()) return XC_OK;
+        return xc__set_error(XC_EINVAL, "COSS: a stripe header in the file disagrees with the index (a cache of "
+                                        "16 stripes or fewer after a stripe's second copy was detached); "
+                                        "lookups that miss after loading a stripe are not mirrored on the device");
+    }
 };
 
 namespace {
-using coss::Change;
-using coss::Loc;
 using coss::SEG;
 using coss::Store;
-using coss::Touch;
-
-uint64_t fingerprint(const uint8_t *p)
-{
-    uint64_t h = 0x9E3779B97F4A7C15ull;
-    for (uint32_t i = 0; i < SEG; i += 8) {
-        uint64_t w;
-        std::memcpy(&w, p + i, 8);
-        h = (h ^ w) * 0x100000001B3ull;
-        h ^= h >> 29;
-    }
-    return h;
-}
-
-// The hashes an operation touched, looked up again without side effects: those the device holds
-// and a lookup no longer finds, and those a lookup finds that the device lacks or holds with other
-// bytes, go into ch (and `known` follows).
-int settle(xc_coss *c, const Touch &t, Change &ch)
-{
-    std::vector<uint64_t> cand(t.hs);
-    for (uint64_t r : t.ranges) c->st.owners(r, cand);
-    for (int s : t.slots) c->st.window_in_slot(s, cand);
-    std::sort(cand.begin(), cand.end());
-    cand.erase(std::unique(cand.begin(), cand.end()), cand.end());
-    uint8_t buf[SEG];
-    for (uint64_t h : cand) {
-        if (!h) continue;
-        const uint8_t *p = nullptr;
-        Loc l{0, 0};
-        const int r = c->st.peek(h, &p, &l);
-        if (r == Store::LOAD_MISS) c->load_miss.insert(h);
-        else c->load_miss.erase(h);
-        if (r == Store::IN_FILE) {
-            if (!c->st.read_segment(l, buf)) return xc__set_error(XC_EDEVICE, "COSS: cannot read the cache file");
-            p = buf;
-        }
-        if (r != Store::FOUND && r != Store::IN_FILE) {
-            if (c->known.erase(h)) ch.removed.push_back(h);
-            continue;
-        }
-        const uint64_t fp = fingerprint(p);
-        auto it = c->known.find(h);
-        if (it != c->known.end() && it->second == fp) continue;
-        c->known[h] = fp;
-        ch.added.push_back(h);
-        ch.bytes.insert(ch.bytes.end(), p, p + SEG);
-    }
-    return XC_OK;
-}
-
-// The device mirror follows a change.
-int mirror(xc_coss *c, const Change &ch)
-{
-    int rc = XC_OK;
-    if (!ch.removed.empty()) rc = xc__cache_kill(c->cache, ch.removed.data(), ch.removed.size());
-    if (!rc && !ch.added.empty() && !(rc = xc__cache_kill(c->cache, ch.added.data(), ch.added.size())))
-        rc = xc__cache_enter_bulk(c->cache, ch.added.data(), ch.bytes.data(), ch.added.size());
-    return rc;
-}
-
-// A store operation on a device-backed COSS cache: the device follows at once.
-int follow(xc_coss *c, const Touch &t)
-{
-    if (!c->cache) return XC_OK;
-    Change ch;
-    int rc = settle(c, t, ch);
-    return rc ? rc : (ch.any() ? mirror(c, ch) : XC_OK);
-}
-
-// Later events of a batch that saw a change: any lookup of a hash it added or removed.
-struct Watch {
-    std::unordered_set<uint64_t> hs;
-    explicit Watch(const Change &ch) : hs(ch.removed.begin(), ch.removed.end())
-    {
-        hs.insert(ch.added.begin(), ch.added.end());
-    }
-    bool has(uint64_t h) const { return hs.count(h) != 0; }
-};
-
-int unmirrorable(xc_coss *c)
-{
-    if (c->load_miss.empty()) return XC_OK;
-    return xc__set_error(XC_EINVAL, "COSS: a stripe header in the file disagrees with the index (a cache of "
-                                    "16 stripes or fewer after a stripe's second copy was detached); "
-                                    "lookups that miss after loading a stripe are not mirrored on the device");
-}
-
-// One cache event of an encoder item, in the reference's order (xcodec_encoder.cc:72-171).
-struct EncEvent {
-    uint64_t pos;       // window end of the lookup / declaration point (~0: flush's declaration)
-    int kind;           // 0 enter (EXTRACT), 1 lookup hit (REF), 2 lookup hit (collision)
-    uint64_t hash;
-    uint64_t out_end;   // output bytes up to the end of this event's token (0 for a collision)
-    uint64_t base;      // source_ start after the event (REF / EXTRACT), or at it (collision)
-    int64_t cand;       // collision: the pending candidate (-1 none)
-    const uint8_t *seg; // EXTRACT payload
-};
-
-int64_t get_be64(const uint8_t *p)
-{
-    uint64_t v = 0;
-    for (int i = 0; i < 8; i++) v = (v << 8) | p[i];
-    return (int64_t)v;
-}
-
-// The encoder's lookup calls (xcodec_encoder.cc:111) at window ends [lo, hi) of an item, whose REF
-// events are ev[0..n): every window end once the window is full, except the 2047 after a REF (the
-// hash restarts, :117-127).  Minus its hits (the replay's Store::lookup counted those): its misses.
-uint64_t enc_misses(uint64_t lo, uint64_t hi, const std::vector<EncEvent> &ev, size_t n)
-{
-    uint64_t calls = 0, hits = 0, cur = lo;
-    for (size_t i = 0; i < n; i++) {
-        const EncEvent &e = ev[i];
-        if (e.kind == 0 || e.pos >= hi) continue;
-        hits++;
-        if (e.kind != 1) continue;
-        if (e.pos >= cur) calls += e.pos + 1 - cur;
-        cur = std::max(cur, e.pos + SEG);
-    }
-    if (hi > cur) calls += hi - cur;
-    return calls > hits ? calls - hits : 0;
-}
+using replay::follow;
+using replay::Touch;
 }  // namespace
 
 extern "C" int xc_coss_open(xc_ctx *ctx, const char *dir, const char *uuid, uint64_t size_mb, xc_coss **out)
@@ -638,8 +540,9 @@ extern "C" int xc_coss_open(xc_ctx *ctx, const char *dir, const char *uuid, uint
         if (ctx) {
             Touch t;
             c->st.all_hashes(t.hs);
-            if ((rc = xc_cache_create(ctx, std::max<uint64_t>(4096, t.hs.size() + t.hs.size() / 4), &c->cache)) ||
-                (rc = follow(c, t))) {
+            if (!(rc = xc_cache_create(ctx, std::max<uint64_t>(4096, t.hs.size() + t.hs.size() / 4), &c->cache)))
+                xc__cache_untracked(c->cache);  // (the Store replays every lookup, its window included)
+            if (rc || (rc = follow(c, t))) {
                 c->st.close();
                 if (c->cache) xc_cache_destroy(c->cache);
                 delete c;
@@ -704,213 +607,6 @@ extern "C" int xc_coss_enter(xc_coss *c, uint64_t h, const uint8_t *seg)
     }
 }
 
-namespace {
-// An encoder batch item over the COSS cache: `data` (len bytes) is an encoder's pending source_
-// followed by its new input, window ends below `start` already looked up, candidate `cand` (or -1),
-// encode() only when `noflush`.  `off`: where data lies in the caller's item (restarts move it).
-struct CItem {
-    uint64_t buf;
-    const uint8_t *data;
-    uint64_t len, start;
-    int64_t cand;
-    uint64_t off;
-    bool noflush;
-};
-
-// The batch on the device, its cache events replayed into the Store in the reference's order
-// (items in order), restarting the rest after a change a later event depends on.  Outputs append
-// at out + out_off[buf]; res_base / res_cand: the new source_ start and candidate of each buffer,
-// relative to its first item's data.
-int coss_encode(xc_coss *c, std::vector<CItem> items, uint8_t *out, const uint64_t *out_off, const uint64_t *out_cap,
-                uint64_t *out_len, uint64_t *res_base, int64_t *res_cand)
-{
-    {
-        {
-        while (!items.empty()) {
-            const uint64_t m = items.size();
-            uint64_t count0 = 0;
-            int rc = xc_cache_count(c->cache, &count0);
-            if (rc) return rc;
-            // the device batch
-            std::vector<uint64_t> ioff(m), ilen(m), start(m), ooff(m), ocap(m), olen(m), rbase(m);
-            std::vector<int64_t> cand(m), rcand(m);
-            std::vector<uint32_t> fl(m, 0u), ccnt(m);
-            for (uint64_t k = 0; k < m; k++) fl[k] = items[k].noflush ? 1u : 0u;  // (SF_NOFLUSH)
-            std::vector<uint32_t> coll(m * coss::COLL_CAP * 4);
-            uint64_t isz = 0, osz = 0;
-            for (uint64_t k = 0; k < m; k++) {
-                ioff[k] = isz;
-                ilen[k] = items[k].len;
-                isz += items[k].len;
-                ooff[k] = osz;
-                ocap[k] = 2 * items[k].len + 16;
-                osz += ocap[k];
-                start[k] = items[k].start;
-                cand[k] = items[k].cand;
-            }
-            std::vector<uint8_t> arena(std::max<uint64_t>(isz, 1)), obuf(std::max<uint64_t>(osz, 1));
-            for (uint64_t k = 0; k < m; k++)
-                if (items[k].len) std::memcpy(&arena[ioff[k]], items[k].data, items[k].len);
-            rc = xc__encode_batch_host_coll(c->cache, arena.data(), ioff.data(), ilen.data(), m, obuf.data(), ooff.data(),
-                                            ocap.data(), olen.data(), start.data(), cand.data(), fl.data(), rbase.data(),
-                                            rcand.data(), ccnt.data(), coll.data());
-            if (rc) return rc;
-            // the batch's cache events, item by item in the reference's order
-            std::vector<std::vector<EncEvent>> ev(m);
-            std::vector<const uint8_t *> payloads;
-            for (uint64_t k = 0; k < m; k++) {
-                if (ccnt[k] > coss::COLL_CAP)
-                    return xc__set_error(XC_EINVAL, "too many hash collisions in one buffer to replay on COSS");
-                const uint8_t *o = &obuf[ooff[k]];
-                const uint64_t n = olen[k], len = items[k].len;
-                uint64_t x = 0, t = 0;  // input offset, output offset
-                while (t < n) {
-                    if (o[t] != 0xF1) { t++; x++; continue; }
-                    const uint8_t op = o[t + 1];
-                    if (op == 0x00) { t += 2; x++; continue; }
-                    if (op == 0x01) {  // EXTRACT: declared at cand + 4095, or by flush()
-                        const uint64_t pos = x + 2 * SEG - 1 < len ? x + 2 * SEG - 1 : ~0ull;
-                        ev[k].push_back({pos, 0, 0, t + 2 + SEG, x + SEG, -1, o + t + 2});
-                        payloads.push_back(o + t + 2);
-                        t += 2 + SEG;
-                        x += SEG;
-                    } else {  // REF at the window's end
-                        ev[k].push_back({x + SEG - 1, 1, (uint64_t)get_be64(o + t + 2), t + 10, x + SEG, -1, nullptr});
-                        t += 10;
-                        x += SEG;
-                    }
-                }
-                for (uint32_t i = 0; i < ccnt[k]; i++) {
-                    const uint32_t *r = &coll[(k * coss::COLL_CAP + i) * 4];
-                    const uint64_t q = r[0];
-                    // source_ start at q: after the last token before it
-                    uint64_t base = 0, oe = 0;
-                    for (const EncEvent &e : ev[k])
-                        if (e.kind != 2 && e.pos <= q) base = e.base, oe = e.out_end;
-                    ev[k].push_back({q, 2, ((uint64_t)r[2] << 32) | r[1], oe, base,
-                                     r[3] == 0xFFFFFFFFu ? -1 : (int64_t)r[3], nullptr});
-                }
-                // (a declaration precedes the lookup at the same position; flush's comes last)
-                std::stable_sort(ev[k].begin(), ev[k].end(), [](const EncEvent &a, const EncEvent &b) {
-                    return a.pos != b.pos ? a.pos < b.pos : a.kind < b.kind;
-                });
-            }
-            // EXTRACT hashes (XCodecHash::hash of the payloads) on the device, one call
-            std::vector<uint64_t> ph(payloads.size());
-            if (!payloads.empty()) {
-                std::vector<uint8_t> segs(payloads.size() * (size_t)SEG);
-                for (size_t i = 0; i < payloads.size(); i++) std::memcpy(&segs[i * SEG], payloads[i], SEG);
-                if ((rc = xc_hash_segments_host(c->ctx, segs.data(), payloads.size(), ph.data()))) return rc;
-            }
-            {
-                size_t pi = 0;
-                for (uint64_t k = 0; k < m; k++) {
-                    // (payload order = EXTRACT order in the output; events were sorted stably)
-                    std::vector<EncEvent *> ex;
-                    for (EncEvent &e : ev[k])
-                        if (e.kind == 0) ex.push_back(&e);
-                    std::stable_sort(ex.begin(), ex.end(), [](const EncEvent *a, const EncEvent *b) {
-                        return a->out_end < b->out_end;
-                    });
-                    for (EncEvent *e : ex) e->hash = ph[pi++];
-                }
-            }
-            // replay; stop at the first change a later event depends on
-            if ((rc = unmirrorable(c))) return rc;
-            uint64_t entered = 0;
-            bool redo = false;
-            std::vector<CItem> next;
-            std::vector<Change> held;  // changes nothing later in the pass saw: mirrored at its end
-            for (uint64_t k = 0; k < m && !redo; k++) {
-                const CItem &it = items[k];
-                for (size_t e = 0; e < ev[k].size(); e++) {
-                    const EncEvent &E = ev[k][e];
-                    Touch t;
-                    if (E.kind == 0) {
-                        c->st.enter(E.hash, E.seg, &t);
-                        c->known[E.hash] = fingerprint(E.seg);  // (the device entered it)
-                        entered++;
-                    } else if (!c->st.lookup(E.hash, &t)) {
-                        return xc__set_error(XC_EDEVICE, "COSS replay: a device hit the store does not find");
-                    }
-                    Change ch;
-                    if ((rc = settle(c, t, ch))) return rc;
-                    if (!ch.any()) continue;
-                    // a segment found now that was not: any lookup after this event may differ
-                    bool dep = !ch.added.empty();
-                    if (!dep) {
-                        const Watch w(ch);
-                        for (uint64_t k2 = k; k2 < m && !dep; k2++)
-                            for (size_t e2 = (k2 == k ? e + 1 : 0); e2 < ev[k2].size() && !dep; e2++)
-                                dep = w.has(ev[k2][e2].hash);
-                    }
-                    if (!dep) {
-                        held.push_back(std::move(ch));
-                        continue;
-                    }
-                    // the lookups up to this event (its own, unless a declaration: the lookup at the
-                    // same position follows it), then roll the device cache back to this event,
-                    // follow the changes, run the rest again
-                    if (E.pos != ~0ull)
-                        c->st.count_misses(enc_misses(std::max<uint64_t>(SEG - 1, it.start),
-                                                      E.kind == 0 ? E.pos : E.pos + 1, ev[k], e + 1));
-                    else
-                        c->st.count_misses(enc_misses(std::max<uint64_t>(SEG - 1, it.start), it.len, ev[k], e + 1));
-                    if ((rc = xc__cache_truncate(c->cache, count0 + entered))) return rc;
-                    for (const Change &h : held)
-                        if ((rc = mirror(c, h))) return rc;
-                    held.clear();
-                    if ((rc = mirror(c, ch))) return rc;
-                    // (after flush()'s declaration only the escaped tail follows: no lookups)
-                    const uint64_t keep = E.pos == ~0ull ? olen[k] : E.out_end;
-                    if (out_len[it.buf] + keep > out_cap[it.buf])
-                        return xc__set_error(XC_EINVAL, "output capacity too small");
-                    std::memcpy(out + out_off[it.buf] + out_len[it.buf], &obuf[ooff[k]], keep);
-                    out_len[it.buf] += keep;
-                    if (E.pos != ~0ull) {
-                        CItem r = it;
-                        r.data = it.data + E.base;
-                        r.len = it.len - E.base;
-                        r.off = it.off + E.base;
-                        if (E.kind == 0) {  // after a declaration: its lookup at the same position is next
-                            r.start = 2 * SEG - 1 - SEG;  // window end 2047 of the rest: not looked up yet
-                            r.cand = -1;
-                        } else if (E.kind == 1) {  // after a REF: a fresh stream
-                            r.start = 0;
-                            r.cand = -1;
-                        } else {  // after a collision: same source_, candidate carried
-                            r.start = E.pos + 1 - E.base;
-                            r.cand = E.cand >= 0 ? E.cand - (int64_t)E.base : -1;
-                        }
-                        next.push_back(r);
-                    } else {  // flush()'s declaration ended the item: source_ is empty
-                        res_base[it.buf] = it.off + it.len;
-                        res_cand[it.buf] = -1;
-                    }
-                    for (uint64_t k2 = k + 1; k2 < m; k2++) next.push_back(items[k2]);
-                    redo = true;
-                    break;
-                }
-                if (!redo) {  // item k is final
-                    c->st.count_misses(enc_misses(std::max<uint64_t>(SEG - 1, it.start), it.len, ev[k], ev[k].size()));
-                    if (out_len[it.buf] + olen[k] > out_cap[it.buf])
-                        return xc__set_error(XC_EINVAL, "output capacity too small");
-                    std::memcpy(out + out_off[it.buf] + out_len[it.buf], &obuf[ooff[k]], olen[k]);
-                    out_len[it.buf] += olen[k];
-                    res_base[it.buf] = it.off + rbase[k];
-                    res_cand[it.buf] = rcand[k] >= 0 ? (int64_t)it.off + rcand[k] : -1;
-                }
-            }
-            for (const Change &h : held)
-                if ((rc = mirror(c, h))) return rc;
-            items.swap(next);
-        }
-        }
-    }
-    return XC_OK;
-}
-}  // namespace
-
 // Encoder batch over the COSS cache: buffer i is one encode()+flush() on a fresh encoder, buffers
 // in index order (xc_encode_batch_host's semantics), the COSS state advanced exactly as the
 // reference's would be.
@@ -921,14 +617,14 @@ extern "C" int xc_coss_encode_batch_host(xc_coss *c, const uint8_t *in, const ui
     if (!c || !c->cache || (nbuf && (!in || !in_off || !in_len || !out || !out_off || !out_cap || !out_len)))
         return xc__set_error(XC_EINVAL, "null (or a host-only COSS store)");
     try {
-        std::vector<CItem> items;
+        std::vector<replay::CItem> items;
         for (uint64_t i = 0; i < nbuf; i++) {
             items.push_back({i, in + in_off[i], in_len[i], 0, -1, 0, false});
             out_len[i] = 0;
         }
         std::vector<uint64_t> rb(nbuf);
         std::vector<int64_t> rc(nbuf);
-        return coss_encode(c, std::move(items), out, out_off, out_cap, out_len, rb.data(), rc.data());
+        return replay::encode(c, std::move(items), out, out_off, out_cap, out_len, rb.data(), rc.data());
     } catch (const std::bad_alloc &) {
         return xc__set_error(XC_ENOMEM, "host allocation failed");
     }
@@ -938,6 +634,35 @@ extern "C" int xc_coss_encode_batch_host(xc_coss *c, const uint8_t *in, const ui
 // cache: item i is head[i] (an encoder's source_) then tail[i] (its new input), with stream state
 // start / cand / flags (SF_NOFLUSH: encode() only); `take` receives each item's output and input
 // after rbase / rcand are set.
+template <class C>
+static int replay_gather(C *c, uint64_t nbuf, const uint8_t *const *head, const uint64_t *head_len,
+                         const uint8_t *const *tail, const uint64_t *tail_len, const uint64_t *start,
+                         const int64_t *cand, const uint32_t *flags, uint64_t *rbase, int64_t *rcand,
+                         int (*take)(void *ctx, uint64_t i, const uint8_t *out, uint64_t out_len, const uint8_t *in),
+                         void *ctx)
+{
+    std::vector<std::vector<uint8_t>> data(nbuf);
+    std::vector<uint64_t> ooff(nbuf), ocap(nbuf), olen(nbuf, 0);
+    std::vector<replay::CItem> items;
+    uint64_t osz = 0;
+    for (uint64_t i = 0; i < nbuf; i++) {
+        data[i].resize(head_len[i] + tail_len[i]);
+        if (head_len[i]) std::memcpy(data[i].data(), head[i], head_len[i]);
+        if (tail_len[i]) std::memcpy(data[i].data() + head_len[i], tail[i], tail_len[i]);
+        ooff[i] = osz;
+        ocap[i] = 2 * data[i].size() + 16;
+        osz += ocap[i];
+        if (start[i] > data[i].size() || cand[i] < -1 ||
+            (cand[i] >= 0 && ((uint64_t)cand[i] + SEG > start[i] || (uint64_t)cand[i] + 2 * SEG - 1 < start[i])))
+            return xc__set_error(XC_EINVAL, "invalid stream state");
+        items.push_back({i, data[i].data(), data[i].size(), start[i], cand[i], 0, (flags[i] & 1u) != 0});
+    }
+    std::vector<uint8_t> obuf(std::max<uint64_t>(osz, 1));
+    int rc = replay::encode(c, std::move(items), obuf.data(), ooff.data(), ocap.data(), olen.data(), rbase, rcand);
+    for (uint64_t i = 0; i < nbuf && !rc; i++) rc = take(ctx, i, obuf.data() + ooff[i], olen[i], data[i].data());
+    return rc;
+}
+
 extern "C" int xc__coss_encode_gather(xc_coss *c, uint64_t nbuf, const uint8_t *const *head, const uint64_t *head_len,
                                       const uint8_t *const *tail, const uint64_t *tail_len, const uint64_t *start,
                                       const int64_t *cand, const uint32_t *flags, uint64_t *rbase, int64_t *rcand,
@@ -949,26 +674,7 @@ extern "C" int xc__coss_encode_gather(xc_coss *c, uint64_t nbuf, const uint8_t *
                                      !rcand || !take)))
         return xc__set_error(XC_EINVAL, "null (or a host-only COSS store)");
     try {
-        std::vector<std::vector<uint8_t>> data(nbuf);
-        std::vector<uint64_t> ooff(nbuf), ocap(nbuf), olen(nbuf, 0);
-        std::vector<CItem> items;
-        uint64_t osz = 0;
-        for (uint64_t i = 0; i < nbuf; i++) {
-            data[i].resize(head_len[i] + tail_len[i]);
-            if (head_len[i]) std::memcpy(data[i].data(), head[i], head_len[i]);
-            if (tail_len[i]) std::memcpy(data[i].data() + head_len[i], tail[i], tail_len[i]);
-            ooff[i] = osz;
-            ocap[i] = 2 * data[i].size() + 16;
-            osz += ocap[i];
-            if (start[i] > data[i].size() || cand[i] < -1 ||
-                (cand[i] >= 0 && ((uint64_t)cand[i] + SEG > start[i] || (uint64_t)cand[i] + 2 * SEG - 1 < start[i])))
-                return xc__set_error(XC_EINVAL, "invalid stream state");
-            items.push_back({i, data[i].data(), data[i].size(), start[i], cand[i], 0, (flags[i] & 1u) != 0});
-        }
-        std::vector<uint8_t> obuf(std::max<uint64_t>(osz, 1));
-        int rc = coss_encode(c, std::move(items), obuf.data(), ooff.data(), ocap.data(), olen.data(), rbase, rcand);
-        for (uint64_t i = 0; i < nbuf && !rc; i++) rc = take(ctx, i, obuf.data() + ooff[i], olen[i], data[i].data());
-        return rc;
+        return replay_gather(c, nbuf, head, head_len, tail, tail_len, start, cand, flags, rbase, rcand, take, ctx);
     } catch (const std::bad_alloc &) {
         return xc__set_error(XC_ENOMEM, "host allocation failed");
     }
@@ -986,139 +692,8 @@ extern "C" int xc_coss_decode_batch_host(xc_coss *c, const uint8_t *in, const ui
                                      !consumed || !status || !unknown || !has_unknown)))
         return xc__set_error(XC_EINVAL, "null (or a host-only COSS store)");
     try {
-        struct Item {
-            uint64_t buf, from;  // stream, input offset of the item
-        };
-        std::vector<Item> items;
-        for (uint64_t i = 0; i < nbuf; i++) {
-            items.push_back({i, 0});
-            out_len[i] = 0;
-        }
-        while (!items.empty()) {
-            const uint64_t m = items.size();
-            uint64_t count0 = 0;
-            int rc = xc_cache_count(c->cache, &count0);
-            if (rc) return rc;
-            std::vector<uint64_t> ioff(m), ilen(m), ooff(m), ocap(m), olen(m), cons(m), unk(m);
-            std::vector<int32_t> st(m), hu(m);
-            uint64_t osz = 0;
-            for (uint64_t k = 0; k < m; k++) {
-                const Item &it = items[k];
-                ioff[k] = in_off[it.buf] + it.from;
-                ilen[k] = in_len[it.buf] - it.from;
-                ooff[k] = osz;
-                ocap[k] = out_cap[it.buf] - out_len[it.buf];
-                osz += ocap[k];
-            }
-            std::vector<uint8_t> obuf(std::max<uint64_t>(osz, 1));
-            rc = xc_decode_batch_host(c->cache, in, ioff.data(), ilen.data(), m, obuf.data(), ooff.data(), ocap.data(),
-                                      olen.data(), cons.data(), st.data(), unk.data(), hu.data());
-            if (rc) return rc;
-            // events: every EXTRACT / REF token the decoder executed (xcodec_decoder.cc:85-173)
-            struct DEv {
-                int kind;  // 0 EXTRACT (lookup, enter if absent), 1 REF (lookup)
-                uint64_t hash, in_end, out_end;
-                const uint8_t *seg;
-            };
-            std::vector<std::vector<DEv>> ev(m);
-            std::vector<const uint8_t *> payloads;
-            for (uint64_t k = 0; k < m; k++) {
-                const uint8_t *p = in + ioff[k];
-                const uint64_t n = ilen[k];
-                // the tokens before the stop, and an EXTRACT the decoder stopped on as a collision
-                const uint64_t lim = cons[k] + (st[k] == 0 && cons[k] >= 2 && cons[k] <= n &&
-                                                p[cons[k] - 2] == 0xF1 && p[cons[k] - 1] == 0x01 ? SEG : 0);
-                uint64_t x = 0, y = 0;
-                while (x < lim && x < n) {
-                    if (p[x] != 0xF1) { x++; y++; continue; }
-                    if (x + 1 >= n) break;
-                    const uint8_t op = p[x + 1];
-                    if (op == 0x00) { x += 2; y++; continue; }
-                    if (op == 0x01 && x + 2 + SEG <= n) {
-                        ev[k].push_back({0, 0, x + 2 + SEG, y + SEG, p + x + 2});
-                        payloads.push_back(p + x + 2);
-                        x += 2 + SEG;
-                        y += SEG;
-                    } else if (op == 0x02 && x + 10 <= n) {
-                        if (x + 10 > cons[k]) break;  // (the unknown REF the decoder stopped on: a miss)
-                        ev[k].push_back({1, (uint64_t)get_be64(p + x + 2), x + 10, y + SEG, nullptr});
-                        x += 10;
-                        y += SEG;
-                    } else {
-                        break;
-                    }
-                }
-            }
-            std::vector<uint64_t> ph(payloads.size());
-            if (!payloads.empty()) {
-                std::vector<uint8_t> segs(payloads.size() * (size_t)SEG);
-                for (size_t i = 0; i < payloads.size(); i++) std::memcpy(&segs[i * SEG], payloads[i], SEG);
-                if ((rc = xc_hash_segments_host(c->ctx, segs.data(), payloads.size(), ph.data()))) return rc;
-                size_t pi = 0;
-                for (auto &v : ev)
-                    for (DEv &e : v)
-                        if (e.kind == 0) e.hash = ph[pi++];
-            }
-            if ((rc = unmirrorable(c))) return rc;
-            uint64_t entered = 0;
-            bool redo = false;
-            std::vector<Item> next;
-            std::vector<Change> held;
-            for (uint64_t k = 0; k < m && !redo; k++) {
-                const Item &it = items[k];
-                for (size_t e = 0; e < ev[k].size(); e++) {
-                    const DEv &E = ev[k][e];
-                    Touch t;
-                    const uint8_t *d = c->st.lookup(E.hash, &t);
-                    if (E.kind == 0 && !d) {
-                        c->st.enter(E.hash, E.seg, &t);
-                        c->known[E.hash] = fingerprint(E.seg);  // (the device entered it)
-                        entered++;
-                    } else if (E.kind == 1 && !d) {
-                        return xc__set_error(XC_EDEVICE, "COSS replay: a device hit the store does not find");
-                    }
-                    Change ch;
-                    if ((rc = settle(c, t, ch))) return rc;
-                    if (!ch.any()) continue;
-                    // later tokens, and the unknown REF a later stream stopped on, that saw the change
-                    const Watch w(ch);
-                    bool dep = false;
-                    for (uint64_t k2 = k; k2 < m && !dep; k2++) {
-                        for (size_t e2 = (k2 == k ? e + 1 : 0); e2 < ev[k2].size() && !dep; e2++)
-                            dep = w.has(ev[k2][e2].hash);
-                        if (hu[k2] && w.has(unk[k2])) dep = true;
-                    }
-                    if (!dep) {
-                        held.push_back(std::move(ch));
-                        continue;
-                    }
-                    if ((rc = xc__cache_truncate(c->cache, count0 + entered))) return rc;
-                    for (const Change &h : held)
-                        if ((rc = mirror(c, h))) return rc;
-                    held.clear();
-                    if ((rc = mirror(c, ch))) return rc;
-                    std::memcpy(out + out_off[it.buf] + out_len[it.buf], &obuf[ooff[k]], E.out_end);
-                    out_len[it.buf] += E.out_end;
-                    next.push_back({it.buf, it.from + E.in_end});
-                    for (uint64_t k2 = k + 1; k2 < m; k2++) next.push_back(items[k2]);
-                    redo = true;
-                    break;
-                }
-                if (!redo) {
-                    if (hu[k]) c->st.count_misses(1);  // (the unknown REF's lookup, :150)
-                    std::memcpy(out + out_off[it.buf] + out_len[it.buf], &obuf[ooff[k]], olen[k]);
-                    out_len[it.buf] += olen[k];
-                    consumed[it.buf] = it.from + cons[k];
-                    status[it.buf] = st[k];
-                    unknown[it.buf] = unk[k];
-                    has_unknown[it.buf] = hu[k];
-                }
-            }
-            for (const Change &h : held)
-                if ((rc = mirror(c, h))) return rc;
-            items.swap(next);
-        }
-        return XC_OK;
+        return replay::decode(c, in, in_off, in_len, nbuf, out, out_off, out_cap, out_len, consumed, status, unknown,
+                              has_unknown);
     } catch (const std::bad_alloc &) {
         return xc__set_error(XC_ENOMEM, "host allocation failed");
     }

@@ -808,6 +808,8 @@ struct xc_dplan {
     hipEvent_t ev_ctl = nullptr;
     int completion = XC_COMPLETE_RUN;  // xc_dplan_set_completion
     uint32_t cache_gen = 0;       // the cache arrays D holds (they move when the cache grows)
+    std::vector<uint32_t> tok_base;  // host copy [ns + 1]
+    bool internal = false;        // run by xc_decode_batch_host (its replay takes a XC__SLOW run)
     template <class T>
     int alloc(T **p, size_t n)
     {
@@ -824,10 +826,22 @@ extern "C" int xc_dplan_set_completion(xc_dplan *p, int mode)
     return XC_OK;
 }
 
+extern "C" void xc__cache_plan_gone_dec(xc_cache *c, void *dplan);
+extern "C" int xc__cache_run_start(xc_cache *c, int *slow);
+extern "C" void xc__cache_run_done_dec(xc_cache *c, void *dplan);
+struct xc_memmodel;
+extern "C" xc_memmodel *xc__cache_mem(xc_cache *c);
+extern "C" int xc__mem_decode_batch(xc_memmodel *m, const uint8_t *in, const uint64_t *in_off,
+                                    const uint64_t *in_len, uint64_t nbuf, uint8_t *out, const uint64_t *out_off,
+                                    const uint64_t *out_cap, uint64_t *out_len, uint64_t *consumed, int32_t *status,
+                                    uint64_t *unknown, int32_t *has_unknown);
+constexpr int XC__SLOW = -1000;  // (xc_runtime.hip)
+
 extern "C" int xc_dplan_destroy(xc_dplan *p)
 {
     if (!p) return XC_OK;
     hipSetDevice(p->dev);
+    if (p->cache) xc__cache_plan_gone_dec(p->cache, p);  // (its tokens are the window's record)
     hipStreamSynchronize(p->s);
     for (void *x : p->owned) xc__pfree(x);
     if (p->h_ctl) xc__pfree(p->h_ctl);
@@ -870,6 +884,8 @@ extern "C" int xc_decode_plan_create(xc_cache *c, const uint64_t *in_len, const 
         nprov += in_len[j] / (XC_SEG + 2) + 1;
     }
     if (ntok > 0xFFFFFFF0ull) { xc_dplan_destroy(p); return xc__set_error(XC_EINVAL, "batch too large"); }
+    p->tok_base.assign(tbase.begin(), tbase.begin() + ns);
+    p->tok_base.push_back((uint32_t)ntok);
     p->in_bytes = itot + 4096;  // the tokenizer's 256-byte windows read past a stream's end
     p->out_bytes = otot + 256;
     p->ntok = ntok;
@@ -937,6 +953,16 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
     if (!d_in || !d_out || !d_out_len || !d_consumed || !d_status || !d_unknown || !d_has_unknown)
         return xc__set_error(XC_EINVAL, "null");
     DHIP(hipSetDevice(p->dev));
+    {   // the recent window (xc_memcache.cpp): the cache's pending run first; with a hash entered
+        // twice that may answer other bytes than the device holds, the host path replays the run
+        int slow = 0;
+        int r = xc__cache_run_start(p->cache, &slow);
+        if (r) return r;
+        if (slow && p->internal) return xc__set_error(XC__SLOW, "a hash entered twice is in the recent window");
+        if (slow)
+            return xc__set_error(XC_EINVAL, "device-resident decode on a cache with a hash entered twice by a "
+                                            "stateful stream: run it through xc_decode_batch_host");
+    }
     DecDev D = p->D;
     D.in = d_in;
     D.out = d_out;
@@ -1061,6 +1087,43 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
     // (k_dalloc advanced the count by exactly the entered segments: a later restore or reserve
     // needs no device read)
     if (count0 >= 0) xc__cache_set_host_count(p->cache, count0 + ctl[DCTL_NENTER]);
+    xc__cache_run_done_dec(p->cache, p);
+    return XC_OK;
+}
+
+// A finished run's lookup hits in the reference's order (xcodec_decoder.cc:120-166): per stream,
+// its executed EXTRACT and REF tokens that found the hash (in the cache or entered by an earlier
+// EXTRACT of the batch), and an EXTRACT it stopped on as a collision.
+extern "C" int xc__dplan_hits(void *dp, uint64_t **hits, uint64_t *n, int *complete)
+{
+    xc_dplan *p = (xc_dplan *)dp;
+    *complete = 1;
+    *n = 0;
+    *hits = nullptr;
+    const uint32_t ns = p->ns;
+    if (!ns) return XC_OK;
+    DHIP(hipSetDevice(p->dev));
+    std::vector<uint32_t> op(p->ntok), st(p->ntok), stop(ns);
+    std::vector<uint64_t> th(p->ntok);
+    DHIP(hipMemcpyAsync(op.data(), p->D.t_op, p->ntok * 4, hipMemcpyDeviceToHost, p->s));
+    DHIP(hipMemcpyAsync(st.data(), p->D.t_stat, p->ntok * 4, hipMemcpyDeviceToHost, p->s));
+    DHIP(hipMemcpyAsync(th.data(), p->D.t_h, p->ntok * 8, hipMemcpyDeviceToHost, p->s));
+    DHIP(hipMemcpyAsync(stop.data(), p->D.s_stop, ns * 4, hipMemcpyDeviceToHost, p->s));
+    DHIP(hipStreamSynchronize(p->s));
+    std::vector<uint64_t> v;
+    for (uint32_t j = 0; j < ns; j++) {
+        const uint32_t tb = p->tok_base[j], ex = std::min(stop[j], p->tok_base[j + 1] - tb);
+        for (uint32_t t = 0; t < ex; t++) {
+            const uint32_t o = op[tb + t], r = st[tb + t];
+            const bool executed = t + 1u < ex;
+            if ((o == T_EXTRACT || o == T_REF) && executed && (r == R_OKCACHE || r == R_OKPROV)) v.push_back(th[tb + t]);
+            else if (o == T_EXTRACT && !executed && r == R_COLL) v.push_back(th[tb + t]);
+        }
+    }
+    *hits = (uint64_t *)malloc(std::max<size_t>(v.size(), 1) * 8);
+    if (!*hits) return xc__set_error(XC_ENOMEM, "host allocation failed");
+    std::copy(v.begin(), v.end(), *hits);
+    *n = v.size();
     return XC_OK;
 }
 
@@ -1078,6 +1141,7 @@ extern "C" int xc_decode_batch_host(xc_cache *c, const uint8_t *in, const uint64
     if (rc) return rc;
     const uint32_t ns = p->ns;
     const hipStream_t s = p->s;
+    p->internal = true;
     uint8_t *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
     uint64_t *d_u64 = nullptr;  // out_len | consumed | unknown
     int32_t *d_i32 = nullptr;   // status | has_unknown
@@ -1119,5 +1183,19 @@ extern "C" int xc_decode_batch_host(xc_cache *c, const uint8_t *in, const uint64
     xc__pfree(d_u64);
     xc__pfree(d_i32);
     xc_dplan_destroy(p);
+    if (rc == XC__SLOW)  // a hash entered twice: the recent window's replay (xc_memcache.cpp)
+        rc = xc__mem_decode_batch(xc__cache_mem(c), in, in_off, in_len, nbuf, out, out_off, out_cap, out_len, consumed,
+                                  status, unknown, has_unknown);
     return rc;
+}
+
+// The replay engines' device batch (the cache's hooks stand aside while they run).
+extern "C" int xc__decode_batch_host_raw(xc_cache *c, const uint8_t *in, const uint64_t *in_off,
+                                         const uint64_t *in_len, uint64_t nbuf, uint8_t *out,
+                                         const uint64_t *out_off, const uint64_t *out_cap, uint64_t *out_len,
+                                         uint64_t *consumed, int32_t *status, uint64_t *unknown,
+                                         int32_t *has_unknown)
+{
+    return xc_decode_batch_host(c, in, in_off, in_len, nbuf, out, out_off, out_cap, out_len, consumed, status,
+                                unknown, has_unknown);
 }

@@ -1220,7 +1220,10 @@ __device__ __forceinline__ uint32_t write_escaped(uint8_t *dst, const uint8_t *p
 }
 
 
-constexpr int EMIT_PAY = 2;  // payloads a wave has in flight
+#ifndef XC_EMIT_PAY
+#define XC_EMIT_PAY 2
+#endif
+constexpr int EMIT_PAY = XC_EMIT_PAY;  // payloads a wave has in flight
 
 // k_alloc's gate (a sub-batch that needs the host stops the device pipeline here).
 __device__ __forceinline__ bool gate_stop(const EmitArgs &a)
@@ -1355,8 +1358,15 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
                 const uint32_t idx = slot0 + ord[t];
                 if (idx < P.seg_cap) {
                     uint32_t s1, s2;
-                    set_insert(P.cache, P.tok_h[tb + t], idx, false, &s1, &s2);
-                    P.undo[idx] = make_uint2(s1, s2);
+                    if (set_insert(P.cache, P.tok_h[tb + t], idx, false, &s1, &s2) || s2 == XC_REVIVED) {
+                        P.undo[idx] = make_uint2(s1, s2);
+                    } else {
+                        // the hash is in the cache: a stateful stream's carried candidate declared
+                        // after another connection entered the hash (xc_memcache.cpp).  The table
+                        // keeps the first entry (nothing to undo); the host replays the run.
+                        P.undo[idx] = make_uint2(NONE, NONE);
+                        atomicAdd(&P.ctl[CTL_DUPS], 1u);
+                    }
                 }
             }
         }
@@ -1776,6 +1786,31 @@ __global__ void k_enter_bulk(PlanDev P, const uint64_t *h, const uint8_t *segs, 
         uint32_t s1, s2;
         set_insert(P.cache, h[i], idx, false, &s1, &s2);
         P.undo[idx] = make_uint2(s1, s2);
+    }
+}
+
+// The table values of n hashes (~0: absent or evicted), no side effects.
+__global__ void k_find(DevSet cache, const uint64_t *h, uint64_t *val, uint32_t n)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t v;
+    val[i] = set_find(cache, h[i], &v) ? v : ~0ull;
+}
+
+// The table value of a present key (evicted or not), set.
+__global__ void k_setval(DevSet cache, uint64_t h, uint64_t val)
+{
+    if (threadIdx.x != 0) return;
+    uint32_t j = key_slot(h, cache.mask);
+    for (;;) {
+        const uint64_t x = cache.keys[j];
+        if (x == h) {
+            cache.vals[j] = val;
+            return;
+        }
+        if (x == XC_EMPTY64) return;
+        j = (j + 1u) & cache.mask;
     }
 }
 

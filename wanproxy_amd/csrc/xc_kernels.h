@@ -45,6 +45,7 @@ enum : uint32_t {
     CTL_SHADOW = 9,    // a walk did not emit a predicted REF whose shadow the scan skipped
     CTL_SCAN_NEXT = 10,  // k_scan work counter (chunks handed out); k_resolve resets it
     CTL_COUNT = 11,      // the cache's segment count after the last k_alloc (for the host)
+    CTL_DUPS = 12,       // k_emit entered hashes the cache held (a duplicate enter: the host replays)
     CTL_WORDS = 16
 };
 constexpr uint32_t ERR_CAPACITY = 1, ERR_TOKENS = 2, ERR_DECLS = 4;  // (ERR_PACK_CAP = 8 below)
@@ -254,6 +255,8 @@ __global__ void k_rehash_owner(uint2 *undo, uint32_t n, const uint32_t *lo_owner
 __global__ void k_enter_one(PlanDev P, uint64_t h, const uint8_t *seg);
 __global__ void k_enter_bulk(PlanDev P, const uint64_t *h, const uint8_t *segs, uint32_t n, uint32_t first);
 __global__ void k_kill(DevSet cache, const uint64_t *h, uint32_t n);
+__global__ void k_find(DevSet cache, const uint64_t *h, uint64_t *val, uint32_t n);
+__global__ void k_setval(DevSet cache, uint64_t h, uint64_t val);
 __global__ void k_lookup_one(PlanDev P, uint64_t h, uint8_t *out, uint32_t *found);
 __global__ void k_selftest(uint32_t *err);
 

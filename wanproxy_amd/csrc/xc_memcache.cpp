@@ -1,0 +1,466 @@
+// xc_memcache.cpp — XCodecMemoryCache's recent window and duplicate enters, on the host.
+//
+// Reference (xcodec/xcodec_cache.h:89-211): lookup() first scans a 64-entry window of the (hash,
+// data pointer) pairs its last map hits remembered (find_recent, :137-147, the first entry with the
+// hash), then the map, remembering a map hit in the next window slot (:130-135, cursor round
+// robin).  enter() asserts that the hash is new (:184); a release build overwrites the map value
+// and leaves the old data alive, so after a second enter of a hash with other bytes the window
+// keeps returning the old bytes until 64 later remembers push its entry out, and the map returns
+// the new ones.  The only way an encoder gets there is a stateful connection whose candidate was
+// looked up (a miss) in one call and is declared in a later one after another connection entered a
+// different segment with the same hash (xcodec_encoder.cc:77-82,203-215; the hash is weak enough to
+// build such pairs).
+//
+// Without such a duplicate the window never changes what a lookup returns (it caches map
+// pointers), so the device cache has no window: a run's lookup hits (the REF tokens and the
+// collisions its walk records; the decoder's executed tokens) are replayed here afterwards, lazily
+// (runtime: the cache's pending run, consumed before the next operation on the cache that needs the
+// order, dropped by a restore).  A duplicate enter (k_emit finds the key, CTL_DUPS) or a run while
+// a duplicated hash may still answer with other bytes than the device holds goes through the replay
+// engine of xc_replay.h with the Store below: the device cache then mirrors, for every hash, the
+// bytes the reference's lookup returns, following each change the window makes.
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "xc_replay.h"
+
+extern "C" int xc__cache_find(xc_cache *c, const uint64_t *h, uint64_t n, uint64_t *val);  // ~0: absent
+extern "C" int xc__cache_read(xc_cache *c, uint64_t h, uint8_t *out, int *found);            // no side effects
+extern "C" int xc__cache_set_value(xc_cache *c, uint64_t h, uint64_t val);
+extern "C" void xc__cache_engine(xc_cache *c, int on);
+
+namespace {
+using replay::SEG;
+using replay::Touch;
+constexpr int WINDOW = 64;  // XCODEC_WINDOW_COUNT, xcodec_cache.h:48
+
+// The memory cache as the reference's lookups see it.
+class MemStore {
+public:
+    xc_cache *cache = nullptr;
+    // the recent window: hash and the version of the bytes it remembered (-1: never used, no data)
+    struct Win {
+        uint64_t h;
+        int32_t v;
+    } win[WINDOW];
+    uint32_t cursor = 0;
+    std::unordered_map<uint64_t, uint32_t> widx;  // non-zero hash -> its window slot (one at most)
+    // hashes entered again with other bytes: every version (ver[0] the first), cur = the map's
+    struct Dup {
+        std::vector<std::vector<uint8_t>> ver;
+        uint32_t cur = 0;
+    };
+    std::unordered_map<uint64_t, Dup> dups;
+    // per replay pass: in the cache before the pass (device), first enters of the pass
+    std::unordered_set<uint64_t> present;
+    std::unordered_map<uint64_t, const uint8_t *> inpass;
+    bool last_dup = false;  // the last enter() found the hash present
+    int err = XC_OK;
+
+    MemStore()
+    {
+        for (auto &w : win) w = {0, -1};
+    }
+
+    // find_recent: the first slot with the hash (hash 0 matches the unused slots, whose data is
+    // null: not found)
+    int find_recent(uint64_t h) const
+    {
+        if (h == 0) {
+            for (int i = 0; i < WINDOW; i++)
+                if (win[i].h == 0) return win[i].v >= 0 ? i : -1;
+            return -1;
+        }
+        auto it = widx.find(h);
+        return it == widx.end() ? -1 : (int)it->second;
+    }
+
+    const uint8_t *bytes(uint64_t h, int32_t v) const
+    {
+        static const uint8_t any[SEG] = {};
+        auto it = dups.find(h);
+        return it == dups.end() ? any : it->second.ver[(size_t)v].data();
+    }
+    int32_t curver(uint64_t h) const
+    {
+        auto it = dups.find(h);
+        return it == dups.end() ? 0 : (int32_t)it->second.cur;
+    }
+    bool is_present(uint64_t h) const { return dups.count(h) || present.count(h) || inpass.count(h); }
+
+    // remember (xcodec_cache.h:130-135); an evicted entry of a duplicated hash may change what a
+    // lookup of that hash returns
+    void remember(uint64_t h, int32_t v, Touch *t)
+    {
+        Win &w = win[cursor];
+        if (w.v >= 0 && w.h) {
+            auto it = widx.find(w.h);
+            if (it != widx.end() && it->second == cursor) widx.erase(it);
+            if (t && dups.count(w.h)) t->hs.push_back(w.h);
+        }
+        w = {h, v};
+        if (h) widx[h] = cursor;
+        cursor = (cursor + 1) & (WINDOW - 1);
+    }
+
+    // XCodecMemoryCache::lookup (:190-210)
+    const uint8_t *lookup(uint64_t h, Touch *t)
+    {
+        const int s = find_recent(h);
+        if (s >= 0) return bytes(h, win[s].v);
+        if (!is_present(h)) return nullptr;
+        const int32_t v = curver(h);
+        remember(h, v, t);
+        return bytes(h, v);
+    }
+
+    // a lookup the device found (a run's hit): the window only
+    void hit(uint64_t h)
+    {
+        if (find_recent(h) < 0) remember(h, curver(h), nullptr);
+    }
+
+    // XCodecMemoryCache::enter (:182-188), release semantics
+    void enter(uint64_t h, const uint8_t *seg, Touch *t)
+    {
+        last_dup = is_present(h);
+        if (!last_dup) {
+            inpass.emplace(h, seg);
+            return;
+        }
+        auto d = dups.find(h);
+        const uint8_t *cur = nullptr;
+        std::vector<uint8_t> dev;
+        if (d != dups.end()) {
+            cur = d->second.ver[d->second.cur].data();
+        } else if (inpass.count(h)) {
+            cur = inpass[h];
+        } else {
+            dev.resize(SEG);
+            int found = 0;
+            if ((err = xc__cache_read(cache, h, dev.data(), &found)) == XC_OK && !found)
+                err = xc__set_error(XC_EDEVICE, "memory cache: a present hash is not on the device");
+            if (err) return;
+            cur = dev.data();
+        }
+        if (std::memcmp(cur, seg, SEG) == 0) return;  // the same bytes again: nothing a lookup sees
+        Dup &x = dups[h];
+        if (x.ver.empty()) x.ver.emplace_back(cur, cur + SEG);
+        x.ver.emplace_back(seg, seg + SEG);
+        x.cur = (uint32_t)x.ver.size() - 1;
+        if (t) t->hs.push_back(h);
+    }
+
+    int peek(uint64_t h, const uint8_t **p, replay::Loc *) const
+    {
+        const int s = find_recent(h);
+        if (s >= 0) {
+            *p = bytes(h, win[s].v);
+            return replay::FOUND;
+        }
+        if (!is_present(h)) return replay::ABSENT;
+        *p = bytes(h, curver(h));
+        return replay::FOUND;
+    }
+    bool read_segment(const replay::Loc &, uint8_t *) const { return false; }
+    void owners(uint64_t, std::vector<uint64_t> &) const {}
+    void window_in_slot(int, std::vector<uint64_t> &) const {}
+    void count_misses(uint64_t) {}
+};
+}  // namespace
+
+// A memory cache's model (xc_replay.h's context).
+struct xc_memmodel {
+    xc_cache *cache = nullptr;
+    xc_ctx *ctx = nullptr;
+    MemStore st;
+    std::unordered_map<uint64_t, uint64_t> known;  // the device's bytes (fingerprint) of duplicated hashes
+    std::unordered_set<uint64_t> load_miss;         // (none: a memory-cache miss has no side effect)
+    bool valid = true;  // false: some run's lookups were not all recorded (the window is unknown)
+    uint64_t extra = 0;  // device segments that are no map entry (a duplicate enter's, a mirror's)
+    // mirrors (hash, the device value before): a restore puts them back
+    std::vector<std::pair<uint64_t, uint64_t>> mirror_log;
+
+    void entered(uint64_t h, const uint8_t *)
+    {
+        if (!st.last_dup) return;
+        extra++;  // (the device took a slot for the declaration; the map has the hash once)
+        if (st.dups.count(h) && !known.count(h)) {
+            // what the device answers for the hash now (its first insert of the batch won)
+            uint8_t b[SEG];
+            int found = 0;
+            if (!st.err && (st.err = xc__cache_read(cache, h, b, &found)) == XC_OK && found)
+                known[h] = replay::fingerprint(b);
+        }
+    }
+    void mirrored(const replay::Change &ch) { extra += ch.added.size(); }
+    int unmirrorable()
+    {
+        if (st.err) return st.err;
+        if (!valid && !st.dups.empty())
+            return xc__set_error(XC_EINVAL, "memory cache: the recent window's state was lost (more than 16 hash "
+                                            "collisions in one buffer) and a hash was entered twice");
+        return XC_OK;
+    }
+    // the pass's device batch has run: the entries below count0 were there before it (the
+    // batch's own are seen through inpass, in the reference's order)
+    int begin_pass(const std::vector<uint64_t> &hs, uint64_t count0)
+    {
+        st.inpass.clear();
+        st.present.clear();
+        std::vector<uint64_t> q;
+        for (uint64_t h : hs)
+            if (!st.dups.count(h)) q.push_back(h);
+        std::sort(q.begin(), q.end());
+        q.erase(std::unique(q.begin(), q.end()), q.end());
+        if (q.empty()) return XC_OK;
+        std::vector<uint64_t> v(q.size());
+        int rc = xc__cache_find(cache, q.data(), q.size(), v.data());
+        if (rc) return rc;
+        for (size_t i = 0; i < q.size(); i++)
+            if (v[i] != ~0ull && v[i] < count0) st.present.insert(q[i]);
+        return XC_OK;
+    }
+    int end_pass()
+    {
+        if (st.err) return st.err;
+        // a duplicated hash whose every window entry and the device answer with the map's bytes
+        // is an ordinary entry again
+        for (auto it = st.dups.begin(); it != st.dups.end();) {
+            const uint64_t h = it->first;
+            const int s = st.find_recent(h);
+            const int32_t cur = (int32_t)it->second.cur;
+            const auto k = known.find(h);
+            if ((s < 0 || st.win[s].v == cur) && k != known.end() &&
+                k->second == replay::fingerprint(it->second.ver[(size_t)cur].data())) {
+                if (s >= 0) st.win[s].v = 0;
+                known.erase(k);
+                it = st.dups.erase(it);
+            } else {
+                ++it;
+            }
+        }
+        st.inpass.clear();
+        st.present.clear();
+        return XC_OK;
+    }
+};
+
+namespace {
+// The engine's device passes: the runtime's hooks stand aside while it runs.
+struct Engine {
+    xc_memmodel *m;
+    explicit Engine(xc_memmodel *mm) : m(mm) { xc__cache_engine(mm->cache, 1); }
+    ~Engine() { xc__cache_engine(m->cache, 0); }
+};
+}  // namespace
+
+extern "C" xc_memmodel *xc__mem_new(xc_cache *c, xc_ctx *ctx)
+{
+    xc_memmodel *m = new (std::nothrow) xc_memmodel();
+    if (!m) return nullptr;
+    m->cache = c;
+    m->ctx = ctx;
+    m->st.cache = c;
+    return m;
+}
+
+extern "C" void xc__mem_free(xc_memmodel *m) { delete m; }
+
+extern "C" xc_memmodel *xc__mem_clone(const xc_memmodel *m)
+{
+    if (!m) return nullptr;
+    try {
+        return new xc_memmodel(*m);
+    } catch (...) {
+        return nullptr;
+    }
+}
+
+// A restore: the model as it was at the snapshot; the device values the mirrors since replaced
+// are put back (the undo log revived or evicted their keys).
+extern "C" int xc__mem_restore(xc_memmodel *m, const xc_memmodel *snap)
+{
+    if (!m || !snap) return XC_OK;
+    int rc = XC_OK;
+    for (size_t i = m->mirror_log.size(); i-- > snap->mirror_log.size() && !rc;)
+        rc = xc__cache_set_value(m->cache, m->mirror_log[i].first, m->mirror_log[i].second);
+    try {
+        *m = *snap;
+    } catch (...) {
+        return xc__set_error(XC_ENOMEM, "host allocation failed");
+    }
+    return rc;
+}
+
+// A run's lookup hits in the reference's order (complete = 0: some were not recorded).
+extern "C" void xc__mem_hits(xc_memmodel *m, const uint64_t *h, uint64_t n, int complete)
+{
+    if (!m) return;
+    for (uint64_t i = 0; i < n; i++) m->st.hit(h[i]);
+    if (!complete) m->valid = false;
+}
+
+// Does a run need the replay engine (a duplicated hash that may answer other bytes)?
+extern "C" int xc__mem_live(const xc_memmodel *m) { return m && !m->st.dups.empty() ? 1 : 0; }
+
+// Device segments that are no entry of the reference's map.
+extern "C" uint64_t xc__mem_extra(const xc_memmodel *m) { return m ? m->extra : 0; }
+
+namespace {
+struct Ctx {
+    xc_memmodel *m;
+    xc_cache *cache;
+    xc_ctx *ctx;
+    MemStore &st;
+    std::unordered_map<uint64_t, uint64_t> &known;
+    std::unordered_set<uint64_t> &load_miss;
+    explicit Ctx(xc_memmodel *mm)
+        : m(mm), cache(mm->cache), ctx(mm->ctx), st(mm->st), known(mm->known), load_miss(mm->load_miss) {}
+    void entered(uint64_t h, const uint8_t *seg) { m->entered(h, seg); }
+    // what a mirror replaces (a restore puts it back)
+    int before_mirror(const replay::Change &ch)
+    {
+        if (ch.added.empty()) return XC_OK;
+        std::vector<uint64_t> v(ch.added.size());
+        int rc = xc__cache_find(cache, ch.added.data(), ch.added.size(), v.data());
+        for (size_t i = 0; i < ch.added.size() && !rc; i++) m->mirror_log.push_back({ch.added[i], v[i]});
+        return rc;
+    }
+    void mirrored(const replay::Change &ch) { m->mirrored(ch); }
+    int unmirrorable() { return m->unmirrorable(); }
+    int begin_pass(const std::vector<uint64_t> &hs, uint64_t count0) { return m->begin_pass(hs, count0); }
+    int end_pass() { return m->end_pass(); }
+};
+
+int bad_alloc() { return xc__set_error(XC_ENOMEM, "host allocation failed"); }
+}  // namespace
+
+// Host batch of fresh encoders (xc_encode_batch_host's semantics) through the engine.
+extern "C" int xc__mem_encode_batch(xc_memmodel *m, const uint8_t *in, const uint64_t *in_off, const uint64_t *in_len,
+                                    uint64_t nbuf, uint8_t *out, const uint64_t *out_off, const uint64_t *out_cap,
+                                    uint64_t *out_len)
+{
+    try {
+        Engine e(m);
+        Ctx c(m);
+        std::vector<replay::CItem> items;
+        for (uint64_t i = 0; i < nbuf; i++) {
+            items.push_back({i, in + in_off[i], in_len[i], 0, -1, 0, false});
+            out_len[i] = 0;
+        }
+        std::vector<uint64_t> rb(nbuf);
+        std::vector<int64_t> rc(nbuf);
+        return replay::encode(&c, std::move(items), out, out_off, out_cap, out_len, rb.data(), rc.data());
+    } catch (const std::bad_alloc &) {
+        return bad_alloc();
+    }
+}
+
+// Stream items (xc__encode_gather's contract, xc_stream.cpp) through the engine.
+extern "C" int xc__mem_encode_gather(xc_memmodel *m, uint64_t nbuf, const uint8_t *const *head,
+                                     const uint64_t *head_len, const uint8_t *const *tail, const uint64_t *tail_len,
+                                     const uint64_t *start, const int64_t *cand, const uint32_t *flags,
+                                     uint64_t *rbase, int64_t *rcand,
+                                     int (*take)(void *ctx, uint64_t i, const uint8_t *out, uint64_t out_len,
+                                                 const uint8_t *in),
+                                     void *ctx)
+{
+    try {
+        Engine e(m);
+        Ctx c(m);
+        std::vector<std::vector<uint8_t>> data(nbuf);
+        std::vector<uint64_t> ooff(nbuf), ocap(nbuf), olen(nbuf, 0);
+        std::vector<replay::CItem> items;
+        uint64_t osz = 0;
+        for (uint64_t i = 0; i < nbuf; i++) {
+            data[i].resize(head_len[i] + tail_len[i]);
+            if (head_len[i]) std::memcpy(data[i].data(), head[i], head_len[i]);
+            if (tail_len[i]) std::memcpy(data[i].data() + head_len[i], tail[i], tail_len[i]);
+            ooff[i] = osz;
+            ocap[i] = 2 * data[i].size() + 16;
+            osz += ocap[i];
+            items.push_back({i, data[i].data(), data[i].size(), start[i], cand[i], 0, (flags[i] & 1u) != 0});
+        }
+        std::vector<uint8_t> obuf(std::max<uint64_t>(osz, 1));
+        int rc = replay::encode(&c, std::move(items), obuf.data(), ooff.data(), ocap.data(), olen.data(), rbase, rcand);
+        for (uint64_t i = 0; i < nbuf && !rc; i++) rc = take(ctx, i, obuf.data() + ooff[i], olen[i], data[i].data());
+        return rc;
+    } catch (const std::bad_alloc &) {
+        return bad_alloc();
+    }
+}
+
+// Decoder batch (xc_decode_batch_host's semantics) through the engine.
+extern "C" int xc__mem_decode_batch(xc_memmodel *m, const uint8_t *in, const uint64_t *in_off, const uint64_t *in_len,
+                                    uint64_t nbuf, uint8_t *out, const uint64_t *out_off, const uint64_t *out_cap,
+                                    uint64_t *out_len, uint64_t *consumed, int32_t *status, uint64_t *unknown,
+                                    int32_t *has_unknown)
+{
+    try {
+        Engine e(m);
+        Ctx c(m);
+        return replay::decode(&c, in, in_off, in_len, nbuf, out, out_off, out_cap, out_len, consumed, status, unknown,
+                              has_unknown);
+    } catch (const std::bad_alloc &) {
+        return bad_alloc();
+    }
+}
+
+// XCodecMemoryCache::lookup (the <ASK> handler's, xcodec_filter.cc:296): found on the device, then
+// the window decides the bytes and remembers a map hit.
+extern "C" int xc__mem_lookup(xc_memmodel *m, uint64_t h, uint8_t *out, int *found)
+{
+    try {
+        Ctx c(m);
+        uint64_t v = 0;
+        int rc = m->st.dups.count(h) ? XC_OK : xc__cache_find(m->cache, &h, 1, &v);
+        if (rc) return rc;
+        if (!m->st.dups.count(h) && v != ~0ull) m->st.present.insert(h);
+        replay::Touch t;
+        const uint8_t *d = m->st.lookup(h, &t);
+        m->st.present.clear();
+        *found = d ? 1 : 0;
+        if (d && m->st.dups.count(h)) {
+            std::memcpy(out, d, SEG);
+        } else if (d) {
+            int f = 0;
+            if ((rc = xc__cache_read(m->cache, h, out, &f))) return rc;
+        }
+        if ((rc = replay::follow(&c, t))) return rc;
+        return m->end_pass();
+    } catch (const std::bad_alloc &) {
+        return bad_alloc();
+    }
+}
+
+// XCodecMemoryCache::enter of a hash the cache holds (release semantics: the map takes the bytes).
+// *dup = 0: the hash is absent, the caller enters it on the device.
+extern "C" int xc__mem_enter(xc_memmodel *m, uint64_t h, const uint8_t *seg, int *dup)
+{
+    try {
+        Ctx c(m);
+        uint64_t v = 0;
+        int rc = m->st.dups.count(h) ? XC_OK : xc__cache_find(m->cache, &h, 1, &v);
+        if (rc) return rc;
+        *dup = m->st.dups.count(h) || v != ~0ull;
+        if (!*dup) return XC_OK;
+        if (!m->st.dups.count(h)) m->st.present.insert(h);
+        replay::Touch t;
+        m->st.enter(h, seg, &t);
+        m->st.present.clear();
+        if (m->st.err) return m->st.err;
+        if (m->st.dups.count(h) && !m->known.count(h)) {  // the device holds the first bytes
+            uint8_t b[SEG];
+            int f = 0;
+            if ((rc = xc__cache_read(m->cache, h, b, &f))) return rc;
+            m->known[h] = replay::fingerprint(b);
+        }
+        if ((rc = replay::follow(&c, t))) return rc;
+        return m->end_pass();
+    } catch (const std::bad_alloc &) {
+        return bad_alloc();
+    }
+}

@@ -267,6 +267,33 @@ struct HostSet {
 };
 
 // ------------------------------------------------------------------ cache ----------
+// The memory cache's recent window and duplicate enters (xc_memcache.cpp).
+struct xc_memmodel;
+extern "C" xc_memmodel *xc__mem_new(xc_cache *c, xc_ctx *ctx);
+extern "C" void xc__mem_free(xc_memmodel *m);
+extern "C" xc_memmodel *xc__mem_clone(const xc_memmodel *m);
+extern "C" int xc__mem_restore(xc_memmodel *m, const xc_memmodel *snap);
+extern "C" void xc__mem_hits(xc_memmodel *m, const uint64_t *h, uint64_t n, int complete);
+extern "C" int xc__mem_live(const xc_memmodel *m);
+extern "C" uint64_t xc__mem_extra(const xc_memmodel *m);
+extern "C" int xc__mem_encode_batch(xc_memmodel *m, const uint8_t *in, const uint64_t *in_off, const uint64_t *in_len,
+                                    uint64_t nbuf, uint8_t *out, const uint64_t *out_off, const uint64_t *out_cap,
+                                    uint64_t *out_len);
+extern "C" int xc__mem_encode_gather(xc_memmodel *m, uint64_t nbuf, const uint8_t *const *head,
+                                     const uint64_t *head_len, const uint8_t *const *tail, const uint64_t *tail_len,
+                                     const uint64_t *start, const int64_t *cand, const uint32_t *flags,
+                                     uint64_t *rbase, int64_t *rcand,
+                                     int (*take)(void *ctx, uint64_t i, const uint8_t *out, uint64_t out_len,
+                                                 const uint8_t *in),
+                                     void *ctx);
+extern "C" int xc__mem_lookup(xc_memmodel *m, uint64_t h, uint8_t *out, int *found);
+extern "C" int xc__mem_enter(xc_memmodel *m, uint64_t h, const uint8_t *seg, int *dup);
+// decode plans (xc_decode.hip): a finished run's lookup hits, in the reference's order
+extern "C" int xc__dplan_hits(void *dplan, uint64_t **hits, uint64_t *n, int *complete);
+// A run on the memory cache needs the replay engine (xc_memcache.cpp): a duplicated hash may
+// answer with other bytes than the device holds, or the run entered a hash twice.
+constexpr int XC__SLOW = -1000;
+
 struct xc_cache {
     xc_ctx *ctx;
     uint64_t cap;
@@ -287,7 +314,18 @@ struct xc_cache {
     int64_t host_count = -1;
     uint32_t gen = 0;  // bumped when the cache grows (its arrays move): plans refresh their copies
     const void *busy = nullptr;  // the plan whose submitted run is in flight on this cache
+    // the reference's recent window and duplicate enters (null: a COSS tier's mirror, whose Store
+    // has its own), its copy at the snapshot, the run whose lookup hits it has not replayed yet
+    // (one encode or decode plan: consumed before the next operation that needs the order, dropped
+    // by a restore), and whether the replay engine drives the cache (no hooks then)
+    xc_memmodel *mem = nullptr;
+    xc_memmodel *mem_snap = nullptr;
+    xc_plan *pend_enc = nullptr;
+    void *pend_dec = nullptr;
+    int engine = 0;
 };
+
+static int cache_settle(xc_cache *c);
 
 // A run submitted on the cache and not finished (xc_encode_submit without poll/wait): every other
 // operation on the cache would read a partial count, or move the arrays that run's kernels (and
@@ -348,8 +386,23 @@ extern "C" int xc_cache_create(xc_ctx *ctx, uint64_t cap, xc_cache **out)
     HIPCHK(hipMemsetAsync(c->count, 0, 4, ctx->stream));
     HIPCHK(hipMemsetAsync(c->ctl, 0, CTL_WORDS * 4, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (!(c->mem = xc__mem_new(c, ctx))) return fail(XC_ENOMEM, "host allocation failed");
     *out = c;
     return XC_OK;
+}
+
+// A COSS tier's device mirror (xc_coss.cpp): its Store replays every lookup, recent window included.
+extern "C" void xc__cache_untracked(xc_cache *c)
+{
+    if (!c) return;
+    xc__mem_free(c->mem);
+    c->mem = nullptr;
+}
+
+// The replay engine drives the cache (xc_memcache.cpp): the hooks stand aside.
+extern "C" void xc__cache_engine(xc_cache *c, int on)
+{
+    if (c) c->engine = on;
 }
 
 extern "C" int xc_cache_destroy(xc_cache *c)
@@ -366,6 +419,8 @@ extern "C" int xc_cache_destroy(xc_cache *c)
     dfree(c->snap_lo_zero);
     dfree(c->snap_count_dev);
     dfree(c->snap_l2);
+    xc__mem_free(c->mem);
+    xc__mem_free(c->mem_snap);
     delete c;
     return XC_OK;
 }
@@ -538,6 +593,18 @@ extern "C" int xc_cache_count(xc_cache *c, uint64_t *n)
     if (rc) return rc;
     uint32_t v = 0;
     if ((rc = cache_count_host(c, &v))) return rc;
+    // (the reference's map holds a hash entered twice once; the device keeps both segments)
+    *n = std::min<uint64_t>(v, c->cap) - std::min<uint64_t>(xc__mem_extra(c->mem), std::min<uint64_t>(v, c->cap));
+    return XC_OK;
+}
+
+// The device's segment count (the replay engine's truncation points).
+extern "C" int xc__cache_count_raw(xc_cache *c, uint64_t *n)
+{
+    int rc = set_dev(c->ctx);
+    if (rc) return rc;
+    uint32_t v = 0;
+    if ((rc = cache_count_host(c, &v))) return rc;
     *n = std::min<uint64_t>(v, c->cap);
     return XC_OK;
 }
@@ -547,7 +614,12 @@ extern "C" int xc_cache_snapshot(xc_cache *c)
     if (!c) return fail(XC_EINVAL, "null");
     int rc = set_dev(c->ctx);
     if (!rc) rc = cache_busy(c);
+    if (!rc) rc = cache_settle(c);
     if (rc) return rc;
+    if (c->mem) {
+        xc__mem_free(c->mem_snap);
+        if (!(c->mem_snap = xc__mem_clone(c->mem))) return fail(XC_ENOMEM, "host allocation failed");
+    }
     if ((rc = cache_count_host(c, &c->snap_count))) return rc;
     c->host_count = c->snap_count;
     hipStream_t s = c->ctx->stream;
@@ -579,6 +651,14 @@ static int cache_restore_async(xc_cache *c, uint32_t cur_count)
     return XC_OK;
 }
 
+// The model as it was at the snapshot (the runs since are undone: their lookups are not replayed).
+static int mem_restore(xc_cache *c)
+{
+    c->pend_enc = nullptr;
+    c->pend_dec = nullptr;
+    return c->mem && c->mem_snap ? xc__mem_restore(c->mem, c->mem_snap) : XC_OK;
+}
+
 extern "C" int xc_cache_restore_async(xc_cache *c)
 {
     if (!c) return fail(XC_EINVAL, "null");
@@ -586,6 +666,10 @@ extern "C" int xc_cache_restore_async(xc_cache *c)
     int rc = set_dev(c->ctx);
     if (!rc) rc = cache_busy(c);
     if (rc) return rc;
+    struct MemAfter {  // (after the device restore is enqueued: a mirror's fix-up follows it)
+        xc_cache *c;
+        ~MemAfter() { mem_restore(c); }
+    } mem_after{c};
     hipStream_t s = c->ctx->stream;
     if (c->host_count >= 0) {
         // one kernel: table slots entered since the snapshot, filters and count from the snapshot
@@ -623,14 +707,13 @@ extern "C" int xc_cache_restore(xc_cache *c)
     if ((rc = cache_restore_async(c, cur))) return rc;
     HIPCHK(hipStreamSynchronize(c->ctx->stream));
     c->host_count = c->snap_count;
-    return XC_OK;
+    return mem_restore(c);
 }
 
-extern "C" int xc_cache_lookup(xc_cache *c, uint64_t h, uint8_t *out, int *found)
+// Lookup without side effects (the device's bytes for the hash).
+extern "C" int xc__cache_read(xc_cache *c, uint64_t h, uint8_t *out, int *found)
 {
-    if (!c || !out || !found) return fail(XC_EINVAL, "null");
     int rc = set_dev(c->ctx);
-    if (!rc) rc = cache_busy(c);
     if (rc) return rc;
     hipStream_t s = c->ctx->stream;
     uint32_t *d_found = c->ctx->d_scratch;
@@ -644,12 +727,61 @@ extern "C" int xc_cache_lookup(xc_cache *c, uint64_t h, uint8_t *out, int *found
     return XC_OK;
 }
 
+// XCodecMemoryCache::lookup (xcodec_cache.h:190-210): the recent window decides the bytes of a
+// hash entered twice, and remembers a map hit.
+extern "C" int xc_cache_lookup(xc_cache *c, uint64_t h, uint8_t *out, int *found)
+{
+    if (!c || !out || !found) return fail(XC_EINVAL, "null");
+    int rc = set_dev(c->ctx);
+    if (!rc) rc = cache_busy(c);
+    if (!rc) rc = cache_settle(c);
+    if (rc) return rc;
+    return c->mem && !c->engine ? xc__mem_lookup(c->mem, h, out, found) : xc__cache_read(c, h, out, found);
+}
+
+// Device values of n hashes (~0: absent), no side effects.
+extern "C" int xc__cache_find(xc_cache *c, const uint64_t *h, uint64_t n, uint64_t *val)
+{
+    if (!n) return XC_OK;
+    int rc = set_dev(c->ctx);
+    if (rc) return rc;
+    hipStream_t s = c->ctx->stream;
+    uint64_t *d = nullptr;
+    HIPCHK(dmalloc(&d, n * 16));
+    HIPCHK(hipMemcpyAsync(d, h, n * 8, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_find, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, c->set.d, (const uint64_t *)d,
+                       d + n, (uint32_t)n);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(val, d + n, n * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    dfree(d);
+    return XC_OK;
+}
+
+// The table value of a present hash, set (a restore puts back what a mirror replaced).
+extern "C" int xc__cache_set_value(xc_cache *c, uint64_t h, uint64_t val)
+{
+    int rc = set_dev(c->ctx);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_setval, dim3(1), dim3(64), 0, c->ctx->stream, c->set.d, h, val);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->ctx->stream));
+    return XC_OK;
+}
+
+// XCodecMemoryCache::enter (xcodec_cache.h:182-188); a hash entered again with other bytes takes
+// the release build's semantics (xc_memcache.cpp).
 extern "C" int xc_cache_enter(xc_cache *c, uint64_t h, const uint8_t *seg)
 {
     if (!c || !seg) return fail(XC_EINVAL, "null");
     int rc = set_dev(c->ctx);
     if (!rc) rc = cache_busy(c);
+    if (!rc) rc = cache_settle(c);
     if (rc) return rc;
+    if (c->mem && !c->engine) {
+        int dup = 0;
+        if ((rc = xc__mem_enter(c->mem, h, seg, &dup)) || dup) return rc;
+    }
     hipStream_t s = c->ctx->stream;
     if ((rc = cache_reserve(c, 1))) return rc;
     c->host_count = -1;
@@ -677,6 +809,11 @@ extern "C" int xc_hash_segments(xc_ctx *ctx, const uint8_t *d_segs, uint64_t n, 
     return XC_OK;
 }
 
+extern "C" int xc_hash_segments_host(xc_ctx *ctx, const uint8_t *segs, uint64_t n, uint64_t *out);
+extern "C" int xc__hash_segments_host_raw(xc_ctx *ctx, const uint8_t *segs, uint64_t n, uint64_t *out)
+{
+    return xc_hash_segments_host(ctx, segs, n, out);
+}
 extern "C" int xc_hash_segments_host(xc_ctx *ctx, const uint8_t *segs, uint64_t n, uint64_t *out)
 {
     if (!ctx || (n && (!segs || !out))) return fail(XC_EINVAL, "null");
@@ -825,8 +962,10 @@ struct xc_plan {
     bool g_off = false;              // capture failed (or XC_NO_GRAPH): enqueue directly
     bool zero_ctl = false;           // the next k_clear_set also clears the run's control words
     uint32_t cache_gen = 0;          // the cache arrays P holds (xc_cache::gen)
-    uint4 *d_coll = nullptr;         // collision records (xc__plan_collisions), else null
+    uint4 *d_coll = nullptr;         // collision records of every buffer (COLL_CAP each)
     uint32_t *d_coll_cnt = nullptr;
+    std::vector<uint32_t> tok_base;  // host copy [nb + 1]
+    int64_t count0 = -1;             // the cache's count before a run that may enter a hash twice
     uint64_t max_new = 0;            // most segments a run can enter (sum of len / 2048 + 1)
 };
 
@@ -978,6 +1117,8 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     p->out_bytes = oo + 256;
     p->nchunks = (uint32_t)chunks.size();
     p->chunk0 = chunk0;
+    tok_base[nbuf] = (uint32_t)toks;
+    p->tok_base = tok_base;
     p->chunk_bytes.assign(chunks.size() + 1, 0);
     for (size_t k = 0; k < chunks.size(); k++) {
         uint64_t n = lengths[chunks[k].x];
@@ -1032,6 +1173,13 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     HIPCHK(dmalloc(&P.tok_dpos, nt * 4));
     HIPCHK(dmalloc(&P.tok_h, nt * 8));
     HIPCHK(dmalloc(&P.tok_known, nt * 4));
+    // every lookup that hits with other bytes (xcodec_encoder.cc:129-137): the recent window's
+    // replay (xc_memcache.cpp) and the COSS tier's (xc_coss.cpp)
+    HIPCHK(dmalloc(&p->d_coll, nb1 * COLL_CAP * sizeof(uint4)));
+    HIPCHK(dmalloc(&p->d_coll_cnt, nb1 * 4));
+    HIPCHK(hipMemsetAsync(p->d_coll_cnt, 0, nb1 * 4, s));
+    P.coll = p->d_coll;
+    P.coll_cnt = p->d_coll_cnt;
     HIPCHK(dmalloc(&P.blk_h, std::max<uint64_t>(nblk, 1) * 8));
     HIPCHK(dmalloc(&P.blk_pref, std::max<uint64_t>(nblk, 1) * 4));
     HIPCHK(hipMemsetAsync(P.blk_pref, 0, std::max<uint64_t>(nblk, 1) * 4, s));
@@ -1098,10 +1246,94 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     return XC_OK;
 }
 
+// A finished run's lookup hits in the reference's order: per buffer, its REF tokens (window end
+// seg + 2047) and its collision lookups, by position.  *complete = 0 when a buffer had more
+// collisions than were recorded.
+static int plan_hits(xc_plan *p, std::vector<uint64_t> &hits, int *complete)
+{
+    *complete = 1;
+    if (!p->nb) return XC_OK;
+    const uint64_t nt = p->tok_base[p->nb];
+    std::vector<uint32_t> cnt(p->nb), op(nt), seg(nt), ccnt(p->nb);
+    std::vector<uint64_t> th(nt);
+    std::vector<uint4> coll((size_t)p->nb * COLL_CAP);
+    hipStream_t s = p->cache->ctx->stream;
+    HIPCHK(hipMemcpyAsync(cnt.data(), p->P.tok_cnt, p->nb * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(op.data(), p->P.tok_op, nt * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(seg.data(), p->P.tok_seg, nt * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(th.data(), p->P.tok_h, nt * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(ccnt.data(), p->d_coll_cnt, p->nb * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(coll.data(), p->d_coll, coll.size() * sizeof(uint4), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    for (uint64_t b = 0; b < p->nb; b++) {
+        const uint32_t tb = p->tok_base[b], n = std::min(cnt[b], p->tok_base[b + 1] - tb);
+        const uint32_t nc = std::min<uint32_t>(ccnt[b], COLL_CAP);
+        if (ccnt[b] > COLL_CAP) *complete = 0;
+        uint32_t ci = 0;
+        for (uint32_t t = 0; t < n; t++) {
+            if (op[tb + t] != OP_REF) continue;
+            const uint32_t q = seg[tb + t] + (XC_SEG - 1u);
+            for (; ci < nc && coll[b * COLL_CAP + ci].x < q; ci++)
+                hits.push_back(((uint64_t)coll[b * COLL_CAP + ci].z << 32) | coll[b * COLL_CAP + ci].y);
+            hits.push_back(th[tb + t]);
+        }
+        for (; ci < nc; ci++) hits.push_back(((uint64_t)coll[b * COLL_CAP + ci].z << 32) | coll[b * COLL_CAP + ci].y);
+    }
+    return XC_OK;
+}
+
+// The pending run's lookup hits into the recent window (before anything that comes after it).
+static int cache_settle(xc_cache *c)
+{
+    if (!c->mem || c->engine) return XC_OK;
+    std::vector<uint64_t> hits;
+    int complete = 1, rc = XC_OK;
+    if (c->pend_enc) {
+        xc_plan *p = c->pend_enc;
+        c->pend_enc = nullptr;
+        if ((rc = set_dev(c->ctx)) || (rc = plan_hits(p, hits, &complete))) return rc;
+        xc__mem_hits(c->mem, hits.data(), hits.size(), complete);
+    }
+    if (c->pend_dec) {
+        void *d = c->pend_dec;
+        c->pend_dec = nullptr;
+        uint64_t *h = nullptr, n = 0;
+        if ((rc = xc__dplan_hits(d, &h, &n, &complete))) return rc;
+        xc__mem_hits(c->mem, h, n, complete);
+        free(h);
+    }
+    return XC_OK;
+}
+
+// For xc_decode.hip: a decode run on the memory cache starts (the pending run is replayed first;
+// *slow: the replay engine must run it) / has finished (its hits are the pending ones now) / its
+// plan is destroyed.
+extern "C" int xc__cache_run_start(xc_cache *c, int *slow)
+{
+    *slow = 0;
+    int rc = cache_settle(c);
+    if (!rc && c->mem && !c->engine) *slow = xc__mem_live(c->mem);
+    return rc;
+}
+extern "C" void xc__cache_run_done_dec(xc_cache *c, void *dplan)
+{
+    if (c->mem && !c->engine) c->pend_dec = dplan;
+}
+extern "C" void xc__cache_plan_gone_dec(xc_cache *c, void *dplan)
+{
+    if (c->pend_dec == dplan) cache_settle(c);
+}
+extern "C" int xc__mem_decode_batch(xc_memmodel *m, const uint8_t *in, const uint64_t *in_off,
+                                    const uint64_t *in_len, uint64_t nbuf, uint8_t *out, const uint64_t *out_off,
+                                    const uint64_t *out_cap, uint64_t *out_len, uint64_t *consumed, int32_t *status,
+                                    uint64_t *unknown, int32_t *has_unknown);
+extern "C" xc_memmodel *xc__cache_mem(xc_cache *c) { return c->mem; }
+
 extern "C" int xc_plan_destroy(xc_plan *p)
 {
     if (!p) return XC_OK;
     hipSetDevice(p->cache->ctx->dev);
+    if (p->cache->pend_enc == p) cache_settle(p->cache);  // (its tokens are the window's record)
     // pooled memory goes back for reuse at once: nothing may still read or write it
     hipStreamSynchronize(p->cache->ctx->stream);
     if (p->hs) hipStreamSynchronize(p->hs);
@@ -1549,7 +1781,9 @@ static int encode_sub_sync(xc_plan *p, uint32_t sb, uint32_t *ctl)
 static bool use_graph(xc_plan *p)
 {
     const char *e = getenv("XC_NO_GRAPH");
-    return !(e && atoi(e)) && !p->g_off && !p->timing && !p->host_path && p->sub.size() == 2;
+    // (nor for stateful streams: a duplicate enter is counted by the emit, after the graph's
+    // published control words)
+    return !(e && atoi(e)) && !p->g_off && !p->timing && !p->host_path && p->sub.size() == 2 && !p->P.stream_st;
 }
 
 // Record ev_ctl after the control words' copy to h_ctl (enqueued by the caller or published by
@@ -1642,7 +1876,19 @@ extern "C" int xc_encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out,
     hipStream_t s = p->cache->ctx->stream;
     // room for every segment this run can declare (the reference's cache never fills)
     xc_cache *c = p->cache;
-    if ((rc = cache_busy(c, p)) || (rc = cache_reserve(c, p->max_new))) return rc;
+    if ((rc = cache_busy(c, p)) || (rc = cache_settle(c))) return rc;
+    if (c->mem && !c->engine) {
+        // a hash entered twice may answer with other bytes than the device holds: the host paths
+        // replay such runs (xc_memcache.cpp)
+        if (xc__mem_live(c->mem)) return fail(XC__SLOW, "a hash entered twice is in the recent window");
+        p->count0 = -1;
+        if (p->P.stream_st) {  // (only a carried candidate can enter a hash twice)
+            uint32_t n = 0;
+            if ((rc = cache_count_host(c, &n))) return rc;
+            p->count0 = n;
+        }
+    }
+    if ((rc = cache_reserve(c, p->max_new))) return rc;
     if (p->cache_gen != c->gen) {  // the cache grew: its arrays moved
         const PlanDev cp = cache_plandev(c);
         p->P.cache = cp.cache;
@@ -1680,7 +1926,7 @@ extern "C" int xc_encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out,
         // the control words, so the host returns before the last emit has finished (no copy of
         // the words after it: a copy landing after the host re-armed the sentinel would clear it)
         const bool pub = p->completion == XC_COMPLETE_STREAM && !p->timing && !p->host_path && nsub > 0 &&
-                         p->sub[nsub] > p->sub[nsub - 1];
+                         p->sub[nsub] > p->sub[nsub - 1] && !p->P.stream_st;
         if (pub) p->h_ctl[CTL_WORDS - 1] = 0xFFFFFFFFu;
         p->pass_published = pub;
         for (size_t k = 0; k < nsub; k++) {
@@ -1746,6 +1992,17 @@ static int encode_finish(xc_plan *p)
     }
     if (ctl[CTL_ERROR] & ERR_PACK_CAP) return fail(XC_EINVAL, "packed output capacity too small");
     if (ctl[CTL_ERROR]) return fail(XC_EDEVICE, "internal encode error " + std::to_string(ctl[CTL_ERROR]));
+    xc_cache *c = p->cache;
+    if (c->mem && !c->engine) {
+        if (ctl[CTL_DUPS]) {
+            // a carried candidate entered a hash the cache held: undone, the host replays the run
+            if (p->count0 < 0) return fail(XC_EDEVICE, "duplicate enter in a run without stream state");
+            if ((rc = cache_rebuild(c, c->cap, (uint32_t)p->count0, true))) return rc;
+            c->host_count = p->count0;
+            return fail(XC__SLOW, "a hash entered twice");
+        }
+        c->pend_enc = p;  // its lookup hits go to the recent window when the order needs them
+    }
     return XC_OK;
 }
 
@@ -1795,8 +2052,11 @@ extern "C" int xc_plan_set_completion(xc_plan *p, int mode)
 extern "C" int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_out_len)
 {
     int rc = xc_encode_submit(p, d_in, d_out, d_out_len);
-    if (rc) return rc;
-    return xc_encode_wait(p);
+    if (!rc) rc = xc_encode_wait(p);
+    if (rc == XC__SLOW && p && !p->host_path)
+        return fail(XC_EINVAL, "device-resident run on a cache with a hash entered twice by a stateful stream: "
+                               "run it through xc_encode_batch_host / xc_encode_streams (the recent window's replay)");
+    return rc;
 }
 
 extern "C" int xc_host_alloc(xc_ctx *ctx, uint64_t bytes, void **out)
@@ -1884,15 +2144,6 @@ extern "C" int xc__encode_batch_host_coll(xc_cache *c, const uint8_t *in, const 
         xc_plan_destroy(p);
         return rc;
     }
-    if (coll_cnt && nbuf) {
-        if (dmalloc(&p->d_coll, (size_t)nbuf * COLL_CAP * sizeof(uint4)) != hipSuccess ||
-            dmalloc(&p->d_coll_cnt, (size_t)nbuf * 4) != hipSuccess) {
-            xc_plan_destroy(p);
-            return fail(XC_ENOMEM, "device allocation failed");
-        }
-        p->P.coll = p->d_coll;
-        p->P.coll_cnt = p->d_coll_cnt;
-    }
     // the end-to-end path (xc_encode_run_host): per-sub-batch input copies overlapping the
     // encode, the encoded streams packed into pinned memory by a kernel; the input arena needs no
     // clearing (bytes past a buffer's end are read but never used)
@@ -1969,6 +2220,9 @@ extern "C" int xc__encode_gather(xc_cache *c, uint64_t nbuf, const uint8_t *cons
     xc_plan_destroy(p);  // (synchronizes before the pinned buffers return to the pool)
     pool_free(h_in);
     pool_free(h_out);
+    if (rc == XC__SLOW)  // a hash entered twice: the recent window's replay (xc_memcache.cpp)
+        rc = xc__mem_encode_gather(c->mem, nbuf, head, head_len, tail, tail_len, start, cand, flags, rbase, rcand,
+                                   take, ctx);
     return rc;
 }
 
@@ -1978,8 +2232,13 @@ extern "C" int xc__encode_batch_host_ex(xc_cache *c, const uint8_t *in, const ui
                                         const uint64_t *start, const int64_t *cand, const uint32_t *flags,
                                         uint64_t *rbase, int64_t *rcand)
 {
-    return xc__encode_batch_host_coll(c, in, in_off, in_len, nbuf, out, out_off, out_cap, out_len, start, cand, flags,
-                                      rbase, rcand, nullptr, nullptr);
+    int rc = xc__encode_batch_host_coll(c, in, in_off, in_len, nbuf, out, out_off, out_cap, out_len, start, cand,
+                                        flags, rbase, rcand, nullptr, nullptr);
+    if (rc == XC__SLOW && !start && !cand && !flags)
+        rc = xc__mem_encode_batch(c->mem, in, in_off, in_len, nbuf, out, out_off, out_cap, out_len);
+    else if (rc == XC__SLOW)
+        rc = fail(XC_EINVAL, "stream state through the host batch with a hash entered twice: use xc_encode_streams");
+    return rc;
 }
 
 extern "C" int xc_encode_batch_host(xc_cache *c, const uint8_t *in, const uint64_t *in_off, const uint64_t *in_len,
