@@ -20,8 +20,8 @@ bool XCodecDecoder::decode(Buffer& output, Buffer& input, std::set<uint64_t>& un
     const uint64_t n = input.length();
     std::vector<uint8_t> in(n);
     input.copyout(&in[0], n);
-    /* a REF (10 bytes) expands to 2048: the output bound of xc__decode_bound, and at least n */
-    uint64_t off = 0, len = n, cap = n * 205 + 16, olen = 0, consumed = 0, unknown = 0;
+    /* a REF (10 bytes) expands to 2048: n plus 2038 per F1 byte (xchip::decode_bound) */
+    uint64_t off = 0, len = n, cap = xchip::decode_bound(&in[0], n), olen = 0, consumed = 0, unknown = 0;
     int32_t status = 0, has_unknown = 0;
     std::vector<uint8_t> out(cap);
     if (cache_->coss())

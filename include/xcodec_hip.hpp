@@ -12,6 +12,8 @@
 #pragma once
 
 #include <cstdint>
+#include <cstring>
+#include <memory>
 #include <set>
 #include <stdexcept>
 #include <string>
@@ -128,15 +130,23 @@ struct StreamCall {
     bool flush;
 };
 
-/* Many connections' calls as one device batch, in order; returns each call's output. */
-inline std::vector<Bytes> encode_streams(const std::vector<StreamCall> &calls)
+/* The outputs of one encode_streams batch: call k's bytes at data + off[k], len[k] of them. */
+struct EncodedBatch {
+    std::unique_ptr<uint8_t[]> data;  // (not value-initialised: the library writes what is read)
+    std::vector<uint64_t> off, len;
+    const uint8_t *at(size_t k) const { return data.get() + off[k]; }
+};
+
+/* Many connections' calls as one device batch, in order, into one output buffer. */
+inline void encode_streams(const std::vector<StreamCall> &calls, EncodedBatch &res)
 {
     const size_t n = calls.size();
-    std::vector<Bytes> res(n);
-    if (n == 0) return res;
+    res.off.assign(n, 0);
+    res.len.assign(n, 0);
+    if (n == 0) return;
     std::vector<xc_encoder *> enc(n);
     std::vector<const uint8_t *> in(n);
-    std::vector<uint64_t> len(n), off(n), cap(n), olen(n);
+    std::vector<uint64_t> len(n), cap(n);
     std::vector<uint32_t> flags(n);
     std::vector<std::pair<xc_encoder *, uint64_t>> pend;  // pending bytes per encoder so far
     uint64_t total = 0;
@@ -154,15 +164,35 @@ inline std::vector<Bytes> encode_streams(const std::vector<StreamCall> &calls)
         }
         *p += len[k];
         cap[k] = 2 * *p + 16;
-        off[k] = total;
+        res.off[k] = total;
         total += cap[k];
     }
-    Bytes out(total ? total : 1);
-    check(xc_encode_streams(enc.data(), in.data(), len.data(), flags.data(), n, out.data(), off.data(),
-                            cap.data(), olen.data()));
-    for (size_t k = 0; k < n; k++)
-        res[k].assign(out.begin() + (ptrdiff_t)off[k], out.begin() + (ptrdiff_t)(off[k] + olen[k]));
+    res.data.reset(new uint8_t[total ? total : 1]);
+    check(xc_encode_streams(enc.data(), in.data(), len.data(), flags.data(), n, res.data.get(), res.off.data(),
+                            cap.data(), res.len.data()));
+}
+
+/* The same, each call's output as its own byte vector. */
+inline std::vector<Bytes> encode_streams(const std::vector<StreamCall> &calls)
+{
+    EncodedBatch b;
+    encode_streams(calls, b);
+    std::vector<Bytes> res(calls.size());
+    for (size_t k = 0; k < calls.size(); k++) res[k].assign(b.at(k), b.at(k) + b.len[k]);
     return res;
+}
+
+/* An output bound for decoding n encoded bytes (xc__decode_bound): every byte, plus 2038 for each
+ * F1 (only a REF grows: 10 -> 2048 bytes), plus 16. */
+inline uint64_t decode_bound(const uint8_t *p, uint64_t n)
+{
+    uint64_t c = 0;
+    const uint8_t *e = p + n;
+    while ((p = (const uint8_t *)std::memchr(p, 0xF1, (size_t)(e - p))) != nullptr) {
+        c++;
+        p++;
+    }
+    return n + 2038u * c + 16u;
 }
 
 /* XCodecDecoder::decode(output, input, unknown_hashes): decodes as far as it can, removes the
@@ -176,7 +206,7 @@ public:
     {
         uint64_t off = 0, len = input.size();
         if (len == 0) return true;
-        uint64_t cap = len * 205 + 16, olen = 0, consumed = 0, unk = 0;
+        uint64_t cap = decode_bound(input.data(), len), olen = 0, consumed = 0, unk = 0;
         int32_t status = 0, has_unknown = 0;
         Bytes out(cap);
         check(xc_decode_batch_host(cache_->get(), input.data(), &off, &len, 1, out.data(), &off, &cap, &olen,

@@ -220,3 +220,64 @@ def run_connections(backend, warm_a, inputs, batched, chunk=None, order_seed=5, 
         c.b_enc.flush(0)
     pump_turns(a, b, conns, chunk)
     return a, b, conns
+
+
+# ---- the C++ filters' scenario files (tests/cpp/pipe_turns.cpp) ----------------------------------
+
+def write_scenario(path, warm, order, inputs, waiting=False, batched=True):
+    """order[t]: the connections' consume order of turn t; inputs[i][t]: connection i's read of turn
+    t (empty: none)."""
+    import struct
+    nconn, turns = len(inputs), len(order)
+    with open(path, "wb") as f:
+        f.write(struct.pack("<IIII", nconn, turns, int(waiting), int(batched)))
+        f.write(struct.pack("<Q", len(warm)))
+        for b in warm:
+            f.write(struct.pack("<Q", len(b)) + bytes(b))
+        for o in order:
+            f.write(struct.pack("<%dI" % nconn, *o))
+        for i in range(nconn):
+            for t in range(turns):
+                b = bytes(inputs[i][t])
+                f.write(struct.pack("<Q", len(b)) + b)
+
+
+def read_outputs(path, nconn):
+    """Per connection: (A->B wire bytes, B->A wire bytes, B's sink, A's sink)."""
+    import struct
+    d = open(path, "rb").read()
+    at, res = 0, []
+    for _ in range(nconn):
+        v = []
+        for _ in range(4):
+            n = struct.unpack_from("<Q", d, at)[0]
+            v.append(d[at + 8:at + 8 + n])
+            at += 8 + n
+        res.append(tuple(v))
+    return res
+
+
+def run_scenario(backend, warm, order, inputs, waiting=False, batched=True):
+    """The scenario of write_scenario through the Python pipes (the expected bytes with the oracle
+    backend): the same steps as pipe_turns.cpp's parity mode."""
+    a = Proxy(backend, UUID_A, warm=lambda s: s.encode_batch(warm), batched=batched, waiting=waiting)
+    b = Proxy(backend, UUID_B, batched=batched)
+    conns = [Conn(a, b) for _ in inputs]
+    for t, o in enumerate(order):
+        for i in o:
+            d = bytes(inputs[i][t])
+            if d:
+                assert conns[i].a_enc.consume(d)
+        a.end_turn()
+        b.end_turn()
+        if waiting:
+            for c in conns:
+                c.a_enc.on_read_timeout()
+        pump_turns(a, b, conns)
+    for c in conns:
+        c.a_enc.flush(0)
+    pump_turns(a, b, conns)
+    for c in conns:
+        c.b_enc.flush(0)
+    pump_turns(a, b, conns)
+    return [(bytes(c.ab.log), bytes(c.ba.log), bytes(c.b_sink.data), bytes(c.a_sink.data)) for c in conns]

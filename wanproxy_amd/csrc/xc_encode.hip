@@ -1789,6 +1789,33 @@ __global__ void k_enter_bulk(PlanDev P, const uint64_t *h, const uint8_t *segs, 
     }
 }
 
+// A run's lookup hits for the recent window (xc_memcache.cpp), one thread per buffer: at
+// out[tok_base[b] + b * (COLL_CAP + 1)] the count (bit 63: more collisions than were recorded), then
+// the hashes in the reference's order: REF tokens (window end seg + 2047) and the recorded collision
+// lookups, by position.
+__global__ void k_hits(PlanDev P, uint64_t *out)
+{
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= P.nb) return;
+    uint64_t *o = out + P.tok_base[b] + (uint64_t)b * (COLL_CAP + 1u);
+    const uint32_t tb = P.tok_base[b], n = P.tok_cnt[b], cc = P.coll_cnt[b], nc = min(cc, COLL_CAP);
+    uint32_t k = 0, ci = 0;
+    for (uint32_t t = 0; t < n; t++) {
+        if (P.tok_op[tb + t] != OP_REF) continue;
+        const uint32_t q = P.tok_seg[tb + t] + (XC_SEG - 1u);
+        for (; ci < nc && P.coll[b * COLL_CAP + ci].x < q; ci++) {
+            const uint4 r = P.coll[b * COLL_CAP + ci];
+            o[1 + k++] = ((uint64_t)r.z << 32) | r.y;
+        }
+        o[1 + k++] = P.tok_h[tb + t];
+    }
+    for (; ci < nc; ci++) {
+        const uint4 r = P.coll[b * COLL_CAP + ci];
+        o[1 + k++] = ((uint64_t)r.z << 32) | r.y;
+    }
+    o[0] = (uint64_t)k | (cc > COLL_CAP ? 1ull << 63 : 0ull);
+}
+
 // The table values of n hashes (~0: absent or evicted), no side effects.
 __global__ void k_find(DevSet cache, const uint64_t *h, uint64_t *val, uint32_t n)
 {

@@ -256,6 +256,7 @@ __global__ void k_enter_one(PlanDev P, uint64_t h, const uint8_t *seg);
 __global__ void k_enter_bulk(PlanDev P, const uint64_t *h, const uint8_t *segs, uint32_t n, uint32_t first);
 __global__ void k_kill(DevSet cache, const uint64_t *h, uint32_t n);
 __global__ void k_find(DevSet cache, const uint64_t *h, uint64_t *val, uint32_t n);
+__global__ void k_hits(PlanDev P, uint64_t *out);
 __global__ void k_setval(DevSet cache, uint64_t h, uint64_t val);
 __global__ void k_lookup_one(PlanDev P, uint64_t h, uint8_t *out, uint32_t *found);
 __global__ void k_selftest(uint32_t *err);

@@ -965,6 +965,7 @@ struct xc_plan {
     uint4 *d_coll = nullptr;         // collision records of every buffer (COLL_CAP each)
     uint32_t *d_coll_cnt = nullptr;
     std::vector<uint32_t> tok_base;  // host copy [nb + 1]
+    uint64_t *h_hits = nullptr;      // pinned: the host path's lookup hits (k_hits)
     int64_t count0 = -1;             // the cache's count before a run that may enter a hash twice
     uint64_t max_new = 0;            // most segments a run can enter (sum of len / 2048 + 1)
 };
@@ -1373,6 +1374,7 @@ extern "C" int xc_plan_destroy(xc_plan *p)
     dfree(p->d_stream_st);
     dfree(p->d_stream_res);
     dfree(p->d_coll);
+    pool_free(p->h_hits);
     dfree(p->d_coll_cnt);
     for (auto &x : p->ev_live) { hipEventDestroy(x.second.first); hipEventDestroy(x.second.second); }
     for (auto e : p->ev_pool) hipEventDestroy(e);
@@ -2119,7 +2121,31 @@ extern "C" int xc_encode_run_host(xc_plan *p, const uint8_t *h_in, uint8_t *h_ou
         HIPCHK(hipMemcpyAsync(h_len, p->e_len, p->nb * 8, hipMemcpyDeviceToHost, s));
         if (h_pos) HIPCHK(hipMemcpyAsync(h_pos, p->e_pos, p->nb * 8, hipMemcpyDeviceToHost, s));
     }
+    // the run's lookup hits for the recent window, written by a kernel into pinned memory beside
+    // the outputs (no copy round trips): replayed once the run has synchronised
+    xc_cache *c = p->cache;
+    const bool hits = c->mem && !c->engine && c->pend_enc == p && p->nb;
+    const size_t hwords = p->tok_base[p->nb] + (size_t)p->nb * (COLL_CAP + 1);
+    if (hits) {
+        if (!p->h_hits && hmalloc((void **)&p->h_hits, hwords * 8) != hipSuccess)
+            return fail(XC_ENOMEM, "pinned allocation failed");
+        void *dev = nullptr;
+        HIPCHK(hipHostGetDevicePointer(&dev, p->h_hits, 0));
+        hipLaunchKernelGGL(k_hits, dim3((p->nb + 255) / 256), dim3(256), 0, s, p->P, (uint64_t *)dev);
+        HIPCHK(hipGetLastError());
+    }
     HIPCHK(hipStreamSynchronize(s));
+    if (hits) {
+        std::vector<uint64_t> v;
+        int complete = 1;
+        for (uint64_t b = 0; b < p->nb; b++) {
+            const uint64_t *r = p->h_hits + p->tok_base[b] + b * (COLL_CAP + 1);
+            if (r[0] >> 63) complete = 0;
+            v.insert(v.end(), r + 1, r + 1 + (r[0] & 0xFFFFFFFFu));
+        }
+        xc__mem_hits(c->mem, v.data(), v.size(), complete);
+        c->pend_enc = nullptr;
+    }
     return XC_OK;
 }
 
