@@ -35,7 +35,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 SEG = 2048
 GOLD = os.path.join(ROOT, "tests", "golden", "fullsize_digests.npz")
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r02")
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r03")
 
 
 def parse():
@@ -265,12 +265,14 @@ def cpu_baseline(args, shard, warm, world) -> dict:
 
 def pmc_traffic(sub_batches: int):
     """HBM bytes per step of the whole encode pipeline from the committed rocprofv3 PMC passes of
-    this command (tools/pmc_kernels.sh -> tools/pmc_traffic.py -> profiles/r02/), or None."""
+    this command (tools/pmc_kernels.sh -> tools/pmc_traffic.py -> profiles/r03/), or None when the
+    record was taken with other library sources than these (its src_stamp) or another layout."""
+    from wanproxy_amd.provenance import source_stamp
     tp = os.path.join(PROFILE_DIR, "pmc_traffic_cfg5.json")
     if not os.path.exists(tp):
         return None
     rec = json.load(open(tp))
-    if rec.get("sub_batches") != sub_batches:
+    if rec.get("sub_batches") != sub_batches or rec.get("src_stamp") != source_stamp():
         return None
     return rec
 

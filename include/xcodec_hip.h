@@ -61,6 +61,9 @@ int xc_cache_capacity(xc_cache *c, uint64_t *cap);
 int xc_cache_destroy(xc_cache *c);
 int xc_cache_count(xc_cache *c, uint64_t *n);
 /* Remember the current contents; xc_cache_restore() rolls every later enter() back. */
+/* Diagnostic: the false-positive rates of the cache's level-1 (LDS) and level-2 (L2) filters for
+ * a random window end, estimated from their word occupancy. */
+int xc_cache_filter_stats(xc_cache *c, double *l1_fp, double *l2_fp);
 int xc_cache_snapshot(xc_cache *c);
 int xc_cache_restore(xc_cache *c);
 /* XCodecCache::lookup (xcodec/xcodec_cache.h:190-210): *found = 1 and 2048 bytes to out (host). */

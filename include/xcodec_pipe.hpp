@@ -206,10 +206,10 @@ public:
             b->submit_encode(this, encoder_.get(), cache_->store.get(), std::move(buf), flush_now, done);
             return true;
         }
-        Bytes enc;
-        encoder_->encode(enc, buf.data(), buf.size());
-        if (flush_now) encoder_->flush(enc);
-        return done(enc.data(), enc.size(), 1, 0, false, 0);
+        // one device call: encode(buf) [+ flush()] (xc_encode_streams with one call)
+        EncodedBatch eb;
+        encode_streams({StreamCall{encoder_.get(), buf.data(), buf.size(), flush_now}}, eb);
+        return done(eb.at(0), eb.len[0], 1, 0, false, 0);
     }
 
     void flush(int flg) override

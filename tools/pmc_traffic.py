@@ -16,7 +16,12 @@ usage: python tools/pmc_traffic.py PMC_DIR OUT_JSON SUB_BATCHES ALG_BYTES_PER_ST
 import collections
 import csv
 import json
+import os
+import subprocess
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from wanproxy_amd.provenance import source_stamp  # noqa: E402
 
 
 def dispatches(path, counter):
@@ -54,7 +59,11 @@ def main():
            "traffic_over_alg": round(kib * 1024 / alg, 3),
            "per_kernel_bytes": {k: {"fetch_x2": int(2 * f * 1024), "write": int(w * 1024)}
                                 for k, (f, w) in sorted(per_kernel.items(), key=lambda x: -(2 * x[1][0] + x[1][1]))},
-           "correction": "FETCH_SIZE x2 (gfx950 wide streaming reads), WRITE_SIZE x1; KiB -> bytes"}
+           "correction": "FETCH_SIZE x2 (gfx950 wide streaming reads), WRITE_SIZE x1; KiB -> bytes",
+           # the sources the passes ran (bench.py attaches the record only to the same sources)
+           "src_stamp": source_stamp(),
+           "commit": subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True,
+                                    text=True).stdout.strip() or None}
     json.dump(rec, open(out_path, "w"), indent=1)
     print(json.dumps(rec, indent=1))
 

@@ -16,6 +16,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -137,6 +138,41 @@ static hipError_t dfree(void *p)
     return hipSuccess;
 }
 static hipError_t hmalloc(void **p, size_t bytes) { return pool_alloc(p, bytes, true); }
+
+// Host copies into / out of the pinned arenas, split over a few threads when a batch is large (one
+// core's memcpy, ~10 GB/s, would otherwise bound a turn's batch of connections).
+struct HostCopy {
+    uint8_t *dst;
+    const uint8_t *src;
+    uint64_t n;
+};
+static void host_copies(const std::vector<HostCopy> &cp)
+{
+    uint64_t total = 0;
+    for (const HostCopy &c : cp) total += c.n;
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const unsigned nt = (unsigned)std::min<uint64_t>({8, hw, total >> 21});  // >= 2 MiB a thread
+    if (nt <= 1) {
+        for (const HostCopy &c : cp)
+            if (c.n) memcpy(c.dst, c.src, c.n);
+        return;
+    }
+    // contiguous byte ranges of the concatenated copies, one a thread
+    auto work = [&](unsigned t) {
+        const uint64_t lo = total * t / nt, hi = total * (t + 1) / nt;
+        uint64_t at = 0;
+        for (const HostCopy &c : cp) {
+            const uint64_t a = std::max(lo, at), b = std::min(hi, at + c.n);
+            if (a < b) memcpy(c.dst + (a - at), c.src + (a - at), b - a);
+            at += c.n;
+            if (at >= hi) break;
+        }
+    };
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < nt; t++) th.emplace_back(work, t);
+    work(0);
+    for (std::thread &x : th) x.join();
+}
 
 // For xc_decode.hip.
 extern "C" int xc__dalloc(void **p, uint64_t bytes)
@@ -737,6 +773,32 @@ extern "C" int xc_cache_lookup(xc_cache *c, uint64_t h, uint8_t *out, int *found
     if (!rc) rc = cache_settle(c);
     if (rc) return rc;
     return c->mem && !c->engine ? xc__mem_lookup(c->mem, h, out, found) : xc__cache_read(c, h, out, found);
+}
+
+// Diagnostic: the false-positive rates a random window end sees in the cache's level-1 (LDS) and
+// level-2 (L2) filters, from their word occupancy (k = 2 bits in one word: the mean of (bits set /
+// 32)^2 over the words).
+extern "C" int xc_cache_filter_stats(xc_cache *c, double *l1_fp, double *l2_fp)
+{
+    if (!c || !l1_fp || !l2_fp) return fail(XC_EINVAL, "null");
+    int rc = set_dev(c->ctx);
+    if (!rc) rc = cache_busy(c);
+    if (rc) return rc;
+    std::vector<uint32_t> f(XC_FILT_WORDS), l2((size_t)XC_L2_WORDS * 2);
+    HIPCHK(hipMemcpyAsync(f.data(), c->set.d.filt, f.size() * 4, hipMemcpyDeviceToHost, c->ctx->stream));
+    HIPCHK(hipMemcpyAsync(l2.data(), c->set.d.l2, l2.size() * 4, hipMemcpyDeviceToHost, c->ctx->stream));
+    HIPCHK(hipStreamSynchronize(c->ctx->stream));
+    auto fp = [](const std::vector<uint32_t> &w) {
+        double a = 0;
+        for (uint32_t x : w) {
+            const double b = __builtin_popcount(x) / 32.0;
+            a += b * b;
+        }
+        return a / (double)w.size();
+    };
+    *l1_fp = fp(f);
+    *l2_fp = fp(l2);
+    return XC_OK;
 }
 
 // Device values of n hashes (~0: absent), no side effects.
@@ -2182,14 +2244,21 @@ extern "C" int xc__encode_batch_host_coll(xc_cache *c, const uint8_t *in, const 
         xc_plan_destroy(p);
         return fail(XC_ENOMEM, "pinned allocation failed");
     }
-    for (uint64_t i = 0; i < nbuf; i++) memcpy(h_in + p->in_off[i], in + in_off[i], in_len[i]);
+    {
+        std::vector<HostCopy> cp(nbuf);
+        for (uint64_t i = 0; i < nbuf; i++) cp[i] = {h_in + p->in_off[i], in + in_off[i], in_len[i]};
+        host_copies(cp);
+    }
     rc = xc_encode_run_host(p, h_in, h_out, cap_total + 16, lens.data(), pos.data());
     if (!rc) {
+        std::vector<HostCopy> cp;
+        cp.reserve(nbuf);
         for (uint64_t i = 0; i < nbuf; i++) {
             out_len[i] = lens[i];
             if (lens[i] > out_cap[i]) { rc = fail(XC_EINVAL, "output capacity too small"); continue; }
-            memcpy(out + out_off[i], h_out + pos[i], lens[i]);
+            cp.push_back({out + out_off[i], h_out + pos[i], lens[i]});
         }
+        host_copies(cp);
         if (!rc && streams && rbase && rcand) rc = xc_plan_stream_results(p, rbase, rcand);
         if (!rc && coll_cnt && nbuf) {
             if (hipMemcpy(coll_cnt, p->d_coll_cnt, nbuf * 4, hipMemcpyDeviceToHost) != hipSuccess ||
@@ -2236,9 +2305,14 @@ extern "C" int xc__encode_gather(xc_cache *c, uint64_t nbuf, const uint8_t *cons
         xc_plan_destroy(p);
         return fail(XC_ENOMEM, "pinned allocation failed");
     }
-    for (uint64_t i = 0; i < nbuf; i++) {
-        if (head_len[i]) memcpy(h_in + p->in_off[i], head[i], head_len[i]);
-        if (tail_len[i]) memcpy(h_in + p->in_off[i] + head_len[i], tail[i], tail_len[i]);
+    {
+        std::vector<HostCopy> cp;
+        cp.reserve(2 * nbuf);
+        for (uint64_t i = 0; i < nbuf; i++) {
+            cp.push_back({h_in + p->in_off[i], head[i], head_len[i]});
+            cp.push_back({h_in + p->in_off[i] + head_len[i], tail[i], tail_len[i]});
+        }
+        host_copies(cp);
     }
     rc = xc_encode_run_host(p, h_in, h_out, cap_total + 16, lens.data(), pos.data());
     if (!rc) rc = xc_plan_stream_results(p, rbase, rcand);

@@ -26,7 +26,7 @@ SEGMENT_LENGTH = 2048
 
 SYMBOLS = [
     "xc_device_count", "xc_ctx_create", "xc_ctx_destroy", "xc_ctx_stream", "xc_ctx_sync",
-    "xc_cache_create", "xc_cache_destroy", "xc_cache_count", "xc_cache_snapshot",
+    "xc_cache_create", "xc_cache_destroy", "xc_cache_count", "xc_cache_snapshot", "xc_cache_filter_stats",
     "xc_cache_restore", "xc_cache_lookup", "xc_cache_enter", "xc_hash_segments",
     "xc_window_hashes", "xc_encode_plan_create", "xc_plan_destroy", "xc_plan_layout",
     "xc_encode_run", "xc_encode_batch_host", "xc_plan_stats", "xc_decode_batch_host",
@@ -103,6 +103,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.xc_cache_count.argtypes = [_vp, C.POINTER(C.c_uint64)]
     lib.xc_cache_capacity.argtypes = [_vp, C.POINTER(C.c_uint64)]
     lib.xc_cache_snapshot.argtypes = [_vp]
+    lib.xc_cache_filter_stats.argtypes = [_vp, C.POINTER(C.c_double), C.POINTER(C.c_double)]
     lib.xc_cache_restore.argtypes = [_vp]
     lib.xc_cache_lookup.argtypes = [_vp, C.c_uint64, _u8p, C.POINTER(C.c_int)]
     lib.xc_cache_enter.argtypes = [_vp, C.c_uint64, _u8p]
@@ -281,6 +282,13 @@ class XCodecCache:
         seg = _as_u8(seg)
         assert seg.size == SEGMENT_LENGTH
         _check(load_library().xc_cache_enter(self.h, h, np.ascontiguousarray(seg)))
+
+    def filter_stats(self) -> dict:
+        """Diagnostic: false-positive rates of the level-1 (LDS) and level-2 (L2) filters for a
+        random window end (from the filters' word occupancy)."""
+        a, b = C.c_double(), C.c_double()
+        _check(load_library().xc_cache_filter_stats(self.h, C.byref(a), C.byref(b)))
+        return {"l1_fp": a.value, "l2_fp": b.value}
 
     def snapshot(self) -> None:
         _check(load_library().xc_cache_snapshot(self.h))
