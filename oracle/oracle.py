@@ -44,6 +44,8 @@ def _load() -> C.CDLL:
     lib.xo_cache_count.argtypes = [C.c_void_p]
     lib.xo_cache_segments.restype = C.c_size_t
     lib.xo_cache_segments.argtypes = [C.c_void_p]
+    lib.xo_cache_coss_load_misses.restype = C.c_uint64
+    lib.xo_cache_coss_load_misses.argtypes = [C.c_void_p]
     lib.xo_cache_coss_stats.restype = C.c_int
     lib.xo_cache_coss_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
     lib.xo_cache_entry.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_uint64), C.c_void_p]
@@ -142,6 +144,11 @@ class Cache:
         o = np.zeros(6, np.uint64)
         assert lib().xo_cache_coss_stats(self.h, o.ctypes.data_as(C.POINTER(C.c_uint64)))
         return dict(zip(["lookups", "found_1", "found_2", "index", "stripe_limit", "serial"], (int(x) for x in o)))
+
+    def coss_load_misses(self) -> int:
+        """(checks only) lookups that loaded a stripe and then missed (the <=16-stripe second-copy
+        state, xcodec_cache_coss.cc:200-220)."""
+        return int(lib().xo_cache_coss_load_misses(self.h))
 
     def entries(self) -> list[tuple[int, bytes]]:
         out = []

@@ -73,6 +73,7 @@ struct xo_coss {
     struct { uint64_t hash; const uint8_t *data; } window[WINDOW];
     unsigned cursor;
     uint64_t lookups, found_1, found_2;
+    uint64_t load_misses; /* (checks only) lookups that loaded a stripe and then missed */
 };
 
 /* ------------------------------------------------------------- index --- */
@@ -359,13 +360,18 @@ int xo_coss_lookup(xo_coss *c, uint64_t h, const uint8_t **data)
     int slot;
     for (slot = 0; slot < LOADED; ++slot)
         if (c->stripe[slot].h.m.stripe_range == range) break;
+    int loaded = 0;
     if (slot >= LOADED) {
+        loaded = 1;
         slot = best_unloadable_slot(c);
         detach_stripe(c, slot);
         load_stripe(c, range, slot);
     }
     stripe_t *s = &c->stripe[slot];
-    if (s->h.hash[pos] != h) return 0;
+    if (s->h.hash[pos] != h) {
+        if (loaded) c->load_misses++;
+        return 0;
+    }
     s->h.m.freshness = ++c->freshness_level;
     s->h.m.uses++;
     s->h.m.credits++;
@@ -378,6 +384,8 @@ int xo_coss_lookup(xo_coss *c, uint64_t h, const uint8_t **data)
 }
 
 size_t xo_coss_count(const xo_coss *c) { return c->icount; }
+
+uint64_t xo_coss_load_misses(const xo_coss *c) { return c->load_misses; }
 
 void xo_coss_stats(const xo_coss *c, uint64_t *out)
 {

@@ -189,6 +189,9 @@ size_t xo_cache_count(const xo_cache *c) { return c->coss ? xo_coss_count(c->cos
 size_t xo_cache_segments(const xo_cache *c) { return c->coss ? xo_coss_count(c->coss) : c->count; }
 
 /* COSSStats of a COSS cache (xcodec_cache_coss.h:179-187); 0 for the memory cache. */
+/* (checks only) lookups that loaded a stripe and then missed: the <=16-stripe second-copy state */
+uint64_t xo_cache_coss_load_misses(const xo_cache *c) { return c->coss ? xo_coss_load_misses(c->coss) : 0; }
+
 int xo_cache_coss_stats(const xo_cache *c, uint64_t *out6)
 {
     if (!c->coss) return 0;

@@ -60,6 +60,7 @@ void xo_coss_close(xo_coss *c);
 void xo_coss_enter(xo_coss *c, uint64_t h, const uint8_t *seg);
 int xo_coss_lookup(xo_coss *c, uint64_t h, const uint8_t **data);
 size_t xo_coss_count(const xo_coss *c);
+uint64_t xo_coss_load_misses(const xo_coss *c);
 void xo_coss_stats(const xo_coss *c, uint64_t *out);
 size_t xo_coss_hashes(const xo_coss *c, uint64_t *out, size_t cap);
 /* An xo_cache whose lookup / enter are the COSS cache's (the encoder and decoder take it like

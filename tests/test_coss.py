@@ -108,3 +108,19 @@ def test_store_equals_oracle(oracle_mod, tmp_path, size_mb):
         assert (da / WPC).read_bytes() == (db / WPC).read_bytes(), phase
     # purges happened: fewer segments than entered survive
     assert sum(1 for op, _ in ops if op == "enter") > len(oracle_mod.Cache.coss(str(da), UUID, size_mb))
+
+
+def test_replay_window_hash_equals_the_oracle(oracle_mod):
+    """The replay's host window hash (wanproxy_amd/csrc/xc_replay.h WindowHash, used only for the
+    lookups that miss with side effects) gives XCodecHash::mix of every window (xcodec/xcodec_hash.h):
+    random bytes with zero bytes (ffs 0) and long 0xFF runs (the 32-bit sums' shifts wrap)."""
+    import wanproxy_amd as w
+    from wanproxy_amd import xcodec as X
+    rng = np.random.default_rng(5)
+    d = rng.integers(0, 256, 9000, dtype=np.uint8)
+    d[100:400] = 0
+    d[3000:6000] = 255
+    got = X._window_hashes_host(d)
+    assert got.size == d.size - 2047
+    for i in list(range(0, 40)) + list(range(900, 1100, 7)) + list(range(2900, 6950, 97)) + [d.size - 2048]:
+        assert int(got[i]) == oracle_mod.hash_segment(d[i:i + 2048]), i

@@ -29,6 +29,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <cstring>
 #include <memory>
 #include <new>
@@ -238,6 +239,20 @@ public:
     }
 
     size_t size() const { return index_.size(); }
+
+    // (tests) the stripe headers read again from the file, as after another writer changed them:
+    // a header that disagrees with the index is the state where a lookup misses after loading the
+    // stripe (LOAD_MISS).  t: every indexed hash.
+    bool reread_headers(Touch *t)
+    {
+        const uint64_t n = std::min<uint64_t>(limit_, file_size_ / sizeof(Stripe));
+        for (uint64_t r = 0; r < n; r++)
+            if (::pread(fd_, &file_hash_[r * STRIPE_SEGS], sizeof(Header::hash),
+                        (off_t)(r * sizeof(Stripe) + offsetof(Header, hash))) != (ssize_t)sizeof(Header::hash))
+                return false;
+        all_hashes(t->hs);
+        return true;
+    }
     // Lookups the device made that missed (a miss outside the one state LOAD_MISS flags has no side
     // effect but the count): stats_.lookups counts every call (:194).
     void count_misses(uint64_t n) { lookups_ += n; }
@@ -505,14 +520,9 @@ struct xc_coss {
         return rc;
     }
     int end_pass() { return err; }
-    int unmirrorable()
-    {
-        if (err) return err;
-        if (load_miss.empty()) return XC_OK;
-        return xc__set_error(XC_EINVAL, "COSS: a stripe header in the file disagrees with the index (a cache of "
-                                        "16 stripes or fewer after a stripe's second copy was detached); "
-                                        "lookups that miss after loading a stripe are not mirrored on the device");
-    }
+    // (lookups that miss after loading a stripe are replayed from the host's window hashes:
+    // xc_replay.h add_load_miss_lookups)
+    int unmirrorable() { return err; }
 };
 
 namespace {
@@ -572,6 +582,31 @@ extern "C" int xc_coss_count(xc_coss *c, uint64_t *n)
     if (!c || !n) return xc__set_error(XC_EINVAL, "null");
     *n = c->st.size();
     return XC_OK;
+}
+
+// (tests) replay::WindowHash: out[i] = the hash of the window d[i .. i + 2047], i < n - 2047.
+extern "C" int xc__window_hashes_host(const uint8_t *d, uint64_t n, uint64_t *out)
+{
+    if (!d || !out) return xc__set_error(XC_EINVAL, "null");
+    replay::WindowHash w(d);
+    for (uint64_t p = 0; p < n; p++) {
+        w.push();
+        if (p >= SEG - 1) out[p - (SEG - 1)] = w.mix();
+    }
+    return XC_OK;
+}
+
+// (tests) Store::reread_headers, and the device mirror follows.
+extern "C" int xc__coss_reread_headers(xc_coss *c)
+{
+    if (!c) return xc__set_error(XC_EINVAL, "null");
+    try {
+        Touch t;
+        if (!c->st.reread_headers(&t)) return xc__set_error(XC_EDEVICE, "COSS: cannot read the cache file");
+        return follow(c, t);
+    } catch (const std::bad_alloc &) {
+        return xc__set_error(XC_ENOMEM, "host allocation failed");
+    }
 }
 
 extern "C" int xc_coss_stats(xc_coss *c, uint64_t *out6)

@@ -73,6 +73,7 @@ struct Change {
     std::vector<uint64_t> removed;  // no longer found
     std::vector<uint64_t> added;    // found now, or found with other bytes
     std::vector<uint8_t> bytes;     // their bytes, SEG each
+    bool new_lm = false;            // a hash became a LOAD_MISS one (a later miss of it has side effects)
     bool any() const { return !removed.empty() || !added.empty(); }
 };
 
@@ -105,7 +106,7 @@ int settle(C *c, const Touch &t, Change &ch)
         const uint8_t *p = nullptr;
         Loc l{0, 0};
         const int r = c->st.peek(h, &p, &l);
-        if (r == LOAD_MISS) c->load_miss.insert(h);
+        if (r == LOAD_MISS) ch.new_lm |= c->load_miss.insert(h).second;
         else c->load_miss.erase(h);
         if (r == IN_FILE) {
             if (!c->st.read_segment(l, buf)) return xc__set_error(XC_EDEVICE, "COSS: cannot read the cache file");
@@ -160,11 +161,12 @@ struct Watch {
 // One cache event of an encoder item, in the reference's order (xcodec_encoder.cc:72-171).
 struct EncEvent {
     uint64_t pos;       // window end of the lookup / declaration point (~0: flush's declaration)
-    int kind;           // 0 enter (EXTRACT), 1 lookup hit (REF), 2 lookup hit (collision)
+    int kind;           // 0 enter (EXTRACT), 1 lookup hit (REF), 2 lookup hit (collision),
+                        // 3 lookup miss with side effects (LOAD_MISS)
     uint64_t hash;
     uint64_t out_end;   // output bytes up to the end of this event's token (0 for a collision)
-    uint64_t base;      // source_ start after the event (REF / EXTRACT), or at it (collision)
-    int64_t cand;       // collision: the pending candidate (-1 none)
+    uint64_t base;      // source_ start after the event (REF / EXTRACT), or at it (kinds 2, 3)
+    int64_t cand;       // kinds 2, 3: the candidate pending after the lookup (-1 none)
     const uint8_t *seg; // EXTRACT payload
 };
 
@@ -193,6 +195,39 @@ inline uint64_t enc_misses(uint64_t lo, uint64_t hi, const std::vector<EncEvent>
     return calls > hits ? calls - hits : 0;
 }
 
+// XCodecHash (xcodec/xcodec_hash.h:31-174) over a sliding 2048-byte window: the hash of the window
+// ending at each byte, as the encoder's rolling hash gives it (the value depends on the window's
+// bytes only).  The device reports every lookup whose answer is a segment; the host needs the
+// hashes of lookups that miss only in the one COSS state where a miss has side effects (below).
+struct WindowHash {
+    uint32_t s1w = 0, s2w = 0, s1b = 0, s2b = 0;
+    uint64_t n = 0;
+    const uint8_t *d;
+    explicit WindowHash(const uint8_t *data) : d(data) {}
+    static uint32_t bit(uint8_t c) { return c ? (uint32_t)__builtin_ctz(c) + 1u : 0u; }  // ffs()
+    void push()  // the next byte d[n]
+    {
+        const uint8_t c = d[n];
+        if (n >= SEG) {  // roll (:57-71): the byte leaving the window
+            const uint8_t o = d[n - SEG];
+            s1w -= o + 1u;
+            s2w -= (o + 1u) * SEG;
+            s1b -= bit(o);
+            s2b -= bit(o) * SEG;
+        }
+        s1w += c + 1u;
+        s2w += s1w;
+        s1b += bit(c);
+        s2b += s1b;
+        n++;
+    }
+    uint64_t mix() const  // (:153-164: 32-bit sums and shifts)
+    {
+        const uint32_t bits = (s1b << 16) + s2b, bytes = (s1w << 20) + s2w;
+        return ((uint64_t)bits << 36) + bytes;
+    }
+};
+
 // An encoder batch item: `data` (len bytes) is an encoder's pending source_ followed by its new
 // input, window ends below `start` already looked up, candidate `cand` (or -1), encode() only when
 // `noflush`.  `off`: where data lies in the caller's item (restarts move it).
@@ -204,6 +239,67 @@ struct CItem {
     uint64_t off;
     bool noflush;
 };
+
+// The lookups of item `it` that miss with side effects (Store::peek's LOAD_MISS: a COSS index entry
+// whose stripe is not loaded and whose header in the file disagrees; xcodec_cache_coss.cc:200-220):
+// every window end the encoder looks up (from max(2047, start); not the 2047 after a REF,
+// xcodec_encoder.cc:111-127) whose hash is such a hash, as kind-3 events; then ev is sorted and each
+// kind-3 event gets the state a restart after it needs (the candidate pending after the miss, the
+// source_ start and output offset of the tokens before it).  The device treated them as the plain
+// misses they are; the Store replays their side effects.
+template <class Item>
+void add_load_miss_lookups(const std::unordered_set<uint64_t> &lm, const Item &it, std::vector<EncEvent> &ev)
+{
+    std::vector<uint64_t> refs;
+    for (const EncEvent &e : ev)
+        if (e.kind == 1) refs.push_back(e.pos);
+    std::sort(refs.begin(), refs.end());
+    uint64_t resume = std::max<uint64_t>(SEG - 1, it.start);
+    size_t ri = 0;
+    WindowHash w(it.data);
+    for (uint64_t p = 0; p < it.len; p++) {
+        w.push();
+        if (p < SEG - 1) continue;
+        while (ri < refs.size() && refs[ri] < p) resume = std::max(resume, refs[ri++] + SEG);
+        if (p < resume || (ri < refs.size() && refs[ri] == p)) continue;
+        const uint64_t h = w.mix();
+        if (lm.count(h)) ev.push_back({p, 3, h, 0, 0, -1, nullptr});
+    }
+}
+
+// After the sort: each kind-3 event's candidate (the first miss after the last REF / declaration
+// sets it, collisions do not, xcodec_encoder.cc:96-170), source_ start and output offset.
+inline void load_miss_state(std::vector<EncEvent> &ev, int64_t cand, uint64_t start)
+{
+    uint64_t a = std::max<uint64_t>(SEG - 1, start), base = 0, oe = 0;  // a: the next lookup
+    for (EncEvent &e : ev) {
+        if (e.pos == ~0ull) break;
+        if (cand < 0 && a < e.pos) cand = (int64_t)(a - (SEG - 1));  // a miss before this event
+        switch (e.kind) {
+        case 0:  // a declaration at e.pos, whose own lookup follows
+            cand = -1;
+            a = e.pos;
+            base = e.base;
+            oe = e.out_end;
+            break;
+        case 1:  // REF: the hash restarts
+            cand = -1;
+            a = e.pos + SEG;
+            base = e.base;
+            oe = e.out_end;
+            break;
+        case 2:  // a collision is no candidate
+            if (cand < 0) a = e.pos + 1;
+            break;
+        default:  // a miss
+            if (cand < 0) cand = (int64_t)(e.pos - (SEG - 1));
+            a = e.pos + 1;
+            e.cand = cand;
+            e.base = base;
+            e.out_end = oe;
+        }
+    }
+}
 
 // The batch on the device, its cache events replayed into the Store in the reference's order
 // (items in order), restarting the rest after a change a later event depends on.  Outputs append
@@ -277,10 +373,13 @@ int encode(C *c, std::vector<CItem> items, uint8_t *out, const uint64_t *out_off
                 ev[k].push_back({q, 2, ((uint64_t)r[2] << 32) | r[1], oe, base,
                                  r[3] == 0xFFFFFFFFu ? -1 : (int64_t)r[3], nullptr});
             }
+            const bool lm = !c->load_miss.empty();
+            if (lm) add_load_miss_lookups(c->load_miss, items[k], ev[k]);
             // (a declaration precedes the lookup at the same position; flush's comes last)
             std::stable_sort(ev[k].begin(), ev[k].end(), [](const EncEvent &a, const EncEvent &b) {
                 return a.pos != b.pos ? a.pos < b.pos : a.kind < b.kind;
             });
+            if (lm) load_miss_state(ev[k], items[k].cand, items[k].start);
         }
         // EXTRACT hashes (XCodecHash::hash of the payloads) on the device, one call
         std::vector<uint64_t> ph(payloads.size());
@@ -323,14 +422,18 @@ int encode(C *c, std::vector<CItem> items, uint8_t *out, const uint64_t *out_off
                     c->st.enter(E.hash, E.seg, &t);
                     c->entered(E.hash, E.seg);
                     entered++;
+                } else if (E.kind == 3) {
+                    if (c->st.lookup(E.hash, &t))
+                        return xc__set_error(XC_EDEVICE, "cache replay: a device miss the store finds");
                 } else if (!c->st.lookup(E.hash, &t)) {
                     return xc__set_error(XC_EDEVICE, "cache replay: a device hit the store does not find");
                 }
                 Change ch;
                 if ((rc = settle(c, t, ch))) return rc;
-                if (!ch.any()) continue;
-                // a segment found now that was not: any lookup after this event may differ
-                bool dep = !ch.added.empty();
+                if (!ch.any() && !ch.new_lm) continue;
+                // a segment found now that was not, or a miss that now has side effects: any lookup
+                // after this event may differ
+                bool dep = !ch.added.empty() || ch.new_lm;
                 if (!dep) {
                     const Watch w(ch);
                     for (uint64_t k2 = k; k2 < m && !dep; k2++)
@@ -371,7 +474,7 @@ int encode(C *c, std::vector<CItem> items, uint8_t *out, const uint64_t *out_off
                     } else if (E.kind == 1) {  // after a REF: a fresh stream
                         r.start = 0;
                         r.cand = -1;
-                    } else {  // after a collision: same source_, candidate carried
+                    } else {  // after a collision / a miss: same source_, candidate carried
                         r.start = E.pos + 1 - E.base;
                         r.cand = E.cand >= 0 ? E.cand - (int64_t)E.base : -1;
                     }
@@ -508,10 +611,10 @@ int decode(C *c, const uint8_t *in, const uint64_t *in_off, const uint64_t *in_l
                 }
                 Change ch;
                 if ((rc = settle(c, t, ch))) return rc;
-                if (!ch.any()) continue;
+                if (!ch.any() && !ch.new_lm) continue;
                 // later tokens, and the unknown REF a later stream stopped on, that saw the change
                 const Watch w(ch);
-                bool dep = false;
+                bool dep = ch.new_lm;
                 for (uint64_t k2 = k; k2 < m && !dep; k2++) {
                     for (size_t e2 = (k2 == k ? e + 1 : 0); e2 < ev[k2].size() && !dep; e2++)
                         dep = w.has(ev[k2][e2].hash);
@@ -534,13 +637,38 @@ int decode(C *c, const uint8_t *in, const uint64_t *in_off, const uint64_t *in_l
                 break;
             }
             if (!redo) {
-                if (hu[k]) c->st.count_misses(1);  // (the unknown REF's lookup, :150)
                 std::memcpy(out + out_off[it.buf] + out_len[it.buf], &obuf[ooff[k]], olen[k]);
                 out_len[it.buf] += olen[k];
                 consumed[it.buf] = it.from + cons[k];
                 status[it.buf] = st[k];
                 unknown[it.buf] = unk[k];
                 has_unknown[it.buf] = hu[k];
+                if (hu[k]) {  // the unknown REF's lookup (:150): a miss, with side effects in one state
+                    Touch t;
+                    if (c->st.lookup(unk[k], &t))
+                        return xc__set_error(XC_EDEVICE, "cache replay: a device miss the store finds");
+                    Change ch;
+                    if ((rc = settle(c, t, ch))) return rc;
+                    if (ch.any() || ch.new_lm) {
+                        const Watch w(ch);
+                        bool dep = ch.new_lm;
+                        for (uint64_t k2 = k + 1; k2 < m && !dep; k2++) {
+                            for (size_t e2 = 0; e2 < ev[k2].size() && !dep; e2++) dep = w.has(ev[k2][e2].hash);
+                            if (hu[k2] && w.has(unk[k2])) dep = true;
+                        }
+                        if (!dep) {
+                            held.push_back(std::move(ch));
+                        } else {  // stream k is done; the later ones run again
+                            if ((rc = xc__cache_truncate(c->cache, count0 + entered))) return rc;
+                            for (const Change &h : held)
+                                if ((rc = mirror(c, h))) return rc;
+                            held.clear();
+                            if ((rc = mirror(c, ch))) return rc;
+                            for (uint64_t k2 = k + 1; k2 < m; k2++) next.push_back(items[k2]);
+                            redo = true;
+                        }
+                    }
+                }
             }
         }
         for (const Change &h : held)

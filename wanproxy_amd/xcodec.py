@@ -353,6 +353,13 @@ class CossCache:
         fn = load_library().xc_coss_store_enter if store_only else load_library().xc_coss_enter
         _check(fn(self.h, h, seg))
 
+    def _reread_headers(self) -> None:
+        """(tests) the stripe headers read again from the file, as after another writer changed
+        them; the device mirror follows (xc__coss_reread_headers)."""
+        lib = load_library()
+        lib.xc__coss_reread_headers.argtypes = [_vp]
+        _check(lib.xc__coss_reread_headers(self.h))
+
     def close(self) -> None:
         """~XCodecCacheCOSS: the loaded stripes are written back."""
         if getattr(self, "h", None):
@@ -364,6 +371,17 @@ class CossCache:
             self.close()
         except Exception:
             pass
+
+
+def _window_hashes_host(data) -> np.ndarray:
+    """(tests) the replay's host window hash (xc_replay.h WindowHash): the hash of every 2048-byte
+    window of ``data``, in order."""
+    d = np.ascontiguousarray(_as_u8(data))
+    out = np.zeros(max(0, d.size - SEGMENT_LENGTH + 1), np.uint64)
+    lib = load_library()
+    lib.xc__window_hashes_host.argtypes = [_u8p, C.c_uint64, _u64p]
+    _check(lib.xc__window_hashes_host(d, d.size, out))
+    return out
 
 
 class XCodecEncoder:
