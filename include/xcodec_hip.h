@@ -53,8 +53,10 @@ int xc_ctx_sync(xc_ctx *ctx);
 /* XCodecMemoryCache(UUID, size) (xcodec/xcodec_cache.h:169-172), device resident.
  * cap_segments is the initial capacity.  Like the reference's map, which is unbounded
  * (xcodec/xcodec_cache.h:164,182-188), the cache grows before any call that could fill it (its
- * tables are rebuilt into larger arrays; snapshots stay valid), up to 2^25 segments (64 GiB of
- * segment store) or the device's memory; only past that does a call fail with XC_ENOSPC. */
+ * tables are rebuilt into larger arrays; snapshots stay valid).  Segment bytes fill 2^25 slots of
+ * HBM (64 GiB) and then spill to pinned host memory (read by the device over PCIe when a lookup
+ * hits them); the tables stay on the device up to 2^28 segments (512 GiB of segments).  Only past
+ * that, or when host memory for the spill tier runs out, does a call fail (XC_ENOSPC / XC_ENOMEM). */
 int xc_cache_create(xc_ctx *ctx, uint64_t cap_segments, xc_cache **out);
 /* Current capacity in segments (grows on demand). */
 int xc_cache_capacity(xc_cache *c, uint64_t *cap);

@@ -1,0 +1,9 @@
+# round-3: spill tier tests, the GPU suite, the bench line
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+out=gpurun_out/${1:-r3i}
+mkdir -p $out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_spill.py -x -v --timeout 200 --timeout-method thread > $out/spill.log 2>&1 || { echo "spill rc $?"; tail -60 $out/spill.log; exit 1; }
+tail -2 $out/spill.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $out/tests_all.log 2>&1 || { echo "all rc $?"; tail -40 $out/tests_all.log; exit 1; }
+tail -2 $out/tests_all.log
+timeout -k 10 300 python bench.py --no-cpu > $out/bench.json 2> $out/bench.err; echo "bench rc $?"; tail -1 $out/bench.json | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['kernel_ms_per_step'], d.get('decode',{}).get('value'), {k: v['value'] for k, v in d.get('other_configs', {}).items()}, d.get('e2e_host_gibs'))"

@@ -54,7 +54,7 @@ struct DecDev {
     uint64_t *out_len, *consumed, *unknown;
     int32_t *status, *has_unknown;
     DevSet cache;
-    uint8_t *segs;
+    SegStore segs;
     uint32_t *seg_count;
     uint32_t seg_cap;
     uint2 *undo;
@@ -319,7 +319,7 @@ __global__ __launch_bounds__(64) void k_dres1(DecDev D)
             // a cached hash: its payload against the cached segment, wave-wide (rare)
             for (uint64_t mh = ballot(hit); mh; mh &= mh - 1) {
                 const int fh = __ffsll((unsigned long long)mh) - 1;
-                const bool eq = wave_equal2048(s + readlane(le, fh) + 2u, D.segs + dreadlane64(v, fh) * XC_SEG);
+                const bool eq = wave_equal2048(s + readlane(le, fh) + 2u, seg_at(D.segs, dreadlane64(v, fh)));
                 if ((int)l == fh) st = eq ? R_OKCACHE : R_COLL;
             }
             if (ex) {
@@ -343,7 +343,7 @@ __global__ __launch_bounds__(64) void k_dres1(DecDev D)
         uint64_t v;
         uint32_t st;
         if (set_find(D.cache, h, &v)) {
-            st = wave_equal2048(pay, D.segs + v * XC_SEG) ? R_OKCACHE : R_COLL;
+            st = wave_equal2048(pay, seg_at(D.segs, v)) ? R_OKCACHE : R_COLL;
         } else {
             st = R_PENDING;
             if (lane_id() == 0 && t < lim) set_insert(D.dset, h, ((uint64_t)j << 32) | t, true, nullptr, nullptr);
@@ -631,7 +631,7 @@ __global__ __launch_bounds__(64 * DEMIT_WAVES) void k_demit(DecDev D)
                     from = (uint64_t)(uintptr_t)(s + le + 2u);
                     if (D.t_stat[tb + t] == R_ENTER) {
                         const uint32_t idx = D.s_slot[j] + (uint32_t)D.t_src[tb + t];
-                        if (idx < D.seg_cap) seg = (uint64_t)(uintptr_t)(D.segs + (size_t)idx * XC_SEG);
+                        if (idx < D.seg_cap) seg = (uint64_t)(uintptr_t)seg_at(D.segs, idx);
                     }
                 } else if (op == T_REF) {
                     const uint64_t src = D.t_src[tb + t];
@@ -639,7 +639,7 @@ __global__ __launch_bounds__(64 * DEMIT_WAVES) void k_demit(DecDev D)
                         const uint32_t pj = (uint32_t)((src >> 32) & 0x7FFFFFFFu), pt = (uint32_t)src;
                         from = (uint64_t)(uintptr_t)(D.in + D.in_off[pj] + D.t_le[D.tok_base[pj] + pt] + 2u);
                     } else {
-                        from = (uint64_t)(uintptr_t)(D.segs + src * XC_SEG);
+                        from = (uint64_t)(uintptr_t)seg_at(D.segs, src);
                     }
                 }
             }
@@ -771,7 +771,7 @@ extern "C" int64_t xc__cache_host_count(xc_cache *c);
 extern "C" void xc__cache_set_host_count(xc_cache *c, int64_t n);
 extern "C" int xc__cache_reserve(xc_cache *c, uint64_t extra);
 extern "C" uint32_t xc__cache_gen(xc_cache *c);
-extern "C" int xc__cache_devset(xc_cache *c, void *devset, uint8_t **segs, uint32_t **count, uint32_t *cap,
+extern "C" int xc__cache_devset(xc_cache *c, void *devset, SegStore *segs, uint32_t **count, uint32_t *cap,
                                 uint2 **undo, void **stream, int *dev);
 extern "C" int xc__set_error(int code, const char *msg);
 extern "C" hipError_t xc__spin_wait(hipEvent_t ev);

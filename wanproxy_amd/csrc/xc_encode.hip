@@ -468,7 +468,7 @@ __device__ __forceinline__ uint32_t resolve_one(const PlanDev &P, int dmode, uin
     uint64_t v = 0;
     if (dmode != 1 && set_find(P.cache, h, &v)) {
         *val_out = v;
-        return wave_equal2048(win, P.segs + v * XC_SEG) ? ST_EQUAL : ST_COLL;
+        return wave_equal2048(win, seg_at(P.segs, v)) ? ST_EQUAL : ST_COLL;
     }
     if (dmode != 0 && set_find(P.dset, h, &v)) {
         *val_out = v;
@@ -564,7 +564,7 @@ __global__ __launch_bounds__(64 * RES_WAVES) void k_resolve(ResolveArgs a)
                 const uint8_t *wp = base + qf - (XC_SEG - 1u) + 32u * l;
                 if (((qf + 1u) & (XC_SEG - 1u)) == 0u) load32_aligned(wp, x[g]);  // a block: 2 x 16 B
                 else load32_unaligned(wp, x[g]);
-                const uint4 *sp = (const uint4 *)(P.segs + vf * XC_SEG + 32u * l);
+                const uint4 *sp = (const uint4 *)(seg_at(P.segs, vf) + 32u * l);
                 const uint4 s0 = sp[0], s1 = sp[1];
                 y[g][0] = s0.x; y[g][1] = s0.y; y[g][2] = s0.z; y[g][3] = s0.w;
                 y[g][4] = s1.x; y[g][5] = s1.y; y[g][6] = s1.z; y[g][7] = s1.w;
@@ -1127,7 +1127,7 @@ __global__ __launch_bounds__(256) void k_blockhash(DeclArgs a)
             for (int i = 0; i < 4; i++) {
                 slot[i] = readlane(cmp, g0 + i);
                 if (slot[i]) {
-                    const uint4 *yp = (const uint4 *)(P.segs + (size_t)(slot[i] - 1u) * XC_SEG + 32u * l);
+                    const uint4 *yp = (const uint4 *)(seg_at(P.segs, slot[i] - 1u) + 32u * l);
                     y[i][0] = yp[0];
                     y[i][1] = yp[1];
                 }
@@ -1423,7 +1423,7 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
             }
 #pragma unroll
             for (int g = 0; g < EMIT_PAY; g++)
-                if (f[g] >= 0) payload_store(d[g], ii[g] < P.seg_cap ? P.segs + (size_t)ii[g] * XC_SEG : nullptr, r[g]);
+                if (f[g] >= 0) payload_store(d[g], ii[g] < P.seg_cap ? seg_at(P.segs, ii[g]) : nullptr, r[g]);
         }
     }
 }
@@ -1761,11 +1761,11 @@ __global__ void k_enter_one(PlanDev P, uint64_t h, const uint8_t *seg)
     }
     uint64_t v;
     if (set_find(P.cache, h, &v)) {  // release-build XCodecMemoryCache::enter overwrites
-        wave_copy(P.segs + v * XC_SEG, seg, XC_SEG);
+        wave_copy(seg_at(P.segs, v), seg, XC_SEG);
         return;
     }
     const uint32_t idx = uniform(P.seg_count[0]);
-    wave_copy(P.segs + (size_t)idx * XC_SEG, seg, XC_SEG);
+    wave_copy(seg_at(P.segs, idx), seg, XC_SEG);
     if (lane_id() == 0) {
         uint32_t s1, s2;
         set_insert(P.cache, h, idx, false, &s1, &s2);
@@ -1781,7 +1781,7 @@ __global__ void k_enter_bulk(PlanDev P, const uint64_t *h, const uint8_t *segs, 
     const uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6);
     if (i >= n) return;
     const uint32_t idx = first + i;
-    wave_copy(P.segs + (size_t)idx * XC_SEG, segs + (size_t)i * XC_SEG, XC_SEG);
+    wave_copy(seg_at(P.segs, idx), segs + (size_t)i * XC_SEG, XC_SEG);
     if (lane_id() == 0) {
         uint32_t s1, s2;
         set_insert(P.cache, h[i], idx, false, &s1, &s2);
@@ -1864,7 +1864,7 @@ __global__ void k_lookup_one(PlanDev P, uint64_t h, uint8_t *out, uint32_t *foun
 {
     uint64_t v;
     if (set_find(P.cache, h, &v)) {
-        wave_copy(out, P.segs + v * XC_SEG, XC_SEG);
+        wave_copy(out, seg_at(P.segs, v), XC_SEG);
         if (lane_id() == 0) *found = 1u;
     } else if (lane_id() == 0) {
         *found = 0u;

@@ -60,6 +60,24 @@ struct Layer {
     uint32_t *bits;  // [nchunks * chunk_len/32]
 };
 
+// The segment store: slots below dev_cap in HBM; the rest, the spill tier of a cache grown past the
+// device's share, in pinned host memory mapped into the device's address space, chunks of
+// 2^SPILL_SHIFT slots (host[k]: chunk k's device address).  Segments are written once (enter) and
+// read by the compares of lookups that hit them, so spilled ones cost PCIe reads, not failures.
+constexpr uint32_t SPILL_SHIFT = 16;
+struct SegStore {
+    uint8_t *dev;
+    uint8_t *const *host;
+    uint32_t dev_cap;
+};
+
+__device__ __forceinline__ uint8_t *seg_at(const SegStore &s, uint64_t i)
+{
+    if (i < s.dev_cap) return s.dev + i * XC_SEG;
+    const uint64_t r = i - s.dev_cap;
+    return s.host[r >> SPILL_SHIFT] + (r & ((1u << SPILL_SHIFT) - 1u)) * XC_SEG;
+}
+
 struct PlanDev {
     const uint8_t *in;
     const uint64_t *buf_off;
@@ -71,7 +89,7 @@ struct PlanDev {
     uint32_t chunk_len;
     Layer S, D;
     DevSet cache;
-    uint8_t *segs;
+    SegStore segs;
     uint32_t *seg_count;
     uint32_t seg_cap;
     uint2 *undo;               // [seg_cap] (full slot, lo slot) of every enter()

@@ -332,15 +332,20 @@ constexpr int XC__SLOW = -1000;
 
 struct xc_cache {
     xc_ctx *ctx;
-    uint64_t cap;
+    uint64_t cap;      // segment slots (the tables are sized for them)
     HostSet set;
-    uint8_t *segs;
+    uint8_t *segs;     // device: the first dev_cap slots
+    uint64_t dev_cap = 0;
+    uint64_t dev_limit = 0;           // the device's share of the slots (SEG_DEV_MAX; a test hook lowers it)
+    std::vector<uint8_t *> spill;     // the spill tier: pinned host chunks of 2^SPILL_SHIFT slots
+    uint8_t **d_spill = nullptr;      // device: their device addresses
     uint32_t *count;   // device
     uint2 *undo;       // device [cap]
     uint32_t *ctl;     // device scratch ctl for single-op kernels
     // snapshot
     bool has_snap = false;
     uint32_t snap_count = 0;
+    uint32_t snap_gen = 0;  // gen at the snapshot: a rebuild since re-placed its keys
     uint32_t *snap_filt = nullptr;
     uint32_t *snap_lo_zero = nullptr;
     uint32_t *snap_count_dev = nullptr;
@@ -375,8 +380,61 @@ static int cache_busy(const xc_cache *c, const void *owner = nullptr)
 
 // The reference's memory cache is unbounded (xcodec/xcodec_cache.h:164,182-188).  The device cache
 // starts at the capacity it was created with and grows (cache_reserve) before any run that could
-// exceed it, up to CAP_MAX segments (64 GiB of segment store) or device memory.
-static const uint64_t CAP_MAX = 1ull << 25;
+// exceed it.  Its tables (keys, lo32 set, undo log) stay in HBM for up to CAP_MAX segments; the
+// segment bytes fill SEG_DEV_MAX slots of HBM (64 GiB) and then spill to pinned host memory
+// (SegStore, xc_kernels.h), so a cache outgrows the device's share instead of failing.
+static const uint64_t CAP_MAX = 1ull << 28;      // 512 GiB of segments: tables of ~12 GB
+static const uint64_t SEG_DEV_MAX = 1ull << 25;  // segment slots in HBM
+static const uint64_t SPILL_CHUNK = 1ull << SPILL_SHIFT;
+
+static SegStore cache_segstore(const xc_cache *c)
+{
+    return SegStore{c->segs, c->d_spill, (uint32_t)c->dev_cap};
+}
+
+// Spill chunks for every slot from `base` (the device part's size: it never changes once chunks
+// exist) up to ncap (pinned, mapped into the device's address space; device addresses in d_spill).
+static int cache_spill_to(xc_cache *c, uint64_t base, uint64_t ncap)
+{
+    if (!c->spill.empty() && base != c->dev_cap) return fail(XC_EDEVICE, "spill tier moved");
+    const uint64_t need = ncap > base ? (ncap - base + SPILL_CHUNK - 1) / SPILL_CHUNK : 0;
+    if (need <= c->spill.size()) return XC_OK;
+    if (!c->d_spill && dmalloc(&c->d_spill, (size_t)(CAP_MAX / SPILL_CHUNK) * sizeof(uint8_t *)) != hipSuccess)
+        return fail(XC_ENOMEM, "device allocation failed");
+    std::vector<uint8_t *> dptr;
+    for (uint64_t k = c->spill.size(); k < need; k++) {
+        void *h = nullptr, *d = nullptr;
+        if (hipHostMalloc(&h, SPILL_CHUNK * XC_SEG + 4096, hipHostMallocMapped) != hipSuccess)
+            return fail(XC_ENOMEM, "host memory for the cache's spill tier exhausted");
+        if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+            hipHostFree(h);
+            return fail(XC_EDEVICE, "spill chunk not mapped");
+        }
+        c->spill.push_back((uint8_t *)h);
+        dptr.push_back((uint8_t *)d);
+    }
+    const size_t k0 = c->spill.size() - dptr.size();
+    HIPCHK(hipMemcpy(c->d_spill + k0, dptr.data(), dptr.size() * sizeof(uint8_t *), hipMemcpyHostToDevice));
+    return XC_OK;
+}
+
+// (tests) The device's share of the segment slots: later growth spills past max(n, the current
+// device part) to host memory.
+extern "C" int xc__cache_set_dev_limit(xc_cache *c, uint64_t n)
+{
+    if (!c || n == 0) return fail(XC_EINVAL, "bad device limit");
+    c->dev_limit = std::min<uint64_t>(n, SEG_DEV_MAX);
+    return XC_OK;
+}
+
+// (tests) The segment slots in HBM and in the spill tier.
+extern "C" int xc__cache_tiers(xc_cache *c, uint64_t *dev_slots, uint64_t *spill_slots)
+{
+    if (!c || !dev_slots || !spill_slots) return fail(XC_EINVAL, "null");
+    *dev_slots = c->dev_cap;
+    *spill_slots = c->spill.size() * SPILL_CHUNK;
+    return XC_OK;
+}
 
 extern "C" void xc__cache_count_unknown(xc_cache *c)
 {
@@ -393,7 +451,7 @@ static PlanDev cache_plandev(xc_cache *c)
 {
     PlanDev P{};
     P.cache = c->set.d;
-    P.segs = c->segs;
+    P.segs = cache_segstore(c);
     P.seg_count = c->count;
     P.seg_cap = (uint32_t)c->cap;
     P.undo = c->undo;
@@ -409,8 +467,11 @@ extern "C" int xc_cache_create(xc_ctx *ctx, uint64_t cap, xc_cache **out)
     xc_cache *c = new xc_cache();
     c->ctx = ctx;
     c->cap = cap;
+    c->dev_limit = SEG_DEV_MAX;
+    c->dev_cap = std::min(cap, c->dev_limit);
     if ((rc = c->set.alloc(cap))) return rc;
-    HIPCHK(dmalloc(&c->segs, (size_t)cap * XC_SEG + 4096));
+    HIPCHK(dmalloc(&c->segs, (size_t)c->dev_cap * XC_SEG + 4096));
+    if ((rc = cache_spill_to(c, c->dev_cap, cap))) return rc;
     HIPCHK(dmalloc(&c->count, 4));
     HIPCHK(dmalloc(&c->undo, (size_t)cap * sizeof(uint2)));
     HIPCHK(dmalloc(&c->ctl, CTL_WORDS * 4));
@@ -448,6 +509,8 @@ extern "C" int xc_cache_destroy(xc_cache *c)
     hipDeviceSynchronize();  // pooled memory is reused at once: every stream must be done with it
     c->set.release();
     dfree(c->segs);
+    for (uint8_t *h : c->spill) hipHostFree(h);
+    dfree(c->d_spill);
     dfree(c->count);
     dfree(c->undo);
     dfree(c->ctl);
@@ -481,13 +544,16 @@ static int cache_rebuild(xc_cache *c, uint64_t ncap, uint32_t keep, bool drop_de
     if (rc) return rc;
     count = std::min<uint32_t>(count, (uint32_t)c->cap);
     const uint32_t kept = std::min(count, keep);
-    const bool move_segs = ncap != c->cap;
+    // the device part of the segment store grows up to the device's share, the spill tier after it
+    const uint64_t ndev = std::max(c->dev_cap, std::min(ncap, c->dev_limit));
+    const bool move_segs = ndev != c->dev_cap;
+    if (ncap > ndev && (rc = cache_spill_to(c, ndev, ncap))) return rc;
     HostSet ns;
     uint8_t *segs = nullptr;
     uint2 *undo = nullptr;
     uint32_t *owner = nullptr;
     if ((rc = ns.alloc(ncap))) return rc;
-    if ((move_segs && dmalloc(&segs, (size_t)ncap * XC_SEG + 4096) != hipSuccess) ||
+    if ((move_segs && dmalloc(&segs, (size_t)ndev * XC_SEG + 4096) != hipSuccess) ||
         dmalloc(&undo, (size_t)ncap * sizeof(uint2)) != hipSuccess || dmalloc(&owner, (size_t)ns.n_lo * 4) != hipSuccess) {
         ns.release();
         dfree(segs);
@@ -502,7 +568,9 @@ static int cache_rebuild(xc_cache *c, uint64_t ncap, uint32_t keep, bool drop_de
     HIPCHK(hipMemsetAsync(ns.d.vals, 0xFF, (size_t)ns.n_full * 8, s));
     HIPCHK(hipMemsetAsync(undo, 0xFF, (size_t)ncap * sizeof(uint2), s));
     HIPCHK(hipMemsetAsync(owner, 0xFF, (size_t)ns.n_lo * 4, s));
-    if (move_segs && kept) HIPCHK(hipMemcpyAsync(segs, c->segs, (size_t)kept * XC_SEG, hipMemcpyDeviceToDevice, s));
+    if (move_segs && kept)
+        HIPCHK(hipMemcpyAsync(segs, c->segs, (size_t)std::min<uint64_t>(kept, c->dev_cap) * XC_SEG,
+                              hipMemcpyDeviceToDevice, s));
     const uint32_t blocks = std::min<uint32_t>((c->set.n_full + 255) / 256, 8192);
     hipLaunchKernelGGL(k_rehash, dim3(blocks), dim3(256), 0, s, c->set.d, ns.d, undo, owner, keep, (int)drop_dead);
     HIPCHK(hipGetLastError());
@@ -517,6 +585,7 @@ static int cache_rebuild(xc_cache *c, uint64_t ncap, uint32_t keep, bool drop_de
     if (move_segs) {
         dfree(c->segs);
         c->segs = segs;
+        c->dev_cap = ndev;
     }
     dfree(c->undo);
     dfree(owner);
@@ -531,7 +600,7 @@ static int cache_rebuild(xc_cache *c, uint64_t ncap, uint32_t keep, bool drop_de
 // Move the cache into arrays for `need` segments (or twice the capacity).
 static int cache_grow(xc_cache *c, uint64_t need)
 {
-    if (need > CAP_MAX) return fail(XC_ENOSPC, "device cache capacity exhausted (2^25 segments)");
+    if (need > CAP_MAX) return fail(XC_ENOSPC, "cache capacity exhausted (2^28 segments)");
     const uint64_t ncap = std::min<uint64_t>(CAP_MAX, std::max<uint64_t>(need + need / 4, 2 * c->cap));
     return cache_rebuild(c, ncap, 0xFFFFFFFFu, false);
 }
@@ -665,6 +734,26 @@ extern "C" int xc_cache_snapshot(xc_cache *c)
     HIPCHK(hipMemcpyAsync(c->snap_l2, c->set.d.l2, (size_t)XC_L2_WORDS * 8, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipStreamSynchronize(s));
     c->has_snap = true;
+    c->snap_gen = c->gen;
+    return XC_OK;
+}
+
+// A restore across a rebuild (the cache grew since the snapshot): the rebuild inserted every key
+// in parallel, so a key entered after the snapshot can sit before an older one on its probe chain,
+// and clearing it (the undo log) would cut the chain.  The tables are rebuilt again from the
+// snapshot's entries instead, and take the snapshot's filters; later restores use the undo log.
+static int cache_restore_rebuilt(xc_cache *c)
+{
+    int rc = cache_rebuild(c, c->cap, c->snap_count, false);
+    if (rc) return rc;
+    hipStream_t s = c->ctx->stream;
+    HIPCHK(hipMemcpyAsync(c->set.d.filt, c->snap_filt, XC_FILT_WORDS * 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->set.d.lo_zero, c->snap_lo_zero, 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->set.d.l2, c->snap_l2, (size_t)XC_L2_WORDS * 8, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->count, &c->snap_count, 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+    c->snap_gen = c->gen;
+    c->host_count = c->snap_count;
     return XC_OK;
 }
 
@@ -706,6 +795,7 @@ extern "C" int xc_cache_restore_async(xc_cache *c)
         xc_cache *c;
         ~MemAfter() { mem_restore(c); }
     } mem_after{c};
+    if (c->gen != c->snap_gen) return cache_restore_rebuilt(c);
     hipStream_t s = c->ctx->stream;
     if (c->host_count >= 0) {
         // one kernel: table slots entered since the snapshot, filters and count from the snapshot
@@ -738,6 +828,10 @@ extern "C" int xc_cache_restore(xc_cache *c)
     int rc = set_dev(c->ctx);
     if (!rc) rc = cache_busy(c);
     if (rc) return rc;
+    if (c->gen != c->snap_gen) {
+        if ((rc = cache_restore_rebuilt(c))) return rc;
+        return mem_restore(c);
+    }
     uint32_t cur = 0;
     if ((rc = cache_count_host(c, &cur))) return rc;
     if ((rc = cache_restore_async(c, cur))) return rc;
@@ -2350,12 +2444,12 @@ extern "C" int xc_encode_batch_host(xc_cache *c, const uint8_t *in, const uint64
 }
 
 // Internal accessors for xc_decode.hip (not part of the public header).
-extern "C" int xc__cache_devset(xc_cache *c, void *devset, uint8_t **segs, uint32_t **count, uint32_t *cap,
+extern "C" int xc__cache_devset(xc_cache *c, void *devset, SegStore *segs, uint32_t **count, uint32_t *cap,
                                 uint2 **undo, void **stream, int *dev)
 {
     if (!c) return fail(XC_EINVAL, "null");
     *(DevSet *)devset = c->set.d;
-    *segs = c->segs;
+    *segs = cache_segstore(c);
     *count = c->count;
     *cap = (uint32_t)c->cap;
     *undo = c->undo;

@@ -272,6 +272,21 @@ class XCodecCache:
         _check(load_library().xc_cache_capacity(self.h, C.byref(n)))
         return n.value
 
+    def _set_device_limit(self, slots: int) -> None:
+        """(tests) The device's share of the segment slots: growth past it spills the segment
+        bytes to pinned host memory (xc__cache_set_dev_limit)."""
+        lib = load_library()
+        lib.xc__cache_set_dev_limit.argtypes = [_vp, C.c_uint64]
+        _check(lib.xc__cache_set_dev_limit(self.h, slots))
+
+    def _tiers(self) -> tuple[int, int]:
+        """(tests) Segment slots in HBM and in the spill tier."""
+        lib = load_library()
+        lib.xc__cache_tiers.argtypes = [_vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        a, b = C.c_uint64(), C.c_uint64()
+        _check(lib.xc__cache_tiers(self.h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
     def lookup(self, h: int) -> bytes | None:
         out = np.zeros(SEGMENT_LENGTH, np.uint8)
         found = C.c_int(0)
