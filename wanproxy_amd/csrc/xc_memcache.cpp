@@ -46,7 +46,9 @@ public:
         int32_t v;
     } win[WINDOW];
     uint32_t cursor = 0;
-    std::unordered_map<uint64_t, uint32_t> widx;  // non-zero hash -> its window slot (one at most)
+    // non-zero window hashes per bucket (h & 4095): a run's hits are replayed here one by one (half
+    // a million per cfg5 step on the host path), and almost none is in the window
+    uint8_t wcnt[4096] = {};
     // hashes entered again with other bytes: every version (ver[0] the first), cur = the map's
     struct Dup {
         std::vector<std::vector<uint8_t>> ver;
@@ -73,8 +75,10 @@ public:
                 if (win[i].h == 0) return win[i].v >= 0 ? i : -1;
             return -1;
         }
-        auto it = widx.find(h);
-        return it == widx.end() ? -1 : (int)it->second;
+        if (!wcnt[h & 4095u]) return -1;
+        for (int i = 0; i < WINDOW; i++)  // (a hash is in the window once at most)
+            if (win[i].h == h && win[i].v >= 0) return i;
+        return -1;
     }
 
     const uint8_t *bytes(uint64_t h, int32_t v) const
@@ -96,12 +100,11 @@ public:
     {
         Win &w = win[cursor];
         if (w.v >= 0 && w.h) {
-            auto it = widx.find(w.h);
-            if (it != widx.end() && it->second == cursor) widx.erase(it);
+            wcnt[w.h & 4095u]--;
             if (t && dups.count(w.h)) t->hs.push_back(w.h);
         }
         w = {h, v};
-        if (h) widx[h] = cursor;
+        if (h) wcnt[h & 4095u]++;
         cursor = (cursor + 1) & (WINDOW - 1);
     }
 
