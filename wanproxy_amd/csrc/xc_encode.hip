@@ -1164,7 +1164,7 @@ __device__ __forceinline__ uint32_t block_predict(const PlanDev &P, uint32_t g, 
     uint64_t v;
     if (stream_carried(P, b)) {
     } else if (set_find(P.cache, h, &v)) {
-        pref = (uint32_t)v + 1u;  // (cache capacity <= 2^23)
+        pref = (uint32_t)v + 1u;  // (cache capacity <= 2^28: bit 31 stays free)
     } else {
         // (the set's level-2 filter is P.l2mix, the combined filter the scan reads)
         uint32_t slot;
