@@ -421,7 +421,8 @@ def main():
                   "out_over_in": round(out_bytes / in_bytes_rank, 4),
                   "sub_batches": int(st.sub_batches), "outer_rounds": int(st.outer_rounds),
                   "walk_rounds": int(st.walk_rounds), "dense_chunks": int(st.dense_chunks),
-                  "redone": int(st.redone), "shadow_misses": int(st.shadow_misses)},
+                  "redone": int(st.redone), "shadow_misses": int(st.shadow_misses),
+                  "anchor_scans": int(st.anchor_scans), "anchor_fallbacks": int(st.anchor_fallbacks)},
         "verified_buffers": verified_job,
         "verified_against": ver["verified_against"] if world == 1 else
         f"oracle digests cfg5_g{world}_r* (every rank, every buffer of its shard)" if case else "oracle run",

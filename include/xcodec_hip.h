@@ -175,8 +175,21 @@ typedef struct {
     uint32_t sub_batches, walk_rounds, outer_rounds, dense_chunks;
     uint32_t redone;     /* sub-batches the asynchronous pass handed back to the host */
     uint32_t shadow_misses; /* ... of which because a predicted REF was not emitted */
+    uint32_t anchor_scans;  /* sub-batches whose first scan took its events from the anchor index */
+    uint32_t anchor_fallbacks; /* ... handed to the exact scan (a collision at a candidate, an
+                               anchorless declaration, an overflowing record list) */
 } xc_run_stats;
 int xc_plan_stats(xc_plan *p, xc_run_stats *st);
+
+/* The first scan of a sub-batch.  XC_SCAN_AUTO (the default): the anchor index
+ * when the run qualifies (a memory cache whose segments all have an anchor, fresh encoders, at
+ * least XC_ANCHOR_MIN_KEYS cached + new segments), else the exact scan, which tests every window
+ * end against the cache.  XC_SCAN_EXACT: always the exact scan.  XC_SCAN_ANCHOR: the anchor index
+ * whenever the run qualifies, whatever its size (tests).  Results are identical in every mode. */
+#define XC_SCAN_AUTO 0
+#define XC_SCAN_EXACT 1
+#define XC_SCAN_ANCHOR 2
+int xc_plan_set_scan(xc_plan *p, int mode);
 
 /* ---- stateful streams: XCodecEncoder across calls (xcodec/xcodec_encoder.h:43-63) ----
  *

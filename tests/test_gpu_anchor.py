@@ -1,0 +1,222 @@
+"""GPU parity tests of the anchor scan: the first-round scan of a sub-batch takes
+its events from the anchor index instead of testing every window end, and the bytes stay those of
+the oracle (the reference's encoder, xcodec/xcodec_encoder.cc:60-260).  Forced with XC_SCAN=anchor
+(the default picks it for large caches only); the whole GPU suite is also run that way
+(tools/gpu_r3m.sh)."""
+import numpy as np
+import pytest
+
+from wanproxy_amd import workloads as W
+
+pytestmark = pytest.mark.gpu
+
+
+def _gear(seg):
+    """G(p) = sum_{k<32} b[p-k] 2^k mod 2^32 of every position (p < 31: partial)."""
+    g = np.zeros(len(seg), np.uint64)
+    acc = 0
+    for p, b in enumerate(seg.tolist()):
+        acc = ((acc << 1) + b) & 0xFFFFFFFF
+        g[p] = acc
+    return g
+
+
+def _last_anchor(seg):
+    """A segment's anchor offset: its last position j >= 63 with G(j) < 2^26 (None: anchorless)."""
+    g = _gear(seg)
+    js = [p for p in range(63, len(seg)) if g[p] < (1 << 26)]
+    return js[-1] if js else None
+
+
+def _collision_pair(seed=1, in_anchor=False):
+    """x, y with equal 64-bit hashes and different bytes (odd bytes, +-2 at (i, i+1, k, k+1) keep
+    both sums); in_anchor: the changes inside the 64-byte context of x's anchor, so the index does
+    not propose y's window for x (the collision is invisible to an anchor scan)."""
+    rng = np.random.default_rng(seed)
+    x = (rng.integers(2, 126, 2048, dtype=np.int64) * 2 + 1).astype(np.uint8)
+    i, k = 100, 1500
+    if in_anchor:
+        j = _last_anchor(x)
+        assert j is not None
+        i, k = j - 40, j - 10
+    y = x.copy()
+    y[i] += 2; y[i + 1] -= 2; y[k] -= 2; y[k + 1] += 2
+    return x, y
+
+
+def _plan_run(ctx, cache, bufs, mode="anchor", completion=False):
+    """One device-resident run of `bufs` (an EncodePlan in scan mode `mode`); the encoded streams
+    and the run's counters."""
+    import torch
+    import wanproxy_amd as w
+    plan = w.EncodePlan(cache, [len(b) for b in bufs])
+    plan.set_scan(mode)
+    if completion:
+        plan.set_completion(True)
+    arena = np.zeros(plan.in_bytes, np.uint8)
+    for i, b in enumerate(bufs):
+        arena[int(plan.in_off[i]):int(plan.in_off[i]) + len(b)] = b
+    d_in = torch.from_numpy(arena).cuda()
+    d_out = torch.zeros(plan.out_bytes, dtype=torch.uint8, device="cuda")
+    d_len = torch.zeros(max(len(bufs), 1), dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    plan.run(d_in.data_ptr(), d_out.data_ptr(), d_len.data_ptr())
+    ctx.sync()
+    out = d_out.cpu().numpy()
+    lens = d_len.cpu().numpy()
+    got = [out[int(plan.out_off[i]):int(plan.out_off[i]) + int(lens[i])].tobytes() for i in range(len(bufs))]
+    st = plan.stats()
+    plan.close()
+    return got, st
+
+
+def _same(got, want):
+    assert len(got) == len(want)
+    for i, (g, e) in enumerate(zip(got, want)):
+        if g != e:
+            n = min(len(g), len(e))
+            d = next((k for k in range(n) if g[k] != e[k]), n)
+            pytest.fail(f"buffer {i}: len gpu {len(g)} oracle {len(e)}, first diff at {d}")
+
+
+def _pool_cache(ctx, oracle_mod, nseg=512, cap=1 << 15):
+    import wanproxy_amd as w
+    pool = W.pool(nseg)
+    warm = [pool[i:i + 65536] for i in range(0, len(pool), 65536)]
+    cache = w.XCodecCache(ctx, cap)
+    oc = oracle_mod.Cache()
+    _same(w.XCodecEncoder(cache).encode_batch(warm), oc.encode_batch(warm))
+    return cache, oc, pool
+
+
+def test_anchor_scan_repeats(gpu_ctx, oracle_mod, monkeypatch):
+    """Aligned pool repeats and fresh data (the cfg workloads' shape): every sub-batch is
+    anchor-scanned, none falls back, the bytes equal the oracle's."""
+    monkeypatch.setenv("XC_SUB_MB", "1")
+    cache, oc, pool = _pool_cache(gpu_ctx, oracle_mod)
+    bufs = W.repeat_buffers(64, 0x5151, np_segments=512, pool_bytes=pool)
+    got, st = _plan_run(gpu_ctx, cache, bufs)
+    _same(got, oc.encode_batch(bufs))
+    assert st.anchor_scans == st.sub_batches > 1 and st.anchor_fallbacks == 0, (st.anchor_scans, st.sub_batches)
+    assert len(cache) == len(oc)
+
+
+def test_anchor_scan_shifted_and_cross_buffer(gpu_ctx, oracle_mod, monkeypatch):
+    """Repeats at unaligned offsets (proposals the index must find between aligned windows),
+    segments declared by earlier buffers of the same batch, a buffer's partial last block."""
+    monkeypatch.setenv("XC_SCAN", "anchor")
+    cache, oc, pool = _pool_cache(gpu_ctx, oracle_mod, 256)
+    a = W.gen(61, 65536)
+    bufs = []
+    for k in range(24):
+        if k % 4 == 0:
+            bufs.append(np.concatenate([W.gen(700 + k, 333 * k + 7), pool[k * 4096 + 99:k * 4096 + 99 + 20000]]))
+        elif k % 4 == 1:
+            bufs.append(np.concatenate([W.gen(800 + k, 1000 + k), a[k * 50:k * 50 + 30000], W.gen(900 + k, 3333)]))
+        elif k % 4 == 2:
+            bufs.append(a[k:].copy())
+        else:
+            bufs.append(np.concatenate([pool[(k % 64) * 2048:(k % 64) * 2048 + 16384], W.gen(950 + k, 5000)]))
+    want = oc.encode_batch(bufs)
+    got, st = _plan_run(gpu_ctx, cache, bufs, mode="auto")
+    _same(got, want)
+    assert st.anchor_scans >= 1
+    assert len(cache) == len(oc)
+
+
+def test_anchor_scan_collisions_fall_back(gpu_ctx, oracle_mod):
+    """A constructed collision (H equal, bytes different: xcodec_encoder.cc:129-137) at a lookup
+    that would set the candidate, invisible to the index (its anchor context differs): the walk
+    takes it for a miss, the declaration's hash check finds the cache entry, and the exact scan
+    redoes the sub-batch.  A REF at an unaligned position (found through the index) puts the
+    lookup there: the hash restarts after it (xcodec_encoder.cc:111-118)."""
+    cache, oc, pool = _pool_cache(gpu_ctx, oracle_mod, 64)
+    x, y = _collision_pair(3, in_anchor=True)
+    warm = [np.concatenate([x, W.gen(71, 4000)])]
+    _same(_plan_run(gpu_ctx, cache, warm)[0], oc.encode_batch(warm))
+    seg = pool[5 * 2048:6 * 2048]
+    bufs = [np.concatenate([W.gen(72, 100), seg, y, W.gen(73, 5000)]), W.gen(75, 40000),
+            np.concatenate([W.gen(76, 300), seg, y])]
+    got, st = _plan_run(gpu_ctx, cache, bufs)
+    _same(got, oc.encode_batch(bufs))
+    assert st.anchor_scans >= 1 and st.anchor_fallbacks >= 1, (st.anchor_scans, st.anchor_fallbacks)
+
+
+@pytest.mark.parametrize("ch", [0, 0x41, 0xF1, 0x7F])
+def test_anchor_scan_char_runs(gpu_ctx, oracle_mod, ch):
+    """Constant runs: every position has the same 64-byte context, so a value's runs are either
+    all anchors (records run-length coded, dense proposals) or none (an anchorless segment sends
+    the run to the exact scan and keeps the cache there)."""
+    import wanproxy_amd as w
+    cache = w.XCodecCache(gpu_ctx, 1 << 12)
+    oc = oracle_mod.Cache()
+    bufs = [np.full(512 * 1024, ch, np.uint8), np.concatenate([W.gen(81, 3000), np.full(70000, ch, np.uint8)])]
+    got, st = _plan_run(gpu_ctx, cache, bufs)
+    _same(got, oc.encode_batch(bufs))
+    assert len(got[0]) == 4600
+    more = [np.concatenate([np.full(9000, ch, np.uint8), W.gen(82, 20000)]), W.gen(83, 30000)]
+    got, st = _plan_run(gpu_ctx, cache, more)
+    _same(got, oc.encode_batch(more))
+
+
+def test_anchor_index_restore_growth_and_backfill(gpu_ctx, oracle_mod):
+    """The index across the cache's life: segments entered by exact runs and by the host API are
+    backfilled before an anchor run, a restore takes out what was indexed after the snapshot, a
+    growth moves the index into the larger tables."""
+    import wanproxy_amd as w
+    cache = w.XCodecCache(gpu_ctx, 1024)
+    oc = oracle_mod.Cache()
+    first = W.random_buffers(8, seed0=0xC000)
+    _same(_plan_run(gpu_ctx, cache, first, mode="exact")[0], oc.encode_batch(first))
+    seg = W.gen(0xC777, 2048)
+    h = oracle_mod.hash_segment(seg)
+    cache.enter(h, seg)
+    oc.enter(h, seg)
+    cache.snapshot()
+    snap = oc.clone()
+    for k in range(3):  # 3 x 1280 segments: the cache grows from 1024
+        bufs = W.random_buffers(40, seed0=0xC100 + 100 * k) + [np.concatenate([first[k], seg, first[k + 1]])]
+        got, st = _plan_run(gpu_ctx, cache, bufs)
+        _same(got, oc.encode_batch(bufs))
+        assert st.anchor_scans >= 1
+    assert cache.capacity > 1024
+    cache.restore()
+    again = W.random_buffers(4, seed0=0xC100) + [np.concatenate([first[5], seg, W.gen(0xC999, 9000)])]
+    got, st = _plan_run(gpu_ctx, cache, again)
+    _same(got, snap.clone().encode_batch(again))
+    for k in range(2):  # restore / rerun cycles (the bench's pattern)
+        cache.restore()
+        got, st = _plan_run(gpu_ctx, cache, again, completion=True)
+        _same(got, snap.clone().encode_batch(again))
+
+
+def test_anchor_scan_recent_window_after_collisions(gpu_ctx, oracle_mod):
+    """The recent window remembers collision lookups that an anchor scan does not look for (a
+    pending candidate makes them irrelevant to the bytes); the tail check finds the run's last ones
+    again.  A stateful connection's carried candidate y is declared after x (same hash) was entered
+    and y's windows were looked up (collisions, remembering x's entry): the map then answers y and
+    the window x (xcodec_cache.h:137-147,182-188), as in the oracle."""
+    import wanproxy_amd as w
+    x, y = _collision_pair(5, in_anchor=True)
+    cache = w.XCodecCache(gpu_ctx, 1 << 12)
+    oc = oracle_mod.Cache()
+    gs, os_ = w.XCodecStreamEncoder(cache), oracle_mod.Encoder(oc)
+    # (a) a candidate y, looked up while absent, carried (encode() only)
+    a = np.concatenate([y, W.gen(91, 100)])
+    assert gs.encode(a) == os_.encode(a)
+    # (b) x entered by an anchor-scanned batch
+    b = [np.concatenate([x, W.gen(92, 3000)])]
+    _same(_plan_run(gpu_ctx, cache, b)[0], oc.encode_batch(b))
+    # (c) y's windows looked up while a candidate is pending: collisions with x (remembered)
+    c = [np.concatenate([W.gen(93, 1000), y, W.gen(94, 3000)]), W.gen(95, 9000)]
+    got, st = _plan_run(gpu_ctx, cache, c)
+    _same(got, oc.encode_batch(c))
+    assert st.anchor_scans >= 1
+    # (d) y declared: the hash entered twice (map: y, window: x)
+    d = W.gen(96, 4096)
+    assert gs.encode(d) == os_.encode(d)
+    assert gs.flush() == os_.flush()
+    # (e) fresh encoders see the window's x
+    e = [np.concatenate([W.gen(97, 500), x, W.gen(98, 200)]), np.concatenate([y, x, W.gen(99, 64)])]
+    assert w.XCodecEncoder(cache).encode_batch(e) == oc.encode_batch(e)
+    assert len(cache) == len(oc)

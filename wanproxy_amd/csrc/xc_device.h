@@ -540,4 +540,125 @@ __device__ __forceinline__ int set_insert(const DevSet &s, uint64_t h, uint64_t 
     return fresh;
 }
 
+// ---- anchor index -----------------------------------------------------------------
+// A content-defined index that finds every window equal to an indexed segment without testing
+// every window end against the key set.  G(p) = sum_{k<32} b[p-k] 2^k mod 2^32
+// is a shift-add hash of the 32 bytes ending at p.  Position p is an anchor when p >= 63 (its
+// 64-byte context lies inside the buffer, or the segment) and G(p) < 2^26 (1/64 of random
+// positions); its fingerprint hashes G(p) and G(p - 32), i.e. the 64 bytes ending at p.  A
+// segment's anchor is its last anchor j (63 <= j <= 2047), indexed as key fp << 11 | j.  If the
+// window ending at q equals the segment, the input position a = q - 2047 + j has the same 64-byte
+// context, so it is an anchor with the same fingerprint: the index proposes q = a + 2047 - j.
+// Segments without an anchor (a 1.6e-14 chance for random bytes; constant runs of some values)
+// keep the cache out of anchor mode (the exact scan, xc_runtime.hip).
+#define ANC_G_LIMIT (1u << 26)
+#define ANC_NONE 0xFFFFFFFFFFFFFFFFull
+#define ANC_FILT_WORDS (1u << 19)  // 2 MB anchor filter (k = 2 bits in a 32-bit word), like level 2
+
+__device__ __forceinline__ uint64_t anc_fp(uint32_t g, uint32_t g2)
+{
+    const uint64_t k = ((uint64_t)g2 << 26) | (g & (ANC_G_LIMIT - 1u));
+    return (k * 0x9E3779B97F4A7C15ull) >> 19;  // 45 bits
+}
+__device__ __forceinline__ uint64_t anc_key(uint64_t fp, uint32_t j) { return (fp << 11) | j; }
+__device__ __forceinline__ uint32_t anc_mix(uint64_t fp) { return (uint32_t)(fp ^ (fp >> 21)) * 0x2C1B3C6Du; }
+__device__ __forceinline__ uint32_t anc_home(uint64_t fp, uint32_t mask) { return (uint32_t)((fp * 0xD6E8FEB86659FD93ull) >> 37) & mask; }
+__device__ __forceinline__ uint32_t anc_fword(uint32_t g) { return g >> 13; }
+__device__ __forceinline__ uint32_t anc_fbits(uint32_t g) { return (1u << (g & 31u)) | (1u << ((g >> 5) & 31u)); }
+__device__ __forceinline__ bool anc_ftest(uint32_t w, uint32_t g) { return ((w >> (g & 31u)) & (w >> ((g >> 5) & 31u)) & 1u) != 0u; }
+
+// An anchor table: open addressing over keys fp << 11 | j, home slot by fp only (a probe walks
+// the chain from home(fp) to the first empty slot and takes every key with that fingerprint).
+struct AncSet {
+    uint64_t *keys;  // mask + 1 slots, XC_EMPTY64 = empty
+    uint32_t *filt;  // ANC_FILT_WORDS
+    uint32_t mask;
+};
+
+// Insert key (fingerprint fp): the slot it took, or NONE when the key was there already.
+__device__ __forceinline__ uint32_t anc_insert(const AncSet &s, uint64_t key)
+{
+    const uint64_t fp = key >> 11;
+    const uint32_t g = anc_mix(fp);
+    atomicOr(&s.filt[anc_fword(g)], anc_fbits(g));
+    uint32_t i = anc_home(fp, s.mask);
+    for (;;) {
+        const uint64_t prev = atomicCAS((unsigned long long *)&s.keys[i], (unsigned long long)XC_EMPTY64,
+                                        (unsigned long long)key);
+        if (prev == XC_EMPTY64) return i;
+        if (prev == key) return 0xFFFFFFFFu;
+        i = (i + 1u) & s.mask;
+    }
+}
+
+// G at a lane's last position from its 32 bytes alone: sum_i b_i 2^(31 - i) (byte dot products
+// with weights 8, 4, 2, 1 per dword, Horner over the dwords).
+__device__ __forceinline__ uint32_t gear32(const uint32_t w[8])
+{
+    uint32_t s = 0;
+#pragma unroll
+    for (int d = 0; d < 8; d++) s = (s << 4) + __builtin_amdgcn_udot4(w[d], 0x01020408u, 0u, false);
+    return s;
+}
+
+// G at the lane's position -1 (the last of the lane before; lane 0: `first`).
+__device__ __forceinline__ uint32_t gear_prev(uint32_t sf, uint32_t first)
+{
+    const uint32_t l = lane_id();
+    const uint32_t up = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * ((l + 63u) & 63u)), (int)sf);
+    return l == 0 ? first : up;
+}
+
+// Anchor mask of the lane's 32 positions (bit 31 - t: position t of the lane is an anchor, before
+// any position bound); TILE: G of every position into tile[t * 64 + lane] too.
+template <bool TILE>
+__device__ __forceinline__ uint32_t gear_mask(const uint32_t w[8], uint32_t g, uint32_t *tile)
+{
+    const uint32_t l = lane_id();
+    uint32_t m = 0;
+#pragma unroll
+    for (int d = 0; d < 8; d++) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            g = (g << 1) + ((w[d] >> (8 * k)) & 0xffu);
+            if (TILE) tile[(4 * d + k) * 64 + l] = g;
+            m = m + m + (g < ANC_G_LIMIT ? 1u : 0u);
+        }
+    }
+    return m;
+}
+
+// G at position t (wave-uniform, < 32) of every lane, from G at position -1.
+__device__ __forceinline__ uint32_t gear_at(const uint32_t w[8], uint32_t g, uint32_t t)
+{
+#pragma unroll
+    for (int d = 0; d < 8; d++) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t gn = (g << 1) + ((w[d] >> (8 * k)) & 0xffu);
+            g = (uint32_t)(4 * d + k) <= t ? gn : g;
+        }
+    }
+    return g;
+}
+
+// The anchor key of a 2048-byte segment held as 32 bytes per lane (lane l: bytes 32 l .. 32 l + 31),
+// or ANC_NONE; every lane returns it.
+__device__ __forceinline__ uint64_t wave_seg_anchor(const uint32_t w[8])
+{
+    const uint32_t l = lane_id();
+    const uint32_t gi = gear_prev(gear32(w), 0u);
+    uint32_t m = gear_mask<false>(w, gi, nullptr);
+    // positions 32 l + t >= 63: lanes >= 2 all, lane 1 only t = 31 (bit 0)
+    m = l >= 2u ? m : (l == 1u ? (m & 1u) : 0u);
+    // the last anchor: the highest lane with one, its lowest bit (largest t)
+    const uint32_t j = m ? 32u * l + 31u - (uint32_t)__builtin_ctz(m) : 0u;
+    const uint64_t has = ballot(m != 0u);
+    if (!has) return ANC_NONE;
+    const int lj = 63 - __builtin_clzll(has);
+    const uint32_t jj = readlane(j, lj), t = jj & 31u;
+    const uint32_t g = gear_at(w, gi, t);
+    return anc_key(anc_fp(readlane(g, lj), readlane(g, lj - 1)), jj);
+}
+
 }  // namespace xc

@@ -448,6 +448,138 @@ template __global__ void k_scan<3>(ScanArgs);
 template __global__ void k_scan<4>(ScanArgs);
 template __global__ void k_scan<5>(ScanArgs);
 
+// ---------------------------------------------------------------- k_ascan ---------------
+// The first-round scan of an anchor-scanned sub-batch, one wave per chunk.  Its
+// events are the aligned windows (always events, as in k_scan) and the window ends the anchor
+// index proposes: an input anchor record (fingerprint fp, position a, a run of n) whose
+// fingerprint the cache or the predicted declarations index as (fp, j) proposes q = a + k + 2047
+// - j for k < n.  Every window equal to an indexed segment is among them (superset: k_resolve
+// decides each exactly).  The records of the 1984 positions before the chunk count too (their
+// proposals can end in it).  Events are collected in an LDS bitmask: sorted and deduplicated.
+constexpr uint32_t ASCAN_WAVES = 4;
+__global__ __launch_bounds__(64 * ASCAN_WAVES) void k_ascan(AScanArgs a)
+{
+    if (aborted(a.P)) return;
+    __shared__ uint32_t bitsl[ASCAN_WAVES][CHUNK_BLOCKS * XC_SEG / 32];
+    const PlanDev &P = a.P;
+    const uint32_t wave = threadIdx.x >> 6, l = lane_id();
+    const uint32_t c = a.ck_lo + blockIdx.x * ASCAN_WAVES + wave;
+    if (c >= a.ck_hi) return;
+    auto wave_sync = []() {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    uint32_t *bm = bitsl[wave];
+    if (uniform(*(volatile const uint32_t *)P.anc_bad)) {  // a segment the index cannot find
+        if (l == 0) {
+            a.L.cnt[c] = 0u;
+            atomicOr(&P.ctl[CTL_AFAIL], 8u);
+        }
+        return;
+    }
+    const uint4 d = P.chunk_desc[c];
+    const uint32_t c0 = uniform(d.x), c1 = uniform(d.y) & 0x3FFFFFFFu;
+    const uint32_t b = uniform(P.chunks[c].x);
+    const uint32_t W = P.chunk_len / 32u;
+    const uint32_t cblk = a.shadow ? uniform(P.chunk_blk[c]) : 0u;
+    for (uint32_t i = l; i < W; i += 64u) bm[i] = 0u;
+    wave_sync();
+    // aligned windows: the block is cached or a predicted declaration (k_resolve decides which)
+    for (uint32_t q = c0 + (XC_SEG - 1u) + XC_SEG * l; q < c1; q += 64u * XC_SEG)
+        atomicOr(&bm[(q - c0) >> 5], 1u << ((q - c0) & 31u));
+    // the records of blocks lo >> 11 .. (c1 - 1) >> 11 (one or two groups), loaded 256 at a time
+    // (four per lane, every load in flight together), then their filter words likewise
+    const uint32_t lo = c0 > 1984u ? c0 - 1984u : 0u;
+    const uint32_t gb = uniform(P.buf_grp0[b]);
+    const uint32_t bl = lo >> 11, bh = (c1 - 1u) >> 11;
+    bool ovf = false;
+    for (uint32_t gg = bl >> 3; gg <= bh >> 3; gg++) {
+        const uint32_t g = gb + gg;
+        const uint32_t cnt = uniform(P.rec_cnt[g]);
+        if (cnt & REC_OVF) {
+            ovf = true;
+            break;
+        }
+        const uint32_t x = gg == (bl >> 3) ? (bl & 7u) : 0u, y = gg == (bh >> 3) ? (bh & 7u) : 7u;
+        const uint32_t r0 = uniform(P.rec_blk[g * BLK_GROUP + x]);
+        const uint32_t r1 = y == 7u ? cnt : min(cnt, uniform(P.rec_blk[g * BLK_GROUP + y + 1u]));
+        const uint32_t gpos = gg << 14;
+        for (uint32_t i0 = r0; i0 < r1; i0 += 256u) {
+            uint64_t r[4];
+            uint32_t fw[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t i = i0 + 64u * k + l;
+                r[k] = i < r1 ? P.rec[(size_t)g * REC_CAP + i] : ~0ull;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) fw[k] = P.amix[r[k] != ~0ull ? anc_fword(anc_mix(r[k] >> 19)) : 0u];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                if (r[k] == ~0ull) continue;
+                const uint64_t fp = r[k] >> 19;
+                const uint32_t ap = gpos + (((uint32_t)r[k] >> 5) & 0x3FFFu), nr = ((uint32_t)r[k] & 31u) + 1u;
+                // proposals of the run end in [ap, ap + nr - 1 + 1984]
+                if (!(ap + nr + 1983u >= c0 && ap < c1 && anc_ftest(fw[k], anc_mix(fp)))) continue;
+#pragma unroll
+                for (int tb = 0; tb < 2; tb++) {
+                    const AncSet &S = tb ? P.danc : P.canc;
+                    uint32_t kk = anc_home(fp, S.mask);
+                    for (;;) {
+                        const uint64_t key = S.keys[kk];
+                        if (key == XC_EMPTY64) break;
+                        if ((key >> 11) == fp) {
+                            const uint32_t j = (uint32_t)key & 2047u;
+                            for (uint32_t e = 0; e < nr; e++) {
+                                const uint32_t aa = ap + e, q = aa + (XC_SEG - 1u) - j;
+                                if (aa < j || q < c0 || q >= c1 || ((q + 1u) & (XC_SEG - 1u)) == 0u) continue;
+                                // REF shadow: the 2047 window ends after a predicted REF are not looked up
+                                if (a.shadow && q >= XC_SEG && blk_cached(P.blk_pref[cblk + (q >> 11) - 1u])) continue;
+                                atomicOr(&bm[(q - c0) >> 5], 1u << ((q - c0) & 31u));
+                            }
+                        }
+                        kk = (kk + 1u) & S.mask;
+                    }
+                }
+            }
+        }
+    }
+    if (ovf) {  // records overflowed (e.g. a long run of one byte value): the exact scan redoes it
+        if (l == 0) {
+            a.L.cnt[c] = 0u;
+            atomicOr(&P.ctl[CTL_AFAIL], 4u);
+        }
+        return;
+    }
+    wave_sync();
+    uint32_t tot = 0;
+    for (uint32_t i = l; i < W; i += 64u) tot += (uint32_t)__popc(bm[i]);
+    tot = wave_sum(tot);
+    if (tot <= EV_CAP) {
+        uint32_t base = 0;
+        for (uint32_t i0 = 0; i0 < W; i0 += 64u) {
+            const uint32_t i = i0 + l;
+            uint32_t v = i < W ? bm[i] : 0u;
+            const uint32_t k = (uint32_t)__popc(v), incl = wave_incl_scan(k);
+            uint32_t o = base + incl - k;
+            while (v) {
+                const uint32_t bit = (uint32_t)__builtin_ctz(v);
+                v &= v - 1u;
+                a.L.pos[c * EV_CAP + o++] = c0 + 32u * i + bit;
+            }
+            base += readlane(incl, 63);
+        }
+        if (l == 0) a.L.cnt[c] = tot;
+    } else {
+        for (uint32_t i = l; i < W; i += 64u) a.L.bits[(size_t)c * W + i] = bm[i];
+        if (l == 0) {
+            a.L.cnt[c] = EV_DENSE | EV_CAP;
+            atomicAdd(&P.ctl[CTL_DENSE], 1u);
+        }
+    }
+}
+
 // ------------------------------------------------------------- k_resolve ----------------
 // One wave per chunk: sort the sparse list, then resolve every event exactly.
 
@@ -1045,6 +1177,13 @@ __device__ __forceinline__ void decl_hash(const PlanDev &P, uint32_t b)
             const uint64_t h = known ? ((uint64_t)uniform((uint32_t)(P.tok_h[tt] >> 32)) << 32) |
                                            uniform((uint32_t)P.tok_h[tt])
                                      : wave_window_hash(base + seg);
+            if (P.anc_scan && !known) {
+                // anchor-scanned: events are the windows equal to indexed segments, so a candidate
+                // outside them was assumed a miss; a cache entry with its hash (other bytes: a
+                // collision, xcodec_encoder.cc:129-137) makes the exact scan redo the sub-batch
+                uint64_t v;
+                if (set_find(P.cache, h, &v) && l == 0) atomicOr(&P.ctl[CTL_AFAIL], 2u);
+            }
             if (l == 0) {
                 P.tok_h[tt] = h;
                 const uint64_t v = ((uint64_t)b << 32) | P.tok_dpos[tt];
@@ -1077,37 +1216,159 @@ __global__ __launch_bounds__(64 * WALK_WAVES_MAX) void k_walk(WalkArgs a)
 // of one buffer (P.blk_grp; [a.j0, a.j1) is a range of groups), four waves per workgroup: a
 // wave has all its loads in flight together.  Depends on the input only, so it runs ahead on a
 // side stream.  (One-wave workgroups made this kernel dispatch-bound.)
-constexpr uint32_t BLK_GROUP = 8;
 
 // Block g (global index; block k of buffer b) with hash h: blocks absent from the cache are the
 // predicted declarations (hit-free data declares exactly these, xcodec_encoder.cc:77-82); they
-// enter the declaration set and the combined level-2 filter before the scan.  Cached blocks are
+// enter the declaration set and the combined level-2 filter before the scan (and, on an
+// anchor-scanned sub-batch, the declaration set's anchor table: akey).  Cached blocks are
 // predicted REFs (REF shadows).
 // Returns the prediction (blk_pref).
-__device__ __forceinline__ uint32_t block_predict(const PlanDev &P, uint32_t g, uint32_t b, uint32_t k, uint64_t h);
+__device__ __forceinline__ uint32_t block_predict(const PlanDev &P, uint32_t g, uint32_t b, uint32_t k, uint64_t h,
+                                                  uint64_t akey);
+
+// The anchors of a k_blockhash group: G of every position of its na blocks
+// (w[i]: block i, lane l: bytes 32 l .. 32 l + 31) into tile (per wave: 32 x 64 values, then the
+// 32 values of the lane before lane 0), the block's anchors compacted into a position-ordered list
+// (list: 2048 entries per wave), then every input anchor into the group's records, 64 list entries
+// at a time (runs of equal fingerprints at consecutive positions, at most 32 and within a 32-byte
+// lane part, as one record); returns, in lane i, the anchor key of full block i (its last anchor at
+// block offset >= 63; ANC_NONE: none).
+__device__ __forceinline__ uint64_t group_anchors(const PlanDev &P, uint32_t g, uint32_t k0, uint32_t len,
+                                                  uint32_t n, uint32_t na, const uint8_t *base,
+                                                  const uint32_t (&w)[BLK_GROUP][8], uint32_t *tile,
+                                                  uint16_t *list)
+{
+    const uint32_t l = lane_id();
+    uint32_t *prev = tile + 32u * 64u;
+    auto wave_sync = []() {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    // G at positions -32 .. -1 before the group (block 0's lane 0 takes G(p - 32) from there) and
+    // at -1 (its G before its first position); a buffer's first group has no anchor below 63
+    uint32_t first = 0;
+    if (k0 > 0) {
+        const uint4 *pp = (const uint4 *)(base + (size_t)k0 * XC_SEG - 64u);
+        const uint4 x0 = pp[0], x1 = pp[1], x2 = pp[2], x3 = pp[3];
+        const uint32_t lo[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        const uint32_t hi[8] = {x2.x, x2.y, x2.z, x2.w, x3.x, x3.y, x3.z, x3.w};
+        uint32_t gg = gear32(lo), mine = 0;  // G(-33), then G(-32 + t)
+#pragma unroll
+        for (int t = 0; t < 32; t++) {
+            gg = (gg << 1) + ((hi[t >> 2] >> (8 * (t & 3))) & 0xffu);
+            mine = l == (uint32_t)t ? gg : mine;
+        }
+        if (l < 32u) prev[l] = mine;
+        first = gg;
+    }
+    uint32_t cnt = 0;
+    uint64_t bkey = ANC_NONE;
+#pragma unroll
+    for (uint32_t i = 0; i < BLK_GROUP; i++) {
+        if (i >= na) break;
+        const uint32_t *wi = w[i];
+        const uint32_t sf = gear32(wi);
+        const uint32_t gi = gear_prev(sf, first);
+        first = readlane(sf, 63);
+        if (i > 0) {  // lane 0's G(p - 32): the last lane of the block before
+            wave_sync();
+            if (l < 32u) prev[l] = tile[l * 64u + 63u];
+            wave_sync();
+        }
+        if (l == 0) P.rec_blk[g * BLK_GROUP + i] = min(cnt, REC_CAP);
+        uint32_t m = gear_mask<true>(wi, gi, tile);
+        // buffer positions p0 + t: anchors need p >= 63 (the context in the buffer) and p < len
+        const uint32_t p0 = (k0 + i) * XC_SEG + 32u * l;
+        if (p0 < 63u) m &= p0 + 31u >= 63u ? ~0u >> (63u - p0) : 0u;  // bit 31 - t: t >= 63 - p0
+        if (p0 + 32u > len) m &= p0 >= len ? 0u : ~(~0u >> (len - p0));  // t < len - p0
+        // compaction: every anchor's block offset, in position order
+        const uint32_t k = (uint32_t)__popc(m), incl = wave_incl_scan(k);
+        const uint32_t total = readlane(incl, 63);
+        uint32_t o = incl - k;
+        while (m) {
+            const uint32_t t = (uint32_t)__builtin_clz(m);
+            m &= ~(0x80000000u >> t);
+            list[o++] = (uint16_t)(32u * l + t);
+        }
+        wave_sync();
+        uint32_t cp = NONE;  // the previous list entry's offset and fingerprint (uniform)
+        uint64_t cfp = 0;
+        for (uint32_t b0 = 0; b0 < total; b0 += 64u) {
+            const uint32_t idx = b0 + l;
+            const bool live = idx < total;
+            const uint32_t p = live ? list[idx] : 0u;
+            const uint32_t ln = p >> 5, t = p & 31u;
+            const uint32_t gv = tile[t * 64u + ln];
+            const uint32_t g2 = ln ? tile[t * 64u + ln - 1u] : prev[t];
+            const uint64_t fp = anc_fp(gv, g2);
+            // a run continues when the entry before has the position before (inside one lane's
+            // 32 positions) and the same fingerprint
+            uint32_t pp = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * ((l + 63u) & 63u)), (int)p);
+            uint32_t fl = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * ((l + 63u) & 63u)), (int)(uint32_t)fp);
+            uint32_t fh = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * ((l + 63u) & 63u)), (int)(uint32_t)(fp >> 32));
+            const uint64_t pfp = ((uint64_t)fh << 32) | fl;
+            // (a run does not continue across 64 entries: a chunk's first entry is a head)
+            const bool cont = live && l != 0u && (p & 31u) != 0u && pp + 1u == p && pfp == fp;
+            const uint64_t heads = ballot(live && !cont);
+            const uint64_t above = heads & (l == 63u ? 0ull : ~0ull << (l + 1u));
+            const uint32_t end = above ? b0 + (uint32_t)__builtin_ctzll(above) : min(total, b0 + 64u);
+            const bool head = live && !cont;
+            if (head) {
+                const uint32_t ri = cnt + mbcnt(heads);
+                if (ri < REC_CAP) P.rec[(size_t)g * REC_CAP + ri] = rec_make(fp, i * XC_SEG + p, end - idx);
+            }
+            cnt += (uint32_t)__popcll(heads);
+            const uint32_t last = min(total - b0, 64u) - 1u;
+            cp = readlane(p, (int)last);
+            cfp = readlane64(fp, (int)last);
+        }
+        if (i < n) {  // the block's anchor: its last one at offset >= 63
+            const uint64_t key = total && cp >= 63u ? anc_key(cfp, cp) : ANC_NONE;
+            if (l == i) bkey = key;
+        }
+        wave_sync();  // (the next block's tile and list overwrite these)
+    }
+    if (l == 0) {
+        P.rec_cnt[g] = cnt <= REC_CAP ? cnt : (REC_OVF | REC_CAP);
+        for (uint32_t i = na; i < BLK_GROUP; i++) P.rec_blk[g * BLK_GROUP + i] = min(cnt, REC_CAP);
+    }
+    return bkey;
+}
 
 // predict: also the predictions of these blocks (the run's first sub-batch, hashed in line after
-// the declaration set's clear: one kernel instead of two)
-template <bool PREDICT>
+// the declaration set's clear: one kernel instead of two).  ANC: the group's anchors too (a run in
+// anchor mode); groups then also cover a buffer's partial last block.
+template <bool PREDICT, bool ANC>
 __global__ __launch_bounds__(256) void k_blockhash(DeclArgs a)
 {
+    __shared__ uint32_t tiles[ANC ? 4 : 1][ANC ? 32 * 64 + 32 : 1];
+    __shared__ uint16_t lists[ANC ? 4 : 1][ANC ? XC_SEG : 1];
     const PlanDev &P = a.P;
     const uint32_t g = a.j0 + blockIdx.x * 4u + (threadIdx.x >> 6);
     if (g >= a.j1) return;
     const uint2 gr = P.blk_grp[g];
     const uint32_t b = gr.x, k0 = gr.y;
+    const uint32_t len = P.buf_len[b];
     const uint8_t *base = P.in + P.buf_off[b];
-    const uint32_t n = min(BLK_GROUP, P.buf_len[b] / XC_SEG - k0);
+    const uint32_t nfull = len / XC_SEG;
+    const uint32_t n = nfull > k0 ? min(BLK_GROUP, nfull - k0) : 0u;
+    const uint32_t na = ANC ? min(BLK_GROUP, (len + XC_SEG - 1u) / XC_SEG - k0) : n;
     uint32_t w[BLK_GROUP][8];  // (kept for the compares below)
-    wave_load_blocks<BLK_GROUP>(base + (size_t)k0 * XC_SEG, n, w);
+    wave_load_blocks<BLK_GROUP>(base + (size_t)k0 * XC_SEG, na, w);
     const uint64_t h = block_group_hash<BLK_GROUP>(w);
+    uint64_t akey = ANC_NONE;
+    if (ANC)
+        akey = group_anchors(P, g, k0, len, n, na, base, w, tiles[(threadIdx.x >> 6) & (ANC ? 3 : 0)],
+                             lists[(threadIdx.x >> 6) & (ANC ? 3 : 0)]);
     const uint32_t l = lane_id();
     const uint32_t gi = P.blk_base[b] + k0 + l;
     uint32_t cmp = 0;  // the cached slot + 1 to compare the block with (blk_cmp)
     if (l < n) {
         P.blk_h[gi] = h;
+        if (ANC) P.blk_anc[gi] = akey;
         if (PREDICT) {
-            const uint32_t pref = block_predict(P, gi, b, k0 + l, h);
+            const uint32_t pref = block_predict(P, gi, b, k0 + l, h, akey);
             if (blk_cached(pref)) cmp = pref;
         } else if (a.limit && !stream_carried(P, b)) {
             // (a concurrent k_alloc may be entering keys: only complete entries are compared)
@@ -1144,8 +1405,10 @@ __global__ __launch_bounds__(256) void k_blockhash(DeclArgs a)
     }
     if (l < n) P.blk_cmp[gi] = verdict;
 }
-template __global__ void k_blockhash<false>(DeclArgs);
-template __global__ void k_blockhash<true>(DeclArgs);
+template __global__ void k_blockhash<false, false>(DeclArgs);
+template __global__ void k_blockhash<true, false>(DeclArgs);
+template __global__ void k_blockhash<false, true>(DeclArgs);
+template __global__ void k_blockhash<true, true>(DeclArgs);
 
 // One lane per aligned block of buffers [j0, j1) (P.blk_buf maps a block to its buffer).
 __global__ __launch_bounds__(256) void k_blockpredict(DeclArgs a)
@@ -1155,10 +1418,11 @@ __global__ __launch_bounds__(256) void k_blockpredict(DeclArgs a)
     const uint32_t g = P.blk_base[a.j0] + blockIdx.x * 256u + threadIdx.x;
     if (g >= P.blk_base[a.j1]) return;
     const uint32_t b = P.blk_buf[g], k = g - P.blk_base[b];
-    block_predict(P, g, b, k, P.blk_h[g]);
+    block_predict(P, g, b, k, P.blk_h[g], P.anc_scan ? P.blk_anc[g] : ANC_NONE);
 }
 
-__device__ __forceinline__ uint32_t block_predict(const PlanDev &P, uint32_t g, uint32_t b, uint32_t k, uint64_t h)
+__device__ __forceinline__ uint32_t block_predict(const PlanDev &P, uint32_t g, uint32_t b, uint32_t k, uint64_t h,
+                                                  uint64_t akey)
 {
     uint32_t pref = 0u;  // blocks relative to a carried source_: no predictions
     uint64_t v;
@@ -1171,6 +1435,11 @@ __device__ __forceinline__ uint32_t block_predict(const PlanDev &P, uint32_t g, 
         set_insert(P.dset, h, ((uint64_t)b << 32) | (k * XC_SEG + 2u * XC_SEG - 1u), true, &slot, nullptr);
         const uint32_t lo = (uint32_t)h;  // (the combined level-1 image the first scan loads)
         atomicOr(&P.fmix[filt_word_n(lo, XC_FILT_WORDS >> P.fmix_fold)], filt_mask(lo));
+        if (P.anc_scan) {
+            // the anchor scan finds windows equal to this block through its anchor
+            if (akey == ANC_NONE) atomicOr(&P.ctl[CTL_AFAIL], 1u);
+            else anc_insert(P.danc, akey);
+        }
         pref = BP_DECL | slot;
     }
     P.blk_pref[g] = pref;
@@ -1229,7 +1498,8 @@ constexpr int EMIT_PAY = XC_EMIT_PAY;  // payloads a wave has in flight
 __device__ __forceinline__ bool gate_stop(const EmitArgs &a)
 {
     const uint32_t *ctl = a.P.ctl;
-    return a.gate_sb != NONE && (ctl[CTL_GREW] || ctl[CTL_SHADOW] || ctl[CTL_FIRST_CROSS] < a.j1 || ctl[CTL_ERROR]);
+    return a.gate_sb != NONE &&
+           (ctl[CTL_GREW] || ctl[CTL_SHADOW] || ctl[CTL_FIRST_CROSS] < a.j1 || ctl[CTL_ERROR] || ctl[CTL_AFAIL]);
 }
 
 __device__ __forceinline__ void gate_abort(const EmitArgs &a)
@@ -1349,12 +1619,39 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
     }
     __syncthreads();
     const uint32_t slot0 = SLOTS ? s_base + s_pre : P.buf_slot[b];
+    if (SLOTS && threadIdx.x == 0) P.buf_slot[b] = slot0;  // (the tail check's visibility test)
     if (wave == EMIT_WAVES - 1u) {  // the wave with the smallest token group (wave 0 did the prefix)
         // XCodecMemoryCache::enter (xcodec_cache.h:182-188) of this buffer's declarations,
         // one lane per EXTRACT token, into the slots k_alloc reserved
         for (uint32_t t0 = 0; t0 < n; t0 += 64u) {
             const uint32_t t = t0 + l;
-            if (t < n && P.tok_op[tb + t] == OP_EXTRACT) {
+            const bool ext = t < n && P.tok_op[tb + t] == OP_EXTRACT;
+            if (P.anc_run) {
+                // the anchor index takes every entered segment: an aligned block's key from
+                // k_blockhash, any other segment's computed here (wave-wide, one at a time)
+                const uint32_t sg = ext ? P.tok_seg[tb + t] : 0u;
+                uint64_t key = ext && (sg & (XC_SEG - 1u)) == 0u ? P.blk_anc[P.blk_base[b] + sg / XC_SEG] : ANC_NONE;
+                for (uint64_t m = ballot(ext && (sg & (XC_SEG - 1u)) != 0u); m; m &= m - 1) {
+                    const int f = __ffsll((unsigned long long)m) - 1;
+                    uint32_t wv[8];
+                    load32_window(base + readlane(sg, f) + 32u * l, wv);
+                    const uint64_t k2 = wave_seg_anchor(wv);
+                    if ((int)l == f) key = k2;
+                }
+                if (ext) {
+                    const uint32_t idx = slot0 + ord[t];
+                    if (idx < P.seg_cap) {
+                        P.anc_of[idx] = key;
+                        if (key != ANC_NONE) {
+                            P.aundo[idx] = anc_insert(P.canc, key);
+                        } else {
+                            P.aundo[idx] = NONE;
+                            atomicMax(P.anc_bad, ~idx);
+                        }
+                    }
+                }
+            }
+            if (ext) {
                 const uint32_t idx = slot0 + ord[t];
                 if (idx < P.seg_cap) {
                     uint32_t s1, s2;
@@ -1610,7 +1907,7 @@ __global__ __launch_bounds__(64) void k_window_hashes(const uint8_t *in, uint32_
 // cache's: one launch instead of a memset per table.
 __global__ void k_clear_set(DevSet s, uint32_t n_lo, uint32_t n_full, uint4 *l2mix, const uint4 *cache_l2,
                             uint32_t *fmix, const uint32_t *cache_filt, uint32_t fold, const uint32_t *count,
-                            uint32_t *count_out, uint32_t *ctl_zero)
+                            uint32_t *count_out, uint32_t *ctl_zero, AncSet danc, uint4 *amix, const uint4 *cache_afilt)
 {
     const uint32_t stride = gridDim.x * blockDim.x;
     const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1638,6 +1935,12 @@ __global__ void k_clear_set(DevSet s, uint32_t n_lo, uint32_t n_full, uint4 *l2m
         ((uint4 *)s.vals)[i] = ones;
     }
     if (i0 == 0) *s.lo_zero = 0u;
+    // an anchor-scanned sub-batch: the declarations' anchor table empty, the combined anchor
+    // filter seeded with the cache's
+    if (amix) {
+        for (uint32_t i = i0; i < ANC_FILT_WORDS / 4; i += stride) amix[i] = cache_afilt[i];
+        for (uint32_t i = i0; i < (danc.mask + 1u) / 2; i += stride) ((uint4 *)danc.keys)[i] = ones;
+    }
 }
 
 __global__ void k_or_words(uint4 *dst, const uint4 *a, const uint4 *b, uint32_t n)
@@ -1885,6 +2188,296 @@ __global__ void k_selftest(uint32_t *err)
     for (uint32_t k = 0; k < 64; k++) {  // the scan's level-2 mix inverts
         const uint32_t v = (x ^ (k * 0x9E3779B9u)) * (k | 1u);
         if (l2_unmix(l2_mix(v)) != v) atomicOr(err, 4u);
+    }
+}
+
+// ------------------------------------------------------------ anchor index upkeep --------
+// Index the segments of slots [from, to) (entered by runs without anchors: while the cache was
+// small, by a decoder, through the host API), one wave per slot.
+__global__ __launch_bounds__(256) void k_anc_backfill(PlanDev P, uint32_t from, uint32_t to, uint32_t *ctl)
+{
+    const uint32_t l = lane_id();
+    for (uint32_t s = from + blockIdx.x * 4u + (threadIdx.x >> 6); s < to; s += gridDim.x * 4u) {
+        const uint4 *sp = (const uint4 *)(seg_at(P.segs, s) + 32u * l);
+        const uint4 x = sp[0], y = sp[1];
+        const uint32_t w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+        const uint64_t key = wave_seg_anchor(w);
+        if (l == 0) {
+            P.anc_of[s] = key;
+            if (key != ANC_NONE) {
+                P.aundo[s] = anc_insert(P.canc, key);
+            } else {
+                P.aundo[s] = NONE;
+                atomicMax(&ctl[CTL_ANCLESS], ~s);
+            }
+        }
+    }
+}
+
+// Restore: the anchor-table slots the segments [from, to) took are emptied (a snapshot's later
+// entries are all removed together, so no probe chain of a kept key passes through them); the
+// filter from the snapshot when snap is given.
+__global__ void k_anc_undo(AncSet s, const uint32_t *aundo, uint32_t from, uint32_t to, uint4 *filt, const uint4 *snap)
+{
+    const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+    for (uint32_t i = from + i0; i < to; i += stride) {
+        const uint32_t a = aundo[i];
+        if (a != NONE) s.keys[a] = XC_EMPTY64;
+    }
+    if (snap)
+        for (uint32_t i = i0; i < ANC_FILT_WORDS / 4; i += stride) filt[i] = snap[i];
+}
+
+// Growth / truncation: the anchors of segments [0, n) into a new table in parallel; a key shared
+// by several segments belongs (undo log) to the oldest, as when they were entered in order:
+// owner[slot] = min segment, k_anc_owner writes aundo.
+__global__ void k_anc_rehash(AncSet to, const uint64_t *anc_of, uint32_t n, uint32_t *aslot, uint32_t *owner)
+{
+    for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += gridDim.x * blockDim.x) {
+        const uint64_t key = anc_of[v];
+        if (key == ANC_NONE) {
+            aslot[v] = NONE;
+            continue;
+        }
+        uint32_t k = anc_home(key >> 11, to.mask);
+        for (;;) {
+            const uint64_t prev = atomicCAS((unsigned long long *)&to.keys[k], (unsigned long long)XC_EMPTY64,
+                                            (unsigned long long)key);
+            if (prev == XC_EMPTY64 || prev == key) break;
+            k = (k + 1u) & to.mask;
+        }
+        aslot[v] = k;
+        atomicMin(&owner[k], v);
+    }
+}
+
+__global__ void k_anc_owner(uint32_t *aundo, const uint32_t *aslot, uint32_t n, const uint32_t *owner)
+{
+    for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += gridDim.x * blockDim.x) {
+        const uint32_t a = aslot[v];
+        aundo[v] = a != NONE && owner[a] == v ? a : NONE;
+    }
+}
+
+// ------------------------------------------------------------ k_tailcheck ----------------
+// After an anchor-scanned run.  The recent window (xcodec_cache.h:89-159,
+// xc_memcache.cpp) remembers every lookup hit, collisions included; an anchor scan's events are
+// the windows equal to indexed segments, and a collision where a candidate is pending changes
+// nothing the walk decides, so those were not looked for.  The window's state after the run
+// depends on its last 64 hits only: for the buffers that hold the run's last >= 64 recorded hits
+// (REF tokens and recorded collisions), every collision lookup is found again here: each looked-up
+// window end (not a REF, not in a REF's shadow) whose hash the cache held at that point (an entry
+// before the buffer's, or one of its own declarations made before it) with other bytes; the
+// buffer's collision records are replaced by them.  Persistent grid, a workgroup per buffer.
+
+// Did buffer b's lookup at q see the entry in slot v (wave-uniform)?
+__device__ __forceinline__ bool tail_visible(const PlanDev &P, uint32_t b, uint32_t q, uint32_t v)
+{
+    const uint32_t s0 = P.buf_slot[b];
+    if (v < s0) return true;
+    const uint32_t i = v - s0;
+    if (i >= P.buf_next[b]) return false;
+    const uint32_t l = lane_id();
+    const uint32_t tb = P.tok_base[b], n = P.tok_cnt[b];
+    uint32_t ord = 0;
+    for (uint32_t t0 = 0; t0 < n; t0 += 64u) {
+        const uint32_t t = t0 + l;
+        const bool ext = t < n && P.tok_op[tb + t] == OP_EXTRACT;
+        const uint32_t incl = wave_incl_scan(ext ? 1u : 0u);
+        const uint64_t m = ballot(ext && ord + incl - 1u == i);
+        if (m) {
+            const uint32_t dpos = readlane(P.tok_dpos[tb + t0 + (uint32_t)(__ffsll((unsigned long long)m) - 1)], 0);
+            return dpos != DPOS_FLUSH && dpos <= q;
+        }
+        ord += readlane(incl, 63);
+    }
+    return false;
+}
+
+// A looked-up window end q whose full hash h the cache holds in slot v (wave-uniform): a collision
+// lookup when the entry was there at that point and its bytes differ.
+__device__ __forceinline__ void tail_candidate(const PlanDev &P, uint32_t b, uint32_t q, uint64_t h, uint32_t v,
+                                               uint4 *cl, uint32_t *ncl)
+{
+    if (!tail_visible(P, b, q, v)) return;
+    const uint8_t *win = P.in + P.buf_off[b] + q - (XC_SEG - 1u);
+    if (wave_equal2048(win, seg_at(P.segs, v))) return;  // (the walk's REF: not a collision)
+    if (lane_id() == 0) {
+        const uint32_t k = atomicAdd(ncl, 1u);
+        if (k < COLL_CAP) cl[k] = make_uint4(q, (uint32_t)h, (uint32_t)(h >> 32), NONE);
+    }
+}
+
+// Window sums of the bits half (w = ffs(byte), xcodec_hash.h:93-135) before a lane's first position,
+// as block_sums gives those of the bytes half.
+__device__ __forceinline__ BlockSums block_sums_ffs(const uint32_t w[8], uint32_t l)
+{
+    uint32_t sf = 0, jf = 0;
+#pragma unroll
+    for (int d = 0; d < 8; d++) {
+        const uint32_t wt = (uint32_t)(4 * d) * 0x01010101u + 0x03020100u;
+        const uint32_t f = ffs_bytes(w[d]);
+        sf = __builtin_amdgcn_udot4(f, 0x01010101u, sf, false);
+        jf = __builtin_amdgcn_udot4(f, wt, jf, false);
+    }
+    const uint32_t A = sf, C = 32u * l * A + jf;
+    const uint32_t ia = wave_incl_scan(A), ic = wave_incl_scan(C);
+    BlockSums s;
+    s.totA = readlane(ia, 63);
+    s.totC = readlane(ic, 63);
+    s.preA = ia - A;
+    s.preC = ic - C;
+    return s;
+}
+
+constexpr uint32_t TAIL_REFS = MAX_BUF / XC_SEG;  // REF tokens a buffer can hold
+
+__global__ __launch_bounds__(256) void k_tailcheck(PlanDev P, uint32_t nb)
+{
+    __shared__ uint32_t jstar, ncl, nrefs;
+    __shared__ uint4 cl[COLL_CAP];
+    __shared__ uint32_t refe[TAIL_REFS];  // the buffer's REF window ends, ascending
+    const uint32_t wave = threadIdx.x >> 6, l = lane_id();
+    if (wave == 0) {
+        // the last buffers whose REF hits reach the window's 64 (all of the run when fewer)
+        uint32_t acc = 0, j = 0;
+        for (uint32_t e = nb; e > 0; e = e > 64u ? e - 64u : 0u) {
+            const bool ok = l < e;
+            const uint32_t v = ok ? P.buf_nref[e - 1u - l] : 0u;
+            const uint32_t incl = wave_incl_scan(v);
+            const uint64_t m = ballot(ok && acc + incl >= 64u);
+            if (m) {
+                j = e - 1u - (uint32_t)(__ffsll((unsigned long long)m) - 1);
+                break;
+            }
+            acc += readlane(incl, 63);
+        }
+        if (l == 0) jstar = j;
+    }
+    __syncthreads();
+    const uint32_t j0 = jstar;
+    for (uint32_t b = j0 + blockIdx.x; b < nb; b += gridDim.x) {
+        const uint32_t len = P.buf_len[b];
+        const uint8_t *base = P.in + P.buf_off[b];
+        if (wave == 0) {  // the REF window ends (tokens are in position order)
+            const uint32_t tb = P.tok_base[b], n = P.tok_cnt[b];
+            uint32_t k = 0;
+            for (uint32_t t0 = 0; t0 < n; t0 += 64u) {
+                const uint32_t t = t0 + l;
+                const bool r = t < n && P.tok_op[tb + t] == OP_REF;
+                const uint64_t m = ballot(r);
+                if (r && k + mbcnt(m) < TAIL_REFS) refe[k + mbcnt(m)] = P.tok_seg[tb + t] + (XC_SEG - 1u);
+                k += (uint32_t)__popcll(m);
+            }
+            if (l == 0) {
+                nrefs = min(k, TAIL_REFS);
+                ncl = 0;
+            }
+        }
+        __syncthreads();
+        const uint32_t nr = nrefs;
+        // window ends [s, s + 2048) of block s (s = 0: the first window, 2047): full hashes by the
+        // rolling recurrences of both halves (k_scan's, plus the bits half), the looked-up ones
+        // (not a REF's and not in the 2047 ends after one) probed in the cache's full table
+        for (uint32_t s = XC_SEG * wave; s < len; s += 4u * XC_SEG) {
+            uint32_t pw[8], w[8];
+            const uint32_t q0 = s + 32u * l;
+            // the REFs whose shadow [e, e + 2047] can reach this lane's ends: the last two <= q0 + 31
+            uint32_t lo_i = 0, hi_i = nr;  // first REF end > q0 + 31
+            while (lo_i < hi_i) {
+                const uint32_t mid = (lo_i + hi_i) >> 1;
+                if (refe[mid] <= q0 + 31u) lo_i = mid + 1u;
+                else hi_i = mid;
+            }
+            uint32_t shadow = 0;  // bit t: end q0 + t is not looked up
+#pragma unroll
+            for (int k = 1; k <= 2; k++) {
+                if (lo_i >= (uint32_t)k) {
+                    const uint32_t e = refe[lo_i - k];
+                    // [e, e + 2047] within [q0, q0 + 31]
+                    const uint32_t a = e > q0 ? e - q0 : 0u, z = e + (XC_SEG - 1u) >= q0 + 31u ? 32u : (e + XC_SEG > q0 ? e + XC_SEG - q0 : 0u);
+                    if (z > a) shadow |= (z - a >= 32u ? ~0u : ((1u << (z - a)) - 1u)) << a;
+                }
+            }
+            uint32_t live = q0 < XC_SEG - 1u ? 0u : ~0u;  // window ends >= 2047
+            if (s == 0) live = l == 63u ? 0x80000000u : 0u;  // (block 0: its last end only)
+            if (q0 + 32u > len) live &= q0 >= len ? 0u : (1u << (len - q0)) - 1u;
+            live &= ~shadow;
+            if (!ballot(live != 0u)) continue;
+            BlockSums ps, cs, pf, cf;
+            if (s == 0) {  // the first window: block 0 after 2048 zero bytes (rolled out by its end)
+                load32_aligned(base + 32u * l, w);
+                for (int d = 0; d < 8; d++) pw[d] = 0u;
+            } else {
+                load32_aligned(base + s - XC_SEG + 32u * l, pw);
+                load32_aligned(base + s + 32u * l, w);
+            }
+            ps = block_sums(pw, l);
+            cs = block_sums(w, l);
+            pf = block_sums_ffs(pw, l);
+            cf = block_sums_ffs(w, l);
+            uint32_t U, V, Uf, Vf;
+            {
+                const uint32_t sufA = ps.totA - ps.preA, sufC = ps.totC - ps.preC;
+                U = sufA + cs.preA - XC_SEG;
+                V = (XC_SEG + 32u * l) * sufA - sufC + 32u * l * cs.preA - cs.preC + 0x80000000u;
+                const uint32_t fA = pf.totA - pf.preA, fC = pf.totC - pf.preC;
+                Uf = fA + cf.preA;
+                Vf = (XC_SEG + 32u * l) * fA - fC + 32u * l * cf.preA - cf.preC;
+            }
+            uint64_t h[32];
+            uint64_t k1[32];
+#pragma unroll
+            for (int d = 0; d < 8; d++) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t ib = (w[d] >> (8 * k)) & 0xffu, ob = (pw[d] >> (8 * k)) & 0xffu;
+                    const uint32_t fi = ffs8(ib), fo = ffs8(ob);
+                    U += ib - ob;
+                    V += U + (uint32_t)__mul24((int)ob, -2048);
+                    Uf += fi - fo;
+                    Vf += Uf - XC_SEG * fo;
+                    const uint32_t lo = (U << 20) + V, bits = (Uf << 16) + Vf;
+                    h[4 * d + k] = ((uint64_t)bits << 36) + lo;
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < 32; t++) k1[t] = P.cache.keys[(live >> t) & 1u ? key_slot(h[t], P.cache.mask) : 0u];
+            uint32_t hit = 0;
+#pragma unroll
+            for (int t = 0; t < 32; t++) {
+                if (!((live >> t) & 1u)) continue;
+                bool x = k1[t] == h[t];
+                if (!x && k1[t] != XC_EMPTY64) {
+                    uint64_t v;
+                    x = set_find(P.cache, h[t], &v);
+                }
+                if (x) hit |= 1u << t;
+            }
+            for (;;) {
+                const uint64_t m = ballot(hit != 0u);
+                if (!m) break;
+                const int f = __ffsll((unsigned long long)m) - 1;
+                const uint32_t t = (uint32_t)__builtin_ctz(readlane(hit, f));
+                uint64_t hh = h[0];
+#pragma unroll
+                for (int tt = 1; tt < 32; tt++) hh = t == (uint32_t)tt ? h[tt] : hh;
+                hh = readlane64(hh, f);
+                if ((int)l == f) hit &= hit - 1u;
+                uint64_t v = 0;
+                if (set_find(P.cache, hh, &v)) tail_candidate(P, b, readlane(q0, f) + t, hh, uniform((uint32_t)v), cl, &ncl);
+            }
+        }
+        __syncthreads();
+        if (wave == 0) {  // sorted by window end into the buffer's collision records
+            const uint32_t n = min(ncl, COLL_CAP);
+            const uint4 e = l < n ? cl[l] : make_uint4(NONE, 0u, 0u, NONE);
+            uint32_t rank = 0;
+            for (uint32_t k = 0; k < n; k++) rank += readlane(e.x, (int)k) < e.x ? 1u : 0u;
+            if (l < n) P.coll[b * COLL_CAP + rank] = e;
+            if (l == 0) P.coll_cnt[b] = ncl;
+        }
+        __syncthreads();
     }
 }
 

@@ -46,6 +46,8 @@ enum : uint32_t {
     CTL_SCAN_NEXT = 10,  // k_scan work counter (chunks handed out); k_resolve resets it
     CTL_COUNT = 11,      // the cache's segment count after the last k_alloc (for the host)
     CTL_DUPS = 12,       // k_emit entered hashes the cache held (a duplicate enter: the host replays)
+    CTL_AFAIL = 13,      // an anchor-scanned sub-batch needs the exact scan
+    CTL_ANCLESS = 14,    // (the cache's scratch words: ~slot of its first segment without an anchor)
     CTL_WORDS = 16
 };
 constexpr uint32_t ERR_CAPACITY = 1, ERR_TOKENS = 2, ERR_DECLS = 4;  // (ERR_PACK_CAP = 8 below)
@@ -147,8 +149,33 @@ struct PlanDev {
     // COLL_CAP: then the host cannot replay the buffer).
     uint4 *coll;
     uint32_t *coll_cnt;
+    // Anchor index.  anc_run: the run hashes anchors (k_blockhash: records and
+    // block anchors) and indexes every segment it enters (k_emit); anc_scan: this sub-batch's
+    // first-round scan takes its events from the index (k_ascan) instead of testing every window
+    // end (k_scan).
+    uint32_t anc_run, anc_scan;
+    AncSet canc;               // the cache's anchor table (its filter: the cache's)
+    AncSet danc;               // the declaration set's (its filter: amix)
+    uint32_t *amix;            // anchor filter of cache | predicted declarations
+    uint64_t *anc_of;          // [seg_cap] anchor key of every indexed segment (ANC_NONE: anchorless)
+    uint32_t *aundo;           // [seg_cap] the anchor-table slot its insert took (NONE: none)
+    uint64_t *blk_anc;         // [blocks] anchor key of every aligned block (k_blockhash)
+    uint64_t *rec;             // [groups * REC_CAP] input anchors: fp << 19 | group position << 5 | run - 1
+    uint32_t *rec_cnt;         // [groups] records (| REC_OVF: more than REC_CAP)
+    uint32_t *rec_blk;         // [groups * 8] the first record of each block of the group
+    const uint32_t *buf_grp0;  // [nb + 1] first k_blockhash group of every buffer
+    // the cache's word: ~slot of its first segment entered without an anchor (0: none; kept on
+    // the device, as the emits after a run's early publication set it: k_ascan reads it)
+    uint32_t *anc_bad;
 };
 constexpr uint32_t COLL_CAP = 16;
+constexpr uint32_t BLK_GROUP = 8;    // aligned blocks per k_blockhash group (one wave)
+constexpr uint32_t REC_CAP = 1024;  // anchor records per k_blockhash group (16 KiB; random data: ~256)
+constexpr uint32_t REC_OVF = 0x80000000u;
+__device__ __forceinline__ uint64_t rec_make(uint64_t fp, uint32_t pos, uint32_t n)
+{
+    return (fp << 19) | ((uint64_t)pos << 5) | (uint64_t)(n - 1u);
+}
 constexpr uint32_t SF_NOFLUSH = 1u;
 constexpr uint32_t BP_DECL = 0x80000000u;  // blk_pref: predicted declaration | D slot
 constexpr uint32_t BC_DIFF = 0x80000000u;  // blk_cmp: the block differs from the cached segment
@@ -188,6 +215,13 @@ struct ScanArgs {
     uint32_t unit;    // chunks per work unit (the plan's scan granularity, <= SCAN_UNIT)
     const uint32_t *filt;  // level-1 image (set's filter, or P.fmix for set | set2), filt_words words
     uint32_t filt_words;
+};
+// k_ascan: one wave per chunk of [ck_lo, ck_hi), events from the anchor records
+struct AScanArgs {
+    PlanDev P;
+    Layer L;
+    uint32_t ck_lo, ck_hi;
+    int shadow;
 };
 struct ResolveArgs {
     PlanDev P;
@@ -254,13 +288,19 @@ __global__ void k_pack_offsets(PackArgs a);
 __global__ void k_pack_copy(PackArgs a);
 __global__ void k_resolve(ResolveArgs a);
 __global__ void k_walk(WalkArgs a);
-template <bool PREDICT> __global__ void k_blockhash(DeclArgs a);
+template <bool PREDICT, bool ANC> __global__ void k_blockhash(DeclArgs a);
+__global__ void k_ascan(AScanArgs a);
+__global__ void k_anc_backfill(PlanDev P, uint32_t from, uint32_t to, uint32_t *ctl);
+__global__ void k_anc_undo(AncSet s, const uint32_t *aundo, uint32_t from, uint32_t to, uint4 *filt, const uint4 *snap);
+__global__ void k_anc_rehash(AncSet to, const uint64_t *anc_of, uint32_t n, uint32_t *aslot, uint32_t *owner);
+__global__ void k_anc_owner(uint32_t *aundo, const uint32_t *aslot, uint32_t n, const uint32_t *owner);
+__global__ void k_tailcheck(PlanDev P, uint32_t nb);
 __global__ void k_blockpredict(DeclArgs a);
 __global__ void k_or_words(uint4 *dst, const uint4 *a, const uint4 *b, uint32_t n);
 __global__ void k_alloc(EmitArgs a);
 __global__ void k_clear_set(DevSet s, uint32_t n_lo, uint32_t n_full, uint4 *l2mix, const uint4 *cache_l2,
                             uint32_t *fmix, const uint32_t *cache_filt, uint32_t fold, const uint32_t *count,
-                            uint32_t *count_out, uint32_t *ctl_zero);
+                            uint32_t *count_out, uint32_t *ctl_zero, AncSet danc, uint4 *amix, const uint4 *cache_afilt);
 __global__ void k_hash_segments(const uint8_t *segs, uint64_t n, uint64_t *out);
 __global__ void k_window_hashes(const uint8_t *in, uint32_t n, uint64_t *out);
 __global__ void k_undo(DevSet cache, const uint2 *undo, uint32_t from, uint32_t to);

@@ -263,8 +263,10 @@ static uint32_t pow2_at_least(uint64_t x, uint32_t minimum)
 
 struct HostSet {
     DevSet d{};
+    AncSet a{};  // the anchor table: keys sized like the full table; a cache's
+                 // own filter, a declaration set's the plan's combined one (amix)
     uint32_t n_lo = 0, n_full = 0;
-    int alloc(uint64_t entries)
+    int alloc(uint64_t entries, bool own_afilt)
     {
         n_full = pow2_at_least(entries * 2, 1024);
         n_lo = pow2_at_least(entries * 4, 1024);
@@ -278,6 +280,9 @@ struct HostSet {
         HIPCHK(dmalloc(&d.vals, (size_t)n_full * 8));
         d.lo_mask = n_lo - 1;
         d.mask = n_full - 1;
+        HIPCHK(dmalloc(&a.keys, (size_t)n_full * 8));
+        if (own_afilt) HIPCHK(dmalloc(&a.filt, (size_t)ANC_FILT_WORDS * 4));
+        a.mask = n_full - 1;
         return XC_OK;
     }
     int clear(hipStream_t s)
@@ -288,9 +293,11 @@ struct HostSet {
         HIPCHK(hipMemsetAsync(d.lo_zero, 0, 4, s));
         HIPCHK(hipMemsetAsync(d.keys, 0xFF, (size_t)n_full * 8, s));
         HIPCHK(hipMemsetAsync(d.vals, 0xFF, (size_t)n_full * 8, s));
+        HIPCHK(hipMemsetAsync(a.keys, 0xFF, (size_t)n_full * 8, s));
+        if (a.filt) HIPCHK(hipMemsetAsync(a.filt, 0, (size_t)ANC_FILT_WORDS * 4, s));
         return XC_OK;
     }
-    void release()
+    void release(bool own_afilt)
     {
         dfree(d.filt);
         dfree(d.l2);
@@ -298,7 +305,10 @@ struct HostSet {
         dfree(d.lo_zero);
         dfree(d.keys);
         dfree(d.vals);
+        dfree(a.keys);
+        if (own_afilt) dfree(a.filt);
         d = DevSet{};
+        a = AncSet{};
     }
 };
 
@@ -364,6 +374,16 @@ struct xc_cache {
     xc_plan *pend_enc = nullptr;
     void *pend_dec = nullptr;
     int engine = 0;
+    // anchor index: segments [0, anc_upto) are in it (runs without anchors and
+    // other enter paths append behind it: a backfill catches up before an anchor run); anc_bad:
+    // the first segment without an anchor (NONE: none), which keeps the cache on the exact scan
+    uint64_t *anc_of = nullptr;  // device [cap]
+    uint32_t *aundo = nullptr;   // device [cap]
+    uint32_t anc_upto = 0, anc_bad = NONE;
+    uint32_t *snap_afilt = nullptr;
+    uint32_t snap_anc_upto = 0;
+    bool anc_dirty = false;  // entries indexed since the snapshot (a restore takes them out)
+    uint32_t anc_bad_word = 0;  // (host source of the device word's reset)
 };
 
 static int cache_settle(xc_cache *c);
@@ -456,6 +476,10 @@ static PlanDev cache_plandev(xc_cache *c)
     P.seg_cap = (uint32_t)c->cap;
     P.undo = c->undo;
     P.ctl = c->ctl;
+    P.canc = c->set.a;
+    P.anc_of = c->anc_of;
+    P.aundo = c->aundo;
+    P.anc_bad = c->ctl + CTL_ANCLESS;
     return P;
 }
 
@@ -469,11 +493,14 @@ extern "C" int xc_cache_create(xc_ctx *ctx, uint64_t cap, xc_cache **out)
     c->cap = cap;
     c->dev_limit = SEG_DEV_MAX;
     c->dev_cap = std::min(cap, c->dev_limit);
-    if ((rc = c->set.alloc(cap))) return rc;
+    if ((rc = c->set.alloc(cap, true))) return rc;
     HIPCHK(dmalloc(&c->segs, (size_t)c->dev_cap * XC_SEG + 4096));
     if ((rc = cache_spill_to(c, c->dev_cap, cap))) return rc;
     HIPCHK(dmalloc(&c->count, 4));
     HIPCHK(dmalloc(&c->undo, (size_t)cap * sizeof(uint2)));
+    HIPCHK(dmalloc(&c->anc_of, (size_t)cap * 8));
+    HIPCHK(dmalloc(&c->aundo, (size_t)cap * 4));
+    HIPCHK(dmalloc(&c->snap_afilt, (size_t)ANC_FILT_WORDS * 4));
     HIPCHK(dmalloc(&c->ctl, CTL_WORDS * 4));
     HIPCHK(dmalloc(&c->snap_filt, XC_FILT_WORDS * 4));
     HIPCHK(dmalloc(&c->snap_lo_zero, 4));
@@ -507,7 +534,10 @@ extern "C" int xc_cache_destroy(xc_cache *c)
     if (!c) return XC_OK;
     hipSetDevice(c->ctx->dev);
     hipDeviceSynchronize();  // pooled memory is reused at once: every stream must be done with it
-    c->set.release();
+    c->set.release(true);
+    dfree(c->anc_of);
+    dfree(c->aundo);
+    dfree(c->snap_afilt);
     dfree(c->segs);
     for (uint8_t *h : c->spill) hipHostFree(h);
     dfree(c->d_spill);
@@ -531,6 +561,55 @@ static int cache_count_host(xc_cache *c, uint32_t *n)
     return XC_OK;
 }
 
+// The anchor index serves a memory cache (a COSS mirror's lookups all go through
+// its Store) whose every segment has an anchor.
+static bool cache_anc_ok(const xc_cache *c) { return c->mem && !c->engine && c->anc_bad == NONE; }
+
+// Index the segments entered since the index last caught up (the count known on the host).
+static int cache_anc_catch_up(xc_cache *c)
+{
+    const uint32_t cnt = (uint32_t)std::min<int64_t>(c->host_count, (int64_t)c->cap);
+    if (c->host_count < 0 || c->anc_upto >= cnt) return XC_OK;
+    hipStream_t s = c->ctx->stream;
+    const uint32_t n = cnt - c->anc_upto;
+    hipLaunchKernelGGL(k_anc_backfill, dim3(std::min<uint32_t>((n + 3) / 4, 8192)), dim3(256), 0, s, cache_plandev(c),
+                       c->anc_upto, cnt, c->ctl);
+    HIPCHK(hipGetLastError());
+    uint32_t bad = 0;
+    HIPCHK(hipMemcpyAsync(&bad, c->ctl + CTL_ANCLESS, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (bad) c->anc_bad = std::min(c->anc_bad, ~bad);
+    c->anc_upto = cnt;
+    c->anc_dirty = true;
+    return XC_OK;
+}
+
+// After a restore: the device's anchorless word as of the snapshot (a segment without an anchor
+// below the snapshot's count was learned by the snapshot's catch-up).
+static int cache_anc_bad_reset(xc_cache *c)
+{
+    if (c->anc_bad >= c->snap_count) c->anc_bad = NONE;
+    c->anc_bad_word = c->anc_bad == NONE ? 0u : ~c->anc_bad;
+    HIPCHK(hipMemcpyAsync(c->ctl + CTL_ANCLESS, &c->anc_bad_word, 4, hipMemcpyHostToDevice, c->ctx->stream));
+    return XC_OK;
+}
+
+// A restore's part of the anchor index: the keys of the segments indexed since the snapshot out,
+// its filter back (enqueued).
+static int cache_anc_restore(xc_cache *c)
+{
+    if (!c->anc_dirty) return XC_OK;
+    hipStream_t s = c->ctx->stream;
+    const uint32_t to = std::max(c->anc_upto, c->snap_count);
+    const uint32_t n = std::max<uint32_t>(to - c->snap_count, ANC_FILT_WORDS / 4);
+    hipLaunchKernelGGL(k_anc_undo, dim3(std::min<uint32_t>((n + 255) / 256, 2048)), dim3(256), 0, s, c->set.a,
+                       (const uint32_t *)c->aundo, c->snap_count, to, (uint4 *)c->set.a.filt, (const uint4 *)c->snap_afilt);
+    HIPCHK(hipGetLastError());
+    c->anc_upto = std::min(c->anc_upto, c->snap_anc_upto);
+    c->anc_dirty = false;
+    return cache_anc_bad_reset(c);
+}
+
 // Rebuild the cache's tables for `ncap` segments, keeping the entries with a segment index below
 // `keep` (and, with drop_dead, only the live ones): the undo log is rewritten for the new slots and
 // the segment store copied when the capacity changes; the filters depend on the keys only and are
@@ -551,13 +630,23 @@ static int cache_rebuild(xc_cache *c, uint64_t ncap, uint32_t keep, bool drop_de
     HostSet ns;
     uint8_t *segs = nullptr;
     uint2 *undo = nullptr;
-    uint32_t *owner = nullptr;
-    if ((rc = ns.alloc(ncap))) return rc;
+    uint32_t *owner = nullptr, *aundo = nullptr, *aslot = nullptr, *aowner = nullptr;
+    uint64_t *anc_of = nullptr;
+    const uint32_t akept = std::min(kept, c->anc_upto);  // segments whose anchors move along
+    if ((rc = ns.alloc(ncap, true))) return rc;
     if ((move_segs && dmalloc(&segs, (size_t)ndev * XC_SEG + 4096) != hipSuccess) ||
-        dmalloc(&undo, (size_t)ncap * sizeof(uint2)) != hipSuccess || dmalloc(&owner, (size_t)ns.n_lo * 4) != hipSuccess) {
-        ns.release();
+        dmalloc(&undo, (size_t)ncap * sizeof(uint2)) != hipSuccess || dmalloc(&owner, (size_t)ns.n_lo * 4) != hipSuccess ||
+        dmalloc(&anc_of, (size_t)ncap * 8) != hipSuccess || dmalloc(&aundo, (size_t)ncap * 4) != hipSuccess ||
+        dmalloc(&aslot, (size_t)std::max<uint32_t>(akept, 1) * 4) != hipSuccess ||
+        dmalloc(&aowner, (size_t)ns.n_full * 4) != hipSuccess) {
+        ns.release(true);
         dfree(segs);
         dfree(undo);
+        dfree(owner);
+        dfree(anc_of);
+        dfree(aundo);
+        dfree(aslot);
+        dfree(aowner);
         return fail(XC_ENOSPC, "device cache capacity exhausted (device memory)");
     }
     HIPCHK(hipMemcpyAsync(ns.d.filt, c->set.d.filt, XC_FILT_WORDS * 4, hipMemcpyDeviceToDevice, s));
@@ -579,9 +668,31 @@ static int cache_rebuild(xc_cache *c, uint64_t ncap, uint32_t keep, bool drop_de
                            undo, kept, (const uint32_t *)owner);
         HIPCHK(hipGetLastError());
     }
+    // the anchor index: the kept segments' keys into the new table (the filter depends on the
+    // keys only and is copied), the undo slots to their oldest owners
+    HIPCHK(hipMemsetAsync(ns.a.keys, 0xFF, (size_t)ns.n_full * 8, s));
+    HIPCHK(hipMemcpyAsync(ns.a.filt, c->set.a.filt, (size_t)ANC_FILT_WORDS * 4, hipMemcpyDeviceToDevice, s));
+    if (akept) {
+        HIPCHK(hipMemcpyAsync(anc_of, c->anc_of, (size_t)akept * 8, hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipMemsetAsync(aowner, 0xFF, (size_t)ns.n_full * 4, s));
+        const uint32_t ab = std::min<uint32_t>((akept + 255) / 256, 8192);
+        hipLaunchKernelGGL(k_anc_rehash, dim3(ab), dim3(256), 0, s, ns.a, (const uint64_t *)anc_of, akept, aslot, aowner);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(k_anc_owner, dim3(ab), dim3(256), 0, s, aundo, (const uint32_t *)aslot, akept,
+                           (const uint32_t *)aowner);
+        HIPCHK(hipGetLastError());
+    }
     if (kept != count) HIPCHK(hipMemcpyAsync(c->count, &kept, 4, hipMemcpyHostToDevice, s));
     HIPCHK(hipStreamSynchronize(s));
-    c->set.release();
+    dfree(aslot);
+    dfree(aowner);
+    dfree(c->anc_of);
+    dfree(c->aundo);
+    c->anc_of = anc_of;
+    c->aundo = aundo;
+    c->anc_upto = akept;
+    if (c->anc_bad >= kept) c->anc_bad = NONE;
+    c->set.release(true);
     if (move_segs) {
         dfree(c->segs);
         c->segs = segs;
@@ -727,7 +838,12 @@ extern "C" int xc_cache_snapshot(xc_cache *c)
     }
     if ((rc = cache_count_host(c, &c->snap_count))) return rc;
     c->host_count = c->snap_count;
+    // (the snapshot includes the anchor index: a restore then leaves nothing to backfill)
+    if (cache_anc_ok(c) && (rc = cache_anc_catch_up(c))) return rc;
     hipStream_t s = c->ctx->stream;
+    HIPCHK(hipMemcpyAsync(c->snap_afilt, c->set.a.filt, (size_t)ANC_FILT_WORDS * 4, hipMemcpyDeviceToDevice, s));
+    c->snap_anc_upto = std::min(c->anc_upto, c->snap_count);
+    c->anc_dirty = false;
     HIPCHK(hipMemcpyAsync(c->snap_filt, c->set.d.filt, XC_FILT_WORDS * 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(c->snap_lo_zero, c->set.d.lo_zero, 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(c->snap_count_dev, c->count, 4, hipMemcpyDeviceToDevice, s));
@@ -750,7 +866,12 @@ static int cache_restore_rebuilt(xc_cache *c)
     HIPCHK(hipMemcpyAsync(c->set.d.filt, c->snap_filt, XC_FILT_WORDS * 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(c->set.d.lo_zero, c->snap_lo_zero, 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(c->set.d.l2, c->snap_l2, (size_t)XC_L2_WORDS * 8, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->set.a.filt, c->snap_afilt, (size_t)ANC_FILT_WORDS * 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(c->count, &c->snap_count, 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+    c->anc_upto = std::min(c->anc_upto, c->snap_anc_upto);
+    c->anc_dirty = false;
+    if ((rc = cache_anc_bad_reset(c))) return rc;
     HIPCHK(hipStreamSynchronize(s));
     c->snap_gen = c->gen;
     c->host_count = c->snap_count;
@@ -773,7 +894,7 @@ static int cache_restore_async(xc_cache *c, uint32_t cur_count)
     HIPCHK(hipMemcpyAsync(c->set.d.lo_zero, c->snap_lo_zero, 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(c->count, &c->snap_count, 4, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(c->set.d.l2, c->snap_l2, (size_t)XC_L2_WORDS * 8, hipMemcpyDeviceToDevice, s));
-    return XC_OK;
+    return cache_anc_restore(c);
 }
 
 // The model as it was at the snapshot (the runs since are undone: their lookups are not replayed).
@@ -807,7 +928,7 @@ extern "C" int xc_cache_restore_async(xc_cache *c)
                            (const uint32_t *)c->snap_lo_zero);
         HIPCHK(hipGetLastError());
         c->host_count = c->snap_count;
-        return XC_OK;
+        return cache_anc_restore(c);
     }
     // one kernel: table slots entered since the snapshot, filters copied back; then the count
     const uint32_t n = (uint32_t)std::max<uint64_t>(c->cap - c->snap_count, XC_L2_WORDS / 2);
@@ -818,7 +939,7 @@ extern "C" int xc_cache_restore_async(xc_cache *c)
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(c->count, c->snap_count_dev, 4, hipMemcpyDeviceToDevice, s));
     c->host_count = c->snap_count;
-    return XC_OK;
+    return cache_anc_restore(c);
 }
 
 extern "C" int xc_cache_restore(xc_cache *c)
@@ -1124,6 +1245,14 @@ struct xc_plan {
     uint64_t *h_hits = nullptr;      // pinned: the host path's lookup hits (k_hits)
     int64_t count0 = -1;             // the cache's count before a run that may enter a hash twice
     uint64_t max_new = 0;            // most segments a run can enter (sum of len / 2048 + 1)
+    // anchor index: xc_plan_set_scan's mode; this run hashes anchors (anc_run),
+    // its remaining sub-batches scan through the index (anc_scan_on), some did (anc_any)
+    int scan_mode = XC_SCAN_AUTO;
+    bool anc_run = false, anc_scan_on = false, anc_any = false, g_anc = false;
+    uint64_t ngroups = 0, nblocks = 0;
+    uint32_t *d_buf_grp0 = nullptr;
+    uint64_t *d_rec = nullptr, *d_blk_anc = nullptr;
+    uint32_t *d_rec_cnt = nullptr, *d_amix = nullptr, *d_rec_blk = nullptr;
 };
 
 static hipEvent_t ev_get(xc_plan *p)
@@ -1212,7 +1341,7 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
         maxdecl = std::max(maxdecl, decl);
         max_sub_blocks = std::max(max_sub_blocks, blocks);
         if (p->sub.back() != nbuf) p->sub.push_back((uint32_t)nbuf);
-        if ((rc = p->dset.alloc(std::max<uint64_t>(maxdecl, 64)))) return rc;
+        if ((rc = p->dset.alloc(std::max<uint64_t>(maxdecl, 64), false))) return rc;
     }
     // scan granularity: the longest chunks and units that still give every SIMD of the chip a
     // work unit in the largest sub-batch (a 16 MiB batch would otherwise keep 16 of 256 CUs busy)
@@ -1367,13 +1496,20 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
         p->grp_base.assign(nbuf + 1, 0);
         for (uint64_t i = 0; i < nbuf; i++) {
             p->grp_base[i] = (uint32_t)grp.size();
-            for (uint32_t k0 = 0; k0 < blk_base[i + 1] - blk_base[i]; k0 += 8) grp.push_back(make_uint2((uint32_t)i, k0));
+            // (a partial last block too: the anchor records cover every position)
+            const uint32_t nbk = lengths[i] >= XC_SEG ? (uint32_t)((lengths[i] + XC_SEG - 1) / XC_SEG) : 0u;
+            for (uint32_t k0 = 0; k0 < nbk; k0 += 8) grp.push_back(make_uint2((uint32_t)i, k0));
         }
         p->grp_base[nbuf] = (uint32_t)grp.size();
         HIPCHK(dmalloc(&p->d_blk_grp, std::max<size_t>(grp.size(), 1) * sizeof(uint2)));
         if (!grp.empty())
             HIPCHK(hipMemcpyAsync(p->d_blk_grp, grp.data(), grp.size() * sizeof(uint2), hipMemcpyHostToDevice, s));
         P.blk_grp = p->d_blk_grp;
+        p->ngroups = grp.size();
+        p->nblocks = nblk;
+        HIPCHK(dmalloc(&p->d_buf_grp0, (nbuf + 1) * 4));
+        HIPCHK(hipMemcpyAsync(p->d_buf_grp0, p->grp_base.data(), (nbuf + 1) * 4, hipMemcpyHostToDevice, s));
+        P.buf_grp0 = p->d_buf_grp0;
     }
     HIPCHK(dmalloc(&p->d_l2mix, (size_t)XC_L2_WORDS * 8));
     P.l2mix = p->d_l2mix;
@@ -1497,7 +1633,13 @@ extern "C" int xc_plan_destroy(xc_plan *p)
     if (p->cs) hipStreamSynchronize(p->cs);
     p->S.release();
     p->D.release();
-    p->dset.release();
+    p->dset.release(false);
+    dfree(p->d_buf_grp0);
+    dfree(p->d_rec);
+    dfree(p->d_rec_cnt);
+    dfree(p->d_rec_blk);
+    dfree(p->d_blk_anc);
+    dfree(p->d_amix);
     dfree(p->d_buf_off);
     dfree(p->d_out_off);
     dfree(p->d_buf_len);
@@ -1589,6 +1731,73 @@ extern "C" int xc_plan_stats(xc_plan *p, xc_run_stats *st)
 {
     if (!p || !st) return fail(XC_EINVAL, "null");
     *st = p->stats;
+    return XC_OK;
+}
+
+extern "C" int xc_plan_set_scan(xc_plan *p, int mode)
+{
+    if (!p || mode < XC_SCAN_AUTO || mode > XC_SCAN_ANCHOR) return fail(XC_EINVAL, "scan mode");
+    if (p->inflight) return fail(XC_EBUSY, "a run of this plan is in flight");
+    p->scan_mode = mode;
+    return XC_OK;
+}
+
+// XC_ANCHOR_MIN_KEYS (default): the cached + new segments from which the anchor index replaces the
+// exact scan in XC_SCAN_AUTO (below it the exact scan's level-1 filter still sorts out nearly
+// every window end).  The environment XC_SCAN=exact|anchor overrides a plan's AUTO mode (tests).
+static const uint64_t ANCHOR_MIN_KEYS = 1u << 16;
+static uint64_t anc_min_keys()
+{
+    const char *e = getenv("XC_ANCHOR_MIN_KEYS");
+    return e ? (uint64_t)atoll(e) : ANCHOR_MIN_KEYS;
+}
+static int scan_mode_of(const xc_plan *p)
+{
+    if (p->scan_mode != XC_SCAN_AUTO) return p->scan_mode;
+    const char *e = getenv("XC_SCAN");
+    if (e && !strcmp(e, "exact")) return XC_SCAN_EXACT;
+    if (e && !strcmp(e, "anchor")) return XC_SCAN_ANCHOR;
+    return XC_SCAN_AUTO;
+}
+
+// Decide whether a run uses the anchor index (the cache's count known on the host): its arrays on
+// first use, the index caught up with segments entered without it.
+static int plan_anchor_setup(xc_plan *p)
+{
+    xc_cache *c = p->cache;
+    p->anc_run = false;
+    const int mode = scan_mode_of(p);
+    if (mode != XC_SCAN_EXACT && cache_anc_ok(c) && !p->P.stream_st && p->nb && c->host_count >= 0) {
+        const uint64_t keys = (uint64_t)c->host_count + p->max_new;
+        p->anc_run = mode == XC_SCAN_ANCHOR || keys >= anc_min_keys();
+    }
+    if (p->anc_run) {
+        hipStream_t s = c->ctx->stream;
+        if (!p->d_rec) {
+            HIPCHK(dmalloc(&p->d_rec, std::max<uint64_t>(p->ngroups, 1) * REC_CAP * 8));
+            HIPCHK(dmalloc(&p->d_rec_cnt, std::max<uint64_t>(p->ngroups, 1) * 4));
+            HIPCHK(dmalloc(&p->d_rec_blk, std::max<uint64_t>(p->ngroups, 1) * BLK_GROUP * 4));
+            HIPCHK(hipMemsetAsync(p->d_rec_blk, 0, std::max<uint64_t>(p->ngroups, 1) * BLK_GROUP * 4, s));
+            HIPCHK(dmalloc(&p->d_blk_anc, std::max<uint64_t>(p->nblocks, 1) * 8));
+            HIPCHK(dmalloc(&p->d_amix, (size_t)ANC_FILT_WORDS * 4));
+            HIPCHK(hipMemsetAsync(p->d_rec_cnt, 0, std::max<uint64_t>(p->ngroups, 1) * 4, s));
+            p->dset.a.filt = p->d_amix;
+            p->P.rec = p->d_rec;
+            p->P.rec_cnt = p->d_rec_cnt;
+            p->P.rec_blk = p->d_rec_blk;
+            p->P.blk_anc = p->d_blk_anc;
+            p->P.amix = p->d_amix;
+            p->P.danc = p->dset.a;
+        }
+        int rc = cache_anc_catch_up(c);
+        if (rc) return rc;
+        if (c->anc_bad != NONE) p->anc_run = false;  // (a segment without an anchor: exact)
+    }
+    p->P.anc_run = p->anc_run ? 1u : 0u;
+    p->P.anc_scan = 0;
+    p->anc_scan_on = p->anc_run;
+    p->anc_any = false;
+    if (p->anc_run) c->anc_dirty = true;
     return XC_OK;
 }
 
@@ -1754,6 +1963,18 @@ static int launch_scan(xc_plan *p, const Layer &L, const DevSet &set, uint32_t c
     return XC_OK;
 }
 
+// The anchor scan of chunks [ck_lo, ck_hi) into layer S.
+static int launch_ascan(xc_plan *p, uint32_t ck_lo, uint32_t ck_hi, int shadow)
+{
+    if (ck_hi <= ck_lo) return XC_OK;
+    AScanArgs a{p->P, p->P.S, ck_lo, ck_hi, shadow};
+    KSpan span(p, XC_K_SCAN);
+    if (p->timing) p->ktimes.scan_bytes += p->chunk_bytes[ck_hi] - p->chunk_bytes[ck_lo];
+    hipLaunchKernelGGL(k_ascan, dim3((ck_hi - ck_lo + 3) / 4), dim3(256), 0, p->cache->ctx->stream, a);
+    HIPCHK(hipGetLastError());
+    return XC_OK;
+}
+
 static int launch_resolve(xc_plan *p, const Layer &L, int dmode, uint32_t ck_lo, uint32_t ck_hi)
 {
     ResolveArgs a{p->P, L, dmode, ck_lo, ck_hi};
@@ -1826,10 +2047,9 @@ static int enqueue_block_hash(xc_plan *p, uint32_t k, hipEvent_t after, hipStrea
     static const bool skip = getenv("XC_ABL_SKIP_BLOCKHASH") && atoi(getenv("XC_ABL_SKIP_BLOCKHASH"));
     if (g1 > g0 && !(skip && side && p->runs_done > 0)) {
         KSpan span(p, XC_K_BLOCKHASH, st);
-        if (predict)
-            hipLaunchKernelGGL(k_blockhash<true>, dim3((g1 - g0 + 3) / 4), dim3(256), 0, st, d);
-        else
-            hipLaunchKernelGGL(k_blockhash<false>, dim3((g1 - g0 + 3) / 4), dim3(256), 0, st, d);
+        auto kern = predict ? (p->anc_run ? k_blockhash<true, true> : k_blockhash<true, false>)
+                            : (p->anc_run ? k_blockhash<false, true> : k_blockhash<false, false>);
+        hipLaunchKernelGGL(kern, dim3((g1 - g0 + 3) / 4), dim3(256), 0, st, d);
         HIPCHK(hipGetLastError());
     }
     if (side) HIPCHK(hipEventRecord(p->ev_hash[k], st));
@@ -1846,9 +2066,11 @@ static int launch_first_round(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t s1,
     const uint32_t ck_lo = p->chunk0[j0], ck_hi = p->chunk0[s1];
     p->stats.outer_rounds++;
     // the set's clear (and, first in a run, the control words' clear)
+    const bool anc = p->P.anc_scan != 0;
     hipLaunchKernelGGL(k_clear_set, dim3(1024), dim3(256), 0, s, p->P.dset, p->dset.n_lo, p->dset.n_full,
                        (uint4 *)p->d_l2mix, (const uint4 *)p->P.cache.l2, p->d_fmix, (const uint32_t *)p->P.cache.filt,
-                       p->P.fmix_fold, p->P.seg_count, p->P.sb_count + sb, p->zero_ctl ? p->P.ctl : nullptr);
+                       p->P.fmix_fold, p->P.seg_count, p->P.sb_count + sb, p->zero_ctl ? p->P.ctl : nullptr,
+                       p->dset.a, anc ? (uint4 *)p->d_amix : nullptr, (const uint4 *)p->P.canc.filt);
     HIPCHK(hipGetLastError());
     p->zero_ctl = false;
     const bool inline_hash = p->next_hash <= sb;
@@ -1872,7 +2094,11 @@ static int launch_first_round(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t s1,
         HIPCHK(hipEventRecord(p->ev_go[sb], s));
         if ((rc = enqueue_block_hash(p, sb + 1, p->ev_go[sb], p->hs))) return rc;
     }
-    if ((rc = launch_scan(p, p->P.S, p->P.cache, ck_lo, ck_hi, &p->P.dset, shadow))) return rc;
+    if (anc) {
+        if ((rc = launch_ascan(p, ck_lo, ck_hi, shadow))) return rc;
+    } else if ((rc = launch_scan(p, p->P.S, p->P.cache, ck_lo, ck_hi, &p->P.dset, shadow))) {
+        return rc;
+    }
     if ((rc = launch_resolve(p, p->P.S, 2, ck_lo, ck_hi))) return rc;
     return launch_walk_round(p, j0, s1, 0, shadow);
 }
@@ -1896,6 +2122,11 @@ static int encode_sub_async(xc_plan *p, uint32_t sb)
     const uint32_t j0 = p->sub[sb], s1 = p->sub[sb + 1];
     int rc;
     p->stats.sub_batches++;
+    p->P.anc_scan = p->anc_scan_on ? 1u : 0u;
+    if (p->anc_scan_on) {
+        p->anc_any = true;
+        p->stats.anchor_scans++;
+    }
     if ((rc = launch_first_round(p, sb, j0, s1, p->shadow))) return rc;
     if ((rc = launch_emit(p, sb, j0, s1, sb))) return rc;
     return launch_pack(p, j0, s1);
@@ -1909,6 +2140,7 @@ static int encode_sub_sync(xc_plan *p, uint32_t sb, uint32_t *ctl)
     const uint32_t s1 = p->sub[sb + 1];
     uint32_t j0 = p->sub[sb];
     int rc;
+    p->P.anc_scan = 0;  // (the exact scan: every window end against the cache)
     while (j0 < s1) {
         const uint32_t ck_lo = p->chunk0[j0], ck_hi = p->chunk0[s1];
         if ((rc = launch_first_round(p, sb, j0, s1, 0))) return rc;
@@ -1964,7 +2196,7 @@ static int graph_launch(xc_plan *p)
     if (rc) return rc;
     const size_t nsub = p->sub.size() - 1;
     if (!p->gexec || p->g_in != p->P.in || p->g_out != p->P.out || p->g_len != p->P.out_len ||
-        p->g_stream != p->P.stream_st) {
+        p->g_stream != p->P.stream_st || p->g_anc != p->anc_run) {
         if (p->gexec) {
             HIPCHK(hipGraphExecDestroy(p->gexec));
             p->gexec = nullptr;
@@ -1992,10 +2224,12 @@ static int graph_launch(xc_plan *p)
             p->g_stats.sub_batches -= st0.sub_batches;
             p->g_stats.outer_rounds -= st0.outer_rounds;
             p->g_stats.walk_rounds -= st0.walk_rounds;
+            p->g_stats.anchor_scans -= st0.anchor_scans;
             p->g_in = p->P.in;
             p->g_out = p->P.out;
             p->g_len = p->P.out_len;
             p->g_stream = p->P.stream_st;
+            p->g_anc = p->anc_run;
             p->g_publish = publish;
         } else {
             p->gexec = nullptr;
@@ -2019,6 +2253,8 @@ static int graph_launch(xc_plan *p)
     p->stats.sub_batches += p->g_stats.sub_batches;
     p->stats.outer_rounds += p->g_stats.outer_rounds;
     p->stats.walk_rounds += p->g_stats.walk_rounds;
+    p->stats.anchor_scans += p->g_stats.anchor_scans;
+    p->anc_any = p->g_stats.anchor_scans != 0;
     p->next_hash = (uint32_t)nsub;  // (the graph hashed every sub-batch's blocks)
     p->pass_published = p->g_publish;
     return record_ctl(p);
@@ -2054,6 +2290,10 @@ extern "C" int xc_encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out,
         p->P.seg_count = cp.seg_count;
         p->P.seg_cap = cp.seg_cap;
         p->P.undo = cp.undo;
+        p->P.canc = cp.canc;
+        p->P.anc_of = cp.anc_of;
+        p->P.aundo = cp.aundo;
+        p->P.anc_bad = cp.anc_bad;
         p->cache_gen = c->gen;
         if (p->gexec) {
             HIPCHK(hipGraphExecDestroy(p->gexec));
@@ -2071,6 +2311,7 @@ extern "C" int xc_encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out,
         while (f < MIX_FOLD_MAX && ((uint64_t)XC_FILT_WORDS * 32u >> (f + 1)) >= 16u * keys) f++;
         p->P.fmix_fold = f;
     }
+    if ((rc = plan_anchor_setup(p))) return rc;
     p->cache->host_count = -1;
     if (p->sub.size() > 1) p->zero_ctl = true;  // (the first k_clear_set clears the control words)
     else HIPCHK(hipMemsetAsync(p->P.ctl, 0, CTL_WORDS * 4, s));
@@ -2123,6 +2364,13 @@ static int encode_finish(xc_plan *p)
         HIPCHK(hipMemsetAsync(p->P.ctl + CTL_ABORT, 0, 4, s));
         if (ctl[CTL_ERROR]) break;
         p->stats.redone++;
+        if (ctl[CTL_AFAIL]) {
+            // the anchor index cannot decide this sub-batch: the exact scan redoes it, and the
+            // rest of the run (a collision or an anchorless segment may concern later ones too)
+            HIPCHK(hipMemsetAsync(p->P.ctl + CTL_AFAIL, 0, 4, s));
+            p->anc_scan_on = false;
+            p->stats.anchor_fallbacks++;
+        }
         if (ctl[CTL_SHADOW]) p->stats.shadow_misses++;
         // that sub-batch, step by step (its pipeline state is discarded and redone)
         if ((rc = encode_sub_sync(p, (uint32_t)si, ctl))) return rc;
@@ -2151,6 +2399,25 @@ static int encode_finish(xc_plan *p)
     if (ctl[CTL_ERROR] & ERR_PACK_CAP) return fail(XC_EINVAL, "packed output capacity too small");
     if (ctl[CTL_ERROR]) return fail(XC_EDEVICE, "internal encode error " + std::to_string(ctl[CTL_ERROR]));
     xc_cache *c = p->cache;
+    if (p->anc_run) {
+        // every segment of the run is indexed; one without an anchor keeps the cache exact (the
+        // emit flags it on the device after the run's early publication: a later anchor scan
+        // falls back, and the host learns it from there)
+        if (p->sub.size() > 1) c->anc_upto = ctl[CTL_COUNT];
+        if (p->stats.anchor_fallbacks) {
+            uint32_t bad = 0;
+            HIPCHK(hipMemcpyAsync(&bad, c->ctl + CTL_ANCLESS, 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            if (bad) c->anc_bad = std::min(c->anc_bad, ~bad);
+        }
+    }
+    if (p->anc_any && c->mem && !c->engine && p->nb) {
+        // the recent window's collision lookups that the anchor scans did not look for (enqueued:
+        // the run's lookup hits are replayed after it)
+        hipLaunchKernelGGL(k_tailcheck, dim3(std::min<uint32_t>(p->nb, 4u * c->ctx->n_cu)), dim3(256), 0, s, p->P,
+                           p->nb);
+        HIPCHK(hipGetLastError());
+    }
     if (c->mem && !c->engine) {
         if (ctl[CTL_DUPS]) {
             // a carried candidate entered a hash the cache held: undone, the host replays the run

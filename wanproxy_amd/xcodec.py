@@ -39,7 +39,7 @@ SYMBOLS = [
     "xc_coss_open", "xc_coss_close", "xc_coss_cache", "xc_coss_count", "xc_coss_stats", "xc_coss_lookup",
     "xc_coss_enter", "xc_coss_encode_batch_host", "xc_coss_decode_batch_host", "xc_coss_store_lookup",
     "xc_coss_store_enter", "xc_coss_encode_streams", "xc_encode_submit", "xc_encode_poll", "xc_encode_wait",
-    "xc_plan_set_completion", "xc_dplan_set_completion",
+    "xc_plan_set_completion", "xc_dplan_set_completion", "xc_plan_set_scan",
 ]
 STREAM_FLUSH = 1  # XC_STREAM_FLUSH
 
@@ -60,7 +60,8 @@ class RunStats(C.Structure):
                 ("out_bytes", C.c_uint64), ("sub_batches", C.c_uint32),
                 ("walk_rounds", C.c_uint32), ("outer_rounds", C.c_uint32),
                 ("dense_chunks", C.c_uint32), ("redone", C.c_uint32),
-                ("shadow_misses", C.c_uint32)]
+                ("shadow_misses", C.c_uint32), ("anchor_scans", C.c_uint32),
+                ("anchor_fallbacks", C.c_uint32)]
 
 
 class DecodeStats(C.Structure):
@@ -118,6 +119,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.xc_encode_poll.argtypes = [_vp, C.POINTER(C.c_int)]
     lib.xc_encode_wait.argtypes = [_vp]
     lib.xc_plan_set_completion.argtypes = [_vp, C.c_int]
+    lib.xc_plan_set_scan.argtypes = [_vp, C.c_int]
     lib.xc_plan_stats.argtypes = [_vp, C.POINTER(RunStats)]
     lib.xc_encode_batch_host.argtypes = [_vp, _u8p, _u64p, _u64p, C.c_uint64, _u8p, _u64p, _u64p,
                                          _u64p]
@@ -585,6 +587,11 @@ class EncodePlan:
         its last device writes complete in the order of the context stream (synchronize with
         ``Context.sync()`` or the device before reading the outputs from another stream)."""
         _check(load_library().xc_plan_set_completion(self.h, 1 if stream_ordered else 0))
+
+    def set_scan(self, mode: str) -> None:
+        """xc_plan_set_scan: "auto" (default), "exact" or "anchor" (DESIGN.md §4.5)."""
+        m = {"auto": 0, "exact": 1, "anchor": 2}[mode]
+        _check(load_library().xc_plan_set_scan(self.h, m))
 
     def submit(self, d_in: int, d_out: int, d_len: int) -> None:
         """Enqueue a run and return at once (xc_encode_submit); finish it with poll() / wait()."""
