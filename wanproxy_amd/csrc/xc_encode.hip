@@ -449,135 +449,165 @@ template __global__ void k_scan<4>(ScanArgs);
 template __global__ void k_scan<5>(ScanArgs);
 
 // ---------------------------------------------------------------- k_ascan ---------------
-// The first-round scan of an anchor-scanned sub-batch, one wave per chunk.  Its
-// events are the aligned windows (always events, as in k_scan) and the window ends the anchor
-// index proposes: an input anchor record (fingerprint fp, position a, a run of n) whose
-// fingerprint the cache or the predicted declarations index as (fp, j) proposes q = a + k + 2047
-// - j for k < n.  Every window equal to an indexed segment is among them (superset: k_resolve
-// decides each exactly).  The records of the 1984 positions before the chunk count too (their
-// proposals can end in it).  Events are collected in an LDS bitmask: sorted and deduplicated.
-constexpr uint32_t ASCAN_WAVES = 4;
-__global__ __launch_bounds__(64 * ASCAN_WAVES) void k_ascan(AScanArgs a)
+// The first-round scan of an anchor-scanned sub-batch.  Its events are the
+// aligned windows (always events, as in k_scan) and the window ends the anchor index proposes: an
+// input anchor record (fingerprint fp, position a, a run of n) whose fingerprint the cache or the
+// predicted declarations index as (fp, j) proposes q = a + k + 2047 - j for k < n.  Every window
+// equal to an indexed segment is among them (superset: k_resolve decides each exactly).
+//
+// k_aprop: one thread per record (a workgroup per k_blockhash group of the sub-batch): the
+// combined anchor filter (amix, 2 MB, L2-resident), for its few positives the two tables, and
+// every proposal (not aligned, not in a predicted REF's shadow) appended to its chunk's list
+// (pcnt / pq).  k_aevents: one lane per chunk writes the aligned windows (no proposal: the common
+// case); a chunk with proposals is sorted and merged by its whole wave in an LDS bitmask.
+
+// (APROP_GROUPS groups per workgroup: every thread's record and filter loads of all of them in
+// flight together; one group per workgroup left the kernel latency-bound)
+constexpr uint32_t APROP_GROUPS = 8;
+__global__ __launch_bounds__(256) void k_aprop(AScanArgs a)
 {
-    if (aborted(a.P)) return;
-    __shared__ uint32_t bitsl[ASCAN_WAVES][CHUNK_BLOCKS * XC_SEG / 32];
     const PlanDev &P = a.P;
-    const uint32_t wave = threadIdx.x >> 6, l = lane_id();
-    const uint32_t c = a.ck_lo + blockIdx.x * ASCAN_WAVES + wave;
-    if (c >= a.ck_hi) return;
-    auto wave_sync = []() {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    };
-    uint32_t *bm = bitsl[wave];
+    if (aborted(P)) return;
     if (uniform(*(volatile const uint32_t *)P.anc_bad)) {  // a segment the index cannot find
-        if (l == 0) {
-            a.L.cnt[c] = 0u;
-            atomicOr(&P.ctl[CTL_AFAIL], 8u);
-        }
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&P.ctl[CTL_AFAIL], 8u);
         return;
     }
-    const uint4 d = P.chunk_desc[c];
-    const uint32_t c0 = uniform(d.x), c1 = uniform(d.y) & 0x3FFFFFFFu;
-    const uint32_t b = uniform(P.chunks[c].x);
-    const uint32_t W = P.chunk_len / 32u;
-    const uint32_t cblk = a.shadow ? uniform(P.chunk_blk[c]) : 0u;
-    for (uint32_t i = l; i < W; i += 64u) bm[i] = 0u;
-    wave_sync();
-    // aligned windows: the block is cached or a predicted declaration (k_resolve decides which)
-    for (uint32_t q = c0 + (XC_SEG - 1u) + XC_SEG * l; q < c1; q += 64u * XC_SEG)
-        atomicOr(&bm[(q - c0) >> 5], 1u << ((q - c0) & 31u));
-    // the records of blocks lo >> 11 .. (c1 - 1) >> 11 (one or two groups), loaded 256 at a time
-    // (four per lane, every load in flight together), then their filter words likewise
-    const uint32_t lo = c0 > 1984u ? c0 - 1984u : 0u;
-    const uint32_t gb = uniform(P.buf_grp0[b]);
-    const uint32_t bl = lo >> 11, bh = (c1 - 1u) >> 11;
+    const uint32_t g0 = a.g_lo + blockIdx.x * APROP_GROUPS;
+    uint32_t cnt[APROP_GROUPS];
+    uint2 gr[APROP_GROUPS];
+#pragma unroll
+    for (uint32_t k = 0; k < APROP_GROUPS; k++) {
+        const bool ok = g0 + k < a.g_hi;
+        cnt[k] = ok ? P.rec_cnt[g0 + k] : 0u;
+        gr[k] = ok ? P.blk_grp[g0 + k] : make_uint2(0u, 0u);
+    }
     bool ovf = false;
-    for (uint32_t gg = bl >> 3; gg <= bh >> 3; gg++) {
-        const uint32_t g = gb + gg;
-        const uint32_t cnt = uniform(P.rec_cnt[g]);
-        if (cnt & REC_OVF) {
-            ovf = true;
-            break;
-        }
-        const uint32_t x = gg == (bl >> 3) ? (bl & 7u) : 0u, y = gg == (bh >> 3) ? (bh & 7u) : 7u;
-        const uint32_t r0 = uniform(P.rec_blk[g * BLK_GROUP + x]);
-        const uint32_t r1 = y == 7u ? cnt : min(cnt, uniform(P.rec_blk[g * BLK_GROUP + y + 1u]));
-        const uint32_t gpos = gg << 14;
-        for (uint32_t i0 = r0; i0 < r1; i0 += 256u) {
-            uint64_t r[4];
-            uint32_t fw[4];
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const uint32_t i = i0 + 64u * k + l;
-                r[k] = i < r1 ? P.rec[(size_t)g * REC_CAP + i] : ~0ull;
-            }
+    for (uint32_t k = 0; k < APROP_GROUPS; k++) ovf |= (cnt[k] & REC_OVF) != 0u;
+    if (ovf) {  // records overflowed (a long run of one byte value, say): the exact scan
+        if (threadIdx.x == 0) atomicOr(&P.ctl[CTL_AFAIL], 4u);
+        return;
+    }
+    uint32_t cmax = 0;
 #pragma unroll
-            for (int k = 0; k < 4; k++) fw[k] = P.amix[r[k] != ~0ull ? anc_fword(anc_mix(r[k] >> 19)) : 0u];
+    for (uint32_t k = 0; k < APROP_GROUPS; k++) cmax = max(cmax, cnt[k]);
+    for (uint32_t i = threadIdx.x; i < cmax; i += 256u) {
+        uint64_t r[APROP_GROUPS];
+        uint32_t fw[APROP_GROUPS];
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                if (r[k] == ~0ull) continue;
-                const uint64_t fp = r[k] >> 19;
-                const uint32_t ap = gpos + (((uint32_t)r[k] >> 5) & 0x3FFFu), nr = ((uint32_t)r[k] & 31u) + 1u;
-                // proposals of the run end in [ap, ap + nr - 1 + 1984]
-                if (!(ap + nr + 1983u >= c0 && ap < c1 && anc_ftest(fw[k], anc_mix(fp)))) continue;
+        for (uint32_t k = 0; k < APROP_GROUPS; k++) r[k] = i < cnt[k] ? P.rec[(size_t)(g0 + k) * REC_CAP + i] : ~0ull;
 #pragma unroll
-                for (int tb = 0; tb < 2; tb++) {
-                    const AncSet &S = tb ? P.danc : P.canc;
-                    uint32_t kk = anc_home(fp, S.mask);
-                    for (;;) {
-                        const uint64_t key = S.keys[kk];
-                        if (key == XC_EMPTY64) break;
-                        if ((key >> 11) == fp) {
-                            const uint32_t j = (uint32_t)key & 2047u;
-                            for (uint32_t e = 0; e < nr; e++) {
-                                const uint32_t aa = ap + e, q = aa + (XC_SEG - 1u) - j;
-                                if (aa < j || q < c0 || q >= c1 || ((q + 1u) & (XC_SEG - 1u)) == 0u) continue;
-                                // REF shadow: the 2047 window ends after a predicted REF are not looked up
-                                if (a.shadow && q >= XC_SEG && blk_cached(P.blk_pref[cblk + (q >> 11) - 1u])) continue;
-                                atomicOr(&bm[(q - c0) >> 5], 1u << ((q - c0) & 31u));
-                            }
+        for (uint32_t k = 0; k < APROP_GROUPS; k++) fw[k] = P.amix[r[k] != ~0ull ? anc_fword(anc_mix(r[k] >> 19)) : 0u];
+#pragma unroll
+        for (uint32_t k = 0; k < APROP_GROUPS; k++) {
+            if (r[k] == ~0ull) continue;
+            const uint64_t fp = r[k] >> 19;
+            if (!anc_ftest(fw[k], anc_mix(fp))) continue;
+            const uint32_t b = gr[k].x, gpos = gr[k].y * XC_SEG;
+            const uint32_t len = P.buf_len[b], ck0 = P.buf_chunk0[b], cblk = P.blk_base[b];
+            const uint32_t ap = gpos + (((uint32_t)r[k] >> 5) & 0x3FFFu), nr = ((uint32_t)r[k] & 31u) + 1u;
+#pragma unroll
+            for (int tb = 0; tb < 2; tb++) {
+                const AncSet &S = tb ? P.danc : P.canc;
+                uint32_t kk = anc_home(fp, S.mask);
+                for (;;) {
+                    const uint64_t key = S.keys[kk];
+                    if (key == XC_EMPTY64) break;
+                    if ((key >> 11) == fp) {
+                        const uint32_t j = (uint32_t)key & 2047u;
+                        for (uint32_t e = 0; e < nr; e++) {
+                            const uint32_t aa = ap + e, q = aa + (XC_SEG - 1u) - j;
+                            if (aa < j || q >= len || ((q + 1u) & (XC_SEG - 1u)) == 0u) continue;
+                            // REF shadow: the 2047 window ends after a predicted REF are not looked up
+                            if (a.shadow && q >= XC_SEG && blk_cached(P.blk_pref[cblk + (q >> 11) - 1u])) continue;
+                            const uint32_t c = ck0 + q / P.chunk_len;
+                            const uint32_t slot = atomicAdd(&a.pcnt[c], 1u);
+                            if (slot < PROP_CAP) a.pq[(size_t)c * PROP_CAP + slot] = q;
                         }
-                        kk = (kk + 1u) & S.mask;
                     }
+                    kk = (kk + 1u) & S.mask;
                 }
             }
         }
     }
-    if (ovf) {  // records overflowed (e.g. a long run of one byte value): the exact scan redoes it
-        if (l == 0) {
-            a.L.cnt[c] = 0u;
-            atomicOr(&P.ctl[CTL_AFAIL], 4u);
-        }
+}
+
+__global__ __launch_bounds__(256) void k_aevents(AScanArgs a)
+{
+    const PlanDev &P = a.P;
+    __shared__ uint32_t bitsl[4][CHUNK_BLOCKS * XC_SEG / 32];
+    const uint32_t wave = threadIdx.x >> 6, l = lane_id();
+    const uint32_t c = a.ck_lo + blockIdx.x * 256u + threadIdx.x;
+    const bool live = c < a.ck_hi;
+    if (aborted(P)) {
+        if (live) a.pcnt[c] = 0u;
         return;
     }
-    wave_sync();
-    uint32_t tot = 0;
-    for (uint32_t i = l; i < W; i += 64u) tot += (uint32_t)__popc(bm[i]);
-    tot = wave_sum(tot);
-    if (tot <= EV_CAP) {
-        uint32_t base = 0;
-        for (uint32_t i0 = 0; i0 < W; i0 += 64u) {
-            const uint32_t i = i0 + l;
-            uint32_t v = i < W ? bm[i] : 0u;
-            const uint32_t k = (uint32_t)__popc(v), incl = wave_incl_scan(k);
-            uint32_t o = base + incl - k;
-            while (v) {
-                const uint32_t bit = (uint32_t)__builtin_ctz(v);
-                v &= v - 1u;
-                a.L.pos[c * EV_CAP + o++] = c0 + 32u * i + bit;
-            }
-            base += readlane(incl, 63);
-        }
-        if (l == 0) a.L.cnt[c] = tot;
-    } else {
-        for (uint32_t i = l; i < W; i += 64u) a.L.bits[(size_t)c * W + i] = bm[i];
-        if (l == 0) {
-            a.L.cnt[c] = EV_DENSE | EV_CAP;
-            atomicAdd(&P.ctl[CTL_DENSE], 1u);
-        }
+    uint32_t c0 = 0, c1 = 0, n = 0;
+    if (live) {
+        const uint4 d = P.chunk_desc[c];
+        c0 = d.x;
+        c1 = d.y & 0x3FFFFFFFu;
+        n = a.pcnt[c];
     }
+    if (n > PROP_CAP) {
+        atomicOr(&P.ctl[CTL_AFAIL], 16u);
+        n = 0;
+    }
+    if (live && n == 0) {  // the aligned windows only (k_resolve sorts nothing: they are in order)
+        uint32_t k = 0;
+        for (uint32_t q = c0 + (XC_SEG - 1u); q < c1; q += XC_SEG) a.L.pos[c * EV_CAP + k++] = q;
+        a.L.cnt[c] = k;
+    }
+    // chunks with proposals: each by the whole wave (LDS bitmask: sorted, deduplicated)
+    uint32_t *bm = bitsl[wave];
+    const uint32_t W = P.chunk_len / 32u;
+    for (uint64_t m = ballot(live && n > 0); m; m &= m - 1) {
+        const int f = __ffsll((unsigned long long)m) - 1;
+        const uint32_t cc = readlane(c, f), cs = readlane(c0, f), ce = readlane(c1, f), nn = readlane(n, f);
+        for (uint32_t i = l; i < W; i += 64u) bm[i] = 0u;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t q = cs + (XC_SEG - 1u) + XC_SEG * l; q < ce; q += 64u * XC_SEG)
+            atomicOr(&bm[(q - cs) >> 5], 1u << ((q - cs) & 31u));
+        if (l < nn) {
+            const uint32_t q = a.pq[(size_t)cc * PROP_CAP + l];
+            atomicOr(&bm[(q - cs) >> 5], 1u << ((q - cs) & 31u));
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint32_t tot = 0;
+        for (uint32_t i = l; i < W; i += 64u) tot += (uint32_t)__popc(bm[i]);
+        tot = wave_sum(tot);
+        if (tot <= EV_CAP) {
+            uint32_t base = 0;
+            for (uint32_t i0 = 0; i0 < W; i0 += 64u) {
+                const uint32_t i = i0 + l;
+                uint32_t v = i < W ? bm[i] : 0u;
+                const uint32_t k = (uint32_t)__popc(v), incl = wave_incl_scan(k);
+                uint32_t o = base + incl - k;
+                while (v) {
+                    const uint32_t bit = (uint32_t)__builtin_ctz(v);
+                    v &= v - 1u;
+                    a.L.pos[cc * EV_CAP + o++] = cs + 32u * i + bit;
+                }
+                base += readlane(incl, 63);
+            }
+            if (l == 0) a.L.cnt[cc] = tot;
+        } else {
+            for (uint32_t i = l; i < W; i += 64u) a.L.bits[(size_t)cc * W + i] = bm[i];
+            if (l == 0) {
+                a.L.cnt[cc] = EV_DENSE | EV_CAP;
+                atomicAdd(&P.ctl[CTL_DENSE], 1u);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (live) a.pcnt[c] = 0u;  // (clean for the next sub-batch)
 }
 
 // ------------------------------------------------------------- k_resolve ----------------
@@ -2294,20 +2324,6 @@ __device__ __forceinline__ bool tail_visible(const PlanDev &P, uint32_t b, uint3
     return false;
 }
 
-// A looked-up window end q whose full hash h the cache holds in slot v (wave-uniform): a collision
-// lookup when the entry was there at that point and its bytes differ.
-__device__ __forceinline__ void tail_candidate(const PlanDev &P, uint32_t b, uint32_t q, uint64_t h, uint32_t v,
-                                               uint4 *cl, uint32_t *ncl)
-{
-    if (!tail_visible(P, b, q, v)) return;
-    const uint8_t *win = P.in + P.buf_off[b] + q - (XC_SEG - 1u);
-    if (wave_equal2048(win, seg_at(P.segs, v))) return;  // (the walk's REF: not a collision)
-    if (lane_id() == 0) {
-        const uint32_t k = atomicAdd(ncl, 1u);
-        if (k < COLL_CAP) cl[k] = make_uint4(q, (uint32_t)h, (uint32_t)(h >> 32), NONE);
-    }
-}
-
 // Window sums of the bits half (w = ffs(byte), xcodec_hash.h:93-135) before a lane's first position,
 // as block_sums gives those of the bytes half.
 __device__ __forceinline__ BlockSums block_sums_ffs(const uint32_t w[8], uint32_t l)
@@ -2330,154 +2346,159 @@ __device__ __forceinline__ BlockSums block_sums_ffs(const uint32_t w[8], uint32_
     return s;
 }
 
-constexpr uint32_t TAIL_REFS = MAX_BUF / XC_SEG;  // REF tokens a buffer can hold
-
-__global__ __launch_bounds__(256) void k_tailcheck(PlanDev P, uint32_t nb)
+// The first buffer of the run's tail (its last buffers whose REF hits reach the window's 64, all of
+// the run when fewer), wave-uniform.
+__device__ __forceinline__ uint32_t tail_first(const PlanDev &P, uint32_t nb)
 {
-    __shared__ uint32_t jstar, ncl, nrefs;
-    __shared__ uint4 cl[COLL_CAP];
-    __shared__ uint32_t refe[TAIL_REFS];  // the buffer's REF window ends, ascending
-    const uint32_t wave = threadIdx.x >> 6, l = lane_id();
-    if (wave == 0) {
-        // the last buffers whose REF hits reach the window's 64 (all of the run when fewer)
-        uint32_t acc = 0, j = 0;
-        for (uint32_t e = nb; e > 0; e = e > 64u ? e - 64u : 0u) {
-            const bool ok = l < e;
-            const uint32_t v = ok ? P.buf_nref[e - 1u - l] : 0u;
-            const uint32_t incl = wave_incl_scan(v);
-            const uint64_t m = ballot(ok && acc + incl >= 64u);
-            if (m) {
-                j = e - 1u - (uint32_t)(__ffsll((unsigned long long)m) - 1);
-                break;
-            }
-            acc += readlane(incl, 63);
-        }
-        if (l == 0) jstar = j;
+    const uint32_t l = lane_id();
+    uint32_t acc = 0;
+    for (uint32_t e = nb; e > 0; e = e > 64u ? e - 64u : 0u) {
+        const bool ok = l < e;
+        const uint32_t v = ok ? P.buf_nref[e - 1u - l] : 0u;
+        const uint32_t incl = wave_incl_scan(v);
+        const uint64_t m = ballot(ok && acc + incl >= 64u);
+        if (m) return e - 1u - (uint32_t)(__ffsll((unsigned long long)m) - 1);
+        acc += readlane(incl, 63);
     }
-    __syncthreads();
-    const uint32_t j0 = jstar;
-    for (uint32_t b = j0 + blockIdx.x; b < nb; b += gridDim.x) {
-        const uint32_t len = P.buf_len[b];
+    return 0u;
+}
+
+// One wave per aligned block of the tail's buffers (window ends [s, s + 2048); block 0: the first
+// window, 2047), all of them in flight across the chip: full hashes by the rolling recurrences of
+// both halves (k_scan's, plus the bits half), the looked-up ends (not a REF's, not in the 2047 ends
+// after one) probed in the cache's full table; collisions into the buffer's scratch list (tcnt,
+// tlist), which k_tailfinal sorts into its records.
+__global__ __launch_bounds__(256) void k_tailcheck(PlanDev P, uint32_t nb, uint32_t *tcnt, uint4 *tlist)
+{
+    __shared__ uint32_t refs[4][4];
+    const uint32_t wave = threadIdx.x >> 6, l = lane_id();
+    const uint32_t j0 = tail_first(P, nb);
+    const uint32_t g0 = P.buf_grp0[j0], g1 = P.buf_grp0[nb];
+    for (uint32_t u = (g0 * BLK_GROUP) + blockIdx.x * 4u + wave; u < g1 * BLK_GROUP; u += gridDim.x * 4u) {
+        const uint2 gr = P.blk_grp[u / BLK_GROUP];
+        const uint32_t b = gr.x, k = gr.y + u % BLK_GROUP;
+        const uint32_t len = P.buf_len[b], s = k * XC_SEG;
+        if (s >= len || len < XC_SEG) continue;
         const uint8_t *base = P.in + P.buf_off[b];
-        if (wave == 0) {  // the REF window ends (tokens are in position order)
+        // the REF window ends e in [s - 2047, s + 2047] (at most two: REFs are >= 2048 apart)
+        uint32_t nr = 0;
+        {
             const uint32_t tb = P.tok_base[b], n = P.tok_cnt[b];
-            uint32_t k = 0;
             for (uint32_t t0 = 0; t0 < n; t0 += 64u) {
                 const uint32_t t = t0 + l;
-                const bool r = t < n && P.tok_op[tb + t] == OP_REF;
+                uint32_t e = 0;
+                bool r = false;
+                if (t < n && P.tok_op[tb + t] == OP_REF) {
+                    e = P.tok_seg[tb + t] + (XC_SEG - 1u);
+                    r = e + (XC_SEG - 1u) >= s && e < s + XC_SEG;
+                }
                 const uint64_t m = ballot(r);
-                if (r && k + mbcnt(m) < TAIL_REFS) refe[k + mbcnt(m)] = P.tok_seg[tb + t] + (XC_SEG - 1u);
-                k += (uint32_t)__popcll(m);
+                if (r && nr + mbcnt(m) < 4u) refs[wave][nr + mbcnt(m)] = e;
+                nr += (uint32_t)__popcll(m);
             }
-            if (l == 0) {
-                nrefs = min(k, TAIL_REFS);
-                ncl = 0;
+            nr = min(nr, 4u);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        const uint32_t q0 = s + 32u * l;
+        uint32_t shadow = 0;  // bit t: end q0 + t is not looked up
+        for (uint32_t r = 0; r < nr; r++) {
+            const uint32_t e = refs[wave][r];
+            const uint32_t a = e > q0 ? e - q0 : 0u;
+            const uint32_t z = e + (XC_SEG - 1u) >= q0 + 31u ? 32u : (e + XC_SEG > q0 ? e + XC_SEG - q0 : 0u);
+            if (z > a && a < 32u) shadow |= (z - a >= 32u ? ~0u : ((1u << (z - a)) - 1u)) << a;
+        }
+        uint32_t live = ~0u;
+        if (s == 0) live = l == 63u ? 0x80000000u : 0u;  // (block 0: its last end only)
+        if (q0 + 32u > len) live &= q0 >= len ? 0u : (1u << (len - q0)) - 1u;
+        live &= ~shadow;
+        if (!ballot(live != 0u)) continue;
+        uint32_t pw[8], w[8];
+        if (s == 0) {  // the first window: block 0 after 2048 zero bytes (rolled out by its end)
+            load32_aligned(base + 32u * l, w);
+            for (int d = 0; d < 8; d++) pw[d] = 0u;
+        } else {
+            load32_aligned(base + s - XC_SEG + 32u * l, pw);
+            load32_aligned(base + s + 32u * l, w);
+        }
+        const BlockSums ps = block_sums(pw, l), cs = block_sums(w, l);
+        const BlockSums pf = block_sums_ffs(pw, l), cf = block_sums_ffs(w, l);
+        const uint32_t sufA = ps.totA - ps.preA, sufC = ps.totC - ps.preC;
+        uint32_t U = sufA + cs.preA - XC_SEG;
+        uint32_t V = (XC_SEG + 32u * l) * sufA - sufC + 32u * l * cs.preA - cs.preC + 0x80000000u;
+        const uint32_t fA = pf.totA - pf.preA, fC = pf.totC - pf.preC;
+        uint32_t Uf = fA + cf.preA;
+        uint32_t Vf = (XC_SEG + 32u * l) * fA - fC + 32u * l * cf.preA - cf.preC;
+        uint64_t h[32];
+        uint64_t k1[32];
+#pragma unroll
+        for (int d = 0; d < 8; d++) {
+#pragma unroll
+            for (int kk = 0; kk < 4; kk++) {
+                const uint32_t ib = (w[d] >> (8 * kk)) & 0xffu, ob = (pw[d] >> (8 * kk)) & 0xffu;
+                const uint32_t fi = ffs8(ib), fo = ffs8(ob);
+                U += ib - ob;
+                V += U + (uint32_t)__mul24((int)ob, -2048);
+                Uf += fi - fo;
+                Vf += Uf - XC_SEG * fo;
+                h[4 * d + kk] = ((uint64_t)((Uf << 16) + Vf) << 36) + ((U << 20) + V);
             }
         }
-        __syncthreads();
-        const uint32_t nr = nrefs;
-        // window ends [s, s + 2048) of block s (s = 0: the first window, 2047): full hashes by the
-        // rolling recurrences of both halves (k_scan's, plus the bits half), the looked-up ones
-        // (not a REF's and not in the 2047 ends after one) probed in the cache's full table
-        for (uint32_t s = XC_SEG * wave; s < len; s += 4u * XC_SEG) {
-            uint32_t pw[8], w[8];
-            const uint32_t q0 = s + 32u * l;
-            // the REFs whose shadow [e, e + 2047] can reach this lane's ends: the last two <= q0 + 31
-            uint32_t lo_i = 0, hi_i = nr;  // first REF end > q0 + 31
-            while (lo_i < hi_i) {
-                const uint32_t mid = (lo_i + hi_i) >> 1;
-                if (refe[mid] <= q0 + 31u) lo_i = mid + 1u;
-                else hi_i = mid;
-            }
-            uint32_t shadow = 0;  // bit t: end q0 + t is not looked up
 #pragma unroll
-            for (int k = 1; k <= 2; k++) {
-                if (lo_i >= (uint32_t)k) {
-                    const uint32_t e = refe[lo_i - k];
-                    // [e, e + 2047] within [q0, q0 + 31]
-                    const uint32_t a = e > q0 ? e - q0 : 0u, z = e + (XC_SEG - 1u) >= q0 + 31u ? 32u : (e + XC_SEG > q0 ? e + XC_SEG - q0 : 0u);
-                    if (z > a) shadow |= (z - a >= 32u ? ~0u : ((1u << (z - a)) - 1u)) << a;
+        for (int t = 0; t < 32; t++) k1[t] = P.cache.keys[(live >> t) & 1u ? key_slot(h[t], P.cache.mask) : 0u];
+        uint32_t hit = 0;
+#pragma unroll
+        for (int t = 0; t < 32; t++) {
+            if (!((live >> t) & 1u)) continue;
+            bool x = k1[t] == h[t];
+            if (!x && k1[t] != XC_EMPTY64) {
+                uint64_t v;
+                x = set_find(P.cache, h[t], &v);
+            }
+            if (x) hit |= 1u << t;
+        }
+        for (;;) {
+            const uint64_t m = ballot(hit != 0u);
+            if (!m) break;
+            const int f = __ffsll((unsigned long long)m) - 1;
+            const uint32_t t = (uint32_t)__builtin_ctz(readlane(hit, f));
+            uint64_t hh = h[0];
+#pragma unroll
+            for (int tt = 1; tt < 32; tt++) hh = t == (uint32_t)tt ? h[tt] : hh;
+            hh = readlane64(hh, f);
+            if ((int)l == f) hit &= hit - 1u;
+            uint64_t v = 0;
+            if (set_find(P.cache, hh, &v)) {
+                const uint32_t q = readlane(q0, f) + t, vv = uniform((uint32_t)v);
+                if (!tail_visible(P, b, q, vv)) continue;
+                const uint8_t *win = base + q - (XC_SEG - 1u);
+                if (wave_equal2048(win, seg_at(P.segs, vv))) continue;  // (the walk's REF)
+                if (l == 0) {
+                    const uint32_t kq = atomicAdd(&tcnt[b], 1u);
+                    if (kq < COLL_CAP) tlist[(size_t)b * COLL_CAP + kq] = make_uint4(q, (uint32_t)hh, (uint32_t)(hh >> 32), NONE);
                 }
-            }
-            uint32_t live = q0 < XC_SEG - 1u ? 0u : ~0u;  // window ends >= 2047
-            if (s == 0) live = l == 63u ? 0x80000000u : 0u;  // (block 0: its last end only)
-            if (q0 + 32u > len) live &= q0 >= len ? 0u : (1u << (len - q0)) - 1u;
-            live &= ~shadow;
-            if (!ballot(live != 0u)) continue;
-            BlockSums ps, cs, pf, cf;
-            if (s == 0) {  // the first window: block 0 after 2048 zero bytes (rolled out by its end)
-                load32_aligned(base + 32u * l, w);
-                for (int d = 0; d < 8; d++) pw[d] = 0u;
-            } else {
-                load32_aligned(base + s - XC_SEG + 32u * l, pw);
-                load32_aligned(base + s + 32u * l, w);
-            }
-            ps = block_sums(pw, l);
-            cs = block_sums(w, l);
-            pf = block_sums_ffs(pw, l);
-            cf = block_sums_ffs(w, l);
-            uint32_t U, V, Uf, Vf;
-            {
-                const uint32_t sufA = ps.totA - ps.preA, sufC = ps.totC - ps.preC;
-                U = sufA + cs.preA - XC_SEG;
-                V = (XC_SEG + 32u * l) * sufA - sufC + 32u * l * cs.preA - cs.preC + 0x80000000u;
-                const uint32_t fA = pf.totA - pf.preA, fC = pf.totC - pf.preC;
-                Uf = fA + cf.preA;
-                Vf = (XC_SEG + 32u * l) * fA - fC + 32u * l * cf.preA - cf.preC;
-            }
-            uint64_t h[32];
-            uint64_t k1[32];
-#pragma unroll
-            for (int d = 0; d < 8; d++) {
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const uint32_t ib = (w[d] >> (8 * k)) & 0xffu, ob = (pw[d] >> (8 * k)) & 0xffu;
-                    const uint32_t fi = ffs8(ib), fo = ffs8(ob);
-                    U += ib - ob;
-                    V += U + (uint32_t)__mul24((int)ob, -2048);
-                    Uf += fi - fo;
-                    Vf += Uf - XC_SEG * fo;
-                    const uint32_t lo = (U << 20) + V, bits = (Uf << 16) + Vf;
-                    h[4 * d + k] = ((uint64_t)bits << 36) + lo;
-                }
-            }
-#pragma unroll
-            for (int t = 0; t < 32; t++) k1[t] = P.cache.keys[(live >> t) & 1u ? key_slot(h[t], P.cache.mask) : 0u];
-            uint32_t hit = 0;
-#pragma unroll
-            for (int t = 0; t < 32; t++) {
-                if (!((live >> t) & 1u)) continue;
-                bool x = k1[t] == h[t];
-                if (!x && k1[t] != XC_EMPTY64) {
-                    uint64_t v;
-                    x = set_find(P.cache, h[t], &v);
-                }
-                if (x) hit |= 1u << t;
-            }
-            for (;;) {
-                const uint64_t m = ballot(hit != 0u);
-                if (!m) break;
-                const int f = __ffsll((unsigned long long)m) - 1;
-                const uint32_t t = (uint32_t)__builtin_ctz(readlane(hit, f));
-                uint64_t hh = h[0];
-#pragma unroll
-                for (int tt = 1; tt < 32; tt++) hh = t == (uint32_t)tt ? h[tt] : hh;
-                hh = readlane64(hh, f);
-                if ((int)l == f) hit &= hit - 1u;
-                uint64_t v = 0;
-                if (set_find(P.cache, hh, &v)) tail_candidate(P, b, readlane(q0, f) + t, hh, uniform((uint32_t)v), cl, &ncl);
             }
         }
-        __syncthreads();
-        if (wave == 0) {  // sorted by window end into the buffer's collision records
-            const uint32_t n = min(ncl, COLL_CAP);
-            const uint4 e = l < n ? cl[l] : make_uint4(NONE, 0u, 0u, NONE);
-            uint32_t rank = 0;
-            for (uint32_t k = 0; k < n; k++) rank += readlane(e.x, (int)k) < e.x ? 1u : 0u;
-            if (l < n) P.coll[b * COLL_CAP + rank] = e;
-            if (l == 0) P.coll_cnt[b] = ncl;
+    }
+}
+
+// The tail's buffers: their collision lookups, sorted by window end, replace the walk's records
+// (one wave per buffer); the scratch counts back to zero.
+__global__ __launch_bounds__(64) void k_tailfinal(PlanDev P, uint32_t nb, uint32_t *tcnt, const uint4 *tlist)
+{
+    const uint32_t l = lane_id();
+    const uint32_t j0 = tail_first(P, nb);
+    for (uint32_t b = j0 + blockIdx.x; b < nb; b += gridDim.x) {
+        const uint32_t c = tcnt[b], n = min(c, COLL_CAP);
+        const uint4 e = l < n ? tlist[(size_t)b * COLL_CAP + l] : make_uint4(NONE, 0u, 0u, NONE);
+        uint32_t rank = 0;
+        for (uint32_t k = 0; k < n; k++) rank += readlane(e.x, (int)k) < e.x ? 1u : 0u;
+        if (l < n) P.coll[b * COLL_CAP + rank] = e;
+        if (l == 0) {
+            P.coll_cnt[b] = c;
+            tcnt[b] = 0u;
         }
-        __syncthreads();
     }
 }
 

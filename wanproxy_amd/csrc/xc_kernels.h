@@ -172,6 +172,7 @@ constexpr uint32_t COLL_CAP = 16;
 constexpr uint32_t BLK_GROUP = 8;    // aligned blocks per k_blockhash group (one wave)
 constexpr uint32_t REC_CAP = 1024;  // anchor records per k_blockhash group (16 KiB; random data: ~256)
 constexpr uint32_t REC_OVF = 0x80000000u;
+constexpr uint32_t PROP_CAP = 64;  // anchor proposals a chunk keeps (more: the exact scan redoes the sub-batch)
 __device__ __forceinline__ uint64_t rec_make(uint64_t fp, uint32_t pos, uint32_t n)
 {
     return (fp << 19) | ((uint64_t)pos << 5) | (uint64_t)(n - 1u);
@@ -222,6 +223,9 @@ struct AScanArgs {
     Layer L;
     uint32_t ck_lo, ck_hi;
     int shadow;
+    uint32_t g_lo, g_hi;  // the sub-batch's k_blockhash groups (k_aprop)
+    uint32_t *pcnt;       // [nchunks] proposals per chunk (zero between sub-batches)
+    uint32_t *pq;         // [nchunks * PROP_CAP] their window ends
 };
 struct ResolveArgs {
     PlanDev P;
@@ -289,12 +293,14 @@ __global__ void k_pack_copy(PackArgs a);
 __global__ void k_resolve(ResolveArgs a);
 __global__ void k_walk(WalkArgs a);
 template <bool PREDICT, bool ANC> __global__ void k_blockhash(DeclArgs a);
-__global__ void k_ascan(AScanArgs a);
+__global__ void k_aprop(AScanArgs a);
+__global__ void k_aevents(AScanArgs a);
 __global__ void k_anc_backfill(PlanDev P, uint32_t from, uint32_t to, uint32_t *ctl);
 __global__ void k_anc_undo(AncSet s, const uint32_t *aundo, uint32_t from, uint32_t to, uint4 *filt, const uint4 *snap);
 __global__ void k_anc_rehash(AncSet to, const uint64_t *anc_of, uint32_t n, uint32_t *aslot, uint32_t *owner);
 __global__ void k_anc_owner(uint32_t *aundo, const uint32_t *aslot, uint32_t n, const uint32_t *owner);
-__global__ void k_tailcheck(PlanDev P, uint32_t nb);
+__global__ void k_tailcheck(PlanDev P, uint32_t nb, uint32_t *tcnt, uint4 *tlist);
+__global__ void k_tailfinal(PlanDev P, uint32_t nb, uint32_t *tcnt, const uint4 *tlist);
 __global__ void k_blockpredict(DeclArgs a);
 __global__ void k_or_words(uint4 *dst, const uint4 *a, const uint4 *b, uint32_t n);
 __global__ void k_alloc(EmitArgs a);

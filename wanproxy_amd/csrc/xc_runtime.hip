@@ -1253,6 +1253,9 @@ struct xc_plan {
     uint32_t *d_buf_grp0 = nullptr;
     uint64_t *d_rec = nullptr, *d_blk_anc = nullptr;
     uint32_t *d_rec_cnt = nullptr, *d_amix = nullptr, *d_rec_blk = nullptr;
+    uint32_t *d_tcnt = nullptr;  // the tail check's collision lists (k_tailcheck / k_tailfinal)
+    uint32_t *d_pcnt = nullptr, *d_pq = nullptr;  // the anchor scan's proposals per chunk
+    uint4 *d_tlist = nullptr;
 };
 
 static hipEvent_t ev_get(xc_plan *p)
@@ -1638,6 +1641,10 @@ extern "C" int xc_plan_destroy(xc_plan *p)
     dfree(p->d_rec);
     dfree(p->d_rec_cnt);
     dfree(p->d_rec_blk);
+    dfree(p->d_tcnt);
+    dfree(p->d_pcnt);
+    dfree(p->d_pq);
+    dfree(p->d_tlist);
     dfree(p->d_blk_anc);
     dfree(p->d_amix);
     dfree(p->d_buf_off);
@@ -1778,6 +1785,12 @@ static int plan_anchor_setup(xc_plan *p)
             HIPCHK(dmalloc(&p->d_rec_cnt, std::max<uint64_t>(p->ngroups, 1) * 4));
             HIPCHK(dmalloc(&p->d_rec_blk, std::max<uint64_t>(p->ngroups, 1) * BLK_GROUP * 4));
             HIPCHK(hipMemsetAsync(p->d_rec_blk, 0, std::max<uint64_t>(p->ngroups, 1) * BLK_GROUP * 4, s));
+            HIPCHK(dmalloc(&p->d_tcnt, std::max<uint64_t>(p->nb, 1) * 4));
+            HIPCHK(hipMemsetAsync(p->d_tcnt, 0, std::max<uint64_t>(p->nb, 1) * 4, s));
+            HIPCHK(dmalloc(&p->d_tlist, std::max<uint64_t>(p->nb, 1) * COLL_CAP * sizeof(uint4)));
+            HIPCHK(dmalloc(&p->d_pcnt, std::max<uint64_t>(p->nchunks, 1) * 4));
+            HIPCHK(hipMemsetAsync(p->d_pcnt, 0, std::max<uint64_t>(p->nchunks, 1) * 4, s));
+            HIPCHK(dmalloc(&p->d_pq, std::max<uint64_t>(p->nchunks, 1) * PROP_CAP * 4));
             HIPCHK(dmalloc(&p->d_blk_anc, std::max<uint64_t>(p->nblocks, 1) * 8));
             HIPCHK(dmalloc(&p->d_amix, (size_t)ANC_FILT_WORDS * 4));
             HIPCHK(hipMemsetAsync(p->d_rec_cnt, 0, std::max<uint64_t>(p->ngroups, 1) * 4, s));
@@ -1963,14 +1976,20 @@ static int launch_scan(xc_plan *p, const Layer &L, const DevSet &set, uint32_t c
     return XC_OK;
 }
 
-// The anchor scan of chunks [ck_lo, ck_hi) into layer S.
-static int launch_ascan(xc_plan *p, uint32_t ck_lo, uint32_t ck_hi, int shadow)
+// The anchor scan of buffers [j0, s1) (chunks [ck_lo, ck_hi)) into layer S.
+static int launch_ascan(xc_plan *p, uint32_t j0, uint32_t s1, uint32_t ck_lo, uint32_t ck_hi, int shadow)
 {
     if (ck_hi <= ck_lo) return XC_OK;
-    AScanArgs a{p->P, p->P.S, ck_lo, ck_hi, shadow};
+    const uint32_t g_lo = p->grp_base[j0], g_hi = p->grp_base[s1];
+    AScanArgs a{p->P, p->P.S, ck_lo, ck_hi, shadow, g_lo, g_hi, p->d_pcnt, p->d_pq};
     KSpan span(p, XC_K_SCAN);
     if (p->timing) p->ktimes.scan_bytes += p->chunk_bytes[ck_hi] - p->chunk_bytes[ck_lo];
-    hipLaunchKernelGGL(k_ascan, dim3((ck_hi - ck_lo + 3) / 4), dim3(256), 0, p->cache->ctx->stream, a);
+    hipStream_t s = p->cache->ctx->stream;
+    if (g_hi > g_lo) {
+        hipLaunchKernelGGL(k_aprop, dim3((g_hi - g_lo + 7) / 8), dim3(256), 0, s, a);
+        HIPCHK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_aevents, dim3((ck_hi - ck_lo + 255) / 256), dim3(256), 0, s, a);
     HIPCHK(hipGetLastError());
     return XC_OK;
 }
@@ -2095,7 +2114,7 @@ static int launch_first_round(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t s1,
         if ((rc = enqueue_block_hash(p, sb + 1, p->ev_go[sb], p->hs))) return rc;
     }
     if (anc) {
-        if ((rc = launch_ascan(p, ck_lo, ck_hi, shadow))) return rc;
+        if ((rc = launch_ascan(p, j0, s1, ck_lo, ck_hi, shadow))) return rc;
     } else if ((rc = launch_scan(p, p->P.S, p->P.cache, ck_lo, ck_hi, &p->P.dset, shadow))) {
         return rc;
     }
@@ -2414,8 +2433,10 @@ static int encode_finish(xc_plan *p)
     if (p->anc_any && c->mem && !c->engine && p->nb) {
         // the recent window's collision lookups that the anchor scans did not look for (enqueued:
         // the run's lookup hits are replayed after it)
-        hipLaunchKernelGGL(k_tailcheck, dim3(std::min<uint32_t>(p->nb, 4u * c->ctx->n_cu)), dim3(256), 0, s, p->P,
-                           p->nb);
+        hipLaunchKernelGGL(k_tailcheck, dim3(4u * c->ctx->n_cu), dim3(256), 0, s, p->P, p->nb, p->d_tcnt, p->d_tlist);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(k_tailfinal, dim3(std::min<uint32_t>(p->nb, 1024u)), dim3(64), 0, s, p->P, p->nb, p->d_tcnt,
+                           (const uint4 *)p->d_tlist);
         HIPCHK(hipGetLastError());
     }
     if (c->mem && !c->engine) {
