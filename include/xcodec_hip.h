@@ -183,7 +183,7 @@ int xc_plan_stats(xc_plan *p, xc_run_stats *st);
 
 /* The first scan of a sub-batch.  XC_SCAN_AUTO (the default): the anchor index
  * when the run qualifies (a memory cache whose segments all have an anchor, fresh encoders, at
- * least XC_ANCHOR_MIN_KEYS cached + new segments), else the exact scan, which tests every window
+ * least 200000 cached + new segments, XC_ANCHOR_MIN_KEYS in the environment), else the exact scan, which tests every window
  * end against the cache.  XC_SCAN_EXACT: always the exact scan.  XC_SCAN_ANCHOR: the anchor index
  * whenever the run qualifies, whatever its size (tests).  Results are identical in every mode. */
 #define XC_SCAN_AUTO 0

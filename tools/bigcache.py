@@ -5,7 +5,8 @@ a snapshot; then cfg3 (4096 x 64 KiB, 50 % repeats of the pool, seed 0x77) with 
 The random segments never match cfg3's windows (a 64-bit hash collision aside), so every cfg3 buffer
 still equals the oracle's digests for cfg3 on the pool alone: checked.  Prints one JSON line per size:
 GiB/s, the scan's time per launch, the kernel breakdown and the filters' false-positive rates.
-usage: python tools/bigcache.py [SEGMENTS ...] (default 0 2000000 8000000)"""
+usage: python tools/bigcache.py [--scan auto|exact|anchor] [SEGMENTS ...] (default 0 2000000 8000000)
+(the scan mode of the timed cfg3 plan; the fills run in the default mode)"""
 import json
 import os
 import sys
@@ -20,7 +21,11 @@ import torch  # noqa: E402
 import wanproxy_amd as w  # noqa: E402
 from wanproxy_amd import workloads as W  # noqa: E402
 
-sizes = [int(x) for x in sys.argv[1:]] or [0, 2_000_000, 8_000_000]
+args = sys.argv[1:]
+scan = "auto"
+if args[:1] == ["--scan"]:
+    scan, args = args[1], args[2:]
+sizes = [int(x) for x in args] or [0, 2_000_000, 8_000_000]
 ctx = w.Context(0)
 gold = np.load(os.path.join(ROOT, "tests", "golden", "fullsize_digests.npz"))
 bufs = list(W.repeat_shard(4096, 0x77))
@@ -52,6 +57,7 @@ for target in sizes:
     fs = cache.filter_stats()
     cache.snapshot()
     plan = w.EncodePlan(cache, lens)
+    plan.set_scan(scan)
     plan.set_completion(True)
     arena = np.zeros(plan.in_bytes, np.uint8)
     for i, b in enumerate(bufs):
@@ -84,7 +90,10 @@ for target in sizes:
     torch.cuda.synchronize()
     plan.set_timing(False)
     kt = plan.kernel_times(reset=True)
-    rec = {"cache_segments": keys, "fill_s": round(fill_s, 1), "cfg3_GiBs": round(int(lens.sum()) / el / 2**30, 2),
+    st = plan.stats()
+    rec = {"cache_segments": keys, "scan": scan, "anchor_scans": int(st.anchor_scans),
+           "anchor_fallbacks": int(st.anchor_fallbacks), "fill_s": round(fill_s, 1),
+           "cfg3_GiBs": round(int(lens.sum()) / el / 2**30, 2),
            "ms_per_step": round(el * 1e3, 3), "scan_ms_per_launch": round(kt["ms"]["scan"] / max(1, kt["launches"]["scan"]), 4),
            "kernel_ms_per_step": {k: round(v / 3, 4) for k, v in kt["ms"].items()},
            "l1_fp": round(fs["l1_fp"], 4), "l2_fp": round(fs["l2_fp"], 4), "equals_oracle_cfg3": ok}

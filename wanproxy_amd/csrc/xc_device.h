@@ -250,17 +250,25 @@ __device__ __forceinline__ uint64_t block_group_hash(const uint32_t w[G][8])
 
 // The words of n <= G consecutive 16-byte-aligned blocks at p (lane l: bytes 32 l .. 32 l + 31 of
 // each; zeros past n), all loads issued together.
-template <int G>
+template <int G, bool NT = false>
 __device__ __forceinline__ void wave_load_blocks(const uint8_t *p, uint32_t n, uint32_t (&w)[G][8])
 {
     const uint32_t l = lane_id();
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 #pragma unroll
     for (int i = 0; i < G; i++) {
 #pragma unroll
         for (int k = 0; k < 8; k++) w[i][k] = 0u;
         if ((uint32_t)i < n) {
-            const uint4 *q = (const uint4 *)(p + (size_t)i * XC_SEG + 32u * l);
-            const uint4 x = q[0], y = q[1];
+            const v4u *q = (const v4u *)(p + (size_t)i * XC_SEG + 32u * l);
+            v4u x, y;
+            if (NT) {  // (streamed once: the L2 keeps the filters the other stream's kernels read)
+                x = __builtin_nontemporal_load(q);
+                y = __builtin_nontemporal_load(q + 1);
+            } else {
+                x = q[0];
+                y = q[1];
+            }
             w[i][0] = x.x; w[i][1] = x.y; w[i][2] = x.z; w[i][3] = x.w;
             w[i][4] = y.x; w[i][5] = y.y; w[i][6] = y.z; w[i][7] = y.w;
         }
@@ -553,7 +561,7 @@ __device__ __forceinline__ int set_insert(const DevSet &s, uint64_t h, uint64_t 
 // keep the cache out of anchor mode (the exact scan, xc_runtime.hip).
 #define ANC_G_LIMIT (1u << 26)
 #define ANC_NONE 0xFFFFFFFFFFFFFFFFull
-#define ANC_FILT_WORDS (1u << 19)  // 2 MB anchor filter (k = 2 bits in a 32-bit word), like level 2
+#define ANC_FILT_WORDS (1u << 18)  // 1 MB anchor filter (k = 2 bits in a 32-bit word): stays in an XCD's L2
 
 __device__ __forceinline__ uint64_t anc_fp(uint32_t g, uint32_t g2)
 {
@@ -563,7 +571,7 @@ __device__ __forceinline__ uint64_t anc_fp(uint32_t g, uint32_t g2)
 __device__ __forceinline__ uint64_t anc_key(uint64_t fp, uint32_t j) { return (fp << 11) | j; }
 __device__ __forceinline__ uint32_t anc_mix(uint64_t fp) { return (uint32_t)(fp ^ (fp >> 21)) * 0x2C1B3C6Du; }
 __device__ __forceinline__ uint32_t anc_home(uint64_t fp, uint32_t mask) { return (uint32_t)((fp * 0xD6E8FEB86659FD93ull) >> 37) & mask; }
-__device__ __forceinline__ uint32_t anc_fword(uint32_t g) { return g >> 13; }
+__device__ __forceinline__ uint32_t anc_fword(uint32_t g) { return g >> 14; }
 __device__ __forceinline__ uint32_t anc_fbits(uint32_t g) { return (1u << (g & 31u)) | (1u << ((g >> 5) & 31u)); }
 __device__ __forceinline__ bool anc_ftest(uint32_t w, uint32_t g) { return ((w >> (g & 31u)) & (w >> ((g >> 5) & 31u)) & 1u) != 0u; }
 
@@ -611,21 +619,59 @@ __device__ __forceinline__ uint32_t gear_prev(uint32_t sf, uint32_t first)
 
 // Anchor mask of the lane's 32 positions (bit 31 - t: position t of the lane is an anchor, before
 // any position bound); TILE: G of every position into tile[t * 64 + lane] too.
+// Per position, all full-rate VOP2/VOPC but one: g + g, then the byte added straight from its
+// dword (SDWA byte select: no extraction), and m = 2 m + (g < 2^26) as a compare into VCC and an
+// add with carry-in (the compiler's select + or forms are VOP3).  The compare of position t is
+// issued before the next position's two adds, so its VCC is read by the carry-in add two
+// instructions later (gfx950 wants a wait state between a VALU write of VCC and its read as carry).
+template <int K>
+__device__ __forceinline__ uint32_t gear_cmp_step(uint32_t &m, uint32_t g, uint32_t w)
+{
+    static_assert(K >= 0 && K < 4, "byte");
+    uint32_t gn;
+#define XC_GEAR_STEP(SEL)                                                                                       \
+    asm("v_cmp_gt_u32_e32 vcc, 0x4000000, %2\n\t"                                                              \
+        "v_add_u32_e32 %0, %2, %2\n\t"                                                                         \
+        "v_add_u32_sdwa %0, %0, %3 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:" SEL "\n\t"    \
+        "v_addc_co_u32_e32 %1, vcc, %1, %1, vcc"                                                               \
+        : "=&v"(gn), "+v"(m) : "v"(g), "v"(w) : "vcc")
+    if (K == 0) XC_GEAR_STEP("BYTE_0");
+    else if (K == 1) XC_GEAR_STEP("BYTE_1");
+    else if (K == 2) XC_GEAR_STEP("BYTE_2");
+    else XC_GEAR_STEP("BYTE_3");
+#undef XC_GEAR_STEP
+    return gn;
+}
+static_assert(ANC_G_LIMIT == 0x4000000u, "gear_cmp_step's literal");
+
+// m after the last position: its compare, a wait state, the carry-in add.
+__device__ __forceinline__ uint32_t mask_last(uint32_t m, uint32_t g)
+{
+    asm("v_cmp_gt_u32_e32 vcc, 0x4000000, %1\n\ts_nop 0\n\tv_addc_co_u32_e32 %0, vcc, %0, %0, vcc"
+        : "+v"(m) : "v"(g) : "vcc");
+    return m;
+}
+
 template <bool TILE>
 __device__ __forceinline__ uint32_t gear_mask(const uint32_t w[8], uint32_t g, uint32_t *tile)
 {
     const uint32_t l = lane_id();
+    // position 0: its G from g (no mask bit before it: the first step's compare shifts in a bit
+    // for "position -1" that the final shift-out below drops)
     uint32_t m = 0;
 #pragma unroll
     for (int d = 0; d < 8; d++) {
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            g = (g << 1) + ((w[d] >> (8 * k)) & 0xffu);
-            if (TILE) tile[(4 * d + k) * 64 + l] = g;
-            m = m + m + (g < ANC_G_LIMIT ? 1u : 0u);
-        }
+        g = gear_cmp_step<0>(m, g, w[d]);
+        if (TILE) tile[(4 * d + 0) * 64 + l] = g;
+        g = gear_cmp_step<1>(m, g, w[d]);
+        if (TILE) tile[(4 * d + 1) * 64 + l] = g;
+        g = gear_cmp_step<2>(m, g, w[d]);
+        if (TILE) tile[(4 * d + 2) * 64 + l] = g;
+        g = gear_cmp_step<3>(m, g, w[d]);
+        if (TILE) tile[(4 * d + 3) * 64 + l] = g;
     }
-    return m;
+    // 32 compares so far: position -1 (shifted out of the word by the 32nd) and positions 0..30
+    return mask_last(m, g);
 }
 
 // G at position t (wave-uniform, < 32) of every lane, from G at position -1.

@@ -1385,7 +1385,8 @@ __global__ __launch_bounds__(256) void k_blockhash(DeclArgs a)
     const uint32_t n = nfull > k0 ? min(BLK_GROUP, nfull - k0) : 0u;
     const uint32_t na = ANC ? min(BLK_GROUP, (len + XC_SEG - 1u) / XC_SEG - k0) : n;
     uint32_t w[BLK_GROUP][8];  // (kept for the compares below)
-    wave_load_blocks<BLK_GROUP>(base + (size_t)k0 * XC_SEG, na, w);
+    if (ANC && a.nt) wave_load_blocks<BLK_GROUP, true>(base + (size_t)k0 * XC_SEG, na, w);
+    else wave_load_blocks<BLK_GROUP>(base + (size_t)k0 * XC_SEG, na, w);
     const uint64_t h = block_group_hash<BLK_GROUP>(w);
     uint64_t akey = ANC_NONE;
     if (ANC)

@@ -255,6 +255,7 @@ struct DeclArgs {
     // k_blockhash on the side stream: the cache count below which entries are complete while it
     // runs (P.sb_count of the sub-batch the main stream is in); null: no block compares
     const uint32_t *limit;
+    int nt;  // k_blockhash<.., true>: non-temporal block loads (XC_BH_NT, experiments)
 };
 struct EmitArgs {
     PlanDev P;

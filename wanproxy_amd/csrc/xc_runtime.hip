@@ -219,7 +219,16 @@ extern "C" int xc_ctx_create(int dev, xc_ctx **out)
     HIPCHK(hipSetDevice(dev));
     xc_ctx *c = new xc_ctx();
     c->dev = dev;
-    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    {
+        // XC_STREAM_PRIO=1 (experiments): the context stream at the highest priority, so that its
+        // latency-bound kernels are dispatched ahead of the side stream's block hashing
+        const char *e = getenv("XC_STREAM_PRIO");
+        int lo = 0, hi = 0;
+        if (e && atoi(e) && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
+            HIPCHK(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi));
+        else
+            HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    }
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, dev));
     c->n_cu = prop.multiProcessorCount;
@@ -1325,9 +1334,13 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
         uint32_t cnt = 0;
         uint64_t decl = 0, maxdecl = 0;
         const uint64_t sub_max = sub_bytes();
+        // XC_FIRST_SUB_MB (experiments): the first sub-batch's bound (its block hashing has
+        // nothing to overlap with)
+        const char *fe = getenv("XC_FIRST_SUB_MB");
+        const uint64_t first_max = fe && atol(fe) > 0 ? (uint64_t)atol(fe) << 20 : sub_max;
         for (uint32_t i = 0; i < nbuf; i++) {
             if (lengths[i] > MAX_BUF) return fail(XC_EINVAL, "buffer longer than 1 MiB");
-            if (cnt && (bytes + lengths[i] > sub_max || cnt >= SUB_BUFS)) {
+            if (cnt && (bytes + lengths[i] > (p->sub.size() == 1 ? first_max : sub_max) || cnt >= SUB_BUFS)) {
                 p->sub.push_back(i);
                 maxdecl = std::max(maxdecl, decl);
                 max_sub_blocks = std::max(max_sub_blocks, blocks);
@@ -1522,7 +1535,14 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     // the declaration set's level-2 filter is the combined one (cache | declarations): every
     // declaration insert lands there directly, and the declaration-layer scans test a superset
     P.dset.l2 = p->d_l2mix;
-    if (!c->ctx->side) HIPCHK(hipStreamCreateWithFlags(&c->ctx->side, hipStreamNonBlocking));
+    if (!c->ctx->side) {
+        const char *e = getenv("XC_STREAM_PRIO");
+        int lo = 0, hi = 0;
+        if (e && atoi(e) && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
+            HIPCHK(hipStreamCreateWithPriority(&c->ctx->side, hipStreamNonBlocking, lo));
+        else
+            HIPCHK(hipStreamCreateWithFlags(&c->ctx->side, hipStreamNonBlocking));
+    }
     p->hs = c->ctx->side;
     HIPCHK(hipEventCreateWithFlags(&p->ev_start, hipEventDisableTiming));
     p->ev_hash.assign(p->sub.size(), nullptr);
@@ -1751,8 +1771,11 @@ extern "C" int xc_plan_set_scan(xc_plan *p, int mode)
 
 // XC_ANCHOR_MIN_KEYS (default): the cached + new segments from which the anchor index replaces the
 // exact scan in XC_SCAN_AUTO (below it the exact scan's level-1 filter still sorts out nearly
-// every window end).  The environment XC_SCAN=exact|anchor overrides a plan's AUTO mode (tests).
-static const uint64_t ANCHOR_MIN_KEYS = 1u << 16;
+// every window end and the anchors' hashing costs more than it saves: cfg5-shaped runs of 4096 /
+// 8192 / 16384 buffers, 143 k / 278 k / 549 k keys, exact 628 / 650 / 626, anchor 565 / 667 / 701
+// GiB/s, profiles/r03/crossover_r3p.txt).  The environment XC_SCAN=exact|anchor overrides a plan's
+// AUTO mode (tests).
+static const uint64_t ANCHOR_MIN_KEYS = 200000;
 static uint64_t anc_min_keys()
 {
     const char *e = getenv("XC_ANCHOR_MIN_KEYS");
@@ -2060,7 +2083,8 @@ static int enqueue_block_hash(xc_plan *p, uint32_t k, hipEvent_t after, hipStrea
     const uint32_t g0 = p->grp_base[p->sub[k]], g1 = p->grp_base[p->sub[k + 1]];
     // a range of block groups; on the side stream (sub-batch k - 1 on the main stream) the block
     // compares against the entries complete when k - 1 started
-    DeclArgs d{p->P, g0, g1, side && k > 0 ? p->P.sb_count + (k - 1) : nullptr};
+    static const int bh_nt = getenv("XC_BH_NT") ? atoi(getenv("XC_BH_NT")) : 0;
+    DeclArgs d{p->P, g0, g1, side && k > 0 ? p->P.sb_count + (k - 1) : nullptr, bh_nt};
     // XC_ABL_SKIP_BLOCKHASH=1 (timing experiments only, valid when every run reads the same input):
     // the side stream's block hashing after the plan's first run is skipped
     static const bool skip = getenv("XC_ABL_SKIP_BLOCKHASH") && atoi(getenv("XC_ABL_SKIP_BLOCKHASH"));
@@ -2068,7 +2092,10 @@ static int enqueue_block_hash(xc_plan *p, uint32_t k, hipEvent_t after, hipStrea
         KSpan span(p, XC_K_BLOCKHASH, st);
         auto kern = predict ? (p->anc_run ? k_blockhash<true, true> : k_blockhash<true, false>)
                             : (p->anc_run ? k_blockhash<false, true> : k_blockhash<false, false>);
-        hipLaunchKernelGGL(kern, dim3((g1 - g0 + 3) / 4), dim3(256), 0, st, d);
+        // XC_BH_LDS=n (experiments): n KiB of dynamic LDS per side-stream block-hashing workgroup,
+        // capping how many share a CU with the main stream's kernels
+        static const uint32_t bh_lds = getenv("XC_BH_LDS") ? (uint32_t)atoi(getenv("XC_BH_LDS")) << 10 : 0u;
+        hipLaunchKernelGGL(kern, dim3((g1 - g0 + 3) / 4), dim3(256), side ? bh_lds : 0u, st, d);
         HIPCHK(hipGetLastError());
     }
     if (side) HIPCHK(hipEventRecord(p->ev_hash[k], st));
