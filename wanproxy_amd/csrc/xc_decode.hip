@@ -152,9 +152,146 @@ __device__ __forceinline__ uint64_t dwin_be64(const DWin &w, uint32_t x)
 __device__ __forceinline__ void dclear_range(const DecDev &D, uint32_t n_lo, uint32_t n_full, uint32_t i0,
                                              uint32_t stride);
 
+// Streaming tokenizer (round 3): the stream is read in 4 KiB windows, two windows ahead of the
+// one being tokenized (lane l: bytes 64 l .. 64 l + 63 of a window, 4 dwordx4 loads), so the
+// per-EXTRACT load latency of the 1 KiB windows (one dependent round trip per payload skipped)
+// becomes a stream of independent loads.  Each window's F1 positions are a 64-bit mask per lane
+// (lane l: positions 64 l ..); its bytes go to the wave's LDS copy, from which the op byte and a
+// REF's hash bytes are read (a token whose 10 bytes cross the window's end reads them from memory).
+// Token semantics as k_dtok_win (xcodec_decoder.cc:85-173).
+constexpr uint32_t DTOK_WIN = 4096;
+
+__device__ __forceinline__ uint32_t magic_mask4(uint32_t d)
+{
+    // bytes equal to F1: x = d ^ F1F1F1F1 has zero bytes there; exact per-byte zero test
+    const uint32_t x = d ^ 0xF1F1F1F1u;
+    const uint32_t t = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;  // bit 7 of each zero byte
+    return ((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u);
+}
+
+__device__ __forceinline__ void dtok_load(uint4 (&v)[4], const uint8_t *s, uint32_t w0)
+{
+    const uint4 *q = (const uint4 *)(s + w0 + 64u * lane_id());
+#pragma unroll
+    for (int i = 0; i < 4; i++) v[i] = q[i];
+}
+
+// The window's F1 mask of lane l (bit i: position w0 + 64 l + i), positions < n only.
+__device__ __forceinline__ uint64_t dtok_mask(const uint4 (&v)[4], uint32_t w0, uint32_t n)
+{
+    uint64_t m = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t d[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+#pragma unroll
+        for (int k = 0; k < 4; k++) m |= (uint64_t)magic_mask4(d[k]) << (16 * i + 4 * k);
+    }
+    const uint32_t base = w0 + 64u * lane_id();
+    if (n < base + 64u) m = n <= base ? 0ull : m & ((1ull << (n - base)) - 1ull);
+    return m;
+}
+
 // first: also the run's prologue, spread over the tokenizer's threads (the control words, every
 // stream's provider limit, the round-0 batch provider table): three launches less.
 __global__ __launch_bounds__(64) void k_dtok(DecDev D, int fill, int first, uint32_t n_lo, uint32_t n_full)
+{
+    __shared__ uint32_t win[DTOK_WIN / 4 + 4];
+    const uint32_t j = blockIdx.x;
+    if (first) {
+        if (j == 0 && threadIdx.x < DCTL_WORDS) D.ctl[threadIdx.x] = 0u;
+        if (j < D.ns && threadIdx.x == 0) D.s_lim[j] = 0xFFFFFFFFu;
+        dclear_range(D, n_lo, n_full, j * 64u + threadIdx.x, gridDim.x * 64u);
+    }
+    if (j >= D.ns) return;
+    const uint8_t *s = D.in + D.in_off[j];
+    const uint32_t n = D.in_len[j];
+    const uint32_t tb = fill ? D.tok_base[j] : 0u;
+    const uint32_t l = lane_id();
+    uint32_t nt = 0, lb = 0, p = 0;
+    auto put = [&](uint32_t op, uint32_t le, uint64_t h) {
+        if (fill && l == 0) {
+            D.t_lb[tb + nt] = lb;
+            D.t_le[tb + nt] = le;
+            D.t_op[tb + nt] = op;
+            D.t_h[tb + nt] = h;
+        }
+        nt++;
+    };
+    const uint32_t nw = (n + DTOK_WIN - 1u) / DTOK_WIN;
+    // (only windows that start inside the stream are read: past the last, it is read again)
+    const uint32_t last = nw ? (nw - 1u) * DTOK_WIN : 0u;
+    uint4 v0[4], v1[4], v2[4];
+    dtok_load(v0, s, 0u);
+    dtok_load(v1, s, min(DTOK_WIN, last));
+    // window k from cur (its loads issued two windows earlier); window k + 2's loads into fut (the
+    // set of window k - 1): three statically named sets, so no register copy waits on a load in flight
+    auto step = [&](uint4 (&cur)[4], uint4 (&fut)[4], uint32_t k) -> bool {
+        const uint32_t w0 = k * DTOK_WIN;
+        dtok_load(fut, s, min(w0 + 2u * DTOK_WIN, last));  // (unconditional: a static vmcnt)
+        const uint64_t mask = dtok_mask(cur, w0, n);
+        // the window into LDS (the previous window's readers are done: every read was waited for)
+        uint4 *wl = (uint4 *)win + 4u * l;
+#pragma unroll
+        for (int i = 0; i < 4; i++) wl[i] = cur[i];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t base = w0 + 64u * l;
+        for (;;) {
+            uint64_t mm = mask;
+            if (p > base) mm = p - base >= 64u ? 0ull : mm & (~0ull << (p - base));
+            const uint64_t b = ballot(mm != 0ull);
+            if (!b) return false;  // no F1 in [p, window end): the literal run goes on
+            const int f = __ffsll((unsigned long long)b) - 1;
+            const uint64_t mf = ((uint64_t)readlane((uint32_t)(mm >> 32), f) << 32) | readlane((uint32_t)mm, f);
+            const uint32_t q = w0 + 64u * (uint32_t)f + (uint32_t)__builtin_ctzll(mf);
+            if (q + 1u >= n) { put(T_WAIT, q, 0); return true; }
+            const uint32_t r = q + 1u - w0;  // the op byte's window offset (<= 4096)
+            uint32_t op;
+            uint64_t h = 0;
+            if (r + 9u <= DTOK_WIN) {  // op and 8 hash bytes inside the window
+                const uint32_t i = r >> 2, o = r & 3u;
+                const uint32_t d0 = win[i], d1 = win[i + 1u], d2 = win[i + 2u];
+                op = (d0 >> (8u * o)) & 0xffu;
+                // hash bytes r + 1 .. r + 8: bytes o + 1 .. o + 8 of d0 d1 d2
+                const uint32_t a = o + 1u;  // 1..4
+                const uint32_t lo = a == 4u ? d1 : __builtin_amdgcn_alignbyte(d1, d0, a);
+                const uint32_t hi = a == 4u ? d2 : __builtin_amdgcn_alignbyte(d2, d1, a);
+                h = ((uint64_t)__builtin_bswap32(lo) << 32) | __builtin_bswap32(hi);
+            } else {
+                op = s[q + 1u];
+                if (op == 0x02u && n - q >= 10u)
+                    for (uint32_t k2 = 0; k2 < 8; k2++) h = (h << 8) | s[q + 2u + k2];
+            }
+            if (op == 0x00u) { p = q + 2u; continue; }  // escape: stays inside the literal run
+            if (op == 0x01u) {
+                if (n - q < 2u + XC_SEG) { put(T_WAIT, q, 0); return true; }
+                put(T_EXTRACT, q, 0);
+                lb = p = q + 2u + XC_SEG;
+                continue;
+            }
+            if (op == 0x02u) {
+                if (n - q < 10u) { put(T_WAIT, q, 0); return true; }
+                put(T_REF, q, h);
+                lb = p = q + 10u;
+                continue;
+            }
+            put(T_BADOP, q, 0);
+            return true;
+        }
+    };
+    bool done = false;
+    for (uint32_t k = 0; k < nw && !done; k += 3u) {
+        done = step(v0, v2, k);
+        if (!done && k + 1u < nw) done = step(v1, v0, k + 1u);
+        if (!done && k + 2u < nw) done = step(v2, v1, k + 2u);
+    }
+    if (!done) put(T_END, n, 0);
+    if (l == 0) D.tok_cnt[j] = nt;
+}
+
+// The round-2 tokenizer (kept for A/B): F1 search in 1 KiB register windows loaded on demand.
+__global__ __launch_bounds__(64) void k_dtok_win(DecDev D, int fill, int first, uint32_t n_lo, uint32_t n_full)
 {
     const uint32_t j = blockIdx.x;
     if (first) {
@@ -995,7 +1132,10 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
     const int64_t count0 = xc__cache_host_count(p->cache);
     xc__cache_count_unknown(p->cache);
     // tokens, with the prologue (control words, provider limits, round 0's provider table)
-    hipLaunchKernelGGL(k_dtok, dim3(std::max<uint32_t>(ns, 256u)), dim3(64), 0, s, D, 1, 1, p->n_lo, p->n_full);
+    // XC_DTOK_WIN=1 (experiments): the round-2 tokenizer
+    static const bool old_tok = getenv("XC_DTOK_WIN") && atoi(getenv("XC_DTOK_WIN"));
+    hipLaunchKernelGGL(old_tok ? k_dtok_win : k_dtok, dim3(std::max<uint32_t>(ns, 256u)), dim3(64), 0, s, D, 1, 1,
+                       p->n_lo, p->n_full);
     DHIP(hipGetLastError());
     // one provider-resolution round (a fresh batch table each time; round 0's came with k_dtok)
     auto resolve_round = [&](int r) -> int {

@@ -360,8 +360,33 @@ __device__ __forceinline__ void payload_load(const uint8_t *src, const uint8_t *
     r.b0 = r.a0;
     r.b1 = r.a1;
     if (head) {
-        if (l < nbody) r.b0 = load16_unaligned(src + head + 16u * l);
-        if (l + 64u < nbody) r.b1 = load16_unaligned(src + head + 1024u + 16u * l);
+        // the wire-aligned chunk of lane l is bytes head .. head + 15 of (chunk l, chunk l + 1): the
+        // next lane's words by a DPP wave shift (lane 63's successor: lane 0 of the second half),
+        // then a funnel by head bytes; no second read of src
+        const uint32_t c0[4] = {r.a0.x, r.a0.y, r.a0.z, r.a0.w}, c1[4] = {r.a1.x, r.a1.y, r.a1.z, r.a1.w};
+        uint32_t n0[4], n1[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t first1 = readlane(c1[k], 0);
+            n0[k] = (uint32_t)__builtin_amdgcn_update_dpp((int)first1, (int)c0[k], 0x130, 0xf, 0xf, false);  // wave_shl:1
+            n1[k] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c1[k], 0x130, 0xf, 0xf, false);
+        }
+        const uint32_t dh = head >> 2, bh = 8u * (head & 3u);
+        auto fun = [&](const uint32_t (&c)[4], const uint32_t (&nx)[4]) {
+            uint32_t d[8] = {c[0], c[1], c[2], c[3], nx[0], nx[1], nx[2], nx[3]};
+            uint32_t o[5];
+#pragma unroll
+            for (int k = 0; k < 5; k++)  // dwords dh .. dh + 4 of the 32 bytes (dh uniform)
+                o[k] = dh == 0 ? d[k] : dh == 1 ? d[k + 1] : dh == 2 ? d[k + 2] : d[min(k + 3, 7)];
+            uint4 v;
+            v.x = bh ? (o[0] >> bh) | (o[1] << (32u - bh)) : o[0];
+            v.y = bh ? (o[1] >> bh) | (o[2] << (32u - bh)) : o[1];
+            v.z = bh ? (o[2] >> bh) | (o[3] << (32u - bh)) : o[2];
+            v.w = bh ? (o[3] >> bh) | (o[4] << (32u - bh)) : o[3];
+            return v;
+        };
+        r.b0 = fun(c0, n0);
+        r.b1 = fun(c1, n1);
     }
     const uint32_t t0 = head + 16u * nbody;
     r.hb = l < head ? src[l] : 0u;

@@ -1256,10 +1256,12 @@ __global__ __launch_bounds__(64 * WALK_WAVES_MAX) void k_walk(WalkArgs a)
 __device__ __forceinline__ uint32_t block_predict(const PlanDev &P, uint32_t g, uint32_t b, uint32_t k, uint64_t h,
                                                   uint64_t akey);
 
+constexpr uint32_t ANC_LIST = 512;  // anchor list entries per pass (a multiple of 64)
+
 // The anchors of a k_blockhash group: G of every position of its na blocks
 // (w[i]: block i, lane l: bytes 32 l .. 32 l + 31) into tile (per wave: 32 x 64 values, then the
 // 32 values of the lane before lane 0), the block's anchors compacted into a position-ordered list
-// (list: 2048 entries per wave), then every input anchor into the group's records, 64 list entries
+// (list: ANC_LIST entries per wave, in passes), then every input anchor into the group's records, 64 list entries
 // at a time (runs of equal fingerprints at consecutive positions, at most 32 and within a 32-byte
 // lane part, as one record); returns, in lane i, the anchor key of full block i (its last anchor at
 // block offset >= 63; ANC_NONE: none).
@@ -1312,22 +1314,26 @@ __device__ __forceinline__ uint64_t group_anchors(const PlanDev &P, uint32_t g, 
         const uint32_t p0 = (k0 + i) * XC_SEG + 32u * l;
         if (p0 < 63u) m &= p0 + 31u >= 63u ? ~0u >> (63u - p0) : 0u;  // bit 31 - t: t >= 63 - p0
         if (p0 + 32u > len) m &= p0 >= len ? 0u : ~(~0u >> (len - p0));  // t < len - p0
-        // compaction: every anchor's block offset, in position order
+        // compaction: every anchor's block offset, in position order, ANC_LIST entries per pass (a
+        // random block has ~32 anchors: one pass; a constant run can make every position one)
         const uint32_t k = (uint32_t)__popc(m), incl = wave_incl_scan(k);
         const uint32_t total = readlane(incl, 63);
-        uint32_t o = incl - k;
-        while (m) {
-            const uint32_t t = (uint32_t)__builtin_clz(m);
-            m &= ~(0x80000000u >> t);
-            list[o++] = (uint16_t)(32u * l + t);
-        }
-        wave_sync();
         uint32_t cp = NONE;  // the previous list entry's offset and fingerprint (uniform)
         uint64_t cfp = 0;
         for (uint32_t b0 = 0; b0 < total; b0 += 64u) {
+            if (b0 % ANC_LIST == 0u) {  // the list's next pass: entries [b0, b0 + ANC_LIST)
+                if (b0) wave_sync();    // (the last pass's readers are done)
+                uint32_t o = incl - k, mm = m;
+                for (; mm && o < b0 + ANC_LIST; o++) {
+                    const uint32_t t = (uint32_t)__builtin_clz(mm);
+                    mm &= ~(0x80000000u >> t);
+                    if (o >= b0) list[o - b0] = (uint16_t)(32u * l + t);
+                }
+                wave_sync();
+            }
             const uint32_t idx = b0 + l;
             const bool live = idx < total;
-            const uint32_t p = live ? list[idx] : 0u;
+            const uint32_t p = live ? list[idx % ANC_LIST] : 0u;
             const uint32_t ln = p >> 5, t = p & 31u;
             const uint32_t gv = tile[t * 64u + ln];
             const uint32_t g2 = ln ? tile[t * 64u + ln - 1u] : prev[t];
@@ -1369,11 +1375,13 @@ __device__ __forceinline__ uint64_t group_anchors(const PlanDev &P, uint32_t g, 
 // predict: also the predictions of these blocks (the run's first sub-batch, hashed in line after
 // the declaration set's clear: one kernel instead of two).  ANC: the group's anchors too (a run in
 // anchor mode); groups then also cover a buffer's partial last block.
+// (LDS 37 KB and <= 128 VGPRs: four workgroups, 16 waves, per CU; with a whole block's list, 49
+// KB and 3 waves per SIMD, the side-stream hashing hid less of its latency: cfg5 A/B +2.3 %)
 template <bool PREDICT, bool ANC>
-__global__ __launch_bounds__(256) void k_blockhash(DeclArgs a)
+__global__ __launch_bounds__(256, 4) void k_blockhash(DeclArgs a)
 {
     __shared__ uint32_t tiles[ANC ? 4 : 1][ANC ? 32 * 64 + 32 : 1];
-    __shared__ uint16_t lists[ANC ? 4 : 1][ANC ? XC_SEG : 1];
+    __shared__ uint16_t lists[ANC ? 4 : 1][ANC ? ANC_LIST : 1];
     const PlanDev &P = a.P;
     const uint32_t g = a.j0 + blockIdx.x * 4u + (threadIdx.x >> 6);
     if (g >= a.j1) return;
