@@ -2379,6 +2379,7 @@ __device__ __forceinline__ uint32_t tail_first(const PlanDev &P, uint32_t nb)
 // tlist), which k_tailfinal sorts into its records.
 __global__ __launch_bounds__(256) void k_tailcheck(PlanDev P, uint32_t nb, uint32_t *tcnt, uint4 *tlist)
 {
+    if (aborted(P)) return;  // (enqueued behind a pass that stopped: the host's redo runs it again)
     __shared__ uint32_t refs[4][4];
     const uint32_t wave = threadIdx.x >> 6, l = lane_id();
     const uint32_t j0 = tail_first(P, nb);
@@ -2496,6 +2497,7 @@ __global__ __launch_bounds__(256) void k_tailcheck(PlanDev P, uint32_t nb, uint3
 // (one wave per buffer); the scratch counts back to zero.
 __global__ __launch_bounds__(64) void k_tailfinal(PlanDev P, uint32_t nb, uint32_t *tcnt, const uint4 *tlist)
 {
+    if (aborted(P)) return;
     const uint32_t l = lane_id();
     const uint32_t j0 = tail_first(P, nb);
     for (uint32_t b = j0 + blockIdx.x; b < nb; b += gridDim.x) {

@@ -1258,6 +1258,7 @@ struct xc_plan {
     // its remaining sub-batches scan through the index (anc_scan_on), some did (anc_any)
     int scan_mode = XC_SCAN_AUTO;
     bool anc_run = false, anc_scan_on = false, anc_any = false, g_anc = false;
+    bool tail_enqueued = false;  // the first pass enqueued the tail check behind itself
     uint64_t ngroups = 0, nblocks = 0;
     uint32_t *d_buf_grp0 = nullptr;
     uint64_t *d_rec = nullptr, *d_blk_anc = nullptr;
@@ -2069,6 +2070,13 @@ static int launch_emit(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t jc, uint32
     return XC_OK;
 }
 
+// XC_BH_GATED=1 (experiments): side-stream block hashing one sub-batch ahead, as in round 2
+static bool bh_gated()
+{
+    static const bool g = getenv("XC_BH_GATED") && atoi(getenv("XC_BH_GATED"));
+    return g;
+}
+
 // Predicted declarations (aligned blocks absent from the cache), then one scan of every
 // position of buffers [j0, s1) against cache + predictions, resolve, first walk round.
 // Hash sub-batch k's aligned blocks on the side stream once `after` (an event of the main
@@ -2084,7 +2092,9 @@ static int enqueue_block_hash(xc_plan *p, uint32_t k, hipEvent_t after, hipStrea
     // a range of block groups; on the side stream (sub-batch k - 1 on the main stream) the block
     // compares against the entries complete when k - 1 started
     static const int bh_nt = getenv("XC_BH_NT") ? atoi(getenv("XC_BH_NT")) : 0;
-    DeclArgs d{p->P, g0, g1, side && k > 0 ? p->P.sb_count + (k - 1) : nullptr, bh_nt};
+    // (chained hashing may run while the main stream is several sub-batches behind: its compares
+    // take the entries complete at the run's start; gated, those complete when k - 1 started)
+    DeclArgs d{p->P, g0, g1, side && k > 0 ? p->P.sb_count + (bh_gated() ? k - 1 : 0) : nullptr, bh_nt};
     // XC_ABL_SKIP_BLOCKHASH=1 (timing experiments only, valid when every run reads the same input):
     // the side stream's block hashing after the plan's first run is skipped
     static const bool skip = getenv("XC_ABL_SKIP_BLOCKHASH") && atoi(getenv("XC_ABL_SKIP_BLOCKHASH"));
@@ -2136,9 +2146,15 @@ static int launch_first_round(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t s1,
         HIPCHK(hipGetLastError());
     }
     // the next sub-batch's block hashes run beside this scan (memory-bound beside LDS/L2-bound)
+    // every later sub-batch's blocks back to back on the side stream, the first after this
+    // sub-batch's predictions: the side stream never waits for the main one, whose sub-batch k then
+    // rarely waits for k's hashes (XC_BH_GATED=1: one sub-batch ahead, each hashed beside the scan
+    // before it, as in round 2)
     if (p->next_hash == sb + 1 && sb + 2 < p->sub.size()) {
         HIPCHK(hipEventRecord(p->ev_go[sb], s));
-        if ((rc = enqueue_block_hash(p, sb + 1, p->ev_go[sb], p->hs))) return rc;
+        const uint32_t last = bh_gated() ? sb + 1 : (uint32_t)p->sub.size() - 2;
+        for (uint32_t k = sb + 1; k <= last; k++)
+            if ((rc = enqueue_block_hash(p, k, k == sb + 1 ? p->ev_go[sb] : nullptr, p->hs))) return rc;
     }
     if (anc) {
         if ((rc = launch_ascan(p, j0, s1, ck_lo, ck_hi, shadow))) return rc;
@@ -2306,6 +2322,8 @@ static int graph_launch(xc_plan *p)
     return record_ctl(p);
 }
 
+static int launch_tailcheck(xc_plan *p);
+
 // Everything of a run up to its first asynchronous pass, which is enqueued with ev_ctl after it.
 extern "C" int xc_encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_out_len)
 {
@@ -2350,6 +2368,7 @@ extern "C" int xc_encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out,
     p->P.out = d_out;
     p->P.out_len = d_out_len;
     p->stats = xc_run_stats{};
+    p->tail_enqueued = false;
     {   // the first scans' level-1 image: folded while it keeps >= 16 bits per key (the keys of
         // the cache at the start, when known, and every segment this run can enter)
         const uint64_t keys = (p->cache->host_count >= 0 ? (uint64_t)p->cache->host_count : p->cache->cap) + p->max_new;
@@ -2384,9 +2403,31 @@ extern "C" int xc_encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out,
         }
         if (!pub) HIPCHK(hipMemcpyAsync(p->h_ctl, p->P.ctl, CTL_WORDS * 4, hipMemcpyDeviceToHost, s));
         if ((rc = record_ctl(p))) return rc;
+        // the tail check right behind the pass (after its event: the host's wait does not cover it),
+        // so that it does not wait for the host's turn (XC_TAIL_LATE=1: from encode_finish, as before)
+        static const bool late = getenv("XC_TAIL_LATE") && atoi(getenv("XC_TAIL_LATE"));
+        if (!late) {
+            if ((rc = launch_tailcheck(p))) return rc;
+            p->tail_enqueued = true;
+        }
     }
     p->inflight = true;
     c->busy = p;
+    return XC_OK;
+}
+
+// The recent window's collision lookups that the anchor scans did not look for (enqueued: the
+// run's lookup hits are replayed after it).  Both kernels stand down behind a stopped pass.
+static int launch_tailcheck(xc_plan *p)
+{
+    xc_cache *c = p->cache;
+    if (!(p->anc_any && c->mem && !c->engine && p->nb)) return XC_OK;
+    hipStream_t s = c->ctx->stream;
+    hipLaunchKernelGGL(k_tailcheck, dim3(4u * c->ctx->n_cu), dim3(256), 0, s, p->P, p->nb, p->d_tcnt, p->d_tlist);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_tailfinal, dim3(std::min<uint32_t>(p->nb, 1024u)), dim3(64), 0, s, p->P, p->nb, p->d_tcnt,
+                       (const uint4 *)p->d_tlist);
+    HIPCHK(hipGetLastError());
     return XC_OK;
 }
 
@@ -2404,8 +2445,10 @@ static int encode_finish(xc_plan *p)
     if (p->pass_published && ctl[CTL_WORDS - 1] != 0u && (rc = read_ctl(p, ctl))) return rc;  // (not published)
     const size_t nsub = p->sub.size() - 1;
     bool fresh = true;  // ctl was read after the last launch
+    bool redone = false;
     while (ctl[CTL_ABORT]) {
         fresh = false;
+        redone = true;
         size_t si = ctl[CTL_ABORT_SB];
         HIPCHK(hipMemsetAsync(p->P.ctl + CTL_ABORT, 0, 4, s));
         if (ctl[CTL_ERROR]) break;
@@ -2457,15 +2500,8 @@ static int encode_finish(xc_plan *p)
             if (bad) c->anc_bad = std::min(c->anc_bad, ~bad);
         }
     }
-    if (p->anc_any && c->mem && !c->engine && p->nb) {
-        // the recent window's collision lookups that the anchor scans did not look for (enqueued:
-        // the run's lookup hits are replayed after it)
-        hipLaunchKernelGGL(k_tailcheck, dim3(4u * c->ctx->n_cu), dim3(256), 0, s, p->P, p->nb, p->d_tcnt, p->d_tlist);
-        HIPCHK(hipGetLastError());
-        hipLaunchKernelGGL(k_tailfinal, dim3(std::min<uint32_t>(p->nb, 1024u)), dim3(64), 0, s, p->P, p->nb, p->d_tcnt,
-                           (const uint4 *)p->d_tlist);
-        HIPCHK(hipGetLastError());
-    }
+    // (the first pass enqueued it behind itself unless a sub-batch was redone since)
+    if (!(p->tail_enqueued && !redone) && (rc = launch_tailcheck(p))) return rc;
     if (c->mem && !c->engine) {
         if (ctl[CTL_DUPS]) {
             // a carried candidate entered a hash the cache held: undone, the host replays the run
