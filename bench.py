@@ -52,6 +52,9 @@ def parse():
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-decode", action="store_true")
     ap.add_argument("--no-legs", action="store_true", help="skip the cfg2 / cfg3 encode lines")
+    ap.add_argument("--diag-env", default="",
+                    help="KEY=VAL set only for the per-kernel diagnostic steps after the timed region and "
+                         "the verification (timing ablations, e.g. XC_ABL_EMIT=4)")
     ap.add_argument("--decode-streams", type=int, default=4096, help="cfg4: streams decoded per step")
     return ap.parse_args()
 
@@ -360,6 +363,9 @@ def main():
         alg_job, verified_job, n_job = alg_rank, ver["verified_buffers"], n_local
 
     diag_steps = 3
+    if args.diag_env:  # (after the timed steps and the verification: ablations only change these)
+        k, v = args.diag_env.split("=", 1)
+        os.environ[k] = v
     plan.kernel_times(reset=True)
     plan.set_timing(True)
     for _ in range(diag_steps):

@@ -409,6 +409,13 @@ __device__ __forceinline__ void payload_store(uint8_t *out, uint8_t *seg, const 
     if (t0 + l < XC_SEG) out[t0 + l] = (uint8_t)r.tb;
 }
 
+__device__ __forceinline__ void payload_store_seg(uint8_t *seg, const PayloadRegs &r)
+{
+    const uint32_t l = lane_id();
+    ((uint4 *)seg)[l] = r.a0;
+    ((uint4 *)seg)[l + 64u] = r.a1;
+}
+
 __device__ __forceinline__ void wave_copy_payload(uint8_t *out, uint8_t *seg, const uint8_t *src)
 {
     PayloadRegs r;

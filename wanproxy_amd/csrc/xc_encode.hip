@@ -461,9 +461,9 @@ template __global__ void k_scan<5>(ScanArgs);
 // (pcnt / pq).  k_aevents: one lane per chunk writes the aligned windows (no proposal: the common
 // case); a chunk with proposals is sorted and merged by its whole wave in an LDS bitmask.
 
-// (APROP_GROUPS groups per workgroup: every thread's record and filter loads of all of them in
-// flight together; one group per workgroup left the kernel latency-bound)
-constexpr uint32_t APROP_GROUPS = 8;
+// (APROP_GROUPS groups per workgroup, xc_kernels.h: every thread's record and filter loads of all
+// of them in flight together; one group per workgroup left the kernel latency-bound, and 2 beat 4
+// and 8 once the side stream's block hashing ran beside it: cfg5 A/B +0.8 %, aprop 0.61 -> 0.53 ms)
 __global__ __launch_bounds__(256) void k_aprop(AScanArgs a)
 {
     const PlanDev &P = a.P;
@@ -1659,7 +1659,7 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
     __syncthreads();
     const uint32_t slot0 = SLOTS ? s_base + s_pre : P.buf_slot[b];
     if (SLOTS && threadIdx.x == 0) P.buf_slot[b] = slot0;  // (the tail check's visibility test)
-    if (wave == EMIT_WAVES - 1u) {  // the wave with the smallest token group (wave 0 did the prefix)
+    if (wave == EMIT_WAVES - 1u && !(a.abl & 4u)) {  // the wave with the smallest token group (wave 0 did the prefix)
         // XCodecMemoryCache::enter (xcodec_cache.h:182-188) of this buffer's declarations,
         // one lane per EXTRACT token, into the slots k_alloc reserved
         for (uint32_t t0 = 0; t0 < n; t0 += 64u) {
@@ -1742,7 +1742,7 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
             o[1] = (uint8_t)OP_EXTRACT;
         }
         // payloads to the wire and into the slots k_alloc reserved, EMIT_PAY at a time
-        for (uint64_t m = ballot(live && op == OP_EXTRACT); m;) {
+        for (uint64_t m = ballot(live && op == OP_EXTRACT && !(a.abl & 8u)); m;) {
             int f[EMIT_PAY];
             uint32_t ii[EMIT_PAY];
             uint8_t *d[EMIT_PAY];
@@ -1759,7 +1759,14 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
             }
 #pragma unroll
             for (int g = 0; g < EMIT_PAY; g++)
-                if (f[g] >= 0) payload_store(d[g], ii[g] < P.seg_cap ? seg_at(P.segs, ii[g]) : nullptr, r[g]);
+                if (f[g] >= 0) {
+                    uint8_t *sg = ii[g] < P.seg_cap && !(a.abl & 1u) ? seg_at(P.segs, ii[g]) : nullptr;
+                    if (a.abl & 2u) {
+                        if (sg) payload_store_seg(sg, r[g]);
+                    } else {
+                        payload_store(d[g], sg, r[g]);
+                    }
+                }
         }
     }
 }

@@ -169,6 +169,10 @@ struct PlanDev {
     uint32_t *anc_bad;
 };
 constexpr uint32_t COLL_CAP = 16;
+#ifndef XC_APROP_GROUPS
+#define XC_APROP_GROUPS 2
+#endif
+constexpr uint32_t APROP_GROUPS = XC_APROP_GROUPS;  // k_aprop: block groups per workgroup
 constexpr uint32_t BLK_GROUP = 8;    // aligned blocks per k_blockhash group (one wave)
 constexpr uint32_t REC_CAP = 1024;  // anchor records per k_blockhash group (16 KiB; random data: ~256)
 constexpr uint32_t REC_OVF = 0x80000000u;
@@ -267,6 +271,8 @@ struct EmitArgs {
     uint32_t *ctl_host;
     const uint32_t *base;  // k_emit<.., true>: the cache count at the sub-batch's start (P.sb_count)
     uint32_t pub_final;
+    uint32_t abl;  // timing ablations (XC_ABL_EMIT, diagnostics only: results are wrong): 1 no segment
+                   // store, 2 no payload wire copy, 4 no cache inserts, 8 no payload loads or stores
 };
 // Sub-batches of at most this many buffers take k_alloc's work inside k_emit (every workgroup
 // sums the buf_next of the buffers before it): one launch less on small batches.

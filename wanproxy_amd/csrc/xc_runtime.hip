@@ -2010,7 +2010,7 @@ static int launch_ascan(xc_plan *p, uint32_t j0, uint32_t s1, uint32_t ck_lo, ui
     if (p->timing) p->ktimes.scan_bytes += p->chunk_bytes[ck_hi] - p->chunk_bytes[ck_lo];
     hipStream_t s = p->cache->ctx->stream;
     if (g_hi > g_lo) {
-        hipLaunchKernelGGL(k_aprop, dim3((g_hi - g_lo + 7) / 8), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_aprop, dim3((g_hi - g_lo + APROP_GROUPS - 1) / APROP_GROUPS), dim3(256), 0, s, a);
         HIPCHK(hipGetLastError());
     }
     hipLaunchKernelGGL(k_aevents, dim3((ck_hi - ck_lo + 255) / 256), dim3(256), 0, s, a);
@@ -2054,7 +2054,9 @@ static int launch_emit(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t jc, uint32
     const bool slots = jc > j0 && jc - j0 <= EMIT_SLOTS_MAX;
     // (the pass's last sub-batch publishes the control words: from the emit when it takes the
     // slots, else from k_alloc; the non-slot emit never reads ctl_host)
-    EmitArgs e{p->P, j0, jc, gate_sb, p->emit_ctl_host, p->P.sb_count + sb, p->emit_pub_final};
+    const char *abl = getenv("XC_ABL_EMIT");  // (read per launch: a diagnostic run sets it late)
+    EmitArgs e{p->P, j0, jc, gate_sb, p->emit_ctl_host, p->P.sb_count + sb, p->emit_pub_final,
+               abl ? (uint32_t)atoi(abl) : 0u};
     if (!slots) {
         hipLaunchKernelGGL(k_alloc, dim3(1), dim3(1024), 0, s, e);
         HIPCHK(hipGetLastError());
