@@ -191,31 +191,94 @@ __device__ __forceinline__ uint64_t dtok_mask(const uint4 (&v)[4], uint32_t w0, 
     return m;
 }
 
+__device__ __forceinline__ uint64_t dreadlane64(uint64_t x, int l)
+{
+    return ((uint64_t)readlane((uint32_t)(x >> 32), l) << 32) | readlane((uint32_t)x, l);
+}
+
+// Bytes x .. x + 31 of the stream from the wave's 8 KiB LDS ring (position p at ring byte p & 8191):
+// three aligned 16-byte reads and a funnel by x & 15 (uniform across the wave when x = start + 32 l).
+__device__ __forceinline__ void ring_read32(const uint32_t *ring, uint32_t x, uint32_t (&o)[8])
+{
+    const uint32_t b = x & (2u * DTOK_WIN - 1u), a16 = b & ~15u, dsh = (b >> 2) & 3u, sh = b & 3u;
+    uint32_t d[12];
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        const uint4 v = *(const uint4 *)((const uint8_t *)ring + ((a16 + 16u * i) & (2u * DTOK_WIN - 1u)));
+        d[4 * i] = v.x; d[4 * i + 1] = v.y; d[4 * i + 2] = v.z; d[4 * i + 3] = v.w;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const uint32_t lo = dsh == 0 ? d[k] : dsh == 1 ? d[k + 1] : dsh == 2 ? d[k + 2] : d[k + 3];
+        const uint32_t hi = dsh == 0 ? d[k + 1] : dsh == 1 ? d[k + 2] : dsh == 2 ? d[k + 3] : d[k + 4];
+        o[k] = __builtin_amdgcn_alignbyte(hi, lo, sh);
+    }
+}
+
 // first: also the run's prologue, spread over the tokenizer's threads (the control words, every
-// stream's provider limit, the round-0 batch provider table): three launches less.
+// stream's provider limit and, unless HASH, the round-0 batch provider table): launches less.
+// HASH: round 0 of the provider resolution too (k_dres1<true>'s work, xcodec_hash.h:166-174 and
+// xcodec_decoder.cc:101-132): every EXTRACT payload is hashed from the wave's LDS ring of the two
+// latest windows as the tokenizer passes it (no second read of the payloads), and 64 at a time the
+// cache probes, collisions and batch-table inserts run lane-parallel (the batch table was cleared by
+// k_dclear before this kernel: its inserts must not race with a clear).
+template <bool HASH>
 __global__ __launch_bounds__(64) void k_dtok(DecDev D, int fill, int first, uint32_t n_lo, uint32_t n_full)
 {
-    __shared__ uint32_t win[DTOK_WIN / 4 + 4];
+    __shared__ uint32_t win[(HASH ? 2u : 1u) * DTOK_WIN / 4 + 8];
     const uint32_t j = blockIdx.x;
     if (first) {
         if (j == 0 && threadIdx.x < DCTL_WORDS) D.ctl[threadIdx.x] = 0u;
         if (j < D.ns && threadIdx.x == 0) D.s_lim[j] = 0xFFFFFFFFu;
-        dclear_range(D, n_lo, n_full, j * 64u + threadIdx.x, gridDim.x * 64u);
+        if (!HASH) dclear_range(D, n_lo, n_full, j * 64u + threadIdx.x, gridDim.x * 64u);
     }
     if (j >= D.ns) return;
     const uint8_t *s = D.in + D.in_off[j];
     const uint32_t n = D.in_len[j];
     const uint32_t tb = fill ? D.tok_base[j] : 0u;
     const uint32_t l = lane_id();
+    constexpr uint32_t RING = (HASH ? 2u : 1u) * DTOK_WIN - 1u;  // ring byte mask
     uint32_t nt = 0, lb = 0, p = 0;
     auto put = [&](uint32_t op, uint32_t le, uint64_t h) {
         if (fill && l == 0) {
             D.t_lb[tb + nt] = lb;
             D.t_le[tb + nt] = le;
             D.t_op[tb + nt] = op;
-            D.t_h[tb + nt] = h;
+            if (!HASH || op != T_EXTRACT) D.t_h[tb + nt] = h;  // (HASH: the probes write it)
         }
         nt++;
+    };
+    // HASH: lane i holds the i-th EXTRACT of the current batch of 64 (hash, token, payload start)
+    uint64_t xh = 0;
+    uint32_t xt = 0, xx = 0, xn = 0;
+    uint32_t pend_x = NONE, pend_t = 0;  // an EXTRACT whose payload ends in the next window
+    auto flush = [&]() {
+        const bool ex = l < xn;
+        uint64_t v = 0;
+        uint32_t st = 0;
+        const bool hit = ex && set_find(D.cache, xh, &v);
+        if (ex && !hit) {
+            st = R_PENDING;
+            set_insert(D.dset, xh, ((uint64_t)j << 32) | xt, true, nullptr, nullptr);  // (round 0: no limit)
+        }
+        for (uint64_t mh = ballot(hit); mh; mh &= mh - 1) {  // a cached hash: the bytes (rare)
+            const int fh = __ffsll((unsigned long long)mh) - 1;
+            const bool eq = wave_equal2048(s + readlane(xx, fh), seg_at(D.segs, dreadlane64(v, fh)));
+            if ((int)l == fh) st = eq ? R_OKCACHE : R_COLL;
+        }
+        if (ex && fill) {
+            D.t_h[tb + xt] = xh;
+            D.t_stat[tb + xt] = st;
+            D.t_src[tb + xt] = st == R_OKCACHE ? v : 0;
+        }
+        xn = 0;
+    };
+    auto hash_at = [&](uint32_t x, uint32_t t) {  // payload x .. x + 2047, inside the ring
+        uint32_t w8[8];
+        ring_read32(win, x + 32u * l, w8);
+        const uint64_t h = wave_hash_regs(w8);
+        if (l == xn) { xh = h; xt = t; xx = x; }
+        if (++xn == 64u) flush();
     };
     const uint32_t nw = (n + DTOK_WIN - 1u) / DTOK_WIN;
     // (only windows that start inside the stream are read: past the last, it is read again)
@@ -229,13 +292,18 @@ __global__ __launch_bounds__(64) void k_dtok(DecDev D, int fill, int first, uint
         const uint32_t w0 = k * DTOK_WIN;
         dtok_load(fut, s, min(w0 + 2u * DTOK_WIN, last));  // (unconditional: a static vmcnt)
         const uint64_t mask = dtok_mask(cur, w0, n);
-        // the window into LDS (the previous window's readers are done: every read was waited for)
-        uint4 *wl = (uint4 *)win + 4u * l;
+        // the window into LDS (the previous window's readers are done: every read was waited for;
+        // HASH: the ring's other half keeps the window before)
+        uint4 *wl = (uint4 *)((uint8_t *)win + (w0 & RING)) + 4u * l;
 #pragma unroll
         for (int i = 0; i < 4; i++) wl[i] = cur[i];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (HASH && pend_x != NONE) {  // its payload ends in this window
+            hash_at(pend_x, pend_t);
+            pend_x = NONE;
+        }
         const uint32_t base = w0 + 64u * l;
         for (;;) {
             uint64_t mm = mask;
@@ -250,7 +318,7 @@ __global__ __launch_bounds__(64) void k_dtok(DecDev D, int fill, int first, uint
             uint32_t op;
             uint64_t h = 0;
             if (r + 9u <= DTOK_WIN) {  // op and 8 hash bytes inside the window
-                const uint32_t i = r >> 2, o = r & 3u;
+                const uint32_t i = ((q + 1u) & RING) >> 2, o = r & 3u;
                 const uint32_t d0 = win[i], d1 = win[i + 1u], d2 = win[i + 2u];
                 op = (d0 >> (8u * o)) & 0xffu;
                 // hash bytes r + 1 .. r + 8: bytes o + 1 .. o + 8 of d0 d1 d2
@@ -266,7 +334,12 @@ __global__ __launch_bounds__(64) void k_dtok(DecDev D, int fill, int first, uint
             if (op == 0x00u) { p = q + 2u; continue; }  // escape: stays inside the literal run
             if (op == 0x01u) {
                 if (n - q < 2u + XC_SEG) { put(T_WAIT, q, 0); return true; }
+                const uint32_t t = nt;
                 put(T_EXTRACT, q, 0);
+                if (HASH) {
+                    if (q + 2u + XC_SEG <= w0 + DTOK_WIN) hash_at(q + 2u, t);
+                    else { pend_x = q + 2u; pend_t = t; }  // (the window's last token)
+                }
                 lb = p = q + 2u + XC_SEG;
                 continue;
             }
@@ -287,8 +360,11 @@ __global__ __launch_bounds__(64) void k_dtok(DecDev D, int fill, int first, uint
         if (!done && k + 2u < nw) done = step(v2, v1, k + 2u);
     }
     if (!done) put(T_END, n, 0);
+    if (HASH && xn) flush();
     if (l == 0) D.tok_cnt[j] = nt;
 }
+template __global__ void k_dtok<false>(DecDev, int, int, uint32_t, uint32_t);
+template __global__ void k_dtok<true>(DecDev, int, int, uint32_t, uint32_t);
 
 // The round-2 tokenizer (kept for A/B): F1 search in 1 KiB register windows loaded on demand.
 __global__ __launch_bounds__(64) void k_dtok_win(DecDev D, int fill, int first, uint32_t n_lo, uint32_t n_full)
@@ -404,10 +480,6 @@ __device__ __forceinline__ void raw_align(const RawWin &r, uint32_t out[8])
     for (int k = 0; k < 8; k++) out[k] = __builtin_amdgcn_alignbyte(r.d[k + 1], r.d[k], r.sh);
 }
 
-__device__ __forceinline__ uint64_t dreadlane64(uint64_t x, int l)
-{
-    return ((uint64_t)readlane((uint32_t)(x >> 32), l) << 32) | readlane((uint32_t)x, l);
-}
 
 template <bool HASH>
 __global__ __launch_bounds__(64) void k_dres1(DecDev D)
@@ -1134,8 +1206,14 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
     // tokens, with the prologue (control words, provider limits, round 0's provider table)
     // XC_DTOK_WIN=1 (experiments): the round-2 tokenizer
     static const bool old_tok = getenv("XC_DTOK_WIN") && atoi(getenv("XC_DTOK_WIN"));
-    hipLaunchKernelGGL(old_tok ? k_dtok_win : k_dtok, dim3(std::max<uint32_t>(ns, 256u)), dim3(64), 0, s, D, 1, 1,
-                       p->n_lo, p->n_full);
+    // XC_DTOK_NOHASH=1 (experiments): round 0's hashes and probes in k_dres1<true>, as before
+    static const bool tok_hash = !old_tok && !(getenv("XC_DTOK_NOHASH") && atoi(getenv("XC_DTOK_NOHASH")));
+    if (tok_hash) {  // (the batch table cleared before the tokenizer inserts into it)
+        hipLaunchKernelGGL(k_dclear, dim3(512), dim3(256), 0, s, D, p->n_lo, p->n_full);
+        DHIP(hipGetLastError());
+    }
+    hipLaunchKernelGGL(old_tok ? k_dtok_win : tok_hash ? k_dtok<true> : k_dtok<false>,
+                       dim3(std::max<uint32_t>(ns, 256u)), dim3(64), 0, s, D, 1, 1, p->n_lo, p->n_full);
     DHIP(hipGetLastError());
     // one provider-resolution round (a fresh batch table each time; round 0's came with k_dtok)
     auto resolve_round = [&](int r) -> int {
@@ -1143,7 +1221,7 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
             hipLaunchKernelGGL(k_dclear, dim3(512), dim3(256), 0, s, D, p->n_lo, p->n_full);
             DHIP(hipGetLastError());
             hipLaunchKernelGGL(k_dres1<false>, dim3(ns, DRES_WAVES), dim3(64), 0, s, D);
-        } else {
+        } else if (!tok_hash) {
             hipLaunchKernelGGL(k_dres1<true>, dim3(ns, DRES_WAVES), dim3(64), 0, s, D);
         }
         DHIP(hipGetLastError());
