@@ -1559,6 +1559,71 @@ __device__ __forceinline__ void ctl_publish(const EmitArgs &a)
     __threadfence_system();
 }
 
+// XCodecMemoryCache::enter (xcodec_cache.h:182-188) of the EXTRACT token t of buffer b (ext) into
+// cache slot idx, one lane per token, the whole wave present: the hash tables (undo record) and, on
+// an anchor run, the anchor index (an aligned block's key from k_blockhash, any other segment's
+// computed here, wave-wide, one at a time).
+__device__ __forceinline__ void enter_tokens(const PlanDev &P, uint32_t b, const uint8_t *base, uint32_t tb,
+                                             uint32_t t, bool ext, uint32_t idx)
+{
+    const uint32_t l = lane_id();
+    if (P.anc_run) {
+        const uint32_t sg = ext ? P.tok_seg[tb + t] : 0u;
+        uint64_t key = ext && (sg & (XC_SEG - 1u)) == 0u ? P.blk_anc[P.blk_base[b] + sg / XC_SEG] : ANC_NONE;
+        for (uint64_t m = ballot(ext && (sg & (XC_SEG - 1u)) != 0u); m; m &= m - 1) {
+            const int f = __ffsll((unsigned long long)m) - 1;
+            uint32_t wv[8];
+            load32_window(base + readlane(sg, f) + 32u * l, wv);
+            const uint64_t k2 = wave_seg_anchor(wv);
+            if ((int)l == f) key = k2;
+        }
+        if (ext && idx < P.seg_cap) {
+            P.anc_of[idx] = key;
+            if (key != ANC_NONE) {
+                P.aundo[idx] = anc_insert(P.canc, key);
+            } else {
+                P.aundo[idx] = NONE;
+                atomicMax(P.anc_bad, ~idx);
+            }
+        }
+    }
+    if (ext && idx < P.seg_cap) {
+        uint32_t s1, s2;
+        if (set_insert(P.cache, P.tok_h[tb + t], idx, false, &s1, &s2) || s2 == XC_REVIVED) {
+            P.undo[idx] = make_uint2(s1, s2);
+        } else {
+            // the hash is in the cache: a stateful stream's carried candidate declared after another
+            // connection entered the hash (xc_memcache.cpp).  The table keeps the first entry
+            // (nothing to undo); the host replays the run.
+            P.undo[idx] = make_uint2(NONE, NONE);
+            atomicAdd(&P.ctl[CTL_DUPS], 1u);
+        }
+    }
+}
+
+// The cache enters of buffers [j0, j1) (a sub-batch without in-emit slots), one wave per buffer, so
+// that every insert of the sub-batch is in flight at once instead of on one wave of each emit
+// workgroup (the emit's critical path): after k_alloc (its slots), before k_emit.
+__global__ __launch_bounds__(256) void k_insert(EmitArgs a)
+{
+    if (aborted(a.P)) return;
+    const PlanDev &P = a.P;
+    const uint32_t b = a.j0 + blockIdx.x * 4u + (threadIdx.x >> 6);
+    if (b >= a.j1) return;
+    const uint32_t l = lane_id();
+    const uint8_t *base = P.in + P.buf_off[b];
+    const uint32_t tb = P.tok_base[b], n = min(P.tok_cnt[b], MAX_TOK);
+    const uint32_t slot0 = P.buf_slot[b];
+    uint32_t carry = 0;  // EXTRACT tokens before this chunk
+    for (uint32_t t0 = 0; t0 < n; t0 += 64u) {
+        const uint32_t t = t0 + l;
+        const bool ext = t < n && P.tok_op[tb + t] == OP_EXTRACT;
+        const uint64_t em = ballot(ext);
+        enter_tokens(P, b, base, tb, t, ext, slot0 + carry + mbcnt(em));
+        carry += (uint32_t)__popcll(em);
+    }
+}
+
 // SLOTS: k_alloc's work too (sub-batches of <= EMIT_SLOTS_MAX buffers), with no extra round trip
 // on a workgroup's path: the gate words, the sub-batch's start count (P.sb_count, written by
 // k_clear_set: the cache count does not change before this kernel) and every buffer's buf_next /
@@ -1659,52 +1724,13 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
     __syncthreads();
     const uint32_t slot0 = SLOTS ? s_base + s_pre : P.buf_slot[b];
     if (SLOTS && threadIdx.x == 0) P.buf_slot[b] = slot0;  // (the tail check's visibility test)
-    if (wave == EMIT_WAVES - 1u && !(a.abl & 4u)) {  // the wave with the smallest token group (wave 0 did the prefix)
-        // XCodecMemoryCache::enter (xcodec_cache.h:182-188) of this buffer's declarations,
-        // one lane per EXTRACT token, into the slots k_alloc reserved
+    // XCodecMemoryCache::enter of this buffer's declarations (SLOTS, or k_insert not split off): the
+    // wave with the smallest token group (wave 0 did the prefix), one lane per EXTRACT token
+    if (wave == EMIT_WAVES - 1u && !(a.abl & 4u) && (SLOTS || !a.split_ins)) {
         for (uint32_t t0 = 0; t0 < n; t0 += 64u) {
             const uint32_t t = t0 + l;
             const bool ext = t < n && P.tok_op[tb + t] == OP_EXTRACT;
-            if (P.anc_run) {
-                // the anchor index takes every entered segment: an aligned block's key from
-                // k_blockhash, any other segment's computed here (wave-wide, one at a time)
-                const uint32_t sg = ext ? P.tok_seg[tb + t] : 0u;
-                uint64_t key = ext && (sg & (XC_SEG - 1u)) == 0u ? P.blk_anc[P.blk_base[b] + sg / XC_SEG] : ANC_NONE;
-                for (uint64_t m = ballot(ext && (sg & (XC_SEG - 1u)) != 0u); m; m &= m - 1) {
-                    const int f = __ffsll((unsigned long long)m) - 1;
-                    uint32_t wv[8];
-                    load32_window(base + readlane(sg, f) + 32u * l, wv);
-                    const uint64_t k2 = wave_seg_anchor(wv);
-                    if ((int)l == f) key = k2;
-                }
-                if (ext) {
-                    const uint32_t idx = slot0 + ord[t];
-                    if (idx < P.seg_cap) {
-                        P.anc_of[idx] = key;
-                        if (key != ANC_NONE) {
-                            P.aundo[idx] = anc_insert(P.canc, key);
-                        } else {
-                            P.aundo[idx] = NONE;
-                            atomicMax(P.anc_bad, ~idx);
-                        }
-                    }
-                }
-            }
-            if (ext) {
-                const uint32_t idx = slot0 + ord[t];
-                if (idx < P.seg_cap) {
-                    uint32_t s1, s2;
-                    if (set_insert(P.cache, P.tok_h[tb + t], idx, false, &s1, &s2) || s2 == XC_REVIVED) {
-                        P.undo[idx] = make_uint2(s1, s2);
-                    } else {
-                        // the hash is in the cache: a stateful stream's carried candidate declared
-                        // after another connection entered the hash (xc_memcache.cpp).  The table
-                        // keeps the first entry (nothing to undo); the host replays the run.
-                        P.undo[idx] = make_uint2(NONE, NONE);
-                        atomicAdd(&P.ctl[CTL_DUPS], 1u);
-                    }
-                }
-            }
+            enter_tokens(P, b, base, tb, t, ext, ext ? slot0 + ord[t] : 0u);
         }
     }
     // wire bytes: wave w takes a contiguous group of tokens, one per lane, so the group's

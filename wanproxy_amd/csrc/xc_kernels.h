@@ -273,6 +273,7 @@ struct EmitArgs {
     uint32_t pub_final;
     uint32_t abl;  // timing ablations (XC_ABL_EMIT, diagnostics only: results are wrong): 1 no segment
                    // store, 2 no payload wire copy, 4 no cache inserts, 8 no payload loads or stores
+    uint32_t split_ins;  // k_emit<.., false>: the cache enters ran in k_insert before it
 };
 // Sub-batches of at most this many buffers take k_alloc's work inside k_emit (every workgroup
 // sums the buf_next of the buffers before it): one launch less on small batches.
@@ -311,6 +312,7 @@ __global__ void k_tailfinal(PlanDev P, uint32_t nb, uint32_t *tcnt, const uint4 
 __global__ void k_blockpredict(DeclArgs a);
 __global__ void k_or_words(uint4 *dst, const uint4 *a, const uint4 *b, uint32_t n);
 __global__ void k_alloc(EmitArgs a);
+__global__ void k_insert(EmitArgs a);
 __global__ void k_clear_set(DevSet s, uint32_t n_lo, uint32_t n_full, uint4 *l2mix, const uint4 *cache_l2,
                             uint32_t *fmix, const uint32_t *cache_filt, uint32_t fold, const uint32_t *count,
                             uint32_t *count_out, uint32_t *ctl_zero, AncSet danc, uint4 *amix, const uint4 *cache_afilt);

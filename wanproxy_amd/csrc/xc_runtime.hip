@@ -2055,14 +2055,21 @@ static int launch_emit(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t jc, uint32
     // (the pass's last sub-batch publishes the control words: from the emit when it takes the
     // slots, else from k_alloc; the non-slot emit never reads ctl_host)
     const char *abl = getenv("XC_ABL_EMIT");  // (read per launch: a diagnostic run sets it late)
-    EmitArgs e{p->P, j0, jc, gate_sb, p->emit_ctl_host, p->P.sb_count + sb, p->emit_pub_final,
-               abl ? (uint32_t)atoi(abl) : 0u};
+    // XC_EMIT_INSERT=1 (experiments): the cache enters inside the emit workgroups, as in round 2
+    static const bool in_emit = getenv("XC_EMIT_INSERT") && atoi(getenv("XC_EMIT_INSERT"));
+    const uint32_t ab = abl ? (uint32_t)atoi(abl) : 0u;
+    EmitArgs e{p->P, j0, jc, gate_sb, p->emit_ctl_host, p->P.sb_count + sb, p->emit_pub_final, ab,
+               !slots && !in_emit ? 1u : 0u};
     if (!slots) {
         hipLaunchKernelGGL(k_alloc, dim3(1), dim3(1024), 0, s, e);
         HIPCHK(hipGetLastError());
     }
     if (jc <= j0) return XC_OK;
     KSpan span(p, XC_K_EMIT);
+    if (e.split_ins && !(ab & 4u)) {
+        hipLaunchKernelGGL(k_insert, dim3((jc - j0 + 3) / 4), dim3(256), 0, s, e);
+        HIPCHK(hipGetLastError());
+    }
     // one workgroup per buffer: 4 waves when the buffers alone fill the chip, 16 for few buffers
     const bool wide = (uint64_t)(jc - j0) * EMIT_WAVES < (uint64_t)p->cache->ctx->n_cu * 16u;
     auto kern = wide ? (slots ? k_emit<16, true> : k_emit<16, false>)
