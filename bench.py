@@ -402,6 +402,23 @@ def main():
     bytes_per_launch = kt_all["scan_bytes"] / launches
     scan_ach = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
 
+    # the step's two heaviest kernels by their own algorithmic bytes (HIP events around each launch in
+    # the diagnostic steps; the side stream's block hashing shares the GPU with the main stream)
+    kernel_rooflines = {}
+    for name, bytes_step, what in (
+            ("blockhash", in_bytes_rank + SEG * int(st.n_ref),
+             "input bytes + the cached segments of predicted REFs compared in registers"),
+            ("emit", 2 * SEG * int(st.n_extract) + out_bytes,
+             "EXTRACT payload reads + wire bytes + segment-store writes (span: k_insert + k_emit)")):
+        n_l = kt_all["launches"].get(name, 0)
+        ms = kt_all["ms"].get(name, 0.0)
+        if n_l and ms > 0:
+            b_l = bytes_step * diag_steps / n_l
+            ach = b_l / (ms / n_l * 1e-3) / 1e9
+            kernel_rooflines[name] = {"achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                      "frac": round(ach / HBM_PEAK_GBS, 4), "avg_launch_ms": round(ms / n_l, 4),
+                                      "alg_bytes_per_launch": int(b_l), "alg_bytes_def": what}
+
     result = {
         "metric": "XCodec encode GiB/s device-resident (cfg5: 32768 x 64 KiB, 50% repeats, warm per-GPU cache)",
         "value": round(value, 3),
@@ -426,6 +443,7 @@ def main():
                           "note": "diagnostic: 1 B per scanned position / scan launch time (rank 0, diagnostic steps)"
                           + ("; the anchor scan reads the block hashing's records (8 B per input anchor, 1/64 of "
                              "the positions), not the input: this is its coverage rate, not its traffic" if anchor else "")},
+        "kernel_rooflines": kernel_rooflines,
         "kernel_ms_per_step": {k: round(v / diag_steps, 4) for k, v in kt_all["ms"].items()},
         "kernel_ms_note": f"HIP events around every kernel in {diag_steps} steps after the timed region (rank 0)",
         "stats": {"n_extract": int(st.n_extract), "n_ref": int(st.n_ref),
