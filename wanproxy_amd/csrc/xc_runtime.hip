@@ -2055,11 +2055,13 @@ static int launch_emit(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t jc, uint32
     // (the pass's last sub-batch publishes the control words: from the emit when it takes the
     // slots, else from k_alloc; the non-slot emit never reads ctl_host)
     const char *abl = getenv("XC_ABL_EMIT");  // (read per launch: a diagnostic run sets it late)
-    // XC_EMIT_INSERT=1 (experiments): the cache enters inside the emit workgroups, as in round 2
+    // the cache enters in k_insert for large sub-batches (cfg5's 8192 buffers: A/B 751 -> 766 GiB/s);
+    // below that the launch costs more than it saves (cfg3's 4096: 650 -> 634), and they stay in
+    // the emit workgroups (XC_EMIT_INSERT=1: always there, as in round 2)
     static const bool in_emit = getenv("XC_EMIT_INSERT") && atoi(getenv("XC_EMIT_INSERT"));
     const uint32_t ab = abl ? (uint32_t)atoi(abl) : 0u;
     EmitArgs e{p->P, j0, jc, gate_sb, p->emit_ctl_host, p->P.sb_count + sb, p->emit_pub_final, ab,
-               !slots && !in_emit ? 1u : 0u};
+               !slots && !in_emit && jc - j0 >= INSERT_SPLIT_MIN ? 1u : 0u};
     if (!slots) {
         hipLaunchKernelGGL(k_alloc, dim3(1), dim3(1024), 0, s, e);
         HIPCHK(hipGetLastError());
