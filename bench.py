@@ -56,6 +56,9 @@ def parse():
                     help="KEY=VAL set only for the per-kernel diagnostic steps after the timed region and "
                          "the verification (timing ablations, e.g. XC_ABL_EMIT=4)")
     ap.add_argument("--decode-streams", type=int, default=4096, help="cfg4: streams decoded per step")
+    ap.add_argument("--no-live", action="store_true", help="skip the steady-state (live cache) leg")
+    ap.add_argument("--live-batches", type=int, default=4)
+    ap.add_argument("--live-reps", type=int, default=3)
     return ap.parse_args()
 
 
@@ -213,6 +216,92 @@ def bench_decode(args, ctx, warm):
             "stats": {"n_extract": int(st.n_extract), "n_ref": int(st.n_ref), "n_entered": int(st.n_entered),
                       "rounds": int(st.rounds)},
             "verified_streams": n}
+
+
+LIVE_GOLD = os.path.join(ROOT, "tests", "golden", "live_digests.npz")
+
+
+def bench_live(args, ctx, warm, d_in0, step_ms):
+    """Steady state: cfg5-shaped batches back to back on ONE live cache, no restore in between (how a
+    proxy's cache runs).  Batch k (seed 0x5555 + k; batch 0 is the headline's) sees every segment the
+    batches before it declared, and each run's lookup hits reach the recent window model while the
+    next run works.  One timed sequence = the batches back to back + the replay of
+    the last run's hits (cache.settle()), from the warm snapshot; every buffer of every batch is then
+    checked against the oracle's digests of the same sequence (tests/golden/make_live.py)."""
+    import torch
+    import wanproxy_amd as w
+    from wanproxy_amd import workloads as W
+    nb = args.live_batches
+    n = 32768
+    cache = w.XCodecCache(ctx, W.POOL_SEGMENTS + nb * n * (W.BUF // SEG + 1) + 1024)
+    w.XCodecEncoder(cache).encode_batch(warm)
+    cache.snapshot()
+    lens = np.full(n, W.BUF, np.uint64)
+    plan = w.EncodePlan(cache, lens)
+    plan.set_completion(True)
+    d_in = [d_in0]
+    for k in range(1, nb):
+        x = torch.zeros(plan.in_bytes, dtype=torch.uint8, device="cuda")
+        x[:n * W.BUF] = torch.from_numpy(W.repeat_shard(n, 0x5555 + k).reshape(-1)).cuda()
+        d_in.append(x)
+    d_out = [torch.zeros(plan.out_bytes, dtype=torch.uint8, device="cuda") for _ in range(nb)]
+    d_len = [torch.zeros(n, dtype=torch.int64, device="cuda") for _ in range(nb)]
+    torch.cuda.synchronize()
+
+    def sequence():
+        for k in range(nb):
+            plan.run(d_in[k].data_ptr(), d_out[k].data_ptr(), d_len[k].data_ptr())
+        cache.settle()
+
+    times, replay = [], []
+    for rep in range(1 + args.live_reps):  # (the first sequence is the warm-up)
+        cache.restore()
+        torch.cuda.synchronize()
+        h0 = cache.hit_stats()
+        t0 = time.perf_counter()
+        sequence()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        h1 = cache.hit_stats()
+        if rep:
+            times.append(t1 - t0)
+            replay.append((h1["host_s"] - h0["host_s"], h1["runs"] - h0["runs"], h1["hits"] - h0["hits"]))
+    # parity: every buffer of every batch (the outputs of the last sequence)
+    verified = 0
+    z = np.load(LIVE_GOLD) if os.path.exists(LIVE_GOLD) else None
+    if z is None or f"live_b{nb - 1}_dig" not in z.files:
+        raise SystemExit("bench: live leg without its oracle digests (tests/golden/make_live.py)")
+    for k in range(nb):
+        olen = d_len[k].cpu().numpy().astype(np.uint64)
+        if not np.array_equal(z[f"live_b{k}_len"].astype(np.uint64), olen):
+            raise SystemExit(f"bench: live batch {k}: encoded lengths differ from the oracle")
+        dig = W.arena_digests(d_out[k].cpu().numpy(), plan.out_off, olen)
+        bad = np.nonzero(dig != z[f"live_b{k}_dig"])[0]
+        if bad.size:
+            raise SystemExit(f"bench: live batch {k}: {bad.size} buffers differ from the oracle, first {bad[:8]}")
+        verified += n
+    st = plan.stats()
+    t = float(np.median(times))
+    rs, rr, rh = (float(np.median([r[i] for r in replay])) for i in range(3))
+    res = {"value": round(nb * n * W.BUF / t / 2**30, 3), "unit": "GiB/s", "batches": nb,
+           "ms_per_batch": round(t / nb * 1e3, 3), "vs_headline": round(step_ms / (t / nb * 1e3), 4),
+           "sequence_ms": [round(x * 1e3, 2) for x in times],
+           "window_replay": {"host_ms_per_run": round(rs / max(rr, 1) * 1e3, 3), "runs": int(rr),
+                             "hits_per_run": int(rh / max(rr, 1)),
+                             "note": "host time replaying each run's lookup hits into the recent window "
+                                     "model, inside the next run's wait (overlapping it) or in the final "
+                                     "settle (inside the timed sequence)"},
+           "cache_segments_after": len(cache), "last_batch_stats": {"n_extract": int(st.n_extract),
+                                                                    "n_ref": int(st.n_ref),
+                                                                    "anchor_scans": int(st.anchor_scans),
+                                                                    "anchor_fallbacks": int(st.anchor_fallbacks)},
+           "verified_buffers": verified, "verified_against": "oracle digests live_b0..live_b%d" % (nb - 1),
+           "workload": f"{nb} cfg5-shaped batches (seeds 0x5555..0x{0x5555 + nb - 1:x}) back to back on one "
+                       "live pool-warmed cache, no restore between them; timed from the warm snapshot to the "
+                       "last run's window replay"}
+    plan.close()
+    cache.close()
+    return res
 
 
 def host_cores() -> int:
@@ -485,6 +574,9 @@ def main():
                               "overlapping the encode -> streams packed into pinned host memory "
                               f"({int(hlens.sum()) >> 20} MiB) by a kernel after each sub-batch; every buffer "
                               "checked against the oracle digests")
+
+    if rank == 0 and world == 1 and not args.no_live and args.total == 32768:
+        result["live_cache"] = bench_live(args, ctx, warm, d_in, step_s * 1e3)
 
     if rank == 0 and world == 1 and not args.no_decode:
         result["decode"] = bench_decode(args, ctx, warm)

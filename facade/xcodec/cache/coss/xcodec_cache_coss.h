@@ -17,38 +17,47 @@
 #include <xcodec/xcodec_cache.h>
 
 class XCodecCacheCOSS : public XCodecCache {
-    xchip::Context ctx_;
+    xc_ctx* ctx_;
     xc_coss* coss_;
 
 public:
     XCodecCacheCOSS(const UUID& uuid, const std::string& cache_dir, size_t cache_size, int gpu = 0)
-    : XCodecCache(uuid, cache_size), ctx_(gpu), coss_(0)
+    : XCodecCache(uuid, cache_size), ctx_(0), coss_(0)
     {
         uint8_t u[UUID_STRING_SIZE + 1];
         uuid.to_string(u);
-        xchip::check(xc_coss_open(ctx_.get(), cache_dir.c_str(), (const char*) u, cache_size, &coss_));
+        xcodec_facade::halt_on(xc_ctx_create(gpu, &ctx_), "/xcodec/cache/coss", "device context");
+        xcodec_facade::halt_on(xc_coss_open(ctx_, cache_dir.c_str(), (const char*) u, cache_size, &coss_),
+                               "/xcodec/cache/coss", "open");
     }
-    ~XCodecCacheCOSS() { xc_coss_close(coss_); }
+    ~XCodecCacheCOSS()
+    {
+        xc_coss_close(coss_);
+        xc_ctx_destroy(ctx_);
+    }
 
     void enter(const uint64_t& hash, const Buffer& buf, unsigned off)
     {
         uint8_t seg[XCODEC_SEGMENT_LENGTH];
         buf.copyout(seg, off, sizeof seg);
-        xchip::check(xc_coss_enter(coss_, hash, seg));
+        xcodec_facade::halt_on(xcodec_facade::call(xc_coss_cache(coss_), [&] { return xc_coss_enter(coss_, hash, seg); }),
+                               "/xcodec/cache/coss", "enter");
     }
 
     bool lookup(const uint64_t& hash, Buffer& buf)
     {
         uint8_t seg[XCODEC_SEGMENT_LENGTH];
         int found = 0;
-        xchip::check(xc_coss_lookup(coss_, hash, seg, &found));
+        xcodec_facade::halt_on(
+            xcodec_facade::call(xc_coss_cache(coss_), [&] { return xc_coss_lookup(coss_, hash, seg, &found); }),
+            "/xcodec/cache/coss", "lookup");
         if (found)
             buf.append(seg, sizeof seg);
         return found != 0;
     }
 
     xc_coss* coss() { return coss_; }
-    xc_ctx* context() { return ctx_.get(); }
+    xc_ctx* context() { return ctx_; }
 };
 
 #endif /* !XCODEC_CACHE_COSS_XCODEC_CACHE_COSS_H */

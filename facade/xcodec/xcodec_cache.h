@@ -18,7 +18,33 @@
 #include <common/uuid/uuid.h>
 #include <xcodec/xcodec.h>
 
-#include "xcodec_hip.hpp" /* include/ of this repository */
+#include "xcodec_hip.h" /* include/ of this repository */
+
+/* The library's status codes in the reference's contract: the reference's encoder and cache cannot
+ * fail (xcodec_encoder.h:53-57, xcodec_cache.h:182-210) and xcodec_filter.cc:122-164 has no
+ * exception handling, so nothing is thrown through it.
+ *  - XC_EBUSY (a run another caller submitted on this cache is in flight): that run is finished
+ *    first (xc_cache_quiesce) and the call is made again;
+ *  - any other failure of an encoder or cache call cannot be continued from: it is logged and the
+ *    process halts, as the reference does when an allocation fails (HALT, common/log.h:195);
+ *  - a decoder's failure is a decode that returns false (DecodeFilter::consume then reports
+ *    "Decoder failed", xcodec_filter.cc). */
+namespace xcodec_facade {
+template <class F>
+inline int call(xc_cache* dev, F f)
+{
+    int rc = f();
+    if (rc == XC_EBUSY && dev && xc_cache_quiesce(dev) == XC_OK)
+        rc = f();
+    return rc;
+}
+
+inline void halt_on(int rc, const LogHandle& log, const char* what)
+{
+    if (rc != XC_OK)
+        HALT(log) << what << ": " << xc_last_error() << " (" << rc << ")";
+}
+}
 
 class XCodecCache {
     UUID uuid_;
@@ -45,31 +71,44 @@ public:
 /* XCodecMemoryCache (xcodec_cache.h:162-211) held in HBM.  The device cache starts at
  * cap_segments and grows like the reference's map before any call that could fill it. */
 class XCodecMemoryCache : public XCodecCache {
-    xchip::Context ctx_;
-    xchip::Cache cache_;
+    xc_ctx* ctx_;
+    xc_cache* cache_;
 
 public:
     XCodecMemoryCache(const UUID& uuid, size_t size, int gpu = 0, uint64_t cap_segments = 1u << 16)
-    : XCodecCache(uuid, size), ctx_(gpu), cache_(ctx_, cap_segments) { }
+    : XCodecCache(uuid, size), ctx_(0), cache_(0)
+    {
+        xcodec_facade::halt_on(xc_ctx_create(gpu, &ctx_), "/xcodec/cache/memory", "device context");
+        xcodec_facade::halt_on(xc_cache_create(ctx_, cap_segments, &cache_), "/xcodec/cache/memory", "device cache");
+    }
+    ~XCodecMemoryCache()
+    {
+        xc_cache_destroy(cache_);
+        xc_ctx_destroy(ctx_);
+    }
 
     void enter(const uint64_t& hash, const Buffer& buf, unsigned off)
     {
         uint8_t seg[XCODEC_SEGMENT_LENGTH];
         buf.copyout(seg, off, sizeof seg);
-        cache_.enter(hash, seg);
+        xcodec_facade::halt_on(xcodec_facade::call(cache_, [&] { return xc_cache_enter(cache_, hash, seg); }),
+                               "/xcodec/cache/memory", "enter");
     }
 
     bool lookup(const uint64_t& hash, Buffer& buf)
     {
-        xchip::Bytes seg;
-        if (!cache_.lookup(hash, seg))
+        uint8_t seg[XCODEC_SEGMENT_LENGTH];
+        int found = 0;
+        xcodec_facade::halt_on(xcodec_facade::call(cache_, [&] { return xc_cache_lookup(cache_, hash, seg, &found); }),
+                               "/xcodec/cache/memory", "lookup");
+        if (!found)
             return false;
-        buf.append(&seg[0], seg.size());
+        buf.append(seg, sizeof seg);
         return true;
     }
 
-    xc_cache *device() { return cache_.get(); }
-    xc_ctx *context() { return ctx_.get(); }
+    xc_cache *device() { return cache_; }
+    xc_ctx *context() { return ctx_; }
 };
 
 #endif /* !XCODEC_XCODEC_CACHE_H */

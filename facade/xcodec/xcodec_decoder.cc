@@ -4,15 +4,20 @@
  */
 #include <vector>
 
+#include "xcodec_hip.hpp" /* xchip::decode_bound */
+
 #include <common/buffer.h>
 #include <xcodec/xcodec.h>
 #include <xcodec/xcodec_cache.h>
 #include <xcodec/xcodec_decoder.h>
 
-XCodecDecoder::XCodecDecoder(XCodecCache* cache) : cache_(cache) { }
+XCodecDecoder::XCodecDecoder(XCodecCache* cache) : log_("/xcodec/decoder"), cache_(cache) { }
 
 XCodecDecoder::~XCodecDecoder() { }
 
+/* The reference's decode returns false on a collision or a bad opcode (xcodec_decoder.cc:76-176);
+ * a library failure is reported the same way (the filter then fails the connection), after a run in
+ * flight on the cache was finished and the call made again (XC_EBUSY). */
 bool XCodecDecoder::decode(Buffer& output, Buffer& input, std::set<uint64_t>& unknown_hashes)
 {
     if (input.empty())
@@ -24,12 +29,22 @@ bool XCodecDecoder::decode(Buffer& output, Buffer& input, std::set<uint64_t>& un
     uint64_t off = 0, len = n, cap = xchip::decode_bound(&in[0], n), olen = 0, consumed = 0, unknown = 0;
     int32_t status = 0, has_unknown = 0;
     std::vector<uint8_t> out(cap);
+    xc_cache* dev = cache_->coss() ? xc_coss_cache(cache_->coss()) : cache_->device();
+    int rc;
     if (cache_->coss())
-        xchip::check(xc_coss_decode_batch_host(cache_->coss(), &in[0], &off, &len, 1, &out[0], &off, &cap, &olen,
-                                               &consumed, &status, &unknown, &has_unknown));
+        rc = xcodec_facade::call(dev, [&] {
+            return xc_coss_decode_batch_host(cache_->coss(), &in[0], &off, &len, 1, &out[0], &off, &cap, &olen,
+                                             &consumed, &status, &unknown, &has_unknown);
+        });
     else
-        xchip::check(xc_decode_batch_host(cache_->device(), &in[0], &off, &len, 1, &out[0], &off, &cap, &olen,
-                                          &consumed, &status, &unknown, &has_unknown));
+        rc = xcodec_facade::call(dev, [&] {
+            return xc_decode_batch_host(dev, &in[0], &off, &len, 1, &out[0], &off, &cap, &olen, &consumed, &status,
+                                        &unknown, &has_unknown);
+        });
+    if (rc != XC_OK) {
+        ERROR(log_) << "device decode failed: " << xc_last_error() << " (" << rc << ")";
+        return false;
+    }
     if (olen)
         output.append(&out[0], olen);
     input.skip(consumed);  /* the reference consumes exactly this much (xcodec_decoder.cc:85-173) */

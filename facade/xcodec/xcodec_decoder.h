@@ -11,9 +11,12 @@
 
 #include <set>
 
+#include <common/log.h>
+
 class XCodecCache;
 
 class XCodecDecoder {
+    LogHandle log_;
     XCodecCache* cache_;
 
 public:

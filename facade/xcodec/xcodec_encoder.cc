@@ -7,10 +7,14 @@
 #include <xcodec/xcodec_cache.h>
 #include <xcodec/xcodec_encoder.h>
 
-XCodecEncoder::XCodecEncoder(XCodecCache* cache) : cache_(cache), enc_(0)
+XCodecEncoder::XCodecEncoder(XCodecCache* cache) : log_("/xcodec/encoder"), cache_(cache), enc_(0)
 {
-    xc_cache* dev = cache->coss() ? xc_coss_cache(cache->coss()) : cache->device();
-    xchip::check(xc_encoder_create(dev, &enc_));
+    xcodec_facade::halt_on(xc_encoder_create(dev(), &enc_), log_, "encoder");
+}
+
+xc_cache* XCodecEncoder::dev() const
+{
+    return cache_->coss() ? xc_coss_cache(cache_->coss()) : cache_->device();
 }
 
 XCodecEncoder::~XCodecEncoder()
@@ -18,17 +22,23 @@ XCodecEncoder::~XCodecEncoder()
     xc_encoder_destroy(enc_);
 }
 
-/* One call of this connection: encode(in) [+ flush()] (xcodec_encoder.cc:60-201). */
+/* One call of this connection: encode(in) [+ flush()] (xcodec_encoder.cc:60-201).  The reference's
+ * encoder cannot fail (xcodec_encoder.h:53-57): a run in flight on the cache is finished first
+ * (XC_EBUSY), anything else halts (xcodec_cache.h's notes). */
 void XCodecEncoder::call(Buffer& output, const uint8_t* in, uint64_t n, uint32_t flags, int* emitted)
 {
     uint64_t pend = 0;
-    xchip::check(xc_encoder_pending(enc_, &pend));
+    xcodec_facade::halt_on(xc_encoder_pending(enc_, &pend), log_, "encoder state");
     std::vector<uint8_t> out(2 * (pend + n) + 16);
     uint64_t off = 0, cap = out.size(), len = 0;
+    int rc;
     if (cache_->coss())
-        xchip::check(xc_coss_encode_streams(cache_->coss(), &enc_, &in, &n, &flags, 1, &out[0], &off, &cap, &len));
+        rc = xcodec_facade::call(dev(), [&] {
+            return xc_coss_encode_streams(cache_->coss(), &enc_, &in, &n, &flags, 1, &out[0], &off, &cap, &len);
+        });
     else
-        xchip::check(xc_encode_streams(&enc_, &in, &n, &flags, 1, &out[0], &off, &cap, &len));
+        rc = xcodec_facade::call(dev(), [&] { return xc_encode_streams(&enc_, &in, &n, &flags, 1, &out[0], &off, &cap, &len); });
+    xcodec_facade::halt_on(rc, log_, "encode");
     if (len)
         output.append(&out[0], len);
     if (emitted)

@@ -12,16 +12,19 @@
 
 #include <vector>
 
+#include <common/log.h>
 #include <xcodec/xcodec_hash.h>
 
-#include "xcodec_hip.hpp"
+#include "xcodec_hip.h"
 
 class XCodecCache;
 
 class XCodecEncoder {
+    LogHandle log_;
     XCodecCache* cache_;
     xc_encoder* enc_;
 
+    xc_cache* dev() const;
     void call(Buffer& output, const uint8_t* in, uint64_t n, uint32_t flags, int* emitted);
 
 public:

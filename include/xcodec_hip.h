@@ -109,10 +109,19 @@ int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_o
  * (yielding the CPU) until then.  Until the run is finished the plan, its cache and the arenas
  * belong to it (another submit on the plan fails with XC_EBUSY).  A run whose sub-batches need
  * the host (declaration growth, cross-buffer conflicts: rare) completes those inside the poll
- * or wait that finishes it.  xc_encode_run = submit + wait. */
+ * or wait that finishes it.  xc_encode_run = submit + wait.  On a memory cache where a stateful
+ * stream entered a hash twice with other bytes (the release build's XCodecMemoryCache::enter,
+ * DESIGN.md §5.6) a device-resident run fails with XC_EINVAL, from the submit or from the call that
+ * finishes it, and leaves the cache as it was before the run; xc_encode_batch_host and
+ * xc_encode_streams run such batches. */
 int xc_encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_out_len);
 int xc_encode_poll(xc_plan *p, int *done);
 int xc_encode_wait(xc_plan *p);
+/* Finish the run in flight on the cache, if any (submitted with xc_encode_submit and not yet
+ * finished by its poll / wait): blocks until it is done; the submitter's next xc_encode_poll /
+ * xc_encode_wait then returns that run's status.  For synchronous callers that met XC_EBUSY (the
+ * drop-in facade): the reference's encoder has no busy state to report. */
+int xc_cache_quiesce(xc_cache *c);
 /* When xc_encode_run / xc_encode_wait / xc_encode_poll report a run finished:
  * XC_COMPLETE_RUN (the default): every device write of the run is complete;
  * XC_COMPLETE_STREAM: the run is decided (its control words are final, the host has nothing left

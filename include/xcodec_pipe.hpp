@@ -155,6 +155,8 @@ public:
     uint64_t device_calls = 0;
 
 private:
+    inline void drain_round(std::vector<Job> &rnd);
+    inline void fail_owner(const void *owner);
     std::vector<Job> jobs_;
     std::vector<const void *> failed_;
     std::set<const void *> failed_set_;
@@ -493,6 +495,29 @@ inline void Batcher::drain()
         }
         std::vector<Job> rnd(std::make_move_iterator(jobs_.begin()), std::make_move_iterator(jobs_.begin() + (ptrdiff_t)r));
         jobs_.erase(jobs_.begin(), jobs_.begin() + (ptrdiff_t)r);
+        try {
+            drain_round(rnd);
+        } catch (...) {
+            // a library error: the device state of this round's encoders is unknown, so every filter
+            // of the round and of the jobs still deferred fails (its next consume refuses, as the
+            // reference's failing consume ends the connection); the caller sees the error
+            for (const Job &j : rnd) fail_owner(j.owner);
+            for (const Job &j : jobs_) fail_owner(j.owner);
+            jobs_.clear();
+            throw;
+        }
+    }
+}
+
+inline void Batcher::fail_owner(const void *owner)
+{
+    if (failed_set_.insert(owner).second) failed_.push_back(owner);
+}
+
+inline void Batcher::drain_round(std::vector<Job> &rnd)
+{
+    const size_t r = rnd.size();
+    {
         std::vector<const uint8_t *> op(r, nullptr);
         std::vector<size_t> on(r, 0);
         std::vector<int> st(r, 1);
@@ -555,10 +580,7 @@ inline void Batcher::drain()
             douts.push_back(std::move(out));
         }
         for (size_t k = 0; k < r; k++)
-            if (!rnd[k].done(op[k], on[k], st[k], cons[k], hu[k] != 0, unk[k])) {
-                failed_.push_back(rnd[k].owner);
-                failed_set_.insert(rnd[k].owner);
-            }
+            if (!rnd[k].done(op[k], on[k], st[k], cons[k], hu[k] != 0, unk[k])) fail_owner(rnd[k].owner);
     }
 }
 

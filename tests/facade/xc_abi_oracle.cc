@@ -15,7 +15,27 @@ struct xc_coss { xc_cache cache; };
 
 static std::string g_err;
 
+/* Test hooks (tests/facade/facade_filter.cc): busy mode models another caller's run left in flight
+ * on the cache after every call (the next call meets XC_EBUSY until xc_cache_quiesce); fail makes
+ * the encoder's or the decoder's device call fail. */
+static bool g_busy_mode = false, g_in_flight = false;
+static int g_quiesced = 0, g_fail_encode = 0, g_fail_decode = 0;
+static int busy_check()
+{
+    if (g_busy_mode && g_in_flight) { g_err = "a run on this cache is in flight"; return XC_EBUSY; }
+    return XC_OK;
+}
+static void busy_after() { if (g_busy_mode) g_in_flight = true; }
+
 extern "C" {
+void xc__test_inject(int busy, int fail_encode, int fail_decode)
+{
+    g_busy_mode = busy != 0;
+    g_fail_encode = fail_encode;
+    g_fail_decode = fail_decode;
+}
+int xc__test_quiesced(void) { return g_quiesced; }
+int xc_cache_quiesce(xc_cache *) { g_in_flight = false; g_quiesced++; return XC_OK; }
 const char *xc_last_error(void) { return g_err.c_str(); }
 int xc_device_count(int *n) { *n = 1; return XC_OK; }
 int xc_ctx_create(int dev, xc_ctx **out) { *out = new xc_ctx{dev}; return XC_OK; }
@@ -25,18 +45,29 @@ int xc_cache_destroy(xc_cache *c) { if (c) xo_cache_free(c->c); delete c; return
 int xc_cache_count(xc_cache *c, uint64_t *n) { *n = xo_cache_count(c->c); return XC_OK; }
 int xc_cache_lookup(xc_cache *c, uint64_t h, uint8_t *out, int *found)
 {
+    if (int rc = busy_check()) return rc;
+    busy_after();
     const uint8_t *d = nullptr;
     *found = xo_cache_lookup(c->c, h, &d);
     if (*found) std::memcpy(out, d, XC_SEGMENT_LENGTH);
     return XC_OK;
 }
-int xc_cache_enter(xc_cache *c, uint64_t h, const uint8_t *seg) { xo_cache_enter(c->c, h, seg); return XC_OK; }
+int xc_cache_enter(xc_cache *c, uint64_t h, const uint8_t *seg)
+{
+    if (int rc = busy_check()) return rc;
+    busy_after();
+    xo_cache_enter(c->c, h, seg);
+    return XC_OK;
+}
 int xc_encoder_create(xc_cache *c, xc_encoder **out) { *out = new xc_encoder{xo_encoder_new(c->c), c}; return XC_OK; }
 int xc_encoder_destroy(xc_encoder *e) { if (e) xo_encoder_free(e->e); delete e; return XC_OK; }
 int xc_encoder_pending(xc_encoder *e, uint64_t *n) { *n = xo_encoder_pending(e->e); return XC_OK; }
 int xc_encode_streams(xc_encoder *const *enc, const uint8_t *const *in, const uint64_t *in_len, const uint32_t *flags,
                       uint64_t n, uint8_t *out, const uint64_t *out_off, const uint64_t *out_cap, uint64_t *out_len)
 {
+    if (int rc = busy_check()) return rc;
+    busy_after();
+    if (g_fail_encode) { g_err = "injected device failure"; return XC_EDEVICE; }
     for (uint64_t k = 0; k < n; k++) {
         xo_bytes b = {nullptr, 0, 0};
         if (in_len[k]) xo_encode(enc[k]->e, in[k], in_len[k], &b);
@@ -52,6 +83,9 @@ int xc_decode_batch_host(xc_cache *c, const uint8_t *in, const uint64_t *in_off,
                          uint8_t *out, const uint64_t *out_off, const uint64_t *out_cap, uint64_t *out_len,
                          uint64_t *consumed, int32_t *status, uint64_t *unknown, int32_t *has_unknown)
 {
+    if (int rc = busy_check()) return rc;
+    busy_after();
+    if (g_fail_decode) { g_err = "injected device failure"; return XC_EDEVICE; }
     return xo_decode_batch(c->c, in, in_off, in_len, nbuf, out, out_off, out_cap, out_len, consumed, status, unknown,
                            has_unknown) ? XC_EINVAL : XC_OK;
 }

@@ -55,3 +55,40 @@ def test_facade_round_trip_with_the_reference_buffer(tmp_path):
          "-Wl,-rpath," + os.path.join(ROOT, "oracle"), "-l:libuuid.so.1"], tmp_path)
     r = subprocess.run([str(tmp_path / "rt")], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "facade ok" in r.stdout, r.stdout + r.stderr
+
+
+def _build_filter_program(tmp_path):
+    """The reference's unchanged xcodec_filter.cc with its event system, Buffer and log, over the
+    facade and the CPU stand-in of the C ABI (tests/facade/facade_filter.cc)."""
+    make = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], capture_output=True, text=True)
+    assert make.returncode == 0, make.stderr
+    fac = os.path.join(ROOT, "facade", "xcodec")
+    t = os.path.join(ROOT, "tests", "facade")
+    ref = [os.path.join(REF, f) for f in ("xcodec/xcodec_filter.cc", "event/event_system.cc", "event/io_service.cc",
+                                          "event/event_poll_epoll.cc", "common/thread/thread.cc", "common/log.cc",
+                                          "common/buffer.cc", "common/uuid/uuid.cc")]
+    # (sections: the DecodeFilter half of the TU needs the proxy's globals, which this program does
+    # not link; the linker drops it, EncodeFilter is what runs)
+    _cc(["-w", "-ffunction-sections", "-fdata-sections", "-Wl,--gc-sections", "-o", "ff",
+         os.path.join(t, "facade_filter.cc"), os.path.join(fac, "xcodec_encoder.cc"),
+         os.path.join(fac, "xcodec_decoder.cc"), os.path.join(t, "xc_abi_oracle.cc")] + ref +
+        ["-L" + os.path.join(ROOT, "oracle"), "-loracle", "-Wl,-rpath," + os.path.join(ROOT, "oracle"),
+         "-l:libuuid.so.1", "-lpthread"], tmp_path)
+    return str(tmp_path / "ff")
+
+
+def test_reference_filter_over_the_facade_never_throws(tmp_path):
+    """No exception crosses the reference's filter (xcodec_filter.cc:122-164 has no handler, and the
+    reference's encoder cannot fail, xcodec_encoder.h:53-57): EncodeFilter::consume meets XC_EBUSY on
+    every library call and the facade finishes the run in flight (xc_cache_quiesce) and calls again,
+    the stream round-trips exactly; a failing decode is decode() == false; a failing encode halts
+    (the reference's HALT: logged, abort), as a failed allocation would."""
+    ff = _build_filter_program(tmp_path)
+    r = subprocess.run([ff], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "facade filter ok" in r.stdout, r.stdout + r.stderr
+    r = subprocess.run([ff, "busy"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "facade filter ok" in r.stdout and " 0 quiesced" not in r.stdout, r.stdout + r.stderr
+    r = subprocess.run([ff, "fail-decode"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "decode false" in r.stdout and "device decode failed" in r.stderr, r.stdout + r.stderr
+    r = subprocess.run([ff, "fail-encode"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == -6 and "Halting: encode" in r.stderr, (r.returncode, r.stdout, r.stderr)

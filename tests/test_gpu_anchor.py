@@ -220,3 +220,84 @@ def test_anchor_scan_recent_window_after_collisions(gpu_ctx, oracle_mod):
     e = [np.concatenate([W.gen(97, 500), x, W.gen(98, 200)]), np.concatenate([y, x, W.gen(99, 64)])]
     assert w.XCodecEncoder(cache).encode_batch(e) == oc.encode_batch(e)
     assert len(cache) == len(oc)
+
+
+@pytest.mark.parametrize("ch", [0x41, 0xF1])
+def test_anchorless_segment_survives_a_host_enter(gpu_ctx, oracle_mod, ch):
+    """An anchor run enters a segment without an anchor (a constant run of a byte whose G never
+    falls below 2^26) at an unaligned position (after a REF found through the index): the emit
+    records it on the device only.  A host-API enter (xc_cache_enter) in between must not erase that
+    record, or the next anchor run would not fall back to the exact scan and would miss the REFs to
+    that segment (xcodec_encoder.cc:111-118)."""
+    cache, oc, pool = _pool_cache(gpu_ctx, oracle_mod, 64)
+    # (2600 bytes: the declared segment right after the REF is all ch, while every aligned block still
+    # has an anchor, so no predicted declaration sends the run to the exact scan)
+    run = np.full(2600, ch, np.uint8)
+    first = [np.concatenate([W.gen(0xA1, 300), pool[7 * 2048:8 * 2048], run, W.gen(0xA2, 3000)])]
+    assert all(_last_anchor(first[0][i:i + 2048]) is not None for i in range(0, len(first[0]) - 2047, 2048))
+    got, st = _plan_run(gpu_ctx, cache, first)
+    _same(got, oc.encode_batch(first))
+    assert st.anchor_scans >= 1 and st.anchor_fallbacks == 0, (st.anchor_scans, st.anchor_fallbacks)
+    seg = W.gen(0xA3, 2048)
+    h = oracle_mod.hash_segment(seg)
+    cache.enter(h, seg)
+    oc.enter(h, seg)
+    again = [np.concatenate([W.gen(0xA4, 777), np.full(4500, ch, np.uint8), W.gen(0xA5, 2000)]),
+             np.concatenate([W.gen(0xA6, 1500), seg, W.gen(0xA7, 100)])]
+    want = oc.encode_batch(again)
+    assert b"\xf1\x02" in want[0]  # the run is a REF to the anchorless segment in the reference
+    got, st = _plan_run(gpu_ctx, cache, again)
+    _same(got, want)
+    assert len(cache) == len(oc)
+
+
+def test_anchor_scan_collision_with_a_twin_declared_in_the_same_sub_batch(gpu_ctx, oracle_mod):
+    """The invisible collision (y's anchor context differs from x's) at a lookup that would set the
+    candidate, where x is not in the cache but declared by an EARLIER buffer of the same anchor-
+    scanned sub-batch (the declaration set D, not the cache): the reference sees x in its map at that
+    lookup and does not take y as the candidate (xcodec_encoder.cc:129-137).  The REF before y (found
+    through the index) puts the lookup exactly at y's window end (xcodec_encoder.cc:111-118)."""
+    cache, oc, pool = _pool_cache(gpu_ctx, oracle_mod, 64)
+    x, y = _collision_pair(7, in_anchor=True)
+    assert oracle_mod.hash_segment(x) == oracle_mod.hash_segment(y)
+    seg = pool[9 * 2048:10 * 2048]
+    bufs = [np.concatenate([x, W.gen(0xB1, 4000)]),                       # x: a (predicted) declaration
+            W.gen(0xB2, 40000),
+            np.concatenate([W.gen(0xB3, 300), seg, y, W.gen(0xB4, 3000)]),  # REF seg, then y's window
+            np.concatenate([W.gen(0xB5, 1300), seg, y]),
+            np.concatenate([y, W.gen(0xB6, 2500)])]                        # aligned: a cross-buffer D match
+    want = oc.encode_batch(bufs)
+    got, st = _plan_run(gpu_ctx, cache, bufs)
+    _same(got, want)
+    assert st.anchor_scans >= 1
+    assert len(cache) == len(oc)
+    # and once more on the grown cache (x now in the cache, y's windows again at candidate lookups)
+    more = [np.concatenate([W.gen(0xB7, 900), seg, y, W.gen(0xB8, 700)]), np.concatenate([x, y])]
+    got, st = _plan_run(gpu_ctx, cache, more)
+    _same(got, oc.encode_batch(more))
+
+
+def test_anchor_scan_twin_against_a_carried_candidate(gpu_ctx, oracle_mod):
+    """A stateful connection carries a pending candidate whose window is y's; an anchor-scanned batch
+    then declares the twin x; the connection's next call completes the lookups after the candidate
+    and declares y (a duplicate enter of the hash: the map takes y, the window keeps what it
+    remembered), and fresh encoders after it see the reference's answers (xcodec_encoder.cc:77-82,
+    203-215; xcodec_cache.h:137-147,182-188)."""
+    import wanproxy_amd as w
+    cache, oc, pool = _pool_cache(gpu_ctx, oracle_mod, 64)
+    x, y = _collision_pair(9, in_anchor=True)
+    seg = pool[3 * 2048:4 * 2048]
+    gs, os_ = w.XCodecStreamEncoder(cache), oracle_mod.Encoder(oc)
+    a = np.concatenate([W.gen(0xC1, 200), seg, y, W.gen(0xC2, 60)])   # candidate y, carried
+    assert gs.encode(a) == os_.encode(a)
+    b = [np.concatenate([x, W.gen(0xC3, 4000)]), np.concatenate([W.gen(0xC4, 700), seg, y, W.gen(0xC5, 900)])]
+    got, st = _plan_run(gpu_ctx, cache, b)
+    _same(got, oc.encode_batch(b))
+    assert st.anchor_scans >= 1
+    c = W.gen(0xC6, 4200)
+    assert gs.encode(c) == os_.encode(c)
+    assert gs.flush() == os_.flush()
+    e = [np.concatenate([W.gen(0xC7, 300), seg, x, W.gen(0xC8, 90)]), np.concatenate([y, x]),
+         np.concatenate([W.gen(0xC9, 300), seg, y])]
+    assert w.XCodecEncoder(cache).encode_batch(e) == oc.encode_batch(e)
+    assert len(cache) == len(oc)

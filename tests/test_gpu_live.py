@@ -1,0 +1,142 @@
+"""Back-to-back device-resident runs on a live cache (no restore in between), as a proxy runs.
+
+The reference remembers every map hit in the recent window inside lookup()
+(xcodec/xcodec_cache.h:130-147,190-210).  The device cache keeps no window: each run's lookup hits
+are packed behind it on the device, copied to pinned memory beside the next run and replayed into
+the host window model while the next run works, or before the next operation whose answer depends
+on the window.  These tests check that the replayed window is the reference's:
+runs back to back through submit / wait (the replay of run k happens inside run k+1's wait), then a
+duplicate enter whose answers depend on what the window holds after them, every byte against the
+stateful oracle (oracle/xc_oracle.c)."""
+import numpy as np
+import pytest
+
+from wanproxy_amd import workloads as W
+
+pytestmark = pytest.mark.gpu
+
+POOL = 96
+
+
+def _collision_pair(seed=1):
+    rng = np.random.default_rng(seed)
+    x = (rng.integers(2, 126, 2048, dtype=np.int64) * 2 + 1).astype(np.uint8)
+    y = x.copy()
+    y[100] += 2; y[101] -= 2; y[1500] -= 2; y[1501] += 2
+    return x, y
+
+
+def _cat(*a):
+    return np.concatenate([np.asarray(v, np.uint8) for v in a])
+
+
+class Runner:
+    """One EncodePlan per batch shape, device arenas kept; run() = submit + wait of one batch."""
+
+    def __init__(self, cache, stream_ordered=True):
+        self.cache = cache
+        self.plans = {}
+        self.stream_ordered = stream_ordered
+
+    def run(self, bufs):
+        import torch
+        import wanproxy_amd as w
+        key = tuple(len(b) for b in bufs)
+        if key not in self.plans:
+            plan = w.EncodePlan(self.cache, list(key))
+            plan.set_completion(self.stream_ordered)
+            d_in = torch.zeros(plan.in_bytes, dtype=torch.uint8, device="cuda")
+            d_out = torch.zeros(plan.out_bytes, dtype=torch.uint8, device="cuda")
+            d_len = torch.zeros(max(len(bufs), 1), dtype=torch.int64, device="cuda")
+            self.plans[key] = (plan, d_in, d_out, d_len)
+        plan, d_in, d_out, d_len = self.plans[key]
+        arena = np.zeros(plan.in_bytes, np.uint8)
+        for i, b in enumerate(bufs):
+            arena[int(plan.in_off[i]):int(plan.in_off[i]) + len(b)] = b
+        d_in.copy_(torch.from_numpy(arena))
+        plan.submit(d_in.data_ptr(), d_out.data_ptr(), d_len.data_ptr())
+        plan.wait()
+        torch.cuda.synchronize()
+        out = d_out.cpu().numpy()
+        lens = d_len.cpu().numpy()
+        return [out[int(plan.out_off[i]):int(plan.out_off[i]) + int(lens[i])].tobytes() for i in range(len(bufs))]
+
+    def close(self):
+        for plan, *_ in self.plans.values():
+            plan.close()
+
+
+def _same(got, want, what):
+    bad = [i for i, (g, e) in enumerate(zip(got, want)) if g != e]
+    assert len(got) == len(want) and not bad, f"{what}: buffers {bad[:8]} differ from the oracle"
+
+
+def test_back_to_back_runs_equal_the_oracle(gpu_ctx, oracle_mod, monkeypatch):
+    """Six runs on one live cache with fresh seeds (pool repeats, new content, repeats of earlier
+    runs' content), two shapes alternating, several sub-batches each: every buffer equals the
+    sequential oracle's, and every run's lookup hits were replayed (the window's record)."""
+    import wanproxy_amd as w
+    monkeypatch.setenv("XC_SUB_MB", "2")
+    pool = W.pool(512)
+    warm = [pool[i:i + 65536] for i in range(0, len(pool), 65536)]
+    cache = w.XCodecCache(gpu_ctx, 1 << 14)
+    oc = oracle_mod.Cache()
+    _same(w.XCodecEncoder(cache).encode_batch(warm), oc.encode_batch(warm), "warm-up")
+    r = Runner(cache)
+    prev = []
+    before = cache.hit_stats()
+    for k in range(6):
+        bufs = W.repeat_buffers(96 if k % 2 == 0 else 64, 0x6100 + k, np_segments=512, pool_bytes=pool)
+        if prev:  # content of the run before, shifted
+            bufs[3] = _cat(W.gen(0x6200 + k, 777), prev[5][:40000])
+        _same(r.run(bufs), oc.encode_batch(bufs), f"run {k}")
+        prev = bufs
+    cache.settle()
+    st = cache.hit_stats()
+    assert st["runs"] - before["runs"] >= 6 and st["hits"] > before["hits"], st
+    assert len(cache) == len(oc)
+    r.close()
+
+
+@pytest.mark.parametrize("evict", [0, 40, 70])
+def test_window_after_back_to_back_runs(gpu_ctx, oracle_mod, evict):
+    """Connection 0 carries candidate x; connection 1 enters the twin y (same hash, other bytes);
+    device-resident run A REFs y (the window remembers y), run B REFs `evict` distinct pool segments
+    (64 push y out), run C is fresh data; then connection 0 declares x (a duplicate enter: the map
+    answers x, the window y while it holds it, xcodec_cache.h:137-147,182-188).  Fresh encoders and
+    a direct lookup afterwards see what the reference's cache returns, which depends on the window
+    the replayed hits of A, B and C built."""
+    import wanproxy_amd as w
+    x, y = _collision_pair()
+    p = W.pool(POOL)
+    warm = W.pool_warmup_buffers(POOL)
+    oc = oracle_mod.Cache()
+    gc = w.XCodecCache(gpu_ctx, 1 << 12)
+    oc.encode_batch(warm)
+    w.XCodecEncoder(gc).encode_batch(warm)
+    o0, g0 = oracle_mod.Encoder(oc), w.XCodecStreamEncoder(gc)
+    o1, g1 = oracle_mod.Encoder(oc), w.XCodecStreamEncoder(gc)
+    a = _cat(x, W.gen(11, 100))
+    assert g0.encode(a) == o0.encode(a)           # candidate x, looked up (a miss), carried
+    assert g1.encode(y) == o1.encode(y)
+    assert g1.flush() == o1.flush()               # y declared: the hash is in the map
+    r = Runner(gc)
+    runs = [[_cat(y, W.gen(12, 50)), W.gen(15, 30000)],                                # A: REF y
+            [_cat(*[p[2048 * i:2048 * (i + 1)] for i in range(evict)]) if evict else W.gen(16, 4096),
+             W.gen(17, 20000)],                                                        # B
+            [W.gen(18, 65536), W.gen(19, 9000)]]                                       # C
+    for k, bufs in enumerate(runs):
+        _same(r.run(bufs), oc.encode_batch(bufs), f"run {'ABC'[k]}")
+    d = W.gen(13, 4096)
+    assert g0.encode(d) == o0.encode(d)           # x declared: the duplicate enter
+    assert g0.flush() == o0.flush()
+    h = int(oracle_mod.hash_segment(x))
+    bufs = [_cat(x, W.gen(20, 99)), _cat(y, W.gen(21, 77)), _cat(W.gen(22, 33), x), y]
+    want = oc.encode_batch(bufs)
+    assert w.XCodecEncoder(gc).encode_batch(bufs) == want
+    # the scenario reaches both answers: y from the window while it holds it, x from the map after
+    has_ref = [b"\xf1\x02" in s for s in want]
+    assert has_ref[1] == (evict < 64) and has_ref[0] == (evict >= 64), has_ref
+    assert gc.lookup(h) == oc.lookup(h)
+    assert len(gc) == len(oc)
+    r.close()

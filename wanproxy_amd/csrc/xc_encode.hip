@@ -2173,7 +2173,8 @@ __global__ void k_hits(PlanDev P, uint64_t *out)
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= P.nb) return;
     uint64_t *o = out + P.tok_base[b] + (uint64_t)b * (COLL_CAP + 1u);
-    const uint32_t tb = P.tok_base[b], n = P.tok_cnt[b], cc = P.coll_cnt[b], nc = min(cc, COLL_CAP);
+    const uint32_t tb = P.tok_base[b], n = min(P.tok_cnt[b], P.tok_base[b + 1] - tb), cc = P.coll_cnt[b];
+    const uint32_t nc = min(cc, COLL_CAP);
     uint32_t k = 0, ci = 0;
     for (uint32_t t = 0; t < n; t++) {
         if (P.tok_op[tb + t] != OP_REF) continue;
@@ -2189,6 +2190,18 @@ __global__ void k_hits(PlanDev P, uint64_t *out)
         o[1 + k++] = ((uint64_t)r.z << 32) | r.y;
     }
     o[0] = (uint64_t)k | (cc > COLL_CAP ? 1ull << 63 : 0ull);
+}
+
+// k_hits' output (device) into pinned host memory, only the words each buffer filled: one wave per
+// buffer, a few workgroups (the writes cross PCIe; the kernel runs beside the next run).
+__global__ void k_hits_out(const uint64_t *stage, uint64_t *host, const uint32_t *tok_base, uint32_t nb)
+{
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); b < nb; b += waves) {
+        const uint64_t off = tok_base[b] + (uint64_t)b * (COLL_CAP + 1u);
+        const uint32_t n = 1u + (uint32_t)(stage[off] & 0xFFFFFFFFu);
+        for (uint32_t i = lane_id(); i < n; i += 64u) host[off + i] = stage[off + i];
+    }
 }
 
 // The table values of n hashes (~0: absent or evicted), no side effects.

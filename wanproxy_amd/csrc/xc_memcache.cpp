@@ -30,6 +30,7 @@ extern "C" int xc__cache_find(xc_cache *c, const uint64_t *h, uint64_t n, uint64
 extern "C" int xc__cache_read(xc_cache *c, uint64_t h, uint8_t *out, int *found);            // no side effects
 extern "C" int xc__cache_set_value(xc_cache *c, uint64_t h, uint64_t val);
 extern "C" void xc__cache_engine(xc_cache *c, int on);
+extern "C" int xc__cache_settle(xc_cache *c);  // the earlier runs' lookup hits into the window first
 
 namespace {
 using replay::SEG;
@@ -346,6 +347,7 @@ extern "C" int xc__mem_encode_batch(xc_memmodel *m, const uint8_t *in, const uin
                                     uint64_t nbuf, uint8_t *out, const uint64_t *out_off, const uint64_t *out_cap,
                                     uint64_t *out_len)
 {
+    if (int rc = xc__cache_settle(m->cache)) return rc;
     try {
         Engine e(m);
         Ctx c(m);
@@ -371,6 +373,7 @@ extern "C" int xc__mem_encode_gather(xc_memmodel *m, uint64_t nbuf, const uint8_
                                                  const uint8_t *in),
                                      void *ctx)
 {
+    if (int rc = xc__cache_settle(m->cache)) return rc;
     try {
         Engine e(m);
         Ctx c(m);
@@ -402,6 +405,7 @@ extern "C" int xc__mem_decode_batch(xc_memmodel *m, const uint8_t *in, const uin
                                     uint64_t *out_len, uint64_t *consumed, int32_t *status, uint64_t *unknown,
                                     int32_t *has_unknown)
 {
+    if (int rc = xc__cache_settle(m->cache)) return rc;
     try {
         Engine e(m);
         Ctx c(m);
@@ -416,6 +420,7 @@ extern "C" int xc__mem_decode_batch(xc_memmodel *m, const uint8_t *in, const uin
 // the window decides the bytes and remembers a map hit.
 extern "C" int xc__mem_lookup(xc_memmodel *m, uint64_t h, uint8_t *out, int *found)
 {
+    if (int rc = xc__cache_settle(m->cache)) return rc;
     try {
         Ctx c(m);
         uint64_t v = 0;
@@ -443,6 +448,7 @@ extern "C" int xc__mem_lookup(xc_memmodel *m, uint64_t h, uint8_t *out, int *fou
 // *dup = 0: the hash is absent, the caller enters it on the device.
 extern "C" int xc__mem_enter(xc_memmodel *m, uint64_t h, const uint8_t *seg, int *dup)
 {
+    if (int rc = xc__cache_settle(m->cache)) return rc;
     try {
         Ctx c(m);
         uint64_t v = 0;

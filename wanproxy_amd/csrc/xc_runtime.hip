@@ -12,7 +12,9 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <chrono>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <mutex>
 #include <string>
@@ -380,8 +382,28 @@ struct xc_cache {
     // by a restore), and whether the replay engine drives the cache (no hooks then)
     xc_memmodel *mem = nullptr;
     xc_memmodel *mem_snap = nullptr;
-    xc_plan *pend_enc = nullptr;
     void *pend_dec = nullptr;
+    // The encoder runs' lookup hits for the window model, in run order: k_hits
+    // packs a finished run's hits into a device slot behind the run on the context stream,
+    // k_hits_out copies them into the slot's pinned memory on hl_stream, and the host replays them
+    // while the next run works (its wait) or before the next operation whose answer depends on the
+    // window (cache_settle); a restore drops them.  Two slots: the next run packs into the other.
+    struct HitSlot {
+        uint64_t *d = nullptr;   // device: per buffer at tok_base[b] + b * (COLL_CAP + 1), count first
+        uint64_t *h = nullptr;   // pinned host copy (same layout), hd its device address
+        uint64_t *hd = nullptr;
+        uint32_t *dtb = nullptr;  // device copy of the run's tok_base (the copy outlives the plan)
+        size_t cap = 0, tb_cap = 0;
+        hipEvent_t ev = nullptr;  // the copy into h is complete
+        std::vector<uint32_t> tok_base;
+        uint32_t nb = 0;
+    } hl[2];
+    std::deque<int> hl_fifo;  // slots whose hits are not replayed yet, oldest first
+    int hl_next = 0;
+    hipStream_t hl_stream = nullptr;
+    hipEvent_t hl_packed = nullptr;
+    uint64_t hl_runs = 0, hl_hits = 0;
+    double hl_sec = 0;  // host time spent replaying
     int engine = 0;
     // anchor index: segments [0, anc_upto) are in it (runs without anchors and
     // other enter paths append behind it: a backfill catches up before an anchor run); anc_bad:
@@ -559,6 +581,14 @@ extern "C" int xc_cache_destroy(xc_cache *c)
     dfree(c->snap_l2);
     xc__mem_free(c->mem);
     xc__mem_free(c->mem_snap);
+    for (auto &sl : c->hl) {
+        dfree(sl.d);
+        dfree(sl.dtb);
+        pool_free(sl.h);
+        if (sl.ev) hipEventDestroy(sl.ev);
+    }
+    if (c->hl_packed) hipEventDestroy(c->hl_packed);
+    if (c->hl_stream) hipStreamDestroy(c->hl_stream);
     delete c;
     return XC_OK;
 }
@@ -630,6 +660,11 @@ static int cache_rebuild(xc_cache *c, uint64_t ncap, uint32_t keep, bool drop_de
     uint32_t count = 0;
     int rc = cache_count_host(c, &count);
     if (rc) return rc;
+    {   // the device's record of an anchorless segment (an anchor run's emit) joins the host's
+        uint32_t bad = 0;
+        HIPCHK(hipMemcpy(&bad, c->ctl + CTL_ANCLESS, 4, hipMemcpyDeviceToHost));
+        if (bad) c->anc_bad = std::min(c->anc_bad, ~bad);
+    }
     count = std::min<uint32_t>(count, (uint32_t)c->cap);
     const uint32_t kept = std::min(count, keep);
     // the device part of the segment store grows up to the device's share, the spill tier after it
@@ -701,6 +736,9 @@ static int cache_rebuild(xc_cache *c, uint64_t ncap, uint32_t keep, bool drop_de
     c->aundo = aundo;
     c->anc_upto = akept;
     if (c->anc_bad >= kept) c->anc_bad = NONE;
+    // the device word follows (a stale one would send every later anchor run to the exact scan)
+    c->anc_bad_word = c->anc_bad == NONE ? 0u : ~c->anc_bad;
+    HIPCHK(hipMemcpy(c->ctl + CTL_ANCLESS, &c->anc_bad_word, 4, hipMemcpyHostToDevice));
     c->set.release(true);
     if (move_segs) {
         dfree(c->segs);
@@ -909,7 +947,7 @@ static int cache_restore_async(xc_cache *c, uint32_t cur_count)
 // The model as it was at the snapshot (the runs since are undone: their lookups are not replayed).
 static int mem_restore(xc_cache *c)
 {
-    c->pend_enc = nullptr;
+    c->hl_fifo.clear();
     c->pend_dec = nullptr;
     return c->mem && c->mem_snap ? xc__mem_restore(c->mem, c->mem_snap) : XC_OK;
 }
@@ -1072,7 +1110,9 @@ extern "C" int xc_cache_enter(xc_cache *c, uint64_t h, const uint8_t *seg)
     if ((rc = cache_reserve(c, 1))) return rc;
     c->host_count = -1;
     HIPCHK(hipMemcpyAsync(c->ctx->d_seg, seg, XC_SEG, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemsetAsync(c->ctl, 0, CTL_WORDS * 4, s));
+    // only the word k_enter_one reports: CTL_ANCLESS is the device's record of an anchorless
+    // segment an anchor run entered, which the host may not have learned yet
+    HIPCHK(hipMemsetAsync(c->ctl + CTL_ERROR, 0, 4, s));
     hipLaunchKernelGGL(k_enter_one, dim3(1), dim3(64), 0, s, cache_plandev(c), h, (const uint8_t *)c->ctx->d_seg);
     HIPCHK(hipGetLastError());
     uint32_t ctl[CTL_WORDS];
@@ -1215,6 +1255,10 @@ struct xc_plan {
     bool pass_published = false;  // the in-flight first pass publishes them (else a copy)
     int completion = XC_COMPLETE_RUN;  // xc_plan_set_completion
     bool inflight = false;        // xc_encode_submit enqueued a run not finished yet
+    // xc_cache_quiesce finished the run for another caller: its status, for the submitter's poll/wait
+    bool parked = false;
+    int parked_rc = XC_OK;
+    std::string parked_msg;
     hipEvent_t ev_ctl = nullptr;
     std::vector<hipEvent_t> ev_hash, ev_go;
     uint32_t next_hash = 0;  // first sub-batch not yet enqueued for hashing in this run
@@ -1251,7 +1295,6 @@ struct xc_plan {
     uint4 *d_coll = nullptr;         // collision records of every buffer (COLL_CAP each)
     uint32_t *d_coll_cnt = nullptr;
     std::vector<uint32_t> tok_base;  // host copy [nb + 1]
-    uint64_t *h_hits = nullptr;      // pinned: the host path's lookup hits (k_hits)
     int64_t count0 = -1;             // the cache's count before a run that may enter a hash twice
     uint64_t max_new = 0;            // most segments a run can enter (sum of len / 2048 + 1)
     // anchor index: xc_plan_set_scan's mode; this run hashes anchors (anc_run),
@@ -1444,7 +1487,7 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
         HIPCHK(hipMemcpyAsync(p->d_buf_off, p->in_off.data(), nbuf * 8, hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(p->d_out_off, p->out_off.data(), nbuf * 8, hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(p->d_buf_len, blen.data(), nbuf * 4, hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemcpyAsync(p->d_tok_base, tok_base.data(), nbuf * 4, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(p->d_tok_base, tok_base.data(), (nbuf + 1) * 4, hipMemcpyHostToDevice, s));
     }
     HIPCHK(hipMemcpyAsync(p->d_chunk0, chunk0.data(), (nbuf + 1) * 4, hipMemcpyHostToDevice, s));
     if (!chunks.empty()) {
@@ -1563,62 +1606,137 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     return XC_OK;
 }
 
-// A finished run's lookup hits in the reference's order: per buffer, its REF tokens (window end
-// seg + 2047) and its collision lookups, by position.  *complete = 0 when a buffer had more
-// collisions than were recorded.
-static int plan_hits(xc_plan *p, std::vector<uint64_t> &hits, int *complete)
+static hipError_t spin_wait(hipEvent_t ev);
+
+// Replay the oldest slot's hits into the window model (per buffer, in the reference's order: its
+// REF tokens and its recorded collision lookups, by position; bit 63 of the count: more collisions
+// than were recorded).  block = false: only when its copy is complete (*done = 0 otherwise).
+static int hits_replay_front(xc_cache *c, bool block, bool *done)
 {
-    *complete = 1;
-    if (!p->nb) return XC_OK;
-    const uint64_t nt = p->tok_base[p->nb];
-    std::vector<uint32_t> cnt(p->nb), op(nt), seg(nt), ccnt(p->nb);
-    std::vector<uint64_t> th(nt);
-    std::vector<uint4> coll((size_t)p->nb * COLL_CAP);
-    hipStream_t s = p->cache->ctx->stream;
-    HIPCHK(hipMemcpyAsync(cnt.data(), p->P.tok_cnt, p->nb * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(op.data(), p->P.tok_op, nt * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(seg.data(), p->P.tok_seg, nt * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(th.data(), p->P.tok_h, nt * 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(ccnt.data(), p->d_coll_cnt, p->nb * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(coll.data(), p->d_coll, coll.size() * sizeof(uint4), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    for (uint64_t b = 0; b < p->nb; b++) {
-        const uint32_t tb = p->tok_base[b], n = std::min(cnt[b], p->tok_base[b + 1] - tb);
-        const uint32_t nc = std::min<uint32_t>(ccnt[b], COLL_CAP);
-        if (ccnt[b] > COLL_CAP) *complete = 0;
-        uint32_t ci = 0;
-        for (uint32_t t = 0; t < n; t++) {
-            if (op[tb + t] != OP_REF) continue;
-            const uint32_t q = seg[tb + t] + (XC_SEG - 1u);
-            for (; ci < nc && coll[b * COLL_CAP + ci].x < q; ci++)
-                hits.push_back(((uint64_t)coll[b * COLL_CAP + ci].z << 32) | coll[b * COLL_CAP + ci].y);
-            hits.push_back(th[tb + t]);
-        }
-        for (; ci < nc; ci++) hits.push_back(((uint64_t)coll[b * COLL_CAP + ci].z << 32) | coll[b * COLL_CAP + ci].y);
+    xc_cache::HitSlot &sl = c->hl[c->hl_fifo.front()];
+    hipError_t e = hipEventQuery(sl.ev);
+    if (e == hipErrorNotReady) {
+        *done = false;
+        if (!block) return XC_OK;
+        e = spin_wait(sl.ev);
+    }
+    if (e != hipSuccess) return fail(XC_EDEVICE, std::string("lookup hits: ") + hipGetErrorString(e));
+    const auto t0 = std::chrono::steady_clock::now();
+    uint64_t n = 0;
+    for (uint32_t b = 0; b < sl.nb; b++) {
+        const uint64_t *r = sl.h + sl.tok_base[b] + (uint64_t)b * (COLL_CAP + 1u);
+        const uint64_t k = r[0] & 0xFFFFFFFFu;
+        xc__mem_hits(c->mem, r + 1, k, (r[0] >> 63) ? 0 : 1);
+        n += k;
+    }
+    c->hl_fifo.pop_front();
+    c->hl_runs++;
+    c->hl_hits += n;
+    c->hl_sec += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    *done = true;
+    return XC_OK;
+}
+
+// Every pending run's hits that are ready (block: all of them, waiting for their copies).
+static int hits_replay(xc_cache *c, bool block)
+{
+    while (!c->hl_fifo.empty()) {
+        bool done = false;
+        if (int rc = hits_replay_front(c, block, &done)) return rc;
+        if (!done) break;
     }
     return XC_OK;
 }
 
-// The pending run's lookup hits into the recent window (before anything that comes after it).
+// A finished run's hits into the next slot (enqueued behind the run: tokens and collision records
+// are final, the tail check's included).
+static int hits_enqueue(xc_plan *p)
+{
+    xc_cache *c = p->cache;
+    if (!p->nb) return XC_OK;
+    const int si = c->hl_next;
+    // the slot's older hits first (the FIFO keeps the runs' order)
+    while (std::find(c->hl_fifo.begin(), c->hl_fifo.end(), si) != c->hl_fifo.end()) {
+        bool done = false;
+        if (int rc = hits_replay_front(c, true, &done)) return rc;
+    }
+    xc_cache::HitSlot &sl = c->hl[si];
+    hipStream_t m = c->ctx->stream;
+    if (!c->hl_stream) {
+        HIPCHK(hipStreamCreateWithFlags(&c->hl_stream, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&c->hl_packed, hipEventDisableTiming));
+    }
+    if (!sl.ev) HIPCHK(hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
+    const size_t words = p->tok_base[p->nb] + (size_t)p->nb * (COLL_CAP + 1u);
+    if (sl.cap < words || sl.tb_cap < (size_t)p->nb + 1) {
+        HIPCHK(hipEventSynchronize(sl.ev));  // (a dropped slot's copy may still run)
+        dfree(sl.d);
+        dfree(sl.dtb);
+        pool_free(sl.h);
+        sl.d = nullptr;
+        sl.h = nullptr;
+        sl.dtb = nullptr;
+        sl.cap = sl.tb_cap = 0;
+        const size_t cap = words + words / 4, tbc = (size_t)p->nb + 1 + p->nb / 4;
+        if (dmalloc(&sl.d, cap * 8) != hipSuccess || dmalloc(&sl.dtb, tbc * 4) != hipSuccess ||
+            hmalloc((void **)&sl.h, cap * 8) != hipSuccess)
+            return fail(XC_ENOMEM, "lookup-hit buffers: allocation failed");
+        void *dp = nullptr;
+        HIPCHK(hipHostGetDevicePointer(&dp, sl.h, 0));
+        sl.hd = (uint64_t *)dp;
+        sl.cap = cap;
+        sl.tb_cap = tbc;
+    }
+    HIPCHK(hipStreamWaitEvent(m, sl.ev, 0));  // the slot's previous copy has read d
+    HIPCHK(hipMemcpyAsync(sl.dtb, p->d_tok_base, ((size_t)p->nb + 1) * 4, hipMemcpyDeviceToDevice, m));
+    hipLaunchKernelGGL(k_hits, dim3((p->nb + 255) / 256), dim3(256), 0, m, p->P, sl.d);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->hl_packed, m));
+    HIPCHK(hipStreamWaitEvent(c->hl_stream, c->hl_packed, 0));
+    hipLaunchKernelGGL(k_hits_out, dim3(std::min<uint32_t>((p->nb + 3) / 4, 64u)), dim3(256), 0, c->hl_stream,
+                       (const uint64_t *)sl.d, sl.hd, (const uint32_t *)sl.dtb, p->nb);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(sl.ev, c->hl_stream));
+    sl.tok_base = p->tok_base;
+    sl.nb = p->nb;
+    c->hl_fifo.push_back(si);
+    c->hl_next = si ^ 1;
+    return XC_OK;
+}
+
+// A pending decode run's hits into the recent window (before anything that comes after it).
+static int cache_settle_dec(xc_cache *c)
+{
+    if (!c->mem || c->engine || !c->pend_dec) return XC_OK;
+    void *d = c->pend_dec;
+    c->pend_dec = nullptr;
+    uint64_t *h = nullptr, n = 0;
+    int complete = 1;
+    if (int rc = xc__dplan_hits(d, &h, &n, &complete)) return rc;
+    xc__mem_hits(c->mem, h, n, complete);
+    free(h);
+    return XC_OK;
+}
+
+// The pending runs' lookup hits into the recent window (before anything that comes after them).
 static int cache_settle(xc_cache *c)
 {
     if (!c->mem || c->engine) return XC_OK;
-    std::vector<uint64_t> hits;
-    int complete = 1, rc = XC_OK;
-    if (c->pend_enc) {
-        xc_plan *p = c->pend_enc;
-        c->pend_enc = nullptr;
-        if ((rc = set_dev(c->ctx)) || (rc = plan_hits(p, hits, &complete))) return rc;
-        xc__mem_hits(c->mem, hits.data(), hits.size(), complete);
-    }
-    if (c->pend_dec) {
-        void *d = c->pend_dec;
-        c->pend_dec = nullptr;
-        uint64_t *h = nullptr, n = 0;
-        if ((rc = xc__dplan_hits(d, &h, &n, &complete))) return rc;
-        xc__mem_hits(c->mem, h, n, complete);
-        free(h);
-    }
+    if (int rc = set_dev(c->ctx)) return rc;
+    if (int rc = hits_replay(c, true)) return rc;
+    return cache_settle_dec(c);
+}
+
+// For the replay engine (xc_memcache.cpp): the window is complete before it reads it.
+extern "C" int xc__cache_settle(xc_cache *c) { return c ? cache_settle(c) : XC_OK; }
+
+// (bench) runs replayed into the window, their hits, host seconds spent.
+extern "C" int xc__cache_hit_stats(xc_cache *c, uint64_t *runs, uint64_t *hits, double *sec)
+{
+    if (!c || !runs || !hits || !sec) return fail(XC_EINVAL, "null");
+    *runs = c->hl_runs;
+    *hits = c->hl_hits;
+    *sec = c->hl_sec;
     return XC_OK;
 }
 
@@ -1650,7 +1768,6 @@ extern "C" int xc_plan_destroy(xc_plan *p)
 {
     if (!p) return XC_OK;
     hipSetDevice(p->cache->ctx->dev);
-    if (p->cache->pend_enc == p) cache_settle(p->cache);  // (its tokens are the window's record)
     // pooled memory goes back for reuse at once: nothing may still read or write it
     hipStreamSynchronize(p->cache->ctx->stream);
     if (p->hs) hipStreamSynchronize(p->hs);
@@ -1700,7 +1817,6 @@ extern "C" int xc_plan_destroy(xc_plan *p)
     dfree(p->d_stream_st);
     dfree(p->d_stream_res);
     dfree(p->d_coll);
-    pool_free(p->h_hits);
     dfree(p->d_coll_cnt);
     for (auto &x : p->ev_live) { hipEventDestroy(x.second.first); hipEventDestroy(x.second.second); }
     for (auto e : p->ev_pool) hipEventDestroy(e);
@@ -1933,11 +2049,26 @@ static hipError_t pass_state(xc_plan *p)
     return published(p) ? hipSuccess : hipStreamQuery(p->cache->ctx->stream);
 }
 
+// While the device works: the earlier runs' lookup hits whose copies are complete go to the window.
+static void replay_while_waiting(xc_plan *p)
+{
+    xc_cache *c = p->cache;
+    if (!c->hl_fifo.empty() && c->mem && !c->engine) hits_replay(c, false);  // (an error shows at the settle)
+}
+
 static hipError_t wait_decided(xc_plan *p)
 {
-    if (!early_done(p)) return spin_wait(p->ev_ctl);
+    if (!early_done(p)) {
+        for (int i = 0;; i++) {
+            const hipError_t e = hipEventQuery(p->ev_ctl);
+            if (e != hipErrorNotReady) return e;
+            replay_while_waiting(p);
+            if (i >= 64) sched_yield();
+        }
+    }
     for (int i = 0;; i++) {
         if (published(p)) return hipSuccess;
+        if ((i & 255) == 0) replay_while_waiting(p);
         if ((i & 255) == 255) {
             const hipError_t e = pass_state(p);
             if (e != hipErrorNotReady) return e;
@@ -2336,8 +2467,9 @@ static int graph_launch(xc_plan *p)
 static int launch_tailcheck(xc_plan *p);
 
 // Everything of a run up to its first asynchronous pass, which is enqueued with ev_ctl after it.
-extern "C" int xc_encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_out_len)
+static int encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_out_len)
 {
+    if (p) p->parked = false;
     if (p && p->inflight) return fail(XC_EBUSY, "a run of this plan is in flight (xc_encode_poll / xc_encode_wait)");
     if (!p || (!d_in && p->nb) || (!d_out && p->nb) || (!d_out_len && p->nb)) return fail(XC_EINVAL, "null");
     int rc = set_dev(p->cache->ctx);
@@ -2345,7 +2477,8 @@ extern "C" int xc_encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out,
     hipStream_t s = p->cache->ctx->stream;
     // room for every segment this run can declare (the reference's cache never fills)
     xc_cache *c = p->cache;
-    if ((rc = cache_busy(c, p)) || (rc = cache_settle(c))) return rc;
+    // (a decode's hits go first; earlier encode runs' hits are replayed while this one works)
+    if ((rc = cache_busy(c, p)) || (rc = cache_settle_dec(c)) || (rc = hits_replay(c, false))) return rc;
     if (c->mem && !c->engine) {
         // a hash entered twice may answer with other bytes than the device holds: the host paths
         // replay such runs (xc_memcache.cpp)
@@ -2521,14 +2654,25 @@ static int encode_finish(xc_plan *p)
             c->host_count = p->count0;
             return fail(XC__SLOW, "a hash entered twice");
         }
-        c->pend_enc = p;  // its lookup hits go to the recent window when the order needs them
+        if ((rc = hits_enqueue(p))) return rc;  // its lookup hits, for the recent window
     }
     return XC_OK;
 }
 
-extern "C" int xc_encode_poll(xc_plan *p, int *done)
+// A run xc_cache_quiesce finished: its status, once, to its submitter.
+static int take_parked(xc_plan *p)
+{
+    p->parked = false;
+    return p->parked_rc ? fail(p->parked_rc, p->parked_msg) : XC_OK;
+}
+
+static int encode_poll(xc_plan *p, int *done)
 {
     if (!p || !done) return fail(XC_EINVAL, "null");
+    if (!p->inflight && p->parked) {
+        *done = 1;
+        return take_parked(p);
+    }
     if (!p->inflight) return fail(XC_EINVAL, "no run in flight");
     int rc = set_dev(p->cache->ctx);
     if (rc) return rc;
@@ -2546,9 +2690,10 @@ extern "C" int xc_encode_poll(xc_plan *p, int *done)
     return encode_finish(p);
 }
 
-extern "C" int xc_encode_wait(xc_plan *p)
+static int encode_wait(xc_plan *p)
 {
     if (!p) return fail(XC_EINVAL, "null");
+    if (!p->inflight && p->parked) return take_parked(p);
     if (!p->inflight) return fail(XC_EINVAL, "no run in flight");
     int rc = set_dev(p->cache->ctx);
     if (rc) return rc;
@@ -2569,14 +2714,51 @@ extern "C" int xc_plan_set_completion(xc_plan *p, int mode)
     return XC_OK;
 }
 
-extern "C" int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_out_len)
+// The library's host paths take an XC__SLOW run to the replay engine; a device-resident caller
+// gets the documented code (the cache is as before the run: a duplicate enter was rolled back).
+static int public_rc(const xc_plan *p, int rc)
 {
-    int rc = xc_encode_submit(p, d_in, d_out, d_out_len);
-    if (!rc) rc = xc_encode_wait(p);
     if (rc == XC__SLOW && p && !p->host_path)
         return fail(XC_EINVAL, "device-resident run on a cache with a hash entered twice by a stateful stream: "
                                "run it through xc_encode_batch_host / xc_encode_streams (the recent window's replay)");
     return rc;
+}
+
+extern "C" int xc_encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_out_len)
+{
+    return public_rc(p, encode_submit(p, d_in, d_out, d_out_len));
+}
+
+extern "C" int xc_encode_poll(xc_plan *p, int *done)
+{
+    return public_rc(p, encode_poll(p, done));
+}
+
+extern "C" int xc_encode_wait(xc_plan *p)
+{
+    return public_rc(p, encode_wait(p));
+}
+
+// Finish the run in flight on the cache (another caller's submit): a synchronous call that met
+// XC_EBUSY can then go ahead; the submitter's next poll / wait returns that run's status.
+extern "C" int xc_cache_quiesce(xc_cache *c)
+{
+    if (!c) return fail(XC_EINVAL, "null");
+    int rc = set_dev(c->ctx);
+    if (rc || !c->busy) return rc;
+    xc_plan *p = (xc_plan *)c->busy;
+    const int r = encode_wait(p);
+    p->parked = true;
+    p->parked_rc = r;
+    p->parked_msg = r ? g_err : std::string();
+    return XC_OK;
+}
+
+extern "C" int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_out_len)
+{
+    int rc = encode_submit(p, d_in, d_out, d_out_len);
+    if (!rc) rc = encode_wait(p);
+    return public_rc(p, rc);
 }
 
 extern "C" int xc_host_alloc(xc_ctx *ctx, uint64_t bytes, void **out)
@@ -2639,31 +2821,8 @@ extern "C" int xc_encode_run_host(xc_plan *p, const uint8_t *h_in, uint8_t *h_ou
         HIPCHK(hipMemcpyAsync(h_len, p->e_len, p->nb * 8, hipMemcpyDeviceToHost, s));
         if (h_pos) HIPCHK(hipMemcpyAsync(h_pos, p->e_pos, p->nb * 8, hipMemcpyDeviceToHost, s));
     }
-    // the run's lookup hits for the recent window, written by a kernel into pinned memory beside
-    // the outputs (no copy round trips): replayed once the run has synchronised
-    xc_cache *c = p->cache;
-    const bool hits = c->mem && !c->engine && c->pend_enc == p && p->nb;
-    const size_t hwords = p->tok_base[p->nb] + (size_t)p->nb * (COLL_CAP + 1);
-    if (hits) {
-        if (!p->h_hits && hmalloc((void **)&p->h_hits, hwords * 8) != hipSuccess)
-            return fail(XC_ENOMEM, "pinned allocation failed");
-        void *dev = nullptr;
-        HIPCHK(hipHostGetDevicePointer(&dev, p->h_hits, 0));
-        hipLaunchKernelGGL(k_hits, dim3((p->nb + 255) / 256), dim3(256), 0, s, p->P, (uint64_t *)dev);
-        HIPCHK(hipGetLastError());
-    }
+    // (the run's lookup hits go to the recent window through the cache's hit log, hits_enqueue)
     HIPCHK(hipStreamSynchronize(s));
-    if (hits) {
-        std::vector<uint64_t> v;
-        int complete = 1;
-        for (uint64_t b = 0; b < p->nb; b++) {
-            const uint64_t *r = p->h_hits + p->tok_base[b] + b * (COLL_CAP + 1);
-            if (r[0] >> 63) complete = 0;
-            v.insert(v.end(), r + 1, r + 1 + (r[0] & 0xFFFFFFFFu));
-        }
-        xc__mem_hits(c->mem, v.data(), v.size(), complete);
-        c->pend_enc = nullptr;
-    }
     return XC_OK;
 }
 

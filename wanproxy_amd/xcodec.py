@@ -39,7 +39,7 @@ SYMBOLS = [
     "xc_coss_open", "xc_coss_close", "xc_coss_cache", "xc_coss_count", "xc_coss_stats", "xc_coss_lookup",
     "xc_coss_enter", "xc_coss_encode_batch_host", "xc_coss_decode_batch_host", "xc_coss_store_lookup",
     "xc_coss_store_enter", "xc_coss_encode_streams", "xc_encode_submit", "xc_encode_poll", "xc_encode_wait",
-    "xc_plan_set_completion", "xc_dplan_set_completion", "xc_plan_set_scan",
+    "xc_plan_set_completion", "xc_dplan_set_completion", "xc_plan_set_scan", "xc_cache_quiesce",
 ]
 STREAM_FLUSH = 1  # XC_STREAM_FLUSH
 
@@ -118,6 +118,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.xc_encode_submit.argtypes = [_vp, _vp, _vp, _vp]
     lib.xc_encode_poll.argtypes = [_vp, C.POINTER(C.c_int)]
     lib.xc_encode_wait.argtypes = [_vp]
+    lib.xc_cache_quiesce.argtypes = [_vp]
     lib.xc_plan_set_completion.argtypes = [_vp, C.c_int]
     lib.xc_plan_set_scan.argtypes = [_vp, C.c_int]
     lib.xc_plan_stats.argtypes = [_vp, C.POINTER(RunStats)]
@@ -316,6 +317,27 @@ class XCodecCache:
     def restore_async(self) -> None:
         """Enqueue the restore on the context stream (no host synchronisation)."""
         _check(load_library().xc_cache_restore_async(self.h))
+
+    def quiesce(self) -> None:
+        """Finish a run submitted on this cache and not yet waited for (xc_cache_quiesce)."""
+        _check(load_library().xc_cache_quiesce(self.h))
+
+    def hit_stats(self) -> dict:
+        """(bench) The recent window's replay of encoder runs' lookup hits: runs and hits replayed,
+        host seconds spent (xc__cache_hit_stats)."""
+        lib = load_library()
+        lib.xc__cache_hit_stats.argtypes = [_vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                            C.POINTER(C.c_double)]
+        r, h, t = C.c_uint64(), C.c_uint64(), C.c_double()
+        _check(lib.xc__cache_hit_stats(self.h, C.byref(r), C.byref(h), C.byref(t)))
+        return {"runs": r.value, "hits": h.value, "host_s": t.value}
+
+    def settle(self) -> None:
+        """(bench) Replay every finished run's lookup hits into the recent window now (what the next
+        window-dependent operation would do first)."""
+        lib = load_library()
+        lib.xc__cache_settle.argtypes = [_vp]
+        _check(lib.xc__cache_settle(self.h))
 
     def close(self) -> None:
         if getattr(self, "h", None):
