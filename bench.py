@@ -56,6 +56,8 @@ def parse():
                     help="KEY=VAL set only for the per-kernel diagnostic steps after the timed region and "
                          "the verification (timing ablations, e.g. XC_ABL_EMIT=4)")
     ap.add_argument("--decode-streams", type=int, default=4096, help="cfg4: streams decoded per step")
+    ap.add_argument("--only", choices=["cfg2", "cfg3", "cfg4"],
+                    help="run just that leg (one GPU) and print its JSON object (kernel traces, A/B)")
     ap.add_argument("--no-live", action="store_true", help="skip the steady-state (live cache) leg")
     ap.add_argument("--live-batches", type=int, default=4)
     ap.add_argument("--live-reps", type=int, default=3)
@@ -239,6 +241,7 @@ def bench_live(args, ctx, warm, d_in0, step_ms):
     lens = np.full(n, W.BUF, np.uint64)
     plan = w.EncodePlan(cache, lens)
     plan.set_completion(True)
+    plan.set_input_ready(True)  # (every batch's arena is written before the timed sequences)
     d_in = [d_in0]
     for k in range(1, nb):
         x = torch.zeros(plan.in_bytes, dtype=torch.uint8, device="cuda")
@@ -393,6 +396,15 @@ def main():
     from wanproxy_amd import workloads as W
 
     ctx = w.Context(dev)
+    if args.only:
+        if args.only == "cfg4":
+            print(json.dumps(bench_decode(args, ctx, W.pool_warmup_buffers())))
+        elif args.only == "cfg2":
+            print(json.dumps(bench_encode_leg(ctx, None, W.random_buffers(256), args.steps, "cfg2")))
+        else:
+            print(json.dumps(bench_encode_leg(ctx, W.pool_warmup_buffers(), list(W.repeat_shard(4096, 0x77)),
+                                              args.steps, "cfg3")))
+        return
     shard = W.repeat_shard(args.total, 0x5555, rank, world)  # (n_local, 65536)
     n_local = shard.shape[0]
     warm = W.pool_warmup_buffers()
@@ -404,6 +416,7 @@ def main():
     lens = np.full(n_local, W.BUF, dtype=np.uint64)
     plan = w.EncodePlan(cache, lens)
     plan.set_completion(True)  # (stream ordered: every read below follows a device synchronize)
+    plan.set_input_ready(True)  # (the input arena is written once, before the first step)
     assert all(int(plan.in_off[i]) == i * W.BUF for i in range(n_local))
     d_in = torch.zeros(plan.in_bytes, dtype=torch.uint8, device="cuda")
     d_in[:n_local * W.BUF] = torch.from_numpy(shard.reshape(-1)).cuda()
@@ -540,7 +553,8 @@ def main():
                   "sub_batches": int(st.sub_batches), "outer_rounds": int(st.outer_rounds),
                   "walk_rounds": int(st.walk_rounds), "dense_chunks": int(st.dense_chunks),
                   "redone": int(st.redone), "shadow_misses": int(st.shadow_misses),
-                  "anchor_scans": int(st.anchor_scans), "anchor_fallbacks": int(st.anchor_fallbacks)},
+                  "anchor_scans": int(st.anchor_scans), "anchor_fallbacks": int(st.anchor_fallbacks),
+                  "early_hashed": int(st.early_hashed)},
         "verified_buffers": verified_job,
         "verified_against": ver["verified_against"] if world == 1 else
         f"oracle digests cfg5_g{world}_r* (every rank, every buffer of its shard)" if case else "oracle run",

@@ -122,6 +122,12 @@ int xc_encode_wait(xc_plan *p);
  * xc_encode_wait then returns that run's status.  For synchronous callers that met XC_EBUSY (the
  * drop-in facade): the reference's encoder has no busy state to report. */
 int xc_cache_quiesce(xc_cache *c);
+/* The caller guarantees that the input arena a run is submitted with is complete when the submit is
+ * called (not written by work still pending on any stream, the context stream included) and stays
+ * unchanged until the run is finished.  The run's first sub-batch is then hashed at once on a side
+ * stream, beside the device work of the plan's previous run (its last kernels and the host's turn),
+ * instead of after everything enqueued before the submit.  Default 0. */
+int xc_plan_set_input_ready(xc_plan *p, int ready);
 /* When xc_encode_run / xc_encode_wait / xc_encode_poll report a run finished:
  * XC_COMPLETE_RUN (the default): every device write of the run is complete;
  * XC_COMPLETE_STREAM: the run is decided (its control words are final, the host has nothing left
@@ -187,6 +193,8 @@ typedef struct {
     uint32_t anchor_scans;  /* sub-batches whose first scan took its events from the anchor index */
     uint32_t anchor_fallbacks; /* ... handed to the exact scan (a collision at a candidate, an
                                anchorless declaration, an overflowing record list) */
+    uint32_t early_hashed;  /* 1: the first sub-batch was hashed at the submit (xc_plan_set_input_ready) */
+    uint32_t reserved;
 } xc_run_stats;
 int xc_plan_stats(xc_plan *p, xc_run_stats *st);
 

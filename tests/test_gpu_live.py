@@ -33,18 +33,20 @@ def _cat(*a):
 class Runner:
     """One EncodePlan per batch shape, device arenas kept; run() = submit + wait of one batch."""
 
-    def __init__(self, cache, stream_ordered=True):
+    def __init__(self, cache, stream_ordered=True, input_ready=False):
         self.cache = cache
         self.plans = {}
         self.stream_ordered = stream_ordered
+        self.input_ready = input_ready
 
-    def run(self, bufs):
+    def run(self, bufs, stats=False):
         import torch
         import wanproxy_amd as w
         key = tuple(len(b) for b in bufs)
         if key not in self.plans:
             plan = w.EncodePlan(self.cache, list(key))
             plan.set_completion(self.stream_ordered)
+            plan.set_input_ready(self.input_ready)
             d_in = torch.zeros(plan.in_bytes, dtype=torch.uint8, device="cuda")
             d_out = torch.zeros(plan.out_bytes, dtype=torch.uint8, device="cuda")
             d_len = torch.zeros(max(len(bufs), 1), dtype=torch.int64, device="cuda")
@@ -53,13 +55,16 @@ class Runner:
         arena = np.zeros(plan.in_bytes, np.uint8)
         for i, b in enumerate(bufs):
             arena[int(plan.in_off[i]):int(plan.in_off[i]) + len(b)] = b
+        torch.cuda.synchronize()  # (the previous run's device work reads d_in: stream-ordered completion)
         d_in.copy_(torch.from_numpy(arena))
+        torch.cuda.synchronize()  # (the input is complete before the submit: input_ready)
         plan.submit(d_in.data_ptr(), d_out.data_ptr(), d_len.data_ptr())
         plan.wait()
         torch.cuda.synchronize()
         out = d_out.cpu().numpy()
         lens = d_len.cpu().numpy()
-        return [out[int(plan.out_off[i]):int(plan.out_off[i]) + int(lens[i])].tobytes() for i in range(len(bufs))]
+        got = [out[int(plan.out_off[i]):int(plan.out_off[i]) + int(lens[i])].tobytes() for i in range(len(bufs))]
+        return (got, plan.stats()) if stats else got
 
     def close(self):
         for plan, *_ in self.plans.values():
@@ -139,4 +144,46 @@ def test_window_after_back_to_back_runs(gpu_ctx, oracle_mod, evict):
     assert has_ref[1] == (evict < 64) and has_ref[0] == (evict >= 64), has_ref
     assert gc.lookup(h) == oc.lookup(h)
     assert len(gc) == len(oc)
+    r.close()
+
+
+def test_first_sub_batch_hashed_ahead(gpu_ctx, oracle_mod, monkeypatch):
+    """xc_plan_set_input_ready: a plan's next run hashes its first sub-batch on the side stream at the
+    submit, beside the previous run's last kernels, its compares taking only the entries complete
+    then.  Runs of one plan back to back (some anchor-scanned), a restore in between (the bench's
+    step), another plan's run and a host enter in between (which write the cache: no early hashing
+    for the next run): every buffer equals the oracle's."""
+    import wanproxy_amd as w
+    monkeypatch.setenv("XC_SUB_MB", "2")
+    pool = W.pool(512)
+    warm = [pool[i:i + 65536] for i in range(0, len(pool), 65536)]
+    cache = w.XCodecCache(gpu_ctx, 1 << 14)
+    oc = oracle_mod.Cache()
+    _same(w.XCodecEncoder(cache).encode_batch(warm), oc.encode_batch(warm), "warm-up")
+    cache.snapshot()
+    snap = oc.clone()
+    r = Runner(cache, input_ready=True)
+    early = []
+    for k in range(9):
+        if k == 3:  # the bench's step: back to the snapshot
+            cache.restore()
+            oc = snap.clone()
+        if k == 5:  # another plan's run writes the cache
+            other = [W.gen(0x6400, 70000), np.concatenate([pool[:30000], W.gen(0x6401, 9000)])]
+            _same(w.XCodecEncoder(cache).encode_batch(other), oc.encode_batch(other), "other plan")
+        if k == 7:  # a host enter
+            seg = W.gen(0x6402, 2048)
+            cache.enter(oracle_mod.hash_segment(seg), seg)
+            oc.enter(oracle_mod.hash_segment(seg), seg)
+        bufs = W.repeat_buffers(96, 0x6300 + k, np_segments=512, pool_bytes=pool)
+        if k % 2:  # repeats of the previous run's content at shifted offsets
+            bufs[7] = _cat(W.gen(0x6310 + k, 1234), prev[11][:50000])
+            bufs[8] = prev[12].copy()
+        got, st = r.run(bufs, stats=True)
+        _same(got, oc.encode_batch(bufs), f"run {k}")
+        early.append(int(st.early_hashed))
+        prev = bufs
+    # every run after one of this plan hashes ahead, except after another plan's run or an enter
+    assert early == [0, 1, 1, 1, 1, 0, 1, 0, 1], early
+    assert len(cache) == len(oc)
     r.close()

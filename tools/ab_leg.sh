@@ -1,4 +1,4 @@
-# A/B timing of one small encode leg (tools/leg.py) on one box, alternating A and B as tools/ab.sh
+# A/B timing of one small encode leg (bench.py --only) on one box, alternating A and B as tools/ab.sh
 # does.  usage (GPU box): bash tools/ab_leg.sh TAG CASE [ROUNDS] [STEPS]
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 out=gpurun_out/${1:-ableg}
@@ -10,7 +10,7 @@ for r in $(seq 1 ${3:-3}); do
     if [ $v = b ]; then
       if [ -n "$B_ENV" ]; then envs="$B_ENV"; else lib=$PWD/wanproxy_amd/${B_LIB:-libxcodec_hip_b.so}; fi
     fi
-    env $envs XC_LIB_PATH=$lib timeout -k 10 200 python tools/leg.py ${2:-cfg2} ${4:-200} > $out/$v$r.log 2>&1 || exit 1
+    env $envs XC_LIB_PATH=$lib timeout -k 10 200 python bench.py --only ${2:-cfg2} --steps ${4:-200} > $out/$v$r.log 2>&1 || exit 1
     python -c "import json; d=json.loads(open('$out/$v$r.log').read().strip().splitlines()[-1]); print('$v', $r, d['value'], d['ms_per_step'])"
   done
 done

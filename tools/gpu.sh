@@ -1,0 +1,84 @@
+# One driver for the GPU box (replaces the per-lease scripts of earlier rounds).
+#
+#   bash tools/gpu.sh TAG STEP [STEP ...]
+#
+# Output under gpurun_out/TAG/.  Steps run in order, each under its own time limit; the first failing
+# step ends the call (no retries on the GPU).  Steps:
+#   tests[:EXPR]   pytest -m gpu (EXPR: a -k expression, ',' for ' or ')
+#   smoke          __graft_entry__.smoke()
+#   bench[:ARGS]   python bench.py ARGS (',' for ' ') -> bench.json
+#   trace[:ARGS]   rocprofv3 --kernel-trace --stats over bench.py ARGS (default: --no-cpu --no-e2e --no-live --steps 10)
+#   pmc            FETCH_SIZE and WRITE_SIZE passes (separate runs) -> pmc_traffic_cfg5.json (stamped)
+#   pmcinst        two SQ counter passes (VALU / LDS / waits) over one cfg5 step -> pmc_inst/
+#   py:SCRIPT[:ARGS]  python SCRIPT ARGS
+set -o pipefail
+tag=${1:?tag}
+shift
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+out=gpurun_out/$tag
+mkdir -p "$out"
+python - > "$out/host.txt" 2>&1 <<'PY'
+import os
+print("cpu_count", os.cpu_count(), "affinity", len(os.sched_getaffinity(0)))
+try:
+    print("cpu.max", open("/sys/fs/cgroup/cpu.max").read().strip())
+except OSError:
+    pass
+PY
+PMC_BENCH="bench.py --steps 1 --warmup 0 --no-cpu --no-e2e --no-decode --no-legs --no-live"
+die() { echo "$1 failed (rc $2)"; tail -40 "$3"; exit 1; }
+for step in "$@"; do
+    name=${step%%:*}
+    arg=""
+    [ "$name" != "$step" ] && arg=${step#*:}
+    echo "== $step"
+    case $name in
+    tests)
+        k=()
+        [ -n "$arg" ] && k=(-k "${arg//,/ or }")
+        timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${k[@]}" \
+            > "$out/tests.log" 2>&1 || die tests $? "$out/tests.log"
+        tail -1 "$out/tests.log" ;;
+    smoke)
+        timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1 \
+            || die smoke $? "$out/smoke.log"
+        tail -1 "$out/smoke.log" ;;
+    bench)
+        timeout -k 10 900 python bench.py ${arg//,/ } > "$out/bench.json" 2> "$out/bench.err" \
+            || die bench $? "$out/bench.err"
+        python tools/bench_summary.py "$out/bench.json" ;;
+    trace)
+        a=${arg//,/ }
+        [ -z "$a" ] && a="--no-cpu --no-e2e --no-live --steps 10"
+        timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run \
+            -- python3 bench.py $a > "$out/trace.log" 2>&1 || die trace $? "$out/trace.log"
+        echo "trace ok" ;;
+    pmc)
+        for c in FETCH_SIZE WRITE_SIZE; do
+            timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d "$out/pmc/$c" -o run -- python3 $PMC_BENCH \
+                > "$out/pmc_$c.log" 2>&1 || die "pmc $c" $? "$out/pmc_$c.log"
+        done
+        python tools/pmc_traffic.py "$out/pmc" "$out/pmc_traffic_cfg5.json" 4 > "$out/pmc_traffic.log" 2>&1 \
+            || die pmc_traffic $? "$out/pmc_traffic.log"
+        tail -3 "$out/pmc_traffic.log" ;;
+    pmcinst)
+        i=0
+        for c in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
+                 "SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_SCA"; do
+            i=$((i + 1))
+            timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d "$out/pmc_inst/p$i" -o run -- python3 $PMC_BENCH \
+                > "$out/pmc_inst_p$i.log" 2>&1 || die "pmcinst p$i" $? "$out/pmc_inst_p$i.log"
+        done
+        echo "pmcinst ok" ;;
+    py)
+        script=${arg%%:*}
+        sargs=""
+        [ "$script" != "$arg" ] && sargs=${arg#*:}
+        timeout -k 10 900 python "$script" ${sargs//,/ } > "$out/$(basename "$script" .py).log" 2>&1 \
+            || die "py $script" $? "$out/$(basename "$script" .py).log"
+        tail -5 "$out/$(basename "$script" .py).log" ;;
+    *)
+        echo "unknown step $step"; exit 2 ;;
+    esac
+done
+echo "all steps ok"

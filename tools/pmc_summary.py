@@ -1,5 +1,5 @@
 """Per-kernel PMC counters of one cfg5 encode step (average over the diagnostic steps), from the
-rocprofv3 passes of tools/pmc_kernels.sh.  usage: python tools/pmc_summary.py PMC_DIR OUT_CSV"""
+rocprofv3 passes of tools/gpu.sh pmcinst (PMC_DIR/p1, p2).  usage: python tools/pmc_summary.py PMC_DIR OUT_CSV"""
 import collections
 import csv
 import os

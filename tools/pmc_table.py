@@ -1,5 +1,5 @@
 """Per-kernel PMC table (mean per dispatch of the largest grid, i.e. the cfg5 step launches) from
-the rocprofv3 passes of tools/pmc_kernels.sh.  usage: pmc_table.py PMC_DIR OUT_CSV"""
+the rocprofv3 passes of tools/gpu.sh pmcinst (PMC_DIR/p1, p2).  usage: pmc_table.py PMC_DIR OUT_CSV"""
 import collections
 import csv
 import glob

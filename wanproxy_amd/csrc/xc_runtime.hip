@@ -376,6 +376,9 @@ struct xc_cache {
     int64_t host_count = -1;
     uint32_t gen = 0;  // bumped when the cache grows (its arrays move): plans refresh their copies
     const void *busy = nullptr;  // the plan whose submitted run is in flight on this cache
+    // the plan whose run was the last thing to change the cache (nothing else wrote segments or
+    // tables since): its next run may hash its first sub-batch ahead (xc_plan_set_input_ready)
+    const void *last_plan = nullptr;
     // the reference's recent window and duplicate enters (null: a COSS tier's mirror, whose Store
     // has its own), its copy at the snapshot, the run whose lookup hits it has not replayed yet
     // (one encode or decode plan: consumed before the next operation that needs the order, dropped
@@ -557,7 +560,10 @@ extern "C" void xc__cache_untracked(xc_cache *c)
 // The replay engine drives the cache (xc_memcache.cpp): the hooks stand aside.
 extern "C" void xc__cache_engine(xc_cache *c, int on)
 {
-    if (c) c->engine = on;
+    if (c) {
+        c->engine = on;
+        c->last_plan = nullptr;
+    }
 }
 
 extern "C" int xc_cache_destroy(xc_cache *c)
@@ -752,6 +758,7 @@ static int cache_rebuild(xc_cache *c, uint64_t ncap, uint32_t keep, bool drop_de
     c->cap = ncap;
     c->host_count = kept;
     c->gen++;
+    c->last_plan = nullptr;
     return XC_OK;
 }
 
@@ -792,6 +799,7 @@ extern "C" int xc__cache_truncate(xc_cache *c, uint64_t keep)
 extern "C" int xc__cache_kill(xc_cache *c, const uint64_t *h, uint64_t n)
 {
     if (!n) return XC_OK;
+    c->last_plan = nullptr;
     int rc = set_dev(c->ctx);
     if (!rc) rc = cache_busy(c);
     if (rc) return rc;
@@ -811,6 +819,7 @@ extern "C" int xc__cache_kill(xc_cache *c, const uint64_t *h, uint64_t n)
 extern "C" int xc__cache_enter_bulk(xc_cache *c, const uint64_t *h, const uint8_t *segs, uint64_t n)
 {
     if (!n) return XC_OK;
+    c->last_plan = nullptr;
     int rc = set_dev(c->ctx);
     if (!rc) rc = cache_busy(c);
     if (rc) return rc;
@@ -1085,6 +1094,7 @@ extern "C" int xc__cache_find(xc_cache *c, const uint64_t *h, uint64_t n, uint64
 // The table value of a present hash, set (a restore puts back what a mirror replaced).
 extern "C" int xc__cache_set_value(xc_cache *c, uint64_t h, uint64_t val)
 {
+    c->last_plan = nullptr;
     int rc = set_dev(c->ctx);
     if (rc) return rc;
     hipLaunchKernelGGL(k_setval, dim3(1), dim3(64), 0, c->ctx->stream, c->set.d, h, val);
@@ -1109,6 +1119,7 @@ extern "C" int xc_cache_enter(xc_cache *c, uint64_t h, const uint8_t *seg)
     hipStream_t s = c->ctx->stream;
     if ((rc = cache_reserve(c, 1))) return rc;
     c->host_count = -1;
+    c->last_plan = nullptr;  // (an enter of a present hash rewrites its segment's bytes)
     HIPCHK(hipMemcpyAsync(c->ctx->d_seg, seg, XC_SEG, hipMemcpyHostToDevice, s));
     // only the word k_enter_one reports: CTL_ANCLESS is the device's record of an anchorless
     // segment an anchor run entered, which the host may not have learned yet
@@ -1261,6 +1272,13 @@ struct xc_plan {
     std::string parked_msg;
     hipEvent_t ev_ctl = nullptr;
     std::vector<hipEvent_t> ev_hash, ev_go;
+    // xc_plan_set_input_ready: the input is complete when a run is submitted, so the run's first
+    // sub-batch is hashed on the side stream at once, beside the previous run's last kernels
+    // (early_ok: the previous run of this plan went through the asynchronous pass unchanged;
+    // ev_sb0: after its first sub-batch's last kernel that reads the block arrays)
+    bool input_ready = false, early_ok = false;
+    hipEvent_t ev_sb0 = nullptr;
+    uint64_t early_runs = 0;
     uint32_t next_hash = 0;  // first sub-batch not yet enqueued for hashing in this run
     // end-to-end host path (xc_encode_run_host): per-sub-batch H2D on a copy stream, packing
     // kernels after every emitted sub-batch
@@ -1593,6 +1611,7 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     p->ev_go.assign(p->sub.size(), nullptr);
     for (auto &e : p->ev_hash) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (auto &e : p->ev_go) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&p->ev_sb0, hipEventDisableTiming));
     HIPCHK(hipMemcpyAsync(p->d_blk_base, blk_base.data(), (nbuf + 1) * 4, hipMemcpyHostToDevice, s));
     P.blk_base = p->d_blk_base;
     HIPCHK(dmalloc(&P.buf_next, nb1 * 4));
@@ -1746,6 +1765,7 @@ extern "C" int xc__cache_hit_stats(xc_cache *c, uint64_t *runs, uint64_t *hits, 
 extern "C" int xc__cache_run_start(xc_cache *c, int *slow)
 {
     *slow = 0;
+    c->last_plan = nullptr;  // (a decode run writes segments and tables)
     int rc = cache_settle(c);
     if (!rc && c->mem && !c->engine) *slow = xc__mem_live(c->mem);
     return rc;
@@ -1841,6 +1861,8 @@ extern "C" int xc_plan_destroy(xc_plan *p)
         if (e) hipEventDestroy(e);
     for (auto e : p->ev_go)
         if (e) hipEventDestroy(e);
+    if (p->ev_sb0) hipEventDestroy(p->ev_sb0);
+    if (p->cache->last_plan == p) p->cache->last_plan = nullptr;
     delete p;
     return XC_OK;
 }
@@ -2225,7 +2247,8 @@ static bool bh_gated()
 // stream) has passed; ev_hash[k] marks completion.
 // On the main stream (st == nullptr: the run's first sub-batch, nothing to overlap with) no
 // events are needed.
-static int enqueue_block_hash(xc_plan *p, uint32_t k, hipEvent_t after, hipStream_t st, bool predict = false)
+static int enqueue_block_hash(xc_plan *p, uint32_t k, hipEvent_t after, hipStream_t st, bool predict = false,
+                              const uint32_t *limit = nullptr)
 {
     const bool side = st == p->hs;
     if (after) HIPCHK(hipStreamWaitEvent(st, after, 0));
@@ -2236,7 +2259,7 @@ static int enqueue_block_hash(xc_plan *p, uint32_t k, hipEvent_t after, hipStrea
     static const int bh_nt = getenv("XC_BH_NT") ? atoi(getenv("XC_BH_NT")) : 0;
     // (chained hashing may run while the main stream is several sub-batches behind: its compares
     // take the entries complete at the run's start; gated, those complete when k - 1 started)
-    DeclArgs d{p->P, g0, g1, side && k > 0 ? p->P.sb_count + (bh_gated() ? k - 1 : 0) : nullptr, bh_nt};
+    DeclArgs d{p->P, g0, g1, limit ? limit : side && k > 0 ? p->P.sb_count + (bh_gated() ? k - 1 : 0) : nullptr, bh_nt};
     // XC_ABL_SKIP_BLOCKHASH=1 (timing experiments only, valid when every run reads the same input):
     // the side stream's block hashing after the plan's first run is skipped
     static const bool skip = getenv("XC_ABL_SKIP_BLOCKHASH") && atoi(getenv("XC_ABL_SKIP_BLOCKHASH"));
@@ -2333,6 +2356,7 @@ static int encode_sub_async(xc_plan *p, uint32_t sb)
     }
     if ((rc = launch_first_round(p, sb, j0, s1, p->shadow))) return rc;
     if ((rc = launch_emit(p, sb, j0, s1, sb))) return rc;
+    if (sb == 0) HIPCHK(hipEventRecord(p->ev_sb0, p->cache->ctx->stream));
     return launch_pack(p, j0, s1);
 }
 
@@ -2521,6 +2545,19 @@ static int encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64
         p->P.fmix_fold = f;
     }
     if ((rc = plan_anchor_setup(p))) return rc;
+    // the first sub-batch's blocks hashed ahead on the side stream (their compares take the entries
+    // complete when the previous run's last sub-batch started: immutable since, nothing else having
+    // written the cache; a restore in between only unmaps later entries, which the predictions then
+    // do not name)
+    const bool early = p->input_ready && p->early_ok && c->last_plan == p && p->sub.size() > 2 &&
+                       !p->P.stream_st && !p->host_path && !use_graph(p) && !p->timing;
+    if (c->last_plan != p) c->last_plan = nullptr;
+    p->early_ok = false;
+    if (early) {
+        if ((rc = enqueue_block_hash(p, 0, p->ev_sb0, p->hs, false, p->P.sb_count + (p->sub.size() - 2)))) return rc;
+        p->early_runs++;
+        p->stats.early_hashed = 1;
+    }
     p->cache->host_count = -1;
     if (p->sub.size() > 1) p->zero_ctl = true;  // (the first k_clear_set clears the control words)
     else HIPCHK(hipMemsetAsync(p->P.ctl, 0, CTL_WORDS * 4, s));
@@ -2646,6 +2683,8 @@ static int encode_finish(xc_plan *p)
     }
     // (the first pass enqueued it behind itself unless a sub-batch was redone since)
     if (!(p->tail_enqueued && !redone) && (rc = launch_tailcheck(p))) return rc;
+    p->early_ok = !redone && p->sub.size() > 2;
+    c->last_plan = p;
     if (c->mem && !c->engine) {
         if (ctl[CTL_DUPS]) {
             // a carried candidate entered a hash the cache held: undone, the host replays the run
@@ -2704,6 +2743,14 @@ static int encode_wait(xc_plan *p)
         return fail(XC_EDEVICE, std::string("run: ") + hipGetErrorString(e));
     }
     return encode_finish(p);
+}
+
+extern "C" int xc_plan_set_input_ready(xc_plan *p, int ready)
+{
+    if (!p) return fail(XC_EINVAL, "null");
+    if (p->inflight) return fail(XC_EBUSY, "a run of this plan is in flight");
+    p->input_ready = ready != 0;
+    return XC_OK;
 }
 
 extern "C" int xc_plan_set_completion(xc_plan *p, int mode)

@@ -40,6 +40,7 @@ SYMBOLS = [
     "xc_coss_enter", "xc_coss_encode_batch_host", "xc_coss_decode_batch_host", "xc_coss_store_lookup",
     "xc_coss_store_enter", "xc_coss_encode_streams", "xc_encode_submit", "xc_encode_poll", "xc_encode_wait",
     "xc_plan_set_completion", "xc_dplan_set_completion", "xc_plan_set_scan", "xc_cache_quiesce",
+    "xc_plan_set_input_ready",
 ]
 STREAM_FLUSH = 1  # XC_STREAM_FLUSH
 
@@ -61,7 +62,7 @@ class RunStats(C.Structure):
                 ("walk_rounds", C.c_uint32), ("outer_rounds", C.c_uint32),
                 ("dense_chunks", C.c_uint32), ("redone", C.c_uint32),
                 ("shadow_misses", C.c_uint32), ("anchor_scans", C.c_uint32),
-                ("anchor_fallbacks", C.c_uint32)]
+                ("anchor_fallbacks", C.c_uint32), ("early_hashed", C.c_uint32), ("reserved", C.c_uint32)]
 
 
 class DecodeStats(C.Structure):
@@ -119,6 +120,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.xc_encode_poll.argtypes = [_vp, C.POINTER(C.c_int)]
     lib.xc_encode_wait.argtypes = [_vp]
     lib.xc_cache_quiesce.argtypes = [_vp]
+    lib.xc_plan_set_input_ready.argtypes = [_vp, C.c_int]
     lib.xc_plan_set_completion.argtypes = [_vp, C.c_int]
     lib.xc_plan_set_scan.argtypes = [_vp, C.c_int]
     lib.xc_plan_stats.argtypes = [_vp, C.POINTER(RunStats)]
@@ -609,6 +611,12 @@ class EncodePlan:
         its last device writes complete in the order of the context stream (synchronize with
         ``Context.sync()`` or the device before reading the outputs from another stream)."""
         _check(load_library().xc_plan_set_completion(self.h, 1 if stream_ordered else 0))
+
+    def set_input_ready(self, ready: bool) -> None:
+        """xc_plan_set_input_ready: the input arena is complete whenever a run is submitted (not
+        written by pending work on any stream), so the first sub-batch is hashed at once beside the
+        previous run's last kernels."""
+        _check(load_library().xc_plan_set_input_ready(self.h, 1 if ready else 0))
 
     def set_scan(self, mode: str) -> None:
         """xc_plan_set_scan: "auto" (default), "exact" or "anchor" (DESIGN.md §4.5)."""
