@@ -506,6 +506,15 @@ __global__ __launch_bounds__(256) void k_aprop(AScanArgs a)
             const uint32_t b = gr[k].x, gpos = gr[k].y * XC_SEG;
             const uint32_t len = P.buf_len[b], ck0 = P.buf_chunk0[b], cblk = P.blk_base[b];
             const uint32_t ap = gpos + (((uint32_t)r[k] >> 5) & 0x3FFFu), nr = ((uint32_t)r[k] & 31u) + 1u;
+            // a record inside predicted REF block kb whose block before is one too (or kb = 0)
+            // proposes nothing to look up: its ends q in [a, a + 1984] are aligned (kb's window), in
+            // kb - 1's shadow (q below kb's end), in kb's (above it), or not a window (q < 2047)
+            if (a.shadow) {
+                const uint32_t kb = ap >> 11;
+                if (cblk + kb < P.blk_base[b + 1] && blk_cached(P.blk_pref[cblk + kb]) &&
+                    (kb == 0u || blk_cached(P.blk_pref[cblk + kb - 1u])))
+                    continue;
+            }
 #pragma unroll
             for (int tb = 0; tb < 2; tb++) {
                 const AncSet &S = tb ? P.danc : P.canc;
@@ -1268,7 +1277,7 @@ constexpr uint32_t ANC_LIST = 512;  // anchor list entries per pass (a multiple 
 __device__ __forceinline__ uint64_t group_anchors(const PlanDev &P, uint32_t g, uint32_t k0, uint32_t len,
                                                   uint32_t n, uint32_t na, const uint8_t *base,
                                                   const uint32_t (&w)[BLK_GROUP][8], uint32_t *tile,
-                                                  uint16_t *list)
+                                                  uint16_t *list, uint32_t abl)
 {
     const uint32_t l = lane_id();
     uint32_t *prev = tile + 32u * 64u;
@@ -1309,7 +1318,12 @@ __device__ __forceinline__ uint64_t group_anchors(const PlanDev &P, uint32_t g, 
             wave_sync();
         }
         if (l == 0) P.rec_blk[g * BLK_GROUP + i] = min(cnt, REC_CAP);
-        uint32_t m = gear_mask<true>(wi, gi, tile);
+        // (timing ablations, XC_ABL_BH: 8 = no G tile, 4 = no anchor list / records)
+        uint32_t m = (abl & 8u) ? gear_mask<false>(wi, gi, nullptr) : gear_mask<true>(wi, gi, tile);
+        if (abl & 12u) {
+            if (l == i) bkey = m;  // (keeps the mask live)
+            continue;
+        }
         // buffer positions p0 + t: anchors need p >= 63 (the context in the buffer) and p < len
         const uint32_t p0 = (k0 + i) * XC_SEG + 32u * l;
         if (p0 < 63u) m &= p0 + 31u >= 63u ? ~0u >> (63u - p0) : 0u;  // bit 31 - t: t >= 63 - p0
@@ -1393,13 +1407,15 @@ __global__ __launch_bounds__(256, 4) void k_blockhash(DeclArgs a)
     const uint32_t n = nfull > k0 ? min(BLK_GROUP, nfull - k0) : 0u;
     const uint32_t na = ANC ? min(BLK_GROUP, (len + XC_SEG - 1u) / XC_SEG - k0) : n;
     uint32_t w[BLK_GROUP][8];  // (kept for the compares below)
-    if (ANC && a.nt) wave_load_blocks<BLK_GROUP, true>(base + (size_t)k0 * XC_SEG, na, w);
+    if (ANC && (a.nt & 1)) wave_load_blocks<BLK_GROUP, true>(base + (size_t)k0 * XC_SEG, na, w);
     else wave_load_blocks<BLK_GROUP>(base + (size_t)k0 * XC_SEG, na, w);
     const uint64_t h = block_group_hash<BLK_GROUP>(w);
     uint64_t akey = ANC_NONE;
-    if (ANC)
+    // XC_ABL_BH (timing ablations only: the results are wrong): 2 = no anchors at all
+    const uint32_t abl = (uint32_t)a.nt & ~1u;
+    if (ANC && !(abl & 2u))
         akey = group_anchors(P, g, k0, len, n, na, base, w, tiles[(threadIdx.x >> 6) & (ANC ? 3 : 0)],
-                             lists[(threadIdx.x >> 6) & (ANC ? 3 : 0)]);
+                             lists[(threadIdx.x >> 6) & (ANC ? 3 : 0)], abl);
     const uint32_t l = lane_id();
     const uint32_t gi = P.blk_base[b] + k0 + l;
     uint32_t cmp = 0;  // the cached slot + 1 to compare the block with (blk_cmp)

@@ -2259,7 +2259,12 @@ static int enqueue_block_hash(xc_plan *p, uint32_t k, hipEvent_t after, hipStrea
     static const int bh_nt = getenv("XC_BH_NT") ? atoi(getenv("XC_BH_NT")) : 0;
     // (chained hashing may run while the main stream is several sub-batches behind: its compares
     // take the entries complete at the run's start; gated, those complete when k - 1 started)
-    DeclArgs d{p->P, g0, g1, limit ? limit : side && k > 0 ? p->P.sb_count + (bh_gated() ? k - 1 : 0) : nullptr, bh_nt};
+    // XC_ABL_BH=m (timing ablations of the block hashing, read per launch: bench.py --diag-env sets
+    // it for the diagnostic steps only; the results are wrong): 2 no anchors, 4 no records, 8 no G tile
+    const char *abl_bh = getenv("XC_ABL_BH");
+    const int nt_abl = bh_nt | (abl_bh ? atoi(abl_bh) & ~1 : 0);
+    DeclArgs d{p->P, g0, g1, limit ? limit : side && k > 0 ? p->P.sb_count + (bh_gated() ? k - 1 : 0) : nullptr,
+               nt_abl};
     // XC_ABL_SKIP_BLOCKHASH=1 (timing experiments only, valid when every run reads the same input):
     // the side stream's block hashing after the plan's first run is skipped
     static const bool skip = getenv("XC_ABL_SKIP_BLOCKHASH") && atoi(getenv("XC_ABL_SKIP_BLOCKHASH"));
