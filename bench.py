@@ -178,6 +178,7 @@ def bench_decode(args, ctx, warm):
     dc.snapshot()
     plan = w.DecodePlan(dc, lens, np.full(n, W.BUF, np.uint64))
     plan.set_completion(True)  # (stream ordered: every read below follows a device synchronize)
+    plan.set_input_ready(True)  # (the encoded streams are written once, before the first step)
     arena = np.zeros(plan.in_bytes, np.uint8)
     for i, x in enumerate(streams):
         arena[int(plan.in_off[i]):int(plan.in_off[i]) + len(x)] = np.frombuffer(x, np.uint8)

@@ -279,6 +279,10 @@ int xc_dplan_stats(xc_dplan *p, xc_decode_stats *st);
  * output copies and cache inserts complete in the order of the plan's stream (the context
  * stream); a batch whose outputs may not fit their capacities returns after the whole run. */
 int xc_dplan_set_completion(xc_dplan *p, int mode);
+/* As xc_plan_set_input_ready for decode runs: the input arena is complete when xc_decode_run is
+ * called and unchanged until the run is finished; the run's input is then parsed (tokens, EXTRACT
+ * hashes) on a side stream at once, beside the device work of the plan's previous run. */
+int xc_dplan_set_input_ready(xc_dplan *p, int ready);
 
 /* ---- persistent COSS cache: XCodecCacheCOSS (xcodec/cache/coss/xcodec_cache_coss.{h,cc}) ----
  *

@@ -118,13 +118,14 @@ def test_gpu_encode_gpu_decode_roundtrip(gpu_ctx):
     assert len(ec) == len(dc)
 
 
-@pytest.mark.parametrize("stream_ordered", [False, True])
-def test_device_resident_decode_plan(gpu_ctx, oracle_mod, stream_ordered):
-    """xc_decode_plan_create + xc_decode_run on HBM arenas, run twice over a restored cache
-    snapshot (the bench's step): same results as the oracle both times.  Stream ordered
+@pytest.mark.parametrize("stream_ordered,input_ready", [(False, False), (True, False), (True, True)])
+def test_device_resident_decode_plan(gpu_ctx, oracle_mod, stream_ordered, input_ready):
+    """xc_decode_plan_create + xc_decode_run on HBM arenas, run three times over a restored cache
+    snapshot (the bench's step): same results as the oracle every time.  Stream ordered
     (xc_dplan_set_completion): the runs return once decided, back to back with no host
-    synchronisation; a plan whose capacities are too small still fails (k_dstop's bound stops the
-    early return)."""
+    synchronisation; input ready (xc_dplan_set_input_ready): each run's parse on the side stream
+    beside the previous run's emit, the token arrays alternating; a plan whose capacities are too
+    small still fails (k_dstop's bound stops the early return)."""
     import torch
     import wanproxy_amd as w
     pool = W.pool(256)
@@ -151,10 +152,11 @@ def test_device_resident_decode_plan(gpu_ctx, oracle_mod, stream_ordered):
     d_in = torch.from_numpy(arena).cuda()
     sets = [(torch.zeros(plan.out_bytes, dtype=torch.uint8, device="cuda"),
              torch.zeros(3 * n, dtype=torch.int64, device="cuda"),
-             torch.zeros(2 * n, dtype=torch.int32, device="cuda")) for _ in range(2)]
+             torch.zeros(2 * n, dtype=torch.int32, device="cuda")) for _ in range(3)]
     plan.set_completion(stream_ordered)
+    plan.set_input_ready(input_ready)
     torch.cuda.synchronize()
-    for rep in range(2):
+    for rep in range(3):
         d_out, u64, i32 = sets[rep]
         if stream_ordered:
             gc.restore_async()
@@ -167,7 +169,7 @@ def test_device_resident_decode_plan(gpu_ctx, oracle_mod, stream_ordered):
             torch.cuda.synchronize()
     gpu_ctx.sync()
     torch.cuda.synchronize()
-    for rep in range(2):
+    for rep in range(3):
         d_out, u64, i32 = sets[rep]
         out = d_out.cpu().numpy()
         r64 = u64.cpu().numpy().astype(np.uint64)

@@ -222,7 +222,10 @@ __device__ __forceinline__ void ring_read32(const uint32_t *ring, uint32_t x, ui
 // latest windows as the tokenizer passes it (no second read of the payloads), and 64 at a time the
 // cache probes, collisions and batch-table inserts run lane-parallel (the batch table was cleared by
 // k_dclear before this kernel: its inserts must not race with a clear).
-template <bool HASH>
+// PROBE = false (with HASH): the parse alone, input-only work (tokens and every EXTRACT's hash): it
+// runs on a side stream as soon as a run is submitted with its input ready, beside the previous
+// run's emit; k_dprobe then does round 0's probes and inserts on the context stream.
+template <bool HASH, bool PROBE>
 __global__ __launch_bounds__(64) void k_dtok(DecDev D, int fill, int first, uint32_t n_lo, uint32_t n_full)
 {
     __shared__ uint32_t win[(HASH ? 2u : 1u) * DTOK_WIN / 4 + 8];
@@ -254,6 +257,11 @@ __global__ __launch_bounds__(64) void k_dtok(DecDev D, int fill, int first, uint
     uint32_t pend_x = NONE, pend_t = 0;  // an EXTRACT whose payload ends in the next window
     auto flush = [&]() {
         const bool ex = l < xn;
+        if (!PROBE) {
+            if (ex && fill) D.t_h[tb + xt] = xh;
+            xn = 0;
+            return;
+        }
         uint64_t v = 0;
         uint32_t st = 0;
         const bool hit = ex && set_find(D.cache, xh, &v);
@@ -363,8 +371,46 @@ __global__ __launch_bounds__(64) void k_dtok(DecDev D, int fill, int first, uint
     if (HASH && xn) flush();
     if (l == 0) D.tok_cnt[j] = nt;
 }
-template __global__ void k_dtok<false>(DecDev, int, int, uint32_t, uint32_t);
-template __global__ void k_dtok<true>(DecDev, int, int, uint32_t, uint32_t);
+template __global__ void k_dtok<false, true>(DecDev, int, int, uint32_t, uint32_t);
+template __global__ void k_dtok<true, true>(DecDev, int, int, uint32_t, uint32_t);
+template __global__ void k_dtok<true, false>(DecDev, int, int, uint32_t, uint32_t);
+
+// Round 0 after an early parse (k_dtok<true, false>): one wave per stream, its EXTRACT tokens 64 at a
+// time, one lane per token: the cache probe (a hit's payload compared wave-wide: rare), else the
+// batch table's insert (xcodec_decoder.cc:101-132); with the run's prologue (control words,
+// provider limits), as k_dtok's first launch does.
+__global__ __launch_bounds__(64) void k_dprobe(DecDev D)
+{
+    const uint32_t j = blockIdx.x, l = lane_id();
+    if (j == 0 && threadIdx.x < DCTL_WORDS) D.ctl[threadIdx.x] = 0u;
+    if (j >= D.ns) return;
+    if (l == 0) D.s_lim[j] = 0xFFFFFFFFu;
+    const uint8_t *s = D.in + D.in_off[j];
+    const uint32_t tb = D.tok_base[j], n = D.tok_cnt[j];
+    for (uint32_t t0 = 0; t0 < n; t0 += 64u) {
+        const uint32_t t = t0 + l;
+        const bool ex = t < n && D.t_op[tb + t] == T_EXTRACT;
+        if (!ballot(ex)) continue;
+        const uint64_t h = ex ? D.t_h[tb + t] : 0ull;
+        uint64_t v = 0;
+        uint32_t st = 0;
+        const bool hit = ex && set_find(D.cache, h, &v);
+        if (ex && !hit) {
+            st = R_PENDING;
+            set_insert(D.dset, h, ((uint64_t)j << 32) | t, true, nullptr, nullptr);  // (round 0: no limit)
+        }
+        for (uint64_t mh = ballot(hit); mh; mh &= mh - 1) {
+            const int fh = __ffsll((unsigned long long)mh) - 1;
+            const uint32_t le = D.t_le[tb + readlane(t, fh)];
+            const bool eq = wave_equal2048(s + le + 2u, seg_at(D.segs, dreadlane64(v, fh)));
+            if ((int)l == fh) st = eq ? R_OKCACHE : R_COLL;
+        }
+        if (ex) {
+            D.t_stat[tb + t] = st;
+            D.t_src[tb + t] = st == R_OKCACHE ? v : 0;
+        }
+    }
+}
 
 // The round-2 tokenizer (kept for A/B): F1 search in 1 KiB register windows loaded on demand.
 __global__ __launch_bounds__(64) void k_dtok_win(DecDev D, int fill, int first, uint32_t n_lo, uint32_t n_full)
@@ -1019,6 +1065,19 @@ struct xc_dplan {
     uint32_t cache_gen = 0;       // the cache arrays D holds (they move when the cache grows)
     std::vector<uint32_t> tok_base;  // host copy [ns + 1]
     bool internal = false;        // run by xc_decode_batch_host (its replay takes a XC__SLOW run)
+    // xc_dplan_set_input_ready: runs parse their input on the side stream ps as soon as they are
+    // submitted, beside the previous run's emit; the tokenizer's arrays alternate between two sets
+    // (tset[k]: tok_cnt, t_lb, t_le, t_op, t_h) so that the parse never writes what a run before it
+    // still reads; ev_free[k] follows the last kernel that read set k
+    bool input_ready = false;
+    struct TokSet {
+        uint32_t *tok_cnt = nullptr, *t_lb = nullptr, *t_le = nullptr, *t_op = nullptr;
+        uint64_t *t_h = nullptr;
+    } tset[2];
+    int tcur = 0;
+    hipStream_t ps = nullptr;
+    hipEvent_t ev_parsed = nullptr, ev_free[2] = {nullptr, nullptr};
+    uint64_t early_runs = 0;
     template <class T>
     int alloc(T **p, size_t n)
     {
@@ -1032,6 +1091,13 @@ extern "C" int xc_dplan_set_completion(xc_dplan *p, int mode)
 {
     if (!p || (mode != XC_COMPLETE_RUN && mode != XC_COMPLETE_STREAM)) return xc__set_error(XC_EINVAL, "completion mode");
     p->completion = mode;
+    return XC_OK;
+}
+
+extern "C" int xc_dplan_set_input_ready(xc_dplan *p, int ready)
+{
+    if (!p) return xc__set_error(XC_EINVAL, "null");
+    p->input_ready = ready != 0;
     return XC_OK;
 }
 
@@ -1052,9 +1118,14 @@ extern "C" int xc_dplan_destroy(xc_dplan *p)
     hipSetDevice(p->dev);
     if (p->cache) xc__cache_plan_gone_dec(p->cache, p);  // (its tokens are the window's record)
     hipStreamSynchronize(p->s);
+    if (p->ps) hipStreamSynchronize(p->ps);
     for (void *x : p->owned) xc__pfree(x);
     if (p->h_ctl) xc__pfree(p->h_ctl);
     if (p->ev_ctl) hipEventDestroy(p->ev_ctl);
+    if (p->ev_parsed) hipEventDestroy(p->ev_parsed);
+    for (auto e : p->ev_free)
+        if (e) hipEventDestroy(e);
+    if (p->ps) hipStreamDestroy(p->ps);
     delete p;
     return XC_OK;
 }
@@ -1125,6 +1196,7 @@ extern "C" int xc_decode_plan_create(xc_cache *c, const uint64_t *in_len, const 
         DHIP(hipMemcpyAsync(d_tbase, tbase.data(), ns * 4, hipMemcpyHostToDevice, s));
     }
     DHIP(hipStreamSynchronize(s));
+    p->tset[0] = {D.tok_cnt, D.t_lb, D.t_le, D.t_op, D.t_h};
     D.in_off = d_ioff;
     D.in_len = d_ilen;
     D.tok_base = d_tbase;
@@ -1172,6 +1244,40 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
             return xc__set_error(XC_EINVAL, "device-resident decode on a cache with a hash entered twice by a "
                                             "stateful stream: run it through xc_decode_batch_host");
     }
+    // the parse of this run's input on the side stream at once (input ready), into the token set the
+    // run before this one did not use (its last reader, two runs back, is long done)
+    static const bool old_tok = getenv("XC_DTOK_WIN") && atoi(getenv("XC_DTOK_WIN"));
+    // XC_DTOK_NOHASH=1 (experiments): round 0's hashes and probes in k_dres1<true>, as before
+    static const bool tok_hash = !old_tok && !(getenv("XC_DTOK_NOHASH") && atoi(getenv("XC_DTOK_NOHASH")));
+    const bool early = p->input_ready && tok_hash && !p->internal;
+    if (early) {
+        if (!p->ps) {  // (the second token set, the side stream and its events, once)
+            xc_dplan::TokSet &t1 = p->tset[1];
+            const size_t nt = std::max<uint64_t>(p->ntok, 1);
+            int ra = XC_OK;
+            if ((ra = p->alloc(&t1.tok_cnt, std::max<uint32_t>(ns, 1))) || (ra = p->alloc(&t1.t_lb, nt)) ||
+                (ra = p->alloc(&t1.t_le, nt)) || (ra = p->alloc(&t1.t_op, nt)) || (ra = p->alloc(&t1.t_h, nt)))
+                return ra;  // (what was allocated goes with the plan)
+            DHIP(hipEventCreateWithFlags(&p->ev_parsed, hipEventDisableTiming));
+            for (auto &e : p->ev_free) DHIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            DHIP(hipStreamCreateWithFlags(&p->ps, hipStreamNonBlocking));
+        }
+        p->tcur ^= 1;
+        const xc_dplan::TokSet &t = p->tset[p->tcur];
+        p->D.tok_cnt = t.tok_cnt;
+        p->D.t_lb = t.t_lb;
+        p->D.t_le = t.t_le;
+        p->D.t_op = t.t_op;
+        p->D.t_h = t.t_h;
+        DecDev Dp = p->D;
+        Dp.in = d_in;
+        DHIP(hipStreamWaitEvent(p->ps, p->ev_free[p->tcur], 0));
+        auto parse = k_dtok<true, false>;
+        hipLaunchKernelGGL(parse, dim3(ns), dim3(64), 0, p->ps, Dp, 1, 0, p->n_lo, p->n_full);
+        DHIP(hipGetLastError());
+        DHIP(hipEventRecord(p->ev_parsed, p->ps));
+        p->early_runs++;
+    }
     DecDev D = p->D;
     D.in = d_in;
     D.out = d_out;
@@ -1204,16 +1310,18 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
     const int64_t count0 = xc__cache_host_count(p->cache);
     xc__cache_count_unknown(p->cache);
     // tokens, with the prologue (control words, provider limits, round 0's provider table)
-    // XC_DTOK_WIN=1 (experiments): the round-2 tokenizer
-    static const bool old_tok = getenv("XC_DTOK_WIN") && atoi(getenv("XC_DTOK_WIN"));
-    // XC_DTOK_NOHASH=1 (experiments): round 0's hashes and probes in k_dres1<true>, as before
-    static const bool tok_hash = !old_tok && !(getenv("XC_DTOK_NOHASH") && atoi(getenv("XC_DTOK_NOHASH")));
+    // (XC_DTOK_WIN=1, experiments: the round-2 tokenizer)
     if (tok_hash) {  // (the batch table cleared before the tokenizer inserts into it)
         hipLaunchKernelGGL(k_dclear, dim3(512), dim3(256), 0, s, D, p->n_lo, p->n_full);
         DHIP(hipGetLastError());
     }
-    hipLaunchKernelGGL(old_tok ? k_dtok_win : tok_hash ? k_dtok<true> : k_dtok<false>,
-                       dim3(std::max<uint32_t>(ns, 256u)), dim3(64), 0, s, D, 1, 1, p->n_lo, p->n_full);
+    if (early) {  // round 0 behind the side stream's parse
+        DHIP(hipStreamWaitEvent(s, p->ev_parsed, 0));
+        hipLaunchKernelGGL(k_dprobe, dim3(ns), dim3(64), 0, s, D);
+    } else {
+        auto tok = old_tok ? k_dtok_win : tok_hash ? k_dtok<true, true> : k_dtok<false, true>;
+        hipLaunchKernelGGL(tok, dim3(std::max<uint32_t>(ns, 256u)), dim3(64), 0, s, D, 1, 1, p->n_lo, p->n_full);
+    }
     DHIP(hipGetLastError());
     // one provider-resolution round (a fresh batch table each time; round 0's came with k_dtok)
     auto resolve_round = [&](int r) -> int {
@@ -1258,6 +1366,7 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
         DHIP(hipGetLastError());
         hipLaunchKernelGGL(k_dcommit, dim3((ns + DCOMMIT_WAVES - 1) / DCOMMIT_WAVES), dim3(64 * DCOMMIT_WAVES), 0, s, D);
         DHIP(hipGetLastError());
+        if (p->ps) DHIP(hipEventRecord(p->ev_free[p->tcur], s));  // (the set's last reader)
         if (pub) {
             for (int i = 0;; i++) {
                 if (*(volatile const uint32_t *)(p->h_ctl + DCTL_WORDS - 1) == 0u) {

@@ -40,7 +40,7 @@ SYMBOLS = [
     "xc_coss_enter", "xc_coss_encode_batch_host", "xc_coss_decode_batch_host", "xc_coss_store_lookup",
     "xc_coss_store_enter", "xc_coss_encode_streams", "xc_encode_submit", "xc_encode_poll", "xc_encode_wait",
     "xc_plan_set_completion", "xc_dplan_set_completion", "xc_plan_set_scan", "xc_cache_quiesce",
-    "xc_plan_set_input_ready",
+    "xc_plan_set_input_ready", "xc_dplan_set_input_ready",
 ]
 STREAM_FLUSH = 1  # XC_STREAM_FLUSH
 
@@ -121,6 +121,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.xc_encode_wait.argtypes = [_vp]
     lib.xc_cache_quiesce.argtypes = [_vp]
     lib.xc_plan_set_input_ready.argtypes = [_vp, C.c_int]
+    lib.xc_dplan_set_input_ready.argtypes = [_vp, C.c_int]
     lib.xc_plan_set_completion.argtypes = [_vp, C.c_int]
     lib.xc_plan_set_scan.argtypes = [_vp, C.c_int]
     lib.xc_plan_stats.argtypes = [_vp, C.POINTER(RunStats)]
@@ -708,6 +709,11 @@ class DecodePlan:
     def set_completion(self, stream_ordered: bool) -> None:
         """xc_dplan_set_completion (see EncodePlan.set_completion)."""
         _check(load_library().xc_dplan_set_completion(self.h, 1 if stream_ordered else 0))
+
+    def set_input_ready(self, ready: bool) -> None:
+        """xc_dplan_set_input_ready (see EncodePlan.set_input_ready): the input is parsed on a side
+        stream as soon as a run is submitted."""
+        _check(load_library().xc_dplan_set_input_ready(self.h, 1 if ready else 0))
 
     def stats(self) -> DecodeStats:
         st = DecodeStats()
