@@ -1560,7 +1560,20 @@ __device__ __forceinline__ bool gate_stop(const EmitArgs &a)
 __device__ __forceinline__ void gate_abort(const EmitArgs &a)
 {
     a.P.ctl[CTL_ABORT_SB] = a.gate_sb;
+    __threadfence();  // (an emit on its own stream reads the sub-batch after seeing the flag)
     a.P.ctl[CTL_ABORT] = 1u;
+}
+
+// The emit's stop: a pass stopped at this sub-batch or before it.  (An emit on its own stream may
+// run after a later sub-batch's gate stopped the pass: its own sub-batch passed its gate, and its
+// bytes are due.)
+__device__ __forceinline__ bool emit_aborted(const EmitArgs &a)
+{
+    if (!aborted(a.P)) return false;
+    if (a.gate_sb == NONE) return true;
+    const uint32_t sb = __builtin_amdgcn_readfirstlane(
+        (int)__atomic_load_n((const uint32_t *)&a.P.ctl[CTL_ABORT_SB], __ATOMIC_ACQUIRE));
+    return sb <= a.gate_sb;
 }
 
 // The control words to the caller's mapped host buffer (one thread).
@@ -1648,7 +1661,7 @@ __global__ __launch_bounds__(256) void k_insert(EmitArgs a)
 template <uint32_t EMIT_WAVES, bool SLOTS>
 __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
 {
-    if (aborted(a.P)) return;
+    if (emit_aborted(a)) return;
     __shared__ uint32_t sz[MAX_TOK];
     __shared__ uint32_t ord[MAX_TOK];
     __shared__ uint4 red[EMIT_WAVES];

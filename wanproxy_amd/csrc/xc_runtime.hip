@@ -1278,6 +1278,14 @@ struct xc_plan {
     // ev_sb0: after its first sub-batch's last kernel that reads the block arrays)
     bool input_ready = false, early_ok = false;
     hipEvent_t ev_sb0 = nullptr;
+    // The emit of a large sub-batch (its wire bytes and segment-store copies) runs on its own stream
+    // es, beside the next sub-batch's predictions and anchor scan; the main stream joins it before
+    // the next resolve (the first reader of the new segments' bytes) and at the pass's end.
+    // ev_ins: after the sub-batch's cache inserts; ev_emit: after its emit; emit_open: an emit
+    // the main stream has not joined yet.
+    hipStream_t es = nullptr;
+    hipEvent_t ev_ins = nullptr, ev_emit = nullptr;
+    bool emit_open = false;
     uint64_t early_runs = 0;
     uint32_t next_hash = 0;  // first sub-batch not yet enqueued for hashing in this run
     // end-to-end host path (xc_encode_run_host): per-sub-batch H2D on a copy stream, packing
@@ -1792,6 +1800,7 @@ extern "C" int xc_plan_destroy(xc_plan *p)
     hipStreamSynchronize(p->cache->ctx->stream);
     if (p->hs) hipStreamSynchronize(p->hs);
     if (p->cs) hipStreamSynchronize(p->cs);
+    if (p->es) hipStreamSynchronize(p->es);
     p->S.release();
     p->D.release();
     p->dset.release(false);
@@ -1862,6 +1871,12 @@ extern "C" int xc_plan_destroy(xc_plan *p)
     for (auto e : p->ev_go)
         if (e) hipEventDestroy(e);
     if (p->ev_sb0) hipEventDestroy(p->ev_sb0);
+    if (p->es) {
+        hipStreamSynchronize(p->es);
+        hipStreamDestroy(p->es);
+    }
+    if (p->ev_ins) hipEventDestroy(p->ev_ins);
+    if (p->ev_emit) hipEventDestroy(p->ev_emit);
     if (p->cache->last_plan == p) p->cache->last_plan = nullptr;
     delete p;
     return XC_OK;
@@ -2229,8 +2244,38 @@ static int launch_emit(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t jc, uint32
     const bool wide = (uint64_t)(jc - j0) * EMIT_WAVES < (uint64_t)p->cache->ctx->n_cu * 16u;
     auto kern = wide ? (slots ? k_emit<16, true> : k_emit<16, false>)
                      : (slots ? k_emit<EMIT_WAVES, true> : k_emit<EMIT_WAVES, false>);
-    hipLaunchKernelGGL(kern, dim3(jc - j0), dim3(64 * (wide ? 16 : EMIT_WAVES)), 0, s, e);
+    // the asynchronous pass's large sub-batches: on the emit stream, after the cache inserts
+    // (XC_EMIT_MAIN=1: in the main stream's order, as in round 3)
+    static const bool emit_main = getenv("XC_EMIT_MAIN") && atoi(getenv("XC_EMIT_MAIN"));
+    // (timing runs keep it in order: the per-kernel spans are of serialized launches)
+    // (a run of one sub-batch has no next sub-batch to overlap: and its pass may be captured as a graph)
+    const bool own = !slots && gate_sb != NONE && !p->host_path && !emit_main && !p->timing && p->sub.size() > 2;
+    hipStream_t es = s;
+    if (own) {
+        if (!p->es) {
+            HIPCHK(hipStreamCreateWithFlags(&p->es, hipStreamNonBlocking));
+            HIPCHK(hipEventCreateWithFlags(&p->ev_ins, hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&p->ev_emit, hipEventDisableTiming));
+        }
+        HIPCHK(hipEventRecord(p->ev_ins, s));
+        HIPCHK(hipStreamWaitEvent(p->es, p->ev_ins, 0));
+        es = p->es;
+    }
+    hipLaunchKernelGGL(kern, dim3(jc - j0), dim3(64 * (wide ? 16 : EMIT_WAVES)), 0, es, e);
     HIPCHK(hipGetLastError());
+    if (own) {
+        HIPCHK(hipEventRecord(p->ev_emit, es));
+        p->emit_open = true;
+    }
+    return XC_OK;
+}
+
+// The main stream waits for the emit on the emit stream (its segments' bytes, its wire bytes).
+static int join_emit(xc_plan *p)
+{
+    if (!p->emit_open) return XC_OK;
+    HIPCHK(hipStreamWaitEvent(p->cache->ctx->stream, p->ev_emit, 0));
+    p->emit_open = false;
     return XC_OK;
 }
 
@@ -2331,6 +2376,8 @@ static int launch_first_round(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t s1,
     } else if ((rc = launch_scan(p, p->P.S, p->P.cache, ck_lo, ck_hi, &p->P.dset, shadow))) {
         return rc;
     }
+    // (the previous sub-batch's emit wrote the segments this resolve may compare)
+    if ((rc = join_emit(p))) return rc;
     if ((rc = launch_resolve(p, p->P.S, 2, ck_lo, ck_hi))) return rc;
     return launch_walk_round(p, j0, s1, 0, shadow);
 }
@@ -2587,6 +2634,7 @@ static int encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64
             p->emit_pub_final = 0;
             if (rc) return rc;
         }
+        if ((rc = join_emit(p))) return rc;  // (the pass's results complete in the context stream's order)
         if (!pub) HIPCHK(hipMemcpyAsync(p->h_ctl, p->P.ctl, CTL_WORDS * 4, hipMemcpyDeviceToHost, s));
         if ((rc = record_ctl(p))) return rc;
         // the tail check right behind the pass (after its event: the host's wait does not cover it),
@@ -2655,6 +2703,7 @@ static int encode_finish(xc_plan *p)
         // the rest asynchronously again: k_alloc's gate stops at the next sub-batch needing the host
         for (size_t k = si; k < nsub; k++)
             if ((rc = encode_sub_async(p, (uint32_t)k))) return rc;
+        if ((rc = join_emit(p))) return rc;
         if ((rc = read_ctl(p, ctl))) return rc;
         fresh = true;
     }
