@@ -2601,8 +2601,10 @@ static int encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64
     // complete when the previous run's last sub-batch started: immutable since, nothing else having
     // written the cache; a restore in between only unmaps later entries, which the predictions then
     // do not name)
+    // (XC_NO_EARLY=1: A/B experiments)
+    static const bool no_early = getenv("XC_NO_EARLY") && atoi(getenv("XC_NO_EARLY"));
     const bool early = p->input_ready && p->early_ok && c->last_plan == p && p->sub.size() > 2 &&
-                       !p->P.stream_st && !p->host_path && !use_graph(p) && !p->timing;
+                       !p->P.stream_st && !p->host_path && !use_graph(p) && !p->timing && !no_early;
     if (c->last_plan != p) c->last_plan = nullptr;
     p->early_ok = false;
     if (early) {
