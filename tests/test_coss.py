@@ -82,12 +82,14 @@ def _apply(cache, ops, segs, hs, store_only):
     return got
 
 
-@pytest.mark.parametrize("size_mb", [3, 6])
-def test_store_equals_oracle(oracle_mod, tmp_path, size_mb):
+@pytest.mark.parametrize("size_mb,nseg,nops", [(3, 9000, 16000), (6, 9000, 16000), (24, 30000, 60000)])
+def test_store_equals_oracle(oracle_mod, tmp_path, size_mb, nseg, nops):
+    """(24 MB: 23 stripes for 16 slots, so lookups load stripes into slots whose data stays in the
+    file until something needs it, and stripes are purged and re-entered)"""
     import wanproxy_amd as w
-    segs = _segs(9000, 7 << 32)
+    segs = _segs(nseg, 7 << 32)
     hs = [oracle_mod.hash_segment(s) for s in segs]
-    ops = _random_ops(np.random.default_rng(size_mb), 16000, segs, hs)
+    ops = _random_ops(np.random.default_rng(size_mb), nops, segs, hs)
     da, db = tmp_path / "o", tmp_path / "p"
     da.mkdir()
     db.mkdir()

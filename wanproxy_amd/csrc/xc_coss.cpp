@@ -100,7 +100,9 @@ public:
         limit_ = (size_mb * 1048576ull + sizeof(Stripe) - 1) / sizeof(Stripe);
         slot_.reset(new (std::nothrow) Stripe[LOADED]());  // COSSStripe(): zeroed headers
         if (!slot_) return XC_ENOMEM;
+        for (auto &r : resident_) r = true;  // (zeroed memory is the slots' content)
         dir_.assign(limit_, Meta{});
+        fstamp_.assign(limit_, 0);
         owner_.assign(limit_ * STRIPE_SEGS, 0);
         file_hash_.assign(limit_ * STRIPE_SEGS, 0);
         fd_ = ::open(path.c_str(), O_RDWR);
@@ -134,6 +136,7 @@ public:
         const uint32_t i = a.h.m.segment_index;
         a.h.hash[i] = h;
         std::memcpy(a.seg[i], seg, SEG);
+        wstamp_[active_][i] = ++stamp_;
         const uint64_t range = a.h.m.stripe_range;
         a.h.m.segment_index++;
         while (a.h.m.segment_index < STRIPE_SEGS && a.h.hash[a.h.m.segment_index]) a.h.m.segment_index++;
@@ -162,7 +165,7 @@ public:
         if (s >= LOADED) {
             s = best_unloadable_slot();
             detach_stripe(s, t);
-            load_stripe(e.range, s, t);
+            load_stripe(e.range, s, t, false);  // (its header: the data stays in the file until needed)
         }
         Stripe &st = slot_[s];
         if (st.h.hash[e.pos] != h) return nullptr;
@@ -187,12 +190,16 @@ public:
     // stripe is loaded from the file first, *l: where the bytes are), ABSENT, or LOAD_MISS (not
     // found, after loading a stripe: a miss with side effects).
     enum { ABSENT = replay::ABSENT, FOUND = replay::FOUND, IN_FILE = replay::IN_FILE, LOAD_MISS = replay::LOAD_MISS };
-    int peek(uint64_t h, const uint8_t **p, Loc *l) const
+    // id (the replay's settle): where the bytes are and their version there -- slot s, position pos
+    // and the stamp of the last load of s or write at (s, pos); or stripe r, position pos of the file
+    // and the stamp of r's last full store -- equal ids have equal bytes.
+    int peek(uint64_t h, const uint8_t **p, Loc *l, uint64_t *id) const
     {
         for (int i = 0; i < WINDOW; i++)
             if (win_[i].hash == h) {
                 if (win_[i].data) {
                     *p = win_[i].data;
+                    slot_id(win_[i].data, id);
                     return FOUND;
                 }
                 break;
@@ -204,11 +211,43 @@ public:
         if (s < LOADED) {
             if (slot_[s].h.hash[e.pos] != h) return ABSENT;
             *p = slot_[s].seg[e.pos];
+            slot_id(*p, id);
             return FOUND;
         }
         *l = e;
         if (e.range * sizeof(Stripe) >= file_size_) return LOAD_MISS;
-        return file_hash_[e.range * STRIPE_SEGS + e.pos] == h ? IN_FILE : LOAD_MISS;
+        if (file_hash_[e.range * STRIPE_SEGS + e.pos] != h) return LOAD_MISS;
+        id[0] = (1ull << 62) | (e.range << 9) | e.pos;
+        id[1] = fstamp_[e.range];
+        return IN_FILE;
+    }
+
+    // The 2048 bytes at p, a pointer into a slot's data (a lookup's result, a window entry): from
+    // memory, or, for a slot whose data was not read in (lazy loads), from the file at the slot's
+    // stripe (the file's bytes there are the slot's: they change only by a full store of that
+    // stripe, which reads every such slot in first).
+    bool copy_bytes(const uint8_t *p, uint8_t *out) const
+    {
+        const uint8_t *b0 = slot_[0].seg[0];
+        const size_t off = (size_t)(p - (const uint8_t *)&slot_[0]);
+        const int s = (int)(off / sizeof(Stripe));
+        if (p < b0 || s >= LOADED || resident_[s]) {
+            std::memcpy(out, p, SEG);
+            return true;
+        }
+        const uint32_t pos = (uint32_t)((p - slot_[s].seg[0]) / SEG);
+        const off_t at = (off_t)(slot_[s].h.m.stripe_range * sizeof(Stripe) + HEADER + (uint64_t)pos * SEG);
+        return ::pread(fd_, out, SEG, at) == (ssize_t)SEG;
+    }
+
+    void slot_id(const uint8_t *p, uint64_t *id) const
+    {
+        const size_t off = (size_t)(p - (const uint8_t *)&slot_[0]);
+        const uint32_t s = (uint32_t)(off / sizeof(Stripe));
+        if (p < slot_[0].seg[0] || s >= (uint32_t)LOADED) return;
+        const uint32_t pos = (uint32_t)((p - slot_[s].seg[0]) / SEG);
+        id[0] = 1u + ((uint64_t)s << 9 | pos);
+        id[1] = std::max(load_stamp_[s], wstamp_[s][pos]);
     }
 
     bool read_segment(const Loc &l, uint8_t *out) const
@@ -352,25 +391,48 @@ private:
         dir_[range] = m;
     }
 
-    bool load_stripe(uint64_t range, int s, Touch *t)
+    // full = false: the header only (a stripe loaded for a lookup: its data is never written back,
+    // and what reads it, copy_bytes, reads the file instead; materialize reads it in when the slot's
+    // memory must hold it)
+    bool load_stripe(uint64_t range, int s, Touch *t, bool full = true)
     {  // :241-260
         const uint64_t pos = range * sizeof(Stripe);
         if (pos < file_size_) {
             retarget(s, range, t);
-            if (::pread(fd_, &slot_[s], sizeof(Stripe), (off_t)pos) == (ssize_t)sizeof(Stripe)) {
+            const size_t n = full ? sizeof(Stripe) : sizeof(Header);
+            load_stamp_[s] = ++stamp_;  // (the slot's bytes are another stripe's now)
+            if (::pread(fd_, &slot_[s], n, (off_t)pos) == (ssize_t)n) {
+                resident_[s] = full;
                 slot_[s].h.m.stripe_range = range;
                 slot_[s].h.m.load_uses = 0;
                 slot_[s].h.m.state = 1;
                 dir_[range].state = 1;
                 return true;
             }
+            resident_[s] = false;  // (a short read: the memory's data is undefined, as in the reference)
         }
         return false;
+    }
+
+    // Slot s's data into its memory (the file's bytes of its stripe, as a full load would have read).
+    void materialize(int s)
+    {
+        if (resident_[s]) return;
+        const uint64_t pos = slot_[s].h.m.stripe_range * sizeof(Stripe) + HEADER;
+        if (::pread(fd_, slot_[s].seg, sizeof(Stripe::seg), (off_t)pos) != (ssize_t)sizeof(Stripe::seg))
+            std::memset(slot_[s].seg, 0, sizeof(Stripe::seg));  // (past the file's end: never loaded)
+        resident_[s] = true;
     }
 
     void store_stripe(int s, size_t size, Touch *t)
     {  // :262-272
         const uint64_t range = slot_[s].h.m.stripe_range, pos = range * sizeof(Stripe);
+        if (size > sizeof(Header)) {
+            materialize(s);
+            for (int i = 0; i < LOADED; i++)  // (their data is the file's: read it before it changes)
+                if (i != s && !resident_[i] && slot_[i].h.m.stripe_range == range) materialize(i);
+        }
+        if (size > sizeof(Header) && range < limit_) fstamp_[range] = ++stamp_;
         if (::pwrite(fd_, &slot_[s], size, (off_t)pos) == (ssize_t)size) {
             if (pos + sizeof(Stripe) > file_size_) file_size_ = pos + sizeof(Stripe);
             if (range < limit_) std::memcpy(&file_hash_[range * STRIPE_SEGS], slot_[s].h.hash, sizeof slot_[s].h.hash);
@@ -382,6 +444,7 @@ private:
     {  // :274-283
         store_stripe(active_, sizeof(Stripe), t);
         active_ = best_unloadable_slot();
+        materialize(active_);  // (the active slot's memory is written back whole: it holds its data)
         detach_stripe(active_, t);
         range_ = best_erasable_stripe();
         if (load_stripe(range_, active_, t)) purge_stripe(active_, t);
@@ -459,6 +522,11 @@ private:
     int fd_ = -1;
     uint64_t file_size_ = 0, serial_ = 0, range_ = 0, limit_ = 0, freshness_ = 0;
     std::unique_ptr<Stripe[]> slot_;
+    bool resident_[LOADED] = {};  // the slot's data is in its memory (else: in the file at its stripe)
+    // versions of the bytes (peek's ids): a counter, the slots' last loads, their positions' last
+    // enters, the stripes' last full stores to the file
+    uint64_t stamp_ = 0, load_stamp_[LOADED] = {}, wstamp_[LOADED][STRIPE_SEGS] = {};
+    std::vector<uint64_t> fstamp_;
     int active_ = 0;
     std::vector<Meta> dir_;
     std::unordered_map<uint64_t, Loc> index_;
@@ -495,6 +563,7 @@ struct xc_coss {
     void entered(uint64_t h, const uint8_t *seg)
     {
         if (pre.count(h)) return;
+        seen.erase(h);
         if (inpass.insert(h).second) {
             known[h] = replay::fingerprint(seg);
             return;
@@ -505,6 +574,19 @@ struct xc_coss {
     }
     int before_mirror(const replay::Change &) { return XC_OK; }
     void mirrored(const replay::Change &) {}
+    // where the mirror's bytes of a hash were last seen in the store (peek's id): unchanged there,
+    // the mirror still holds them (xc_replay.h settle)
+    std::unordered_map<uint64_t, std::pair<uint64_t, uint64_t>> seen;
+    bool same_bytes(uint64_t h, const uint64_t *id) const
+    {
+        auto it = seen.find(h);
+        return it != seen.end() && it->second.first == id[0] && it->second.second == id[1] && known.count(h);
+    }
+    void note_bytes(uint64_t h, const uint64_t *id)
+    {
+        if (id && id[0]) seen[h] = {id[0], id[1]};
+        else seen.erase(h);
+    }
     int begin_pass(const std::vector<uint64_t> &hs, uint64_t count0)
     {
         pre.clear();
@@ -623,7 +705,7 @@ extern "C" int xc_coss_lookup(xc_coss *c, uint64_t h, uint8_t *out, int *found)
         Touch t;
         const uint8_t *d = c->st.lookup(h, &t);
         *found = d ? 1 : 0;
-        if (d) std::memcpy(out, d, SEG);
+        if (d && !c->st.copy_bytes(d, out)) return xc__set_error(XC_EDEVICE, "COSS: cannot read the cache file");
         return follow(c, t);
     } catch (const std::bad_alloc &) {
         return xc__set_error(XC_ENOMEM, "host allocation failed");
@@ -740,7 +822,7 @@ extern "C" int xc_coss_store_lookup(xc_coss *c, uint64_t h, uint8_t *out, int *f
     if (!c || !out || !found) return xc__set_error(XC_EINVAL, "null");
     const uint8_t *d = c->st.lookup(h, nullptr);
     *found = d ? 1 : 0;
-    if (d) std::memcpy(out, d, SEG);
+    if (d && !c->st.copy_bytes(d, out)) return xc__set_error(XC_EDEVICE, "COSS: cannot read the cache file");
     return XC_OK;
 }
 extern "C" int xc_coss_store_enter(xc_coss *c, uint64_t h, const uint8_t *seg)

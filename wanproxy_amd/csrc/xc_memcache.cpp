@@ -157,7 +157,7 @@ public:
         if (t) t->hs.push_back(h);
     }
 
-    int peek(uint64_t h, const uint8_t **p, replay::Loc *) const
+    int peek(uint64_t h, const uint8_t **p, replay::Loc *, uint64_t *) const
     {
         const int s = find_recent(h);
         if (s >= 0) {
@@ -169,6 +169,11 @@ public:
         return replay::FOUND;
     }
     bool read_segment(const replay::Loc &, uint8_t *) const { return false; }
+    bool copy_bytes(const uint8_t *p, uint8_t *out) const
+    {
+        std::memcpy(out, p, SEG);
+        return true;
+    }
     void owners(uint64_t, std::vector<uint64_t> &) const {}
     void window_in_slot(int, std::vector<uint64_t> &) const {}
     void count_misses(uint64_t) {}
@@ -335,6 +340,9 @@ struct Ctx {
     }
     void mirrored(const replay::Change &ch) { m->mirrored(ch); }
     int unmirrorable() { return m->unmirrorable(); }
+    // (the memory cache's bytes have no place to version: every settle fingerprints)
+    bool same_bytes(uint64_t, const uint64_t *) const { return false; }
+    void note_bytes(uint64_t, const uint64_t *) {}
     int begin_pass(const std::vector<uint64_t> &hs, uint64_t count0) { return m->begin_pass(hs, count0); }
     int end_pass() { return m->end_pass(); }
 };

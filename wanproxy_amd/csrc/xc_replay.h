@@ -105,18 +105,27 @@ int settle(C *c, const Touch &t, Change &ch)
         if (!h) continue;
         const uint8_t *p = nullptr;
         Loc l{0, 0};
-        const int r = c->st.peek(h, &p, &l);
+        uint64_t id[2] = {0, 0};  // where the bytes are, and their version there (0: unknown)
+        const int r = c->st.peek(h, &p, &l, id);
         if (r == LOAD_MISS) ch.new_lm |= c->load_miss.insert(h).second;
         else c->load_miss.erase(h);
+        // the same bytes as when the mirror last took this hash's (no read, no fingerprint): the
+        // common case after a stripe load, whose 1024 hashes are all looked at
+        if ((r == FOUND || r == IN_FILE) && id[0] && c->same_bytes(h, id)) continue;
         if (r == IN_FILE) {
             if (!c->st.read_segment(l, buf)) return xc__set_error(XC_EDEVICE, "COSS: cannot read the cache file");
             p = buf;
+        } else if (r == FOUND) {  // (a slot whose data stayed in the file: its bytes from there)
+            if (!c->st.copy_bytes(p, buf)) return xc__set_error(XC_EDEVICE, "COSS: cannot read the cache file");
+            p = buf;
         }
         if (r != FOUND && r != IN_FILE) {
+            c->note_bytes(h, nullptr);
             if (c->known.erase(h)) ch.removed.push_back(h);
             continue;
         }
         const uint64_t fp = fingerprint(p);
+        c->note_bytes(h, id);
         auto it = c->known.find(h);
         if (it != c->known.end() && it->second == fp) continue;
         c->known[h] = fp;
