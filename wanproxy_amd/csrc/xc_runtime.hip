@@ -2605,6 +2605,11 @@ static int encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64
     static const bool no_early = getenv("XC_NO_EARLY") && atoi(getenv("XC_NO_EARLY"));
     const bool early = p->input_ready && p->early_ok && c->last_plan == p && p->sub.size() > 2 &&
                        !p->P.stream_st && !p->host_path && !use_graph(p) && !p->timing && !no_early;
+    static const bool dbg_early = getenv("XC_DEBUG_EARLY") && atoi(getenv("XC_DEBUG_EARLY"));
+    if (dbg_early)
+        fprintf(stderr, "early=%d input_ready=%d early_ok=%d last=%d nsub=%zu stream=%d host=%d graph=%d timing=%d\n",
+                (int)early, (int)p->input_ready, (int)p->early_ok, (int)(c->last_plan == p), p->sub.size() - 1,
+                (int)(p->P.stream_st != nullptr), (int)p->host_path, (int)use_graph(p), p->timing);
     if (c->last_plan != p) c->last_plan = nullptr;
     p->early_ok = false;
     if (early) {
@@ -2615,7 +2620,7 @@ static int encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64
     p->cache->host_count = -1;
     if (p->sub.size() > 1) p->zero_ctl = true;  // (the first k_clear_set clears the control words)
     else HIPCHK(hipMemsetAsync(p->P.ctl, 0, CTL_WORDS * 4, s));
-    p->next_hash = 0;
+    p->next_hash = early ? 1u : 0u;  // (sub-batch 0 hashed ahead: its predictions wait for ev_hash[0])
     const size_t nsub = p->sub.size() - 1;
     if ((rc = ctl_buffers(p))) return rc;
     if (use_graph(p)) {
@@ -2665,6 +2670,12 @@ static int launch_tailcheck(xc_plan *p)
                        (const uint4 *)p->d_tlist);
     HIPCHK(hipGetLastError());
     return XC_OK;
+}
+
+static bool dbg_finish()
+{
+    static const bool d = getenv("XC_DEBUG_EARLY") && atoi(getenv("XC_DEBUG_EARLY"));
+    return d;
 }
 
 // After the first pass's ev_ctl: its control words, then the sub-batches that need the host
@@ -2740,6 +2751,7 @@ static int encode_finish(xc_plan *p)
     // (the first pass enqueued it behind itself unless a sub-batch was redone since)
     if (!(p->tail_enqueued && !redone) && (rc = launch_tailcheck(p))) return rc;
     p->early_ok = !redone && p->sub.size() > 2;
+    if (dbg_finish()) fprintf(stderr, "finish redone=%d nsub=%zu\n", (int)redone, p->sub.size() - 1);
     c->last_plan = p;
     if (c->mem && !c->engine) {
         if (ctl[CTL_DUPS]) {
