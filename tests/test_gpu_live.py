@@ -177,8 +177,8 @@ def test_first_sub_batch_hashed_ahead(gpu_ctx, oracle_mod, monkeypatch):
             oc.enter(oracle_mod.hash_segment(seg), seg)
         bufs = W.repeat_buffers(96, 0x6300 + k, np_segments=512, pool_bytes=pool)
         monkeypatch.setenv("XC_SCAN", "anchor" if k % 2 else "auto")
-        if k % 2:  # repeats of the previous run's content at shifted offsets
-            bufs[7] = _cat(W.gen(0x6310 + k, 1234), prev[11][:50000])
+        if k % 2:  # repeats of the previous run's content at shifted offsets (the same lengths: one plan)
+            bufs[7] = _cat(W.gen(0x6310 + k, 1234), prev[11][:65536 - 1234])
             bufs[8] = prev[12].copy()
         got, st = r.run(bufs, stats=True)
         _same(got, oc.encode_batch(bufs), f"run {k}")
