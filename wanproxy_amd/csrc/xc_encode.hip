@@ -2193,17 +2193,31 @@ __global__ void k_enter_bulk(PlanDev P, const uint64_t *h, const uint8_t *segs, 
     }
 }
 
-// A run's lookup hits for the recent window (xc_memcache.cpp), one thread per buffer: at
+// A run's lookup hits for the recent window (xc_memcache.cpp), one wave per buffer: at
 // out[tok_base[b] + b * (COLL_CAP + 1)] the count (bit 63: more collisions than were recorded), then
 // the hashes in the reference's order: REF tokens (window end seg + 2047) and the recorded collision
-// lookups, by position.
-__global__ void k_hits(PlanDev P, uint64_t *out)
+// lookups, by position.  Without collision records (the common case) the REF tokens are compacted
+// 64 at a time by ballot; with them, lane 0 merges the two lists.
+__global__ __launch_bounds__(256) void k_hits(PlanDev P, uint64_t *out)
 {
-    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t b = blockIdx.x * 4u + (threadIdx.x >> 6), l = lane_id();
     if (b >= P.nb) return;
     uint64_t *o = out + P.tok_base[b] + (uint64_t)b * (COLL_CAP + 1u);
     const uint32_t tb = P.tok_base[b], n = min(P.tok_cnt[b], P.tok_base[b + 1] - tb), cc = P.coll_cnt[b];
     const uint32_t nc = min(cc, COLL_CAP);
+    if (nc == 0u) {
+        uint32_t k = 0;
+        for (uint32_t t0 = 0; t0 < n; t0 += 64u) {
+            const uint32_t t = t0 + l;
+            const bool ref = t < n && P.tok_op[tb + t] == OP_REF;
+            const uint64_t m = ballot(ref);
+            if (ref) o[1u + k + mbcnt(m)] = P.tok_h[tb + t];
+            k += (uint32_t)__popcll(m);
+        }
+        if (l == 0) o[0] = (uint64_t)k;
+        return;
+    }
+    if (l != 0) return;
     uint32_t k = 0, ci = 0;
     for (uint32_t t = 0; t < n; t++) {
         if (P.tok_op[tb + t] != OP_REF) continue;

@@ -11,6 +11,7 @@
 #include <sched.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <chrono>
 #include <cstring>
@@ -400,6 +401,7 @@ struct xc_cache {
         hipEvent_t ev = nullptr;  // the copy into h is complete
         std::vector<uint32_t> tok_base;
         uint32_t nb = 0;
+        uint64_t serial = 0;  // the plan whose layout dtb / tok_base hold
     } hl[2];
     std::deque<int> hl_fifo;  // slots whose hits are not replayed yet, oldest first
     int hl_next = 0;
@@ -1224,7 +1226,10 @@ struct HostLayer {
     }
 };
 
+static std::atomic<uint64_t> g_plan_serial{0};
+
 struct xc_plan {
+    uint64_t serial = ++g_plan_serial;  // (never reused, unlike the plan's address)
     xc_cache *cache;
     uint32_t nb;
     std::vector<uint64_t> len, in_off, out_off;
@@ -1704,6 +1709,7 @@ static int hits_enqueue(xc_plan *p)
         sl.h = nullptr;
         sl.dtb = nullptr;
         sl.cap = sl.tb_cap = 0;
+        sl.serial = 0;
         const size_t cap = words + words / 4, tbc = (size_t)p->nb + 1 + p->nb / 4;
         if (dmalloc(&sl.d, cap * 8) != hipSuccess || dmalloc(&sl.dtb, tbc * 4) != hipSuccess ||
             hmalloc((void **)&sl.h, cap * 8) != hipSuccess)
@@ -1715,8 +1721,12 @@ static int hits_enqueue(xc_plan *p)
         sl.tb_cap = tbc;
     }
     HIPCHK(hipStreamWaitEvent(m, sl.ev, 0));  // the slot's previous copy has read d
-    HIPCHK(hipMemcpyAsync(sl.dtb, p->d_tok_base, ((size_t)p->nb + 1) * 4, hipMemcpyDeviceToDevice, m));
-    hipLaunchKernelGGL(k_hits, dim3((p->nb + 255) / 256), dim3(256), 0, m, p->P, sl.d);
+    if (sl.serial != p->serial) {  // (the layout of another plan: its tok_base)
+        HIPCHK(hipMemcpyAsync(sl.dtb, p->d_tok_base, ((size_t)p->nb + 1) * 4, hipMemcpyDeviceToDevice, m));
+        sl.tok_base = p->tok_base;
+        sl.serial = p->serial;
+    }
+    hipLaunchKernelGGL(k_hits, dim3((p->nb + 3) / 4), dim3(256), 0, m, p->P, sl.d);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->hl_packed, m));
     HIPCHK(hipStreamWaitEvent(c->hl_stream, c->hl_packed, 0));
@@ -1724,7 +1734,6 @@ static int hits_enqueue(xc_plan *p)
                        (const uint64_t *)sl.d, sl.hd, (const uint32_t *)sl.dtb, p->nb);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(sl.ev, c->hl_stream));
-    sl.tok_base = p->tok_base;
     sl.nb = p->nb;
     c->hl_fifo.push_back(si);
     c->hl_next = si ^ 1;
