@@ -1730,9 +1730,17 @@ static int hits_enqueue(xc_plan *p)
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->hl_packed, m));
     HIPCHK(hipStreamWaitEvent(c->hl_stream, c->hl_packed, 0));
-    hipLaunchKernelGGL(k_hits_out, dim3(std::min<uint32_t>((p->nb + 3) / 4, 64u)), dim3(256), 0, c->hl_stream,
-                       (const uint64_t *)sl.d, sl.hd, (const uint32_t *)sl.dtb, p->nb);
-    HIPCHK(hipGetLastError());
+    // the slot to pinned memory by the copy engine (no compute units: a kernel writing only the
+    // filled words across PCIe took ~250 us of CU slots beside the next run, cfg5)
+    // (XC_HITS_KERNEL=1: that kernel, for A/B)
+    static const bool hk = getenv("XC_HITS_KERNEL") && atoi(getenv("XC_HITS_KERNEL"));
+    if (hk) {
+        hipLaunchKernelGGL(k_hits_out, dim3(std::min<uint32_t>((p->nb + 3) / 4, 64u)), dim3(256), 0, c->hl_stream,
+                           (const uint64_t *)sl.d, sl.hd, (const uint32_t *)sl.dtb, p->nb);
+        HIPCHK(hipGetLastError());
+    } else {
+        HIPCHK(hipMemcpyAsync(sl.h, sl.d, words * 8, hipMemcpyDeviceToHost, c->hl_stream));
+    }
     HIPCHK(hipEventRecord(sl.ev, c->hl_stream));
     sl.nb = p->nb;
     c->hl_fifo.push_back(si);
@@ -2253,9 +2261,10 @@ static int launch_emit(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t jc, uint32
     const bool wide = (uint64_t)(jc - j0) * EMIT_WAVES < (uint64_t)p->cache->ctx->n_cu * 16u;
     auto kern = wide ? (slots ? k_emit<16, true> : k_emit<16, false>)
                      : (slots ? k_emit<EMIT_WAVES, true> : k_emit<EMIT_WAVES, false>);
-    // the asynchronous pass's large sub-batches: on the emit stream, after the cache inserts
-    // (XC_EMIT_MAIN=1: in the main stream's order, as in round 3)
-    static const bool emit_main = getenv("XC_EMIT_MAIN") && atoi(getenv("XC_EMIT_MAIN"));
+    // XC_EMIT_OWN=1 (experiments): the asynchronous pass's large sub-batches on the emit stream,
+    // after the cache inserts, beside the next sub-batch's predictions and anchor scan (cfg5 A/B
+    // -1.3 %: the emit's bandwidth beside the side stream's block hashing; not the default)
+    static const bool emit_main = !(getenv("XC_EMIT_OWN") && atoi(getenv("XC_EMIT_OWN")));
     // (timing runs keep it in order: the per-kernel spans are of serialized launches)
     // (a run of one sub-batch has no next sub-batch to overlap: and its pass may be captured as a graph)
     const bool own = !slots && gate_sb != NONE && !p->host_path && !emit_main && !p->timing && p->sub.size() > 2;
