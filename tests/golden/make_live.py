@@ -1,7 +1,7 @@
 """Generate tests/golden/live_digests.npz: per-buffer digests of the ORACLE encoder's output for
 the steady-state leg of bench.py (a live cache, no restore between batches), run here on the CPU.
 
-Batches k = 0 .. 3 of cfg5's shape (32768 x 64 KiB, 50 % repeats of the 8192-segment pool) with
+Batches k = 0 .. 7 of cfg5's shape (32768 x 64 KiB, 50 % repeats of the 8192-segment pool) with
 seeds 0x5555 + k, encoded one after another against ONE cache warmed with the pool: batch k sees
 every segment batches 0 .. k-1 declared (xcodec/xcodec_encoder.cc:60-201, buffers in index order,
 each a fresh encoder's encode() + flush(); the oracle is oracle/xc_oracle.c).  Batch 0 is cfg5
@@ -23,7 +23,7 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
-BATCHES = 4
+BATCHES = 8
 TOTAL = 32768
 SEED0 = 0x5555
 GROUP = 1024

@@ -47,9 +47,10 @@ public:
         int32_t v;
     } win[WINDOW];
     uint32_t cursor = 0;
-    // non-zero window hashes per bucket (h & 4095): a run's hits are replayed here one by one (half
-    // a million per cfg5 step on the host path), and almost none is in the window
-    uint8_t wcnt[4096] = {};
+    // non-zero window hashes per bucket (bucket(h)): a run's hits are replayed here one by one (half
+    // a million per cfg5 step), and almost none is in the window
+    uint16_t wcnt[16384] = {};
+    static uint32_t bucket(uint64_t h) { return (uint32_t)(h ^ (h >> 29)) & 16383u; }
     // hashes entered again with other bytes: every version (ver[0] the first), cur = the map's
     struct Dup {
         std::vector<std::vector<uint8_t>> ver;
@@ -76,7 +77,7 @@ public:
                 if (win[i].h == 0) return win[i].v >= 0 ? i : -1;
             return -1;
         }
-        if (!wcnt[h & 4095u]) return -1;
+        if (!wcnt[bucket(h)]) return -1;
         for (int i = 0; i < WINDOW; i++)  // (a hash is in the window once at most)
             if (win[i].h == h && win[i].v >= 0) return i;
         return -1;
@@ -103,11 +104,11 @@ public:
     {
         Win &w = win[cursor];
         if (w.v >= 0 && w.h) {
-            wcnt[w.h & 4095u]--;
+            wcnt[bucket(w.h)]--;
             if (t && dups.count(w.h)) t->hs.push_back(w.h);
         }
         w = {h, v};
-        if (h) wcnt[h & 4095u]++;
+        if (h) wcnt[bucket(h)]++;
         cursor = (cursor + 1) & (WINDOW - 1);
     }
 
@@ -134,18 +135,23 @@ public:
             for (uint64_t i = 0; i < n; i++) hit(h[i]);
             return;
         }
+        uint32_t c = cursor;
         for (uint64_t i = 0; i < n; i++) {
             const uint64_t x = h[i];
-            if (x && !wcnt[x & 4095u]) {  // (not in the window: remembered, version 0)
-                Win &w = win[cursor];
-                if (w.v >= 0 && w.h) wcnt[w.h & 4095u]--;
+            const uint32_t bx = bucket(x);
+            if (__builtin_expect(x != 0 && wcnt[bx] == 0, 1)) {  // (not in the window: remembered, version 0)
+                Win &w = win[c];
+                if (w.v >= 0 && w.h) wcnt[bucket(w.h)]--;
                 w = {x, 0};
-                wcnt[x & 4095u]++;
-                cursor = (cursor + 1) & (WINDOW - 1);
-            } else if (find_recent(x) < 0) {
-                remember(x, 0, nullptr);
+                wcnt[bx]++;
+                c = (c + 1) & (WINDOW - 1);
+            } else {
+                cursor = c;
+                if (find_recent(x) < 0) remember(x, 0, nullptr);
+                c = cursor;
             }
         }
+        cursor = c;
     }
 
     // XCodecMemoryCache::enter (:182-188), release semantics

@@ -401,6 +401,7 @@ struct xc_cache {
         hipEvent_t ev = nullptr;  // the copy into h is complete
         std::vector<uint32_t> tok_base;
         uint32_t nb = 0;
+        uint32_t next_b = 0;  // replay progress: the first buffer not replayed yet
         uint64_t serial = 0;  // the plan whose layout dtb / tok_base hold
     } hl[2];
     std::deque<int> hl_fifo;  // slots whose hits are not replayed yet, oldest first
@@ -1643,29 +1644,35 @@ static hipError_t spin_wait(hipEvent_t ev);
 // Replay the oldest slot's hits into the window model (per buffer, in the reference's order: its
 // REF tokens and its recorded collision lookups, by position; bit 63 of the count: more collisions
 // than were recorded).  block = false: only when its copy is complete (*done = 0 otherwise).
-static int hits_replay_front(xc_cache *c, bool block, bool *done)
+// max_b: at most that many buffers of it (a host waiting for the device replays in steps, checking
+// the device between them; progress is kept in the slot).
+static int hits_replay_front(xc_cache *c, bool block, bool *done, uint32_t max_b = 0xFFFFFFFFu)
 {
     xc_cache::HitSlot &sl = c->hl[c->hl_fifo.front()];
     hipError_t e = hipEventQuery(sl.ev);
+    *done = false;
     if (e == hipErrorNotReady) {
-        *done = false;
         if (!block) return XC_OK;
         e = spin_wait(sl.ev);
     }
     if (e != hipSuccess) return fail(XC_EDEVICE, std::string("lookup hits: ") + hipGetErrorString(e));
     const auto t0 = std::chrono::steady_clock::now();
     uint64_t n = 0;
-    for (uint32_t b = 0; b < sl.nb; b++) {
+    const uint32_t end = block ? sl.nb : (uint32_t)std::min<uint64_t>(sl.nb, (uint64_t)sl.next_b + max_b);
+    for (uint32_t b = sl.next_b; b < end; b++) {
         const uint64_t *r = sl.h + sl.tok_base[b] + (uint64_t)b * (COLL_CAP + 1u);
         const uint64_t k = r[0] & 0xFFFFFFFFu;
         xc__mem_hits(c->mem, r + 1, k, (r[0] >> 63) ? 0 : 1);
         n += k;
     }
-    c->hl_fifo.pop_front();
-    c->hl_runs++;
+    sl.next_b = end;
     c->hl_hits += n;
     c->hl_sec += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    *done = true;
+    if (end == sl.nb) {
+        c->hl_fifo.pop_front();
+        c->hl_runs++;
+        *done = true;
+    }
     return XC_OK;
 }
 
@@ -1743,6 +1750,7 @@ static int hits_enqueue(xc_plan *p)
     }
     HIPCHK(hipEventRecord(sl.ev, c->hl_stream));
     sl.nb = p->nb;
+    sl.next_b = 0;
     c->hl_fifo.push_back(si);
     c->hl_next = si ^ 1;
     return XC_OK;
@@ -2107,7 +2115,9 @@ static hipError_t pass_state(xc_plan *p)
 static void replay_while_waiting(xc_plan *p)
 {
     xc_cache *c = p->cache;
-    if (!c->hl_fifo.empty() && c->mem && !c->engine) hits_replay(c, false);  // (an error shows at the settle)
+    if (c->hl_fifo.empty() || !c->mem || c->engine) return;
+    bool done = false;
+    hits_replay_front(c, false, &done, 1024);  // (~0.1 ms of host work; an error shows at the settle)
 }
 
 static hipError_t wait_decided(xc_plan *p)
@@ -2122,7 +2132,7 @@ static hipError_t wait_decided(xc_plan *p)
     }
     for (int i = 0;; i++) {
         if (published(p)) return hipSuccess;
-        if ((i & 255) == 0) replay_while_waiting(p);
+        replay_while_waiting(p);
         if ((i & 255) == 255) {
             const hipError_t e = pass_state(p);
             if (e != hipErrorNotReady) return e;
