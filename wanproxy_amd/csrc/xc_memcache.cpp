@@ -20,8 +20,15 @@
 // engine of xc_replay.h with the Store below: the device cache then mirrors, for every hash, the
 // bytes the reference's lookup returns, following each change the window makes.
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "xc_replay.h"
@@ -41,15 +48,14 @@ constexpr int WINDOW = 64;  // XCODEC_WINDOW_COUNT, xcodec_cache.h:48
 class MemStore {
 public:
     xc_cache *cache = nullptr;
-    // the recent window: hash and the version of the bytes it remembered (-1: never used, no data)
-    struct Win {
-        uint64_t h;
-        int32_t v;
-    } win[WINDOW];
+    // the recent window: hash and the version of the bytes it remembered (-1: never used, no data),
+    // slot by slot (the replay's inner loop reads the hashes alone)
+    uint64_t wh[WINDOW] = {};
+    int32_t wv[WINDOW];
     uint32_t cursor = 0;
-    // non-zero window hashes per bucket (bucket(h)): a run's hits are replayed here one by one (half
-    // a million per cfg5 step), and almost none is in the window
-    uint16_t wcnt[16384] = {};
+    // window slots per bucket(hash), the unused ones (hash 0) included: a run's hits are replayed
+    // here one by one (half a million per cfg5 step), and almost none is in the window
+    uint8_t wcnt[16384] = {};
     static uint32_t bucket(uint64_t h) { return (uint32_t)(h ^ (h >> 29)) & 16383u; }
     // hashes entered again with other bytes: every version (ver[0] the first), cur = the map's
     struct Dup {
@@ -65,7 +71,8 @@ public:
 
     MemStore()
     {
-        for (auto &w : win) w = {0, -1};
+        for (auto &v : wv) v = -1;
+        wcnt[bucket(0)] = WINDOW;
     }
 
     // find_recent: the first slot with the hash (hash 0 matches the unused slots, whose data is
@@ -74,12 +81,12 @@ public:
     {
         if (h == 0) {
             for (int i = 0; i < WINDOW; i++)
-                if (win[i].h == 0) return win[i].v >= 0 ? i : -1;
+                if (wh[i] == 0) return wv[i] >= 0 ? i : -1;
             return -1;
         }
         if (!wcnt[bucket(h)]) return -1;
         for (int i = 0; i < WINDOW; i++)  // (a hash is in the window once at most)
-            if (win[i].h == h && win[i].v >= 0) return i;
+            if (wh[i] == h) return i;
         return -1;
     }
 
@@ -102,13 +109,12 @@ public:
     // lookup of that hash returns
     void remember(uint64_t h, int32_t v, Touch *t)
     {
-        Win &w = win[cursor];
-        if (w.v >= 0 && w.h) {
-            wcnt[bucket(w.h)]--;
-            if (t && dups.count(w.h)) t->hs.push_back(w.h);
-        }
-        w = {h, v};
-        if (h) wcnt[bucket(h)]++;
+        const uint64_t o = wh[cursor];
+        if (t && wv[cursor] >= 0 && o && dups.count(o)) t->hs.push_back(o);
+        wcnt[bucket(o)]--;
+        wh[cursor] = h;
+        wv[cursor] = v;
+        wcnt[bucket(h)]++;
         cursor = (cursor + 1) & (WINDOW - 1);
     }
 
@@ -116,7 +122,7 @@ public:
     const uint8_t *lookup(uint64_t h, Touch *t)
     {
         const int s = find_recent(h);
-        if (s >= 0) return bytes(h, win[s].v);
+        if (s >= 0) return bytes(h, wv[s]);
         if (!is_present(h)) return nullptr;
         const int32_t v = curver(h);
         remember(h, v, t);
@@ -139,16 +145,134 @@ public:
         for (uint64_t i = 0; i < n; i++) {
             const uint64_t x = h[i];
             const uint32_t bx = bucket(x);
-            if (__builtin_expect(x != 0 && wcnt[bx] == 0, 1)) {  // (not in the window: remembered, version 0)
-                Win &w = win[c];
-                if (w.v >= 0 && w.h) wcnt[bucket(w.h)]--;
-                w = {x, 0};
-                wcnt[bx]++;
+            if (__builtin_expect(wcnt[bx] != 0, 0)) {  // (maybe in the window)
+                if (x == 0) {
+                    cursor = c;
+                    hit(x);
+                    c = cursor;
+                    continue;
+                }
+                bool in = false;
+                for (int j = 0; j < WINDOW; j++) in |= wh[j] == x;
+                if (in) continue;
+            }
+            // not in the window: remembered, version 0
+            wcnt[bucket(wh[c])]--;
+            wh[c] = x;
+            wv[c] = 0;
+            wcnt[bx]++;
+            c = (c + 1) & (WINDOW - 1);
+        }
+        cursor = c;
+    }
+
+    // ---- a run's hits on several threads (no hash entered twice) ----
+    // Whatever the window held, after a stretch of hits that inserted 64 hashes it holds those 64,
+    // in that order.  So a chunk of a run's hits is simulated ahead from an empty window (its
+    // insert decisions recorded), and the exact simulation from the true window, run over the chunk
+    // afterwards, stops as soon as the two decided alike on a stretch with 64 insertions: from there
+    // on they are the same simulation, and the chunk's end state is the ahead run's.
+    struct Spec {
+        std::vector<uint64_t> dec;  // bit i: hit i of the chunk inserted
+        uint64_t win[WINDOW];
+        uint32_t cur = 0;
+        uint64_t nins = 0;
+        bool ok = false;  // false: a hash 0 in the chunk (the window's unused slots): no shortcut
+    };
+    // A run's packed hits: buffer b's record at h + tok_base[b] + b * stride (count in the low word
+    // of its first entry, the hashes after it).
+    struct Run {
+        const uint64_t *h;
+        const uint32_t *tok_base;
+        uint32_t stride;
+        const uint64_t *rec(uint32_t b) const { return h + tok_base[b] + (uint64_t)b * stride; }
+    };
+
+    static void spec_sim(const Run &R, uint32_t b0, uint32_t b1, Spec &o)
+    {
+        uint64_t n = 0;
+        for (uint32_t b = b0; b < b1; b++) n += R.rec(b)[0] & 0xFFFFFFFFu;
+        o.dec.assign((n + 63) / 64, 0);
+        o.ok = false;
+        uint64_t w[WINDOW] = {};
+        uint8_t cnt[16384] = {};
+        cnt[bucket(0)] = WINDOW;
+        uint32_t c = 0;
+        uint64_t i = 0, nins = 0;
+        for (uint32_t b = b0; b < b1; b++) {
+            const uint64_t *r = R.rec(b);
+            const uint64_t k = r[0] & 0xFFFFFFFFu;
+            for (uint64_t j = 0; j < k; j++, i++) {
+                const uint64_t x = r[1 + j];
+                if (!x) return;
+                const uint32_t bx = bucket(x);
+                if (__builtin_expect(cnt[bx] != 0, 0)) {
+                    bool in = false;
+                    for (int s = 0; s < WINDOW; s++) in |= w[s] == x;
+                    if (in) continue;
+                }
+                cnt[bucket(w[c])]--;
+                w[c] = x;
+                cnt[bx]++;
                 c = (c + 1) & (WINDOW - 1);
-            } else {
-                cursor = c;
-                if (find_recent(x) < 0) remember(x, 0, nullptr);
-                c = cursor;
+                nins++;
+                o.dec[i >> 6] |= 1ull << (i & 63);
+            }
+        }
+        std::memcpy(o.win, w, sizeof w);
+        o.cur = c;
+        o.nins = nins;
+        o.ok = true;
+    }
+
+    // The exact simulation of chunk [b0, b1) from the window as it is, taking o's end state once
+    // they agree (o: spec_sim of the same chunk).
+    void hits_fixup(const Run &R, uint32_t b0, uint32_t b1, const Spec &o)
+    {
+        if (!o.ok || !dups.empty()) {
+            for (uint32_t b = b0; b < b1; b++) {
+                const uint64_t *r = R.rec(b);
+                hits(r + 1, r[0] & 0xFFFFFFFFu);
+            }
+            return;
+        }
+        uint32_t c = cursor, agree = 0;
+        uint64_t i = 0, sins = 0;
+        for (uint32_t b = b0; b < b1; b++) {
+            const uint64_t *r = R.rec(b);
+            const uint64_t k = r[0] & 0xFFFFFFFFu;
+            for (uint64_t j = 0; j < k; j++, i++) {
+                const uint64_t x = r[1 + j];  // (non-zero: o.ok)
+                const uint32_t bx = bucket(x);
+                bool ins = true;
+                if (wcnt[bx]) {
+                    bool in = false;
+                    for (int s = 0; s < WINDOW; s++) in |= wh[s] == x;
+                    ins = !in;
+                }
+                if (ins) {
+                    wcnt[bucket(wh[c])]--;
+                    wh[c] = x;
+                    wv[c] = 0;
+                    wcnt[bx]++;
+                    c = (c + 1) & (WINDOW - 1);
+                }
+                const bool sd = (o.dec[i >> 6] >> (i & 63)) & 1u;
+                sins += sd;
+                if (ins != sd) {
+                    agree = 0;
+                } else if (ins && ++agree == WINDOW) {
+                    // the same 64 insertions: the windows are equal; the rest of the chunk is o's
+                    const uint32_t cf = (uint32_t)((c + (o.nins - sins)) & (WINDOW - 1));
+                    for (int s = 0; s < WINDOW; s++) wcnt[bucket(wh[s])]--;
+                    for (int s = 0; s < WINDOW; s++) {
+                        wh[(cf + s) & (WINDOW - 1)] = o.win[(o.cur + s) & (WINDOW - 1)];
+                        wv[s] = 0;
+                    }
+                    for (int s = 0; s < WINDOW; s++) wcnt[bucket(wh[s])]++;
+                    cursor = cf;
+                    return;
+                }
             }
         }
         cursor = c;
@@ -189,7 +313,7 @@ public:
     {
         const int s = find_recent(h);
         if (s >= 0) {
-            *p = bytes(h, win[s].v);
+            *p = bytes(h, wv[s]);
             return replay::FOUND;
         }
         if (!is_present(h)) return replay::ABSENT;
@@ -270,9 +394,9 @@ struct xc_memmodel {
             const int s = st.find_recent(h);
             const int32_t cur = (int32_t)it->second.cur;
             const auto k = known.find(h);
-            if ((s < 0 || st.win[s].v == cur) && k != known.end() &&
+            if ((s < 0 || st.wv[s] == cur) && k != known.end() &&
                 k->second == replay::fingerprint(it->second.ver[(size_t)cur].data())) {
-                if (s >= 0) st.win[s].v = 0;
+                if (s >= 0) st.wv[s] = 0;
                 known.erase(k);
                 it = st.dups.erase(it);
             } else {
@@ -338,6 +462,120 @@ extern "C" void xc__mem_hits(xc_memmodel *m, const uint64_t *h, uint64_t n, int 
     if (!m) return;
     m->st.hits(h, n);
     if (!complete) m->valid = false;
+}
+
+namespace {
+// Helper threads for the chunks simulated ahead (XC_REPLAY_THREADS, default 6; 0: none).  Made
+// at the first use and never joined (they wait on the pool's condition between runs).
+class ReplayPool {
+public:
+    static ReplayPool *get()
+    {
+        static ReplayPool *p = [] {
+            const char *e = getenv("XC_REPLAY_THREADS");
+            const int n = e ? std::max(0, std::min(32, atoi(e))) : 6;
+            ReplayPool *q = new (std::nothrow) ReplayPool();
+            if (q && !q->start(n)) q->nthreads = 0;
+            return q;
+        }();
+        return p;
+    }
+    int threads() const { return nthreads; }
+    // run job(j) for j in [0, n) on the helpers; done[j] is set (release) as each finishes
+    void launch(uint32_t n, std::function<void(uint32_t)> job, std::atomic<int> *done)
+    {
+        std::lock_guard<std::mutex> g(mu);
+        fn = std::move(job);
+        flags = done;
+        njobs = n;
+        gen++;
+        next.store(gen << 32);
+        cv.notify_all();
+    }
+
+private:
+    bool start(int n)
+    {
+        try {
+            for (int i = 0; i < n; i++) std::thread([this] { loop(); }).detach();
+        } catch (...) {
+            return false;
+        }
+        nthreads = n;
+        return true;
+    }
+    void loop()
+    {
+        uint64_t seen = 0;
+        for (;;) {
+            std::function<void(uint32_t)> f;
+            std::atomic<int> *d;
+            uint32_t n;
+            {
+                std::unique_lock<std::mutex> g(mu);
+                cv.wait(g, [&] { return gen != seen; });
+                seen = gen;
+                f = fn;
+                d = flags;
+                n = njobs;
+            }
+            // (the job counter carries its generation: a helper that wakes late takes no job of a
+            // later launch with this one's function)
+            for (;;) {
+                uint64_t v = next.load();
+                if ((v >> 32) != seen || (uint32_t)v >= n) break;
+                if (!next.compare_exchange_weak(v, v + 1)) continue;
+                f((uint32_t)v);
+                d[(uint32_t)v].store(1, std::memory_order_release);
+            }
+        }
+    }
+    std::mutex mu;
+    std::condition_variable cv;
+    std::function<void(uint32_t)> fn;
+    std::atomic<int> *flags = nullptr;
+    uint32_t njobs = 0;
+    std::atomic<uint64_t> next{0};  // generation << 32 | the next job
+    uint64_t gen = 0;
+    int nthreads = 0;
+};
+}  // namespace
+
+// A run's packed lookup hits, buffers [0, nb) (record of buffer b at h + tok_base[b] + b * stride,
+// bit 63 of its count: more than were recorded), in order.  With no hash entered twice and enough
+// of them, chunks of buffers are simulated ahead on the helper threads while this thread replays
+// the first exactly, then each next one exactly until it agrees with its ahead run.
+extern "C" void xc__mem_hits_run(xc_memmodel *m, const uint64_t *h, const uint32_t *tok_base, uint32_t stride,
+                                 uint32_t nb)
+{
+    if (!m || !nb) return;
+    const MemStore::Run R{h, tok_base, stride};
+    for (uint32_t b = 0; b < nb; b++)
+        if (R.rec(b)[0] >> 63) m->valid = false;
+    ReplayPool *pool = m->st.dups.empty() && nb >= 1024 ? ReplayPool::get() : nullptr;
+    const uint32_t nt = pool ? (uint32_t)pool->threads() : 0u;
+    if (!nt) {
+        for (uint32_t b = 0; b < nb; b++) {
+            const uint64_t *r = R.rec(b);
+            m->st.hits(r + 1, r[0] & 0xFFFFFFFFu);
+        }
+        return;
+    }
+    const uint32_t nc = nt + 1;  // chunk 0 here, 1 .. nt ahead
+    std::vector<uint32_t> cut(nc + 1);
+    for (uint32_t j = 0; j <= nc; j++) cut[j] = (uint32_t)((uint64_t)nb * j / nc);
+    std::vector<MemStore::Spec> spec(nc);
+    std::unique_ptr<std::atomic<int>[]> done(new std::atomic<int>[nc]);
+    for (uint32_t j = 0; j < nc; j++) done[j].store(0);
+    pool->launch(nt, [&](uint32_t j) { MemStore::spec_sim(R, cut[j + 1], cut[j + 2], spec[j + 1]); }, done.get() + 1);
+    for (uint32_t b = cut[0]; b < cut[1]; b++) {
+        const uint64_t *r = R.rec(b);
+        m->st.hits(r + 1, r[0] & 0xFFFFFFFFu);
+    }
+    for (uint32_t j = 1; j < nc; j++) {
+        while (!done[j].load(std::memory_order_acquire)) std::this_thread::yield();
+        m->st.hits_fixup(R, cut[j], cut[j + 1], spec[j]);
+    }
 }
 
 // Does a run need the replay engine (a duplicated hash that may answer other bytes)?
@@ -508,4 +746,10 @@ extern "C" int xc__mem_enter(xc_memmodel *m, uint64_t h, const uint8_t *seg, int
     } catch (const std::bad_alloc &) {
         return bad_alloc();
     }
+}
+
+// The window's hashes, oldest first (tests).
+extern "C" void xc__mem_window(const xc_memmodel *m, uint64_t *out)
+{
+    for (int s = 0; s < WINDOW; s++) out[s] = m ? m->st.wh[(m->st.cursor + s) & (WINDOW - 1)] : 0;
 }
