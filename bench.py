@@ -59,7 +59,7 @@ def parse():
     ap.add_argument("--only", choices=["cfg2", "cfg3", "cfg4"],
                     help="run just that leg (one GPU) and print its JSON object (kernel traces, A/B)")
     ap.add_argument("--no-live", action="store_true", help="skip the steady-state (live cache) leg")
-    ap.add_argument("--live-batches", type=int, default=4)
+    ap.add_argument("--live-batches", type=int, default=8)
     ap.add_argument("--live-reps", type=int, default=3)
     return ap.parse_args()
 
