@@ -650,7 +650,7 @@ __device__ __forceinline__ uint32_t gear_prev(uint32_t sf, uint32_t first)
 }
 
 // Anchor mask of the lane's 32 positions (bit 31 - t: position t of the lane is an anchor, before
-// any position bound); TILE: G of every position into tile[t * 64 + lane] too.
+// any position bound); TILE: G of every position into tile[t * XC_TILE_ROW + lane] too.
 // Per position, all full-rate VOP2/VOPC but one: g + g, then the byte added straight from its
 // dword (SDWA byte select: no extraction), and m = 2 m + (g < 2^26) as a compare into VCC and an
 // add with carry-in (the compiler's select + or forms are VOP3).  The compare of position t is
@@ -684,6 +684,9 @@ __device__ __forceinline__ uint32_t mask_last(uint32_t m, uint32_t g)
     return m;
 }
 
+// (a row of 64 values and one pad word: the anchor pass gathers G(p) and G(p - 32) of a lane's
+// several anchors, at different t, from different banks)
+#define XC_TILE_ROW 65u
 template <bool TILE>
 __device__ __forceinline__ uint32_t gear_mask(const uint32_t w[8], uint32_t g, uint32_t *tile)
 {
@@ -694,13 +697,13 @@ __device__ __forceinline__ uint32_t gear_mask(const uint32_t w[8], uint32_t g, u
 #pragma unroll
     for (int d = 0; d < 8; d++) {
         g = gear_cmp_step<0>(m, g, w[d]);
-        if (TILE) tile[(4 * d + 0) * 64 + l] = g;
+        if (TILE) tile[(4 * d + 0) * XC_TILE_ROW + l] = g;
         g = gear_cmp_step<1>(m, g, w[d]);
-        if (TILE) tile[(4 * d + 1) * 64 + l] = g;
+        if (TILE) tile[(4 * d + 1) * XC_TILE_ROW + l] = g;
         g = gear_cmp_step<2>(m, g, w[d]);
-        if (TILE) tile[(4 * d + 2) * 64 + l] = g;
+        if (TILE) tile[(4 * d + 2) * XC_TILE_ROW + l] = g;
         g = gear_cmp_step<3>(m, g, w[d]);
-        if (TILE) tile[(4 * d + 3) * 64 + l] = g;
+        if (TILE) tile[(4 * d + 3) * XC_TILE_ROW + l] = g;
     }
     // 32 compares so far: position -1 (shifted out of the word by the 32nd) and positions 0..30
     return mask_last(m, g);

@@ -1268,7 +1268,7 @@ __device__ __forceinline__ uint32_t block_predict(const PlanDev &P, uint32_t g, 
 constexpr uint32_t ANC_LIST = 512;  // anchor list entries per pass (a multiple of 64)
 
 // The anchors of a k_blockhash group: G of every position of its na blocks
-// (w[i]: block i, lane l: bytes 32 l .. 32 l + 31) into tile (per wave: 32 x 64 values, then the
+// (w[i]: block i, lane l: bytes 32 l .. 32 l + 31) into tile (per wave: 32 rows of 64 values and a pad word, then the
 // 32 values of the lane before lane 0), the block's anchors compacted into a position-ordered list
 // (list: ANC_LIST entries per wave, in passes), then every input anchor into the group's records, 64 list entries
 // at a time (runs of equal fingerprints at consecutive positions, at most 32 and within a 32-byte
@@ -1280,7 +1280,7 @@ __device__ __forceinline__ uint64_t group_anchors(const PlanDev &P, uint32_t g, 
                                                   uint16_t *list, uint32_t abl)
 {
     const uint32_t l = lane_id();
-    uint32_t *prev = tile + 32u * 64u;
+    uint32_t *prev = tile + 32u * XC_TILE_ROW;
     auto wave_sync = []() {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -1314,7 +1314,7 @@ __device__ __forceinline__ uint64_t group_anchors(const PlanDev &P, uint32_t g, 
         first = readlane(sf, 63);
         if (i > 0) {  // lane 0's G(p - 32): the last lane of the block before
             wave_sync();
-            if (l < 32u) prev[l] = tile[l * 64u + 63u];
+            if (l < 32u) prev[l] = tile[l * XC_TILE_ROW + 63u];
             wave_sync();
         }
         if (l == 0) P.rec_blk[g * BLK_GROUP + i] = min(cnt, REC_CAP);
@@ -1349,8 +1349,8 @@ __device__ __forceinline__ uint64_t group_anchors(const PlanDev &P, uint32_t g, 
             const bool live = idx < total;
             const uint32_t p = live ? list[idx % ANC_LIST] : 0u;
             const uint32_t ln = p >> 5, t = p & 31u;
-            const uint32_t gv = tile[t * 64u + ln];
-            const uint32_t g2 = ln ? tile[t * 64u + ln - 1u] : prev[t];
+            const uint32_t gv = tile[t * XC_TILE_ROW + ln];
+            const uint32_t g2 = ln ? tile[t * XC_TILE_ROW + ln - 1u] : prev[t];
             const uint64_t fp = anc_fp(gv, g2);
             // a run continues when the entry before has the position before (inside one lane's
             // 32 positions) and the same fingerprint
@@ -1389,12 +1389,12 @@ __device__ __forceinline__ uint64_t group_anchors(const PlanDev &P, uint32_t g, 
 // predict: also the predictions of these blocks (the run's first sub-batch, hashed in line after
 // the declaration set's clear: one kernel instead of two).  ANC: the group's anchors too (a run in
 // anchor mode); groups then also cover a buffer's partial last block.
-// (LDS 37 KB and <= 128 VGPRs: four workgroups, 16 waves, per CU; with a whole block's list, 49
+// (LDS 38 KB and <= 128 VGPRs: four workgroups, 16 waves, per CU; with a whole block's list, 49
 // KB and 3 waves per SIMD, the side-stream hashing hid less of its latency: cfg5 A/B +2.3 %)
 template <bool PREDICT, bool ANC>
 __global__ __launch_bounds__(256, 4) void k_blockhash(DeclArgs a)
 {
-    __shared__ uint32_t tiles[ANC ? 4 : 1][ANC ? 32 * 64 + 32 : 1];
+    __shared__ uint32_t tiles[ANC ? 4 : 1][ANC ? 32 * XC_TILE_ROW + 32 : 1];
     __shared__ uint16_t lists[ANC ? 4 : 1][ANC ? ANC_LIST : 1];
     const PlanDev &P = a.P;
     const uint32_t g = a.j0 + blockIdx.x * 4u + (threadIdx.x >> 6);
