@@ -301,3 +301,44 @@ def test_anchor_scan_twin_against_a_carried_candidate(gpu_ctx, oracle_mod):
          np.concatenate([W.gen(0xC9, 300), seg, y])]
     assert w.XCodecEncoder(cache).encode_batch(e) == oc.encode_batch(e)
     assert len(cache) == len(oc)
+
+
+def _anchorless_random():
+    """A 2048-byte segment of random-looking bytes without an anchor (G >= 2^26 at every offset >= 63):
+    anchors cluster (G(p) shifts G(p - 1) up), so about one random segment in 10^7 has none; this one
+    was declared by the bench's live-cache leg (batch seed 0x555a, tests/golden/anchorless_segment.bin)."""
+    import os
+    seg = np.fromfile(os.path.join(os.path.dirname(__file__), "golden", "anchorless_segment.bin"), np.uint8)
+    assert len(seg) == 2048 and _last_anchor(seg) is None
+    return seg
+
+
+def test_anchor_scan_finds_a_cached_anchorless_segment(gpu_ctx, oracle_mod, monkeypatch):
+    """A cached segment without an anchor keeps the cache in anchor mode: windows with no input
+    anchor at offsets 63 .. 2047 (gap windows) are proposed beside the index's, so every repeat of
+    the segment is found (unaligned, aligned, at a buffer's start and end, across a k_blockhash
+    group boundary, twice in a row, right after a REF) with no sub-batch falling back."""
+    monkeypatch.setenv("XC_SUB_MB", "1")
+    cache, oc, pool = _pool_cache(gpu_ctx, oracle_mod, 64)
+    s = _anchorless_random()
+    first = [np.concatenate([s, W.gen(0xB2, 5000)])]  # (declared: the buffer's first segment)
+    got, st = _plan_run(gpu_ctx, cache, first)
+    _same(got, oc.encode_batch(first))
+    g = lambda k, n: W.gen(0xB400 + k, n)
+    bufs = [np.concatenate([g(0, 1), s, g(1, 3000)]),
+            np.concatenate([g(2, 555), s, g(3, 70)]),
+            np.concatenate([g(4, 2047), s, g(5, 2047)]),
+            np.concatenate([g(6, 2048), s, g(7, 4096)]),           # aligned
+            np.concatenate([s, g(8, 9000)]),                        # at the start
+            np.concatenate([g(9, 12000), s]),                       # at the end
+            np.concatenate([g(10, 16384 - 700), s, g(11, 9000)]),  # across the first group boundary
+            np.concatenate([g(12, 300), s, s, g(13, 1000)]),        # twice
+            np.concatenate([g(14, 100), pool[3 * 2048:4 * 2048], s, g(15, 500)])]  # after a REF
+    bufs += W.repeat_buffers(40, 0xB5, np_segments=64, pool_bytes=pool)  # (more sub-batches)
+    want = oc.encode_batch(bufs)
+    assert all(want[i].count(b"\xf1\x02") >= 1 + (i == 7) for i in range(9))
+    got, st = _plan_run(gpu_ctx, cache, bufs)
+    _same(got, want)
+    assert st.anchor_scans == st.sub_batches > 1 and st.anchor_fallbacks == 0, \
+        (st.anchor_scans, st.sub_batches, st.anchor_fallbacks)
+    assert len(cache) == len(oc)

@@ -49,9 +49,11 @@ def main():
             h0 = cache.hit_stats()["host_s"]
             cache.settle()
             t2 = time.perf_counter()
+            st = plan.stats()
             iso.append((round((t1 - t0) * 1e3, 3), round((t2 - t1) * 1e3, 3),
-                        round((cache.hit_stats()["host_s"] - h0) * 1e3, 3)))
-        print("isolated (run ms, settle ms, replay ms):", iso, flush=True)
+                        round((cache.hit_stats()["host_s"] - h0) * 1e3, 3), int(st.anchor_scans),
+                        int(st.anchor_fallbacks), len(cache)))
+        print("isolated (run ms, settle ms, replay ms, anchor scans, fallbacks, segments):", iso, flush=True)
         cache.restore()
         torch.cuda.synchronize()
         ts = [time.perf_counter()]

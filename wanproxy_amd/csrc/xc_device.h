@@ -723,13 +723,26 @@ __device__ __forceinline__ uint32_t gear_at(const uint32_t w[8], uint32_t g, uin
     return g;
 }
 
-// The anchor key of a 2048-byte segment held as 32 bytes per lane (lane l: bytes 32 l .. 32 l + 31),
-// or ANC_NONE; every lane returns it.
-__device__ __forceinline__ uint64_t wave_seg_anchor(const uint32_t w[8])
+// Anchor mask of the lane's 32 positions below `lim` (bit 31 - t: position t), from G at position -1
+// (the plain form of gear_mask for the other levels of a segment's key).
+__device__ __forceinline__ uint32_t gear_mask_below(const uint32_t w[8], uint32_t g, uint32_t lim)
+{
+    uint32_t m = 0;
+#pragma unroll
+    for (int d = 0; d < 8; d++) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            g = (g << 1) + ((w[d] >> (8 * k)) & 0xffu);
+            m = (m << 1) | (g < lim ? 1u : 0u);
+        }
+    }
+    return m;
+}
+
+// The segment's key from its anchor mask m (one level): its last anchor j >= 63, or ANC_NONE.
+__device__ __forceinline__ uint64_t seg_key_of_mask(const uint32_t w[8], uint32_t gi, uint32_t m)
 {
     const uint32_t l = lane_id();
-    const uint32_t gi = gear_prev(gear32(w), 0u);
-    uint32_t m = gear_mask<false>(w, gi, nullptr);
     // positions 32 l + t >= 63: lanes >= 2 all, lane 1 only t = 31 (bit 0)
     m = l >= 2u ? m : (l == 1u ? (m & 1u) : 0u);
     // the last anchor: the highest lane with one, its lowest bit (largest t)
@@ -740,6 +753,21 @@ __device__ __forceinline__ uint64_t wave_seg_anchor(const uint32_t w[8])
     const uint32_t jj = readlane(j, lj), t = jj & 31u;
     const uint32_t g = gear_at(w, gi, t);
     return anc_key(anc_fp(readlane(g, lj), readlane(g, lj - 1)), jj);
+}
+
+// The anchor key of a 2048-byte segment held as 32 bytes per lane (lane l: bytes 32 l .. 32 l + 31),
+// or ANC_NONE; every lane returns it.  Level 0: its last anchor (G < 2^26).  A segment with none
+// (anchors cluster: about one random segment in 10^7) takes its last position with G < 2^27, or
+// with G < 2^28 (levels 1, 2): the anchor scan finds those through the gap windows (k_aprop);
+// ANC_NONE past level 2 (a constant run of most byte values, say).
+__device__ __forceinline__ uint64_t wave_seg_anchor(const uint32_t w[8])
+{
+    const uint32_t gi = gear_prev(gear32(w), 0u);
+    const uint64_t k0 = seg_key_of_mask(w, gi, gear_mask<false>(w, gi, nullptr));
+    if (k0 != ANC_NONE) return k0;
+    const uint64_t k1 = seg_key_of_mask(w, gi, gear_mask_below(w, gi, ANC_G_LIMIT << 1));
+    if (k1 != ANC_NONE) return k1;
+    return seg_key_of_mask(w, gi, gear_mask_below(w, gi, ANC_G_LIMIT << 2));
 }
 
 }  // namespace xc

@@ -461,6 +461,123 @@ template __global__ void k_scan<5>(ScanArgs);
 // (pcnt / pq).  k_aevents: one lane per chunk writes the aligned windows (no proposal: the common
 // case); a chunk with proposals is sorted and merged by its whole wave in an LDS bitmask.
 
+// A proposal: window end q of buffer b (chunk list of its chunk), unless aligned (an event anyway)
+// or in a predicted REF's shadow.
+__device__ __forceinline__ void propose(const PlanDev &P, const AScanArgs &a, uint32_t b, uint32_t q)
+{
+    if (((q + 1u) & (XC_SEG - 1u)) == 0u) return;
+    const uint32_t cblk = P.blk_base[b];
+    if (a.shadow && q >= XC_SEG && blk_cached(P.blk_pref[cblk + (q >> 11) - 1u])) return;
+    const uint32_t c = P.buf_chunk0[b] + q / P.chunk_len;
+    const uint32_t slot = atomicAdd(&a.pcnt[c], 1u);
+    if (slot < PROP_CAP) a.pq[(size_t)c * PROP_CAP + slot] = q;
+}
+
+// Gap windows.  A segment without a level-0 anchor is indexed by a later level's
+// (its last position j with G < 2^27, or < 2^28: wave_seg_anchor), and a window equal to it has no
+// input anchor at offsets 63 .. 2047: its end q has none in [q - 1984, q].  So the input positions
+// of every run of at least 1985 positions without an input anchor (between two records, before a
+// buffer's first) are probed with their own fingerprints where G < 2^28.  k_aprop's threads note
+// the gaps (gap_note), its workgroup probes them together (gap_probe).  A cache segment with no key
+// at all (anc_bad: past level 2) sends a sub-batch with a gap to the exact scan.
+constexpr uint32_t GAP_MAX = 16;  // gaps per k_aprop workgroup (more: the exact scan)
+struct GapList {
+    uint32_t n;
+    uint32_t b[GAP_MAX], lo[GAP_MAX], hi[GAP_MAX];
+};
+
+// The first input anchor of buffer b at or after group g (its groups up to the sub-batch's end), or
+// the buffer's length.
+__device__ __forceinline__ uint32_t next_anchor(const PlanDev &P, const AScanArgs &a, uint32_t g, uint32_t b,
+                                                uint32_t len)
+{
+    for (; g < a.g_hi; g++) {
+        const uint2 gr = P.blk_grp[g];
+        if (gr.x != b) break;
+        const uint32_t f = P.ainfo[g].x;
+        if (f != NONE) return gr.y * XC_SEG + f;
+    }
+    return len;
+}
+
+// Anchor-free positions lo .. hi (inclusive) of buffer b: a gap when they hold a window's 1985.
+__device__ __forceinline__ void gap_note(const PlanDev &P, GapList &G, uint32_t b, uint32_t lo, uint32_t hi, bool hard)
+{
+    if (hi < lo || hi - lo + 1u < XC_SEG - 63u) return;
+    if (hard) {
+        atomicOr(&P.ctl[CTL_AFAIL], 8u);
+        return;
+    }
+    const uint32_t k = atomicAdd(&G.n, 1u);
+    if (k < GAP_MAX) {
+        G.b[k] = b;
+        G.lo[k] = lo;
+        G.hi[k] = hi;
+    } else {
+        atomicOr(&P.ctl[CTL_AFAIL], 8u);
+    }
+}
+
+// The gaps of group g from k_blockhash's record of it (inf) and of the group after it (inf1, gr1:
+// loaded by the caller ahead of its record work): inside it, after its last anchor (to the buffer's
+// next), and for a buffer's first group the one before its first anchor (positions below 63 are no
+// anchors).  The buffer's length is read only when a gap can reach its end.
+__device__ __forceinline__ void gaps_of_group(const PlanDev &P, const AScanArgs &a, GapList &G, uint32_t g, uint4 inf,
+                                              uint2 gr, uint4 inf1, uint2 gr1, bool hard)
+{
+    const uint32_t b = gr.x, gpos = gr.y * XC_SEG;
+    if (inf.z > AGAP_CAP) {
+        atomicOr(&P.ctl[CTL_AFAIL], 8u);
+        return;
+    }
+    for (uint32_t j = 0; j < inf.z; j++) {
+        const uint2 v = P.agap[g * AGAP_CAP + j];
+        gap_note(P, G, b, gpos + v.x + 1u, gpos + v.y - 1u, hard);
+    }
+    const bool same = g + 1u < a.g_hi && gr1.x == b;
+    uint32_t next = NONE;  // the buffer's first input anchor after the group (or its length)
+    if (same && inf1.x != NONE) next = gr1.y * XC_SEG + inf1.x;
+    if (inf.y != NONE) {
+        if (next == NONE) next = same ? next_anchor(P, a, g + 2u, b, P.buf_len[b]) : P.buf_len[b];
+        gap_note(P, G, b, gpos + inf.y + 1u, next - 1u, hard);  // (next <= the length)
+    }
+    if (gr.y == 0u) {
+        uint32_t first = gpos + inf.x;
+        if (inf.x == NONE) first = next != NONE ? next : next_anchor(P, a, g + 1u, b, P.buf_len[b]);
+        gap_note(P, G, b, 63u, first - 1u, hard);
+    }
+}
+
+// Wave 0 of k_aprop's workgroup over one gap: lane t takes a stretch of its positions, G(p) and G(p - 32) by two
+// rolling sums over the bytes (31 bytes of history each), and probes the fingerprints of the
+// positions with G < 2^28 (the combined filter first, then both tables).
+__device__ __forceinline__ void gap_probe(const PlanDev &P, const AScanArgs &a, uint32_t b, uint32_t lo, uint32_t hi)
+{
+    const uint8_t *base = P.in + P.buf_off[b];
+    const uint32_t len = P.buf_len[b], n = hi - lo + 1u, S = (n + 63u) / 64u;
+    const uint32_t p0 = lo + lane_id() * S, p1 = min(p0 + S, hi + 1u);
+    if (p0 >= p1) return;
+    uint32_t g1 = 0, g2 = 0;
+    for (uint32_t p = p0 - 31u; p < p1; p++) {
+        g1 = (g1 << 1) + base[p];
+        g2 = (g2 << 1) + base[p - 32u];
+        if (p < p0 || g1 >= (ANC_G_LIMIT << 2)) continue;
+        const uint64_t fp = anc_fp(g1, g2);
+        const uint32_t mx = anc_mix(fp);
+        if (!anc_ftest(P.amix[anc_fword(mx)], mx)) continue;
+        for (int tb = 0; tb < 2; tb++) {
+            const AncSet &T = tb ? P.danc : P.canc;
+            for (uint32_t kk = anc_home(fp, T.mask);; kk = (kk + 1u) & T.mask) {
+                const uint64_t key = T.keys[kk];
+                if (key == XC_EMPTY64) break;
+                if ((key >> 11) != fp) continue;
+                const uint32_t j = (uint32_t)key & 2047u, q = p + (XC_SEG - 1u) - j;
+                if (p >= j && q < len) propose(P, a, b, q);
+            }
+        }
+    }
+}
+
 // (APROP_GROUPS groups per workgroup, xc_kernels.h: every thread's record and filter loads of all
 // of them in flight together; one group per workgroup left the kernel latency-bound, and 2 beat 4
 // and 8 once the side stream's block hashing ran beside it: cfg5 A/B +0.8 %, aprop 0.61 -> 0.53 ms)
@@ -468,10 +585,9 @@ __global__ __launch_bounds__(256) void k_aprop(AScanArgs a)
 {
     const PlanDev &P = a.P;
     if (aborted(P)) return;
-    if (uniform(*(volatile const uint32_t *)P.anc_bad)) {  // a segment the index cannot find
-        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&P.ctl[CTL_AFAIL], 8u);
-        return;
-    }
+    __shared__ GapList G;
+    // a cached segment without any key (anc_bad): a sub-batch with a gap takes the exact scan
+    const bool hard = uniform(*(volatile const uint32_t *)P.anc_bad) != 0u;
     const uint32_t g0 = a.g_lo + blockIdx.x * APROP_GROUPS;
     uint32_t cnt[APROP_GROUPS];
     uint2 gr[APROP_GROUPS];
@@ -488,6 +604,21 @@ __global__ __launch_bounds__(256) void k_aprop(AScanArgs a)
         if (threadIdx.x == 0) atomicOr(&P.ctl[CTL_AFAIL], 4u);
         return;
     }
+    // the gaps of the workgroup's groups: wave 0's lane k loads group g0 + k's record of them (and
+    // the next group's) ahead of its records, notes them after, and the wave probes them
+    const bool gl = threadIdx.x < APROP_GROUPS && g0 + threadIdx.x < a.g_hi;
+    uint4 ginf = make_uint4(0u, 0u, 0u, 0u), ginf1 = ginf;
+    uint2 ggr = make_uint2(0u, 0u), ggr1 = make_uint2(NONE, 0u);
+    if (gl) {
+        const uint32_t g = g0 + threadIdx.x;
+        ginf = P.ainfo[g];
+        ggr = P.blk_grp[g];
+        if (g + 1u < a.g_hi) {
+            ginf1 = P.ainfo[g + 1u];
+            ggr1 = P.blk_grp[g + 1u];
+        }
+    }
+    if (threadIdx.x == 0) G.n = 0;
     uint32_t cmax = 0;
 #pragma unroll
     for (uint32_t k = 0; k < APROP_GROUPS; k++) cmax = max(cmax, cnt[k]);
@@ -539,6 +670,13 @@ __global__ __launch_bounds__(256) void k_aprop(AScanArgs a)
             }
         }
     }
+    if (threadIdx.x >= 64u) return;
+    if (gl) gaps_of_group(P, a, G, g0 + threadIdx.x, ginf, ggr, ginf1, ggr1, hard);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t ng = min(uniform(G.n), GAP_MAX);
+    for (uint32_t k = 0; k < ng; k++) gap_probe(P, a, G.b[k], G.lo[k], G.hi[k]);
 }
 
 __global__ __launch_bounds__(256) void k_aevents(AScanArgs a)
@@ -1305,6 +1443,9 @@ __device__ __forceinline__ uint64_t group_anchors(const PlanDev &P, uint32_t g, 
     }
     uint32_t cnt = 0;
     uint64_t bkey = ANC_NONE;
+    // the group's first and last input anchor and its gaps (anchors >= 1986 apart, group-relative
+    // positions: k_aprop's gap windows)
+    uint32_t firstp = NONE, lastp = NONE, ngap = 0;
 #pragma unroll
     for (uint32_t i = 0; i < BLK_GROUP; i++) {
         if (i >= na) break;
@@ -1360,6 +1501,16 @@ __device__ __forceinline__ uint64_t group_anchors(const PlanDev &P, uint32_t g, 
             const uint64_t pfp = ((uint64_t)fh << 32) | fl;
             // (a run does not continue across 64 entries: a chunk's first entry is a head)
             const bool cont = live && l != 0u && (p & 31u) != 0u && pp + 1u == p && pfp == fp;
+            {
+                const uint32_t gp = i * XC_SEG + p, prv = l == 0u ? lastp : i * XC_SEG + pp;
+                for (uint64_t gm = ballot(live && prv != NONE && gp - prv >= XC_SEG - 62u); gm; gm &= gm - 1) {
+                    const int f = __ffsll((unsigned long long)gm) - 1;
+                    const uint32_t x = readlane(prv, f), y = readlane(gp, f);
+                    if (l == 0 && ngap < AGAP_CAP) P.agap[g * AGAP_CAP + ngap] = make_uint2(x, y);
+                    ngap++;
+                }
+                if (firstp == NONE) firstp = i * XC_SEG + readlane(p, 0);
+            }
             const uint64_t heads = ballot(live && !cont);
             const uint64_t above = heads & (l == 63u ? 0ull : ~0ull << (l + 1u));
             const uint32_t end = above ? b0 + (uint32_t)__builtin_ctzll(above) : min(total, b0 + 64u);
@@ -1372,14 +1523,17 @@ __device__ __forceinline__ uint64_t group_anchors(const PlanDev &P, uint32_t g, 
             const uint32_t last = min(total - b0, 64u) - 1u;
             cp = readlane(p, (int)last);
             cfp = readlane64(fp, (int)last);
+            lastp = i * XC_SEG + cp;
         }
         if (i < n) {  // the block's anchor: its last one at offset >= 63
-            const uint64_t key = total && cp >= 63u ? anc_key(cfp, cp) : ANC_NONE;
+            uint64_t key = total && cp >= 63u ? anc_key(cfp, cp) : ANC_NONE;
+            if (key == ANC_NONE) key = wave_seg_anchor(wi);  // (none: a later level's, rarely)
             if (l == i) bkey = key;
         }
         wave_sync();  // (the next block's tile and list overwrite these)
     }
     if (l == 0) {
+        P.ainfo[g] = make_uint4(firstp, lastp, ngap, 0u);
         P.rec_cnt[g] = cnt <= REC_CAP ? cnt : (REC_OVF | REC_CAP);
         for (uint32_t i = na; i < BLK_GROUP; i++) P.rec_blk[g * BLK_GROUP + i] = min(cnt, REC_CAP);
     }
@@ -1599,7 +1753,8 @@ __device__ __forceinline__ void enter_tokens(const PlanDev &P, uint32_t b, const
     if (P.anc_run) {
         const uint32_t sg = ext ? P.tok_seg[tb + t] : 0u;
         uint64_t key = ext && (sg & (XC_SEG - 1u)) == 0u ? P.blk_anc[P.blk_base[b] + sg / XC_SEG] : ANC_NONE;
-        for (uint64_t m = ballot(ext && (sg & (XC_SEG - 1u)) != 0u); m; m &= m - 1) {
+        // (an aligned block without a level-0 anchor too: its key of a later level)
+        for (uint64_t m = ballot(ext && key == ANC_NONE); m; m &= m - 1) {
             const int f = __ffsll((unsigned long long)m) - 1;
             uint32_t wv[8];
             load32_window(base + readlane(sg, f) + 32u * l, wv);

@@ -163,6 +163,8 @@ struct PlanDev {
     uint64_t *rec;             // [groups * REC_CAP] input anchors: fp << 19 | group position << 5 | run - 1
     uint32_t *rec_cnt;         // [groups] records (| REC_OVF: more than REC_CAP)
     uint32_t *rec_blk;         // [groups * 8] the first record of each block of the group
+    uint4 *ainfo;              // [groups] first and last input anchor (group-relative, NONE: none), gaps
+    uint2 *agap;               // [groups * AGAP_CAP] anchors >= 1986 apart inside the group (k_aprop's gaps)
     const uint32_t *buf_grp0;  // [nb + 1] first k_blockhash group of every buffer
     // the cache's word: ~slot of its first segment entered without an anchor (0: none; kept on
     // the device, as the emits after a run's early publication set it: k_ascan reads it)
@@ -176,6 +178,7 @@ constexpr uint32_t APROP_GROUPS = XC_APROP_GROUPS;  // k_aprop: block groups per
 constexpr uint32_t BLK_GROUP = 8;    // aligned blocks per k_blockhash group (one wave)
 constexpr uint32_t REC_CAP = 1024;  // anchor records per k_blockhash group (16 KiB; random data: ~256)
 constexpr uint32_t REC_OVF = 0x80000000u;
+constexpr uint32_t AGAP_CAP = 4;   // gaps a k_blockhash group records (more: the exact scan)
 constexpr uint32_t PROP_CAP = 64;  // anchor proposals a chunk keeps (more: the exact scan redoes the sub-batch)
 __device__ __forceinline__ uint64_t rec_make(uint64_t fp, uint32_t pos, uint32_t n)
 {

@@ -612,8 +612,8 @@ static int cache_count_host(xc_cache *c, uint32_t *n)
 }
 
 // The anchor index serves a memory cache (a COSS mirror's lookups all go through
-// its Store) whose every segment has an anchor.
-static bool cache_anc_ok(const xc_cache *c) { return c->mem && !c->engine && c->anc_bad == NONE; }
+// its Store); its segments without an anchor (anc_bad) are found through the gap windows.
+static bool cache_anc_ok(const xc_cache *c) { return c->mem && !c->engine; }
 
 // Index the segments entered since the index last caught up (the count known on the host).
 static int cache_anc_catch_up(xc_cache *c)
@@ -1340,6 +1340,8 @@ struct xc_plan {
     uint32_t *d_buf_grp0 = nullptr;
     uint64_t *d_rec = nullptr, *d_blk_anc = nullptr;
     uint32_t *d_rec_cnt = nullptr, *d_amix = nullptr, *d_rec_blk = nullptr;
+    uint4 *d_ainfo = nullptr;
+    uint2 *d_agap = nullptr;
     uint32_t *d_tcnt = nullptr;  // the tail check's collision lists (k_tailcheck / k_tailfinal)
     uint32_t *d_pcnt = nullptr, *d_pq = nullptr;  // the anchor scan's proposals per chunk
     uint4 *d_tlist = nullptr;
@@ -1842,6 +1844,8 @@ extern "C" int xc_plan_destroy(xc_plan *p)
     dfree(p->d_rec);
     dfree(p->d_rec_cnt);
     dfree(p->d_rec_blk);
+    dfree(p->d_ainfo);
+    dfree(p->d_agap);
     dfree(p->d_tcnt);
     dfree(p->d_pcnt);
     dfree(p->d_pq);
@@ -1995,6 +1999,8 @@ static int plan_anchor_setup(xc_plan *p)
             HIPCHK(dmalloc(&p->d_rec, std::max<uint64_t>(p->ngroups, 1) * REC_CAP * 8));
             HIPCHK(dmalloc(&p->d_rec_cnt, std::max<uint64_t>(p->ngroups, 1) * 4));
             HIPCHK(dmalloc(&p->d_rec_blk, std::max<uint64_t>(p->ngroups, 1) * BLK_GROUP * 4));
+            HIPCHK(dmalloc(&p->d_ainfo, std::max<uint64_t>(p->ngroups, 1) * sizeof(uint4)));
+            HIPCHK(dmalloc(&p->d_agap, std::max<uint64_t>(p->ngroups, 1) * AGAP_CAP * sizeof(uint2)));
             HIPCHK(hipMemsetAsync(p->d_rec_blk, 0, std::max<uint64_t>(p->ngroups, 1) * BLK_GROUP * 4, s));
             HIPCHK(dmalloc(&p->d_tcnt, std::max<uint64_t>(p->nb, 1) * 4));
             HIPCHK(hipMemsetAsync(p->d_tcnt, 0, std::max<uint64_t>(p->nb, 1) * 4, s));
@@ -2009,13 +2015,14 @@ static int plan_anchor_setup(xc_plan *p)
             p->P.rec = p->d_rec;
             p->P.rec_cnt = p->d_rec_cnt;
             p->P.rec_blk = p->d_rec_blk;
+            p->P.ainfo = p->d_ainfo;
+            p->P.agap = p->d_agap;
             p->P.blk_anc = p->d_blk_anc;
             p->P.amix = p->d_amix;
             p->P.danc = p->dset.a;
         }
         int rc = cache_anc_catch_up(c);
         if (rc) return rc;
-        if (c->anc_bad != NONE) p->anc_run = false;  // (a segment without an anchor: exact)
     }
     p->P.anc_run = p->anc_run ? 1u : 0u;
     p->P.anc_scan = 0;
@@ -2738,6 +2745,8 @@ static int encode_finish(xc_plan *p)
         if (ctl[CTL_ERROR]) break;
         p->stats.redone++;
         if (ctl[CTL_AFAIL]) {
+            static const bool dbg_af = getenv("XC_DEBUG_AFAIL") && atoi(getenv("XC_DEBUG_AFAIL"));
+            if (dbg_af) fprintf(stderr, "anchor fallback: sub-batch %zu, flags %u\n", si, ctl[CTL_AFAIL]);
             // the anchor index cannot decide this sub-batch: the exact scan redoes it, and the
             // rest of the run (a collision or an anchorless segment may concern later ones too)
             HIPCHK(hipMemsetAsync(p->P.ctl + CTL_AFAIL, 0, 4, s));
@@ -2783,6 +2792,16 @@ static int encode_finish(xc_plan *p)
             HIPCHK(hipMemcpyAsync(&bad, c->ctl + CTL_ANCLESS, 4, hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));
             if (bad) c->anc_bad = std::min(c->anc_bad, ~bad);
+            static const bool dbg_anc = getenv("XC_DEBUG_ANC") && atoi(getenv("XC_DEBUG_ANC"));
+            if (dbg_anc && bad && ~bad < c->dev_cap) {
+                std::vector<uint8_t> sb(XC_SEG);
+                uint64_t key = 0;
+                HIPCHK(hipMemcpy(sb.data(), c->segs + (size_t)~bad * XC_SEG, XC_SEG, hipMemcpyDeviceToHost));
+                HIPCHK(hipMemcpy(&key, c->anc_of + ~bad, 8, hipMemcpyDeviceToHost));
+                fprintf(stderr, "anchorless segment %u key %016llx bytes ", ~bad, (unsigned long long)key);
+                for (uint8_t v : sb) fprintf(stderr, "%02x", v);
+                fprintf(stderr, "\n");
+            }
         }
     }
     // (the first pass enqueued it behind itself unless a sub-batch was redone since)
