@@ -339,6 +339,9 @@ __device__ __forceinline__ uint4 load16_unaligned(const uint8_t *p)
 // cache slot (16-byte aligned), split into a load half and a store half so that a wave can
 // have several payloads in flight.  Every store is a whole 16-byte aligned store except the
 // wire copy's head and tail bytes; the wire-aligned reads of src hit the cache.
+#ifndef XC_NT_STORE
+#define XC_NT_STORE 0
+#endif
 struct PayloadRegs {
     uint4 a0, a1;  // slot-aligned chunks: src + 16 l, src + 1024 + 16 l
     uint4 b0, b1;  // wire-aligned chunks
@@ -393,6 +396,18 @@ __device__ __forceinline__ void payload_load(const uint8_t *src, const uint8_t *
     r.tb = t0 + l < XC_SEG ? src[t0 + l] : 0u;
 }
 
+// 16-byte store; XC_NT_STORE=1 (a build flag for A/B runs): non-temporal
+__device__ __forceinline__ void store16(void *p, const uint4 &v)
+{
+#if XC_NT_STORE
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    v4u x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, (v4u *)p);
+#else
+    *(uint4 *)p = v;
+#endif
+}
+
 __device__ __forceinline__ void payload_store(uint8_t *out, uint8_t *seg, const PayloadRegs &r)
 {
     const uint32_t l = lane_id();
@@ -400,11 +415,11 @@ __device__ __forceinline__ void payload_store(uint8_t *out, uint8_t *seg, const 
     const uint32_t nbody = (XC_SEG - head) >> 4;
     const uint32_t t0 = head + 16u * nbody;
     if (seg) {
-        ((uint4 *)seg)[l] = r.a0;
-        ((uint4 *)seg)[l + 64u] = r.a1;
+        store16((uint4 *)seg + l, r.a0);
+        store16((uint4 *)seg + l + 64u, r.a1);
     }
-    if (l < nbody) *(uint4 *)(out + head + 16u * l) = r.b0;
-    if (l + 64u < nbody) *(uint4 *)(out + head + 1024u + 16u * l) = r.b1;
+    if (l < nbody) store16(out + head + 16u * l, r.b0);
+    if (l + 64u < nbody) store16(out + head + 1024u + 16u * l, r.b1);
     if (l < head) out[l] = (uint8_t)r.hb;
     if (t0 + l < XC_SEG) out[t0 + l] = (uint8_t)r.tb;
 }

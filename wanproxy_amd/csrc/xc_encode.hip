@@ -1197,6 +1197,7 @@ __device__ __forceinline__ void walk_seq(const WalkArgs &a, uint32_t b, uint64_t
         P.buf_next[b] = n_ext;
         P.buf_nref[b] = n_ref;
         if (P.coll_cnt) P.coll_cnt[b] = n_coll;
+        if (n_coll) atomicOr(&P.ctl[CTL_COLLS], 1u);
         if (ntok > tcap) atomicOr(&P.ctl[CTL_ERROR], ERR_TOKENS);
         if (cross) atomicMin(&P.ctl[CTL_FIRST_CROSS], b);
     }

@@ -48,7 +48,8 @@ enum : uint32_t {
     CTL_DUPS = 12,       // k_emit entered hashes the cache held (a duplicate enter: the host replays)
     CTL_AFAIL = 13,      // an anchor-scanned sub-batch needs the exact scan
     CTL_ANCLESS = 14,    // (the cache's scratch words: ~slot of its first segment without an anchor)
-    CTL_WORDS = 16
+    CTL_COLLS = 15,      // some walk recorded a collision lookup (the run's hits are more than its REFs)
+    CTL_WORDS = 17       // (the last word: the host's publication sentinel)
 };
 constexpr uint32_t ERR_CAPACITY = 1, ERR_TOKENS = 2, ERR_DECLS = 4;  // (ERR_PACK_CAP = 8 below)
 

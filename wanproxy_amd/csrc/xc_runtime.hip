@@ -2817,7 +2817,9 @@ static int encode_finish(xc_plan *p)
             c->host_count = p->count0;
             return fail(XC__SLOW, "a hash entered twice");
         }
-        if ((rc = hits_enqueue(p))) return rc;  // its lookup hits, for the recent window
+        // its lookup hits, for the recent window (none: no REF, no collision recorded, no tail
+        // check behind the run that could record one)
+        if ((ctl[CTL_NREF] || ctl[CTL_COLLS] || p->anc_any) && (rc = hits_enqueue(p))) return rc;
     }
     return XC_OK;
 }
