@@ -340,7 +340,7 @@ __device__ __forceinline__ uint4 load16_unaligned(const uint8_t *p)
 // have several payloads in flight.  Every store is a whole 16-byte aligned store except the
 // wire copy's head and tail bytes; the wire-aligned reads of src hit the cache.
 #ifndef XC_NT_STORE
-#define XC_NT_STORE 0
+#define XC_NT_STORE 1
 #endif
 struct PayloadRegs {
     uint4 a0, a1;  // slot-aligned chunks: src + 16 l, src + 1024 + 16 l
@@ -396,7 +396,8 @@ __device__ __forceinline__ void payload_load(const uint8_t *src, const uint8_t *
     r.tb = t0 + l < XC_SEG ? src[t0 + l] : 0u;
 }
 
-// 16-byte store; XC_NT_STORE=1 (a build flag for A/B runs): non-temporal
+// 16-byte store, non-temporal (the wire bytes and the segment store are not read back by this
+// pass; cfg5 A/B +1.6 %, profiles/r04/ab_nt_store.txt); -DXC_NT_STORE=0: plain stores
 __device__ __forceinline__ void store16(void *p, const uint4 &v)
 {
 #if XC_NT_STORE

@@ -21,7 +21,9 @@
 // count_misses.
 #pragma once
 #include <algorithm>
+#include <atomic>
 #include <cstring>
+#include <thread>
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
@@ -256,8 +258,21 @@ struct CItem {
 // kind-3 event gets the state a restart after it needs (the candidate pending after the miss, the
 // source_ start and output offset of the tokens before it).  The device treated them as the plain
 // misses they are; the Store replays their side effects.
+// A bit per 2^20 buckets of the load-miss hashes: almost every window end is rejected by one
+// L2-resident load before the set's probe.
+struct LmFilter {
+    std::vector<uint64_t> bits;
+    explicit LmFilter(const std::unordered_set<uint64_t> &lm) : bits(1u << 14, 0)
+    {
+        for (uint64_t h : lm) bits[bucket(h) >> 6] |= 1ull << (bucket(h) & 63);
+    }
+    static uint32_t bucket(uint64_t h) { return (uint32_t)((h ^ (h >> 31)) * 0x9E3779B97F4A7C15ull >> 44); }
+    bool maybe(uint64_t h) const { return (bits[bucket(h) >> 6] >> (bucket(h) & 63)) & 1u; }
+};
+
 template <class Item>
-void add_load_miss_lookups(const std::unordered_set<uint64_t> &lm, const Item &it, std::vector<EncEvent> &ev)
+void add_load_miss_lookups(const std::unordered_set<uint64_t> &lm, const LmFilter &f, const Item &it,
+                           std::vector<EncEvent> &ev)
 {
     std::vector<uint64_t> refs;
     for (const EncEvent &e : ev)
@@ -272,7 +287,7 @@ void add_load_miss_lookups(const std::unordered_set<uint64_t> &lm, const Item &i
         while (ri < refs.size() && refs[ri] < p) resume = std::max(resume, refs[ri++] + SEG);
         if (p < resume || (ri < refs.size() && refs[ri] == p)) continue;
         const uint64_t h = w.mix();
-        if (lm.count(h)) ev.push_back({p, 3, h, 0, 0, -1, nullptr});
+        if (f.maybe(h) && lm.count(h)) ev.push_back({p, 3, h, 0, 0, -1, nullptr});
     }
 }
 
@@ -382,8 +397,29 @@ int encode(C *c, std::vector<CItem> items, uint8_t *out, const uint64_t *out_off
                 ev[k].push_back({q, 2, ((uint64_t)r[2] << 32) | r[1], oe, base,
                                  r[3] == 0xFFFFFFFFu ? -1 : (int64_t)r[3], nullptr});
             }
-            const bool lm = !c->load_miss.empty();
-            if (lm) add_load_miss_lookups(c->load_miss, items[k], ev[k]);
+        }
+        // the lookups that miss with side effects: a host pass of the rolling hash over every item,
+        // items over up to 16 threads (independent: each writes its own events)
+        const bool lm = !c->load_miss.empty();
+        if (lm) {
+            const LmFilter f(c->load_miss);
+            uint64_t total = 0;
+            for (uint64_t k = 0; k < m; k++) total += items[k].len;
+            const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+            const unsigned nt = (unsigned)std::min<uint64_t>({16, hw, m, std::max<uint64_t>(total >> 20, 1)});
+            std::atomic<uint64_t> next{0};
+            auto work = [&]() {
+                for (uint64_t k; (k = next.fetch_add(1)) < m;) add_load_miss_lookups(c->load_miss, f, items[k], ev[k]);
+            };
+            std::vector<std::thread> th;
+            try {
+                for (unsigned t = 1; t < nt; t++) th.emplace_back(work);
+            } catch (...) {
+            }
+            work();
+            for (std::thread &x : th) x.join();
+        }
+        for (uint64_t k = 0; k < m; k++) {
             // (a declaration precedes the lookup at the same position; flush's comes last)
             std::stable_sort(ev[k].begin(), ev[k].end(), [](const EncEvent &a, const EncEvent &b) {
                 return a.pos != b.pos ? a.pos < b.pos : a.kind < b.kind;
