@@ -608,6 +608,7 @@ __device__ __forceinline__ int set_insert(const DevSet &s, uint64_t h, uint64_t 
 // Segments without an anchor (a 1.6e-14 chance for random bytes; constant runs of some values)
 // keep the cache out of anchor mode (the exact scan, xc_runtime.hip).
 #define ANC_G_LIMIT (1u << 26)
+#define NONE_U32 0xFFFFFFFFu
 #define ANC_NONE 0xFFFFFFFFFFFFFFFFull
 #define ANC_FILT_WORDS (1u << 18)  // 1 MB anchor filter (k = 2 bits in a 32-bit word): stays in an XCD's L2
 
@@ -769,6 +770,29 @@ __device__ __forceinline__ uint64_t seg_key_of_mask(const uint32_t w[8], uint32_
     const uint32_t jj = readlane(j, lj), t = jj & 31u;
     const uint32_t g = gear_at(w, gi, t);
     return anc_key(anc_fp(readlane(g, lj), readlane(g, lj - 1)), jj);
+}
+
+// wave_seg_anchor's key by one lane (a rare case inside a lane-per-block kernel): G(p) and G(p - 32)
+// by two rolling sums, the last position of each level.
+__device__ __forceinline__ uint64_t seg_key_serial(const uint8_t *seg)
+{
+    uint32_t g1 = 0, g2 = 0, j[3] = {NONE_U32, NONE_U32, NONE_U32}, a[3] = {0, 0, 0}, c[3] = {0, 0, 0};
+    for (uint32_t p = 0; p < XC_SEG; p++) {
+        g1 = (g1 << 1) + seg[p];
+        g2 = (g2 << 1) + (p >= 32u ? seg[p - 32u] : 0u);
+        if (p < 63u) continue;
+#pragma unroll
+        for (int v = 0; v < 3; v++)
+            if (g1 < (ANC_G_LIMIT << v)) {
+                j[v] = p;
+                a[v] = g1;
+                c[v] = g2;
+            }
+    }
+#pragma unroll
+    for (int v = 0; v < 3; v++)
+        if (j[v] != NONE_U32) return anc_key(anc_fp(a[v], c[v]), j[v]);
+    return ANC_NONE;
 }
 
 // The anchor key of a 2048-byte segment held as 32 bytes per lane (lane l: bytes 32 l .. 32 l + 31),

@@ -1526,9 +1526,9 @@ __device__ __forceinline__ uint64_t group_anchors(const PlanDev &P, uint32_t g, 
             cfp = readlane64(fp, (int)last);
             lastp = i * XC_SEG + cp;
         }
-        if (i < n) {  // the block's anchor: its last one at offset >= 63
-            uint64_t key = total && cp >= 63u ? anc_key(cfp, cp) : ANC_NONE;
-            if (key == ANC_NONE) key = wave_seg_anchor(wi);  // (none: a later level's, rarely)
+        if (i < n) {  // the block's anchor: its last one at offset >= 63 (none: block_predict and
+                      // the emit take a later level's, seg_key_serial / wave_seg_anchor)
+            const uint64_t key = total && cp >= 63u ? anc_key(cfp, cp) : ANC_NONE;
             if (l == i) bkey = key;
         }
         wave_sync();  // (the next block's tile and list overwrite these)
@@ -1646,7 +1646,9 @@ __device__ __forceinline__ uint32_t block_predict(const PlanDev &P, uint32_t g, 
         const uint32_t lo = (uint32_t)h;  // (the combined level-1 image the first scan loads)
         atomicOr(&P.fmix[filt_word_n(lo, XC_FILT_WORDS >> P.fmix_fold)], filt_mask(lo));
         if (P.anc_scan) {
-            // the anchor scan finds windows equal to this block through its anchor
+            // the anchor scan finds windows equal to this block through its anchor (a block
+            // without a level-0 anchor: a later level's, found through the gap windows)
+            if (akey == ANC_NONE) akey = seg_key_serial(P.in + P.buf_off[b] + (size_t)k * XC_SEG);
             if (akey == ANC_NONE) atomicOr(&P.ctl[CTL_AFAIL], 1u);
             else anc_insert(P.danc, akey);
         }
