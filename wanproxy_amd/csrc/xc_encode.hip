@@ -604,21 +604,23 @@ __global__ __launch_bounds__(256) void k_aprop(AScanArgs a)
         if (threadIdx.x == 0) atomicOr(&P.ctl[CTL_AFAIL], 4u);
         return;
     }
-    // the gaps of the workgroup's groups: wave 0's lane k loads group g0 + k's record of them (and
-    // the next group's) ahead of its records, notes them after, and the wave probes them
-    const bool gl = threadIdx.x < APROP_GROUPS && g0 + threadIdx.x < a.g_hi;
-    uint4 ginf = make_uint4(0u, 0u, 0u, 0u), ginf1 = ginf;
-    uint2 ggr = make_uint2(0u, 0u), ggr1 = make_uint2(NONE, 0u);
-    if (gl) {
-        const uint32_t g = g0 + threadIdx.x;
-        ginf = P.ainfo[g];
-        ggr = P.blk_grp[g];
-        if (g + 1u < a.g_hi) {
-            ginf1 = P.ainfo[g + 1u];
-            ggr1 = P.blk_grp[g + 1u];
+    // the gaps of the workgroup's groups: wave 0 (lane k: group g0 + k) notes them from
+    // k_blockhash's record of them, then probes them, before its share of the records (nothing of
+    // it stays live across the record loop: the kernel keeps its register count and occupancy)
+    if (threadIdx.x < 64u) {
+        if (threadIdx.x == 0) G.n = 0;
+        if (threadIdx.x < APROP_GROUPS && g0 + threadIdx.x < a.g_hi) {
+            const uint32_t g = g0 + threadIdx.x;
+            const bool nx = g + 1u < a.g_hi;
+            gaps_of_group(P, a, G, g, P.ainfo[g], P.blk_grp[g], nx ? P.ainfo[g + 1u] : make_uint4(0u, 0u, 0u, 0u),
+                          nx ? P.blk_grp[g + 1u] : make_uint2(NONE, 0u), hard);
         }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t ng = min(uniform(G.n), GAP_MAX);
+        for (uint32_t k = 0; k < ng; k++) gap_probe(P, a, G.b[k], G.lo[k], G.hi[k]);
     }
-    if (threadIdx.x == 0) G.n = 0;
     uint32_t cmax = 0;
 #pragma unroll
     for (uint32_t k = 0; k < APROP_GROUPS; k++) cmax = max(cmax, cnt[k]);
@@ -670,13 +672,6 @@ __global__ __launch_bounds__(256) void k_aprop(AScanArgs a)
             }
         }
     }
-    if (threadIdx.x >= 64u) return;
-    if (gl) gaps_of_group(P, a, G, g0 + threadIdx.x, ginf, ggr, ginf1, ggr1, hard);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint32_t ng = min(uniform(G.n), GAP_MAX);
-    for (uint32_t k = 0; k < ng; k++) gap_probe(P, a, G.b[k], G.lo[k], G.hi[k]);
 }
 
 __global__ __launch_bounds__(256) void k_aevents(AScanArgs a)

@@ -22,6 +22,9 @@
 #pragma once
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 #include <unordered_map>
@@ -158,16 +161,6 @@ int follow(C *c, const Touch &t)
     int rc = settle(c, t, ch);
     return rc ? rc : (ch.any() ? mirror(c, ch) : XC_OK);
 }
-
-// Later events of a batch that saw a change: any lookup of a hash it added or removed.
-struct Watch {
-    std::unordered_set<uint64_t> hs;
-    explicit Watch(const Change &ch) : hs(ch.removed.begin(), ch.removed.end())
-    {
-        hs.insert(ch.added.begin(), ch.added.end());
-    }
-    bool has(uint64_t h) const { return hs.count(h) != 0; }
-};
 
 // One cache event of an encoder item, in the reference's order (xcodec_encoder.cc:72-171).
 struct EncEvent {
@@ -333,8 +326,31 @@ template <class C>
 int encode(C *c, std::vector<CItem> items, uint8_t *out, const uint64_t *out_off, const uint64_t *out_cap,
            uint64_t *out_len, uint64_t *res_base, int64_t *res_cand)
 {
+    // (XC_REPLAY_PROF=1: passes, their items and the time of each phase, to stderr)
+    static const bool prof = getenv("XC_REPLAY_PROF") && atoi(getenv("XC_REPLAY_PROF"));
+    using clk = std::chrono::steady_clock;
+    double t_dev = 0, t_ev = 0, t_rep = 0;
+    uint64_t passes = 0, items0 = items.size(), items_run = 0;
+    const auto t_all = clk::now();
+    struct Report {
+        bool on;
+        const double &a, &b, &d, &e;
+        const uint64_t &p, &i0, &ir;
+        clk::time_point t0;
+        ~Report()
+        {
+            if (on)
+                fprintf(stderr, "replay: %llu items, %llu passes over %llu items; device %.1f ms, events %.1f ms, "
+                                "store %.1f ms, total %.1f ms\n",
+                        (unsigned long long)i0, (unsigned long long)p, (unsigned long long)ir, a * 1e3, b * 1e3,
+                        d * 1e3, std::chrono::duration<double>(clk::now() - t0).count() * 1e3);
+        }
+    } report{prof, t_dev, t_ev, t_rep, t_rep, passes, items0, items_run, t_all};
     while (!items.empty()) {
         const uint64_t m = items.size();
+        passes++;
+        items_run += m;
+        auto t0 = clk::now();
         uint64_t count0 = 0;
         int rc = xc__cache_count_raw(c->cache, &count0);
         if (rc) return rc;
@@ -362,6 +378,8 @@ int encode(C *c, std::vector<CItem> items, uint8_t *out, const uint64_t *out_off
                                         ocap.data(), olen.data(), start.data(), cand.data(), fl.data(), rbase.data(),
                                         rcand.data(), ccnt.data(), coll.data());
         if (rc) return rc;
+        t_dev += std::chrono::duration<double>(clk::now() - t0).count();
+        t0 = clk::now();
         // the batch's cache events, item by item in the reference's order
         std::vector<std::vector<EncEvent>> ev(m);
         std::vector<const uint8_t *> payloads;
@@ -452,8 +470,22 @@ int encode(C *c, std::vector<CItem> items, uint8_t *out, const uint64_t *out_off
                 for (const EncEvent &e : v) hs.push_back(e.hash);
             if ((rc = c->begin_pass(hs, count0))) return rc;
         }
-        // replay; stop at the first change a later event depends on
+        t_ev += std::chrono::duration<double>(clk::now() - t0).count();
+        t0 = clk::now();
+        // replay; stop at the first change a later event depends on.  last[h]: the pass's last
+        // event (in order) of hash h, so that a change is checked against the later events in the
+        // time of its own hashes (a scan of them all after every change was quadratic: COSS)
         if ((rc = c->unmirrorable())) return rc;
+        std::unordered_map<uint64_t, uint64_t> last;
+        {
+            uint64_t n = 0;
+            for (const auto &v : ev) n += v.size();
+            last.reserve(n);
+            uint64_t gi = 0;
+            for (const auto &v : ev)
+                for (const EncEvent &e : v) last[e.hash] = gi++;
+        }
+        uint64_t gbase = 0;  // the global index of item k's first event
         uint64_t entered = 0;
         bool redo = false;
         std::vector<CItem> next;
@@ -480,10 +512,14 @@ int encode(C *c, std::vector<CItem> items, uint8_t *out, const uint64_t *out_off
                 // after this event may differ
                 bool dep = !ch.added.empty() || ch.new_lm;
                 if (!dep) {
-                    const Watch w(ch);
-                    for (uint64_t k2 = k; k2 < m && !dep; k2++)
-                        for (size_t e2 = (k2 == k ? e + 1 : 0); e2 < ev[k2].size() && !dep; e2++)
-                            dep = w.has(ev[k2][e2].hash);
+                    const uint64_t cur = gbase + e;
+                    for (uint64_t h : ch.removed) {
+                        const auto it = last.find(h);
+                        if (it != last.end() && it->second > cur) {
+                            dep = true;
+                            break;
+                        }
+                    }
                 }
                 if (!dep) {
                     held.push_back(std::move(ch));
@@ -532,6 +568,7 @@ int encode(C *c, std::vector<CItem> items, uint8_t *out, const uint64_t *out_off
                 redo = true;
                 break;
             }
+            gbase += ev[k].size();
             if (!redo) {  // item k is final
                 c->st.count_misses(enc_misses(std::max<uint64_t>(SEG - 1, it.start), it.len, ev[k], ev[k].size()));
                 if (out_len[it.buf] + olen[k] > out_cap[it.buf])
@@ -545,6 +582,7 @@ int encode(C *c, std::vector<CItem> items, uint8_t *out, const uint64_t *out_off
         for (const Change &h : held)
             if ((rc = mirror(c, h))) return rc;
         if ((rc = c->end_pass())) return rc;
+        t_rep += std::chrono::duration<double>(clk::now() - t0).count();
         items.swap(next);
     }
     return XC_OK;
@@ -637,6 +675,28 @@ int decode(C *c, const uint8_t *in, const uint64_t *in_off, const uint64_t *in_l
             if ((rc = c->begin_pass(hs, count0))) return rc;
         }
         if ((rc = c->unmirrorable())) return rc;
+        // last[h]: the pass's last token of hash h in order (a stream's unknown REF after its tokens):
+        // a change is checked against the later ones in the time of its own hashes
+        std::unordered_map<uint64_t, uint64_t> last;
+        std::vector<uint64_t> gbase(m + 1, 0);
+        {
+            uint64_t gi = 0;
+            for (uint64_t k = 0; k < m; k++) {
+                gbase[k] = gi;
+                for (const DEv &e : ev[k]) last[e.hash] = gi++;
+                if (hu[k]) last[unk[k]] = gi;
+                gi++;
+            }
+            gbase[m] = gi;
+        }
+        auto later = [&](const Change &ch, uint64_t cur) {
+            for (const auto *v : {&ch.added, &ch.removed})
+                for (uint64_t h : *v) {
+                    const auto it = last.find(h);
+                    if (it != last.end() && it->second > cur) return true;
+                }
+            return false;
+        };
         uint64_t entered = 0;
         bool redo = false;
         std::vector<Item> next;
@@ -658,13 +718,7 @@ int decode(C *c, const uint8_t *in, const uint64_t *in_off, const uint64_t *in_l
                 if ((rc = settle(c, t, ch))) return rc;
                 if (!ch.any() && !ch.new_lm) continue;
                 // later tokens, and the unknown REF a later stream stopped on, that saw the change
-                const Watch w(ch);
-                bool dep = ch.new_lm;
-                for (uint64_t k2 = k; k2 < m && !dep; k2++) {
-                    for (size_t e2 = (k2 == k ? e + 1 : 0); e2 < ev[k2].size() && !dep; e2++)
-                        dep = w.has(ev[k2][e2].hash);
-                    if (hu[k2] && w.has(unk[k2])) dep = true;
-                }
+                const bool dep = ch.new_lm || later(ch, gbase[k] + e);
                 if (!dep) {
                     held.push_back(std::move(ch));
                     continue;
@@ -695,12 +749,7 @@ int decode(C *c, const uint8_t *in, const uint64_t *in_off, const uint64_t *in_l
                     Change ch;
                     if ((rc = settle(c, t, ch))) return rc;
                     if (ch.any() || ch.new_lm) {
-                        const Watch w(ch);
-                        bool dep = ch.new_lm;
-                        for (uint64_t k2 = k + 1; k2 < m && !dep; k2++) {
-                            for (size_t e2 = 0; e2 < ev[k2].size() && !dep; e2++) dep = w.has(ev[k2][e2].hash);
-                            if (hu[k2] && w.has(unk[k2])) dep = true;
-                        }
+                        const bool dep = ch.new_lm || later(ch, gbase[k] + ev[k].size());
                         if (!dep) {
                             held.push_back(std::move(ch));
                         } else {  // stream k is done; the later ones run again
