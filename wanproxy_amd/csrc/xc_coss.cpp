@@ -150,7 +150,7 @@ public:
     const uint8_t *lookup(uint64_t h, Touch *t)
     {
         lookups_++;
-        for (int i = 0; i < WINDOW; i++)  // find_recent (xcodec_cache.h:137-147): the first match
+        for (int i = 0; i < (wcnt_[wbucket(h)] ? WINDOW : 0); i++)  // find_recent (xcodec_cache.h:137-147)
             if (win_[i].hash == h) {
                 if (win_[i].data) {
                     found_1_++;
@@ -179,7 +179,7 @@ public:
             t->hs.push_back(h);
             t->hs.push_back(win_[cursor_].hash);
         }
-        win_[cursor_].hash = h;
+        wset(cursor_, h);
         win_[cursor_].data = d;
         cursor_ = (cursor_ + 1) & (WINDOW - 1);
         found_2_++;
@@ -195,7 +195,7 @@ public:
     // and the stamp of r's last full store -- equal ids have equal bytes.
     int peek(uint64_t h, const uint8_t **p, Loc *l, uint64_t *id) const
     {
-        for (int i = 0; i < WINDOW; i++)
+        for (int i = 0; i < (wcnt_[wbucket(h)] ? WINDOW : 0); i++)
             if (win_[i].hash == h) {
                 if (win_[i].data) {
                     *p = win_[i].data;
@@ -240,12 +240,28 @@ public:
         return ::pread(fd_, out, SEG, at) == (ssize_t)SEG;
     }
 
+    // A position of a slot loaded from the file and not written since holds the file's bytes of the
+    // version it was loaded at: the file's id, so that loading a stripe (a lookup's, every 512 of its
+    // hashes settled) reads and fingerprints nothing the mirror already took from the file.
+    // p (a lookup's result) points at bytes held in memory (not a lazily loaded slot's)
+    bool in_memory(const uint8_t *p) const
+    {
+        const size_t off = (size_t)(p - (const uint8_t *)&slot_[0]);
+        const int s = (int)(off / sizeof(Stripe));
+        return p < slot_[0].seg[0] || s >= LOADED || resident_[s];
+    }
+
     void slot_id(const uint8_t *p, uint64_t *id) const
     {
         const size_t off = (size_t)(p - (const uint8_t *)&slot_[0]);
         const uint32_t s = (uint32_t)(off / sizeof(Stripe));
         if (p < slot_[0].seg[0] || s >= (uint32_t)LOADED) return;
         const uint32_t pos = (uint32_t)((p - slot_[s].seg[0]) / SEG);
+        if (from_file_[s] && wstamp_[s][pos] < load_stamp_[s]) {
+            id[0] = (1ull << 62) | (slot_[s].h.m.stripe_range << 9) | pos;
+            id[1] = load_fstamp_[s];
+            return;
+        }
         id[0] = 1u + ((uint64_t)s << 9 | pos);
         id[1] = std::max(load_stamp_[s], wstamp_[s][pos]);
     }
@@ -381,6 +397,8 @@ private:
     void initialize_stripe(uint64_t range, int s, Touch *t)
     {  // :230-239
         retarget(s, range, t);
+        load_stamp_[s] = ++stamp_;
+        from_file_[s] = false;
         std::memset(&slot_[s].h, 0, sizeof(Header));
         Meta &m = slot_[s].h.m;
         m.signature = SIGNATURE;
@@ -401,8 +419,11 @@ private:
             retarget(s, range, t);
             const size_t n = full ? sizeof(Stripe) : sizeof(Header);
             load_stamp_[s] = ++stamp_;  // (the slot's bytes are another stripe's now)
+            from_file_[s] = false;
             if (::pread(fd_, &slot_[s], n, (off_t)pos) == (ssize_t)n) {
                 resident_[s] = full;
+                from_file_[s] = range < limit_;
+                load_fstamp_[s] = range < limit_ ? fstamp_[range] : 0;
                 slot_[s].h.m.stripe_range = range;
                 slot_[s].h.m.load_uses = 0;
                 slot_[s].h.m.state = 1;
@@ -489,7 +510,7 @@ private:
             if (st.h.flags[i] & 1u) {
                 for (int w = 0; w < WINDOW; w++)  // forget (xcodec_cache.h:150-158)
                     if (win_[w].hash == st.h.hash[i]) {
-                        win_[w].hash = 0;
+                        wset(w, 0);
                         if (t) t->hs.push_back(st.h.hash[i]);
                     }
                 st.h.flags[i] &= ~1u;
@@ -526,6 +547,9 @@ private:
     // versions of the bytes (peek's ids): a counter, the slots' last loads, their positions' last
     // enters, the stripes' last full stores to the file
     uint64_t stamp_ = 0, load_stamp_[LOADED] = {}, wstamp_[LOADED][STRIPE_SEGS] = {};
+    // a slot loaded from the file (its unwritten positions: the file's bytes at load_fstamp_)
+    bool from_file_[LOADED] = {};
+    uint64_t load_fstamp_[LOADED] = {};
     std::vector<uint64_t> fstamp_;
     int active_ = 0;
     std::vector<Meta> dir_;
@@ -536,6 +560,15 @@ private:
         uint64_t hash;
         const uint8_t *data;
     } win_[WINDOW] = {};
+    // window slots per bucket of their hash (peek skips the 64 compares for almost every hash)
+    uint8_t wcnt_[4096] = {WINDOW};
+    static uint32_t wbucket(uint64_t h) { return (uint32_t)(h ^ (h >> 27)) & 4095u; }
+    void wset(int i, uint64_t h)
+    {
+        wcnt_[wbucket(win_[i].hash)]--;
+        win_[i].hash = h;
+        wcnt_[wbucket(h)]++;
+    }
     unsigned cursor_ = 0;
     uint64_t lookups_ = 0, found_1_ = 0, found_2_ = 0;
 };
@@ -566,6 +599,14 @@ struct xc_coss {
         seen.erase(h);
         if (inpass.insert(h).second) {
             known[h] = replay::fingerprint(seg);
+            // where the store's lookup finds these bytes now (the settle after the enter then reads
+            // and fingerprints nothing)
+            const uint8_t *p = nullptr;
+            replay::Loc l{0, 0};
+            uint64_t id[2] = {0, 0};
+            if (st.peek(h, &p, &l, id) == replay::FOUND && id[0] && p && st.in_memory(p) &&
+                std::memcmp(p, seg, replay::SEG) == 0)
+                seen[h] = {id[0], id[1]};
             return;
         }
         uint8_t b[replay::SEG];

@@ -97,14 +97,34 @@ inline uint64_t fingerprint(const uint8_t *p)
 // The hashes an operation touched, looked up again without side effects: those the device holds
 // and a lookup no longer finds, and those a lookup finds that the device lacks or holds with other
 // bytes, go into ch (and `known` follows).
+struct SettleStats {  // (XC_REPLAY_PROF)
+    uint64_t calls = 0, cand = 0, same = 0, reads = 0, copies = 0, ranges = 0;
+};
+inline SettleStats g_settle;
+
 template <class C>
 int settle(C *c, const Touch &t, Change &ch)
 {
+    // the touched hashes and window entries (few: sorted, deduplicated), then the owners of the
+    // touched ranges (each hash owns one place: no duplicates among them; the COSS replay settles
+    // ~a million per batch, whose sort dominated)
     std::vector<uint64_t> cand(t.hs);
-    for (uint64_t r : t.ranges) c->st.owners(r, cand);
     for (int s : t.slots) c->st.window_in_slot(s, cand);
     std::sort(cand.begin(), cand.end());
     cand.erase(std::unique(cand.begin(), cand.end()), cand.end());
+    if (!t.ranges.empty()) {
+        std::vector<uint64_t> rs(t.ranges);
+        std::sort(rs.begin(), rs.end());
+        rs.erase(std::unique(rs.begin(), rs.end()), rs.end());
+        const size_t n0 = cand.size();
+        std::vector<uint64_t> own;
+        for (uint64_t r : rs) c->st.owners(r, own);
+        for (uint64_t h : own)
+            if (!std::binary_search(cand.begin(), cand.begin() + (ptrdiff_t)n0, h)) cand.push_back(h);
+    }
+    g_settle.calls++;
+    g_settle.cand += cand.size();
+    g_settle.ranges += t.ranges.size();
     uint8_t buf[SEG];
     for (uint64_t h : cand) {
         if (!h) continue;
@@ -116,11 +136,16 @@ int settle(C *c, const Touch &t, Change &ch)
         else c->load_miss.erase(h);
         // the same bytes as when the mirror last took this hash's (no read, no fingerprint): the
         // common case after a stripe load, whose 1024 hashes are all looked at
-        if ((r == FOUND || r == IN_FILE) && id[0] && c->same_bytes(h, id)) continue;
+        if ((r == FOUND || r == IN_FILE) && id[0] && c->same_bytes(h, id)) {
+            g_settle.same++;
+            continue;
+        }
         if (r == IN_FILE) {
+            g_settle.reads++;
             if (!c->st.read_segment(l, buf)) return xc__set_error(XC_EDEVICE, "COSS: cannot read the cache file");
             p = buf;
         } else if (r == FOUND) {  // (a slot whose data stayed in the file: its bytes from there)
+            g_settle.copies++;
             if (!c->st.copy_bytes(p, buf)) return xc__set_error(XC_EDEVICE, "COSS: cannot read the cache file");
             p = buf;
         }
@@ -329,7 +354,8 @@ int encode(C *c, std::vector<CItem> items, uint8_t *out, const uint64_t *out_off
     // (XC_REPLAY_PROF=1: passes, their items and the time of each phase, to stderr)
     static const bool prof = getenv("XC_REPLAY_PROF") && atoi(getenv("XC_REPLAY_PROF"));
     using clk = std::chrono::steady_clock;
-    double t_dev = 0, t_ev = 0, t_rep = 0;
+    double t_dev = 0, t_ev = 0, t_rep = 0, t_set = 0, t_mir = 0;
+    uint64_t n_set = 0, n_mir = 0, n_held = 0;
     uint64_t passes = 0, items0 = items.size(), items_run = 0;
     const auto t_all = clk::now();
     struct Report {
@@ -346,6 +372,22 @@ int encode(C *c, std::vector<CItem> items, uint8_t *out, const uint64_t *out_off
                         d * 1e3, std::chrono::duration<double>(clk::now() - t0).count() * 1e3);
         }
     } report{prof, t_dev, t_ev, t_rep, t_rep, passes, items0, items_run, t_all};
+    struct Report2 {
+        bool on;
+        const double &s, &mi;
+        const uint64_t &ns, &nm, &nh;
+        ~Report2()
+        {
+            if (on)
+                fprintf(stderr, "replay store: settle %.1f ms (%llu with changes), mirror %.1f ms (%llu), held %llu; "
+                                "settles %llu, candidates %llu, same %llu, reads %llu, copies %llu, ranges %llu\n",
+                        s * 1e3, (unsigned long long)ns, mi * 1e3, (unsigned long long)nm, (unsigned long long)nh,
+                        (unsigned long long)g_settle.calls, (unsigned long long)g_settle.cand,
+                        (unsigned long long)g_settle.same, (unsigned long long)g_settle.reads,
+                        (unsigned long long)g_settle.copies, (unsigned long long)g_settle.ranges);
+            g_settle = SettleStats{};
+        }
+    } report2{prof, t_set, t_mir, n_set, n_mir, n_held};
     while (!items.empty()) {
         const uint64_t m = items.size();
         passes++;
@@ -506,8 +548,11 @@ int encode(C *c, std::vector<CItem> items, uint8_t *out, const uint64_t *out_off
                     return xc__set_error(XC_EDEVICE, "cache replay: a device hit the store does not find");
                 }
                 Change ch;
+                const auto ts = clk::now();
                 if ((rc = settle(c, t, ch))) return rc;
+                if (prof) t_set += std::chrono::duration<double>(clk::now() - ts).count();
                 if (!ch.any() && !ch.new_lm) continue;
+                n_set++;
                 // a segment found now that was not, or a miss that now has side effects: any lookup
                 // after this event may differ
                 bool dep = !ch.added.empty() || ch.new_lm;
@@ -523,6 +568,7 @@ int encode(C *c, std::vector<CItem> items, uint8_t *out, const uint64_t *out_off
                 }
                 if (!dep) {
                     held.push_back(std::move(ch));
+                    n_held++;
                     continue;
                 }
                 // the lookups up to this event (its own, unless a declaration: the lookup at the
@@ -579,8 +625,13 @@ int encode(C *c, std::vector<CItem> items, uint8_t *out, const uint64_t *out_off
                 res_cand[it.buf] = rcand[k] >= 0 ? (int64_t)it.off + rcand[k] : -1;
             }
         }
-        for (const Change &h : held)
-            if ((rc = mirror(c, h))) return rc;
+        {
+            const auto tm = clk::now();
+            for (const Change &h : held)
+                if ((rc = mirror(c, h))) return rc;
+            n_mir += held.size();
+            t_mir += std::chrono::duration<double>(clk::now() - tm).count();
+        }
         if ((rc = c->end_pass())) return rc;
         t_rep += std::chrono::duration<double>(clk::now() - t0).count();
         items.swap(next);
