@@ -1471,6 +1471,7 @@ __device__ __forceinline__ uint64_t group_anchors(const PlanDev &P, uint32_t g, 
         const uint32_t total = readlane(incl, 63);
         uint32_t cp = NONE;  // the previous list entry's offset and fingerprint (uniform)
         uint64_t cfp = 0;
+        uint32_t fb = 0;  // the block's first anchor offset (uniform)
         for (uint32_t b0 = 0; b0 < total; b0 += 64u) {
             if (b0 % ANC_LIST == 0u) {  // the list's next pass: entries [b0, b0 + ANC_LIST)
                 if (b0) wave_sync();    // (the last pass's readers are done)
@@ -1497,16 +1498,7 @@ __device__ __forceinline__ uint64_t group_anchors(const PlanDev &P, uint32_t g, 
             const uint64_t pfp = ((uint64_t)fh << 32) | fl;
             // (a run does not continue across 64 entries: a chunk's first entry is a head)
             const bool cont = live && l != 0u && (p & 31u) != 0u && pp + 1u == p && pfp == fp;
-            {
-                const uint32_t gp = i * XC_SEG + p, prv = l == 0u ? lastp : i * XC_SEG + pp;
-                for (uint64_t gm = ballot(live && prv != NONE && gp - prv >= XC_SEG - 62u); gm; gm &= gm - 1) {
-                    const int f = __ffsll((unsigned long long)gm) - 1;
-                    const uint32_t x = readlane(prv, f), y = readlane(gp, f);
-                    if (l == 0 && ngap < AGAP_CAP) P.agap[g * AGAP_CAP + ngap] = make_uint2(x, y);
-                    ngap++;
-                }
-                if (firstp == NONE) firstp = i * XC_SEG + readlane(p, 0);
-            }
+            if (b0 == 0u) fb = readlane(p, 0);
             const uint64_t heads = ballot(live && !cont);
             const uint64_t above = heads & (l == 63u ? 0ull : ~0ull << (l + 1u));
             const uint32_t end = above ? b0 + (uint32_t)__builtin_ctzll(above) : min(total, b0 + 64u);
@@ -1519,6 +1511,24 @@ __device__ __forceinline__ uint64_t group_anchors(const PlanDev &P, uint32_t g, 
             const uint32_t last = min(total - b0, 64u) - 1u;
             cp = readlane(p, (int)last);
             cfp = readlane64(fp, (int)last);
+        }
+        if (total) {  // the group's anchor record (k_aprop's gap windows): anchors >= 1986 apart
+            const uint32_t gf = i * XC_SEG + fb;
+            if (firstp == NONE) firstp = gf;
+            if (lastp != NONE && gf - lastp >= XC_SEG - 62u) {
+                if (l == 0 && ngap < AGAP_CAP) P.agap[g * AGAP_CAP + ngap] = make_uint2(lastp, gf);
+                ngap++;
+            }
+            if (cp - fb >= XC_SEG - 62u) {  // (rare: <= 62 anchors, one list pass, still in LDS)
+                const uint32_t p = l < total ? list[l] : 0u;
+                const uint32_t pp = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * ((l + 63u) & 63u)), (int)p);
+                for (uint64_t gm = ballot(l > 0u && l < total && p - pp >= XC_SEG - 62u); gm; gm &= gm - 1) {
+                    const int f = __ffsll((unsigned long long)gm) - 1;
+                    const uint32_t x = i * XC_SEG + readlane(pp, f), y = i * XC_SEG + readlane(p, f);
+                    if (l == 0 && ngap < AGAP_CAP) P.agap[g * AGAP_CAP + ngap] = make_uint2(x, y);
+                    ngap++;
+                }
+            }
             lastp = i * XC_SEG + cp;
         }
         if (i < n) {  // the block's anchor: its last one at offset >= 63 (none: block_predict and
