@@ -2365,7 +2365,7 @@ __global__ __launch_bounds__(256) void k_hits(PlanDev P, uint64_t *out)
 {
     const uint32_t b = blockIdx.x * 4u + (threadIdx.x >> 6), l = lane_id();
     if (b >= P.nb) return;
-    uint64_t *o = out + P.tok_base[b] + (uint64_t)b * (COLL_CAP + 1u);
+    uint64_t *o = out + P.hit_base[b];  // (room for every REF, len / 2048, and COLL_CAP collisions)
     const uint32_t tb = P.tok_base[b], n = min(P.tok_cnt[b], P.tok_base[b + 1] - tb), cc = P.coll_cnt[b];
     const uint32_t nc = min(cc, COLL_CAP);
     if (nc == 0u) {
@@ -2400,11 +2400,11 @@ __global__ __launch_bounds__(256) void k_hits(PlanDev P, uint64_t *out)
 
 // k_hits' output (device) into pinned host memory, only the words each buffer filled: one wave per
 // buffer, a few workgroups (the writes cross PCIe; the kernel runs beside the next run).
-__global__ void k_hits_out(const uint64_t *stage, uint64_t *host, const uint32_t *tok_base, uint32_t nb)
+__global__ void k_hits_out(const uint64_t *stage, uint64_t *host, const uint32_t *hit_base, uint32_t nb)
 {
     const uint32_t waves = gridDim.x * (blockDim.x >> 6);
     for (uint32_t b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); b < nb; b += waves) {
-        const uint64_t off = tok_base[b] + (uint64_t)b * (COLL_CAP + 1u);
+        const uint64_t off = hit_base[b];
         const uint32_t n = 1u + (uint32_t)(stage[off] & 0xFFFFFFFFu);
         for (uint32_t i = lane_id(); i < n; i += 64u) host[off + i] = stage[off + i];
     }

@@ -98,6 +98,7 @@ struct PlanDev {
     uint2 *undo;               // [seg_cap] (full slot, lo slot) of every enter()
     DevSet dset;
     const uint32_t *tok_base;  // [nb + 1]
+    const uint32_t *hit_base;  // [nb + 1] k_hits' records: buffer b's at hit_base[b], len / 2048 + 1 + COLL_CAP + 1 words
     uint32_t *tok_cnt;
     uint32_t *tok_lb, *tok_le, *tok_seg, *tok_op, *tok_dpos;
     uint32_t *tok_known;       // EXTRACT hash known from a resolved event (no rehash needed)
@@ -335,7 +336,7 @@ __global__ void k_enter_bulk(PlanDev P, const uint64_t *h, const uint8_t *segs, 
 __global__ void k_kill(DevSet cache, const uint64_t *h, uint32_t n);
 __global__ void k_find(DevSet cache, const uint64_t *h, uint64_t *val, uint32_t n);
 __global__ void k_hits(PlanDev P, uint64_t *out);
-__global__ void k_hits_out(const uint64_t *stage, uint64_t *host, const uint32_t *tok_base, uint32_t nb);
+__global__ void k_hits_out(const uint64_t *stage, uint64_t *host, const uint32_t *hit_base, uint32_t nb);
 __global__ void k_setval(DevSet cache, uint64_t h, uint64_t val);
 __global__ void k_lookup_one(PlanDev P, uint64_t h, uint8_t *out, uint32_t *found);
 __global__ void k_selftest(uint32_t *err);

@@ -395,16 +395,16 @@ struct xc_cache {
     // while the next run works (its wait) or before the next operation whose answer depends on the
     // window (cache_settle); a restore drops them.  Two slots: the next run packs into the other.
     struct HitSlot {
-        uint64_t *d = nullptr;   // device: per buffer at tok_base[b] + b * (COLL_CAP + 1), count first
+        uint64_t *d = nullptr;   // device: buffer b's record at rec_base[b] (the plan's hit_base), count first
         uint64_t *h = nullptr;   // pinned host copy (same layout), hd its device address
         uint64_t *hd = nullptr;
-        uint32_t *dtb = nullptr;  // device copy of the run's tok_base (the copy outlives the plan)
+        uint32_t *dtb = nullptr;  // device copy of the run's hit_base (the copy outlives the plan)
         size_t cap = 0, tb_cap = 0;
         hipEvent_t ev = nullptr;  // the copy into h is complete
-        std::vector<uint32_t> tok_base;
+        std::vector<uint32_t> rec_base;
         uint32_t nb = 0;
         uint32_t next_b = 0;  // replay progress: the first buffer not replayed yet
-        uint64_t serial = 0;  // the plan whose layout dtb / tok_base hold
+        uint64_t serial = 0;  // the plan whose layout dtb / rec_base hold
     } hl[2];
     std::deque<int> hl_fifo;  // slots whose hits are not replayed yet, oldest first
     int hl_next = 0;
@@ -1329,6 +1329,8 @@ struct xc_plan {
     uint4 *d_coll = nullptr;         // collision records of every buffer (COLL_CAP each)
     uint32_t *d_coll_cnt = nullptr;
     std::vector<uint32_t> tok_base;  // host copy [nb + 1]
+    std::vector<uint32_t> hit_base;  // host copy [nb + 1] (k_hits' layout)
+    uint32_t *d_hit_base = nullptr;
     int64_t count0 = -1;             // the cache's count before a run that may enter a hash twice
     uint64_t max_new = 0;            // most segments a run can enter (sum of len / 2048 + 1)
     // anchor index: xc_plan_set_scan's mode; this run hashes anchors (anc_run),
@@ -1456,7 +1458,8 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
         }
     }
     const uint32_t chunk_len = p->chunk_len;
-    std::vector<uint32_t> blen(nbuf), chunk0(nbuf + 1), tok_base(nbuf + 1), blk_base(nbuf + 1);
+    std::vector<uint32_t> blen(nbuf), chunk0(nbuf + 1), tok_base(nbuf + 1), blk_base(nbuf + 1), hit_base(nbuf + 1);
+    uint64_t hits = 0;
     uint64_t nblk = 0;
     std::vector<uint2> chunks;
     std::vector<uint4> descs;
@@ -1482,6 +1485,8 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
             }
         p->max_decl = std::max<uint32_t>(p->max_decl, (uint32_t)(n / XC_SEG) + 2u);
         tok_base[i] = (uint32_t)toks;
+        hit_base[i] = (uint32_t)hits;
+        hits += n / XC_SEG + 1 + COLL_CAP + 1;
         blk_base[i] = (uint32_t)nblk;
         nblk += n / XC_SEG;
         toks += 2 * (n / XC_SEG) + 3;
@@ -1501,6 +1506,9 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     p->chunk0 = chunk0;
     tok_base[nbuf] = (uint32_t)toks;
     p->tok_base = tok_base;
+    if (hits > 0xFFFFFFF0ull) return fail(XC_EINVAL, "batch too large");
+    hit_base[nbuf] = (uint32_t)hits;
+    p->hit_base = hit_base;
     p->chunk_bytes.assign(chunks.size() + 1, 0);
     for (size_t k = 0; k < chunks.size(); k++) {
         uint64_t n = lengths[chunks[k].x];
@@ -1516,6 +1524,7 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     HIPCHK(dmalloc(&p->d_buf_len, nb1 * 4));
     HIPCHK(dmalloc(&p->d_chunk0, (nbuf + 1) * 4));
     HIPCHK(dmalloc(&p->d_tok_base, (nbuf + 1) * 4));
+    HIPCHK(dmalloc(&p->d_hit_base, (nbuf + 1) * 4));
     HIPCHK(dmalloc(&p->d_chunks, std::max<size_t>(chunks.size(), 1) * sizeof(uint2)));
     HIPCHK(dmalloc(&p->d_desc, std::max<size_t>(chunks.size(), 1) * sizeof(uint4)));
     hipStream_t s = c->ctx->stream;
@@ -1526,6 +1535,7 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
         HIPCHK(hipMemcpyAsync(p->d_tok_base, tok_base.data(), (nbuf + 1) * 4, hipMemcpyHostToDevice, s));
     }
     HIPCHK(hipMemcpyAsync(p->d_chunk0, chunk0.data(), (nbuf + 1) * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(p->d_hit_base, hit_base.data(), (nbuf + 1) * 4, hipMemcpyHostToDevice, s));
     if (!chunks.empty()) {
         HIPCHK(hipMemcpyAsync(p->d_chunks, chunks.data(), chunks.size() * sizeof(uint2), hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(p->d_desc, descs.data(), descs.size() * sizeof(uint4), hipMemcpyHostToDevice, s));
@@ -1546,6 +1556,7 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     P.D = p->D.d;
     P.dset = p->dset.d;
     P.tok_base = p->d_tok_base;
+    P.hit_base = p->d_hit_base;
     size_t nt = std::max<uint64_t>(toks, 1);
     HIPCHK(dmalloc(&P.tok_cnt, nb1 * 4));
     HIPCHK(dmalloc(&P.tok_lb, nt * 4));
@@ -1666,12 +1677,12 @@ static int hits_replay_front(xc_cache *c, bool block, bool *done, uint32_t max_b
     if (sl.next_b == 0 && !xc__mem_live(c->mem)) {
         // no hash entered twice: the whole run at once, chunks of it simulated ahead on helper
         // threads (a fraction of a millisecond for a cfg5 batch)
-        xc__mem_hits_run(c->mem, sl.h, sl.tok_base.data(), COLL_CAP + 1u, sl.nb);
-        for (uint32_t b = 0; b < sl.nb; b++) n += sl.h[sl.tok_base[b] + (uint64_t)b * (COLL_CAP + 1u)] & 0xFFFFFFFFu;
+        xc__mem_hits_run(c->mem, sl.h, sl.rec_base.data(), 0u, sl.nb);
+        for (uint32_t b = 0; b < sl.nb; b++) n += sl.h[sl.rec_base[b]] & 0xFFFFFFFFu;
         end = sl.next_b = sl.nb;
     }
     for (uint32_t b = sl.next_b; b < end; b++) {
-        const uint64_t *r = sl.h + sl.tok_base[b] + (uint64_t)b * (COLL_CAP + 1u);
+        const uint64_t *r = sl.h + sl.rec_base[b];
         const uint64_t k = r[0] & 0xFFFFFFFFu;
         xc__mem_hits(c->mem, r + 1, k, (r[0] >> 63) ? 0 : 1);
         n += k;
@@ -1717,7 +1728,7 @@ static int hits_enqueue(xc_plan *p)
         HIPCHK(hipEventCreateWithFlags(&c->hl_packed, hipEventDisableTiming));
     }
     if (!sl.ev) HIPCHK(hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
-    const size_t words = p->tok_base[p->nb] + (size_t)p->nb * (COLL_CAP + 1u);
+    const size_t words = p->hit_base[p->nb];
     if (sl.cap < words || sl.tb_cap < (size_t)p->nb + 1) {
         HIPCHK(hipEventSynchronize(sl.ev));  // (a dropped slot's copy may still run)
         dfree(sl.d);
@@ -1739,9 +1750,9 @@ static int hits_enqueue(xc_plan *p)
         sl.tb_cap = tbc;
     }
     HIPCHK(hipStreamWaitEvent(m, sl.ev, 0));  // the slot's previous copy has read d
-    if (sl.serial != p->serial) {  // (the layout of another plan: its tok_base)
-        HIPCHK(hipMemcpyAsync(sl.dtb, p->d_tok_base, ((size_t)p->nb + 1) * 4, hipMemcpyDeviceToDevice, m));
-        sl.tok_base = p->tok_base;
+    if (sl.serial != p->serial) {  // (the layout of another plan: its hit_base)
+        HIPCHK(hipMemcpyAsync(sl.dtb, p->d_hit_base, ((size_t)p->nb + 1) * 4, hipMemcpyDeviceToDevice, m));
+        sl.rec_base = p->hit_base;
         sl.serial = p->serial;
     }
     hipLaunchKernelGGL(k_hits, dim3((p->nb + 3) / 4), dim3(256), 0, m, p->P, sl.d);
@@ -1857,6 +1868,7 @@ extern "C" int xc_plan_destroy(xc_plan *p)
     dfree(p->d_buf_len);
     dfree(p->d_chunk0);
     dfree(p->d_tok_base);
+    dfree(p->d_hit_base);
     dfree(p->d_chunks);
     dfree(p->d_desc);
     dfree(p->P.tok_cnt);
@@ -2819,7 +2831,9 @@ static int encode_finish(xc_plan *p)
         }
         // its lookup hits, for the recent window (none: no REF, no collision recorded, no tail
         // check behind the run that could record one)
-        if ((ctl[CTL_NREF] || ctl[CTL_COLLS] || p->anc_any) && (rc = hits_enqueue(p))) return rc;
+        // (XC_NO_HITS=1: none at all, a timing diagnostic only: the window model is then wrong)
+        static const bool no_hits = getenv("XC_NO_HITS") && atoi(getenv("XC_NO_HITS"));
+        if (!no_hits && (ctl[CTL_NREF] || ctl[CTL_COLLS] || p->anc_any) && (rc = hits_enqueue(p))) return rc;
     }
     return XC_OK;
 }
