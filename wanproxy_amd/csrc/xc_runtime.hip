@@ -407,6 +407,10 @@ struct xc_cache {
         uint64_t serial = 0;  // the plan whose layout dtb / rec_base hold
     } hl[2];
     std::deque<int> hl_fifo;  // slots whose hits are not replayed yet, oldest first
+    // a finished run whose hits are not packed yet: packed (k_hits, its copy) at the next operation
+    // on the cache, before anything can overwrite its token arrays; a restore drops it unpacked
+    // (the bench's restore-per-step headline then pays nothing for the window)
+    xc_plan *hl_pend = nullptr;
     int hl_next = 0;
     hipStream_t hl_stream = nullptr;
     hipEvent_t hl_packed = nullptr;
@@ -426,6 +430,7 @@ struct xc_cache {
 };
 
 static int cache_settle(xc_cache *c);
+static int hits_flush(xc_cache *c);
 
 // A run submitted on the cache and not finished (xc_encode_submit without poll/wait): every other
 // operation on the cache would read a partial count, or move the arrays that run's kernels (and
@@ -962,6 +967,7 @@ static int cache_restore_async(xc_cache *c, uint32_t cur_count)
 static int mem_restore(xc_cache *c)
 {
     c->hl_fifo.clear();
+    c->hl_pend = nullptr;
     c->pend_dec = nullptr;
     return c->mem && c->mem_snap ? xc__mem_restore(c->mem, c->mem_snap) : XC_OK;
 }
@@ -1778,6 +1784,15 @@ static int hits_enqueue(xc_plan *p)
     return XC_OK;
 }
 
+// The pending run's hits packed and on their way to the host (hit log).
+static int hits_flush(xc_cache *c)
+{
+    xc_plan *p = c->hl_pend;
+    if (!p) return XC_OK;
+    c->hl_pend = nullptr;
+    return hits_enqueue(p);
+}
+
 // A pending decode run's hits into the recent window (before anything that comes after it).
 static int cache_settle_dec(xc_cache *c)
 {
@@ -1797,6 +1812,7 @@ static int cache_settle(xc_cache *c)
 {
     if (!c->mem || c->engine) return XC_OK;
     if (int rc = set_dev(c->ctx)) return rc;
+    if (int rc = hits_flush(c)) return rc;
     if (int rc = hits_replay(c, true)) return rc;
     return cache_settle_dec(c);
 }
@@ -1843,6 +1859,7 @@ extern "C" int xc_plan_destroy(xc_plan *p)
 {
     if (!p) return XC_OK;
     hipSetDevice(p->cache->ctx->dev);
+    if (p->cache->hl_pend == p) hits_flush(p->cache);  // (its hits, before its arrays go)
     // pooled memory goes back for reuse at once: nothing may still read or write it
     hipStreamSynchronize(p->cache->ctx->stream);
     if (p->hs) hipStreamSynchronize(p->hs);
@@ -2610,7 +2627,8 @@ static int encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64
     // room for every segment this run can declare (the reference's cache never fills)
     xc_cache *c = p->cache;
     // (a decode's hits go first; earlier encode runs' hits are replayed while this one works)
-    if ((rc = cache_busy(c, p)) || (rc = cache_settle_dec(c)) || (rc = hits_replay(c, false))) return rc;
+    if ((rc = cache_busy(c, p)) || (rc = hits_flush(c)) || (rc = cache_settle_dec(c)) || (rc = hits_replay(c, false)))
+        return rc;
     if (c->mem && !c->engine) {
         // a hash entered twice may answer with other bytes than the device holds: the host paths
         // replay such runs (xc_memcache.cpp)
@@ -2833,7 +2851,10 @@ static int encode_finish(xc_plan *p)
         // check behind the run that could record one)
         // (XC_NO_HITS=1: none at all, a timing diagnostic only: the window model is then wrong)
         static const bool no_hits = getenv("XC_NO_HITS") && atoi(getenv("XC_NO_HITS"));
-        if (!no_hits && (ctl[CTL_NREF] || ctl[CTL_COLLS] || p->anc_any) && (rc = hits_enqueue(p))) return rc;
+        if (!no_hits && (ctl[CTL_NREF] || ctl[CTL_COLLS] || p->anc_any)) {
+            if ((rc = hits_flush(c))) return rc;
+            c->hl_pend = p;  // (packed at the next operation on the cache)
+        }
     }
     return XC_OK;
 }
