@@ -20,6 +20,12 @@
 // host re-runs the batch from that buffer after committing everything before it.
 #include "xc_kernels.h"
 
+// Timing ablations (XC_ABL_BH, XC_ABL_EMIT: the results are wrong) only in builds with
+// -DXC_ABLATIONS=1 (tools/build_variant.sh): production kernels carry no such branch.
+#ifndef XC_ABLATIONS
+#define XC_ABLATIONS 0
+#endif
+
 namespace xc {
 
 // ---------------------------------------------------------------- k_scan ----------------
@@ -639,15 +645,9 @@ __global__ __launch_bounds__(256) void k_aprop(AScanArgs a)
             const uint32_t b = gr[k].x, gpos = gr[k].y * XC_SEG;
             const uint32_t len = P.buf_len[b], ck0 = P.buf_chunk0[b], cblk = P.blk_base[b];
             const uint32_t ap = gpos + (((uint32_t)r[k] >> 5) & 0x3FFFu), nr = ((uint32_t)r[k] & 31u) + 1u;
-            // a record inside predicted REF block kb whose block before is one too (or kb = 0)
-            // proposes nothing to look up: its ends q in [a, a + 1984] are aligned (kb's window), in
-            // kb - 1's shadow (q below kb's end), in kb's (above it), or not a window (q < 2047)
-            if (a.shadow) {
-                const uint32_t kb = ap >> 11;
-                if (cblk + kb < P.blk_base[b + 1] && blk_cached(P.blk_pref[cblk + kb]) &&
-                    (kb == 0u || blk_cached(P.blk_pref[cblk + kb - 1u])))
-                    continue;
-            }
+            // (skipping the probes of a record inside a predicted REF block after another one, whose
+            // proposals all fall in REF shadows, cost more in dependent loads than it saved: cfg5
+            // A/B -1.1 %; the shadow test stays per proposal, below)
 #pragma unroll
             for (int tb = 0; tb < 2; tb++) {
                 const AncSet &S = tb ? P.danc : P.canc;
@@ -1571,8 +1571,9 @@ __global__ __launch_bounds__(256, 4) void k_blockhash(DeclArgs a)
     else wave_load_blocks<BLK_GROUP>(base + (size_t)k0 * XC_SEG, na, w);
     const uint64_t h = block_group_hash<BLK_GROUP>(w);
     uint64_t akey = ANC_NONE;
-    // XC_ABL_BH (timing ablations only: the results are wrong): 2 = no anchors at all
-    const uint32_t abl = (uint32_t)a.nt & ~1u;
+    // XC_ABL_BH (timing ablations only: the results are wrong; in builds with -DXC_ABLATIONS=1):
+    // 2 = no anchors at all
+    const uint32_t abl = XC_ABLATIONS ? (uint32_t)a.nt & ~1u : 0u;
     if (ANC && !(abl & 2u))
         akey = group_anchors(P, g, k0, len, n, na, base, w, tiles[(threadIdx.x >> 6) & (ANC ? 3 : 0)],
                              lists[(threadIdx.x >> 6) & (ANC ? 3 : 0)], abl);
@@ -1825,6 +1826,7 @@ template <uint32_t EMIT_WAVES, bool SLOTS>
 __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
 {
     if (emit_aborted(a)) return;
+    const uint32_t eabl = XC_ABLATIONS ? a.abl : 0u;  // (XC_ABL_EMIT timing ablations: -DXC_ABLATIONS=1 builds)
     __shared__ uint32_t sz[MAX_TOK];
     __shared__ uint32_t ord[MAX_TOK];
     __shared__ uint4 red[EMIT_WAVES];
@@ -1918,7 +1920,7 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
     if (SLOTS && threadIdx.x == 0) P.buf_slot[b] = slot0;  // (the tail check's visibility test)
     // XCodecMemoryCache::enter of this buffer's declarations (SLOTS, or k_insert not split off): the
     // wave with the smallest token group (wave 0 did the prefix), one lane per EXTRACT token
-    if (wave == EMIT_WAVES - 1u && !(a.abl & 4u) && (SLOTS || !a.split_ins)) {
+    if (wave == EMIT_WAVES - 1u && !(eabl & 4u) && (SLOTS || !a.split_ins)) {
         for (uint32_t t0 = 0; t0 < n; t0 += 64u) {
             const uint32_t t = t0 + l;
             const bool ext = t < n && P.tok_op[tb + t] == OP_EXTRACT;
@@ -1960,7 +1962,7 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
             o[1] = (uint8_t)OP_EXTRACT;
         }
         // payloads to the wire and into the slots k_alloc reserved, EMIT_PAY at a time
-        for (uint64_t m = ballot(live && op == OP_EXTRACT && !(a.abl & 8u)); m;) {
+        for (uint64_t m = ballot(live && op == OP_EXTRACT && !(eabl & 8u)); m;) {
             int f[EMIT_PAY];
             uint32_t ii[EMIT_PAY];
             uint8_t *d[EMIT_PAY];
@@ -1978,8 +1980,8 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
 #pragma unroll
             for (int g = 0; g < EMIT_PAY; g++)
                 if (f[g] >= 0) {
-                    uint8_t *sg = ii[g] < P.seg_cap && !(a.abl & 1u) ? seg_at(P.segs, ii[g]) : nullptr;
-                    if (a.abl & 2u) {
+                    uint8_t *sg = ii[g] < P.seg_cap && !(eabl & 1u) ? seg_at(P.segs, ii[g]) : nullptr;
+                    if (eabl & 2u) {
                         if (sg) payload_store_seg(sg, r[g]);
                     } else {
                         payload_store(d[g], sg, r[g]);
