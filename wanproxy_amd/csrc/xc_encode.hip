@@ -524,14 +524,16 @@ __device__ __forceinline__ void gap_note(const PlanDev &P, GapList &G, uint32_t 
     }
 }
 
-// The gaps of group g from k_blockhash's record of it (inf) and of the group after it (inf1, gr1:
-// loaded by the caller ahead of its record work): inside it, after its last anchor (to the buffer's
-// next), and for a buffer's first group the one before its first anchor (positions below 63 are no
-// anchors).  The buffer's length is read only when a gap can reach its end.
-__device__ __forceinline__ void gaps_of_group(const PlanDev &P, const AScanArgs &a, GapList &G, uint32_t g, uint4 inf,
-                                              uint2 gr, uint4 inf1, uint2 gr1, bool hard)
+// The gaps a flagged group (REC_GAP) answers for, from k_blockhash's records: those inside it; the
+// one after its last anchor (to the buffer's next); the one before its first anchor when the group
+// before it (which would answer for it) is not flagged, or the buffer's leading one (positions
+// below 63 are no anchors); a group without an anchor answers for the gap across it when the group
+// before it has anchors and is not flagged.  Each gap is noted once.
+__device__ __forceinline__ void gaps_of_group(const PlanDev &P, const AScanArgs &a, GapList &G, uint32_t g, bool hard)
 {
-    const uint32_t b = gr.x, gpos = gr.y * XC_SEG;
+    const uint4 inf = P.ainfo[g];
+    const uint2 gr = P.blk_grp[g];
+    const uint32_t b = gr.x, gpos = gr.y * XC_SEG, len = P.buf_len[b];
     if (inf.z > AGAP_CAP) {
         atomicOr(&P.ctl[CTL_AFAIL], 8u);
         return;
@@ -540,17 +542,17 @@ __device__ __forceinline__ void gaps_of_group(const PlanDev &P, const AScanArgs 
         const uint2 v = P.agap[g * AGAP_CAP + j];
         gap_note(P, G, b, gpos + v.x + 1u, gpos + v.y - 1u, hard);
     }
-    const bool same = g + 1u < a.g_hi && gr1.x == b;
-    uint32_t next = NONE;  // the buffer's first input anchor after the group (or its length)
-    if (same && inf1.x != NONE) next = gr1.y * XC_SEG + inf1.x;
+    uint32_t next = NONE;  // the buffer's first input anchor after this group (or its length)
     if (inf.y != NONE) {
-        if (next == NONE) next = same ? next_anchor(P, a, g + 2u, b, P.buf_len[b]) : P.buf_len[b];
-        gap_note(P, G, b, gpos + inf.y + 1u, next - 1u, hard);  // (next <= the length)
+        next = next_anchor(P, a, g + 1u, b, len);
+        gap_note(P, G, b, gpos + inf.y + 1u, next - 1u, hard);
     }
+    const uint32_t first = inf.x != NONE ? gpos + inf.x : (next != NONE ? next : next_anchor(P, a, g + 1u, b, len));
     if (gr.y == 0u) {
-        uint32_t first = gpos + inf.x;
-        if (inf.x == NONE) first = next != NONE ? next : next_anchor(P, a, g + 1u, b, P.buf_len[b]);
         gap_note(P, G, b, 63u, first - 1u, hard);
+    } else if (g > a.g_lo) {
+        const uint4 pr = P.ainfo[g - 1u];  // (the same buffer: a buffer's groups are consecutive)
+        if (!pr.w && pr.y != NONE) gap_note(P, G, b, (gr.y - BLK_GROUP) * XC_SEG + pr.y + 1u, first - 1u, hard);
     }
 }
 
@@ -603,6 +605,12 @@ __global__ __launch_bounds__(256) void k_aprop(AScanArgs a)
         cnt[k] = ok ? P.rec_cnt[g0 + k] : 0u;
         gr[k] = ok ? P.blk_grp[g0 + k] : make_uint2(0u, 0u);
     }
+    uint32_t gflag = 0;  // groups whose anchor record k_aprop reads (REC_GAP)
+#pragma unroll
+    for (uint32_t k = 0; k < APROP_GROUPS; k++) {
+        gflag |= (cnt[k] & REC_GAP) ? 1u << k : 0u;
+        cnt[k] &= ~REC_GAP;
+    }
     bool ovf = false;
 #pragma unroll
     for (uint32_t k = 0; k < APROP_GROUPS; k++) ovf |= (cnt[k] & REC_OVF) != 0u;
@@ -613,14 +621,9 @@ __global__ __launch_bounds__(256) void k_aprop(AScanArgs a)
     // the gaps of the workgroup's groups: wave 0 (lane k: group g0 + k) notes them from
     // k_blockhash's record of them, then probes them, before its share of the records (nothing of
     // it stays live across the record loop: the kernel keeps its register count and occupancy)
-    if (threadIdx.x < 64u) {
+    if (gflag && threadIdx.x < 64u) {  // (rare: ~50 flagged groups per 512 MiB sub-batch of random data)
         if (threadIdx.x == 0) G.n = 0;
-        if (threadIdx.x < APROP_GROUPS && g0 + threadIdx.x < a.g_hi) {
-            const uint32_t g = g0 + threadIdx.x;
-            const bool nx = g + 1u < a.g_hi;
-            gaps_of_group(P, a, G, g, P.ainfo[g], P.blk_grp[g], nx ? P.ainfo[g + 1u] : make_uint4(0u, 0u, 0u, 0u),
-                          nx ? P.blk_grp[g + 1u] : make_uint2(NONE, 0u), hard);
-        }
+        if (threadIdx.x < APROP_GROUPS && ((gflag >> threadIdx.x) & 1u)) gaps_of_group(P, a, G, g0 + threadIdx.x, hard);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1539,8 +1542,13 @@ __device__ __forceinline__ uint64_t group_anchors(const PlanDev &P, uint32_t g, 
         wave_sync();  // (the next block's tile and list overwrite these)
     }
     if (l == 0) {
-        P.ainfo[g] = make_uint4(firstp, lastp, ngap, 0u);
-        P.rec_cnt[g] = cnt <= REC_CAP ? cnt : (REC_OVF | REC_CAP);
+        // REC_GAP: a gap (>= 1985 positions without an anchor) may touch this group: one inside it,
+        // none at all, or 993 positions without one at its start or its end (a gap across the
+        // boundary has that on one side at least); k_aprop reads the record of such groups only
+        const uint32_t span = min(len - k0 * XC_SEG, na * XC_SEG);
+        const bool chk = ngap || lastp == NONE || firstp >= 993u || span - 1u - lastp >= 993u;
+        P.ainfo[g] = make_uint4(firstp, lastp, ngap, chk ? 1u : 0u);
+        P.rec_cnt[g] = (cnt <= REC_CAP ? cnt : (REC_OVF | REC_CAP)) | (chk ? REC_GAP : 0u);
         for (uint32_t i = na; i < BLK_GROUP; i++) P.rec_blk[g * BLK_GROUP + i] = min(cnt, REC_CAP);
     }
     return bkey;

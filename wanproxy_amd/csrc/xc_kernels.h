@@ -180,6 +180,7 @@ constexpr uint32_t APROP_GROUPS = XC_APROP_GROUPS;  // k_aprop: block groups per
 constexpr uint32_t BLK_GROUP = 8;    // aligned blocks per k_blockhash group (one wave)
 constexpr uint32_t REC_CAP = 1024;  // anchor records per k_blockhash group (16 KiB; random data: ~256)
 constexpr uint32_t REC_OVF = 0x80000000u;
+constexpr uint32_t REC_GAP = 0x40000000u;  // the group may border a gap (k_aprop looks at its anchor record)
 constexpr uint32_t AGAP_CAP = 4;   // gaps a k_blockhash group records (more: the exact scan)
 constexpr uint32_t PROP_CAP = 64;  // anchor proposals a chunk keeps (more: the exact scan redoes the sub-batch)
 __device__ __forceinline__ uint64_t rec_make(uint64_t fp, uint32_t pos, uint32_t n)
