@@ -529,11 +529,17 @@ __device__ __forceinline__ void gap_note(const PlanDev &P, GapList &G, uint32_t 
 // before it (which would answer for it) is not flagged, or the buffer's leading one (positions
 // below 63 are no anchors); a group without an anchor answers for the gap across it when the group
 // before it has anchors and is not flagged.  Each gap is noted once.
-__device__ __forceinline__ void gaps_of_group(const PlanDev &P, const AScanArgs &a, GapList &G, uint32_t g, bool hard)
+__device__ __forceinline__ void gaps_of_group(const PlanDev &P, const AScanArgs &a, GapList &G, uint32_t g, uint2 gr,
+                                              bool hard)
 {
+    // (every load at once: the group's record, its neighbours', the buffer's length)
+    const uint32_t b = gr.x, gpos = gr.y * XC_SEG;
+    const bool has_prev = gr.y != 0u, has_next = g + 1u < a.g_hi;
     const uint4 inf = P.ainfo[g];
-    const uint2 gr = P.blk_grp[g];
-    const uint32_t b = gr.x, gpos = gr.y * XC_SEG, len = P.buf_len[b];
+    const uint4 pr = has_prev ? P.ainfo[g - 1u] : make_uint4(NONE, NONE, 0u, 1u);
+    const uint4 nx = has_next ? P.ainfo[g + 1u] : make_uint4(NONE, NONE, 0u, 1u);
+    const uint2 nxgr = has_next ? P.blk_grp[g + 1u] : make_uint2(NONE, 0u);
+    const uint32_t len = P.buf_len[b];
     if (inf.z > AGAP_CAP) {
         atomicOr(&P.ctl[CTL_AFAIL], 8u);
         return;
@@ -542,18 +548,13 @@ __device__ __forceinline__ void gaps_of_group(const PlanDev &P, const AScanArgs 
         const uint2 v = P.agap[g * AGAP_CAP + j];
         gap_note(P, G, b, gpos + v.x + 1u, gpos + v.y - 1u, hard);
     }
-    uint32_t next = NONE;  // the buffer's first input anchor after this group (or its length)
-    if (inf.y != NONE) {
-        next = next_anchor(P, a, g + 1u, b, len);
-        gap_note(P, G, b, gpos + inf.y + 1u, next - 1u, hard);
-    }
-    const uint32_t first = inf.x != NONE ? gpos + inf.x : (next != NONE ? next : next_anchor(P, a, g + 1u, b, len));
-    if (gr.y == 0u) {
-        gap_note(P, G, b, 63u, first - 1u, hard);
-    } else if (g > a.g_lo) {
-        const uint4 pr = P.ainfo[g - 1u];  // (the same buffer: a buffer's groups are consecutive)
-        if (!pr.w && pr.y != NONE) gap_note(P, G, b, (gr.y - BLK_GROUP) * XC_SEG + pr.y + 1u, first - 1u, hard);
-    }
+    // the buffer's first input anchor after this group (or its length)
+    uint32_t next = len;
+    if (nxgr.x == b) next = nx.x != NONE ? nxgr.y * XC_SEG + nx.x : next_anchor(P, a, g + 2u, b, len);
+    if (inf.y != NONE) gap_note(P, G, b, gpos + inf.y + 1u, next - 1u, hard);
+    const uint32_t first = inf.x != NONE ? gpos + inf.x : next;
+    if (!has_prev) gap_note(P, G, b, 63u, first - 1u, hard);
+    else if (!pr.w && pr.y != NONE) gap_note(P, G, b, gpos - BLK_GROUP * XC_SEG + pr.y + 1u, first - 1u, hard);
 }
 
 // Wave 0 of k_aprop's workgroup over one gap: lane t takes a stretch of its positions, G(p) and G(p - 32) by two
@@ -623,7 +624,8 @@ __global__ __launch_bounds__(256) void k_aprop(AScanArgs a)
     // it stays live across the record loop: the kernel keeps its register count and occupancy)
     if (gflag && threadIdx.x < 64u) {  // (rare: ~50 flagged groups per 512 MiB sub-batch of random data)
         if (threadIdx.x == 0) G.n = 0;
-        if (threadIdx.x < APROP_GROUPS && ((gflag >> threadIdx.x) & 1u)) gaps_of_group(P, a, G, g0 + threadIdx.x, hard);
+        if (threadIdx.x < APROP_GROUPS && ((gflag >> threadIdx.x) & 1u))
+            gaps_of_group(P, a, G, g0 + threadIdx.x, P.blk_grp[g0 + threadIdx.x], hard);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
