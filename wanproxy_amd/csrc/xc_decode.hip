@@ -11,13 +11,12 @@
 //              false, xcodec_decoder.cc:120-132); absent -> candidate provider, min-merged
 //              by (stream, token) into the batch table
 //   k_dres2    every token against cache + earlier providers: REF data source or unknown
-//              (xcodec_decoder.cc:142-166); later duplicate EXTRACTs compared with the first
-//   k_dstop    per stream: first token that stops the decode, ENTER ordinals
-//   (host)     re-resolve if a provider lies past its own stream's stop (rare)
-//   k_dalloc   cache slots of the ENTER tokens (prefix over streams)
+//              (xcodec_decoder.cc:142-166); later duplicate EXTRACTs compared with the first;
+//              per stream the first token that stops the decode, ENTER ordinals
+//   k_dfin     round consistency (a provider past its own stream's stop: the host re-resolves,
+//              rare), then in its last workgroup the cache slots of the ENTER tokens
 //   k_demit    unescape literals, copy EXTRACT payloads (first-seen ones into their cache
-//              slots too), gather REF segments
-//   k_dcommit  enter the first-seen EXTRACT hashes in the cache
+//              slots too), gather REF segments; enter the first-seen hashes in the cache
 #include <hip/hip_runtime.h>
 #include <sched.h>
 
@@ -47,7 +46,7 @@ struct DecDev {
     uint32_t *s_stop;          // executed tokens per stream (the stop token included: its literal runs)
     uint32_t *s_lim;           // tokens eligible as EXTRACT providers this round
     uint32_t *s_slot;          // first cache slot of the stream's entered segments
-    uint2 *s_cnt;              // executed (REF, EXTRACT) tokens of the stream (k_dalloc sums them)
+    uint2 *s_cnt;              // executed (REF, EXTRACT) tokens of the stream (k_dfin sums them)
     uint8_t *out;
     const uint64_t *out_off;
     const uint64_t *out_cap;
@@ -60,13 +59,17 @@ struct DecDev {
     uint2 *undo;
     DevSet dset;
     uint32_t *ctl;
-    int count;                 // k_dstop: count executed REF / EXTRACT tokens into ctl
-    uint32_t *ctl_host;        // k_dalloc: publish the control words here (mapped host memory)
+    int count;                 // k_dfin: count executed REF / EXTRACT tokens into ctl
+    uint32_t *ctl_host;        // k_dfin: publish the control words here (mapped host memory)
 };
 
-enum : uint32_t { DCTL_FIX = 0, DCTL_ERR = 1, DCTL_NENTER = 2, DCTL_NREF = 3, DCTL_NEXTRACT = 4, DCTL_WORDS = 8 };
-// DCTL_ERR bits: 1 an output capacity is too small (k_demit), 2 the cache is full (k_dalloc),
-// 4 an output may not fit (k_dstop's bound: the words are then final only after k_demit)
+enum : uint32_t {
+    DCTL_FIX = 0, DCTL_ERR = 1, DCTL_NENTER = 2, DCTL_NREF = 3, DCTL_NEXTRACT = 4,
+    DCTL_TICKET = 6,  // k_dfin's finished workgroups (its last one resets it)
+    DCTL_WORDS = 8
+};
+// DCTL_ERR bits: 1 an output capacity is too small (k_demit), 2 the cache is full (k_dfin),
+// 4 an output may not fit (k_dres2's bound: the words are then final only after k_demit)
 constexpr uint32_t DERR_MAYBE_OUT = 4u;
 
 // The control words to the run's mapped host buffer, the last word (unused: the host's sentinel)
@@ -497,10 +500,6 @@ __global__ __launch_bounds__(64) void k_dtok_win(DecDev D, int fill, int first, 
 #define XC_DRES_WAVES 4
 #endif
 constexpr uint32_t DRES_WAVES = XC_DRES_WAVES;
-#ifndef XC_DCOMMIT_WAVES
-#define XC_DCOMMIT_WAVES 4
-#endif
-constexpr uint32_t DCOMMIT_WAVES = XC_DCOMMIT_WAVES;  // k_dcommit: streams (waves) per workgroup
 
 // EXTRACTs against the cache; absent ones become provider candidates in the batch table.
 // HASH (round 0): the payloads' hashes H first (xcodec_hash.h:166-174), kept in t_h.
@@ -611,9 +610,14 @@ __global__ __launch_bounds__(64) void k_dres1(DecDev D)
 }
 
 
-// Provider resolution in (stream, token) order: one wave per stream, one lane per token (every
-// probe of 64 tokens in flight together); an EXTRACT with an earlier provider then takes a
-// wave-wide 2048-byte comparison (rare: the same new segment twice in a batch).
+// Provider resolution in (stream, token) order, and the stream's stop: one wave per stream, one lane
+// per token (every probe of 64 tokens in flight together); an EXTRACT with an earlier provider then
+// takes a wave-wide 2048-byte comparison (rare: the same new segment twice in a batch). The first
+// token that stops the decode (terminal, unknown REF or colliding EXTRACT) ends the walk; the
+// stream's executed token count, status / consumed bytes, and the ordinal of every first-seen
+// EXTRACT (ENTER) among its executed tokens, kept in t_src (unused for ENTER tokens); s_slot[j] =
+// the stream's ENTER count (k_dfin prefixes it). Tokens past the stop are left as they were: no
+// later kernel reads them.
 __global__ __launch_bounds__(64) void k_dres2(DecDev D)
 {
     const uint32_t j = blockIdx.x;
@@ -621,15 +625,22 @@ __global__ __launch_bounds__(64) void k_dres2(DecDev D)
     const uint8_t *s = D.in + D.in_off[j];
     const uint32_t tb = D.tok_base[j], n = D.tok_cnt[j];
     const uint32_t l = lane_id();
-    for (uint32_t t0 = 64u * blockIdx.y; t0 < n; t0 += 64u * gridDim.y) {
+    uint32_t stop = n, nr = 0, ne = 0, nent = 0;
+    uint64_t lit = 0;  // literal bytes of the executed tokens and the stop token (escapes counted twice)
+    for (uint32_t t0 = 0; t0 < n; t0 += 64u) {
         const uint32_t t = t0 + l;
-        const uint32_t op = t < n ? D.t_op[tb + t] : T_END;
+        uint32_t op = T_END, ll = 0;
+        if (t < n) {
+            op = D.t_op[tb + t];
+            ll = D.t_le[tb + t] - D.t_lb[tb + t];
+        }
         const uint64_t self = ((uint64_t)j << 32) | t;
         uint32_t st = 0;
         uint64_t src = 0, pv = 0;
         bool wst = false, wsrc = false, cmp = false;
         if (op == T_EXTRACT) {
-            if (D.t_stat[tb + t] == R_PENDING) {
+            st = D.t_stat[tb + t];  // (round 0's cache probe, or k_dres1's)
+            if (st == R_PENDING) {
                 const uint64_t h = D.t_h[tb + t];
                 uint64_t v;
                 st = R_ENTER;
@@ -664,42 +675,20 @@ __global__ __launch_bounds__(64) void k_dres2(DecDev D)
             const bool eq = wave_equal2048(s + D.t_le[tb + tf] + 2u, pp);
             if ((int)l == f) st = eq ? R_OKPROV : R_COLL;
         }
-        if (wst) D.t_stat[tb + t] = st;
-        if (wsrc) D.t_src[tb + t] = src;
-    }
-}
-
-// Per stream (one wave each, 64 tokens per step): executed token count, the decode's status /
-// consumed bytes, and the ordinal of every first-seen EXTRACT (ENTER) among the stream's executed
-// tokens, kept in t_src (unused for ENTER tokens); s_slot[j] = the stream's ENTER count (k_dalloc
-// prefixes it).
-__global__ __launch_bounds__(256) void k_dstop(DecDev D)
-{
-    const uint32_t j = blockIdx.x * 4u + (threadIdx.x >> 6), l = lane_id();
-    if (j >= D.ns) return;
-    const uint32_t tb = D.tok_base[j], n = D.tok_cnt[j];
-    uint32_t t = n, nr = 0, ne = 0, nent = 0;
-    uint64_t lit = 0;  // literal bytes of the executed tokens and the stop token (escapes counted twice)
-    for (uint32_t t0 = 0; t0 < n; t0 += 64u) {
-        const uint32_t i = t0 + l;
-        uint32_t op = T_END, st = 0, ll = 0;
-        if (i < n) {
-            op = D.t_op[tb + i];
-            st = D.t_stat[tb + i];
-            ll = D.t_le[tb + i] - D.t_lb[tb + i];
-        }
-        // the first token that stops the decode: terminal, unknown REF or colliding EXTRACT
-        const uint64_t brk = ballot(i < n && ((op != T_EXTRACT && op != T_REF) || st == R_UNKNOWN || st == R_COLL));
+        // the first token of these 64 that stops the decode
+        const uint64_t brk = ballot(t < n && ((op != T_EXTRACT && op != T_REF) || st == R_UNKNOWN || st == R_COLL));
         const uint32_t k = brk ? (uint32_t)__ffsll((unsigned long long)brk) - 1u : 64u;
         lit += wave_sum(l <= k ? ll : 0u);
-        const bool ex = l < k && i < n;
+        const bool ex = l < k && t < n;
         nr += (uint32_t)__popcll(ballot(ex && op == T_REF));
         ne += (uint32_t)__popcll(ballot(ex && op == T_EXTRACT));
         const uint64_t em = ballot(ex && st == R_ENTER);
-        if (ex && st == R_ENTER) D.t_src[tb + i] = nent + mbcnt(em);
+        if (ex && st == R_ENTER) src = nent + mbcnt(em);
         nent += (uint32_t)__popcll(em);
+        if (wst) D.t_stat[tb + t] = st;
+        if (wsrc) D.t_src[tb + t] = src;
         if (brk) {
-            t = t0 + k;
+            stop = t0 + k;
             break;
         }
     }
@@ -707,38 +696,20 @@ __global__ __launch_bounds__(256) void k_dstop(DecDev D)
     // the output is at most the literal bytes plus a segment per executed EXTRACT / REF: when
     // that may exceed the capacity, only k_demit's exact sizes decide (no early publication)
     if (lit + (uint64_t)XC_SEG * (nr + ne) > D.out_cap[j]) atomicOr(&D.ctl[DCTL_ERR], DERR_MAYBE_OUT);
-    // t = stopping token; its literal is output
-    D.s_stop[j] = t + 1u;
+    // stop = the stopping token; its literal is output
+    D.s_stop[j] = stop + 1u;
     D.s_slot[j] = nent;
-    D.s_cnt[j] = make_uint2(nr, ne);  // (one device-wide atomic per stream serializes: k_dalloc sums)
-    const uint32_t op = D.t_op[tb + t], le = D.t_le[tb + t];
+    D.s_cnt[j] = make_uint2(nr, ne);  // (one device-wide atomic per stream serializes: k_dfin sums)
+    const uint32_t op = D.t_op[tb + stop], le = D.t_le[tb + stop];
     int32_t status = 1, hu = 0;
     uint64_t cons = le, unk = 0;
     if (op == T_BADOP) status = 0;
-    else if (op == T_REF) { hu = 1; unk = D.t_h[tb + t]; }              // unknown REF
+    else if (op == T_REF) { hu = 1; unk = D.t_h[tb + stop]; }           // unknown REF
     else if (op == T_EXTRACT) { status = 0; cons = le + 2u; }           // collision
     D.status[j] = status;
     D.consumed[j] = cons;
     D.has_unknown[j] = hu;
     D.unknown[j] = unk;
-}
-
-// Consistency of a resolution round: every provider used by an executed token must itself be
-// executed, and (after round 0) the executed tokens must be exactly the eligible providers.
-__global__ __launch_bounds__(64) void k_dcheck(DecDev D, int round)
-{
-    const uint32_t j = blockIdx.x;
-    if (j >= D.ns) return;
-    const uint32_t tb = D.tok_base[j], ex = D.s_stop[j] - 1u;
-    if (round > 0 && lane_id() == 0 && ex != D.s_lim[j]) atomicOr(&D.ctl[DCTL_FIX], 1u);
-    for (uint32_t t = lane_id(); t < ex; t += 64u) {
-        const uint64_t src = D.t_src[tb + t];
-        const uint32_t st = D.t_stat[tb + t];
-        if ((st == R_OKPROV || st == R_COLL) && (src & SRC_PROV)) {
-            const uint32_t pj = (uint32_t)((src >> 32) & 0x7FFFFFFFu), pt = (uint32_t)src;
-            if (pt + 1u >= D.s_stop[pj]) atomicOr(&D.ctl[DCTL_FIX], 1u);
-        }
-    }
 }
 
 __device__ __forceinline__ void dclear_range(const DecDev &D, uint32_t n_lo, uint32_t n_full, uint32_t i0,
@@ -765,6 +736,7 @@ __global__ void k_dclear(DecDev D, uint32_t n_lo, uint32_t n_full)
         D.ctl[DCTL_FIX] = 0u;
         D.ctl[DCTL_NREF] = 0u;
         D.ctl[DCTL_NEXTRACT] = 0u;
+        D.ctl[DCTL_TICKET] = 0u;
     }
 }
 
@@ -835,6 +807,7 @@ __global__ __launch_bounds__(64 * DEMIT_WAVES) void k_demit(DecDev D)
     const uint32_t tb = D.tok_base[j];
     const uint32_t lim = min(D.tok_cnt[j], D.s_stop[j]);
     if (threadIdx.x == 0) base_off = 0;
+    bool ovf = false;  // (uniform: an output past its capacity ends the writes)
     for (uint32_t t0 = 0; t0 < lim; t0 += DMAX_TOK) {
         const uint32_t nb = min(DMAX_TOK, lim - t0);
         __syncthreads();
@@ -867,7 +840,8 @@ __global__ __launch_bounds__(64 * DEMIT_WAVES) void k_demit(DecDev D)
         __syncthreads();
         if (off[nb] > D.out_cap[j]) {
             if (threadIdx.x == 0) atomicOr(&D.ctl[DCTL_ERR], 1u);
-            return;
+            ovf = true;
+            break;
         }
         // wave w: tokens [w G, (w+1) G) of the block, one per lane
         const uint32_t G = (nb + DEMIT_WAVES - 1u) / DEMIT_WAVES;
@@ -877,7 +851,7 @@ __global__ __launch_bounds__(64 * DEMIT_WAVES) void k_demit(DecDev D)
             const bool live = i < g_end;
             uint32_t lb = 0, le = 0, op = T_END;
             uint64_t from = 0;  // source of the token's 2048 bytes
-            uint64_t seg = 0;   // first-seen EXTRACT: its cache slot (k_dalloc), written here too
+            uint64_t seg = 0;   // first-seen EXTRACT: its cache slot (k_dfin), written here too
             if (live) {
                 lb = D.t_lb[tb + t];
                 le = D.t_le[tb + t];
@@ -922,87 +896,132 @@ __global__ __launch_bounds__(64 * DEMIT_WAVES) void k_demit(DecDev D)
         }
     }
     __syncthreads();
-    if (threadIdx.x == 0) D.out_len[j] = base_off;
-}
-
-// Cache slots of the streams' ENTER tokens: exclusive prefix of the per-stream counts k_dstop
-// left in s_slot, on top of the current segment count (one workgroup).
-__global__ __launch_bounds__(1024) void k_dalloc(DecDev D)
-{
-    if (fix_pending(D)) {  // another resolution round: the host decides it now
-        if (threadIdx.x == 0) dctl_publish(D);
-        return;
-    }
-    __shared__ uint32_t wsum[16];
-    __shared__ uint2 csum[16];
-    __shared__ uint32_t carry;
-    const uint32_t wave = threadIdx.x >> 6, l = lane_id();
-    if (threadIdx.x == 0) carry = *D.seg_count;
-    __syncthreads();
-    const uint32_t start = carry;
-    uint32_t nr = 0, ne = 0;  // executed REF / EXTRACT tokens (decode statistics)
-    for (uint32_t j0 = 0; j0 < D.ns; j0 += 1024u) {
-        const uint32_t j = j0 + threadIdx.x;
-        const uint32_t v = j < D.ns ? D.s_slot[j] : 0u;
-        if (j < D.ns) {
-            const uint2 c = D.s_cnt[j];
-            nr += c.x;
-            ne += c.y;
-        }
-        const uint32_t inc = wave_incl_scan(v);
-        if (l == 63) wsum[wave] = inc;
-        __syncthreads();
-        uint32_t o = carry;
-        for (uint32_t k = 0; k < wave; k++) o += wsum[k];
-        if (j < D.ns) D.s_slot[j] = o + inc - v;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t tot = 0;
-            for (uint32_t k = 0; k < 16; k++) tot += wsum[k];
-            carry += tot;
-        }
-        __syncthreads();
-    }
-    nr = wave_sum(nr);
-    ne = wave_sum(ne);
-    if (l == 0) csum[wave] = make_uint2(nr, ne);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        if (D.count) {
-            uint2 t = make_uint2(0, 0);
-            for (uint32_t k = 0; k < 16; k++) {
-                t.x += csum[k].x;
-                t.y += csum[k].y;
-            }
-            D.ctl[DCTL_NREF] = t.x;
-            D.ctl[DCTL_NEXTRACT] = t.y;
-        }
-        *D.seg_count = carry;
-        D.ctl[DCTL_NENTER] = carry - start;
-        if (carry > D.seg_cap) D.ctl[DCTL_ERR] |= 2u;
-        // final unless an output may overflow (k_demit then sets bit 1): the rest of the run
-        // changes no control word
-        if (!(D.ctl[DCTL_ERR] & DERR_MAYBE_OUT)) dctl_publish(D);
-    }
-}
-
-// XCodecMemoryCache::enter for first-seen EXTRACT payloads (xcodec_decoder.cc:133-135).
-// grid (streams, 8): wave y takes the stream's executed tokens y, y + 8, ...
-__global__ __launch_bounds__(64 * DCOMMIT_WAVES) void k_dcommit(DecDev D)
-{
-    if (fix_pending(D)) return;
-    // one wave per stream (4 per workgroup), one lane per token; k_demit already wrote the
-    // payloads into their slots
-    const uint32_t j = blockIdx.x * DCOMMIT_WAVES + (threadIdx.x >> 6);
-    if (j >= D.ns) return;
-    const uint32_t tb = D.tok_base[j], lim = min(D.tok_cnt[j], D.s_stop[j] - 1u);
-    for (uint32_t t = lane_id(); t < lim; t += 64u) {
+    if (threadIdx.x == 0 && !ovf) D.out_len[j] = base_off;
+    // XCodecMemoryCache::enter for the first-seen EXTRACT payloads (xcodec_decoder.cc:133-135),
+    // whose slots this workgroup filled above; one thread per token
+    const uint32_t clim = min(D.tok_cnt[j], D.s_stop[j] - 1u);
+    for (uint32_t t = threadIdx.x; t < clim; t += 64u * DEMIT_WAVES) {
         if (D.t_stat[tb + t] != R_ENTER) continue;
         const uint32_t idx = D.s_slot[j] + (uint32_t)D.t_src[tb + t];
         if (idx >= D.seg_cap) continue;
         uint32_t s1, s2;
         set_insert(D.cache, D.t_h[tb + t], idx, false, &s1, &s2);
         D.undo[idx] = make_uint2(s1, s2);
+    }
+}
+
+// The end of a resolution round. Its consistency first, one wave per stream: every provider used by
+// an executed token must itself be executed, and (after round 0) the executed tokens must be
+// exactly the eligible providers. Then the last workgroup to finish (a ticket in the control words)
+// takes the cache slots of the streams' ENTER tokens: the exclusive prefix of the per-stream counts
+// k_dres2 left in s_slot, on top of the current segment count, and publishes the control words.
+constexpr uint32_t DFIN_WAVES = 16, DFIN_REG = 8;
+__global__ __launch_bounds__(64 * DFIN_WAVES) void k_dfin(DecDev D, int round)
+{
+    __shared__ uint32_t wsum[DFIN_WAVES];
+    __shared__ uint2 csum[DFIN_WAVES];
+    __shared__ uint32_t last;
+    const uint32_t wave = threadIdx.x >> 6, l = lane_id();
+    {
+        const uint32_t j = blockIdx.x * DFIN_WAVES + wave;
+        if (j < D.ns) {
+            const uint32_t tb = D.tok_base[j], ex = D.s_stop[j] - 1u;
+            if (round > 0 && l == 0 && ex != D.s_lim[j]) atomicOr(&D.ctl[DCTL_FIX], 1u);
+            for (uint32_t t = l; t < ex; t += 64u) {
+                const uint64_t src = D.t_src[tb + t];
+                const uint32_t st = D.t_stat[tb + t];
+                if ((st == R_OKPROV || st == R_COLL) && (src & SRC_PROV)) {
+                    const uint32_t pj = (uint32_t)((src >> 32) & 0x7FFFFFFFu), pt = (uint32_t)src;
+                    if (pt + 1u >= D.s_stop[pj]) atomicOr(&D.ctl[DCTL_FIX], 1u);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();  // (release: this workgroup's FIX)
+        last = atomicAdd(&D.ctl[DCTL_TICKET], 1u) == gridDim.x - 1u;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();  // (acquire: every workgroup's FIX)
+    if (fix_pending(D)) {  // another resolution round: the host decides it now
+        if (threadIdx.x == 0) {
+            D.ctl[DCTL_TICKET] = 0u;
+            dctl_publish(D);
+        }
+        return;
+    }
+    // a contiguous range of streams per thread: its sums, a block prefix, its slots (up to
+    // DFIN_REG streams per thread with every load in flight at once)
+    const uint32_t start = *D.seg_count;
+    const uint32_t per = (D.ns + 64u * DFIN_WAVES - 1u) / (64u * DFIN_WAVES);
+    const uint32_t j0 = min(D.ns, threadIdx.x * per), j1 = min(D.ns, j0 + per);
+    uint32_t sum = 0, nr = 0, ne = 0;  // ENTER tokens; executed REF / EXTRACT tokens (decode statistics)
+    uint32_t v[DFIN_REG];
+    if (per <= DFIN_REG) {
+        uint2 c[DFIN_REG];
+#pragma unroll
+        for (uint32_t k = 0; k < DFIN_REG; k++) {
+            const bool in = j0 + k < j1;
+            v[k] = in ? D.s_slot[j0 + k] : 0u;
+            c[k] = in ? D.s_cnt[j0 + k] : make_uint2(0, 0);
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < DFIN_REG; k++) {
+            sum += v[k];
+            nr += c[k].x;
+            ne += c[k].y;
+        }
+    } else {
+        for (uint32_t j = j0; j < j1; j++) {
+            sum += D.s_slot[j];
+            const uint2 c = D.s_cnt[j];
+            nr += c.x;
+            ne += c.y;
+        }
+    }
+    const uint32_t inc = wave_incl_scan(sum);
+    nr = wave_sum(nr);
+    ne = wave_sum(ne);
+    if (l == 63) wsum[wave] = inc;
+    if (l == 0) csum[wave] = make_uint2(nr, ne);
+    __syncthreads();
+    uint32_t o = start + inc - sum;
+    for (uint32_t k = 0; k < wave; k++) o += wsum[k];
+    if (per <= DFIN_REG) {
+#pragma unroll
+        for (uint32_t k = 0; k < DFIN_REG; k++)
+            if (j0 + k < j1) {
+                D.s_slot[j0 + k] = o;
+                o += v[k];
+            }
+    } else {
+        for (uint32_t j = j0; j < j1; j++) {
+            const uint32_t x = D.s_slot[j];
+            D.s_slot[j] = o;
+            o += x;
+        }
+    }
+    if (threadIdx.x == 0) {
+        uint32_t carry = start;
+        uint2 t = make_uint2(0, 0);
+        for (uint32_t k = 0; k < DFIN_WAVES; k++) {
+            carry += wsum[k];
+            t.x += csum[k].x;
+            t.y += csum[k].y;
+        }
+        if (D.count) {
+            D.ctl[DCTL_NREF] = t.x;
+            D.ctl[DCTL_NEXTRACT] = t.y;
+        }
+        D.ctl[DCTL_TICKET] = 0u;
+        *D.seg_count = carry;
+        D.ctl[DCTL_NENTER] = carry - start;
+        if (carry > D.seg_cap) D.ctl[DCTL_ERR] |= 2u;
+        // final unless an output may overflow (k_demit then sets bit 1): the rest of the run
+        // changes no control word
+        if (!(D.ctl[DCTL_ERR] & DERR_MAYBE_OUT)) dctl_publish(D);
     }
 }
 
@@ -1059,7 +1078,7 @@ struct xc_dplan {
     xc_decode_stats stats{};
     std::vector<void *> owned;
     uint32_t *h_ctl = nullptr;    // pinned copy of the control words (the run's host wait)
-    uint32_t *d_hctl = nullptr;   // its device address (k_dalloc publishes there)
+    uint32_t *d_hctl = nullptr;   // its device address (k_dfin publishes there)
     hipEvent_t ev_ctl = nullptr;
     int completion = XC_COMPLETE_RUN;  // xc_dplan_set_completion
     uint32_t cache_gen = 0;       // the cache arrays D holds (they move when the cache grows)
@@ -1335,16 +1354,12 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
         DHIP(hipGetLastError());
         hipLaunchKernelGGL(k_dres2, dim3(ns), dim3(64), 0, s, D);  // (a wave per stream)
         DHIP(hipGetLastError());
-        hipLaunchKernelGGL(k_dstop, dim3((ns + 3) / 4), dim3(256), 0, s, D);
-        DHIP(hipGetLastError());
-        hipLaunchKernelGGL(k_dcheck, dim3(ns), dim3(64), 0, s, D, r);
-        DHIP(hipGetLastError());
         return XC_OK;
     };
     // output and cache commit: these kernels return at once while DCTL_FIX is set, so round 0
     // and the emit are enqueued together and the host waits once in the common case
     int rc0 = XC_OK;
-    auto emit = [&]() -> int {
+    auto emit = [&](int r) -> int {
         if (!p->h_ctl) {
             if ((rc0 = xc__halloc((void **)&p->h_ctl, DCTL_WORDS * 4))) return rc0;
             void *dp = nullptr;
@@ -1352,19 +1367,17 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
             p->d_hctl = (uint32_t *)dp;
             DHIP(hipEventCreateWithFlags(&p->ev_ctl, hipEventDisableTiming));
         }
-        // stream-ordered completion: k_dalloc publishes the words when they are final (a sentinel
-        // in the last word, cleared last) and the host returns while k_demit / k_dcommit run
+        // stream-ordered completion: k_dfin publishes the words when they are final (a sentinel
+        // in the last word, cleared last) and the host returns while k_demit runs
         const bool pub = p->completion == XC_COMPLETE_STREAM;
         DecDev Da = D;
         if (pub) {
             p->h_ctl[DCTL_WORDS - 1] = 0xFFFFFFFFu;
             Da.ctl_host = p->d_hctl;
         }
-        hipLaunchKernelGGL(k_dalloc, dim3(1), dim3(1024), 0, s, Da);  // slots first: k_demit fills them
-        DHIP(hipGetLastError());
+        hipLaunchKernelGGL(k_dfin, dim3((ns + DFIN_WAVES - 1) / DFIN_WAVES), dim3(64 * DFIN_WAVES), 0, s, Da, r);
+        DHIP(hipGetLastError());  // (slots first: k_demit fills them)
         hipLaunchKernelGGL(k_demit, dim3(ns), dim3(64 * DEMIT_WAVES), 0, s, D);
-        DHIP(hipGetLastError());
-        hipLaunchKernelGGL(k_dcommit, dim3((ns + DCOMMIT_WAVES - 1) / DCOMMIT_WAVES), dim3(64 * DCOMMIT_WAVES), 0, s, D);
         DHIP(hipGetLastError());
         if (p->ps) DHIP(hipEventRecord(p->ev_free[p->tcur], s));  // (the set's last reader)
         if (pub) {
@@ -1390,14 +1403,14 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
         return XC_OK;
     };
     int rc;
-    if ((rc = resolve_round(0)) || (rc = emit())) return rc;
+    if ((rc = resolve_round(0)) || (rc = emit(0))) return rc;
     while (ctl[DCTL_FIX]) {
         // a provider lies past its own stream's stop: re-resolve with the executed prefixes
         // as the only eligible providers, until the executed sets agree
         if (++rounds > 64) return xc__set_error(XC_EDEVICE, "decode provider resolution did not converge");
         hipLaunchKernelGGL(k_dlim, dim3((ns + 255) / 256), dim3(256), 0, s, D, 0);
         DHIP(hipGetLastError());
-        if ((rc = resolve_round(rounds)) || (rc = emit())) return rc;
+        if ((rc = resolve_round(rounds)) || (rc = emit(rounds))) return rc;
     }
     p->stats.in_bytes = p->in_total;
     p->stats.n_ref = ctl[DCTL_NREF];
@@ -1411,7 +1424,7 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
         return xc__set_error(XC_ENOSPC, "device cache capacity exhausted");
     }
     if (ctl[DCTL_ERR] & 1u) return xc__set_error(XC_EINVAL, "output capacity too small");
-    // (k_dalloc advanced the count by exactly the entered segments: a later restore or reserve
+    // (k_dfin advanced the count by exactly the entered segments: a later restore or reserve
     // needs no device read)
     if (count0 >= 0) xc__cache_set_host_count(p->cache, count0 + ctl[DCTL_NENTER]);
     xc__cache_run_done_dec(p->cache, p);
