@@ -58,6 +58,8 @@ struct DecDev {
     uint32_t seg_cap;
     uint2 *undo;
     DevSet dset;
+    DevSet dset_next;          // k_dfin clears it (when clr_full): the next early run's batch table
+    uint32_t clr_lo, clr_full;
     uint32_t *ctl;
     int count;                 // k_dfin: count executed REF / EXTRACT tokens into ctl
     uint32_t *ctl_host;        // k_dfin: publish the control words here (mapped host memory)
@@ -261,6 +263,10 @@ __global__ __launch_bounds__(64) void k_dtok(DecDev D, int fill, int first, uint
     auto flush = [&]() {
         const bool ex = l < xn;
         if (!PROBE) {
+            // every EXTRACT into the batch table (cleared before the parse): the table is consulted
+            // only for hashes the cache lacks, and a hash the cache holds is held for every token
+            // that carries it, so entering those too changes no answer (k_dprobe probes the cache)
+            if (ex) set_insert(D.dset, xh, ((uint64_t)j << 32) | xt, true, nullptr, nullptr);  // (round 0: no limit)
             if (ex && fill) D.t_h[tb + xt] = xh;
             xn = 0;
             return;
@@ -378,10 +384,10 @@ template __global__ void k_dtok<false, true>(DecDev, int, int, uint32_t, uint32_
 template __global__ void k_dtok<true, true>(DecDev, int, int, uint32_t, uint32_t);
 template __global__ void k_dtok<true, false>(DecDev, int, int, uint32_t, uint32_t);
 
-// Round 0 after an early parse (k_dtok<true, false>): one wave per stream, its EXTRACT tokens 64 at a
-// time, one lane per token: the cache probe (a hit's payload compared wave-wide: rare), else the
-// batch table's insert (xcodec_decoder.cc:101-132); with the run's prologue (control words,
-// provider limits), as k_dtok's first launch does.
+// Round 0 after an early parse (k_dtok<true, false>, which entered every EXTRACT in the batch table):
+// one wave per stream, its EXTRACT tokens 64 at a time, one lane per token: the cache probe (a hit's
+// payload compared wave-wide: rare; xcodec_decoder.cc:101-132); with the run's prologue (control
+// words, provider limits), as k_dtok's first launch does.
 __global__ __launch_bounds__(64) void k_dprobe(DecDev D)
 {
     const uint32_t j = blockIdx.x, l = lane_id();
@@ -398,10 +404,7 @@ __global__ __launch_bounds__(64) void k_dprobe(DecDev D)
         uint64_t v = 0;
         uint32_t st = 0;
         const bool hit = ex && set_find(D.cache, h, &v);
-        if (ex && !hit) {
-            st = R_PENDING;
-            set_insert(D.dset, h, ((uint64_t)j << 32) | t, true, nullptr, nullptr);  // (round 0: no limit)
-        }
+        if (ex && !hit) st = R_PENDING;
         for (uint64_t mh = ballot(hit); mh; mh &= mh - 1) {
             const int fh = __ffsll((unsigned long long)mh) - 1;
             const uint32_t le = D.t_le[tb + readlane(t, fh)];
@@ -712,10 +715,9 @@ __global__ __launch_bounds__(64) void k_dres2(DecDev D)
     D.unknown[j] = unk;
 }
 
-__device__ __forceinline__ void dclear_range(const DecDev &D, uint32_t n_lo, uint32_t n_full, uint32_t i0,
-                                             uint32_t stride)
+__device__ __forceinline__ void dset_clear_range(const DevSet &s, uint32_t n_lo, uint32_t n_full, uint32_t i0,
+                                                 uint32_t stride)
 {
-    const DevSet &s = D.dset;
     const uint4 z = make_uint4(0, 0, 0, 0), ones = make_uint4(~0u, ~0u, ~0u, ~0u);
     for (uint32_t i = i0; i < XC_FILT_WORDS / 4; i += stride) ((uint4 *)s.filt)[i] = z;
     for (uint32_t i = i0; i < XC_L2_WORDS / 2; i += stride) ((uint4 *)s.l2)[i] = z;
@@ -725,6 +727,12 @@ __device__ __forceinline__ void dclear_range(const DecDev &D, uint32_t n_lo, uin
         ((uint4 *)s.vals)[i] = ones;
     }
     if (i0 == 0) *s.lo_zero = 0u;
+}
+
+__device__ __forceinline__ void dclear_range(const DecDev &D, uint32_t n_lo, uint32_t n_full, uint32_t i0,
+                                             uint32_t stride)
+{
+    dset_clear_range(D.dset, n_lo, n_full, i0, stride);
 }
 
 // A resolution round's fresh batch provider table, its FIX flag and the token counters.
@@ -922,6 +930,9 @@ __global__ __launch_bounds__(64 * DFIN_WAVES) void k_dfin(DecDev D, int round)
     __shared__ uint2 csum[DFIN_WAVES];
     __shared__ uint32_t last;
     const uint32_t wave = threadIdx.x >> 6, l = lane_id();
+    if (D.clr_full)
+        dset_clear_range(D.dset_next, D.clr_lo, D.clr_full, blockIdx.x * blockDim.x + threadIdx.x,
+                         gridDim.x * blockDim.x);
     {
         const uint32_t j = blockIdx.x * DFIN_WAVES + wave;
         if (j < D.ns) {
@@ -1096,6 +1107,11 @@ struct xc_dplan {
     int tcur = 0;
     hipStream_t ps = nullptr;
     hipEvent_t ev_parsed = nullptr, ev_free[2] = {nullptr, nullptr};
+    // the batch provider tables of the two token sets: an early run's parse enters its EXTRACTs in
+    // dsets[tcur], which the run before it cleared in its k_dfin (next_clean), or the side stream does
+    DevSet dsets[2] = {};
+    bool next_clean = false;
+    hipEvent_t ev_fin = nullptr;  // after the last k_dfin of the run before (that clear)
     uint64_t early_runs = 0;
     template <class T>
     int alloc(T **p, size_t n)
@@ -1142,6 +1158,7 @@ extern "C" int xc_dplan_destroy(xc_dplan *p)
     if (p->h_ctl) xc__pfree(p->h_ctl);
     if (p->ev_ctl) hipEventDestroy(p->ev_ctl);
     if (p->ev_parsed) hipEventDestroy(p->ev_parsed);
+    if (p->ev_fin) hipEventDestroy(p->ev_fin);
     for (auto e : p->ev_free)
         if (e) hipEventDestroy(e);
     if (p->ps) hipStreamDestroy(p->ps);
@@ -1206,6 +1223,7 @@ extern "C" int xc_decode_plan_create(xc_cache *c, const uint64_t *in_len, const 
 #undef DA
     ds.mask = p->n_full - 1;
     ds.lo_mask = p->n_lo - 1;
+    p->dsets[0] = ds;
     const hipStream_t s = p->s;
     if (ns) {
         DHIP(hipMemcpyAsync(d_ioff, p->ioff.data(), ns * 8, hipMemcpyHostToDevice, s));
@@ -1277,6 +1295,13 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
             if ((ra = p->alloc(&t1.tok_cnt, std::max<uint32_t>(ns, 1))) || (ra = p->alloc(&t1.t_lb, nt)) ||
                 (ra = p->alloc(&t1.t_le, nt)) || (ra = p->alloc(&t1.t_op, nt)) || (ra = p->alloc(&t1.t_h, nt)))
                 return ra;  // (what was allocated goes with the plan)
+            DevSet &d1 = p->dsets[1];
+            d1 = p->dsets[0];
+            if ((ra = p->alloc(&d1.filt, XC_FILT_WORDS)) || (ra = p->alloc(&d1.l2, 2 * (size_t)XC_L2_WORDS)) ||
+                (ra = p->alloc(&d1.lo_keys, p->n_lo)) || (ra = p->alloc(&d1.lo_zero, 1)) ||
+                (ra = p->alloc(&d1.keys, p->n_full)) || (ra = p->alloc(&d1.vals, p->n_full)))
+                return ra;
+            DHIP(hipEventCreateWithFlags(&p->ev_fin, hipEventDisableTiming));
             DHIP(hipEventCreateWithFlags(&p->ev_parsed, hipEventDisableTiming));
             for (auto &e : p->ev_free) DHIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
             DHIP(hipStreamCreateWithFlags(&p->ps, hipStreamNonBlocking));
@@ -1288,9 +1313,16 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
         p->D.t_le = t.t_le;
         p->D.t_op = t.t_op;
         p->D.t_h = t.t_h;
+        p->D.dset = p->dsets[p->tcur];
         DecDev Dp = p->D;
         Dp.in = d_in;
         DHIP(hipStreamWaitEvent(p->ps, p->ev_free[p->tcur], 0));
+        if (p->next_clean) {
+            DHIP(hipStreamWaitEvent(p->ps, p->ev_fin, 0));
+        } else {  // (the run before was not an early one: the table is cleared here)
+            hipLaunchKernelGGL(k_dclear, dim3(512), dim3(256), 0, p->ps, Dp, p->n_lo, p->n_full);
+        }
+        p->next_clean = false;
         auto parse = k_dtok<true, false>;
         hipLaunchKernelGGL(parse, dim3(ns), dim3(64), 0, p->ps, Dp, 1, 0, p->n_lo, p->n_full);
         DHIP(hipGetLastError());
@@ -1330,7 +1362,7 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
     xc__cache_count_unknown(p->cache);
     // tokens, with the prologue (control words, provider limits, round 0's provider table)
     // (XC_DTOK_WIN=1, experiments: the round-2 tokenizer)
-    if (tok_hash) {  // (the batch table cleared before the tokenizer inserts into it)
+    if (tok_hash && !early) {  // (the batch table cleared before the tokenizer inserts into it)
         hipLaunchKernelGGL(k_dclear, dim3(512), dim3(256), 0, s, D, p->n_lo, p->n_full);
         DHIP(hipGetLastError());
     }
@@ -1371,12 +1403,19 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
         // in the last word, cleared last) and the host returns while k_demit runs
         const bool pub = p->completion == XC_COMPLETE_STREAM;
         DecDev Da = D;
+        Da.clr_full = 0;
+        if (early) {  // the next early run's batch table, cleared by the grid
+            Da.dset_next = p->dsets[p->tcur ^ 1];
+            Da.clr_lo = p->n_lo;
+            Da.clr_full = p->n_full;
+        }
         if (pub) {
             p->h_ctl[DCTL_WORDS - 1] = 0xFFFFFFFFu;
             Da.ctl_host = p->d_hctl;
         }
         hipLaunchKernelGGL(k_dfin, dim3((ns + DFIN_WAVES - 1) / DFIN_WAVES), dim3(64 * DFIN_WAVES), 0, s, Da, r);
         DHIP(hipGetLastError());  // (slots first: k_demit fills them)
+        if (early) DHIP(hipEventRecord(p->ev_fin, s));
         hipLaunchKernelGGL(k_demit, dim3(ns), dim3(64 * DEMIT_WAVES), 0, s, D);
         DHIP(hipGetLastError());
         if (p->ps) DHIP(hipEventRecord(p->ev_free[p->tcur], s));  // (the set's last reader)
@@ -1427,6 +1466,7 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
     // (k_dfin advanced the count by exactly the entered segments: a later restore or reserve
     // needs no device read)
     if (count0 >= 0) xc__cache_set_host_count(p->cache, count0 + ctl[DCTL_NENTER]);
+    p->next_clean = early;
     xc__cache_run_done_dec(p->cache, p);
     return XC_OK;
 }
