@@ -58,8 +58,7 @@ struct DecDev {
     uint32_t seg_cap;
     uint2 *undo;
     DevSet dset;
-    DevSet dset_next;          // k_dfin clears it (when clr_full): the next early run's batch table
-    uint32_t clr_lo, clr_full;
+    uint32_t clr_lo, clr_full;  // k_dfin clears dset after its last reader, k_dres2 (when clr_full)
     uint32_t *ctl;
     int count;                 // k_dfin: count executed REF / EXTRACT tokens into ctl
     uint32_t *ctl_host;        // k_dfin: publish the control words here (mapped host memory)
@@ -931,7 +930,7 @@ __global__ __launch_bounds__(64 * DFIN_WAVES) void k_dfin(DecDev D, int round)
     __shared__ uint32_t last;
     const uint32_t wave = threadIdx.x >> 6, l = lane_id();
     if (D.clr_full)
-        dset_clear_range(D.dset_next, D.clr_lo, D.clr_full, blockIdx.x * blockDim.x + threadIdx.x,
+        dset_clear_range(D.dset, D.clr_lo, D.clr_full, blockIdx.x * blockDim.x + threadIdx.x,
                          gridDim.x * blockDim.x);
     {
         const uint32_t j = blockIdx.x * DFIN_WAVES + wave;
@@ -1108,10 +1107,10 @@ struct xc_dplan {
     hipStream_t ps = nullptr;
     hipEvent_t ev_parsed = nullptr, ev_free[2] = {nullptr, nullptr};
     // the batch provider tables of the two token sets: an early run's parse enters its EXTRACTs in
-    // dsets[tcur], which the run before it cleared in its k_dfin (next_clean), or the side stream does
+    // dsets[tcur], which the last early run on that set cleared in its k_dfin (clean[tcur]; the
+    // parse waits for that run's emit anyway, ev_free), or else the side stream clears first
     DevSet dsets[2] = {};
-    bool next_clean = false;
-    hipEvent_t ev_fin = nullptr;  // after the last k_dfin of the run before (that clear)
+    bool clean[2] = {false, false};
     uint64_t early_runs = 0;
     template <class T>
     int alloc(T **p, size_t n)
@@ -1158,7 +1157,6 @@ extern "C" int xc_dplan_destroy(xc_dplan *p)
     if (p->h_ctl) xc__pfree(p->h_ctl);
     if (p->ev_ctl) hipEventDestroy(p->ev_ctl);
     if (p->ev_parsed) hipEventDestroy(p->ev_parsed);
-    if (p->ev_fin) hipEventDestroy(p->ev_fin);
     for (auto e : p->ev_free)
         if (e) hipEventDestroy(e);
     if (p->ps) hipStreamDestroy(p->ps);
@@ -1301,7 +1299,6 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
                 (ra = p->alloc(&d1.lo_keys, p->n_lo)) || (ra = p->alloc(&d1.lo_zero, 1)) ||
                 (ra = p->alloc(&d1.keys, p->n_full)) || (ra = p->alloc(&d1.vals, p->n_full)))
                 return ra;
-            DHIP(hipEventCreateWithFlags(&p->ev_fin, hipEventDisableTiming));
             DHIP(hipEventCreateWithFlags(&p->ev_parsed, hipEventDisableTiming));
             for (auto &e : p->ev_free) DHIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
             DHIP(hipStreamCreateWithFlags(&p->ps, hipStreamNonBlocking));
@@ -1317,17 +1314,16 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
         DecDev Dp = p->D;
         Dp.in = d_in;
         DHIP(hipStreamWaitEvent(p->ps, p->ev_free[p->tcur], 0));
-        if (p->next_clean) {
-            DHIP(hipStreamWaitEvent(p->ps, p->ev_fin, 0));
-        } else {  // (the run before was not an early one: the table is cleared here)
+        if (!p->clean[p->tcur])  // (not left clean by an early run: cleared here)
             hipLaunchKernelGGL(k_dclear, dim3(512), dim3(256), 0, p->ps, Dp, p->n_lo, p->n_full);
-        }
-        p->next_clean = false;
+        p->clean[p->tcur] = false;
         auto parse = k_dtok<true, false>;
         hipLaunchKernelGGL(parse, dim3(ns), dim3(64), 0, p->ps, Dp, 1, 0, p->n_lo, p->n_full);
         DHIP(hipGetLastError());
         DHIP(hipEventRecord(p->ev_parsed, p->ps));
         p->early_runs++;
+    } else {
+        p->clean[p->tcur] = false;  // (this run's tokenizer enters into p->D.dset = dsets[tcur])
     }
     DecDev D = p->D;
     D.in = d_in;
@@ -1404,8 +1400,7 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
         const bool pub = p->completion == XC_COMPLETE_STREAM;
         DecDev Da = D;
         Da.clr_full = 0;
-        if (early) {  // the next early run's batch table, cleared by the grid
-            Da.dset_next = p->dsets[p->tcur ^ 1];
+        if (early) {  // the batch table cleared for the next early run on this set
             Da.clr_lo = p->n_lo;
             Da.clr_full = p->n_full;
         }
@@ -1415,7 +1410,6 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
         }
         hipLaunchKernelGGL(k_dfin, dim3((ns + DFIN_WAVES - 1) / DFIN_WAVES), dim3(64 * DFIN_WAVES), 0, s, Da, r);
         DHIP(hipGetLastError());  // (slots first: k_demit fills them)
-        if (early) DHIP(hipEventRecord(p->ev_fin, s));
         hipLaunchKernelGGL(k_demit, dim3(ns), dim3(64 * DEMIT_WAVES), 0, s, D);
         DHIP(hipGetLastError());
         if (p->ps) DHIP(hipEventRecord(p->ev_free[p->tcur], s));  // (the set's last reader)
@@ -1466,7 +1460,7 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
     // (k_dfin advanced the count by exactly the entered segments: a later restore or reserve
     // needs no device read)
     if (count0 >= 0) xc__cache_set_host_count(p->cache, count0 + ctl[DCTL_NENTER]);
-    p->next_clean = early;
+    if (early) p->clean[p->tcur] = true;
     xc__cache_run_done_dec(p->cache, p);
     return XC_OK;
 }
