@@ -195,6 +195,21 @@ __device__ __forceinline__ uint64_t dtok_mask(const uint4 (&v)[4], uint32_t w0, 
     return m;
 }
 
+// The batch provider table's insert: the least (stream, token) per hash (xcodec_decoder.cc:101-132,
+// the first EXTRACT of a hash provides it). set_find reads only the keys and values, so the
+// decoder's tables keep no filters: one CAS claim and one atomicMin.
+__device__ __forceinline__ void prov_insert(const DevSet &s, uint64_t h, uint64_t val)
+{
+    uint32_t i = key_slot(h, s.mask);
+    for (;;) {
+        const uint64_t prev = atomicCAS((unsigned long long *)&s.keys[i], (unsigned long long)XC_EMPTY64,
+                                        (unsigned long long)h);
+        if (prev == XC_EMPTY64 || prev == h) break;
+        i = (i + 1u) & s.mask;
+    }
+    atomicMin((unsigned long long *)&s.vals[i], (unsigned long long)val);
+}
+
 __device__ __forceinline__ uint64_t dreadlane64(uint64_t x, int l)
 {
     return ((uint64_t)readlane((uint32_t)(x >> 32), l) << 32) | readlane((uint32_t)x, l);
@@ -265,7 +280,7 @@ __global__ __launch_bounds__(64) void k_dtok(DecDev D, int fill, int first, uint
             // every EXTRACT into the batch table (cleared before the parse): the table is consulted
             // only for hashes the cache lacks, and a hash the cache holds is held for every token
             // that carries it, so entering those too changes no answer (k_dprobe probes the cache)
-            if (ex) set_insert(D.dset, xh, ((uint64_t)j << 32) | xt, true, nullptr, nullptr);  // (round 0: no limit)
+            if (ex) prov_insert(D.dset, xh, ((uint64_t)j << 32) | xt);  // (round 0: no limit)
             if (ex && fill) D.t_h[tb + xt] = xh;
             xn = 0;
             return;
@@ -275,7 +290,7 @@ __global__ __launch_bounds__(64) void k_dtok(DecDev D, int fill, int first, uint
         const bool hit = ex && set_find(D.cache, xh, &v);
         if (ex && !hit) {
             st = R_PENDING;
-            set_insert(D.dset, xh, ((uint64_t)j << 32) | xt, true, nullptr, nullptr);  // (round 0: no limit)
+            prov_insert(D.dset, xh, ((uint64_t)j << 32) | xt);  // (round 0: no limit)
         }
         for (uint64_t mh = ballot(hit); mh; mh &= mh - 1) {  // a cached hash: the bytes (rare)
             const int fh = __ffsll((unsigned long long)mh) - 1;
@@ -570,7 +585,7 @@ __global__ __launch_bounds__(64) void k_dres1(DecDev D)
             const bool hit = ex && set_find(D.cache, hl, &v);
             if (ex && !hit) {
                 st = R_PENDING;
-                if (tl < lim) set_insert(D.dset, hl, ((uint64_t)j << 32) | tl, true, nullptr, nullptr);
+                if (tl < lim) prov_insert(D.dset, hl, ((uint64_t)j << 32) | tl);
             }
             // a cached hash: its payload against the cached segment, wave-wide (rare)
             for (uint64_t mh = ballot(hit); mh; mh &= mh - 1) {
@@ -602,7 +617,7 @@ __global__ __launch_bounds__(64) void k_dres1(DecDev D)
             st = wave_equal2048(pay, seg_at(D.segs, v)) ? R_OKCACHE : R_COLL;
         } else {
             st = R_PENDING;
-            if (lane_id() == 0 && t < lim) set_insert(D.dset, h, ((uint64_t)j << 32) | t, true, nullptr, nullptr);
+            if (lane_id() == 0 && t < lim) prov_insert(D.dset, h, ((uint64_t)j << 32) | t);
         }
         if (lane_id() == 0) {
             D.t_stat[tb + t] = st;
@@ -717,15 +732,13 @@ __global__ __launch_bounds__(64) void k_dres2(DecDev D)
 __device__ __forceinline__ void dset_clear_range(const DevSet &s, uint32_t n_lo, uint32_t n_full, uint32_t i0,
                                                  uint32_t stride)
 {
-    const uint4 z = make_uint4(0, 0, 0, 0), ones = make_uint4(~0u, ~0u, ~0u, ~0u);
-    for (uint32_t i = i0; i < XC_FILT_WORDS / 4; i += stride) ((uint4 *)s.filt)[i] = z;
-    for (uint32_t i = i0; i < XC_L2_WORDS / 2; i += stride) ((uint4 *)s.l2)[i] = z;
-    for (uint32_t i = i0; i < n_lo / 4; i += stride) ((uint4 *)s.lo_keys)[i] = z;
+    // (keys and values only: prov_insert and set_find use nothing else)
+    (void)n_lo;
+    const uint4 ones = make_uint4(~0u, ~0u, ~0u, ~0u);
     for (uint32_t i = i0; i < n_full / 2; i += stride) {
         ((uint4 *)s.keys)[i] = ones;
         ((uint4 *)s.vals)[i] = ones;
     }
-    if (i0 == 0) *s.lo_zero = 0u;
 }
 
 __device__ __forceinline__ void dclear_range(const DecDev &D, uint32_t n_lo, uint32_t n_full, uint32_t i0,
@@ -1097,7 +1110,9 @@ struct xc_dplan {
     // xc_dplan_set_input_ready: runs parse their input on the side stream ps as soon as they are
     // submitted, beside the previous run's emit; the tokenizer's arrays alternate between two sets
     // (tset[k]: tok_cnt, t_lb, t_le, t_op, t_h) so that the parse never writes what a run before it
-    // still reads; ev_free[k] follows the last kernel that read set k
+    // still reads. Set k's last readers are the kernels of the run two back, which precede the
+    // run before's k_dfin on the context stream: once that run returned from its emit (settled),
+    // the parse needs no event; else it waits for an event recorded on the context stream then
     bool input_ready = false;
     struct TokSet {
         uint32_t *tok_cnt = nullptr, *t_lb = nullptr, *t_le = nullptr, *t_op = nullptr;
@@ -1105,10 +1120,11 @@ struct xc_dplan {
     } tset[2];
     int tcur = 0;
     hipStream_t ps = nullptr;
-    hipEvent_t ev_parsed = nullptr, ev_free[2] = {nullptr, nullptr};
+    hipEvent_t ev_parsed = nullptr, ev_free = nullptr;
+    bool settled = false;
     // the batch provider tables of the two token sets: an early run's parse enters its EXTRACTs in
-    // dsets[tcur], which the last early run on that set cleared in its k_dfin (clean[tcur]; the
-    // parse waits for that run's emit anyway, ev_free), or else the side stream clears first
+    // dsets[tcur], which the last early run on that set cleared in its k_dfin (clean[tcur]; done
+    // before the parse starts, as above), or else the side stream clears first
     DevSet dsets[2] = {};
     bool clean[2] = {false, false};
     uint64_t early_runs = 0;
@@ -1157,8 +1173,7 @@ extern "C" int xc_dplan_destroy(xc_dplan *p)
     if (p->h_ctl) xc__pfree(p->h_ctl);
     if (p->ev_ctl) hipEventDestroy(p->ev_ctl);
     if (p->ev_parsed) hipEventDestroy(p->ev_parsed);
-    for (auto e : p->ev_free)
-        if (e) hipEventDestroy(e);
+    if (p->ev_free) hipEventDestroy(p->ev_free);
     if (p->ps) hipStreamDestroy(p->ps);
     delete p;
     return XC_OK;
@@ -1300,7 +1315,7 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
                 (ra = p->alloc(&d1.keys, p->n_full)) || (ra = p->alloc(&d1.vals, p->n_full)))
                 return ra;
             DHIP(hipEventCreateWithFlags(&p->ev_parsed, hipEventDisableTiming));
-            for (auto &e : p->ev_free) DHIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            DHIP(hipEventCreateWithFlags(&p->ev_free, hipEventDisableTiming));
             DHIP(hipStreamCreateWithFlags(&p->ps, hipStreamNonBlocking));
         }
         p->tcur ^= 1;
@@ -1313,7 +1328,10 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
         p->D.dset = p->dsets[p->tcur];
         DecDev Dp = p->D;
         Dp.in = d_in;
-        DHIP(hipStreamWaitEvent(p->ps, p->ev_free[p->tcur], 0));
+        if (!p->settled) {
+            DHIP(hipEventRecord(p->ev_free, p->s));
+            DHIP(hipStreamWaitEvent(p->ps, p->ev_free, 0));
+        }
         if (!p->clean[p->tcur])  // (not left clean by an early run: cleared here)
             hipLaunchKernelGGL(k_dclear, dim3(512), dim3(256), 0, p->ps, Dp, p->n_lo, p->n_full);
         p->clean[p->tcur] = false;
@@ -1412,7 +1430,6 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
         DHIP(hipGetLastError());  // (slots first: k_demit fills them)
         hipLaunchKernelGGL(k_demit, dim3(ns), dim3(64 * DEMIT_WAVES), 0, s, D);
         DHIP(hipGetLastError());
-        if (p->ps) DHIP(hipEventRecord(p->ev_free[p->tcur], s));  // (the set's last reader)
         if (pub) {
             for (int i = 0;; i++) {
                 if (*(volatile const uint32_t *)(p->h_ctl + DCTL_WORDS - 1) == 0u) {
@@ -1436,7 +1453,9 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
         return XC_OK;
     };
     int rc;
+    p->settled = false;
     if ((rc = resolve_round(0)) || (rc = emit(0))) return rc;
+    p->settled = true;  // (this run's k_dfin ran: every kernel of the run before is done)
     while (ctl[DCTL_FIX]) {
         // a provider lies past its own stream's stop: re-resolve with the executed prefixes
         // as the only eligible providers, until the executed sets agree
