@@ -58,7 +58,8 @@ struct DecDev {
     uint32_t seg_cap;
     uint2 *undo;
     DevSet dset;
-    uint32_t clr_lo, clr_full;  // k_dfin clears dset after its last reader, k_dres2 (when clr_full)
+    DevSet dset_other;          // k_dprobe clears it (when clr_full): the other token set's table,
+    uint32_t clr_lo, clr_full;  // whose last reader, the run before's k_dres2, is done
     uint32_t *ctl;
     int count;                 // k_dfin: count executed REF / EXTRACT tokens into ctl
     uint32_t *ctl_host;        // k_dfin: publish the control words here (mapped host memory)
@@ -155,6 +156,8 @@ __device__ __forceinline__ uint64_t dwin_be64(const DWin &w, uint32_t x)
 // EXTRACT, whose 2048-byte payload is skipped, or the window's end, loads a new window.
 __device__ __forceinline__ void dclear_range(const DecDev &D, uint32_t n_lo, uint32_t n_full, uint32_t i0,
                                              uint32_t stride);
+__device__ __forceinline__ void dset_clear_range(const DevSet &s, uint32_t n_lo, uint32_t n_full, uint32_t i0,
+                                                 uint32_t stride);
 
 // Streaming tokenizer (round 3): the stream is read in 4 KiB windows, two windows ahead of the
 // one being tokenized (lane l: bytes 64 l .. 64 l + 63 of a window, 4 dwordx4 loads), so the
@@ -406,6 +409,7 @@ __global__ __launch_bounds__(64) void k_dprobe(DecDev D)
 {
     const uint32_t j = blockIdx.x, l = lane_id();
     if (j == 0 && threadIdx.x < DCTL_WORDS) D.ctl[threadIdx.x] = 0u;
+    if (D.clr_full) dset_clear_range(D.dset_other, D.clr_lo, D.clr_full, j * 64u + l, gridDim.x * 64u);
     if (j >= D.ns) return;
     if (l == 0) D.s_lim[j] = 0xFFFFFFFFu;
     const uint8_t *s = D.in + D.in_off[j];
@@ -942,9 +946,6 @@ __global__ __launch_bounds__(64 * DFIN_WAVES) void k_dfin(DecDev D, int round)
     __shared__ uint2 csum[DFIN_WAVES];
     __shared__ uint32_t last;
     const uint32_t wave = threadIdx.x >> 6, l = lane_id();
-    if (D.clr_full)
-        dset_clear_range(D.dset, D.clr_lo, D.clr_full, blockIdx.x * blockDim.x + threadIdx.x,
-                         gridDim.x * blockDim.x);
     {
         const uint32_t j = blockIdx.x * DFIN_WAVES + wave;
         if (j < D.ns) {
@@ -1123,8 +1124,8 @@ struct xc_dplan {
     hipEvent_t ev_parsed = nullptr, ev_free = nullptr;
     bool settled = false;
     // the batch provider tables of the two token sets: an early run's parse enters its EXTRACTs in
-    // dsets[tcur], which the last early run on that set cleared in its k_dfin (clean[tcur]; done
-    // before the parse starts, as above), or else the side stream clears first
+    // dsets[tcur], which the early run before it cleared in its k_dprobe (clean[tcur]; done before
+    // the parse starts, as above), or else the side stream clears first
     DevSet dsets[2] = {};
     bool clean[2] = {false, false};
     uint64_t early_runs = 0;
@@ -1382,7 +1383,11 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
     }
     if (early) {  // round 0 behind the side stream's parse
         DHIP(hipStreamWaitEvent(s, p->ev_parsed, 0));
-        hipLaunchKernelGGL(k_dprobe, dim3(ns), dim3(64), 0, s, D);
+        DecDev Dq = D;  // (and the other set's table cleared for the next early run on it)
+        Dq.dset_other = p->dsets[p->tcur ^ 1];
+        Dq.clr_lo = p->n_lo;
+        Dq.clr_full = p->n_full;
+        hipLaunchKernelGGL(k_dprobe, dim3(ns), dim3(64), 0, s, Dq);
     } else {
         auto tok = old_tok ? k_dtok_win : tok_hash ? k_dtok<true, true> : k_dtok<false, true>;
         hipLaunchKernelGGL(tok, dim3(std::max<uint32_t>(ns, 256u)), dim3(64), 0, s, D, 1, 1, p->n_lo, p->n_full);
@@ -1417,11 +1422,6 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
         // in the last word, cleared last) and the host returns while k_demit runs
         const bool pub = p->completion == XC_COMPLETE_STREAM;
         DecDev Da = D;
-        Da.clr_full = 0;
-        if (early) {  // the batch table cleared for the next early run on this set
-            Da.clr_lo = p->n_lo;
-            Da.clr_full = p->n_full;
-        }
         if (pub) {
             p->h_ctl[DCTL_WORDS - 1] = 0xFFFFFFFFu;
             Da.ctl_host = p->d_hctl;
@@ -1479,7 +1479,7 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
     // (k_dfin advanced the count by exactly the entered segments: a later restore or reserve
     // needs no device read)
     if (count0 >= 0) xc__cache_set_host_count(p->cache, count0 + ctl[DCTL_NENTER]);
-    if (early) p->clean[p->tcur] = true;
+    if (early) p->clean[p->tcur ^ 1] = true;
     xc__cache_run_done_dec(p->cache, p);
     return XC_OK;
 }
