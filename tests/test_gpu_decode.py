@@ -125,7 +125,7 @@ def test_device_resident_decode_plan(gpu_ctx, oracle_mod, stream_ordered, input_
     (xc_dplan_set_completion): the runs return once decided, back to back with no host
     synchronisation; input ready (xc_dplan_set_input_ready): each run's parse on the side stream
     beside the previous run's emit, the token arrays alternating; a plan whose capacities are too
-    small still fails (k_dstop's bound stops the early return)."""
+    small still fails (k_dres2's bound stops the early return)."""
     import torch
     import wanproxy_amd as w
     pool = W.pool(256)
@@ -191,3 +191,56 @@ def test_device_resident_decode_plan(gpu_ctx, oracle_mod, stream_ordered, input_
         small.run(d_in.data_ptr(), d_out.data_ptr(), u64.data_ptr(), u64.data_ptr() + 8 * n,
                   i32.data_ptr(), u64.data_ptr() + 16 * n, i32.data_ptr() + 4 * n)
     gpu_ctx.sync()
+
+
+@pytest.mark.parametrize("input_ready", [False, True])
+def test_device_resident_resolution_rounds(gpu_ctx, oracle_mod, input_ready):
+    """Providers past their own stream's stop (test_cross_stream_order's streams, among ordinary
+    ones) through the device-resident plan, four runs back to back over a restored snapshot: the
+    round check of k_dfin asks for another resolution round, and with the input ready every run's
+    parse enters its EXTRACTs into the batch table of its token set, which alternates between runs
+    (xcodec_decoder.cc:101-166)."""
+    import torch
+    import wanproxy_amd as w
+    a, b, c = W.gen(40, 2048), W.gen(41, 2048), W.gen(42, 2048)
+    ha, hb, hc = (oracle_mod.hash_segment(s) for s in (a, b, c))
+    ref = lambda h: b"\xf1\x02" + int(h).to_bytes(8, "big")  # noqa: E731
+    ext = lambda s: b"\xf1\x01" + s.tobytes()  # noqa: E731
+    pool = W.pool(64)
+    eo = oracle_mod.Cache()
+    streams = eo.encode_batch(W.repeat_buffers(12, 0x79, 50, np_segments=64, pool_bytes=pool))
+    streams[2:2] = [b"hello" + ref(hb) + b"x", ext(a) + b"mid" + ref(ha) + ext(b), ref(hb) + ref(ha) + b"ok",
+                    ref(hc) + ext(c), ref(hc) + b"z", ext(c) + ref(hc)]
+    want = oracle_mod.Cache().decode_batch(streams)
+    gc = w.XCodecCache(gpu_ctx, 1 << 14)
+    gc.snapshot()
+    lens = np.array([len(s) for s in streams], np.uint64)
+    plan = w.DecodePlan(gc, lens, lens * 205 + 16)
+    arena = np.zeros(plan.in_bytes, np.uint8)
+    for i, s in enumerate(streams):
+        arena[int(plan.in_off[i]):int(plan.in_off[i]) + len(s)] = np.frombuffer(s, np.uint8)
+    n = len(streams)
+    d_in = torch.from_numpy(arena).cuda()
+    plan.set_completion(True)
+    plan.set_input_ready(input_ready)
+    sets = [(torch.zeros(plan.out_bytes, dtype=torch.uint8, device="cuda"),
+             torch.zeros(3 * n, dtype=torch.int64, device="cuda"),
+             torch.zeros(2 * n, dtype=torch.int32, device="cuda")) for _ in range(4)]
+    torch.cuda.synchronize()
+    for d_out, u64, i32 in sets:
+        gc.restore_async()
+        plan.run(d_in.data_ptr(), d_out.data_ptr(), u64.data_ptr(), u64.data_ptr() + 8 * n,
+                 i32.data_ptr(), u64.data_ptr() + 16 * n, i32.data_ptr() + 4 * n)
+        assert plan.stats().rounds >= 2
+    gpu_ctx.sync()
+    torch.cuda.synchronize()
+    for rep, (d_out, u64, i32) in enumerate(sets):
+        out = d_out.cpu().numpy()
+        r64 = u64.cpu().numpy().astype(np.uint64)
+        r32 = i32.cpu().numpy()
+        for i, (st, data, cons, unk) in enumerate(want):
+            o = int(plan.out_off[i])
+            assert int(r32[i]) == st, (rep, i, "status")
+            assert int(r64[n + i]) == cons, (rep, i, "consumed")
+            assert (int(r64[2 * n + i]) if r32[n + i] else None) == unk, (rep, i, "unknown")
+            assert out[o:o + int(r64[i])].tobytes() == data, (rep, i, "bytes")
