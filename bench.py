@@ -59,6 +59,9 @@ def parse():
     ap.add_argument("--only", choices=["cfg2", "cfg3", "cfg4"],
                     help="run just that leg (one GPU) and print its JSON object (kernel traces, A/B)")
     ap.add_argument("--no-live", action="store_true", help="skip the steady-state (live cache) leg")
+    ap.add_argument("--tail-steps", type=int, default=0,
+                    help="untimed production steps (no timing events) after the diagnostic ones, so that a "
+                         "kernel trace's last step is one of the timed kind (tools/timeline.py)")
     ap.add_argument("--live-batches", type=int, default=8)
     ap.add_argument("--live-reps", type=int, default=3)
     return ap.parse_args()
@@ -476,6 +479,9 @@ def main():
     torch.cuda.synchronize()
     plan.set_timing(False)
     kt_all = plan.kernel_times(reset=True)
+    for _ in range(args.tail_steps):
+        step()
+    torch.cuda.synchronize()
 
     total_in = n_job * W.BUF
     value = total_in * args.steps / elapsed / 2**30

@@ -17,6 +17,13 @@ __global__ void k_write(uint4 *p, size_t n)
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
         p[i] = make_uint4((uint32_t)i, 1, 2, 3);
 }
+// holds the stream for ~2 ms so that the host has enqueued a whole phase before it runs (the gaps
+// measured behind it are the device's, not the host's launch rate)
+__global__ void k_spin(long long cycles)
+{
+    const long long t0 = wall_clock64();
+    while (wall_clock64() - t0 < cycles) __builtin_amdgcn_s_sleep(8);
+}
 __global__ void k_grid(uint32_t *p, uint32_t v) { if (v == 0xFFFFFFFFu) p[blockIdx.x] = v; }
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); return 1; } } while (0)
@@ -51,6 +58,7 @@ int main()
     CK(hipStreamSynchronize(s));
     // each phase enqueued whole before it runs: a long head kernel keeps the host ahead
     for (int phase = 0; phase < 8; phase++) {
+        k_spin<<<1, 64, 0, s>>>(200000);  // 2 ms at the 100 MHz wall clock
         k_write<<<1024, 256, 0, s>>>(w, nw);
         if (phase == 7)  // another stream's long kernel beside the chain
             for (int r = 0; r < 8; r++) k_write<<<256, 256, 0, hs>>>(w2, nw);  // head: 64 MiB written (the host enqueues behind it)

@@ -1,5 +1,7 @@
 """Print the kernel timeline of the last bench step from a rocprofv3 kernel trace:
-start offset, duration and the gap before each launch (us).  usage: timeline.py TRACE.csv [N]"""
+start offset, duration and the gap before each launch (us).  usage: timeline.py TRACE.csv [N]
+(trace bench.py with --tail-steps 2: its last steps are otherwise the diagnostic ones, whose timing events
+add ~6 us before and after every span)"""
 import csv
 import sys
 
