@@ -2418,6 +2418,14 @@ static int launch_first_round(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t s1,
     HIPCHK(hipGetLastError());
     p->zero_ctl = false;
     const bool inline_hash = p->next_hash <= sb;
+    // a run whose first sub-batch was hashed ahead: the later sub-batches' hashing may start once the
+    // set is cleared (their compares read the cache count k_clear_set noted), not after this
+    // sub-batch's predictions: sub-batch 1 then no longer waits for its hashes (the production trace's
+    // 35 us, profiles/r04/gaps); XC_GO_EARLY=1 (A/B; default: the event after the predictions)
+    static const bool go_first = getenv("XC_GO_EARLY") && atoi(getenv("XC_GO_EARLY"));
+    const bool chain = p->next_hash == sb + 1 && sb + 2 < p->sub.size();
+    const bool go_early = chain && !inline_hash && go_first;
+    if (go_early) HIPCHK(hipEventRecord(p->ev_go[sb], s));
     if (inline_hash) {
         // first sub-batch of the run: nothing to overlap with, its blocks are hashed in line
         // (after whatever the caller enqueued on the context stream to fill the input), and
@@ -2438,8 +2446,8 @@ static int launch_first_round(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t s1,
     // sub-batch's predictions: the side stream never waits for the main one, whose sub-batch k then
     // rarely waits for k's hashes (XC_BH_GATED=1: one sub-batch ahead, each hashed beside the scan
     // before it, as in round 2)
-    if (p->next_hash == sb + 1 && sb + 2 < p->sub.size()) {
-        HIPCHK(hipEventRecord(p->ev_go[sb], s));
+    if (chain) {
+        if (!go_early) HIPCHK(hipEventRecord(p->ev_go[sb], s));
         const uint32_t last = bh_gated() ? sb + 1 : (uint32_t)p->sub.size() - 2;
         for (uint32_t k = sb + 1; k <= last; k++)
             if ((rc = enqueue_block_hash(p, k, k == sb + 1 ? p->ev_go[sb] : nullptr, p->hs))) return rc;
