@@ -21,11 +21,13 @@ class XCodecCacheCOSS : public XCodecCache {
     xc_coss* coss_;
 
 public:
-    XCodecCacheCOSS(const UUID& uuid, const std::string& cache_dir, size_t cache_size, int gpu = 0)
+    XCodecCacheCOSS(const UUID& uuid, const std::string& cache_dir, size_t cache_size, int gpu = -1)
     : XCodecCache(uuid, cache_size), ctx_(0), coss_(0)
     {
         uint8_t u[UUID_STRING_SIZE + 1];
         uuid.to_string(u);
+        if (gpu < 0)  /* (the reference's three-argument construction: xcodec_facade::place) */
+            gpu = xcodec_facade::place(uuid, "/xcodec/cache/coss");
         xcodec_facade::halt_on(xc_ctx_create(gpu, &ctx_), "/xcodec/cache/coss", "device context");
         xcodec_facade::halt_on(xc_coss_open(ctx_, cache_dir.c_str(), (const char*) u, cache_size, &coss_),
                                "/xcodec/cache/coss", "open");

@@ -44,6 +44,20 @@ inline void halt_on(int rc, const LogHandle& log, const char* what)
     if (rc != XC_OK)
         HALT(log) << what << ": " << xc_last_error() << " (" << rc << ")";
 }
+
+/* The device of a cache the proxy constructs with the reference's arguments (WanProxyCore::add_cache,
+ * proxy/wanproxy.h:106-116, passes no device): xc_device_place over the visible devices, i.e. caches
+ * dealt round-robin in creation order, XC_DEVICE=d (or a list) to pin them, XC_DEVICE_POLICY=uuid to
+ * place by UUID. */
+inline int place(const UUID& uuid, const char* log)
+{
+    int n = 0;
+    halt_on(xc_device_count(&n), log, "device count");
+    const int d = xc_device_place((const uint8_t*) &uuid.uuid_, sizeof uuid.uuid_, n);
+    if (d < 0)
+        halt_on(d, log, "device placement");
+    return d;
+}
 }
 
 class XCodecCache {
@@ -69,15 +83,18 @@ public:
 };
 
 /* XCodecMemoryCache (xcodec_cache.h:162-211) held in HBM.  The device cache starts at
- * cap_segments and grows like the reference's map before any call that could fill it. */
+ * cap_segments and grows like the reference's map before any call that could fill it.  gpu < 0 (what
+ * the reference's two-argument construction gets): the device xcodec_facade::place picks. */
 class XCodecMemoryCache : public XCodecCache {
     xc_ctx* ctx_;
     xc_cache* cache_;
 
 public:
-    XCodecMemoryCache(const UUID& uuid, size_t size, int gpu = 0, uint64_t cap_segments = 1u << 16)
+    XCodecMemoryCache(const UUID& uuid, size_t size, int gpu = -1, uint64_t cap_segments = 1u << 16)
     : XCodecCache(uuid, size), ctx_(0), cache_(0)
     {
+        if (gpu < 0)
+            gpu = xcodec_facade::place(uuid, "/xcodec/cache/memory");
         xcodec_facade::halt_on(xc_ctx_create(gpu, &ctx_), "/xcodec/cache/memory", "device context");
         xcodec_facade::halt_on(xc_cache_create(ctx_, cap_segments, &cache_), "/xcodec/cache/memory", "device cache");
     }

@@ -23,22 +23,26 @@ bool XCodecDecoder::decode(Buffer& output, Buffer& input, std::set<uint64_t>& un
     if (input.empty())
         return true;
     const uint64_t n = input.length();
-    std::vector<uint8_t> in(n);
-    input.copyout(&in[0], n);
+    if (in_.size() < n)
+        in_.resize(n);
+    uint8_t* in = &in_[0];
+    input.copyout(in, n);
     /* a REF (10 bytes) expands to 2048: n plus 2038 per F1 byte (xchip::decode_bound) */
-    uint64_t off = 0, len = n, cap = xchip::decode_bound(&in[0], n), olen = 0, consumed = 0, unknown = 0;
+    uint64_t off = 0, len = n, cap = xchip::decode_bound(in, n), olen = 0, consumed = 0, unknown = 0;
     int32_t status = 0, has_unknown = 0;
-    std::vector<uint8_t> out(cap);
+    if (out_.size() < cap)
+        out_.resize(cap);
+    uint8_t* out = &out_[0];
     xc_cache* dev = cache_->coss() ? xc_coss_cache(cache_->coss()) : cache_->device();
     int rc;
     if (cache_->coss())
         rc = xcodec_facade::call(dev, [&] {
-            return xc_coss_decode_batch_host(cache_->coss(), &in[0], &off, &len, 1, &out[0], &off, &cap, &olen,
+            return xc_coss_decode_batch_host(cache_->coss(), in, &off, &len, 1, out, &off, &cap, &olen,
                                              &consumed, &status, &unknown, &has_unknown);
         });
     else
         rc = xcodec_facade::call(dev, [&] {
-            return xc_decode_batch_host(dev, &in[0], &off, &len, 1, &out[0], &off, &cap, &olen, &consumed, &status,
+            return xc_decode_batch_host(dev, in, &off, &len, 1, out, &off, &cap, &olen, &consumed, &status,
                                         &unknown, &has_unknown);
         });
     if (rc != XC_OK) {
@@ -46,7 +50,7 @@ bool XCodecDecoder::decode(Buffer& output, Buffer& input, std::set<uint64_t>& un
         return false;
     }
     if (olen)
-        output.append(&out[0], olen);
+        output.append(out, olen);
     input.skip(consumed);  /* the reference consumes exactly this much (xcodec_decoder.cc:85-173) */
     if (has_unknown)
         unknown_hashes.insert(unknown);

@@ -10,6 +10,7 @@
 #define XCODEC_XCODEC_DECODER_H
 
 #include <set>
+#include <vector>
 
 #include <common/log.h>
 
@@ -18,6 +19,7 @@ class XCodecCache;
 class XCodecDecoder {
     LogHandle log_;
     XCodecCache* cache_;
+    std::vector<uint8_t> in_, out_;  /* host staging, kept across calls (grown, never shrunk) */
 
 public:
     XCodecDecoder(XCodecCache*);

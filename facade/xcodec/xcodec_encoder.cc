@@ -29,27 +29,30 @@ void XCodecEncoder::call(Buffer& output, const uint8_t* in, uint64_t n, uint32_t
 {
     uint64_t pend = 0;
     xcodec_facade::halt_on(xc_encoder_pending(enc_, &pend), log_, "encoder state");
-    std::vector<uint8_t> out(2 * (pend + n) + 16);
-    uint64_t off = 0, cap = out.size(), len = 0;
+    if (out_.size() < 2 * (pend + n) + 16)
+        out_.resize(2 * (pend + n) + 16);
+    uint8_t* out = &out_[0];
+    uint64_t off = 0, cap = 2 * (pend + n) + 16, len = 0;
     int rc;
     if (cache_->coss())
         rc = xcodec_facade::call(dev(), [&] {
-            return xc_coss_encode_streams(cache_->coss(), &enc_, &in, &n, &flags, 1, &out[0], &off, &cap, &len);
+            return xc_coss_encode_streams(cache_->coss(), &enc_, &in, &n, &flags, 1, out, &off, &cap, &len);
         });
     else
-        rc = xcodec_facade::call(dev(), [&] { return xc_encode_streams(&enc_, &in, &n, &flags, 1, &out[0], &off, &cap, &len); });
+        rc = xcodec_facade::call(dev(), [&] { return xc_encode_streams(&enc_, &in, &n, &flags, 1, out, &off, &cap, &len); });
     xcodec_facade::halt_on(rc, log_, "encode");
     if (len)
-        output.append(&out[0], len);
+        output.append(out, len);
     if (emitted)
         *emitted = len > 0;
 }
 
 void XCodecEncoder::encode(Buffer& output, Buffer& input)
 {
-    std::vector<uint8_t> in(input.length() + 1);
-    input.copyout(&in[0], input.length());  /* (read, not consumed: source_.append(input), :65) */
-    call(output, &in[0], input.length(), 0, 0);
+    if (in_.size() < input.length() + 1)
+        in_.resize(input.length() + 1);
+    input.copyout(&in_[0], input.length());  /* (read, not consumed: source_.append(input), :65) */
+    call(output, &in_[0], input.length(), 0, 0);
 }
 
 bool XCodecEncoder::flush(Buffer& output)

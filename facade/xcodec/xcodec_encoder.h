@@ -23,6 +23,7 @@ class XCodecEncoder {
     LogHandle log_;
     XCodecCache* cache_;
     xc_encoder* enc_;
+    std::vector<uint8_t> in_, out_;  /* host staging, kept across calls (grown, never shrunk) */
 
     xc_cache* dev() const;
     void call(Buffer& output, const uint8_t* in, uint64_t n, uint32_t flags, int* emitted);

@@ -42,9 +42,21 @@ typedef struct xc_plan xc_plan;   /* a device-resident batch layout + workspace 
 /* Number of visible HIP devices. */
 int xc_device_count(int *n);
 
+/* Device placement of a new cache among ndev devices (the drop-in facade's two-argument
+ * XCodecMemoryCache(uuid, size) / XCodecCacheCOSS(uuid, dir, size), which the unchanged
+ * WanProxyCore::add_cache calls, proxy/wanproxy.h:106-116).  key = the cache's 16 UUID bytes.
+ * XC_DEVICE in the environment: "d" pins every cache to device d, "d0,d1,..." deals caches over
+ * that list; XC_DEVICE_POLICY=uuid places by a hash of the key (the same UUID lands on the same
+ * device in every process); otherwise caches are dealt round-robin over all ndev devices in
+ * creation order (process-wide).  Returns the device index, or XC_EINVAL (ndev < 1, or XC_DEVICE
+ * names a device >= ndev).  Touches no device. */
+int xc_device_place(const uint8_t *key, uint64_t key_len, int ndev);
+
 /* Context on device `dev` with its own HIP stream. */
 int xc_ctx_create(int dev, xc_ctx **out);
 int xc_ctx_destroy(xc_ctx *ctx);
+/* The device the context is on. */
+int xc_ctx_device(xc_ctx *ctx, int *dev);
 /* The context's hipStream_t, as void*. */
 void *xc_ctx_stream(xc_ctx *ctx);
 /* Wait for all work queued on the context stream. */

@@ -38,6 +38,8 @@ int xc__test_quiesced(void) { return g_quiesced; }
 int xc_cache_quiesce(xc_cache *) { g_in_flight = false; g_quiesced++; return XC_OK; }
 const char *xc_last_error(void) { return g_err.c_str(); }
 int xc_device_count(int *n) { *n = 1; return XC_OK; }
+int xc_device_place(const uint8_t *, uint64_t, int) { return 0; }
+int xc_ctx_device(xc_ctx *c, int *dev) { *dev = c->dev; return XC_OK; }
 int xc_ctx_create(int dev, xc_ctx **out) { *out = new xc_ctx{dev}; return XC_OK; }
 int xc_ctx_destroy(xc_ctx *c) { delete c; return XC_OK; }
 int xc_cache_create(xc_ctx *, uint64_t, xc_cache **out) { *out = new xc_cache{xo_cache_new()}; return XC_OK; }

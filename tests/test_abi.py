@@ -63,3 +63,34 @@ def test_cpp_host_layer_compiles_and_links():
     assert os.access(prog, os.X_OK), "built by wanproxy_amd/csrc/Makefile (__graft_entry__.build())"
     out = subprocess.run(["ldd", prog], capture_output=True, text=True, check=True).stdout
     assert "libxcodec_hip.so" in out and "not found" not in out
+
+
+def test_device_placement_of_caches(monkeypatch):
+    """xc_device_place (the facade's placement of caches the proxy constructs with the reference's
+    arguments, proxy/wanproxy.h:106-116): round-robin in creation order by default, XC_DEVICE pins
+    or deals over a list, XC_DEVICE_POLICY=uuid is a function of the UUID.  No device is touched."""
+    import numpy as np
+    lib = ctypes.CDLL(LIB)
+    lib.xc_device_place.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int]
+    rng = np.random.default_rng(7)
+    uuids = [rng.integers(0, 256, 16, dtype=np.uint8).tobytes() for _ in range(64)]
+    monkeypatch.delenv("XC_DEVICE", raising=False)
+    monkeypatch.delenv("XC_DEVICE_POLICY", raising=False)
+    got = [lib.xc_device_place(u, 16, 8) for u in uuids]
+    assert sorted(got) == sorted(list(range(8)) * 8)           # 64 caches: 8 on each of 8 devices
+    assert all(got[i + 1] == (got[i] + 1) % 8 for i in range(63))
+    monkeypatch.setenv("XC_DEVICE", "3")
+    assert {lib.xc_device_place(u, 16, 8) for u in uuids} == {3}
+    monkeypatch.setenv("XC_DEVICE", "1,5,6")
+    got = [lib.xc_device_place(u, 16, 8) for u in uuids[:30]]
+    assert sorted(set(got)) == [1, 5, 6] and all(got.count(d) == 10 for d in (1, 5, 6))
+    monkeypatch.setenv("XC_DEVICE", "8")
+    assert lib.xc_device_place(uuids[0], 16, 8) == -22      # no such device
+    monkeypatch.setenv("XC_DEVICE", "2,x")
+    assert lib.xc_device_place(uuids[0], 16, 8) == -22
+    monkeypatch.delenv("XC_DEVICE")
+    monkeypatch.setenv("XC_DEVICE_POLICY", "uuid")
+    a = [lib.xc_device_place(u, 16, 8) for u in uuids]
+    assert a == [lib.xc_device_place(u, 16, 8) for u in uuids]  # the same UUID, the same device
+    assert set(a) == set(range(8))
+    assert lib.xc_device_place(uuids[0], 16, 0) == -22

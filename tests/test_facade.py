@@ -92,3 +92,37 @@ def test_reference_filter_over_the_facade_never_throws(tmp_path):
     assert r.returncode == 0 and "decode false" in r.stdout and "device decode failed" in r.stderr, r.stdout + r.stderr
     r = subprocess.run([ff, "fail-encode"], capture_output=True, text=True, timeout=120)
     assert r.returncode == -6 and "Halting: encode" in r.stderr, (r.returncode, r.stdout, r.stderr)
+
+
+def test_filter_turns_driver_over_the_stand_in(tmp_path):
+    """The driver of the GPU drop-in test (tests/facade/filter_turns.cc, tests/test_gpu_facade.py)
+    with the CPU stand-in of the C ABI: the reference's EncodeFilter / DecodeFilter pipes between two
+    proxies, <ASK>/<LEARN> included, give the oracle pipes' bytes.  (This checks the harness; the GPU
+    test runs the same driver over the product library.)"""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    from pipe_harness import OracleBackend, read_outputs, run_scenario, write_scenario
+    from test_gpu_pipe_cpp import _scenario
+    make = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], capture_output=True, text=True)
+    assert make.returncode == 0, make.stderr
+    fac = os.path.join(ROOT, "facade", "xcodec")
+    t = os.path.join(ROOT, "tests", "facade")
+    ref = [os.path.join(REF, f) for f in ("xcodec/xcodec_filter.cc", "event/event_system.cc", "event/io_service.cc",
+                                          "event/event_poll_epoll.cc", "common/thread/thread.cc", "common/log.cc",
+                                          "common/buffer.cc", "common/uuid/uuid.cc")]
+    _cc(["-w", "-ffunction-sections", "-fdata-sections", "-Wl,--gc-sections", "-o", "ft",
+         os.path.join(t, "filter_turns.cc"), os.path.join(fac, "xcodec_encoder.cc"),
+         os.path.join(fac, "xcodec_decoder.cc"), os.path.join(t, "xc_abi_oracle.cc")] + ref +
+        ["-L" + os.path.join(ROOT, "oracle"), "-loracle", "-Wl,-rpath," + os.path.join(ROOT, "oracle"),
+         "-l:libuuid.so.1", "-lpthread"], tmp_path)
+    warm, order, inputs = _scenario(3, nconn=6, turns=3)
+    sc, out = tmp_path / "sc.bin", tmp_path / "out.bin"
+    write_scenario(sc, warm, order, inputs, waiting=False, batched=False)
+    r = subprocess.run([str(tmp_path / "ft"), "parity", str(sc), str(out)], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and "parity ok" in r.stdout, r.stdout + r.stderr
+    got = read_outputs(out, len(inputs))
+    want = run_scenario(OracleBackend(oracle), warm, order, inputs, waiting=False, batched=False)
+    assert got == want
+    assert sum(g[1].count(b"\xfd") for g in got) > 0

@@ -150,7 +150,9 @@ def test_window_after_back_to_back_runs(gpu_ctx, oracle_mod, evict):
 def test_first_sub_batch_hashed_ahead(gpu_ctx, oracle_mod, monkeypatch):
     """xc_plan_set_input_ready: a plan's next run hashes its first sub-batch on the side stream at the
     submit, beside the previous run's last kernels, its compares taking only the entries complete
-    then.  Runs of one plan back to back (some anchor-scanned), a restore in between (the bench's
+    then; the later sub-batches' hashing then starts on the side stream right after sub-batch 0's
+    set clear, beside sub-batch 0's predictions (xc_runtime.hip launch_first_round: every run here
+    has >= 3 sub-batches).  Runs of one plan back to back (some anchor-scanned), a restore in between (the bench's
     step), another plan's run and a host enter in between (which write the cache: no early hashing
     for the next run): every buffer equals the oracle's."""
     import wanproxy_amd as w
@@ -182,6 +184,7 @@ def test_first_sub_batch_hashed_ahead(gpu_ctx, oracle_mod, monkeypatch):
             bufs[8] = prev[12].copy()
         got, st = r.run(bufs, stats=True)
         _same(got, oc.encode_batch(bufs), f"run {k}")
+        assert st.sub_batches >= 3, st.sub_batches
         early.append(int(st.early_hashed))
         redone.append(int(st.redone))
         prev = bufs

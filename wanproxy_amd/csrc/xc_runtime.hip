@@ -257,6 +257,13 @@ extern "C" int xc_ctx_destroy(xc_ctx *ctx)
 
 extern "C" void *xc_ctx_stream(xc_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
 
+extern "C" int xc_ctx_device(xc_ctx *ctx, int *dev)
+{
+    if (!ctx || !dev) return fail(XC_EINVAL, "null");
+    *dev = ctx->dev;
+    return XC_OK;
+}
+
 extern "C" int xc_ctx_sync(xc_ctx *ctx)
 {
     if (!ctx) return fail(XC_EINVAL, "null");
@@ -2421,10 +2428,11 @@ static int launch_first_round(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t s1,
     // a run whose first sub-batch was hashed ahead: the later sub-batches' hashing may start once the
     // set is cleared (their compares read the cache count k_clear_set noted), not after this
     // sub-batch's predictions: sub-batch 1 then no longer waits for its hashes (the production trace's
-    // 35 us, profiles/r04/gaps); XC_GO_EARLY=1 (A/B; default: the event after the predictions)
-    static const bool go_first = getenv("XC_GO_EARLY") && atoi(getenv("XC_GO_EARLY"));
+    // 35 us, profiles/r04/gaps; cfg5 A/B 762-764 -> 771-773 GiB/s, profiles/r05/ab/go_early_r5.txt).
+    // Nothing sub-batch 0's predictions write is read by the side stream's hashing (the declaration
+    // set and the combined filters are not; block hashes and records are per sub-batch).
     const bool chain = p->next_hash == sb + 1 && sb + 2 < p->sub.size();
-    const bool go_early = chain && !inline_hash && go_first;
+    const bool go_early = chain && !inline_hash;
     if (go_early) HIPCHK(hipEventRecord(p->ev_go[sb], s));
     if (inline_hash) {
         // first sub-batch of the run: nothing to overlap with, its blocks are hashed in line

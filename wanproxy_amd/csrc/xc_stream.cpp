@@ -12,6 +12,8 @@
 // with the reference's single-threaded order (call k sees the cache after calls < k).  A batch
 // round holds each encoder at most once; a later call of the same encoder starts a new round.
 #include <algorithm>
+#include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <stdexcept>
@@ -39,7 +41,38 @@ extern "C" int xc__coss_encode_gather(xc_coss *c, uint64_t nbuf, const uint8_t *
 namespace {
 constexpr uint64_t MAX_BUFFER = 1u << 20;  // longest device batch item (xc_kernels.h MAX_BUF)
 constexpr uint32_t SF_NOFLUSH = 1u;        // xc_kernels.h
+std::atomic<uint64_t> g_placed{0};  // caches placed round-robin so far (xc_device_place)
 }  // namespace
+
+// Where a proxy's caches go (include/xcodec_hip.h): WanProxyCore::add_cache constructs every cache
+// with two arguments (proxy/wanproxy.h:106-116) and a cache's calls are sequential by contract
+// (one cache = one stream of codec calls in the reference's order), so the unit of placement is the
+// cache: a codec's encoder cache and each peer's decoder cache each live on one device.
+extern "C" int xc_device_place(const uint8_t *key, uint64_t key_len, int ndev)
+{
+    if (ndev < 1) return xc__set_error(XC_EINVAL, "no device to place a cache on");
+    std::vector<int> devs;
+    if (const char *e = std::getenv("XC_DEVICE"); e && *e) {
+        for (const char *p = e; *p;) {
+            char *end = nullptr;
+            const long d = std::strtol(p, &end, 10);
+            if (end == p || d < 0 || d >= ndev) return xc__set_error(XC_EINVAL, "XC_DEVICE names no visible device");
+            devs.push_back((int)d);
+            p = *end == ',' ? end + 1 : end;
+            if (*end && *end != ',') return xc__set_error(XC_EINVAL, "XC_DEVICE: a device index or a comma list");
+        }
+    } else {
+        for (int d = 0; d < ndev; d++) devs.push_back(d);
+    }
+    const char *pol = std::getenv("XC_DEVICE_POLICY");
+    if (pol && std::strcmp(pol, "uuid") == 0) {
+        if (!key && key_len) return xc__set_error(XC_EINVAL, "null key");
+        uint64_t h = 1469598103934665603ull;  // FNV-1a 64
+        for (uint64_t i = 0; i < key_len; i++) h = (h ^ key[i]) * 1099511628211ull;
+        return devs[(size_t)(h % devs.size())];
+    }
+    return devs[(size_t)(g_placed.fetch_add(1) % devs.size())];
+}
 
 struct xc_encoder {
     xc_cache *cache;

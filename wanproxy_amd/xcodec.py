@@ -25,7 +25,7 @@ LIB_PATH = os.environ.get("XC_LIB_PATH") or os.path.join(HERE, "libxcodec_hip.so
 SEGMENT_LENGTH = 2048
 
 SYMBOLS = [
-    "xc_device_count", "xc_ctx_create", "xc_ctx_destroy", "xc_ctx_stream", "xc_ctx_sync",
+    "xc_device_count", "xc_device_place", "xc_ctx_device", "xc_ctx_create", "xc_ctx_destroy", "xc_ctx_stream", "xc_ctx_sync",
     "xc_cache_create", "xc_cache_destroy", "xc_cache_count", "xc_cache_snapshot", "xc_cache_filter_stats",
     "xc_cache_restore", "xc_cache_lookup", "xc_cache_enter", "xc_hash_segments",
     "xc_window_hashes", "xc_encode_plan_create", "xc_plan_destroy", "xc_plan_layout",
@@ -97,6 +97,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.xc_ctx_stream.restype = _vp
     lib.xc_ctx_stream.argtypes = [_vp]
     lib.xc_device_count.argtypes = [C.POINTER(C.c_int)]
+    lib.xc_device_place.argtypes = [_u8p, C.c_uint64, C.c_int]
+    lib.xc_ctx_device.argtypes = [_vp, C.POINTER(C.c_int)]
     lib.xc_ctx_create.argtypes = [C.c_int, C.POINTER(_vp)]
     lib.xc_ctx_destroy.argtypes = [_vp]
     lib.xc_ctx_sync.argtypes = [_vp]
