@@ -131,7 +131,8 @@ int xc_encode_poll(xc_plan *p, int *done);
 int xc_encode_wait(xc_plan *p);
 /* Finish the run in flight on the cache, if any (submitted with xc_encode_submit and not yet
  * finished by its poll / wait): blocks until it is done; the submitter's next xc_encode_poll /
- * xc_encode_wait then returns that run's status.  For synchronous callers that met XC_EBUSY (the
+ * xc_encode_wait then returns that run's status (until then a submit on that plan fails with
+ * XC_EBUSY, so the status cannot be lost).  For synchronous callers that met XC_EBUSY (the
  * drop-in facade): the reference's encoder has no busy state to report. */
 int xc_cache_quiesce(xc_cache *c);
 /* The caller guarantees that the input arena a run is submitted with is complete when the submit is

@@ -78,6 +78,32 @@ def test_error_paths(gpu_ctx, oracle_mod):
     _check(gpu_ctx, oracle_mod, streams)
 
 
+def test_output_overflow_leaves_the_cache_unchanged(gpu_ctx, oracle_mod):
+    """A batch whose middle stream's output overflows its capacity fails with XC_EINVAL and enters
+    nothing: no EXTRACT of any stream of the batch is found afterwards (the slots of the overflowing
+    stream's later EXTRACTs were never written), and the same batch with room decodes as the oracle
+    does."""
+    import wanproxy_amd as w
+    segs = [W.gen(0x7700 + i, 2048) for i in range(8)]
+    ext = [b"\xf1\x01" + s.tobytes() for s in segs]
+    streams = [b"a" + ext[0], b"b" + b"".join(ext[1:6]) + b"c", b"d" + ext[6] + ext[7]]
+    gc = w.XCodecCache(gpu_ctx, 1 << 12)
+    dec = w.XCodecDecoder(gc)
+    seed = [W.gen(0x7800, 2048)]
+    assert dec.decode_batch([b"\xf1\x01" + seed[0].tobytes()])[0][0] == 1
+    n0 = len(gc)
+    with pytest.raises(Exception, match="capacity"):
+        dec.decode_batch(streams, out_cap=3 * 2048)
+    assert len(gc) == n0
+    for s in segs:
+        assert gc.lookup(int(oracle_mod.hash_segment(s))) is None
+    assert gc.lookup(int(oracle_mod.hash_segment(seed[0]))) is not None
+    oc = oracle_mod.Cache()
+    oc.decode_batch([b"\xf1\x01" + seed[0].tobytes()])
+    assert dec.decode_batch(streams) == oc.decode_batch(streams)
+    assert len(gc) == len(oc)
+
+
 def test_cross_stream_order(gpu_ctx, oracle_mod):
     a, b, c = W.gen(40, 2048), W.gen(41, 2048), W.gen(42, 2048)
     ha, hb, hc = (oracle_mod.hash_segment(s) for s in (a, b, c))

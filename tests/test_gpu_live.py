@@ -195,3 +195,84 @@ def test_first_sub_batch_hashed_ahead(gpu_ctx, oracle_mod, monkeypatch):
     assert sum(early) >= 4, (early, redone)
     assert len(cache) == len(oc)
     r.close()
+
+
+def test_two_caches_replay_from_two_threads(gpu_ctx, oracle_mod):
+    """Two caches (two contexts) driven from two host threads at once, as two proxies' event threads
+    would (include/xcodec_hip.h: one context per thread): both replay their runs' lookup hits into
+    their recent windows through the process's one helper pool (runs of >= 1024 buffers use it).  One
+    run at a time owns the helpers, the other replays on its own thread; neither waits forever, and
+    every buffer of both equals the oracle's."""
+    import threading
+    import wanproxy_amd as w
+    pool = W.pool(256)
+    warm = [pool[i:i + 65536] for i in range(0, len(pool), 65536)]
+    res = {}
+
+    def drive(k):
+        try:
+            ctx = w.Context(0)
+            cache = w.XCodecCache(ctx, 1 << 14)
+            oc = oracle_mod.Cache()
+            w.XCodecEncoder(cache).encode_batch(warm)
+            oc.encode_batch(warm)
+            r = Runner(cache)
+            before = cache.hit_stats()
+            for run in range(3):
+                bufs = W.repeat_buffers(1100, 0x6500 + 16 * k + run, slots=4, np_segments=256, pool_bytes=pool)
+                _same(r.run(bufs), oc.encode_batch(bufs), f"thread {k} run {run}")
+            cache.settle()
+            st = cache.hit_stats()
+            assert st["runs"] - before["runs"] >= 3 and st["hits"] > before["hits"], st
+            assert len(cache) == len(oc)
+            r.close()
+            res[k] = "ok"
+        except BaseException as e:  # noqa: BLE001 (reported below)
+            res[k] = repr(e)
+
+    ts = [threading.Thread(target=drive, args=(k,)) for k in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(240)
+    assert not any(t.is_alive() for t in ts), "a replay did not finish"
+    assert res == {0: "ok", 1: "ok"}, res
+
+
+def test_quiesced_run_status_is_not_dropped(gpu_ctx, oracle_mod):
+    """A run finished by another caller (xc_cache_quiesce, the facade's answer to XC_EBUSY) parks its
+    status for its submitter: a new submit on that plan fails with XC_EBUSY until the submitter's
+    poll / wait took the status; then runs go on, every buffer equal to the oracle's."""
+    import torch
+    import wanproxy_amd as w
+    pool = W.pool(128)
+    cache = w.XCodecCache(gpu_ctx, 1 << 12)
+    oc = oracle_mod.Cache()
+    warm = [pool[i:i + 65536] for i in range(0, len(pool), 65536)]
+    w.XCodecEncoder(cache).encode_batch(warm)
+    oc.encode_batch(warm)
+    bufs = W.repeat_buffers(24, 0x6600, np_segments=128, pool_bytes=pool)
+    plan = w.EncodePlan(cache, [len(b) for b in bufs])
+    arena = np.zeros(plan.in_bytes, np.uint8)
+    for i, b in enumerate(bufs):
+        arena[int(plan.in_off[i]):int(plan.in_off[i]) + len(b)] = b
+    d_in = torch.from_numpy(arena).cuda()
+    d_out = torch.zeros(plan.out_bytes, dtype=torch.uint8, device="cuda")
+    d_len = torch.zeros(len(bufs), dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+
+    def outputs():
+        torch.cuda.synchronize()
+        out, lens = d_out.cpu().numpy(), d_len.cpu().numpy()
+        return [out[int(plan.out_off[i]):int(plan.out_off[i]) + int(lens[i])].tobytes() for i in range(len(bufs))]
+
+    plan.submit(d_in.data_ptr(), d_out.data_ptr(), d_len.data_ptr())
+    cache.quiesce()                                    # another caller finishes the run
+    with pytest.raises(w.XCodecError, match="-16"):    # the status is parked: no new run yet
+        plan.submit(d_in.data_ptr(), d_out.data_ptr(), d_len.data_ptr())
+    assert plan.poll()                                 # the submitter takes it
+    _same(outputs(), oc.encode_batch(bufs), "quiesced run")
+    plan.submit(d_in.data_ptr(), d_out.data_ptr(), d_len.data_ptr())
+    plan.wait()
+    _same(outputs(), oc.encode_batch(bufs), "next run")
+    plan.close()

@@ -1066,6 +1066,7 @@ using namespace xc;
 // The cache object is defined in xc_runtime.hip; these accessors expose what we need.
 extern "C" void xc__cache_count_unknown(xc_cache *c);
 extern "C" int64_t xc__cache_host_count(xc_cache *c);
+extern "C" int xc__cache_truncate(xc_cache *c, uint64_t keep);
 extern "C" void xc__cache_set_host_count(xc_cache *c, int64_t n);
 extern "C" int xc__cache_reserve(xc_cache *c, uint64_t extra);
 extern "C" uint32_t xc__cache_gen(xc_cache *c);
@@ -1231,9 +1232,12 @@ extern "C" int xc_decode_plan_create(xc_cache *c, const uint64_t *in_len, const 
     DA(&D.tok_cnt, ns); DA(&D.s_stop, ns); DA(&D.s_slot, ns); DA(&D.s_cnt, ns); DA(&D.s_lim, ns); DA(&D.ctl, DCTL_WORDS);
     DA(&D.t_lb, ntok); DA(&D.t_le, ntok); DA(&D.t_op, ntok); DA(&D.t_stat, ntok); DA(&D.t_h, ntok);
     DA(&D.t_src, ntok);
+    // The batch provider tables (two when the parse runs ahead, dsets[1] below) are keys and values
+    // only: prov_insert / set_find / dset_clear_range read nothing else.  Their filter and lo32 arrays
+    // stay null, so set_insert / set_has_lo on them would fault at once rather than probe stale words.
     DevSet &ds = D.dset;
-    DA(&ds.filt, XC_FILT_WORDS); DA(&ds.l2, 2 * (size_t)XC_L2_WORDS); DA(&ds.lo_keys, p->n_lo);
-    DA(&ds.lo_zero, 1); DA(&ds.keys, p->n_full); DA(&ds.vals, p->n_full);
+    ds.filt = nullptr; ds.l2 = nullptr; ds.lo_keys = nullptr; ds.lo_zero = nullptr;
+    DA(&ds.keys, p->n_full); DA(&ds.vals, p->n_full);
 #undef DA
     ds.mask = p->n_full - 1;
     ds.lo_mask = p->n_lo - 1;
@@ -1311,9 +1315,7 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
                 return ra;  // (what was allocated goes with the plan)
             DevSet &d1 = p->dsets[1];
             d1 = p->dsets[0];
-            if ((ra = p->alloc(&d1.filt, XC_FILT_WORDS)) || (ra = p->alloc(&d1.l2, 2 * (size_t)XC_L2_WORDS)) ||
-                (ra = p->alloc(&d1.lo_keys, p->n_lo)) || (ra = p->alloc(&d1.lo_zero, 1)) ||
-                (ra = p->alloc(&d1.keys, p->n_full)) || (ra = p->alloc(&d1.vals, p->n_full)))
+            if ((ra = p->alloc(&d1.keys, p->n_full)) || (ra = p->alloc(&d1.vals, p->n_full)))  // (keys, values)
                 return ra;
             DHIP(hipEventCreateWithFlags(&p->ev_parsed, hipEventDisableTiming));
             DHIP(hipEventCreateWithFlags(&p->ev_free, hipEventDisableTiming));
@@ -1475,7 +1477,21 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
         hipStreamSynchronize(s);
         return xc__set_error(XC_ENOSPC, "device cache capacity exhausted");
     }
-    if (ctl[DCTL_ERR] & 1u) return xc__set_error(XC_EINVAL, "output capacity too small");
+    if (ctl[DCTL_ERR] & 1u) {
+        // An output overflowed: k_demit stopped that stream's copies, so some of the slots k_dfin gave
+        // its ENTER tokens were never filled.  The run is rolled back whole: the cache is left as it
+        // was before the call (the tables rebuilt from the first count0 entries, as a COSS roll back
+        // does), and no hit of the run reaches the recent window.
+        DHIP(hipStreamSynchronize(s));
+        int64_t before = count0;
+        if (before < 0) {
+            uint64_t n = 0;
+            if ((rc = xc_cache_count(p->cache, &n))) return rc;
+            before = (int64_t)n - (int64_t)ctl[DCTL_NENTER];
+        }
+        if (ctl[DCTL_NENTER] && (rc = xc__cache_truncate(p->cache, (uint64_t)before))) return rc;
+        return xc__set_error(XC_EINVAL, "output capacity too small");
+    }
     // (k_dfin advanced the count by exactly the entered segments: a later restore or reserve
     // needs no device read)
     if (count0 >= 0) xc__cache_set_host_count(p->cache, count0 + ctl[DCTL_NENTER]);

@@ -481,6 +481,9 @@ public:
         return p;
     }
     int threads() const { return nthreads; }
+    // One run at a time owns the helpers (caches of different contexts may be driven from different
+    // host threads): xc__mem_hits_run holds this from its launch until every job it launched is done.
+    std::mutex &owner() { return own; }
     // run job(j) for j in [0, n) on the helpers; done[j] is set (release) as each finishes
     void launch(uint32_t n, std::function<void(uint32_t)> job, std::atomic<int> *done)
     {
@@ -530,7 +533,7 @@ private:
             }
         }
     }
-    std::mutex mu;
+    std::mutex mu, own;
     std::condition_variable cv;
     std::function<void(uint32_t)> fn;
     std::atomic<int> *flags = nullptr;
@@ -553,7 +556,10 @@ extern "C" void xc__mem_hits_run(xc_memmodel *m, const uint64_t *h, const uint32
     for (uint32_t b = 0; b < nb; b++)
         if (R.rec(b)[0] >> 63) m->valid = false;
     ReplayPool *pool = m->st.dups.empty() && nb >= 1024 ? ReplayPool::get() : nullptr;
-    const uint32_t nt = pool ? (uint32_t)pool->threads() : 0u;
+    // (another cache's replay holds the helpers: this one runs on the calling thread alone)
+    std::unique_lock<std::mutex> own;
+    if (pool) own = std::unique_lock<std::mutex>(pool->owner(), std::try_to_lock);
+    const uint32_t nt = pool && own.owns_lock() ? (uint32_t)pool->threads() : 0u;
     if (!nt) {
         for (uint32_t b = 0; b < nb; b++) {
             const uint64_t *r = R.rec(b);

@@ -2634,8 +2634,11 @@ static int launch_tailcheck(xc_plan *p);
 // Everything of a run up to its first asynchronous pass, which is enqueued with ev_ctl after it.
 static int encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_out_len)
 {
-    if (p) p->parked = false;
     if (p && p->inflight) return fail(XC_EBUSY, "a run of this plan is in flight (xc_encode_poll / xc_encode_wait)");
+    // (a run another caller finished, xc_cache_quiesce: its status waits for the submitter's poll /
+    // wait, which alone clears it, so that no failure of it is dropped)
+    if (p && p->parked)
+        return fail(XC_EBUSY, "a finished run's status waits for xc_encode_poll / xc_encode_wait");
     if (!p || (!d_in && p->nb) || (!d_out && p->nb) || (!d_out_len && p->nb)) return fail(XC_EINVAL, "null");
     int rc = set_dev(p->cache->ctx);
     if (rc) return rc;
