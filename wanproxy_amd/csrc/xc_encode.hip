@@ -1412,11 +1412,14 @@ constexpr uint32_t ANC_LIST = 512;  // anchor list entries per pass (a multiple 
 // (list: ANC_LIST entries per wave, in passes), then every input anchor into the group's records, 64 list entries
 // at a time (runs of equal fingerprints at consecutive positions, at most 32 and within a 32-byte
 // lane part, as one record); returns, in lane i, the anchor key of full block i (its last anchor at
-// block offset >= 63; ANC_NONE: none).
+// block offset >= 63; ANC_NONE: none).  drop: blocks whose records are not written (bit i: block i
+// and the one before it are cached, so every proposal of its anchors falls on an aligned window or in
+// the shadow of a predicted REF, which k_aprop skips anyway; the group's anchor record and gaps still
+// count them).
 __device__ __forceinline__ uint64_t group_anchors(const PlanDev &P, uint32_t g, uint32_t k0, uint32_t len,
                                                   uint32_t n, uint32_t na, const uint8_t *base,
                                                   const uint32_t (&w)[BLK_GROUP][8], uint32_t *tile,
-                                                  uint16_t *list, uint32_t abl)
+                                                  uint16_t *list, uint32_t abl, uint32_t drop)
 {
     const uint32_t l = lane_id();
     uint32_t *prev = tile + 32u * XC_TILE_ROW;
@@ -1459,7 +1462,7 @@ __device__ __forceinline__ uint64_t group_anchors(const PlanDev &P, uint32_t g, 
             if (l < 32u) prev[l] = tile[l * XC_TILE_ROW + 63u];
             wave_sync();
         }
-        if (l == 0) P.rec_blk[g * BLK_GROUP + i] = min(cnt, REC_CAP);
+        const bool keep = !((drop >> i) & 1u);
         // (timing ablations, XC_ABL_BH: 8 = no G tile, 4 = no anchor list / records)
         uint32_t m = (abl & 8u) ? gear_mask<false>(wi, gi, nullptr) : gear_mask<true>(wi, gi, tile);
         if (abl & 12u) {
@@ -1508,11 +1511,13 @@ __device__ __forceinline__ uint64_t group_anchors(const PlanDev &P, uint32_t g, 
             const uint64_t above = heads & (l == 63u ? 0ull : ~0ull << (l + 1u));
             const uint32_t end = above ? b0 + (uint32_t)__builtin_ctzll(above) : min(total, b0 + 64u);
             const bool head = live && !cont;
-            if (head) {
-                const uint32_t ri = cnt + mbcnt(heads);
-                if (ri < REC_CAP) P.rec[(size_t)g * REC_CAP + ri] = rec_make(fp, i * XC_SEG + p, end - idx);
+            if (keep) {
+                if (head) {
+                    const uint32_t ri = cnt + mbcnt(heads);
+                    if (ri < REC_CAP) P.rec[(size_t)g * REC_CAP + ri] = rec_make(fp, i * XC_SEG + p, end - idx);
+                }
+                cnt += (uint32_t)__popcll(heads);
             }
-            cnt += (uint32_t)__popcll(heads);
             const uint32_t last = min(total - b0, 64u) - 1u;
             cp = readlane(p, (int)last);
             cfp = readlane64(fp, (int)last);
@@ -1551,7 +1556,6 @@ __device__ __forceinline__ uint64_t group_anchors(const PlanDev &P, uint32_t g, 
         const bool chk = ngap || lastp == NONE || firstp >= 993u || span - 1u - lastp >= 993u;
         P.ainfo[g] = make_uint4(firstp, lastp, ngap, chk ? 1u : 0u);
         P.rec_cnt[g] = (cnt <= REC_CAP ? cnt : (REC_OVF | REC_CAP)) | (chk ? REC_GAP : 0u);
-        for (uint32_t i = na; i < BLK_GROUP; i++) P.rec_blk[g * BLK_GROUP + i] = min(cnt, REC_CAP);
     }
     return bkey;
 }
@@ -1580,26 +1584,34 @@ __global__ __launch_bounds__(256, 4) void k_blockhash(DeclArgs a)
     if (ANC && (a.nt & 1)) wave_load_blocks<BLK_GROUP, true>(base + (size_t)k0 * XC_SEG, na, w);
     else wave_load_blocks<BLK_GROUP>(base + (size_t)k0 * XC_SEG, na, w);
     const uint64_t h = block_group_hash<BLK_GROUP>(w);
+    const uint32_t l = lane_id();
+    const uint32_t gi = P.blk_base[b] + k0 + l;
+    uint32_t cmp = 0;  // the cached slot + 1 to compare the block with (blk_cmp)
+    if (!PREDICT && l < n && a.limit && !stream_carried(P, b)) {
+        // (a concurrent k_alloc may be entering keys: only complete entries are compared)
+        uint64_t v;
+        if (set_find(P.cache, h, &v) && (uint32_t)v < *a.limit) cmp = (uint32_t)v + 1u;
+    }
+    // blocks cached with the block before them cached too (entries complete at the run's start are
+    // also found by k_blockpredict: these blocks are predicted REFs after a predicted REF)
+    uint32_t drop = 0;
+    if (ANC && !PREDICT && a.drop_shadowed) {
+        const uint32_t m = (uint32_t)ballot(cmp != 0u);
+        drop = m & (m << 1);
+    }
     uint64_t akey = ANC_NONE;
     // XC_ABL_BH (timing ablations only: the results are wrong; in builds with -DXC_ABLATIONS=1):
     // 2 = no anchors at all
     const uint32_t abl = XC_ABLATIONS ? (uint32_t)a.nt & ~1u : 0u;
     if (ANC && !(abl & 2u))
         akey = group_anchors(P, g, k0, len, n, na, base, w, tiles[(threadIdx.x >> 6) & (ANC ? 3 : 0)],
-                             lists[(threadIdx.x >> 6) & (ANC ? 3 : 0)], abl);
-    const uint32_t l = lane_id();
-    const uint32_t gi = P.blk_base[b] + k0 + l;
-    uint32_t cmp = 0;  // the cached slot + 1 to compare the block with (blk_cmp)
+                             lists[(threadIdx.x >> 6) & (ANC ? 3 : 0)], abl, drop);
     if (l < n) {
         P.blk_h[gi] = h;
         if (ANC) P.blk_anc[gi] = akey;
         if (PREDICT) {
             const uint32_t pref = block_predict(P, gi, b, k0 + l, h, akey);
             if (blk_cached(pref)) cmp = pref;
-        } else if (a.limit && !stream_carried(P, b)) {
-            // (a concurrent k_alloc may be entering keys: only complete entries are compared)
-            uint64_t v;
-            if (set_find(P.cache, h, &v) && (uint32_t)v < *a.limit) cmp = (uint32_t)v + 1u;
         }
     }
     // the compares of a predicted REF's bytes, off k_resolve's critical path, against the block

@@ -164,7 +164,6 @@ struct PlanDev {
     uint64_t *blk_anc;         // [blocks] anchor key of every aligned block (k_blockhash)
     uint64_t *rec;             // [groups * REC_CAP] input anchors: fp << 19 | group position << 5 | run - 1
     uint32_t *rec_cnt;         // [groups] records (| REC_OVF: more than REC_CAP)
-    uint32_t *rec_blk;         // [groups * 8] the first record of each block of the group
     uint4 *ainfo;              // [groups] first and last input anchor (group-relative, NONE: none), gaps
     uint2 *agap;               // [groups * AGAP_CAP] anchors >= 1986 apart inside the group (k_aprop's gaps)
     const uint32_t *buf_grp0;  // [nb + 1] first k_blockhash group of every buffer
@@ -266,6 +265,10 @@ struct DeclArgs {
     // runs (P.sb_count of the sub-batch the main stream is in); null: no block compares
     const uint32_t *limit;
     int nt;  // k_blockhash<.., true>: non-temporal block loads (XC_BH_NT, experiments)
+    // k_blockhash<false, true> with compares (limit): no anchor records for a block whose block and
+    // the one before are cached (every proposal of them would fall on an aligned window or in a
+    // predicted REF's shadow; the async pass's shadows are on: xc_plan.shadow)
+    int drop_shadowed;
 };
 struct EmitArgs {
     PlanDev P;

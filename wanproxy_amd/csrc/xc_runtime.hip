@@ -1354,7 +1354,7 @@ struct xc_plan {
     uint64_t ngroups = 0, nblocks = 0;
     uint32_t *d_buf_grp0 = nullptr;
     uint64_t *d_rec = nullptr, *d_blk_anc = nullptr;
-    uint32_t *d_rec_cnt = nullptr, *d_amix = nullptr, *d_rec_blk = nullptr;
+    uint32_t *d_rec_cnt = nullptr, *d_amix = nullptr;
     uint4 *d_ainfo = nullptr;
     uint2 *d_agap = nullptr;
     uint32_t *d_tcnt = nullptr;  // the tail check's collision lists (k_tailcheck / k_tailfinal)
@@ -1878,7 +1878,6 @@ extern "C" int xc_plan_destroy(xc_plan *p)
     dfree(p->d_buf_grp0);
     dfree(p->d_rec);
     dfree(p->d_rec_cnt);
-    dfree(p->d_rec_blk);
     dfree(p->d_ainfo);
     dfree(p->d_agap);
     dfree(p->d_tcnt);
@@ -2034,10 +2033,8 @@ static int plan_anchor_setup(xc_plan *p)
         if (!p->d_rec) {
             HIPCHK(dmalloc(&p->d_rec, std::max<uint64_t>(p->ngroups, 1) * REC_CAP * 8));
             HIPCHK(dmalloc(&p->d_rec_cnt, std::max<uint64_t>(p->ngroups, 1) * 4));
-            HIPCHK(dmalloc(&p->d_rec_blk, std::max<uint64_t>(p->ngroups, 1) * BLK_GROUP * 4));
             HIPCHK(dmalloc(&p->d_ainfo, std::max<uint64_t>(p->ngroups, 1) * sizeof(uint4)));
             HIPCHK(dmalloc(&p->d_agap, std::max<uint64_t>(p->ngroups, 1) * AGAP_CAP * sizeof(uint2)));
-            HIPCHK(hipMemsetAsync(p->d_rec_blk, 0, std::max<uint64_t>(p->ngroups, 1) * BLK_GROUP * 4, s));
             HIPCHK(dmalloc(&p->d_tcnt, std::max<uint64_t>(p->nb, 1) * 4));
             HIPCHK(hipMemsetAsync(p->d_tcnt, 0, std::max<uint64_t>(p->nb, 1) * 4, s));
             HIPCHK(dmalloc(&p->d_tlist, std::max<uint64_t>(p->nb, 1) * COLL_CAP * sizeof(uint4)));
@@ -2050,7 +2047,6 @@ static int plan_anchor_setup(xc_plan *p)
             p->dset.a.filt = p->d_amix;
             p->P.rec = p->d_rec;
             p->P.rec_cnt = p->d_rec_cnt;
-            p->P.rec_blk = p->d_rec_blk;
             p->P.ainfo = p->d_ainfo;
             p->P.agap = p->d_agap;
             p->P.blk_anc = p->d_blk_anc;
@@ -2389,7 +2385,7 @@ static int enqueue_block_hash(xc_plan *p, uint32_t k, hipEvent_t after, hipStrea
     const char *abl_bh = getenv("XC_ABL_BH");
     const int nt_abl = bh_nt | (abl_bh ? atoi(abl_bh) & ~1 : 0);
     DeclArgs d{p->P, g0, g1, limit ? limit : side && k > 0 ? p->P.sb_count + (bh_gated() ? k - 1 : 0) : nullptr,
-               nt_abl};
+               nt_abl, p->shadow};
     // XC_ABL_SKIP_BLOCKHASH=1 (timing experiments only, valid when every run reads the same input):
     // the side stream's block hashing after the plan's first run is skipped
     static const bool skip = getenv("XC_ABL_SKIP_BLOCKHASH") && atoi(getenv("XC_ABL_SKIP_BLOCKHASH"));
