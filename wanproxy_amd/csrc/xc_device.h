@@ -596,6 +596,21 @@ __device__ __forceinline__ int set_insert(const DevSet &s, uint64_t h, uint64_t 
     return fresh;
 }
 
+// set_insert into the keys and values alone (no filter bits, no lo32 key): a declaration set read
+// only through set_find (an anchor-scanned sub-batch's, block_predict); values atomicMin-merged.
+__device__ __forceinline__ void set_insert_kv(const DevSet &s, uint64_t h, uint64_t val, uint32_t *slot_out)
+{
+    uint32_t i = key_slot(h, s.mask);
+    for (;;) {
+        const uint64_t prev = atomicCAS((unsigned long long *)&s.keys[i], (unsigned long long)XC_EMPTY64,
+                                        (unsigned long long)h);
+        if (prev == XC_EMPTY64 || prev == h) break;
+        i = (i + 1u) & s.mask;
+    }
+    atomicMin((unsigned long long *)&s.vals[i], (unsigned long long)val);
+    *slot_out = i;
+}
+
 // ---- anchor index -----------------------------------------------------------------
 // A content-defined index that finds every window equal to an indexed segment without testing
 // every window end against the key set.  G(p) = sum_{k<32} b[p-k] 2^k mod 2^32

@@ -1668,11 +1668,19 @@ __device__ __forceinline__ uint32_t block_predict(const PlanDev &P, uint32_t g, 
     } else if (set_find(P.cache, h, &v)) {
         pref = (uint32_t)v + 1u;  // (cache capacity <= 2^28: bit 31 stays free)
     } else {
-        // (the set's level-2 filter is P.l2mix, the combined filter the scan reads)
         uint32_t slot;
-        set_insert(P.dset, h, ((uint64_t)b << 32) | (k * XC_SEG + 2u * XC_SEG - 1u), true, &slot, nullptr);
-        const uint32_t lo = (uint32_t)h;  // (the combined level-1 image the first scan loads)
-        atomicOr(&P.fmix[filt_word_n(lo, XC_FILT_WORDS >> P.fmix_fold)], filt_mask(lo));
+        const uint64_t val = ((uint64_t)b << 32) | (k * XC_SEG + 2u * XC_SEG - 1u);
+        if (P.anc_scan) {
+            // an anchor-scanned sub-batch reads the set's keys and values only (k_aprop proposes
+            // through the anchor table, k_resolve and k_walk look keys up); its filters and lo32
+            // keys serve the exact scan, which a redo of the sub-batch runs after clearing the set
+            set_insert_kv(P.dset, h, val, &slot);
+        } else {
+            // (the set's level-2 filter is P.l2mix, the combined filter the scan reads)
+            set_insert(P.dset, h, val, true, &slot, nullptr);
+            const uint32_t lo = (uint32_t)h;  // (the combined level-1 image the first scan loads)
+            atomicOr(&P.fmix[filt_word_n(lo, XC_FILT_WORDS >> P.fmix_fold)], filt_mask(lo));
+        }
         if (P.anc_scan) {
             // the anchor scan finds windows equal to this block through its anchor (a block
             // without a level-0 anchor: a later level's, found through the gap windows)
@@ -2193,6 +2201,8 @@ __global__ __launch_bounds__(64) void k_window_hashes(const uint8_t *in, uint32_
 
 // Clear a declaration set (all of its tables) and seed the combined level-2 filter with the
 // cache's: one launch instead of a memset per table.
+// With amix (an anchor-scanned sub-batch, whose set is keys and values only: block_predict) the
+// filters, the lo32 keys and the combined level-1 / level-2 images are left alone.
 __global__ void k_clear_set(DevSet s, uint32_t n_lo, uint32_t n_full, uint4 *l2mix, const uint4 *cache_l2,
                             uint32_t *fmix, const uint32_t *cache_filt, uint32_t fold, const uint32_t *count,
                             uint32_t *count_out, uint32_t *ctl_zero, AncSet danc, uint4 *amix, const uint4 *cache_afilt)
@@ -2211,18 +2221,20 @@ __global__ void k_clear_set(DevSet s, uint32_t n_lo, uint32_t n_full, uint4 *l2m
     // kernels after this one)
     if (ctl_zero && i0 < CTL_WORDS) ctl_zero[i0] = 0u;
     const uint4 z = make_uint4(0, 0, 0, 0), ones = make_uint4(~0u, ~0u, ~0u, ~0u);
-    for (uint32_t i = i0; i < XC_FILT_WORDS / 4; i += stride) ((uint4 *)s.filt)[i] = z;
-    const bool own_l2 = (const void *)s.l2 != (const void *)l2mix;  // (plans alias the two)
-    for (uint32_t i = i0; i < XC_L2_WORDS / 2; i += stride) {
-        if (own_l2) ((uint4 *)s.l2)[i] = z;
-        l2mix[i] = cache_l2[i];
+    if (!amix) {
+        for (uint32_t i = i0; i < XC_FILT_WORDS / 4; i += stride) ((uint4 *)s.filt)[i] = z;
+        const bool own_l2 = (const void *)s.l2 != (const void *)l2mix;  // (plans alias the two)
+        for (uint32_t i = i0; i < XC_L2_WORDS / 2; i += stride) {
+            if (own_l2) ((uint4 *)s.l2)[i] = z;
+            l2mix[i] = cache_l2[i];
+        }
+        for (uint32_t i = i0; i < n_lo / 4; i += stride) ((uint4 *)s.lo_keys)[i] = z;
+        if (i0 == 0) *s.lo_zero = 0u;
     }
-    for (uint32_t i = i0; i < n_lo / 4; i += stride) ((uint4 *)s.lo_keys)[i] = z;
     for (uint32_t i = i0; i < n_full / 2; i += stride) {
         ((uint4 *)s.keys)[i] = ones;
         ((uint4 *)s.vals)[i] = ones;
     }
-    if (i0 == 0) *s.lo_zero = 0u;
     // an anchor-scanned sub-batch: the declarations' anchor table empty, the combined anchor
     // filter seeded with the cache's
     if (amix) {

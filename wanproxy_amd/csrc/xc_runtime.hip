@@ -2415,7 +2415,8 @@ static int launch_first_round(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t s1,
     // the set's clear (and, first in a run, the control words' clear)
     const bool anc = p->P.anc_scan != 0;
     hipLaunchKernelGGL(k_clear_set, dim3(1024), dim3(256), 0, s, p->P.dset, p->dset.n_lo, p->dset.n_full,
-                       (uint4 *)p->d_l2mix, (const uint4 *)p->P.cache.l2, p->d_fmix, (const uint32_t *)p->P.cache.filt,
+                       (uint4 *)p->d_l2mix, (const uint4 *)p->P.cache.l2, anc ? nullptr : p->d_fmix,
+                       (const uint32_t *)p->P.cache.filt,
                        p->P.fmix_fold, p->P.seg_count, p->P.sb_count + sb, p->zero_ctl ? p->P.ctl : nullptr,
                        p->dset.a, anc ? (uint4 *)p->d_amix : nullptr, (const uint4 *)p->P.canc.filt);
     HIPCHK(hipGetLastError());
