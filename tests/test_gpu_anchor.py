@@ -190,13 +190,19 @@ def test_anchor_index_restore_growth_and_backfill(gpu_ctx, oracle_mod):
         _same(got, snap.clone().encode_batch(again))
 
 
-def test_anchor_scan_recent_window_after_collisions(gpu_ctx, oracle_mod):
+@pytest.mark.parametrize("wide", [False, True])
+def test_anchor_scan_recent_window_after_collisions(gpu_ctx, oracle_mod, monkeypatch, wide):
     """The recent window remembers collision lookups that an anchor scan does not look for (a
     pending candidate makes them irrelevant to the bytes); the tail check finds the run's last ones
     again.  A stateful connection's carried candidate y is declared after x (same hash) was entered
     and y's windows were looked up (collisions, remembering x's entry): the map then answers y and
-    the window x (xcodec_cache.h:137-147,182-188), as in the oracle."""
+    the window x (xcodec_cache.h:137-147,182-188), as in the oracle.  wide: run (c) also carries
+    20000 small buffers in two sub-batches of > 8192 buffers, so that its cache enters run in
+    k_insert and the tail check's probes beside its last emit on the side stream (xc_runtime.hip
+    tail_check_side), the compares behind it."""
     import wanproxy_amd as w
+    if wide:
+        monkeypatch.setenv("XC_SUB_MB", "1")
     x, y = _collision_pair(5, in_anchor=True)
     cache = w.XCodecCache(gpu_ctx, 1 << 12)
     oc = oracle_mod.Cache()
@@ -209,9 +215,13 @@ def test_anchor_scan_recent_window_after_collisions(gpu_ctx, oracle_mod):
     _same(_plan_run(gpu_ctx, cache, b)[0], oc.encode_batch(b))
     # (c) y's windows looked up while a candidate is pending: collisions with x (remembered)
     c = [np.concatenate([W.gen(93, 1000), y, W.gen(94, 3000)]), W.gen(95, 9000)]
+    if wide:
+        c += [W.gen(0x9500 + i, 100) for i in range(20000)]
     got, st = _plan_run(gpu_ctx, cache, c)
     _same(got, oc.encode_batch(c))
     assert st.anchor_scans >= 1
+    if wide:
+        assert st.sub_batches >= 2 and st.redone == 0, (st.sub_batches, st.redone)
     # (d) y declared: the hash entered twice (map: y, window: x)
     d = W.gen(96, 4096)
     assert gs.encode(d) == os_.encode(d)
