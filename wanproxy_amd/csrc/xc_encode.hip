@@ -587,9 +587,53 @@ __device__ __forceinline__ void gap_probe(const PlanDev &P, const AScanArgs &a, 
     }
 }
 
+// The proposals of record r (fingerprint fp, its positions) for the indexed key (fp, j).
+__device__ __forceinline__ void propose_key(const PlanDev &P, const AScanArgs &a, uint64_t key, uint32_t ap,
+                                            uint32_t nr, uint32_t len, uint32_t ck0, uint32_t cblk)
+{
+    const uint32_t j = (uint32_t)key & 2047u;
+    for (uint32_t e = 0; e < nr; e++) {
+        const uint32_t aa = ap + e, q = aa + (XC_SEG - 1u) - j;
+        if (aa < j || q >= len || ((q + 1u) & (XC_SEG - 1u)) == 0u) continue;
+        // REF shadow: the 2047 window ends after a predicted REF are not looked up
+        if (a.shadow && q >= XC_SEG && blk_cached(P.blk_pref[cblk + (q >> 11) - 1u])) continue;
+        const uint32_t c = ck0 + q / P.chunk_len;
+        const uint32_t slot = atomicAdd(&a.pcnt[c], 1u);
+        if (slot < PROP_CAP) a.pq[(size_t)c * PROP_CAP + slot] = q;
+    }
+}
+
+// A record that passed the combined filter: the cache's and the declarations' anchor tables, both
+// chains walked together (their loads in flight at once), every key with its fingerprint proposing.
+__device__ __forceinline__ void aprop_probe(const PlanDev &P, const AScanArgs &a, uint64_t r, uint2 gr)
+{
+    const uint64_t fp = r >> 19;
+    const uint32_t b = gr.x, gpos = gr.y * XC_SEG;
+    const uint32_t len = P.buf_len[b], ck0 = P.buf_chunk0[b], cblk = P.blk_base[b];
+    const uint32_t ap = gpos + (((uint32_t)r >> 5) & 0x3FFFu), nr = ((uint32_t)r & 31u) + 1u;
+    uint32_t kc = anc_home(fp, P.canc.mask), kd = anc_home(fp, P.danc.mask);
+    uint64_t yc = P.canc.keys[kc], yd = P.danc.keys[kd];
+    while (yc != XC_EMPTY64 || yd != XC_EMPTY64) {
+        if (yc != XC_EMPTY64) {
+            if ((yc >> 11) == fp) propose_key(P, a, yc, ap, nr, len, ck0, cblk);
+            kc = (kc + 1u) & P.canc.mask;
+            yc = P.canc.keys[kc];
+        }
+        if (yd != XC_EMPTY64) {
+            if ((yd >> 11) == fp) propose_key(P, a, yd, ap, nr, len, ck0, cblk);
+            kd = (kd + 1u) & P.danc.mask;
+            yd = P.danc.keys[kd];
+        }
+    }
+}
+
 // (APROP_GROUPS groups per workgroup, xc_kernels.h: every thread's record and filter loads of all
 // of them in flight together; one group per workgroup left the kernel latency-bound, and 2 beat 4
 // and 8 once the side stream's block hashing ran beside it: cfg5 A/B +0.8 %, aprop 0.61 -> 0.53 ms)
+// A thread's records i and i + 256 of each group are loaded with the counts, before they are known
+// (REC_CAP >= 512: in bounds; the slots past a count are masked after): a group has ~200 records.
+constexpr uint32_t APROP_SPEC = 2;
+static_assert(REC_CAP >= 256u * APROP_SPEC, "k_aprop's speculative record loads stay in bounds");
 __global__ __launch_bounds__(256) void k_aprop(AScanArgs a)
 {
     const PlanDev &P = a.P;
@@ -600,11 +644,15 @@ __global__ __launch_bounds__(256) void k_aprop(AScanArgs a)
     const uint32_t g0 = a.g_lo + blockIdx.x * APROP_GROUPS;
     uint32_t cnt[APROP_GROUPS];
     uint2 gr[APROP_GROUPS];
+    uint64_t r[APROP_SPEC][APROP_GROUPS];
 #pragma unroll
     for (uint32_t k = 0; k < APROP_GROUPS; k++) {
         const bool ok = g0 + k < a.g_hi;
         cnt[k] = ok ? P.rec_cnt[g0 + k] : 0u;
         gr[k] = ok ? P.blk_grp[g0 + k] : make_uint2(0u, 0u);
+#pragma unroll
+        for (uint32_t u = 0; u < APROP_SPEC; u++)
+            r[u][k] = ok ? P.rec[(size_t)(g0 + k) * REC_CAP + 256u * u + threadIdx.x] : ~0ull;
     }
     uint32_t gflag = 0;  // groups whose anchor record k_aprop reads (REC_GAP)
 #pragma unroll
@@ -632,50 +680,33 @@ __global__ __launch_bounds__(256) void k_aprop(AScanArgs a)
         const uint32_t ng = min(uniform(G.n), GAP_MAX);
         for (uint32_t k = 0; k < ng; k++) gap_probe(P, a, G.b[k], G.lo[k], G.hi[k]);
     }
+    uint32_t fw[APROP_SPEC][APROP_GROUPS];
+#pragma unroll
+    for (uint32_t u = 0; u < APROP_SPEC; u++)
+#pragma unroll
+        for (uint32_t k = 0; k < APROP_GROUPS; k++) {
+            if (256u * u + threadIdx.x >= cnt[k]) r[u][k] = ~0ull;
+            fw[u][k] = P.amix[r[u][k] != ~0ull ? anc_fword(anc_mix(r[u][k] >> 19)) : 0u];
+        }
+#pragma unroll
+    for (uint32_t u = 0; u < APROP_SPEC; u++)
+#pragma unroll
+        for (uint32_t k = 0; k < APROP_GROUPS; k++)
+            if (r[u][k] != ~0ull && anc_ftest(fw[u][k], anc_mix(r[u][k] >> 19))) aprop_probe(P, a, r[u][k], gr[k]);
+    // (more than 512 records in a group: rare for random data)
     uint32_t cmax = 0;
 #pragma unroll
     for (uint32_t k = 0; k < APROP_GROUPS; k++) cmax = max(cmax, cnt[k]);
-    for (uint32_t i = threadIdx.x; i < cmax; i += 256u) {
-        uint64_t r[APROP_GROUPS];
-        uint32_t fw[APROP_GROUPS];
+    for (uint32_t i = 256u * APROP_SPEC + threadIdx.x; i < cmax; i += 256u) {
+        uint64_t rr[APROP_GROUPS];
+        uint32_t fv[APROP_GROUPS];
 #pragma unroll
-        for (uint32_t k = 0; k < APROP_GROUPS; k++) r[k] = i < cnt[k] ? P.rec[(size_t)(g0 + k) * REC_CAP + i] : ~0ull;
+        for (uint32_t k = 0; k < APROP_GROUPS; k++) rr[k] = i < cnt[k] ? P.rec[(size_t)(g0 + k) * REC_CAP + i] : ~0ull;
 #pragma unroll
-        for (uint32_t k = 0; k < APROP_GROUPS; k++) fw[k] = P.amix[r[k] != ~0ull ? anc_fword(anc_mix(r[k] >> 19)) : 0u];
+        for (uint32_t k = 0; k < APROP_GROUPS; k++) fv[k] = P.amix[rr[k] != ~0ull ? anc_fword(anc_mix(rr[k] >> 19)) : 0u];
 #pragma unroll
-        for (uint32_t k = 0; k < APROP_GROUPS; k++) {
-            if (r[k] == ~0ull) continue;
-            const uint64_t fp = r[k] >> 19;
-            if (!anc_ftest(fw[k], anc_mix(fp))) continue;
-            const uint32_t b = gr[k].x, gpos = gr[k].y * XC_SEG;
-            const uint32_t len = P.buf_len[b], ck0 = P.buf_chunk0[b], cblk = P.blk_base[b];
-            const uint32_t ap = gpos + (((uint32_t)r[k] >> 5) & 0x3FFFu), nr = ((uint32_t)r[k] & 31u) + 1u;
-            // (skipping the probes of a record inside a predicted REF block after another one, whose
-            // proposals all fall in REF shadows, cost more in dependent loads than it saved: cfg5
-            // A/B -1.1 %; the shadow test stays per proposal, below)
-#pragma unroll
-            for (int tb = 0; tb < 2; tb++) {
-                const AncSet &S = tb ? P.danc : P.canc;
-                uint32_t kk = anc_home(fp, S.mask);
-                for (;;) {
-                    const uint64_t key = S.keys[kk];
-                    if (key == XC_EMPTY64) break;
-                    if ((key >> 11) == fp) {
-                        const uint32_t j = (uint32_t)key & 2047u;
-                        for (uint32_t e = 0; e < nr; e++) {
-                            const uint32_t aa = ap + e, q = aa + (XC_SEG - 1u) - j;
-                            if (aa < j || q >= len || ((q + 1u) & (XC_SEG - 1u)) == 0u) continue;
-                            // REF shadow: the 2047 window ends after a predicted REF are not looked up
-                            if (a.shadow && q >= XC_SEG && blk_cached(P.blk_pref[cblk + (q >> 11) - 1u])) continue;
-                            const uint32_t c = ck0 + q / P.chunk_len;
-                            const uint32_t slot = atomicAdd(&a.pcnt[c], 1u);
-                            if (slot < PROP_CAP) a.pq[(size_t)c * PROP_CAP + slot] = q;
-                        }
-                    }
-                    kk = (kk + 1u) & S.mask;
-                }
-            }
-        }
+        for (uint32_t k = 0; k < APROP_GROUPS; k++)
+            if (rr[k] != ~0ull && anc_ftest(fv[k], anc_mix(rr[k] >> 19))) aprop_probe(P, a, rr[k], gr[k]);
     }
 }
 
