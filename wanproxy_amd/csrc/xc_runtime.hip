@@ -1209,12 +1209,20 @@ static_assert(CHUNK_LEN == CHUNK_BLOCKS * XC_SEG, "k_scan loads a chunk's shadow
 static const uint64_t SUB_BYTES_DEFAULT = 512ull << 20;  // sub-batch: bound on input bytes (tuned on cfg5)
 static const uint32_t SUB_BUFS = 32768;                  // sub-batch: bound on buffers
 
-// XC_SUB_MB overrides the sub-batch byte bound (tuning experiments).
-static uint64_t sub_bytes()
+static const uint64_t SUB_BYTES_MAX = 1024ull << 20;    // ... grown up to this while the run keeps two
+// The sub-batch byte bound of a run of `total` input bytes: half the run, between 512 MiB and 1 GiB,
+// so that a large run has two sub-batches or more (its later sub-batches hashed on the side stream
+// beside the earlier ones) and as few as that allows: per sub-batch, each of the ~9 dependent kernels
+// of the main stream pays its ramp-down (cfg5, 2 GiB: A/B 512 MiB 845-847 / 768 MiB 848-853 /
+// 1 GiB 856-858 GiB/s, profiles/r05/ab/sub_batch_size_r5j.txt).  XC_SUB_MB overrides it (tests,
+// tuning experiments).
+static uint64_t sub_bytes(uint64_t total)
 {
     const char *e = getenv("XC_SUB_MB");
     const long v = e ? atol(e) : 0;
-    return v > 0 ? (uint64_t)v << 20 : SUB_BYTES_DEFAULT;
+    if (v > 0) return (uint64_t)v << 20;
+    const uint64_t half = ((total / 2 + (1u << 20) - 1) >> 20) << 20;
+    return std::min(SUB_BYTES_MAX, std::max(SUB_BYTES_DEFAULT, half));
 }
 static const uint32_t MAX_ROUNDS = 64;
 
@@ -1428,7 +1436,9 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
         uint64_t bytes = 0, blocks = 0;
         uint32_t cnt = 0;
         uint64_t decl = 0, maxdecl = 0;
-        const uint64_t sub_max = sub_bytes();
+        uint64_t total = 0;
+        for (uint32_t i = 0; i < nbuf; i++) total += lengths[i];
+        const uint64_t sub_max = sub_bytes(total);
         // XC_FIRST_SUB_MB (experiments): the first sub-batch's bound (its block hashing has
         // nothing to overlap with)
         const char *fe = getenv("XC_FIRST_SUB_MB");
