@@ -352,3 +352,68 @@ def test_anchor_scan_finds_a_cached_anchorless_segment(gpu_ctx, oracle_mod, monk
     assert st.anchor_scans == st.sub_batches > 1 and st.anchor_fallbacks == 0, \
         (st.anchor_scans, st.sub_batches, st.anchor_fallbacks)
     assert len(cache) == len(oc)
+
+
+def test_early_hashing_after_an_async_restore(gpu_ctx, oracle_mod, monkeypatch):
+    """The bench's step (xc_cache_restore_async, then the next run of the same plan with its input
+    ready, no host synchronisation between): the next run's first sub-batch is hashed on the side
+    stream at once, possibly before the restore has removed the previous run's entries.  Run A
+    declares blocks X0, X1; after a restore, run B holds [X0][X1][Y] whose window across X1 | Y
+    equals a pool segment S, found only through an anchor of S that lies in X1.  The stale tables
+    still hold X0 and X1, but a block counts as cached for the anchor records (a cached block after
+    a cached block writes none) only through entries that survive the restore: X1's records are
+    written and the REF to S is found.  (Which of the two the device runs first is not forced here:
+    the test fails only on the interleaving that exposes a stale block, xc_cache.removed_floor.)"""
+    import torch
+    import wanproxy_amd as w
+    monkeypatch.setenv("XC_SUB_MB", "2")
+    pool = W.pool(512)
+    warm = [pool[i:i + 65536] for i in range(0, len(pool), 65536)]
+    S = pool[77 * 2048:78 * 2048]
+    j = _last_anchor(S)
+    assert j is not None and j < 2000
+    o = (2048 - j) // 2  # S = X1[o:] + Y[:o], S's anchor in the X1 part
+    X0, X1, Y = W.gen(0x7A00, 2048), W.gen(0x7A01, 2048).copy(), W.gen(0x7A02, 2048 * 3).copy()
+    X1[o:] = S[:2048 - o]
+    Y[:o] = S[2048 - o:]
+    fill = W.gen(0x7A03, 65536 - 5 * 2048)
+    runs = {"A": W.repeat_buffers(96, 0x7A10, np_segments=512, pool_bytes=pool)}
+    runs["B"] = [b.copy() for b in runs["A"]]
+    runs["A"][5] = np.concatenate([X0, X1, W.gen(0x7A04, 3 * 2048), fill])
+    runs["B"][5] = np.concatenate([X0, X1, Y, fill])
+    cache = w.XCodecCache(gpu_ctx, 1 << 14)
+    oc = oracle_mod.Cache()
+    w.XCodecEncoder(cache).encode_batch(warm)
+    oc.encode_batch(warm)
+    cache.snapshot()
+    want = {k: oc.clone().encode_batch(v) for k, v in runs.items()}
+    assert b"\xf1\x02" + int(oracle_mod.hash_segment(S)).to_bytes(8, "big") in want["B"][5]
+    plan = w.EncodePlan(cache, [65536] * 96)
+    plan.set_completion(True)
+    plan.set_input_ready(True)
+    plan.set_scan("anchor")
+    arenas = {}
+    for k, bufs in runs.items():
+        arena = np.zeros(plan.in_bytes, np.uint8)
+        for i, b in enumerate(bufs):
+            arena[int(plan.in_off[i]):int(plan.in_off[i]) + len(b)] = b
+        arenas[k] = torch.from_numpy(arena).cuda()
+    d_in = torch.zeros(plan.in_bytes, dtype=torch.uint8, device="cuda")
+    d_out = torch.zeros(plan.out_bytes, dtype=torch.uint8, device="cuda")
+    d_len = torch.zeros(96, dtype=torch.int64, device="cuda")
+    early = []
+    for n, k in enumerate("ABABAB"):
+        gpu_ctx.sync()
+        d_in.copy_(arenas[k])
+        torch.cuda.synchronize()  # (the input is complete at the submit)
+        if n:
+            cache.restore_async()  # (no host synchronisation between it and the next submit)
+        plan.submit(d_in.data_ptr(), d_out.data_ptr(), d_len.data_ptr())
+        plan.wait()
+        early.append(int(plan.stats().early_hashed))
+        gpu_ctx.sync()
+        out, lens = d_out.cpu().numpy(), d_len.cpu().numpy()
+        got = [out[int(plan.out_off[i]):int(plan.out_off[i]) + int(lens[i])].tobytes() for i in range(96)]
+        _same(got, want[k])
+    assert early[1::2] == [1, 1, 1], early  # (every B run hashed ahead: the A run before it ran clean)
+    plan.close()

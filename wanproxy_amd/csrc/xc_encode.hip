@@ -1621,7 +1621,7 @@ __global__ __launch_bounds__(256, 4) void k_blockhash(DeclArgs a)
     if (!PREDICT && l < n && a.limit && !stream_carried(P, b)) {
         // (a concurrent k_alloc may be entering keys: only complete entries are compared)
         uint64_t v;
-        if (set_find(P.cache, h, &v) && (uint32_t)v < *a.limit) cmp = (uint32_t)v + 1u;
+        if (set_find(P.cache, h, &v) && (uint32_t)v < min(*a.limit, a.limit_cap)) cmp = (uint32_t)v + 1u;
     }
     // blocks cached with the block before them cached too (entries complete at the run's start are
     // also found by k_blockpredict: these blocks are predicted REFs after a predicted REF)

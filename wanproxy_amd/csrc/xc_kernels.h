@@ -269,6 +269,9 @@ struct DeclArgs {
     // the one before are cached (every proposal of them would fall on an aligned window or in a
     // predicted REF's shadow; the async pass's shadows are on: xc_plan.shadow)
     int drop_shadowed;
+    // ... and below this count too (the early hashing of a run's first sub-batch: entries at or above
+    // it were removed by a restore or truncation that the hashing may run before)
+    uint32_t limit_cap;
 };
 struct EmitArgs {
     PlanDev P;

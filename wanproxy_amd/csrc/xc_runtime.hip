@@ -364,6 +364,9 @@ constexpr int XC__SLOW = -1000;
 struct xc_cache {
     xc_ctx *ctx;
     uint64_t cap;      // segment slots (the tables are sized for them)
+    // the lowest count a removal (a restore, a truncation, an eviction) left since the last run's
+    // submit: a plan's next early hashing compares only with entries below it (they survived)
+    uint32_t removed_floor = 0xFFFFFFFFu;
     HostSet set;
     uint8_t *segs;     // device: the first dev_cap slots
     uint64_t dev_cap = 0;
@@ -678,6 +681,7 @@ static int cache_anc_restore(xc_cache *c)
 // copied.  Snapshots stay valid: the rebuilt undo log records the new slots.
 static int cache_rebuild(xc_cache *c, uint64_t ncap, uint32_t keep, bool drop_dead)
 {
+    c->removed_floor = std::min(c->removed_floor, keep);
     hipStream_t s = c->ctx->stream;
     HIPCHK(hipDeviceSynchronize());  // (plans' side streams too: nothing may use the old arrays)
     uint32_t count = 0;
@@ -816,6 +820,7 @@ extern "C" int xc__cache_truncate(xc_cache *c, uint64_t keep)
 extern "C" int xc__cache_kill(xc_cache *c, const uint64_t *h, uint64_t n)
 {
     if (!n) return XC_OK;
+    c->removed_floor = 0;  // (evicted entries of any age)
     c->last_plan = nullptr;
     int rc = set_dev(c->ctx);
     if (!rc) rc = cache_busy(c);
@@ -954,6 +959,7 @@ static int cache_restore_rebuilt(xc_cache *c)
 // Enqueue the restore on the context stream (no host sync): for timed loops.
 static int cache_restore_async(xc_cache *c, uint32_t cur_count)
 {
+    c->removed_floor = std::min(c->removed_floor, c->snap_count);
     hipStream_t s = c->ctx->stream;
     uint32_t to = std::min<uint32_t>(cur_count, (uint32_t)c->cap);
     if (to > c->snap_count) {
@@ -991,6 +997,7 @@ extern "C" int xc_cache_restore_async(xc_cache *c)
         ~MemAfter() { mem_restore(c); }
     } mem_after{c};
     if (c->gen != c->snap_gen) return cache_restore_rebuilt(c);
+    c->removed_floor = std::min(c->removed_floor, c->snap_count);
     hipStream_t s = c->ctx->stream;
     if (c->host_count >= 0) {
         // one kernel: table slots entered since the snapshot, filters and count from the snapshot
@@ -2379,7 +2386,7 @@ static bool bh_gated()
 // On the main stream (st == nullptr: the run's first sub-batch, nothing to overlap with) no
 // events are needed.
 static int enqueue_block_hash(xc_plan *p, uint32_t k, hipEvent_t after, hipStream_t st, bool predict = false,
-                              const uint32_t *limit = nullptr)
+                              const uint32_t *limit = nullptr, uint32_t limit_cap = 0xFFFFFFFFu)
 {
     const bool side = st == p->hs;
     if (after) HIPCHK(hipStreamWaitEvent(st, after, 0));
@@ -2395,7 +2402,7 @@ static int enqueue_block_hash(xc_plan *p, uint32_t k, hipEvent_t after, hipStrea
     const char *abl_bh = getenv("XC_ABL_BH");
     const int nt_abl = bh_nt | (abl_bh ? atoi(abl_bh) & ~1 : 0);
     DeclArgs d{p->P, g0, g1, limit ? limit : side && k > 0 ? p->P.sb_count + (bh_gated() ? k - 1 : 0) : nullptr,
-               nt_abl, p->shadow};
+               nt_abl, p->shadow, limit_cap};
     // XC_ABL_SKIP_BLOCKHASH=1 (timing experiments only, valid when every run reads the same input):
     // the side stream's block hashing after the plan's first run is skipped
     static const bool skip = getenv("XC_ABL_SKIP_BLOCKHASH") && atoi(getenv("XC_ABL_SKIP_BLOCKHASH"));
@@ -2712,8 +2719,14 @@ static int encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64
                 (int)(p->P.stream_st != nullptr), (int)p->host_path, (int)use_graph(p), p->timing);
     if (c->last_plan != p) c->last_plan = nullptr;
     p->early_ok = false;
+    // (a restore or a truncation since the last run removed the entries from its floor up, and the
+    // hashing below may run before it on the side stream: only the entries under it are compared,
+    // which k_blockpredict, after it, finds too)
+    const uint32_t floor = c->removed_floor;
+    c->removed_floor = 0xFFFFFFFFu;
     if (early) {
-        if ((rc = enqueue_block_hash(p, 0, p->ev_sb0, p->hs, false, p->P.sb_count + (p->sub.size() - 2)))) return rc;
+        if ((rc = enqueue_block_hash(p, 0, p->ev_sb0, p->hs, false, p->P.sb_count + (p->sub.size() - 2), floor)))
+            return rc;
         p->early_runs++;
         p->stats.early_hashed = 1;
     }
