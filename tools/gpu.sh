@@ -58,7 +58,7 @@ for step in "$@"; do
             timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d "$out/pmc/$c" -o run -- python3 $PMC_BENCH \
                 > "$out/pmc_$c.log" 2>&1 || die "pmc $c" $? "$out/pmc_$c.log"
         done
-        python tools/pmc_traffic.py "$out/pmc" "$out/pmc_traffic_cfg5.json" 4 > "$out/pmc_traffic.log" 2>&1 \
+        python tools/pmc_traffic.py "$out/pmc" "$out/pmc_traffic_cfg5.json" auto > "$out/pmc_traffic.log" 2>&1 \
             || die pmc_traffic $? "$out/pmc_traffic.log"
         tail -3 "$out/pmc_traffic.log" ;;
     pmcinst)

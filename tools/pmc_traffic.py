@@ -11,7 +11,7 @@ doubled; WRITE_SIZE is exact for 16-B-per-lane streaming stores.  Narrow gathers
 and set probes, the tables' random reads) are not calibrated: doubling them overstates them, so the
 figure is an upper bound on the bytes the step moves.
 
-usage: python tools/pmc_traffic.py PMC_DIR OUT_JSON SUB_BATCHES [ALG_BYTES_PER_STEP]
+usage: python tools/pmc_traffic.py PMC_DIR OUT_JSON SUB_BATCHES|auto [ALG_BYTES_PER_STEP]
 (PMC_DIR holds FETCH_SIZE/ and WRITE_SIZE/ runs (tools/gpu.sh pmc), or p3/ and p4/; without
 ALG_BYTES_PER_STEP it is the roofline's alg_bytes_per_step of the bench line the FETCH_SIZE pass
 printed, PMC_DIR/../pmc_FETCH_SIZE.log)
@@ -45,13 +45,15 @@ def steps(disp, n=3):
 
 def main():
     d, out_path = sys.argv[1], sys.argv[2]
-    sub_batches = int(sys.argv[3])
+    log = os.path.join(os.path.dirname(os.path.normpath(d)), "pmc_FETCH_SIZE.log")
+    line = json.loads([x for x in open(log).read().splitlines() if x.startswith("{")][-1]) \
+        if os.path.exists(log) else None
+    # (auto: the sub-batches of the bench line the FETCH_SIZE pass printed)
+    sub_batches = int(line["stats"]["sub_batches"]) if sys.argv[3] == "auto" else int(sys.argv[3])
     if len(sys.argv) > 4:
         alg = int(sys.argv[4])
     else:
-        log = os.path.join(os.path.dirname(os.path.normpath(d)), "pmc_FETCH_SIZE.log")
-        line = [x for x in open(log).read().splitlines() if x.startswith("{")][-1]
-        alg = int(json.loads(line)["roofline"]["alg_bytes_per_step"])
+        alg = int(line["roofline"]["alg_bytes_per_step"])
     fd, wd = ("FETCH_SIZE", "WRITE_SIZE") if os.path.isdir(f"{d}/FETCH_SIZE") else ("p3", "p4")
     fetch = dispatches(f"{d}/{fd}/run_counter_collection.csv", "FETCH_SIZE")
     write = dispatches(f"{d}/{wd}/run_counter_collection.csv", "WRITE_SIZE")
