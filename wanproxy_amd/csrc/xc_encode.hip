@@ -2760,7 +2760,7 @@ __global__ __launch_bounds__(256) void k_tailcheck(PlanDev P, uint32_t nb, uint3
         uint32_t Uf = fA + cf.preA;
         uint32_t Vf = (XC_SEG + 32u * l) * fA - fC + 32u * l * cf.preA - cf.preC;
         uint64_t h[32];
-        uint64_t k1[32];
+        uint32_t fw[32];
 #pragma unroll
         for (int d = 0; d < 8; d++) {
 #pragma unroll
@@ -2774,18 +2774,16 @@ __global__ __launch_bounds__(256) void k_tailcheck(PlanDev P, uint32_t nb, uint3
                 h[4 * d + kk] = ((uint64_t)((Uf << 16) + Vf) << 36) + ((U << 20) + V);
             }
         }
+        // the cache's level-2 filter first (2 MB, L2-resident: every key of the table has its bits,
+        // set_insert), the table only for its few positives
 #pragma unroll
-        for (int t = 0; t < 32; t++) k1[t] = P.cache.keys[(live >> t) & 1u ? key_slot(h[t], P.cache.mask) : 0u];
+        for (int t = 0; t < 32; t++) fw[t] = P.cache.l2[(live >> t) & 1u ? l2_word(l2_mix((uint32_t)h[t])) : 0u];
         uint32_t hit = 0;
 #pragma unroll
         for (int t = 0; t < 32; t++) {
-            if (!((live >> t) & 1u)) continue;
-            bool x = k1[t] == h[t];
-            if (!x && k1[t] != XC_EMPTY64) {
-                uint64_t v;
-                x = set_find(P.cache, h[t], &v);
-            }
-            if (x) hit |= 1u << t;
+            if (!((live >> t) & 1u) || !l2_test(fw[t], l2_mix((uint32_t)h[t]))) continue;
+            uint64_t v;
+            if (set_find(P.cache, h[t], &v)) hit |= 1u << t;
         }
         for (;;) {
             const uint64_t m = ballot(hit != 0u);
