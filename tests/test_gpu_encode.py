@@ -395,16 +395,17 @@ def test_input_written_on_context_stream(gpu_ctx, oracle_mod):
             assert out[o:o + int(lens[i])].tobytes() == want[i], (seed, i)
 
 
-@pytest.mark.parametrize("no_graph", ["0", "1"])
-def test_graph_replay_and_recapture(gpu_ctx, oracle_mod, monkeypatch, no_graph):
-    """xc_encode_run replays the asynchronous pass of a single-sub-batch plan as a HIP graph
-    captured on the first run with the given arenas; a run with other arenas captures again, and a
-    sub-batch the gate hands back to the host (cross-buffer duplicates, self references) still
-    takes the step-by-step path after the graph.  Every run equals the oracle; XC_NO_GRAPH=1 (direct enqueue) gives the same bytes."""
+@pytest.mark.parametrize("graph", ["1", "0"])
+def test_graph_replay_and_recapture(gpu_ctx, oracle_mod, monkeypatch, graph):
+    """With XC_GRAPH=1, xc_encode_run replays the asynchronous pass of a single-sub-batch plan as a
+    HIP graph captured on the first run with the given arenas; a run with other arenas captures
+    again, and a sub-batch the gate hands back to the host (cross-buffer duplicates, self
+    references) still takes the step-by-step path after the graph.  Every run equals the oracle;
+    the default (direct enqueue) gives the same bytes."""
     import torch
     import wanproxy_amd as w
     monkeypatch.setenv("XC_SUB_MB", "64")  # one sub-batch: the graph path
-    monkeypatch.setenv("XC_NO_GRAPH", no_graph)
+    monkeypatch.setenv("XC_GRAPH", graph)
     bufs, warm = _mixed_batch()
     oc = oracle_mod.Cache()
     for batch in warm:

@@ -1,6 +1,6 @@
 """Host time of a cfg5 bench step, by phase: restore_async, submit (everything up to the first
 asynchronous pass enqueued), wait (the control words and encode_finish), against the device step.
-usage (GPU box): python tools/host_overhead.py [steps]"""
+usage (GPU box): python tools/host_overhead.py [steps] [cfg2]  (cfg2: 256 random 64 KiB buffers, empty cache)"""
 import json
 import os
 import sys
@@ -16,11 +16,13 @@ from wanproxy_amd import workloads as W  # noqa: E402
 
 def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    cfg2 = len(sys.argv) > 2 and sys.argv[2] == "cfg2"
     ctx = w.Context(0)
-    shard = W.repeat_shard(32768, 0x5555, 0, 1)
+    shard = np.stack(W.random_buffers(256)) if cfg2 else W.repeat_shard(32768, 0x5555, 0, 1)
     n = shard.shape[0]
     cache = w.XCodecCache(ctx, W.POOL_SEGMENTS + n * (W.BUF // 2048 + 1) + 1024)
-    w.XCodecEncoder(cache).encode_batch(W.pool_warmup_buffers())
+    if not cfg2:
+        w.XCodecEncoder(cache).encode_batch(W.pool_warmup_buffers())
     cache.snapshot()
     plan = w.EncodePlan(cache, np.full(n, W.BUF, dtype=np.uint64))
     plan.set_completion(True)

@@ -2,7 +2,10 @@
 N connections of one proxy, each EncodeFilter consuming one 64 KiB read per event-loop turn (cfg5
 data: 50 % repeats of the warm pool), the Batcher running each turn's calls as one device batch,
 then the peer's DecodeFilters decoding every pipe; the same with one device call per consume (the
-reference's pattern).  Prints one JSON line.  usage: python tools/pipe_bench_cpp.py [N] [TURNS] [OUT]"""
+reference's pattern); and the reference's own, unchanged EncodeFilter over the drop-in facade
+(oracle/_ref/filter_turns bench, built in the container from the reference's sources: one device call
+per consume, xcodec_filter.cc:146-157).  Prints one JSON line.
+usage: python tools/pipe_bench_cpp.py [N] [TURNS] [OUT]"""
 import json
 import os
 import subprocess
@@ -30,6 +33,14 @@ with tempfile.TemporaryDirectory() as d:
         if r.returncode:
             raise SystemExit(r.stdout + r.stderr)
         res["batched" if batched else "unbatched"] = json.loads(r.stdout.strip().splitlines()[-1])
+    ref = os.path.join(ROOT, "oracle", "_ref", "filter_turns")
+    if os.path.exists(ref):
+        sc = os.path.join(d, "sc.bin")
+        write_scenario(sc, W.pool_warmup_buffers(), order, inputs, batched=False)
+        r = subprocess.run([ref, "bench", sc], capture_output=True, text=True, timeout=600)
+        if r.returncode:
+            raise SystemExit(r.stdout + r.stderr)
+        res["reference_filter_unbatched"] = json.loads(r.stdout.strip().splitlines()[-1])
 print(json.dumps(res))
 if len(sys.argv) > 3:
     open(sys.argv[3], "w").write(json.dumps(res) + "\n")

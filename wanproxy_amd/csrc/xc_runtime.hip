@@ -2551,12 +2551,17 @@ static int encode_sub_sync(xc_plan *p, uint32_t sb, uint32_t *ctl)
 // events.  (With several sub-batches the graph loses the side stream's block hashing beside the
 // scans: cfg5 A/B on one box, graph 489-507 GiB/s against 515-525 enqueued directly; the host's
 // launches are hidden behind the long kernels there anyway.)
+// A HIP graph of a one-sub-batch run's launches: no longer the default (ROCm 7.2: hipGraphLaunch
+// starts its first node ~15-20 us after the call, where seven direct launches keep the host ahead
+// of the device after the first: cfg2 A/B 187-188 -> 204-206 GiB/s, cfg3 678-682 -> 695-696,
+// profiles/r05/ab/graph_vs_direct_r5s.txt).  XC_GRAPH=1 replays the graph (experiments).
 static bool use_graph(xc_plan *p)
 {
-    const char *e = getenv("XC_NO_GRAPH");
+    const char *e = getenv("XC_GRAPH");  // (read per run: tests switch it)
+    const bool on = e && atoi(e);
     // (nor for stateful streams: a duplicate enter is counted by the emit, after the graph's
     // published control words)
-    return !(e && atoi(e)) && !p->g_off && !p->timing && !p->host_path && p->sub.size() == 2 && !p->P.stream_st;
+    return on && !p->g_off && !p->timing && !p->host_path && p->sub.size() == 2 && !p->P.stream_st;
 }
 
 // Record ev_ctl after the control words' copy to h_ctl (enqueued by the caller or published by
