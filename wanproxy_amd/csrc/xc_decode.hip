@@ -1228,7 +1228,16 @@ extern "C" int xc_decode_plan_create(xc_cache *c, const uint64_t *in_len, const 
     uint32_t *d_ilen, *d_tbase;
 #define DA(ptr, n) if ((rc = p->alloc(ptr, n))) { xc_dplan_destroy(p); return rc; }
     if (hipSetDevice(p->dev) != hipSuccess) { xc_dplan_destroy(p); return xc__set_error(XC_EDEVICE, "hipSetDevice"); }
-    DA(&d_ioff, ns); DA(&d_ooff, ns); DA(&d_ocap, ns); DA(&d_ilen, ns); DA(&d_tbase, ns);
+    // the five per-stream layout arrays in one device block, uploaded by one copy from pinned staging
+    // (five pageable copies cost ~10 us each of a small call's host time)
+    uint8_t *d_lay = nullptr;
+    const size_t lay = (size_t)std::max<uint32_t>(ns, 1) * 32u;
+    DA(&d_lay, lay);
+    d_ioff = (uint64_t *)d_lay;
+    d_ooff = d_ioff + std::max<uint32_t>(ns, 1);
+    d_ocap = d_ooff + std::max<uint32_t>(ns, 1);
+    d_ilen = (uint32_t *)(d_ocap + std::max<uint32_t>(ns, 1));
+    d_tbase = d_ilen + std::max<uint32_t>(ns, 1);
     DA(&D.tok_cnt, ns); DA(&D.s_stop, ns); DA(&D.s_slot, ns); DA(&D.s_cnt, ns); DA(&D.s_lim, ns); DA(&D.ctl, DCTL_WORDS);
     DA(&D.t_lb, ntok); DA(&D.t_le, ntok); DA(&D.t_op, ntok); DA(&D.t_stat, ntok); DA(&D.t_h, ntok);
     DA(&D.t_src, ntok);
@@ -1244,13 +1253,22 @@ extern "C" int xc_decode_plan_create(xc_cache *c, const uint64_t *in_len, const 
     p->dsets[0] = ds;
     const hipStream_t s = p->s;
     if (ns) {
-        DHIP(hipMemcpyAsync(d_ioff, p->ioff.data(), ns * 8, hipMemcpyHostToDevice, s));
-        DHIP(hipMemcpyAsync(d_ooff, p->ooff.data(), ns * 8, hipMemcpyHostToDevice, s));
-        DHIP(hipMemcpyAsync(d_ocap, out_cap, ns * 8, hipMemcpyHostToDevice, s));
-        DHIP(hipMemcpyAsync(d_ilen, ilen.data(), ns * 4, hipMemcpyHostToDevice, s));
-        DHIP(hipMemcpyAsync(d_tbase, tbase.data(), ns * 4, hipMemcpyHostToDevice, s));
+        uint8_t *h_lay = nullptr;
+        if (xc__halloc((void **)&h_lay, lay)) { xc_dplan_destroy(p); return xc__set_error(XC_ENOMEM, "pinned allocation failed"); }
+        const size_t n1 = std::max<uint32_t>(ns, 1);
+        memcpy(h_lay, p->ioff.data(), ns * 8);
+        memcpy(h_lay + 8 * n1, p->ooff.data(), ns * 8);
+        memcpy(h_lay + 16 * n1, out_cap, ns * 8);
+        memcpy(h_lay + 24 * n1, ilen.data(), ns * 4);
+        memcpy(h_lay + 28 * n1, tbase.data(), ns * 4);
+        const hipError_t e = hipMemcpyAsync(d_lay, h_lay, lay, hipMemcpyHostToDevice, s);
+        const hipError_t e2 = hipStreamSynchronize(s);
+        xc__pfree(h_lay);
+        DHIP(e);
+        DHIP(e2);
+    } else {
+        DHIP(hipStreamSynchronize(s));
     }
-    DHIP(hipStreamSynchronize(s));
     p->tset[0] = {D.tok_cnt, D.t_lb, D.t_le, D.t_op, D.t_h};
     D.in_off = d_ioff;
     D.in_len = d_ilen;
@@ -1551,18 +1569,19 @@ extern "C" int xc_decode_batch_host(xc_cache *c, const uint8_t *in, const uint64
     const uint32_t ns = p->ns;
     const hipStream_t s = p->s;
     p->internal = true;
-    uint8_t *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
+    uint8_t *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr, *h_res = nullptr, *d_res = nullptr;
     uint64_t *d_u64 = nullptr;  // out_len | consumed | unknown
-    int32_t *d_i32 = nullptr;   // status | has_unknown
-    std::vector<uint64_t> u64(3 * (size_t)ns);
-    std::vector<int32_t> i32(2 * (size_t)ns);
+    int32_t *d_i32 = nullptr;   // status | has_unknown   (one block: one copy back into pinned h_res)
+    const size_t res_bytes = (size_t)ns * (3 * 8 + 2 * 4);
     auto run = [&]() -> int {
-        if (xc__halloc((void **)&h_in, p->in_bytes) || xc__halloc((void **)&h_out, p->out_bytes))
+        if (xc__halloc((void **)&h_in, p->in_bytes) || xc__halloc((void **)&h_out, p->out_bytes) ||
+            xc__halloc((void **)&h_res, res_bytes))
             return XC_ENOMEM;
         DHIP(dalloc(&d_in, p->in_bytes));
         DHIP(dalloc(&d_out, p->out_bytes));
-        DHIP(dalloc(&d_u64, 3 * (size_t)ns));
-        DHIP(dalloc(&d_i32, 2 * (size_t)ns));
+        DHIP(dalloc(&d_res, res_bytes));
+        d_u64 = (uint64_t *)d_res;
+        d_i32 = (int32_t *)(d_u64 + 3 * (size_t)ns);
         // (the padding between streams needs no clearing: the tokenizer clips every window to its
         // stream's length)
         for (uint32_t j = 0; j < ns; j++) memcpy(h_in + p->ioff[j], in + in_off[j], in_len[j]);
@@ -1570,9 +1589,10 @@ extern "C" int xc_decode_batch_host(xc_cache *c, const uint8_t *in, const uint64
         int r = xc_decode_run(p, d_in, d_out, d_u64, d_u64 + ns, d_i32, d_u64 + 2 * ns, d_i32 + ns);
         if (r) return r;
         DHIP(hipMemcpyAsync(h_out, d_out, p->out_bytes, hipMemcpyDeviceToHost, s));
-        DHIP(hipMemcpyAsync(u64.data(), d_u64, 3 * (size_t)ns * 8, hipMemcpyDeviceToHost, s));
-        DHIP(hipMemcpyAsync(i32.data(), d_i32, 2 * (size_t)ns * 4, hipMemcpyDeviceToHost, s));
+        DHIP(hipMemcpyAsync(h_res, d_res, res_bytes, hipMemcpyDeviceToHost, s));
         DHIP(hipStreamSynchronize(s));
+        const uint64_t *u64 = (const uint64_t *)h_res;
+        const int32_t *i32 = (const int32_t *)(u64 + 3 * (size_t)ns);
         for (uint32_t j = 0; j < ns; j++) {
             out_len[j] = u64[j];
             consumed[j] = u64[ns + j];
@@ -1587,10 +1607,10 @@ extern "C" int xc_decode_batch_host(xc_cache *c, const uint8_t *in, const uint64
     hipStreamSynchronize(s);
     xc__pfree(h_in);
     xc__pfree(h_out);
+    xc__pfree(h_res);
     xc__pfree(d_in);
     xc__pfree(d_out);
-    xc__pfree(d_u64);
-    xc__pfree(d_i32);
+    xc__pfree(d_res);
     xc_dplan_destroy(p);
     if (rc == XC__SLOW)  // a hash entered twice: the recent window's replay (xc_memcache.cpp)
         rc = xc__mem_decode_batch(xc__cache_mem(c), in, in_off, in_len, nbuf, out, out_off, out_cap, out_len, consumed,

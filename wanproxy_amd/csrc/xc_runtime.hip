@@ -367,6 +367,10 @@ struct xc_cache {
     // the lowest count a removal (a restore, a truncation, an eviction) left since the last run's
     // submit: a plan's next early hashing compares only with entries below it (they survived)
     uint32_t removed_floor = 0xFFFFFFFFu;
+    // host-path plans of small batches kept for the next call with the same buffer lengths (a
+    // proxy's one-read consume, xcodec_filter.cc:146-157: its plan's ~15 uploads and allocations
+    // cost more than the encode); plan_acquire / plan_release, oldest dropped past PLAN_POOL_MAX
+    std::vector<xc_plan *> plan_pool;
     HostSet set;
     uint8_t *segs;     // device: the first dev_cap slots
     uint64_t dev_cap = 0;
@@ -586,10 +590,13 @@ extern "C" void xc__cache_engine(xc_cache *c, int on)
     }
 }
 
+static void plan_pool_drain(xc_cache *c);
+
 extern "C" int xc_cache_destroy(xc_cache *c)
 {
     if (!c) return XC_OK;
     hipSetDevice(c->ctx->dev);
+    plan_pool_drain(c);
     hipDeviceSynchronize();  // pooled memory is reused at once: every stream must be done with it
     c->set.release(true);
     dfree(c->anc_of);
@@ -1332,6 +1339,7 @@ struct xc_plan {
     uint8_t *e_in = nullptr, *e_out = nullptr;
     uint64_t *e_len = nullptr, *e_pos = nullptr, *e_total = nullptr;
     uint8_t *pack_dst = nullptr;
+    uint64_t *h_lenpos = nullptr;  // pinned: the host path's lengths and positions (xc_encode_run_host)
     uint64_t pack_cap = 0;
     int shadow = 1;          // REF shadows in the async pass (XC_NO_SHADOW=1 disables)
     uint32_t max_decl = 2;   // longest buffer / 2048 + 2 (k_walk's LDS)
@@ -1961,6 +1969,7 @@ extern "C" int xc_plan_destroy(xc_plan *p)
     for (auto e : p->ev_go)
         if (e) hipEventDestroy(e);
     if (p->ev_sb0) hipEventDestroy(p->ev_sb0);
+    pool_free(p->h_lenpos);
     if (p->es) {
         hipStreamSynchronize(p->es);
         hipStreamDestroy(p->es);
@@ -3069,12 +3078,18 @@ extern "C" int xc_encode_run_host(xc_plan *p, const uint8_t *h_in, uint8_t *h_ou
         hipStreamSynchronize(p->cs);
         return rc;
     }
-    if (p->nb) {
-        HIPCHK(hipMemcpyAsync(h_len, p->e_len, p->nb * 8, hipMemcpyDeviceToHost, s));
-        if (h_pos) HIPCHK(hipMemcpyAsync(h_pos, p->e_pos, p->nb * 8, hipMemcpyDeviceToHost, s));
+    if (p->nb) {  // (through the plan's pinned copy of them: pageable copies stage synchronously)
+        if (!p->h_lenpos && hmalloc((void **)&p->h_lenpos, (size_t)p->nb * 16) != hipSuccess)
+            return fail(XC_ENOMEM, "pinned allocation failed");
+        HIPCHK(hipMemcpyAsync(p->h_lenpos, p->e_len, p->nb * 8, hipMemcpyDeviceToHost, s));
+        if (h_pos) HIPCHK(hipMemcpyAsync(p->h_lenpos + p->nb, p->e_pos, p->nb * 8, hipMemcpyDeviceToHost, s));
     }
     // (the run's lookup hits go to the recent window through the cache's hit log, hits_enqueue)
     HIPCHK(hipStreamSynchronize(s));
+    if (p->nb) {
+        memcpy(h_len, p->h_lenpos, p->nb * 8);
+        if (h_pos) memcpy(h_pos, p->h_lenpos + p->nb, p->nb * 8);
+    }
     return XC_OK;
 }
 
@@ -3083,6 +3098,44 @@ extern "C" int xc_encode_run_host(xc_plan *p, const uint8_t *h_in, uint8_t *h_ou
 // Host-to-host batch with stream state (xc_stream.cpp) and, when coll_cnt is given, every buffer's
 // collision lookups (the COSS tier's replay, xc_coss.cpp): coll_cnt[i] records in
 // coll[i * COLL_CAP * 4 ..] as {window end, hash lo, hash hi, 0} (at most COLL_CAP kept).
+// The host paths' plans (xc__encode_batch_host_coll, xc__encode_gather): a plan of these exact
+// lengths from the cache's pool, else a new one; released plans go back (small batches only: a
+// pooled plan holds its device workspace).
+static const size_t PLAN_POOL_MAX = 8;
+static const uint64_t PLAN_POOL_NBUF = 64;
+static int plan_acquire(xc_cache *c, const uint64_t *len, uint64_t nbuf, xc_plan **out)
+{
+    for (size_t k = c->plan_pool.size(); k-- > 0;) {
+        xc_plan *p = c->plan_pool[k];
+        if (p->nb == nbuf && std::equal(p->len.begin(), p->len.end(), len)) {
+            c->plan_pool.erase(c->plan_pool.begin() + (ptrdiff_t)k);
+            *out = p;
+            return XC_OK;
+        }
+    }
+    return xc_encode_plan_create(c, len, nbuf, out);
+}
+static void plan_release(xc_cache *c, xc_plan *p)
+{
+    if (!p) return;
+    if (p->nb > PLAN_POOL_NBUF || p->inflight || xc_plan_set_streams(p, nullptr, nullptr, nullptr) != XC_OK) {
+        xc_plan_destroy(p);
+        return;
+    }
+    c->plan_pool.push_back(p);
+    if (c->plan_pool.size() > PLAN_POOL_MAX) {
+        xc_plan *old = c->plan_pool.front();
+        c->plan_pool.erase(c->plan_pool.begin());
+        xc_plan_destroy(old);
+    }
+}
+static void plan_pool_drain(xc_cache *c)
+{
+    std::vector<xc_plan *> v;
+    v.swap(c->plan_pool);
+    for (xc_plan *p : v) xc_plan_destroy(p);
+}
+
 extern "C" int xc__encode_batch_host_coll(xc_cache *c, const uint8_t *in, const uint64_t *in_off,
                                           const uint64_t *in_len, uint64_t nbuf, uint8_t *out,
                                           const uint64_t *out_off, const uint64_t *out_cap, uint64_t *out_len,
@@ -3092,7 +3145,7 @@ extern "C" int xc__encode_batch_host_coll(xc_cache *c, const uint8_t *in, const 
     if (!c || (nbuf && (!in || !in_off || !in_len || !out || !out_off || !out_cap || !out_len)))
         return fail(XC_EINVAL, "null");
     xc_plan *p = nullptr;
-    int rc = xc_encode_plan_create(c, in_len, nbuf, &p);
+    int rc = plan_acquire(c, in_len, nbuf, &p);
     if (rc) return rc;
     const bool streams = start || cand || flags;
     if (streams && (rc = xc_plan_set_streams(p, start, cand, flags))) {
@@ -3133,7 +3186,10 @@ extern "C" int xc__encode_batch_host_coll(xc_cache *c, const uint8_t *in, const 
                 rc = fail(XC_EDEVICE, "collision records copy");
         }
     }
-    xc_plan_destroy(p);  // (synchronizes before the pinned buffers return to the pool)
+    // (nothing of the run may still touch the pinned buffers when they return to the pool)
+    if (hipStreamSynchronize(c->ctx->stream) != hipSuccess && !rc) rc = fail(XC_EDEVICE, "stream synchronize");
+    if (rc) xc_plan_destroy(p);
+    else plan_release(c, p);
     pool_free(h_in);
     pool_free(h_out);
     return rc;
@@ -3157,7 +3213,7 @@ extern "C" int xc__encode_gather(xc_cache *c, uint64_t nbuf, const uint8_t *cons
     std::vector<uint64_t> len(nbuf);
     for (uint64_t i = 0; i < nbuf; i++) len[i] = head_len[i] + tail_len[i];
     xc_plan *p = nullptr;
-    int rc = xc_encode_plan_create(c, len.data(), nbuf, &p);
+    int rc = plan_acquire(c, len.data(), nbuf, &p);
     if (rc) return rc;
     if ((rc = xc_plan_set_streams(p, start, cand, flags))) {
         xc_plan_destroy(p);
@@ -3184,7 +3240,9 @@ extern "C" int xc__encode_gather(xc_cache *c, uint64_t nbuf, const uint8_t *cons
     rc = xc_encode_run_host(p, h_in, h_out, cap_total + 16, lens.data(), pos.data());
     if (!rc) rc = xc_plan_stream_results(p, rbase, rcand);
     for (uint64_t i = 0; i < nbuf && !rc; i++) rc = take(ctx, i, h_out + pos[i], lens[i], h_in + p->in_off[i]);
-    xc_plan_destroy(p);  // (synchronizes before the pinned buffers return to the pool)
+    if (hipStreamSynchronize(c->ctx->stream) != hipSuccess && !rc) rc = fail(XC_EDEVICE, "stream synchronize");
+    if (rc) xc_plan_destroy(p);
+    else plan_release(c, p);
     pool_free(h_in);
     pool_free(h_out);
     if (rc == XC__SLOW)  // a hash entered twice: the recent window's replay (xc_memcache.cpp)
