@@ -939,25 +939,24 @@ __global__ __launch_bounds__(64 * DEMIT_WAVES) void k_demit(DecDev D)
 // exactly the eligible providers. Then the last workgroup to finish (a ticket in the control words)
 // takes the cache slots of the streams' ENTER tokens: the exclusive prefix of the per-stream counts
 // k_dres2 left in s_slot, on top of the current segment count, and publishes the control words.
-constexpr uint32_t DFIN_WAVES = 16, DFIN_REG = 8;
+constexpr uint32_t DFIN_WAVES = 16, DFIN_REG = 8, DFIN_GRID = 128;
 __global__ __launch_bounds__(64 * DFIN_WAVES) void k_dfin(DecDev D, int round)
 {
     __shared__ uint32_t wsum[DFIN_WAVES];
     __shared__ uint2 csum[DFIN_WAVES];
     __shared__ uint32_t last;
     const uint32_t wave = threadIdx.x >> 6, l = lane_id();
-    {
-        const uint32_t j = blockIdx.x * DFIN_WAVES + wave;
-        if (j < D.ns) {
-            const uint32_t tb = D.tok_base[j], ex = D.s_stop[j] - 1u;
-            if (round > 0 && l == 0 && ex != D.s_lim[j]) atomicOr(&D.ctl[DCTL_FIX], 1u);
-            for (uint32_t t = l; t < ex; t += 64u) {
-                const uint64_t src = D.t_src[tb + t];
-                const uint32_t st = D.t_stat[tb + t];
-                if ((st == R_OKPROV || st == R_COLL) && (src & SRC_PROV)) {
-                    const uint32_t pj = (uint32_t)((src >> 32) & 0x7FFFFFFFu), pt = (uint32_t)src;
-                    if (pt + 1u >= D.s_stop[pj]) atomicOr(&D.ctl[DCTL_FIX], 1u);
-                }
+    // (a grid of at most DFIN_GRID workgroups, each wave a stride of streams: every workgroup takes a
+    // ticket below, and device-scope atomics on one word serialize across the XCDs)
+    for (uint32_t j = blockIdx.x * DFIN_WAVES + wave; j < D.ns; j += gridDim.x * DFIN_WAVES) {
+        const uint32_t tb = D.tok_base[j], ex = D.s_stop[j] - 1u;
+        if (round > 0 && l == 0 && ex != D.s_lim[j]) atomicOr(&D.ctl[DCTL_FIX], 1u);
+        for (uint32_t t = l; t < ex; t += 64u) {
+            const uint64_t src = D.t_src[tb + t];
+            const uint32_t st = D.t_stat[tb + t];
+            if ((st == R_OKPROV || st == R_COLL) && (src & SRC_PROV)) {
+                const uint32_t pj = (uint32_t)((src >> 32) & 0x7FFFFFFFu), pt = (uint32_t)src;
+                if (pt + 1u >= D.s_stop[pj]) atomicOr(&D.ctl[DCTL_FIX], 1u);
             }
         }
     }
@@ -1074,6 +1073,7 @@ extern "C" int xc__cache_devset(xc_cache *c, void *devset, SegStore *segs, uint3
                                 uint2 **undo, void **stream, int *dev);
 extern "C" int xc__set_error(int code, const char *msg);
 extern "C" hipError_t xc__spin_wait(hipEvent_t ev);
+extern "C" bool xc__query_due(int64_t *t0);
 extern "C" int xc__dalloc(void **p, uint64_t bytes);
 extern "C" int xc__halloc(void **p, uint64_t bytes);
 extern "C" void xc__pfree(void *p);
@@ -1446,11 +1446,14 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
             p->h_ctl[DCTL_WORDS - 1] = 0xFFFFFFFFu;
             Da.ctl_host = p->d_hctl;
         }
-        hipLaunchKernelGGL(k_dfin, dim3((ns + DFIN_WAVES - 1) / DFIN_WAVES), dim3(64 * DFIN_WAVES), 0, s, Da, r);
+        static const uint32_t dfin_grid = getenv("XC_DFIN_GRID") ? (uint32_t)atoi(getenv("XC_DFIN_GRID")) : DFIN_GRID;
+        hipLaunchKernelGGL(k_dfin, dim3(std::max(1u, std::min(dfin_grid, (ns + DFIN_WAVES - 1) / DFIN_WAVES))),
+                           dim3(64 * DFIN_WAVES), 0, s, Da, r);
         DHIP(hipGetLastError());  // (slots first: k_demit fills them)
         hipLaunchKernelGGL(k_demit, dim3(ns), dim3(64 * DEMIT_WAVES), 0, s, D);
         DHIP(hipGetLastError());
         if (pub) {
+            int64_t t0 = 0;
             for (int i = 0;; i++) {
                 if (*(volatile const uint32_t *)(p->h_ctl + DCTL_WORDS - 1) == 0u) {
                     __atomic_thread_fence(__ATOMIC_ACQUIRE);
@@ -1458,9 +1461,11 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
                     return XC_OK;
                 }
                 if ((i & 255) == 255) {
-                    const hipError_t e = hipStreamQuery(s);
-                    if (e == hipSuccess) break;  // drained without a publication: read the words
-                    if (e != hipErrorNotReady) DHIP(e);
+                    if (xc__query_due(&t0)) {  // (a query enqueues a marker: only after ~2 ms)
+                        const hipError_t e = hipStreamQuery(s);
+                        if (e == hipSuccess) break;  // drained without a publication: read the words
+                        if (e != hipErrorNotReady) DHIP(e);
+                    }
                     if (i >= 4096) sched_yield();
                 }
             }

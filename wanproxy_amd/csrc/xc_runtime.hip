@@ -1320,6 +1320,7 @@ struct xc_plan {
     // (early_ok: the previous run of this plan went through the asynchronous pass unchanged;
     // ev_sb0: after its first sub-batch's last kernel that reads the block arrays)
     bool input_ready = false, early_ok = false;
+    bool rec_sb0 = false;  // (this run records ev_sb0: only a plan of several sub-batches with its input ready uses it)
     hipEvent_t ev_sb0 = nullptr;
     // The emit of a large sub-batch (its wire bytes and segment-store copies) runs on its own stream
     // es, beside the next sub-batch's predictions and anchor scan; the main stream joins it before
@@ -2185,6 +2186,19 @@ static hipError_t pass_state(xc_plan *p)
     return published(p) ? hipSuccess : hipStreamQuery(p->cache->ctx->stream);
 }
 
+// A publication poll asks the stream whether it drained only after XC_QUERY_US (2000) us without a
+// publication (checked every 256 polls): hipStreamQuery on a stream with kernels in flight enqueues
+// a marker behind them, whose release leaves the device idle for ~6 us before the next kernel (the
+// decoder's emit -> the next restore, cfg4).  A pass that publishes nothing still ends the poll.
+extern "C" bool xc__query_due(int64_t *t0)
+{
+    static const int64_t lim = getenv("XC_QUERY_US") ? atoll(getenv("XC_QUERY_US")) * 1000 : 2000000;
+    const int64_t t = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                          std::chrono::steady_clock::now().time_since_epoch()).count();
+    if (*t0 == 0) *t0 = t;
+    return t - *t0 >= lim;
+}
+
 // While the device works: the earlier runs' lookup hits whose copies are complete go to the window.
 static void replay_while_waiting(xc_plan *p)
 {
@@ -2204,12 +2218,15 @@ static hipError_t wait_decided(xc_plan *p)
             if (i >= 64) sched_yield();
         }
     }
+    int64_t t0 = 0;
     for (int i = 0;; i++) {
         if (published(p)) return hipSuccess;
         replay_while_waiting(p);
         if ((i & 255) == 255) {
-            const hipError_t e = pass_state(p);
-            if (e != hipErrorNotReady) return e;
+            if (xc__query_due(&t0)) {
+                const hipError_t e = pass_state(p);
+                if (e != hipErrorNotReady) return e;
+            }
             if (i >= 4096) sched_yield();
         }
     }
@@ -2520,7 +2537,8 @@ static int encode_sub_async(xc_plan *p, uint32_t sb)
     }
     if ((rc = launch_first_round(p, sb, j0, s1, p->shadow))) return rc;
     if ((rc = launch_emit(p, sb, j0, s1, sb))) return rc;
-    if (sb == 0) HIPCHK(hipEventRecord(p->ev_sb0, p->cache->ctx->stream));
+    // (an event recorded between two kernels leaves the device idle ~6 us: only when a next run uses it)
+    if (sb == 0 && p->rec_sb0) HIPCHK(hipEventRecord(p->ev_sb0, p->cache->ctx->stream));
     return launch_pack(p, j0, s1);
 }
 
@@ -2750,6 +2768,7 @@ static int encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64
     p->next_hash = early ? 1u : 0u;  // (sub-batch 0 hashed ahead: its predictions wait for ev_hash[0])
     const size_t nsub = p->sub.size() - 1;
     if ((rc = ctl_buffers(p))) return rc;
+    p->rec_sb0 = p->input_ready && p->sub.size() > 2;
     if (use_graph(p)) {
         if ((rc = graph_launch(p))) return rc;
     } else {
@@ -2889,7 +2908,7 @@ static int encode_finish(xc_plan *p)
     }
     // (the first pass enqueued it behind itself unless a sub-batch was redone since)
     if (!(p->tail_enqueued && !redone) && (rc = launch_tailcheck(p))) return rc;
-    p->early_ok = !redone && p->sub.size() > 2;
+    p->early_ok = !redone && p->sub.size() > 2 && p->rec_sb0;
     if (dbg_finish()) fprintf(stderr, "finish redone=%d nsub=%zu\n", (int)redone, p->sub.size() - 1);
     c->last_plan = p;
     if (c->mem && !c->engine) {

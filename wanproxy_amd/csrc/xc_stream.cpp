@@ -109,6 +109,61 @@ struct Item {
 };
 }  // namespace
 
+// XCodecHash::hash of one 2048-byte segment (xcodec/xcodec_hash.h:166-174: the window sums of byte + 1
+// and of ffs(byte), weights 2048 - j, mixed with the uint32 shifts of :155-164).
+static uint64_t segment_hash(const uint8_t *p)
+{
+    uint32_t s1w = 0, s2w = 0, s1f = 0, s2f = 0;
+    for (uint32_t j = 0; j < XC_SEGMENT_LENGTH; j++) {
+        const uint32_t w = p[j] + 1u, f = p[j] ? (uint32_t)__builtin_ctz(p[j]) + 1u : 0u;
+        s1w += w;
+        s2w += (XC_SEGMENT_LENGTH - j) * w;
+        s1f += f;
+        s2f += (XC_SEGMENT_LENGTH - j) * f;
+    }
+    const uint32_t bits = (s1f << 16) + s2f, bytes = (s1w << 20) + s2w;
+    return ((uint64_t)bits << 36) + bytes;
+}
+
+// encode_escape (xcodec_encoder.cc:217-239): bytes with F1 -> F1 00, appended at o.
+static uint64_t escape(uint8_t *o, const uint8_t *p, uint64_t n)
+{
+    uint64_t k = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        o[k++] = p[i];
+        if (p[i] == 0xF1) o[k++] = 0x00;
+    }
+    return k;
+}
+
+// XCodecEncoder::flush (xcodec_encoder.cc:175-201) of an encoder over a memory cache, on the host: it
+// looks nothing up, so it needs no device batch -- the pending candidate declared (its bytes escaped
+// before it, F1 01 + the 2048 bytes, cache_->enter: xc_cache_enter, with the memory cache's release
+// semantics for a hash already entered), the rest of source_ escaped.  A proxy's EncodeFilter calls
+// it after every consume's encode (xcodec_filter.cc:146-157): one device call per consume, not two.
+static int host_flush(xc_encoder *e, uint8_t *out, uint64_t *out_len)
+{
+    const uint8_t *s = e->source.data();
+    const uint64_t n = e->source.size();
+    uint64_t k = 0, at = 0;
+    if (e->cand >= 0) {
+        const uint64_t c = (uint64_t)e->cand;
+        if (c + XC_SEGMENT_LENGTH > n) return xc__set_error(XC_EDEVICE, "inconsistent stream state");
+        k += escape(out + k, s, c);
+        out[k++] = 0xF1;
+        out[k++] = 0x01;
+        std::memcpy(out + k, s + c, XC_SEGMENT_LENGTH);
+        k += XC_SEGMENT_LENGTH;
+        if (int rc = xc_cache_enter(e->cache, segment_hash(s + c), s + c)) return rc;
+        at = c + XC_SEGMENT_LENGTH;
+    }
+    k += escape(out + k, s + at, n - at);
+    *out_len += k;
+    e->source.clear();
+    e->cand = -1;
+    return XC_OK;
+}
+
 // coss: the encoders' cache is that COSS cache's device mirror, and the batches run through the
 // COSS replay (xc__coss_encode_gather); else the memory cache (xc__encode_gather).
 static int encode_streams(xc_coss *coss, xc_encoder *const *enc, const uint8_t *const *in, const uint64_t *in_len,
@@ -141,6 +196,12 @@ static int encode_streams(xc_coss *coss, xc_encoder *const *enc, const uint8_t *
     std::vector<uint64_t> done(n, 0);  // input bytes of call k consumed so far
     uint64_t k0 = 0;
     while (k0 < n) {
+        // a flush with no input at the head of the remaining calls: on the host (memory caches)
+        if (!coss && in_len[k0] == 0 && flags && (flags[k0] & XC_STREAM_FLUSH)) {
+            if (int rc = host_flush(enc[k0], out + out_off[k0] + out_len[k0], &out_len[k0])) return rc;
+            k0++;
+            continue;
+        }
         // build the round
         std::vector<Item> items;
         std::vector<const xc_encoder *> used;
