@@ -148,3 +148,23 @@ def test_long_call_is_split(gpu_ctx, oracle_mod):
     data = np.concatenate([W.gen(51, 700000), pool[:65536], W.gen(52, 500000)])
     calls = [(0, W.gen(53, 3000), False), (0, data, False), (0, W.gen(54, 100), True)]
     _run_both(gpu_ctx, oracle_mod, 1, calls, warm=[pool[:65536]])
+
+
+@pytest.mark.parametrize("batch", [True, False])
+def test_fresh_calls_without_flush(gpu_ctx, oracle_mod, batch):
+    """encode() on a clean encoder, flush() after (the reference filter's consume, xcodec_filter.cc:
+    146-157), taken by the block-parallel walk: the last block's candidate stays pending (new last
+    block), or the tail after a REF of it does; sub-window and exact-multiple lengths; another
+    connection repeating a block still pending in the first (not entered yet: declared again)."""
+    pool = W.pool(32)
+    a, b = W.gen(61, 10240), W.gen(62, 9000)
+    calls = [
+        (0, a, False), (0, b"", True),                                   # last block new: pending
+        (0, np.concatenate([W.gen(63, 4096), pool[:2048]]), False), (0, b"", True),  # last block REF
+        (0, np.concatenate([W.gen(64, 3000), pool[2048:4096], W.gen(65, 500)]), False), (0, b"", True),
+        (0, W.gen(66, 1500), False), (0, b"", True),                     # no full window
+        (0, W.gen(67, 2048), False), (0, b"", True),                     # exactly one block
+        (1, b, False), (2, b[-2048 * 3:], False), (1, b"", True), (2, b"", True),  # pending twice
+        (3, np.concatenate([pool[4096:8192], a[:6144]]), False), (3, W.gen(68, 700), True),
+    ]
+    _run_both(gpu_ctx, oracle_mod, 4, calls, warm=[pool[:32768]], batch=batch)

@@ -1265,7 +1265,7 @@ __device__ __forceinline__ bool walk_blocks(const WalkArgs &a, uint32_t b, WalkS
     const uint32_t nblk = len / XC_SEG;
     const uint32_t ck0 = P.buf_chunk0[b], ck1 = P.buf_chunk0[b + 1];
     const uint32_t tb = P.tok_base[b];
-    if (!stream_plain(P, b)) return false;  // carried state or no flush: the sequential walk
+    if (!stream_plain(P, b)) return false;  // carried state: the sequential walk
     if (threadIdx.x == 0) sh = WalkShared{0u, 0u, 0u, 0u, 0u};
     __syncthreads();
     bool ok = true, cross = false;
@@ -1348,21 +1348,41 @@ __device__ __forceinline__ bool walk_blocks(const WalkArgs &a, uint32_t b, WalkS
     __syncthreads();
     if (sh.fail) return false;
     if (threadIdx.x == 0) {
-        const uint32_t t = tb + nblk;  // END: the tail after the last block, escaped by flush()
+        uint32_t t = tb + nblk;  // END: the tail after the last block, escaped by flush()
+        uint32_t end = len, n_ext = sh.n_ext, n_unk = sh.n_unk;
+        uint2 res = make_uint2(len, NONE);  // flushed: source_ empty
+        if (stream_noflush(P, b)) {
+            // encode() without flush() (xcodec_encoder.cc:60-170): the last block's candidate is
+            // due at cand + 4095 >= len, so it stays pending with the bytes from it in source_;
+            // after a REF of the last block the tail stays in source_ (no candidate)
+            end = nblk * XC_SEG;
+            res = make_uint2(end, NONE);
+            if (nblk && P.tok_op[t - 1u] == OP_EXTRACT) {
+                t--;
+                end -= XC_SEG;
+                res = make_uint2(end, end);
+                n_ext--;
+                n_unk -= P.tok_known[t] == 1u ? 0u : 1u;
+            }
+            P.tok_cnt[b] = t - tb + 1u;
+        } else {
+            P.tok_cnt[b] = nblk + 1u;
+        }
         P.tok_op[t] = OP_END;
         P.tok_known[t] = 0u;
-        P.tok_lb[t] = nblk * XC_SEG;
-        P.tok_le[t] = len;
+        P.tok_lb[t] = t == tb + nblk ? nblk * XC_SEG : end;
+        P.tok_le[t] = end;
         P.tok_seg[t] = 0u;
         P.tok_dpos[t] = 0u;
         P.tok_h[t] = 0u;
-        P.tok_cnt[b] = nblk + 1u;
-        P.buf_next[b] = sh.n_ext;
+        P.buf_next[b] = n_ext;
         P.buf_nref[b] = sh.n_ref;
+        sh.n_unk = n_unk;
         if (P.coll_cnt) P.coll_cnt[b] = 0u;  // (a collision makes the walk sequential)
-        if (P.stream_res) P.stream_res[b] = make_uint2(len, NONE);  // flushed: source_ empty
+        if (P.stream_res) P.stream_res[b] = res;
         if (sh.cross) atomicMin(&P.ctl[CTL_FIRST_CROSS], b);
     }
+    __syncthreads();  // (sh.n_unk: k_walk reads it)
     return true;
 }
 
@@ -2126,7 +2146,7 @@ __global__ __launch_bounds__(1024) void k_pack_offsets(PackArgs a)
     __shared__ uint64_t wsum[16];
     __shared__ uint64_t carry;
     const uint32_t wave = threadIdx.x >> 6, l = lane_id();
-    if (threadIdx.x == 0) carry = *a.total;
+    if (threadIdx.x == 0) carry = a.j0 == 0u ? 0ull : *a.total;  // (the run's first buffers: from 0)
     __syncthreads();
     for (uint32_t b0 = a.j0; b0 < a.j1; b0 += 1024u) {
         const uint32_t b = b0 + threadIdx.x;

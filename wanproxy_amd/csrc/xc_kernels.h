@@ -198,11 +198,16 @@ __device__ __forceinline__ bool stream_carried(const PlanDev &P, uint32_t b)
     const uint4 st = P.stream_st[b];
     return st.x != 0u || st.y != NONE;
 }
+// A buffer with no carried-over state: a fresh encoder's call, flushed at its end or not.
 __device__ __forceinline__ bool stream_plain(const PlanDev &P, uint32_t b)
 {
     if (!P.stream_st) return true;
     const uint4 st = P.stream_st[b];
-    return st.x == 0u && st.y == NONE && !(st.z & SF_NOFLUSH);
+    return st.x == 0u && st.y == NONE;
+}
+__device__ __forceinline__ bool stream_noflush(const PlanDev &P, uint32_t b)
+{
+    return P.stream_st && (P.stream_st[b].z & SF_NOFLUSH);
 }
 
 // kernel argument blocks (shared by xc_encode.hip and xc_runtime.hip)

@@ -419,6 +419,8 @@ struct xc_cache {
         uint32_t nb = 0;
         uint32_t next_b = 0;  // replay progress: the first buffer not replayed yet
         uint64_t serial = 0;  // the plan whose layout dtb / rec_base hold
+        bool copying = false;    // an asynchronous copy into h was issued and not seen complete
+        bool host_sync = false;  // written into h on the context stream: complete once it is synchronised
     } hl[2];
     std::deque<int> hl_fifo;  // slots whose hits are not replayed yet, oldest first
     // a finished run whose hits are not packed yet: packed (k_hits, its copy) at the next operation
@@ -1338,9 +1340,16 @@ struct xc_plan {
     hipStream_t cs = nullptr;
     std::vector<hipEvent_t> ev_h2d;
     uint8_t *e_in = nullptr, *e_out = nullptr;
+    // (one block: lengths, packed positions, stream results; one copy back)
     uint64_t *e_len = nullptr, *e_pos = nullptr, *e_total = nullptr;
+    uint2 *e_res = nullptr;
+    bool h2d_inline = false;  // a one-sub-batch host-path run copies its input on the context stream
     uint8_t *pack_dst = nullptr;
-    uint64_t *h_lenpos = nullptr;  // pinned: the host path's lengths and positions (xc_encode_run_host)
+    uint64_t *h_lenpos = nullptr;  // pinned: the host path's lengths, positions and stream results (xc_encode_run_host)
+    bool res_staged = false;       // the last host-path run's stream results are in h_lenpos + 2 nb
+    std::vector<uint4> st_dev;     // the stream states d_stream_st holds (set_streams skips an equal upload)
+    uint4 *h_st = nullptr;         // pinned staging of their upload
+    bool cand_carried = false;     // a stream state carries a candidate (a hash may be entered twice)
     uint64_t pack_cap = 0;
     int shadow = 1;          // REF shadows in the async pass (XC_NO_SHADOW=1 disables)
     uint32_t max_decl = 2;   // longest buffer / 2048 + 2 (k_walk's LDS)
@@ -1703,13 +1712,18 @@ static hipError_t spin_wait(hipEvent_t ev);
 static int hits_replay_front(xc_cache *c, bool block, bool *done, uint32_t max_b = 0xFFFFFFFFu)
 {
     xc_cache::HitSlot &sl = c->hl[c->hl_fifo.front()];
-    hipError_t e = hipEventQuery(sl.ev);
+    if (sl.host_sync) {  // (a host-path run's host synchronises behind it: normally done already)
+        HIPCHK(hipStreamSynchronize(c->ctx->stream));
+        sl.host_sync = false;
+    }
+    hipError_t e = sl.copying ? hipEventQuery(sl.ev) : hipSuccess;
     *done = false;
     if (e == hipErrorNotReady) {
         if (!block) return XC_OK;
         e = spin_wait(sl.ev);
     }
     if (e != hipSuccess) return fail(XC_EDEVICE, std::string("lookup hits: ") + hipGetErrorString(e));
+    sl.copying = false;
     const auto t0 = std::chrono::steady_clock::now();
     uint64_t n = 0;
     uint32_t end = block ? sl.nb : (uint32_t)std::min<uint64_t>(sl.nb, (uint64_t)sl.next_b + max_b);
@@ -1750,22 +1764,21 @@ static int hits_replay(xc_cache *c, bool block)
 
 // A finished run's hits into the next slot (enqueued behind the run: tokens and collision records
 // are final, the tail check's included).
-static int hits_enqueue(xc_plan *p)
+// The host paths' plan pools (plan_acquire): at most this many plans of at most this many buffers.
+static const size_t PLAN_POOL_MAX = 8;
+static const uint64_t PLAN_POOL_NBUF = 64;
+
+// The next slot for run p's hits: its older hits replayed first (the FIFO keeps the runs' order),
+// buffers of the run's size.
+static int hits_slot(xc_plan *p, int *slot)
 {
     xc_cache *c = p->cache;
-    if (!p->nb) return XC_OK;
-    const int si = c->hl_next;
-    // the slot's older hits first (the FIFO keeps the runs' order)
+    const int si = *slot = c->hl_next;
     while (std::find(c->hl_fifo.begin(), c->hl_fifo.end(), si) != c->hl_fifo.end()) {
         bool done = false;
         if (int rc = hits_replay_front(c, true, &done)) return rc;
     }
     xc_cache::HitSlot &sl = c->hl[si];
-    hipStream_t m = c->ctx->stream;
-    if (!c->hl_stream) {
-        HIPCHK(hipStreamCreateWithFlags(&c->hl_stream, hipStreamNonBlocking));
-        HIPCHK(hipEventCreateWithFlags(&c->hl_packed, hipEventDisableTiming));
-    }
     if (!sl.ev) HIPCHK(hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
     const size_t words = p->hit_base[p->nb];
     if (sl.cap < words || sl.tb_cap < (size_t)p->nb + 1) {
@@ -1787,6 +1800,49 @@ static int hits_enqueue(xc_plan *p)
         sl.hd = (uint64_t *)dp;
         sl.cap = cap;
         sl.tb_cap = tbc;
+        sl.copying = false;
+    }
+    return XC_OK;
+}
+
+// A host-path run's hits (its host synchronises the context stream right after the run): k_hits
+// writes them straight into the slot's pinned memory behind the run, with no copy, stream or event.
+static int hits_enqueue_direct(xc_plan *p)
+{
+    xc_cache *c = p->cache;
+    if (!p->nb) return XC_OK;
+    int si = 0;
+    if (int rc = hits_slot(p, &si)) return rc;
+    xc_cache::HitSlot &sl = c->hl[si];
+    if (sl.copying) {  // (a dropped slot's copy may still run into h)
+        HIPCHK(hipEventSynchronize(sl.ev));
+        sl.copying = false;
+    }
+    hipLaunchKernelGGL(k_hits, dim3((p->nb + 3) / 4), dim3(256), 0, c->ctx->stream, p->P, sl.hd);
+    HIPCHK(hipGetLastError());
+    sl.rec_base = p->hit_base;
+    sl.serial = 0;  // (dtb does not hold this layout)
+    sl.nb = p->nb;
+    sl.next_b = 0;
+    sl.host_sync = true;
+    c->hl_fifo.push_back(si);
+    c->hl_next = si ^ 1;
+    return XC_OK;
+}
+
+// A finished run's hits into the next slot (enqueued behind the run: tokens and collision records
+// are final, the tail check's included), copied to the host on the hit-log stream.
+static int hits_enqueue(xc_plan *p)
+{
+    xc_cache *c = p->cache;
+    if (!p->nb) return XC_OK;
+    int si = 0;
+    if (int rc = hits_slot(p, &si)) return rc;
+    xc_cache::HitSlot &sl = c->hl[si];
+    hipStream_t m = c->ctx->stream;
+    if (!c->hl_stream) {
+        HIPCHK(hipStreamCreateWithFlags(&c->hl_stream, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&c->hl_packed, hipEventDisableTiming));
     }
     HIPCHK(hipStreamWaitEvent(m, sl.ev, 0));  // the slot's previous copy has read d
     if (sl.serial != p->serial) {  // (the layout of another plan: its hit_base)
@@ -1807,9 +1863,11 @@ static int hits_enqueue(xc_plan *p)
                            (const uint64_t *)sl.d, sl.hd, (const uint32_t *)sl.dtb, p->nb);
         HIPCHK(hipGetLastError());
     } else {
-        HIPCHK(hipMemcpyAsync(sl.h, sl.d, words * 8, hipMemcpyDeviceToHost, c->hl_stream));
+        HIPCHK(hipMemcpyAsync(sl.h, sl.d, (size_t)p->hit_base[p->nb] * 8, hipMemcpyDeviceToHost, c->hl_stream));
     }
     HIPCHK(hipEventRecord(sl.ev, c->hl_stream));
+    sl.copying = true;
+    sl.host_sync = false;
     sl.nb = p->nb;
     sl.next_b = 0;
     c->hl_fifo.push_back(si);
@@ -1963,7 +2021,6 @@ extern "C" int xc_plan_destroy(xc_plan *p)
     dfree(p->e_in);
     dfree(p->e_out);
     dfree(p->e_len);
-    dfree(p->e_pos);
     dfree(p->e_total);
     for (auto e : p->ev_hash)
         if (e) hipEventDestroy(e);
@@ -1971,6 +2028,7 @@ extern "C" int xc_plan_destroy(xc_plan *p)
         if (e) hipEventDestroy(e);
     if (p->ev_sb0) hipEventDestroy(p->ev_sb0);
     pool_free(p->h_lenpos);
+    pool_free(p->h_st);
     if (p->es) {
         hipStreamSynchronize(p->es);
         hipStreamDestroy(p->es);
@@ -2102,7 +2160,9 @@ extern "C" int xc_plan_set_streams(xc_plan *p, const uint64_t *start, const int6
         p->P.stream_res = nullptr;
         return XC_OK;
     }
+    if (p->inflight) return fail(XC_EBUSY, "a run of this plan is in flight (xc_encode_poll / xc_encode_wait)");
     std::vector<uint4> st(p->nb);
+    bool carried = false;
     for (uint32_t i = 0; i < p->nb; i++) {
         const uint64_t n = p->len[i], a = start ? start[i] : 0;
         const int64_t c = cand ? cand[i] : -1;
@@ -2111,14 +2171,28 @@ extern "C" int xc_plan_set_streams(xc_plan *p, const uint64_t *start, const int6
         if (a > n || (c >= 0 && ((uint64_t)c + XC_SEG > a || (uint64_t)c + 2 * XC_SEG - 1 < a)) || c < -1)
             return fail(XC_EINVAL, "invalid stream state for buffer " + std::to_string(i));
         st[i] = make_uint4((uint32_t)a, c < 0 ? NONE : (uint32_t)c, flags ? flags[i] & SF_NOFLUSH : 0u, 0u);
+        carried |= c >= 0;
     }
     const size_t nb1 = std::max<uint32_t>(p->nb, 1);
     if (!p->d_stream_st) {
         HIPCHK(dmalloc(&p->d_stream_st, nb1 * sizeof(uint4)));
         HIPCHK(dmalloc(&p->d_stream_res, nb1 * sizeof(uint2)));
+        if (hmalloc((void **)&p->h_st, nb1 * sizeof(uint4)) != hipSuccess) return fail(XC_ENOMEM, "pinned allocation failed");
     }
-    if (p->nb) HIPCHK(hipMemcpyAsync(p->d_stream_st, st.data(), p->nb * sizeof(uint4), hipMemcpyHostToDevice, s));
-    HIPCHK(hipStreamSynchronize(s));
+    // (the same states as the device holds, e.g. a pooled plan of one connection's calls: no copy;
+    // else through pinned staging, ordered before the run on the context stream: no host wait.
+    // The staging is rewritten only here, after the plan's last run, which the copy preceded)
+    const bool same = p->st_dev.size() == st.size() &&
+                      std::equal(st.begin(), st.end(), p->st_dev.begin(), [](const uint4 &x, const uint4 &y) {
+                          return x.x == y.x && x.y == y.y && x.z == y.z && x.w == y.w;
+                      });
+    if (p->nb && !same) {
+        HIPCHK(hipStreamSynchronize(s));  // (an earlier upload from the staging has been done)
+        std::copy(st.begin(), st.end(), p->h_st);
+        HIPCHK(hipMemcpyAsync(p->d_stream_st, p->h_st, p->nb * sizeof(uint4), hipMemcpyHostToDevice, s));
+        p->st_dev = st;
+    }
+    p->cand_carried = carried;
     p->P.stream_st = p->d_stream_st;
     p->P.stream_res = p->d_stream_res;
     return XC_OK;
@@ -2131,7 +2205,8 @@ extern "C" int xc_plan_stream_results(xc_plan *p, uint64_t *base, int64_t *cand)
     int rc = set_dev(p->cache->ctx);
     if (rc) return rc;
     std::vector<uint2> r(p->nb);
-    if (p->nb) HIPCHK(hipMemcpy(r.data(), p->d_stream_res, p->nb * sizeof(uint2), hipMemcpyDeviceToHost));
+    if (p->res_staged && p->nb) memcpy(r.data(), p->h_lenpos + 2 * (size_t)p->nb, p->nb * sizeof(uint2));  // (nb >= 1)
+    else if (p->nb) HIPCHK(hipMemcpy(r.data(), p->d_stream_res, p->nb * sizeof(uint2), hipMemcpyDeviceToHost));
     for (uint32_t i = 0; i < p->nb; i++) {
         base[i] = r[i].x;
         cand[i] = r[i].y == NONE ? -1 : (int64_t)r[i].y;
@@ -2416,7 +2491,7 @@ static int enqueue_block_hash(xc_plan *p, uint32_t k, hipEvent_t after, hipStrea
 {
     const bool side = st == p->hs;
     if (after) HIPCHK(hipStreamWaitEvent(st, after, 0));
-    if (p->host_path) HIPCHK(hipStreamWaitEvent(st, p->ev_h2d[k], 0));  // its input has landed
+    if (p->host_path && !p->h2d_inline) HIPCHK(hipStreamWaitEvent(st, p->ev_h2d[k], 0));  // its input has landed
     const uint32_t g0 = p->grp_base[p->sub[k]], g1 = p->grp_base[p->sub[k + 1]];
     // a range of block groups; on the side stream (sub-batch k - 1 on the main stream) the block
     // compares against the entries complete when k - 1 started
@@ -2699,9 +2774,10 @@ static int encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64
         // replay such runs (xc_memcache.cpp)
         if (xc__mem_live(c->mem)) return fail(XC__SLOW, "a hash entered twice is in the recent window");
         p->count0 = -1;
-        if (p->P.stream_st) {  // (only a carried candidate can enter a hash twice)
+        if (p->P.stream_st && p->cand_carried) {  // (only a carried candidate can enter a hash twice)
             uint32_t n = 0;
-            if ((rc = cache_count_host(c, &n))) return rc;
+            if (c->host_count >= 0) n = (uint32_t)c->host_count;
+            else if ((rc = cache_count_host(c, &n))) return rc;
             p->count0 = n;
         }
     }
@@ -2728,6 +2804,7 @@ static int encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64
     p->P.out_len = d_out_len;
     p->stats = xc_run_stats{};
     p->tail_enqueued = false;
+    p->res_staged = false;
     {   // the first scans' level-1 image: folded while it keeps >= 16 bits per key (the keys of
         // the cache at the start, when known, and every segment this run can enter)
         const uint64_t keys = (p->cache->host_count >= 0 ? (uint64_t)p->cache->host_count : p->cache->cap) + p->max_new;
@@ -2925,7 +3002,10 @@ static int encode_finish(xc_plan *p)
         static const bool no_hits = getenv("XC_NO_HITS") && atoi(getenv("XC_NO_HITS"));
         if (!no_hits && (ctl[CTL_NREF] || ctl[CTL_COLLS] || p->anc_any)) {
             if ((rc = hits_flush(c))) return rc;
-            c->hl_pend = p;  // (packed at the next operation on the cache)
+            // (a small host-path run: into pinned memory now, its host's synchronisation follows)
+            if (p->host_path && p->nb <= PLAN_POOL_NBUF) rc = hits_enqueue_direct(p);
+            else c->hl_pend = p;  // (packed at the next operation on the cache)
+            if (rc) return rc;
         }
     }
     return XC_OK;
@@ -3066,8 +3146,10 @@ extern "C" int xc_encode_run_host(xc_plan *p, const uint8_t *h_in, uint8_t *h_ou
     if (!p->e_in) {  // device arenas and the copy stream, kept for later runs
         HIPCHK(dmalloc(&p->e_in, p->in_bytes));
         HIPCHK(dmalloc(&p->e_out, p->out_bytes));
-        HIPCHK(dmalloc(&p->e_len, std::max<uint64_t>(p->nb, 1) * 8));
-        HIPCHK(dmalloc(&p->e_pos, std::max<uint64_t>(p->nb, 1) * 8));
+        const uint64_t nb1 = std::max<uint64_t>(p->nb, 1);
+        HIPCHK(dmalloc(&p->e_len, nb1 * 24));
+        p->e_pos = p->e_len + nb1;
+        p->e_res = (uint2 *)(p->e_len + 2 * nb1);
         HIPCHK(dmalloc(&p->e_total, 8));
         if (!p->cache->ctx->copy) HIPCHK(hipStreamCreateWithFlags(&p->cache->ctx->copy, hipStreamNonBlocking));
         p->cs = p->cache->ctx->copy;
@@ -3078,33 +3160,46 @@ extern "C" int xc_encode_run_host(xc_plan *p, const uint8_t *h_in, uint8_t *h_ou
     if (hipHostGetDevicePointer(&dev_out, h_out, 0) != hipSuccess || !dev_out)
         return fail(XC_EINVAL, "h_out is not pinned host memory (use xc_host_alloc)");
     // every sub-batch's input on the copy stream, in order; sub-batch k's block hashing (the
-    // first kernel to read it) waits for its event
-    HIPCHK(hipEventRecord(p->ev_start, s));
-    HIPCHK(hipStreamWaitEvent(p->cs, p->ev_start, 0));
-    for (size_t k = 0; k + 1 < p->sub.size(); k++) {
-        const uint64_t a = p->nb ? p->in_off[p->sub[k]] : 0;
-        const uint64_t b = p->sub[k + 1] < p->nb ? p->in_off[p->sub[k + 1]] : p->in_bytes;
-        if (b > a) HIPCHK(hipMemcpyAsync(p->e_in + a, h_in + a, b - a, hipMemcpyHostToDevice, p->cs));
-        HIPCHK(hipEventRecord(p->ev_h2d[k], p->cs));
+    // first kernel to read it) waits for its event.  A run of one sub-batch has nothing to overlap
+    // the copy with: on the context stream, no events (a cross-stream wait idles the device ~6 us)
+    p->h2d_inline = p->sub.size() <= 2;
+    if (p->h2d_inline) {
+        if (p->in_bytes) HIPCHK(hipMemcpyAsync(p->e_in, h_in, p->in_bytes, hipMemcpyHostToDevice, s));
+    } else {
+        HIPCHK(hipEventRecord(p->ev_start, s));
+        HIPCHK(hipStreamWaitEvent(p->cs, p->ev_start, 0));
+        for (size_t k = 0; k + 1 < p->sub.size(); k++) {
+            const uint64_t a = p->nb ? p->in_off[p->sub[k]] : 0;
+            const uint64_t b = p->sub[k + 1] < p->nb ? p->in_off[p->sub[k + 1]] : p->in_bytes;
+            if (b > a) HIPCHK(hipMemcpyAsync(p->e_in + a, h_in + a, b - a, hipMemcpyHostToDevice, p->cs));
+            HIPCHK(hipEventRecord(p->ev_h2d[k], p->cs));
+        }
     }
-    HIPCHK(hipMemsetAsync(p->e_total, 0, 8, s));
+    // (the packed total starts at 0 with the run's first buffers: k_pack_offsets)
     p->host_path = true;
     p->pack_dst = (uint8_t *)dev_out;
     p->pack_cap = h_out_cap;
+    uint2 *const res_dev = p->P.stream_res;  // (the run's stream results into the same block)
+    if (res_dev) p->P.stream_res = p->e_res;
     rc = xc_encode_run(p, p->e_in, p->e_out, p->e_len);
+    p->P.stream_res = res_dev;
     p->host_path = false;
     if (rc) {
         hipStreamSynchronize(p->cs);
+        hipStreamSynchronize(s);
         return rc;
     }
     if (p->nb) {  // (through the plan's pinned copy of them: pageable copies stage synchronously)
-        if (!p->h_lenpos && hmalloc((void **)&p->h_lenpos, (size_t)p->nb * 16) != hipSuccess)
+        const uint64_t nb1 = std::max<uint64_t>(p->nb, 1);
+        if (!p->h_lenpos && hmalloc((void **)&p->h_lenpos, (size_t)nb1 * 24) != hipSuccess)
             return fail(XC_ENOMEM, "pinned allocation failed");
-        HIPCHK(hipMemcpyAsync(p->h_lenpos, p->e_len, p->nb * 8, hipMemcpyDeviceToHost, s));
-        if (h_pos) HIPCHK(hipMemcpyAsync(p->h_lenpos + p->nb, p->e_pos, p->nb * 8, hipMemcpyDeviceToHost, s));
+        // lengths, positions and (xc_plan_stream_results reads them from here) stream results
+        HIPCHK(hipMemcpyAsync(p->h_lenpos, p->e_len, nb1 * (res_dev ? 24 : 16), hipMemcpyDeviceToHost, s));
+        p->res_staged = res_dev != nullptr;
     }
     // (the run's lookup hits go to the recent window through the cache's hit log, hits_enqueue)
     HIPCHK(hipStreamSynchronize(s));
+    for (auto &sl : p->cache->hl) sl.host_sync = false;  // (written behind the run: complete now)
     if (p->nb) {
         memcpy(h_len, p->h_lenpos, p->nb * 8);
         if (h_pos) memcpy(h_pos, p->h_lenpos + p->nb, p->nb * 8);
@@ -3120,8 +3215,6 @@ extern "C" int xc_encode_run_host(xc_plan *p, const uint8_t *h_in, uint8_t *h_ou
 // The host paths' plans (xc__encode_batch_host_coll, xc__encode_gather): a plan of these exact
 // lengths from the cache's pool, else a new one; released plans go back (small batches only: a
 // pooled plan holds its device workspace).
-static const size_t PLAN_POOL_MAX = 8;
-static const uint64_t PLAN_POOL_NBUF = 64;
 static int plan_acquire(xc_cache *c, const uint64_t *len, uint64_t nbuf, xc_plan **out)
 {
     for (size_t k = c->plan_pool.size(); k-- > 0;) {
