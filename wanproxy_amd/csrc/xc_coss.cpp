@@ -815,9 +815,10 @@ static int replay_gather(C *c, uint64_t nbuf, const uint8_t *const *head, const 
             return xc__set_error(XC_EINVAL, "invalid stream state");
         items.push_back({i, data[i].data(), data[i].size(), start[i], cand[i], 0, (flags[i] & 1u) != 0});
     }
-    std::vector<uint8_t> obuf(std::max<uint64_t>(osz, 1));
-    int rc = replay::encode(c, std::move(items), obuf.data(), ooff.data(), ocap.data(), olen.data(), rbase, rcand);
-    for (uint64_t i = 0; i < nbuf && !rc; i++) rc = take(ctx, i, obuf.data() + ooff[i], olen[i], data[i].data());
+    static thread_local replay::Scratch s_out;  // (grow-only, not zeroed)
+    uint8_t *const obuf = s_out.get(osz);
+    int rc = replay::encode(c, std::move(items), obuf, ooff.data(), ocap.data(), olen.data(), rbase, rcand);
+    for (uint64_t i = 0; i < nbuf && !rc; i++) rc = take(ctx, i, obuf + ooff[i], olen[i], data[i].data());
     return rc;
 }
 

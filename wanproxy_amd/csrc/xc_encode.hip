@@ -1524,6 +1524,42 @@ __device__ __forceinline__ uint64_t group_anchors(const PlanDev &P, uint32_t g, 
         const uint32_t p0 = (k0 + i) * XC_SEG + 32u * l;
         if (p0 < 63u) m &= p0 + 31u >= 63u ? ~0u >> (63u - p0) : 0u;  // bit 31 - t: t >= 63 - p0
         if (p0 + 32u > len) m &= p0 >= len ? 0u : ~(~0u >> (len - p0));  // t < len - p0
+        if (!keep) {
+            // a block whose records are dropped: only its first and last anchor (the group record)
+            // and its key, from the masks and two tile reads (no list, no fingerprints); a block
+            // whose anchors may hold a gap inside it takes the full pass below
+            const uint64_t lanes = ballot(m != 0u);
+            if (!lanes) {
+                if (i < n && l == i) bkey = ANC_NONE;
+                wave_sync();
+                continue;
+            }
+            const int f = __ffsll((unsigned long long)lanes) - 1, L = 63 - __builtin_clzll(lanes);
+            const uint32_t fbk = 32u * (uint32_t)f + (uint32_t)__builtin_clz(readlane(m, f));
+            const uint32_t cpk = 32u * (uint32_t)L + 31u - (uint32_t)__builtin_ctz(readlane(m, L));
+            if (cpk - fbk < XC_SEG - 62u) {
+                const uint32_t gf = i * XC_SEG + fbk;
+                if (firstp == NONE) firstp = gf;
+                if (lastp != NONE && gf - lastp >= XC_SEG - 62u) {
+                    if (l == 0 && ngap < AGAP_CAP) P.agap[g * AGAP_CAP + ngap] = make_uint2(lastp, gf);
+                    ngap++;
+                }
+                lastp = i * XC_SEG + cpk;
+                if (i < n) {
+                    uint64_t key = ANC_NONE;
+                    if (cpk >= 63u) {
+                        wave_sync();  // (the gear pass's tile writes of the other lanes)
+                        const uint32_t ln = cpk >> 5, t = cpk & 31u;
+                        const uint32_t gv = tile[t * XC_TILE_ROW + ln];
+                        const uint32_t g2 = ln ? tile[t * XC_TILE_ROW + ln - 1u] : prev[t];
+                        key = anc_key(anc_fp(gv, g2), cpk);
+                    }
+                    if (l == i) bkey = key;
+                }
+                wave_sync();  // (the next block's tile overwrites this one)
+                continue;
+            }
+        }
         // compaction: every anchor's block offset, in position order, ANC_LIST entries per pass (a
         // random block has ~32 anchors: one pass; a constant run can make every position one)
         const uint32_t k = (uint32_t)__popc(m), incl = wave_incl_scan(k);
@@ -1551,21 +1587,27 @@ __device__ __forceinline__ uint64_t group_anchors(const PlanDev &P, uint32_t g, 
             const uint64_t fp = anc_fp(gv, g2);
             // a run continues when the entry before has the position before (inside one lane's
             // 32 positions) and the same fingerprint
-            uint32_t pp = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * ((l + 63u) & 63u)), (int)p);
-            uint32_t fl = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * ((l + 63u) & 63u)), (int)(uint32_t)fp);
-            uint32_t fh = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * ((l + 63u) & 63u)), (int)(uint32_t)(fp >> 32));
-            const uint64_t pfp = ((uint64_t)fh << 32) | fl;
+            // the entry before's position and fingerprint (lane l - 1: a DPP wave shift, no LDS)
+            const uint32_t pp = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)p, 0x138, 0xf, 0xf, false);
+            const uint32_t fl = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)fp, 0x138, 0xf, 0xf, false);
+            const uint32_t fh = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(fp >> 32), 0x138, 0xf, 0xf, false);
             // (a run does not continue across 64 entries: a chunk's first entry is a head)
-            const bool cont = live && l != 0u && (p & 31u) != 0u && pp + 1u == p && pfp == fp;
+            const bool cont = live && l != 0u && (p & 31u) != 0u && pp + 1u == p && fl == (uint32_t)fp &&
+                              fh == (uint32_t)(fp >> 32);
             if (b0 == 0u) fb = readlane(p, 0);
-            const uint64_t heads = ballot(live && !cont);
-            const uint64_t above = heads & (l == 63u ? 0ull : ~0ull << (l + 1u));
-            const uint32_t end = above ? b0 + (uint32_t)__builtin_ctzll(above) : min(total, b0 + 64u);
             const bool head = live && !cont;
+            const uint64_t heads = ballot(head);
+            const bool runs = ballot(cont) != 0ull;  // (every lane: a ballot inside the branch below sees heads only)
             if (keep) {
                 if (head) {
+                    // a run's length: up to the next head (without runs, the common case: 1)
+                    uint32_t n1 = 1u;
+                    if (runs) {
+                        const uint64_t above = heads & (l == 63u ? 0ull : ~0ull << (l + 1u));
+                        n1 = (above ? b0 + (uint32_t)__builtin_ctzll(above) : min(total, b0 + 64u)) - idx;
+                    }
                     const uint32_t ri = cnt + mbcnt(heads);
-                    if (ri < REC_CAP) P.rec[(size_t)g * REC_CAP + ri] = rec_make(fp, i * XC_SEG + p, end - idx);
+                    if (ri < REC_CAP) P.rec[(size_t)g * REC_CAP + ri] = rec_make(fp, i * XC_SEG + p, n1);
                 }
                 cnt += (uint32_t)__popcll(heads);
             }

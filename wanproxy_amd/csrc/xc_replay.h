@@ -29,6 +29,7 @@
 #include <thread>
 #include <unordered_map>
 #include <unordered_set>
+#include <memory>
 #include <vector>
 
 #include "../../include/xcodec_hip.h"
@@ -97,6 +98,24 @@ inline uint64_t fingerprint(const uint8_t *p)
 // The hashes an operation touched, looked up again without side effects: those the device holds
 // and a lookup no longer finds, and those a lookup finds that the device lacks or holds with other
 // bytes, go into ch (and `known` follows).
+// Grow-only byte scratch, not value-initialised: a COSS batch's arenas (64 MiB in, 128 MiB out, 32
+// MiB of payloads per 1024 x 64 KiB) as fresh std::vectors cost more in zeroing and first-touch page
+// faults than the device's encode of them.  One per purpose and thread (the engine runs on the
+// caller's thread).
+struct Scratch {
+    std::unique_ptr<uint8_t[]> p;
+    size_t n = 0;
+    uint8_t *get(size_t m)
+    {
+        m = std::max<size_t>(m, 1);
+        if (m > n) {
+            p.reset(new uint8_t[m]);
+            n = m;
+        }
+        return p.get();
+    }
+};
+
 struct SettleStats {  // (XC_REPLAY_PROF)
     uint64_t calls = 0, cand = 0, same = 0, reads = 0, copies = 0, ranges = 0;
 };
@@ -413,10 +432,11 @@ int encode(C *c, std::vector<CItem> items, uint8_t *out, const uint64_t *out_off
             start[k] = items[k].start;
             cand[k] = items[k].cand;
         }
-        std::vector<uint8_t> arena(std::max<uint64_t>(isz, 1)), obuf(std::max<uint64_t>(osz, 1));
+        static thread_local Scratch s_arena, s_obuf;
+        uint8_t *const arena = s_arena.get(isz), *const obuf = s_obuf.get(osz);
         for (uint64_t k = 0; k < m; k++)
             if (items[k].len) std::memcpy(&arena[ioff[k]], items[k].data, items[k].len);
-        rc = xc__encode_batch_host_coll(c->cache, arena.data(), ioff.data(), ilen.data(), m, obuf.data(), ooff.data(),
+        rc = xc__encode_batch_host_coll(c->cache, arena, ioff.data(), ilen.data(), m, obuf, ooff.data(),
                                         ocap.data(), olen.data(), start.data(), cand.data(), fl.data(), rbase.data(),
                                         rcand.data(), ccnt.data(), coll.data());
         if (rc) return rc;
@@ -489,9 +509,10 @@ int encode(C *c, std::vector<CItem> items, uint8_t *out, const uint64_t *out_off
         // EXTRACT hashes (XCodecHash::hash of the payloads) on the device, one call
         std::vector<uint64_t> ph(payloads.size());
         if (!payloads.empty()) {
-            std::vector<uint8_t> segs(payloads.size() * (size_t)SEG);
+            static thread_local Scratch s_segs;
+            uint8_t *const segs = s_segs.get(payloads.size() * (size_t)SEG);
             for (size_t i = 0; i < payloads.size(); i++) std::memcpy(&segs[i * SEG], payloads[i], SEG);
-            if ((rc = xc__hash_segments_host_raw(c->ctx, segs.data(), payloads.size(), ph.data()))) return rc;
+            if ((rc = xc__hash_segments_host_raw(c->ctx, segs, payloads.size(), ph.data()))) return rc;
         }
         {
             size_t pi = 0;
@@ -670,8 +691,9 @@ int decode(C *c, const uint8_t *in, const uint64_t *in_off, const uint64_t *in_l
             ocap[k] = out_cap[it.buf] - out_len[it.buf];
             osz += ocap[k];
         }
-        std::vector<uint8_t> obuf(std::max<uint64_t>(osz, 1));
-        rc = xc__decode_batch_host_raw(c->cache, in, ioff.data(), ilen.data(), m, obuf.data(), ooff.data(),
+        static thread_local Scratch s_dout;
+        uint8_t *const obuf = s_dout.get(osz);
+        rc = xc__decode_batch_host_raw(c->cache, in, ioff.data(), ilen.data(), m, obuf, ooff.data(),
                                        ocap.data(), olen.data(), cons.data(), st.data(), unk.data(), hu.data());
         if (rc) return rc;
         // events: every EXTRACT / REF token the decoder executed (xcodec_decoder.cc:85-173)
@@ -711,9 +733,10 @@ int decode(C *c, const uint8_t *in, const uint64_t *in_off, const uint64_t *in_l
         }
         std::vector<uint64_t> ph(payloads.size());
         if (!payloads.empty()) {
-            std::vector<uint8_t> segs(payloads.size() * (size_t)SEG);
+            static thread_local Scratch s_dsegs;
+            uint8_t *const segs = s_dsegs.get(payloads.size() * (size_t)SEG);
             for (size_t i = 0; i < payloads.size(); i++) std::memcpy(&segs[i * SEG], payloads[i], SEG);
-            if ((rc = xc__hash_segments_host_raw(c->ctx, segs.data(), payloads.size(), ph.data()))) return rc;
+            if ((rc = xc__hash_segments_host_raw(c->ctx, segs, payloads.size(), ph.data()))) return rc;
             size_t pi = 0;
             for (auto &v : ev)
                 for (DEv &e : v)

@@ -2887,10 +2887,14 @@ static int launch_tailcheck(xc_plan *p)
     xc_cache *c = p->cache;
     if (!(p->anc_any && c->mem && !c->engine && p->nb)) return XC_OK;
     hipStream_t s = c->ctx->stream;
-    hipLaunchKernelGGL(k_tailcheck, dim3(4u * c->ctx->n_cu), dim3(256), 0, s, p->P, p->nb, p->d_tcnt, p->d_tlist);
+    // a small grid (the tail is a few buffers: ~100 blocks on cfg5): the next run's early block hashing
+    // fills the CUs meanwhile, and each workgroup of a wide grid waits for a slot, even one with
+    // nothing to do (1024 workgroups: 340 us per cfg5 step instead of 30)
+    static const uint32_t grid = getenv("XC_TAIL_GRID") ? (uint32_t)atoi(getenv("XC_TAIL_GRID")) : 64u;
+    hipLaunchKernelGGL(k_tailcheck, dim3(std::max(1u, grid)), dim3(256), 0, s, p->P, p->nb, p->d_tcnt, p->d_tlist);
     HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_tailfinal, dim3(std::min<uint32_t>(p->nb, 1024u)), dim3(64), 0, s, p->P, p->nb, p->d_tcnt,
-                       (const uint4 *)p->d_tlist);
+    hipLaunchKernelGGL(k_tailfinal, dim3(std::min<uint32_t>(p->nb, std::max(1u, grid))), dim3(64), 0, s, p->P, p->nb,
+                       p->d_tcnt, (const uint4 *)p->d_tlist);
     HIPCHK(hipGetLastError());
     return XC_OK;
 }
