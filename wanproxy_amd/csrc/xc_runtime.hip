@@ -2833,16 +2833,26 @@ static int encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64
     // which k_blockpredict, after it, finds too)
     const uint32_t floor = c->removed_floor;
     c->removed_floor = 0xFFFFFFFFu;
+    // (XC_EARLY_ALL=0, A/B: only sub-batch 0 ahead, the later ones chained after its set clear)
+    static const bool early_all = !(getenv("XC_EARLY_ALL") && !atoi(getenv("XC_EARLY_ALL")));
+    uint32_t hashed = 0;
     if (early) {
-        if ((rc = enqueue_block_hash(p, 0, p->ev_sb0, p->hs, false, p->P.sb_count + (p->sub.size() - 2), floor)))
-            return rc;
+        // every sub-batch's blocks ahead, back to back on the side stream (their compares take the
+        // same entries: complete when the previous run's last sub-batch started, under the floor);
+        // the main stream then records no start event for them (an event between two of its
+        // kernels idles the device ~6 us) and sub-batch 1's hashing starts as soon as 0's ends
+        const uint32_t *lim = p->P.sb_count + (p->sub.size() - 2);
+        const uint32_t upto = early_all ? (uint32_t)p->sub.size() - 1 : 1u;
+        for (uint32_t k = 0; k < upto; k++)
+            if ((rc = enqueue_block_hash(p, k, k == 0 ? p->ev_sb0 : nullptr, p->hs, false, lim, floor))) return rc;
+        hashed = upto;
         p->early_runs++;
         p->stats.early_hashed = 1;
     }
     p->cache->host_count = -1;
     if (p->sub.size() > 1) p->zero_ctl = true;  // (the first k_clear_set clears the control words)
     else HIPCHK(hipMemsetAsync(p->P.ctl, 0, CTL_WORDS * 4, s));
-    p->next_hash = early ? 1u : 0u;  // (sub-batch 0 hashed ahead: its predictions wait for ev_hash[0])
+    p->next_hash = hashed;  // (sub-batches hashed ahead: their predictions wait for ev_hash[k])
     const size_t nsub = p->sub.size() - 1;
     if ((rc = ctl_buffers(p))) return rc;
     p->rec_sb0 = p->input_ready && p->sub.size() > 2;
