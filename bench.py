@@ -35,7 +35,11 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 SEG = 2048
 GOLD = os.path.join(ROOT, "tests", "golden", "fullsize_digests.npz")
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r04")
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r05")
+# The secondary legs (cfg2, cfg3, cfg4) time at least this many steps: their steps are 0.07-0.36 ms, so
+# 20 steps (a few ms) measured the first steps' launch ramp too (cfg4: 1319-1333 GiB/s over 20 steps,
+# 1367-1379 over 200, profiles/r05/ab/leg_steps_r5d.txt)
+LEG_STEPS = 200
 
 
 def parse():
@@ -146,7 +150,7 @@ def bench_encode_leg(ctx, warm, bufs, steps, case):
     alg = int(lens.sum()) + int(olen.sum()) + SEG * (int(st.n_extract) + int(st.n_ref))
     plan.close()
     cache.close()
-    return dict({"value": round(int(lens.sum()) / el / 2**30, 3), "unit": "GiB/s", "ms_per_step": round(el * 1e3, 3),
+    return dict({"value": round(int(lens.sum()) / el / 2**30, 3), "unit": "GiB/s", "ms_per_step": round(el * 1e3, 3), "steps": steps,
                  "buffers": n, "out_over_in": round(float(olen.sum()) / float(lens.sum()), 4),
                  "roofline": {"alg_bytes_per_step": alg, "achieved": round(alg / el / 1e9, 1),
                               "frac": round(alg / el / 1e9 / HBM_PEAK_GBS, 4)}}, **ver)
@@ -195,14 +199,15 @@ def bench_decode(args, ctx, warm):
         dc.restore_async()
         plan.run(d_in.data_ptr(), d_out.data_ptr(), p64, p64 + 8 * n, p32, p64 + 16 * n, p32 + 4 * n)
 
+    steps = max(args.steps, LEG_STEPS)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     torch.cuda.synchronize()
-    el = (time.perf_counter() - t0) / args.steps
+    el = (time.perf_counter() - t0) / steps
     st = plan.stats()
     # round trip: decoded stream i == buffer i, status true, everything consumed
     assert all(int(plan.out_off[i]) == i * W.BUF for i in range(n))
@@ -215,7 +220,7 @@ def bench_decode(args, ctx, warm):
     enc_bytes, dec_bytes = int(lens.sum()), n * W.BUF
     alg = enc_bytes + dec_bytes + SEG * (int(st.n_entered) + int(st.n_ref))
     return {"workload": "cfg4", "streams": n, "value": round(dec_bytes / el / 2**30, 3),
-            "unit": "GiB/s decoded (device resident)", "ms_per_step": round(el * 1e3, 3),
+            "unit": "GiB/s decoded (device resident)", "ms_per_step": round(el * 1e3, 3), "steps": steps,
             "enc_GiBs": round(enc_bytes / el / 2**30, 3),
             "roofline": {"bound": "hbm", "alg_bytes_per_step": alg, "achieved": round(alg / el / 1e9, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(alg / el / 1e9 / HBM_PEAK_GBS, 4)},
@@ -605,9 +610,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_legs:
         # BASELINE.json configs[1] and [2] (parity-test cases; value stays cfg5)
         result["other_configs"] = {
-            "cfg2": dict(bench_encode_leg(ctx, None, W.random_buffers(256), 20, "cfg2"),
+            "cfg2": dict(bench_encode_leg(ctx, None, W.random_buffers(256), max(args.steps, LEG_STEPS), "cfg2"),
                          workload="256 x 64 KiB, 0% repeats, cold (empty) cache"),
-            "cfg3": dict(bench_encode_leg(ctx, warm, list(W.repeat_shard(4096, 0x77)), 20, "cfg3"),
+            "cfg3": dict(bench_encode_leg(ctx, warm, list(W.repeat_shard(4096, 0x77)), max(args.steps, LEG_STEPS),
+                                          "cfg3"),
                          workload="4096 x 64 KiB, 50% repeats, seed 0x77, warm pool cache"),
         }
 

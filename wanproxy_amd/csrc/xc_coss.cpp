@@ -195,19 +195,52 @@ public:
     // and the stamp of r's last full store -- equal ids have equal bytes.
     int peek(uint64_t h, const uint8_t **p, Loc *l, uint64_t *id) const
     {
+        if (peek_window(h, p, id)) return FOUND;
+        auto it = index_.find(h);
+        if (it == index_.end()) return ABSENT;
+        const Loc e = it->second;
+        return peek_at(h, e, first_slot(e.range), p, l, id);
+    }
+
+    // The owners of stripe `range` (the hashes whose index entries point into it), each peeked:
+    // f(hash, peek's result, p, l, id).  The index entry of an owner is (range, its position) and
+    // the first slot is the range's for every owner: no index lookup, no slot search per hash (the
+    // replay's settle peeks every owner of every touched range, ~a million per 64 MiB batch).
+    template <class F>
+    void peek_owners(uint64_t range, F f) const
+    {
+        if (range >= limit_) return;
+        const int s = first_slot(range);
+        const uint64_t *own = &owner_[range * STRIPE_SEGS];
+        for (uint32_t i = 0; i < STRIPE_SEGS; i++) {
+            const uint64_t h = own[i];
+            if (!h) continue;
+            const uint8_t *p = nullptr;
+            Loc l{0, 0};
+            uint64_t id[2] = {0, 0};
+            const int r = peek_window(h, &p, id) ? FOUND : peek_at(h, Loc{range, i}, s, &p, &l, id);
+            f(h, r, p, l, id);
+        }
+    }
+
+    // peek's first step: the recent window (find_recent, xcodec_cache.h:137-147)
+    bool peek_window(uint64_t h, const uint8_t **p, uint64_t *id) const
+    {
         for (int i = 0; i < (wcnt_[wbucket(h)] ? WINDOW : 0); i++)
             if (win_[i].hash == h) {
                 if (win_[i].data) {
                     *p = win_[i].data;
                     slot_id(win_[i].data, id);
-                    return FOUND;
+                    return true;
                 }
                 break;
             }
-        auto it = index_.find(h);
-        if (it == index_.end()) return ABSENT;
-        const Loc e = it->second;
-        const int s = first_slot(e.range);
+        return false;
+    }
+
+    // peek's rest, for a hash not in the window whose index entry is e, the first slot of its range s
+    int peek_at(uint64_t h, Loc e, int s, const uint8_t **p, Loc *l, uint64_t *id) const
+    {
         if (s < LOADED) {
             if (slot_[s].h.hash[e.pos] != h) return ABSENT;
             *p = slot_[s].seg[e.pos];
@@ -290,7 +323,7 @@ public:
 
     void all_hashes(std::vector<uint64_t> &out) const
     {
-        for (const auto &kv : index_) out.push_back(kv.first);
+        index_.for_each([&](const Index::Entry &e) { out.push_back(e.first); });
     }
 
     size_t size() const { return index_.size(); }
@@ -453,8 +486,24 @@ private:
             for (int i = 0; i < LOADED; i++)  // (their data is the file's: read it before it changes)
                 if (i != s && !resident_[i] && slot_[i].h.m.stripe_range == range) materialize(i);
         }
+        // the positions' ids before the store (their bytes are the file's after it)
+        replay::IdMove mv[STRIPE_SEGS];
+        uint16_t mpos[STRIPE_SEGS];
+        uint32_t nmv = 0;
+        if (t && size > sizeof(Header) && range < limit_)
+            for (uint32_t i = 0; i < STRIPE_SEGS; i++)
+                if (slot_[s].h.hash[i]) {
+                    mv[nmv] = replay::IdMove{slot_[s].h.hash[i], {0, 0}, {0, 0}};
+                    slot_id(slot_[s].seg[i], mv[nmv].from);
+                    mpos[nmv++] = (uint16_t)i;
+                }
         if (size > sizeof(Header) && range < limit_) fstamp_[range] = ++stamp_;
         if (::pwrite(fd_, &slot_[s], size, (off_t)pos) == (ssize_t)size) {
+            for (uint32_t k = 0; k < nmv; k++) {  // (peek's IN_FILE id of the position now)
+                mv[k].to[0] = (1ull << 62) | (range << 9) | mpos[k];
+                mv[k].to[1] = fstamp_[range];
+                if (mv[k].from[0]) t->moves.push_back(mv[k]);
+            }
             if (pos + sizeof(Stripe) > file_size_) file_size_ = pos + sizeof(Stripe);
             if (range < limit_) std::memcpy(&file_hash_[range * STRIPE_SEGS], slot_[s].h.hash, sizeof slot_[s].h.hash);
             if (t) t->ranges.push_back(range);
@@ -553,7 +602,8 @@ private:
     std::vector<uint64_t> fstamp_;
     int active_ = 0;
     std::vector<Meta> dir_;
-    std::unordered_map<uint64_t, Loc> index_;
+    using Index = replay::FlatMap<Loc>;
+    Index index_;
     std::vector<uint64_t> owner_;      // [range * 512 + pos]: the hash whose index entry is there
     std::vector<uint64_t> file_hash_;  // [range * 512 + pos]: the stripe headers as in the file
     struct {
@@ -581,7 +631,7 @@ struct xc_coss {
     xc_cache *cache = nullptr;  // the device mirror (null for a host-only store)
     coss::Store st;
     // what the device cache holds: hash -> fingerprint of its bytes
-    std::unordered_map<uint64_t, uint64_t> known;
+    replay::FlatMap<uint64_t> known;
     // hashes a lookup misses only after loading a stripe (a miss with side effects)
     std::unordered_set<uint64_t> load_miss;
 
@@ -606,7 +656,7 @@ struct xc_coss {
             uint64_t id[2] = {0, 0};
             if (st.peek(h, &p, &l, id) == replay::FOUND && id[0] && p && st.in_memory(p) &&
                 std::memcmp(p, seg, replay::SEG) == 0)
-                seen[h] = {id[0], id[1]};
+                seen[h] = Seen{{id[0], id[1]}, {0, 0}};
             return;
         }
         uint8_t b[replay::SEG];
@@ -617,16 +667,34 @@ struct xc_coss {
     void mirrored(const replay::Change &) {}
     // where the mirror's bytes of a hash were last seen in the store (peek's id): unchanged there,
     // the mirror still holds them (xc_replay.h settle)
-    std::unordered_map<uint64_t, std::pair<uint64_t, uint64_t>> seen;
+    // (a hash in seen is in known: both are set together, seen is erased first)
+    // Two ids per hash: where the bytes were last seen, and (a full store of their stripe since) the
+    // file's id of the same bytes -- the slot keeps them after the store, the file after the slot
+    // takes another stripe, and both name them.
+    struct Seen {
+        uint64_t a[2], b[2];
+    };
+    replay::FlatMap<Seen> seen;
     bool same_bytes(uint64_t h, const uint64_t *id) const
     {
         auto it = seen.find(h);
-        return it != seen.end() && it->second.first == id[0] && it->second.second == id[1] && known.count(h);
+        if (it == seen.end()) return false;
+        const Seen &v = it->second;
+        return (v.a[0] == id[0] && v.a[1] == id[1]) || (v.b[0] && v.b[0] == id[0] && v.b[1] == id[1]);
     }
     void note_bytes(uint64_t h, const uint64_t *id)
     {
-        if (id && id[0]) seen[h] = {id[0], id[1]};
+        if (id && id[0]) seen[h] = Seen{{id[0], id[1]}, {0, 0}};
         else seen.erase(h);
+    }
+    // the mirror's bytes of m.h, seen under id m.from, are those under m.to too (a full stripe store)
+    void move_id(const replay::IdMove &m)
+    {
+        // (an id never names other bytes later: versions are stamps, never reused)
+        if (!same_bytes(m.h, m.from)) return;
+        Seen &v = seen.find(m.h)->second;
+        v.b[0] = m.to[0];
+        v.b[1] = m.to[1];
     }
     int begin_pass(const std::vector<uint64_t> &hs, uint64_t count0)
     {

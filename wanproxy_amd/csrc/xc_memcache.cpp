@@ -327,6 +327,8 @@ public:
         return true;
     }
     void owners(uint64_t, std::vector<uint64_t> &) const {}
+    template <class F>
+    void peek_owners(uint64_t, F) const {}  // (no stripe ranges)
     void window_in_slot(int, std::vector<uint64_t> &) const {}
     void count_misses(uint64_t) {}
 };
@@ -615,6 +617,7 @@ struct Ctx {
     // (the memory cache's bytes have no place to version: every settle fingerprints)
     bool same_bytes(uint64_t, const uint64_t *) const { return false; }
     void note_bytes(uint64_t, const uint64_t *) {}
+    void move_id(const replay::IdMove &) {}
     int begin_pass(const std::vector<uint64_t> &hs, uint64_t count0) { return m->begin_pass(hs, count0); }
     int end_pass() { return m->end_pass(); }
 };

@@ -64,9 +64,17 @@ struct Loc {
 
 // What a Store operation touched: the hashes and stripe ranges whose lookup result may have
 // changed, and the slots whose bytes were replaced (recent-window entries point into them).
+// moves: ids (Store::peek's versions of bytes) that name the same bytes as others now -- a full store of
+// a stripe slot writes the slot's bytes to the file, so every position's slot (or earlier file) id and
+// its new file id name the same bytes -- so that the settle does not read and fingerprint them again.
+struct IdMove {
+    uint64_t h;             // the hash stored at the position when its bytes were written
+    uint64_t from[2], to[2];
+};
 struct Touch {
     std::vector<uint64_t> hs, ranges;
     std::vector<int> slots;
+    std::vector<IdMove> moves;
 };
 
 // Store::peek results: FOUND (*p: the bytes), IN_FILE (the stripe is loaded from the file first,
@@ -81,6 +89,110 @@ struct Change {
     std::vector<uint8_t> bytes;     // their bytes, SEG each
     bool new_lm = false;            // a hash became a LOAD_MISS one (a later miss of it has side effects)
     bool any() const { return !removed.empty() || !added.empty(); }
+};
+
+// A hash map keyed by 64-bit hashes: open addressing, linear probing, backward-shift deletion, at
+// most half full.  The COSS replay's settle looks up ~a million hashes per 64 MiB batch (the owners
+// of every touched stripe range), and a node-based std::unordered_map spent most of that time in
+// cache misses.  The subset of std::unordered_map's interface the replay uses: find (an entry
+// pointer, end() = null), count, operator[], emplace, erase, size, clear, for_each.  Inserts and
+// erases invalidate entry pointers.
+template <class V>
+class FlatMap {
+public:
+    struct Entry {
+        uint64_t first;
+        V second;
+    };
+    Entry *end() const { return nullptr; }
+    const Entry *find(uint64_t k) const { return const_cast<FlatMap *>(this)->find(k); }
+    Entry *find(uint64_t k)
+    {
+        if (k == 0) return has0_ ? &zero_ : nullptr;
+        if (!n_) return nullptr;
+        for (size_t i = home(k);; i = (i + 1) & mask_) {
+            if (t_[i].first == k) return &t_[i];
+            if (t_[i].first == 0) return nullptr;
+        }
+    }
+    size_t count(uint64_t k) const { return find(k) ? 1 : 0; }
+    V &operator[](uint64_t k) { return emplace(k, V{}).first->second; }
+    std::pair<Entry *, bool> emplace(uint64_t k, const V &v)
+    {
+        if (k == 0) {
+            if (has0_) return {&zero_, false};
+            has0_ = true;
+            zero_ = Entry{0, v};
+            return {&zero_, true};
+        }
+        if (2 * (n_ + 1) > cap()) grow();
+        size_t i = home(k);
+        for (; t_[i].first != 0; i = (i + 1) & mask_)
+            if (t_[i].first == k) return {&t_[i], false};
+        t_[i] = Entry{k, v};
+        n_++;
+        return {&t_[i], true};
+    }
+    size_t erase(uint64_t k)
+    {
+        Entry *e = find(k);
+        if (!e) return 0;
+        erase(e);
+        return 1;
+    }
+    void erase(Entry *e)
+    {
+        if (e == &zero_) {
+            has0_ = false;
+            return;
+        }
+        size_t i = (size_t)(e - t_.data());
+        for (size_t j = (i + 1) & mask_; t_[j].first != 0; j = (j + 1) & mask_) {
+            // an entry may fill the hole when the hole lies between its home and its slot
+            if (((j - home(t_[j].first)) & mask_) >= ((j - i) & mask_)) {
+                t_[i] = t_[j];
+                i = j;
+            }
+        }
+        t_[i].first = 0;
+        n_--;
+    }
+    size_t size() const { return n_ + (has0_ ? 1 : 0); }
+    bool empty() const { return size() == 0; }
+    void clear()
+    {
+        std::fill(t_.begin(), t_.end(), Entry{0, V{}});
+        n_ = 0;
+        has0_ = false;
+    }
+    template <class F>
+    void for_each(F f) const
+    {
+        if (has0_) f(zero_);
+        for (const Entry &e : t_)
+            if (e.first != 0) f(e);
+    }
+
+private:
+    size_t cap() const { return t_.size(); }
+    size_t home(uint64_t k) const { return (size_t)((k * 0x9E3779B97F4A7C15ull) >> shift_); }
+    void grow()
+    {
+        std::vector<Entry> old;
+        old.swap(t_);
+        const size_t c = old.empty() ? 64 : 2 * old.size();
+        t_.assign(c, Entry{0, V{}});
+        mask_ = c - 1;
+        shift_ = 64u - (unsigned)__builtin_ctzll(c);
+        n_ = 0;
+        for (const Entry &e : old)
+            if (e.first != 0) emplace(e.first, e.second);
+    }
+    std::vector<Entry> t_;
+    size_t mask_ = 0, n_ = 0;
+    unsigned shift_ = 64;
+    bool has0_ = false;
+    Entry zero_{0, V{}};
 };
 
 inline uint64_t fingerprint(const uint8_t *p)
@@ -127,37 +239,25 @@ int settle(C *c, const Touch &t, Change &ch)
     // the touched hashes and window entries (few: sorted, deduplicated), then the owners of the
     // touched ranges (each hash owns one place: no duplicates among them; the COSS replay settles
     // ~a million per batch, whose sort dominated)
+    for (const IdMove &m : t.moves) c->move_id(m);
     std::vector<uint64_t> cand(t.hs);
     for (int s : t.slots) c->st.window_in_slot(s, cand);
     std::sort(cand.begin(), cand.end());
     cand.erase(std::unique(cand.begin(), cand.end()), cand.end());
-    if (!t.ranges.empty()) {
-        std::vector<uint64_t> rs(t.ranges);
-        std::sort(rs.begin(), rs.end());
-        rs.erase(std::unique(rs.begin(), rs.end()), rs.end());
-        const size_t n0 = cand.size();
-        std::vector<uint64_t> own;
-        for (uint64_t r : rs) c->st.owners(r, own);
-        for (uint64_t h : own)
-            if (!std::binary_search(cand.begin(), cand.begin() + (ptrdiff_t)n0, h)) cand.push_back(h);
-    }
     g_settle.calls++;
     g_settle.cand += cand.size();
     g_settle.ranges += t.ranges.size();
     uint8_t buf[SEG];
-    for (uint64_t h : cand) {
-        if (!h) continue;
-        const uint8_t *p = nullptr;
-        Loc l{0, 0};
-        uint64_t id[2] = {0, 0};  // where the bytes are, and their version there (0: unknown)
-        const int r = c->st.peek(h, &p, &l, id);
+    int rc = XC_OK;
+    // one candidate h, peeked: r, p, l, id (where the bytes are, and their version there; 0: unknown)
+    auto one = [&](uint64_t h, int r, const uint8_t *p, const Loc &l, const uint64_t *id) -> int {
         if (r == LOAD_MISS) ch.new_lm |= c->load_miss.insert(h).second;
-        else c->load_miss.erase(h);
+        else if (!c->load_miss.empty()) c->load_miss.erase(h);
         // the same bytes as when the mirror last took this hash's (no read, no fingerprint): the
         // common case after a stripe load, whose 1024 hashes are all looked at
         if ((r == FOUND || r == IN_FILE) && id[0] && c->same_bytes(h, id)) {
             g_settle.same++;
-            continue;
+            return XC_OK;
         }
         if (r == IN_FILE) {
             g_settle.reads++;
@@ -171,17 +271,39 @@ int settle(C *c, const Touch &t, Change &ch)
         if (r != FOUND && r != IN_FILE) {
             c->note_bytes(h, nullptr);
             if (c->known.erase(h)) ch.removed.push_back(h);
-            continue;
+            return XC_OK;
         }
         const uint64_t fp = fingerprint(p);
         c->note_bytes(h, id);
         auto it = c->known.find(h);
-        if (it != c->known.end() && it->second == fp) continue;
+        if (it != c->known.end() && it->second == fp) return XC_OK;
         c->known[h] = fp;
         ch.added.push_back(h);
         ch.bytes.insert(ch.bytes.end(), p, p + SEG);
+        return XC_OK;
+    };
+    for (uint64_t h : cand) {
+        if (!h) continue;
+        const uint8_t *p = nullptr;
+        Loc l{0, 0};
+        uint64_t id[2] = {0, 0};
+        const int r = c->st.peek(h, &p, &l, id);
+        if ((rc = one(h, r, p, l, id))) return rc;
     }
-    return XC_OK;
+    if (!t.ranges.empty()) {
+        // then the owners of the touched ranges not among them, range by range (each hash owns one
+        // place: no duplicates among them)
+        std::vector<uint64_t> rs(t.ranges);
+        std::sort(rs.begin(), rs.end());
+        rs.erase(std::unique(rs.begin(), rs.end()), rs.end());
+        for (uint64_t rg : rs)
+            c->st.peek_owners(rg, [&](uint64_t h, int r, const uint8_t *p, const Loc &l, const uint64_t *id) {
+                if (rc || std::binary_search(cand.begin(), cand.end(), h)) return;
+                g_settle.cand++;
+                rc = one(h, r, p, l, id);
+            });
+    }
+    return rc;
 }
 
 // The device mirror follows a change.
