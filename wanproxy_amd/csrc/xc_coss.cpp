@@ -137,6 +137,7 @@ public:
         a.h.hash[i] = h;
         std::memcpy(a.seg[i], seg, SEG);
         wstamp_[active_][i] = ++stamp_;
+        written_[active_] = true;
         const uint64_t range = a.h.m.stripe_range;
         a.h.m.segment_index++;
         while (a.h.m.segment_index < STRIPE_SEGS && a.h.hash[a.h.m.segment_index]) a.h.m.segment_index++;
@@ -164,8 +165,25 @@ public:
         int s = first_slot(e.range);
         if (s >= LOADED) {
             s = best_unloadable_slot();
-            detach_stripe(s, t);
-            load_stripe(e.range, s, t, false);  // (its header: the data stays in the file until needed)
+            // A slot read from the file and not written since names the file's bytes at every
+            // position (peek's file ids), as the file does once it is detached, and a stripe read
+            // from the file into it names the same ids it had in the file: when the two stripes'
+            // headers agree with the file and no other slot holds either, no owner of them finds
+            // other bytes or a miss of another kind, and their ~1000 owners need no settle (the
+            // slot's window entries and the window's forgotten hashes still do).
+            const uint64_t old = slot_[s].h.m.stripe_range;
+            const bool quiet = t && slot_[s].h.m.signature != 0 && slot_[s].h.m.state == 1 && from_file_[s] &&
+                               !written_[s] && old < limit_ && e.range < limit_ && only_holder(s, old) &&
+                               std::memcmp(slot_[s].h.hash, &file_hash_[old * STRIPE_SEGS], sizeof(Header::hash)) == 0 &&
+                               owners_agree(old) && owners_agree(e.range);
+            Touch q;
+            detach_stripe(s, quiet ? &q : t);
+            const bool loaded = load_stripe(e.range, s, quiet ? &q : t, false);  // (its header: the data stays in the file)
+            if (quiet) {
+                t->hs.insert(t->hs.end(), q.hs.begin(), q.hs.end());
+                t->slots.insert(t->slots.end(), q.slots.begin(), q.slots.end());
+                if (!loaded || !from_file_[s]) t->ranges.insert(t->ranges.end(), q.ranges.begin(), q.ranges.end());
+            }
         }
         Stripe &st = slot_[s];
         if (st.h.hash[e.pos] != h) return nullptr;
@@ -355,6 +373,24 @@ public:
     }
 
 private:
+    // no slot but s holds stripe `range`
+    bool only_holder(int s, uint64_t range) const
+    {
+        for (int i = 0; i < LOADED; i++)
+            if (i != s && slot_[i].h.m.stripe_range == range) return false;
+        return true;
+    }
+
+    // every owner of stripe `range` is the hash the file's header has at its position (a lookup
+    // through the file finds it, no load miss)
+    bool owners_agree(uint64_t range) const
+    {
+        const uint64_t *o = &owner_[range * STRIPE_SEGS], *f = &file_hash_[range * STRIPE_SEGS];
+        for (uint32_t i = 0; i < STRIPE_SEGS; i++)
+            if (o[i] && o[i] != f[i]) return false;
+        return true;
+    }
+
     // lookup takes the first slot whose stripe_range matches (:200-207): an unused slot (zeroed
     // header, stripe_range 0) or a second copy of a stripe can shadow the one that holds it
     int first_slot(uint64_t range) const
@@ -432,6 +468,7 @@ private:
         retarget(s, range, t);
         load_stamp_[s] = ++stamp_;
         from_file_[s] = false;
+        written_[s] = false;
         std::memset(&slot_[s].h, 0, sizeof(Header));
         Meta &m = slot_[s].h.m;
         m.signature = SIGNATURE;
@@ -453,6 +490,7 @@ private:
             const size_t n = full ? sizeof(Stripe) : sizeof(Header);
             load_stamp_[s] = ++stamp_;  // (the slot's bytes are another stripe's now)
             from_file_[s] = false;
+            written_[s] = false;
             if (::pread(fd_, &slot_[s], n, (off_t)pos) == (ssize_t)n) {
                 resident_[s] = full;
                 from_file_[s] = range < limit_;
@@ -571,6 +609,7 @@ private:
     void purge_stripe(int s, Touch *t)
     {  // :347-377
         Stripe &st = slot_[s];
+        written_[s] = true;  // (its header is not the file's any more)
         if (t) t->ranges.push_back(st.h.m.stripe_range);
         for (int i = (int)STRIPE_SEGS - 1; i >= 0; --i) {
             const uint64_t h = st.h.hash[i];
@@ -598,6 +637,8 @@ private:
     uint64_t stamp_ = 0, load_stamp_[LOADED] = {}, wstamp_[LOADED][STRIPE_SEGS] = {};
     // a slot loaded from the file (its unwritten positions: the file's bytes at load_fstamp_)
     bool from_file_[LOADED] = {};
+    // a slot written (enter) or purged since it took its stripe
+    bool written_[LOADED] = {};
     uint64_t load_fstamp_[LOADED] = {};
     std::vector<uint64_t> fstamp_;
     int active_ = 0;
@@ -636,7 +677,7 @@ struct xc_coss {
     std::unordered_set<uint64_t> load_miss;
 
     // per replay pass: hashes the device held before the pass's batch, and those entered in it
-    std::unordered_set<uint64_t> pre, inpass;
+    replay::FlatMap<char> pre, inpass;  // (sets)
     int err = XC_OK;
 
     // the device entered a declared segment: its bytes, unless the hash was there already (the
@@ -647,7 +688,7 @@ struct xc_coss {
     {
         if (pre.count(h)) return;
         seen.erase(h);
-        if (inpass.insert(h).second) {
+        if (inpass.emplace(h, 1).second) {
             known[h] = replay::fingerprint(seg);
             // where the store's lookup finds these bytes now (the settle after the enter then reads
             // and fingerprints nothing)
@@ -707,7 +748,7 @@ struct xc_coss {
         std::vector<uint64_t> v(q.size());
         int rc = xc__cache_find(cache, q.data(), q.size(), v.data());
         for (size_t i = 0; i < q.size() && !rc; i++)
-            if (v[i] != ~0ull && v[i] < count0) pre.insert(q[i]);
+            if (v[i] != ~0ull && v[i] < count0) pre.emplace(q[i], 1);
         return rc;
     }
     int end_pass() { return err; }

@@ -75,6 +75,13 @@ struct Touch {
     std::vector<uint64_t> hs, ranges;
     std::vector<int> slots;
     std::vector<IdMove> moves;
+    void clear()
+    {
+        hs.clear();
+        ranges.clear();
+        slots.clear();
+        moves.clear();
+    }
 };
 
 // Store::peek results: FOUND (*p: the bytes), IN_FILE (the stripe is loaded from the file first,
@@ -89,6 +96,13 @@ struct Change {
     std::vector<uint8_t> bytes;     // their bytes, SEG each
     bool new_lm = false;            // a hash became a LOAD_MISS one (a later miss of it has side effects)
     bool any() const { return !removed.empty() || !added.empty(); }
+    void clear()
+    {
+        removed.clear();
+        added.clear();
+        bytes.clear();
+        new_lm = false;
+    }
 };
 
 // A hash map keyed by 64-bit hashes: open addressing, linear probing, backward-shift deletion, at
@@ -158,6 +172,10 @@ public:
         n_--;
     }
     size_t size() const { return n_ + (has0_ ? 1 : 0); }
+    void reserve(size_t n)
+    {
+        while (2 * n > cap()) grow();
+    }
     bool empty() const { return size() == 0; }
     void clear()
     {
@@ -195,16 +213,25 @@ private:
     Entry zero_{0, V{}};
 };
 
+// (four independent chains over interleaved words, then combined: the chain's multiply latency,
+// not its throughput, bounded one chain; the replay fingerprints every entered segment)
 inline uint64_t fingerprint(const uint8_t *p)
 {
-    uint64_t h = 0x9E3779B97F4A7C15ull;
-    for (uint32_t i = 0; i < SEG; i += 8) {
-        uint64_t w;
-        std::memcpy(&w, p + i, 8);
-        h = (h ^ w) * 0x100000001B3ull;
-        h ^= h >> 29;
+    uint64_t h[4] = {0x9E3779B97F4A7C15ull, 0xC2B2AE3D27D4EB4Full, 0x165667B19E3779F9ull, 0x27D4EB2F165667C5ull};
+    for (uint32_t i = 0; i < SEG; i += 32) {
+        uint64_t w[4];
+        std::memcpy(w, p + i, 32);
+        for (int k = 0; k < 4; k++) {
+            h[k] = (h[k] ^ w[k]) * 0x100000001B3ull;
+            h[k] ^= h[k] >> 29;
+        }
     }
-    return h;
+    uint64_t r = h[0];
+    for (int k = 1; k < 4; k++) {
+        r = (r ^ h[k]) * 0x100000001B3ull;
+        r ^= r >> 29;
+    }
+    return r;
 }
 
 // The hashes an operation touched, looked up again without side effects: those the device holds
@@ -240,7 +267,8 @@ int settle(C *c, const Touch &t, Change &ch)
     // touched ranges (each hash owns one place: no duplicates among them; the COSS replay settles
     // ~a million per batch, whose sort dominated)
     for (const IdMove &m : t.moves) c->move_id(m);
-    std::vector<uint64_t> cand(t.hs);
+    static thread_local std::vector<uint64_t> cand;  // (one settle at a time per thread: no allocation)
+    cand.assign(t.hs.begin(), t.hs.end());
     for (int s : t.slots) c->st.window_in_slot(s, cand);
     std::sort(cand.begin(), cand.end());
     cand.erase(std::unique(cand.begin(), cand.end()), cand.end());
@@ -661,7 +689,7 @@ int encode(C *c, std::vector<CItem> items, uint8_t *out, const uint64_t *out_off
         // event (in order) of hash h, so that a change is checked against the later events in the
         // time of its own hashes (a scan of them all after every change was quadratic: COSS)
         if ((rc = c->unmirrorable())) return rc;
-        std::unordered_map<uint64_t, uint64_t> last;
+        FlatMap<uint64_t> last;
         {
             uint64_t n = 0;
             for (const auto &v : ev) n += v.size();
@@ -675,11 +703,13 @@ int encode(C *c, std::vector<CItem> items, uint8_t *out, const uint64_t *out_off
         bool redo = false;
         std::vector<CItem> next;
         std::vector<Change> held;  // changes nothing later in the pass saw: mirrored at its end
+        Touch t;                   // (reused: no allocation per event)
+        Change ch;
         for (uint64_t k = 0; k < m && !redo; k++) {
             const CItem &it = items[k];
             for (size_t e = 0; e < ev[k].size(); e++) {
                 const EncEvent &E = ev[k][e];
-                Touch t;
+                t.clear();
                 if (E.kind == 0) {
                     c->st.enter(E.hash, E.seg, &t);
                     c->entered(E.hash, E.seg);
@@ -690,8 +720,8 @@ int encode(C *c, std::vector<CItem> items, uint8_t *out, const uint64_t *out_off
                 } else if (!c->st.lookup(E.hash, &t)) {
                     return xc__set_error(XC_EDEVICE, "cache replay: a device hit the store does not find");
                 }
-                Change ch;
-                const auto ts = clk::now();
+                ch.clear();
+                const auto ts = prof ? clk::now() : clk::time_point{};
                 if ((rc = settle(c, t, ch))) return rc;
                 if (prof) t_set += std::chrono::duration<double>(clk::now() - ts).count();
                 if (!ch.any() && !ch.new_lm) continue;
