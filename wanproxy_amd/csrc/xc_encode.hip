@@ -215,12 +215,7 @@ __global__ __launch_bounds__(64 * SCAN_WAVES) void k_scan(ScanArgs a)
     uint2 *queue = queues[wave];
     const uint32_t l = lane_id();
 
-    // the level-1 image (the first round's is cache | predicted declarations, folded for small
-    // key counts: a multiple of 4 words)
     const uint32_t fw = a.filt_words;
-    for (uint32_t i = threadIdx.x * 4u; i < fw; i += 256u * SCAN_WAVES)
-        *(uint4 *)(filt + i) = *(const uint4 *)(a.filt + i);
-    __syncthreads();
 
     // Work distribution: waves take runs of a.unit consecutive chunks from a counter (chunks
     // of one buffer continue the block stream and its prefetch without a restart), the next run
@@ -239,16 +234,27 @@ __global__ __launch_bounds__(64 * SCAN_WAVES) void k_scan(ScanArgs a)
         return a.ck_lo + nwaves * a.unit + uniform(t);
     };
     uint32_t c = a.ck_lo + (blockIdx.x * SCAN_WAVES + wave) * a.unit;
-    if (c >= a.ck_hi) return;
-    uint32_t c_end = min(c + a.unit, a.ck_hi);
-    uint32_t c_nxt = claim();
-
-    // chunk descriptors: {c0, c1, arena offset lo, hi}; the next one is always in flight
-    uint4 dsc = a.P.chunk_desc[c];
-    uint32_t gblk = a.shadow ? uniform(a.P.chunk_blk[c]) : 0u;
+    const bool idle = c >= a.ck_hi;  // (a wave without chunks still loads its share of the image)
+    uint32_t c_end = 0, c_nxt = 0, gblk = 0;
+    uint4 dsc = make_uint4(0, 0, 0, 0), dn = dsc;
     uint32_t pw[8], w[8], wn[8];
-    first_blocks(desc_base(a, dsc), uniform(dsc.x), l, pw, w, wn);
-    uint4 dn = a.P.chunk_desc[c + 1u < c_end ? c + 1u : min(c_nxt, a.ck_hi - 1u)];
+    if (!idle) {
+        // the first chunk's descriptor and blocks before the level-1 image: their memory latency
+        // overlaps the image's copy (a small batch's waves scan 2 blocks each: the prologue counts)
+        c_end = min(c + a.unit, a.ck_hi);
+        c_nxt = claim();
+        // chunk descriptors: {c0, c1, arena offset lo, hi}; the next one is always in flight
+        dsc = a.P.chunk_desc[c];
+        gblk = a.shadow ? uniform(a.P.chunk_blk[c]) : 0u;
+        first_blocks(desc_base(a, dsc), uniform(dsc.x), l, pw, w, wn);
+        dn = a.P.chunk_desc[c + 1u < c_end ? c + 1u : min(c_nxt, a.ck_hi - 1u)];
+    }
+    // the level-1 image (the first round's is cache | predicted declarations, folded for small
+    // key counts: a multiple of 4 words)
+    for (uint32_t i = threadIdx.x * 4u; i < fw; i += 256u * SCAN_WAVES)
+        *(uint4 *)(filt + i) = *(const uint4 *)(a.filt + i);
+    __syncthreads();
+    if (idle) return;
 
     Pending pd;
     pd.n = 0;
