@@ -1755,6 +1755,13 @@ __global__ __launch_bounds__(256) void k_blockpredict(DeclArgs a)
     const uint32_t g = P.blk_base[a.j0] + blockIdx.x * 256u + threadIdx.x;
     if (g >= P.blk_base[a.j1]) return;
     const uint32_t b = P.blk_buf[g], k = g - P.blk_base[b];
+    // a block the hashing found cached (an entry complete then, under the removal floor: still
+    // there, at the same segment index) is a predicted REF without another probe of the cache
+    const uint32_t cmp = P.blk_cmp[g] & ~BC_DIFF;
+    if (cmp && !stream_carried(P, b)) {
+        P.blk_pref[g] = cmp;
+        return;
+    }
     block_predict(P, g, b, k, P.blk_h[g], P.anc_scan ? P.blk_anc[g] : ANC_NONE);
 }
 

@@ -224,10 +224,11 @@ extern "C" int xc_ctx_create(int dev, xc_ctx **out)
     c->dev = dev;
     {
         // XC_STREAM_PRIO=1 (experiments): the context stream at the highest priority, so that its
-        // latency-bound kernels are dispatched ahead of the side stream's block hashing
+        // latency-bound kernels are dispatched ahead of the side stream's block hashing (the side
+        // stream's own priority: xc_plan creation below)
         const char *e = getenv("XC_STREAM_PRIO");
         int lo = 0, hi = 0;
-        if (e && atoi(e) && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
+        if (e && atoi(e) == 1 && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
             HIPCHK(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi));
         else
             HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
@@ -1675,10 +1676,15 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     // declaration insert lands there directly, and the declaration-layer scans test a superset
     P.dset.l2 = p->d_l2mix;
     if (!c->ctx->side) {
+        // the side stream (block hashing) at the highest priority: a cfg5 step is a loop through
+        // the side stream's hashing, which the main stream waits for (cfg5 A/B
+        // 869-870 -> 874-875 GiB/s, profiles/r05/ab/side_priority_r5s.txt).  XC_STREAM_PRIO=0: both
+        // streams at the default priority; =1: the context stream high, the side stream low
         const char *e = getenv("XC_STREAM_PRIO");
+        const int mode = e ? atoi(e) : 2;
         int lo = 0, hi = 0;
-        if (e && atoi(e) && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
-            HIPCHK(hipStreamCreateWithPriority(&c->ctx->side, hipStreamNonBlocking, lo));
+        if (mode && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
+            HIPCHK(hipStreamCreateWithPriority(&c->ctx->side, hipStreamNonBlocking, mode == 1 ? lo : hi));
         else
             HIPCHK(hipStreamCreateWithFlags(&c->ctx->side, hipStreamNonBlocking));
     }
