@@ -1676,12 +1676,12 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
     // declaration insert lands there directly, and the declaration-layer scans test a superset
     P.dset.l2 = p->d_l2mix;
     if (!c->ctx->side) {
-        // the side stream (block hashing) at the highest priority: a cfg5 step is a loop through
-        // the side stream's hashing, which the main stream waits for (cfg5 A/B
-        // 869-870 -> 874-875 GiB/s, profiles/r05/ab/side_priority_r5s.txt).  XC_STREAM_PRIO=0: both
-        // streams at the default priority; =1: the context stream high, the side stream low
+        // XC_STREAM_PRIO (experiments): 1 = the context stream high, the side stream low; 2 = the
+        // side stream (block hashing) high: cfg5 A/B 869-870 -> 874-875 GiB/s, but a stream of
+        // another priority on the device slows the decoder's streams (cfg4 1370 -> 826 GiB/s with
+        // an idle high-priority side stream, profiles/r05/ab/side_priority_r5s.txt): not the default
         const char *e = getenv("XC_STREAM_PRIO");
-        const int mode = e ? atoi(e) : 2;
+        const int mode = e ? atoi(e) : 0;
         int lo = 0, hi = 0;
         if (mode && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
             HIPCHK(hipStreamCreateWithPriority(&c->ctx->side, hipStreamNonBlocking, mode == 1 ? lo : hi));
