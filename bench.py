@@ -40,6 +40,7 @@ PROFILE_DIR = os.path.join(ROOT, "profiles", "r05")
 # 20 steps (a few ms) measured the first steps' launch ramp too (cfg4: 1319-1333 GiB/s over 20 steps,
 # 1367-1379 over 200, profiles/r05/ab/leg_steps_r5d.txt)
 LEG_STEPS = 200
+HOST_SUB_MB = 256  # sub-batch bound of the end-to-end (host memory) leg's plan
 
 
 def parse():
@@ -577,17 +578,21 @@ def main():
         # end-to-end from host memory (xc_encode_run_host): the input arena in pinned host
         # memory, each sub-batch copied in on a copy stream while earlier ones encode, and every
         # sub-batch's encoded streams packed into pinned host memory by a kernel as it is emitted
-        h_in = w.HostBuffer(ctx, plan.in_bytes)
+        # (a plan of 256 MiB sub-batches: its copies and packing overlap more of the encode than 1 GiB
+        # ones, xc_encode_plan_create_sub: 38 -> 43 GiB/s, profiles/r05/ab/e2e_sub_batches_r5x.txt)
+        hplan = w.EncodePlan(cache, lens, sub_bytes=HOST_SUB_MB << 20)
+        assert hplan.in_bytes == plan.in_bytes and np.array_equal(hplan.in_off, plan.in_off)
+        h_in = w.HostBuffer(ctx, hplan.in_bytes)
         h_in.array[:] = d_in.cpu().numpy()
-        h_out = w.HostBuffer(ctx, plan.out_bytes)
+        h_out = w.HostBuffer(ctx, hplan.out_bytes)
         cache.restore_async()
-        plan.run_host(h_in, h_out)  # warm-up (device arenas of the host path)
+        hplan.run_host(h_in, h_out)  # warm-up (device arenas of the host path)
         reps = 3
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(reps):
             cache.restore_async()
-            hlens, pos = plan.run_host(h_in, h_out)
+            hlens, pos = hplan.run_host(h_in, h_out)
         e2e = (time.perf_counter() - t0) / reps
         if not np.array_equal(hlens.astype(np.uint64), got_len):
             raise SystemExit("bench: host path output lengths differ from the device-resident run")
@@ -596,7 +601,8 @@ def main():
                 raise SystemExit("bench: host path output differs from the oracle")
         result["e2e_host_gibs"] = round(in_bytes_rank / e2e / 2**30, 3)
         result["e2e_ms"] = round(e2e * 1e3, 2)
-        result["e2e_note"] = ("xc_encode_run_host: pinned host input arena -> per-sub-batch H2D "
+        hplan.close()
+        result["e2e_note"] = (f"xc_encode_run_host ({HOST_SUB_MB} MiB sub-batches): pinned host input arena -> per-sub-batch H2D "
                               "overlapping the encode -> streams packed into pinned host memory "
                               f"({int(hlens.sum()) >> 20} MiB) by a kernel after each sub-batch; every buffer "
                               "checked against the oracle digests")

@@ -104,6 +104,12 @@ int xc_window_hashes(xc_ctx *ctx, const uint8_t *d_in, uint64_t n, uint64_t *d_o
  * buffer i's encoded stream at out_off[i] with capacity 2*len+16
  * (the reference's worst case is 2*len: every byte an escaped 0xF1). */
 int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint64_t nbuf, xc_plan **out);
+/* The same with a bound on each sub-batch's input bytes (0: the default, half the batch between
+ * 512 MiB and 1 GiB; at least 1 MiB).  A plan run from host memory (xc_encode_run_host) copies
+ * and packs per sub-batch, so smaller sub-batches overlap more of its PCIe transfers: 256 MiB
+ * (cfg5 end to end 38 -> 43 GiB/s); device-resident runs are fastest with the default. */
+int xc_encode_plan_create_sub(xc_cache *c, const uint64_t *lengths, uint64_t nbuf, uint64_t sub_bytes,
+                              xc_plan **out);
 int xc_plan_destroy(xc_plan *p);
 /* Arena sizes and per-buffer offsets (host arrays of nbuf, may be NULL). */
 int xc_plan_layout(xc_plan *p, uint64_t *in_off, uint64_t *out_off, uint64_t *in_bytes,

@@ -1223,6 +1223,7 @@ extern "C" int xc_window_hashes(xc_ctx *ctx, const uint8_t *d_in, uint64_t n, ui
 // ------------------------------------------------------------------ plan ----------
 static const uint32_t CHUNK_LEN = 16384;  // the longest scan chunk (plans of small batches use shorter ones)
 static_assert(CHUNK_LEN == CHUNK_BLOCKS * XC_SEG, "k_scan loads a chunk's shadow flags in one wave load");
+static const uint64_t HOST_SUB_BYTES = 256ull << 20;      // ... of plans run from host memory (copies pipelined)
 static const uint64_t SUB_BYTES_DEFAULT = 512ull << 20;  // sub-batch: bound on input bytes (tuned on cfg5)
 static const uint32_t SUB_BUFS = 32768;                  // sub-batch: bound on buffers
 
@@ -1233,11 +1234,12 @@ static const uint64_t SUB_BYTES_MAX = 1024ull << 20;    // ... grown up to this 
 // of the main stream pays its ramp-down (cfg5, 2 GiB: A/B 512 MiB 845-847 / 768 MiB 848-853 /
 // 1 GiB 856-858 GiB/s, profiles/r05/ab/sub_batch_size_r5j.txt).  XC_SUB_MB overrides it (tests,
 // tuning experiments).
-static uint64_t sub_bytes(uint64_t total)
+static uint64_t sub_bytes(uint64_t total, uint64_t bound)
 {
     const char *e = getenv("XC_SUB_MB");
     const long v = e ? atol(e) : 0;
     if (v > 0) return (uint64_t)v << 20;
+    if (bound) return bound;
     const uint64_t half = ((total / 2 + (1u << 20) - 1) >> 20) << 20;
     return std::min(SUB_BYTES_MAX, std::max(SUB_BYTES_DEFAULT, half));
 }
@@ -1445,8 +1447,15 @@ static void ev_collect(xc_plan *p)
 
 extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint64_t nbuf, xc_plan **out)
 {
+    return xc_encode_plan_create_sub(c, lengths, nbuf, 0, out);
+}
+
+extern "C" int xc_encode_plan_create_sub(xc_cache *c, const uint64_t *lengths, uint64_t nbuf, uint64_t sub_bytes_max,
+                                         xc_plan **out)
+{
     if (!c || !out || (!lengths && nbuf)) return fail(XC_EINVAL, "null");
     if (nbuf > (1u << 24)) return fail(XC_EINVAL, "too many buffers");
+    if (sub_bytes_max && sub_bytes_max < MAX_BUF) return fail(XC_EINVAL, "sub-batch bound below 1 MiB");
     int rc = set_dev(c->ctx);
     if (rc) return rc;
     xc_plan *p = new xc_plan();
@@ -1464,7 +1473,7 @@ extern "C" int xc_encode_plan_create(xc_cache *c, const uint64_t *lengths, uint6
         uint64_t decl = 0, maxdecl = 0;
         uint64_t total = 0;
         for (uint32_t i = 0; i < nbuf; i++) total += lengths[i];
-        const uint64_t sub_max = sub_bytes(total);
+        const uint64_t sub_max = sub_bytes(total, sub_bytes_max);
         // XC_FIRST_SUB_MB (experiments): the first sub-batch's bound (its block hashing has
         // nothing to overlap with)
         const char *fe = getenv("XC_FIRST_SUB_MB");
@@ -3245,7 +3254,8 @@ static int plan_acquire(xc_cache *c, const uint64_t *len, uint64_t nbuf, xc_plan
             return XC_OK;
         }
     }
-    return xc_encode_plan_create(c, len, nbuf, out);
+    // (host-path plans: sub-batches of 256 MiB pipeline the copies, xc_encode_plan_create_sub)
+    return xc_encode_plan_create_sub(c, len, nbuf, HOST_SUB_BYTES, out);
 }
 static void plan_release(xc_cache *c, xc_plan *p)
 {

@@ -28,7 +28,7 @@ SYMBOLS = [
     "xc_device_count", "xc_device_place", "xc_ctx_device", "xc_ctx_create", "xc_ctx_destroy", "xc_ctx_stream", "xc_ctx_sync",
     "xc_cache_create", "xc_cache_destroy", "xc_cache_count", "xc_cache_snapshot", "xc_cache_filter_stats",
     "xc_cache_restore", "xc_cache_lookup", "xc_cache_enter", "xc_hash_segments",
-    "xc_window_hashes", "xc_encode_plan_create", "xc_plan_destroy", "xc_plan_layout",
+    "xc_window_hashes", "xc_encode_plan_create", "xc_encode_plan_create_sub", "xc_plan_destroy", "xc_plan_layout",
     "xc_encode_run", "xc_encode_batch_host", "xc_plan_stats", "xc_decode_batch_host",
     "xc_selftest", "xc_last_error", "xc_cache_restore_async", "xc_plan_set_timing",
     "xc_plan_kernel_times", "xc_host_alloc", "xc_host_free", "xc_encode_run_host",
@@ -115,6 +115,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.xc_hash_segments_host.argtypes = [_vp, _u8p, C.c_uint64, _u64p]
     lib.xc_window_hashes.argtypes = [_vp, _vp, C.c_uint64, _vp, _vp]
     lib.xc_encode_plan_create.argtypes = [_vp, _u64p, C.c_uint64, C.POINTER(_vp)]
+    lib.xc_encode_plan_create_sub.argtypes = [_vp, _u64p, C.c_uint64, C.c_uint64, C.POINTER(_vp)]
     lib.xc_plan_destroy.argtypes = [_vp]
     lib.xc_plan_layout.argtypes = [_vp, _u64p, _u64p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     lib.xc_encode_run.argtypes = [_vp, _vp, _vp, _vp]
@@ -588,13 +589,15 @@ class EncodePlan:
 
     ``run(d_in, d_out, d_len)`` takes raw device pointers (e.g. ``tensor.data_ptr()``)."""
 
-    def __init__(self, cache: XCodecCache, lengths):
+    def __init__(self, cache: XCodecCache, lengths, sub_bytes: int = 0):
+        """``sub_bytes``: the sub-batch bound on input bytes (0: the library's default;
+        xc_encode_plan_create_sub).  A plan for ``run_host`` pipelines its copies per sub-batch."""
         self.cache = cache
         lens = np.ascontiguousarray(lengths, dtype=np.uint64)
         self.nbuf = len(lens)
         self.lengths = lens
         self.h = _vp()
-        _check(load_library().xc_encode_plan_create(cache.h, lens, self.nbuf, C.byref(self.h)))
+        _check(load_library().xc_encode_plan_create_sub(cache.h, lens, self.nbuf, int(sub_bytes), C.byref(self.h)))
         self.in_off = np.zeros(self.nbuf, np.uint64)
         self.out_off = np.zeros(self.nbuf, np.uint64)
         ib, ob = C.c_uint64(), C.c_uint64()
