@@ -25,7 +25,9 @@ try:
 except OSError:
     pass
 PY
-PMC_BENCH="bench.py --steps 1 --warmup 0 --no-cpu --no-e2e --no-decode --no-legs --no-live"
+# (--tail-steps 4: the passes average the last 3 steps, production steps after the diagnostic ones:
+# early side-stream hashing, records of shadowed blocks dropped, as in the timed steps)
+PMC_BENCH="bench.py --steps 1 --warmup 0 --no-cpu --no-e2e --no-decode --no-legs --no-live --tail-steps 4"
 die() { echo "$1 failed (rc $2)"; tail -40 "$3"; exit 1; }
 for step in "$@"; do
     name=${step%%:*}

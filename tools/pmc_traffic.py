@@ -1,8 +1,10 @@
 """HBM traffic of one cfg5 encode step, every kernel, from rocprofv3 PMC passes (tools/gpu.sh pmc).
 
 A step is a cache restore (k_undo_known, or k_undo_dev) followed by the encode's kernels; the PMC runs are
-`bench.py --steps 1 --warmup 0 --no-cpu --no-e2e --no-decode --no-legs`, whose last 3 steps are the
-diagnostic steps after the timed one.  Each of those steps spans the dispatches from its
+`bench.py --steps 1 --warmup 0 --no-cpu --no-e2e --no-decode --no-legs --tail-steps 4`, whose last 3
+steps are production steps (after the diagnostic ones: the next run's blocks hashed ahead on the side
+stream, the records of shadowed blocks dropped, as in the timed steps; round 4's records measured the
+diagnostic steps, whose first sub-batch is hashed in line without those drops).  Each of those steps spans the dispatches from its
 restore kernel to the next one (the last to the end); only the library's kernels (xc::) count.
 
 FETCH_SIZE and WRITE_SIZE are in KiB.  Per MI355X_MICROARCH.md (HBM section), on gfx950
