@@ -1228,20 +1228,26 @@ static const uint64_t SUB_BYTES_DEFAULT = 512ull << 20;  // sub-batch: bound on 
 static const uint32_t SUB_BUFS = 32768;                  // sub-batch: bound on buffers
 
 static const uint64_t SUB_BYTES_MAX = 1024ull << 20;    // ... grown up to this while the run keeps two
-// The sub-batch byte bound of a run of `total` input bytes: half the run, between 512 MiB and 1 GiB,
+// The sub-batch byte bound of a run of `total` input bytes: half the run, between 256 MiB and 1 GiB,
 // so that a large run has two sub-batches or more (its later sub-batches hashed on the side stream
 // beside the earlier ones) and as few as that allows: per sub-batch, each of the ~9 dependent kernels
 // of the main stream pays its ramp-down (cfg5, 2 GiB: A/B 512 MiB 845-847 / 768 MiB 848-853 /
 // 1 GiB 856-858 GiB/s, profiles/r05/ab/sub_batch_size_r5j.txt).  XC_SUB_MB overrides it (tests,
 // tuning experiments).
+// Runs of 512 MiB to 1 GiB take two halves too (at least 256 MiB each): the N=4 rank's 512 MiB shard
+// of cfg5 722-732 -> 756 GiB/s with two, its hashing of the second beside the first's main-stream
+// kernels (profiles/r05/ab/rank_sub_batches_r5ab.txt); below 512 MiB one sub-batch (cfg3 and the
+// N=8 rank's 256 MiB: two of 128 MiB 596 against 686, shard8_sub_batches_r5o.txt).
+static const uint64_t SUB_BYTES_MIN = 256ull << 20;
 static uint64_t sub_bytes(uint64_t total, uint64_t bound)
 {
     const char *e = getenv("XC_SUB_MB");
     const long v = e ? atol(e) : 0;
     if (v > 0) return (uint64_t)v << 20;
     if (bound) return bound;
+    if (total < 2 * SUB_BYTES_MIN) return SUB_BYTES_DEFAULT;
     const uint64_t half = ((total / 2 + (1u << 20) - 1) >> 20) << 20;
-    return std::min(SUB_BYTES_MAX, std::max(SUB_BYTES_DEFAULT, half));
+    return std::min(SUB_BYTES_MAX, std::max(SUB_BYTES_MIN, half));
 }
 static const uint32_t MAX_ROUNDS = 64;
 
