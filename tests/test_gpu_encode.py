@@ -311,7 +311,7 @@ def _plan_run(ctx, oracle_mod, bufs, warm):
     return plan.stats()
 
 
-def _host_path(ctx, oracle_mod, bufs, warm, cap=None):
+def _host_path(ctx, oracle_mod, bufs, warm, cap=None, sub_bytes=0):
     import wanproxy_amd as w
     oc = oracle_mod.Cache()
     for batch in warm:
@@ -320,7 +320,7 @@ def _host_path(ctx, oracle_mod, bufs, warm, cap=None):
     cache = w.XCodecCache(ctx, 1 << 15)
     for batch in warm:
         w.XCodecEncoder(cache).encode_batch(batch)
-    plan = w.EncodePlan(cache, [len(b) for b in bufs])
+    plan = w.EncodePlan(cache, [len(b) for b in bufs], sub_bytes=sub_bytes)
     h_in = w.HostBuffer(ctx, plan.in_bytes)
     for i, b in enumerate(bufs):
         h_in.array[int(plan.in_off[i]):int(plan.in_off[i]) + len(b)] = b
@@ -352,6 +352,23 @@ def test_host_path_packed(gpu_ctx, oracle_mod, monkeypatch):
     st = _host_path(gpu_ctx, oracle_mod, bufs, warm)
     assert st.redone >= 1
     _host_path(gpu_ctx, oracle_mod, [W.gen(5, 65536) for _ in range(4)], [])
+
+
+def test_plan_sub_batch_bound(gpu_ctx, oracle_mod):
+    """xc_encode_plan_create_sub: a plan's sub-batch bound (the host path's 256 MiB, here 1 and 3 MiB
+    over a 6 MiB batch: several sub-batches, their copies and packing pipelined) gives the same
+    streams as the oracle; a bound below one buffer's 1 MiB is refused."""
+    import wanproxy_amd as w
+    pool = W.pool(24 * 32)  # (24 x 64 KiB)
+    warm = [[pool[i:i + 65536] for i in range(0, 16 * 65536, 65536)]]
+    bufs = [pool[(k % 24) * 65536:(k % 24) * 65536 + 65536].copy() if k % 3 else W.gen(300 + k, 65536)
+            for k in range(96)]
+    for mb in (1, 3):
+        st = _host_path(gpu_ctx, oracle_mod, bufs, warm, sub_bytes=mb << 20)
+        assert st.sub_batches >= 6 // mb, (mb, st.sub_batches)
+    cache = w.XCodecCache(gpu_ctx, 1 << 12)
+    with pytest.raises(w.XCodecError):
+        w.EncodePlan(cache, [65536] * 4, sub_bytes=(1 << 20) - 1)
 
 
 def test_host_path_capacity(gpu_ctx, oracle_mod):
