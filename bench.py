@@ -368,16 +368,24 @@ def cpu_baseline(args, shard, warm, world) -> dict:
     return res
 
 
-def pmc_traffic(sub_batches: int):
+def pmc_traffic_path(buffers: int) -> str:
+    """The committed PMC record of a cfg5 step over `buffers` buffers per GPU: the whole job at N=1,
+    a rank's shard at N>1 (measured on one GPU with bench.py --total <shard>, tools/gpu.sh pmc)."""
+    return os.path.join(PROFILE_DIR, "pmc_traffic_cfg5.json" if buffers == 32768 else f"pmc_traffic_cfg5_b{buffers}.json")
+
+
+def pmc_traffic(sub_batches: int, buffers: int = 32768):
     """HBM bytes per step of the whole encode pipeline from the committed rocprofv3 PMC passes of
-    this command (tools/pmc_kernels.sh -> tools/pmc_traffic.py -> profiles/r03/), or None when the
+    this command (tools/gpu.sh pmc -> tools/pmc_traffic.py -> profiles/r05/), or None when the
     record was taken with other library sources than these (its src_stamp) or another layout."""
     from wanproxy_amd.provenance import source_stamp
-    tp = os.path.join(PROFILE_DIR, "pmc_traffic_cfg5.json")
+    tp = pmc_traffic_path(buffers)
     if not os.path.exists(tp):
         return None
     rec = json.load(open(tp))
     if rec.get("sub_batches") != sub_batches or rec.get("src_stamp") != source_stamp():
+        return None
+    if rec.get("buffers", 32768) != buffers:
         return None
     return rec
 
@@ -498,15 +506,19 @@ def main():
     # pipeline is the unit: no single kernel carries the step (kernel_ms_per_step).
     peak = HBM_PEAK_GBS * world
     achieved = alg_job / step_s / 1e9
-    tr = pmc_traffic(int(st.sub_batches)) if world == 1 and args.total == 32768 else None
+    # (N>1: every rank's step moves its own shard's bytes on its own GPU; the record is of a rank-sized
+    # shard on one GPU, its bytes times N)
+    tr = pmc_traffic(int(st.sub_batches), n_local) if args.total == 32768 else None
+    tr_job = tr["traffic_bytes_per_step"] * world if tr else None
     anchor = int(st.anchor_scans) > 0
     roofline = {"bound": "hbm", "kernel": "encode step (k_blockhash, k_blockpredict, "
                                           + ("k_aprop, k_aevents" if anchor else "k_scan")
                                           + ", k_resolve, k_walk, k_alloc, k_emit" + (", k_tailcheck)" if anchor else ")"),
                 "achieved": round(achieved, 1), "peak": peak, "unit": "GB/s", "frac": round(achieved / peak, 4),
-                "traffic": tr["traffic_bytes_per_step"] if tr else None,
-                "traffic_over_alg": round(tr["traffic_bytes_per_step"] / alg_rank, 3) if tr else None,
-                "traffic_source": os.path.relpath(os.path.join(PROFILE_DIR, "pmc_traffic_cfg5.json"), ROOT)
+                "traffic": tr_job,
+                "traffic_over_alg": round(tr_job / alg_job, 3) if tr else None,
+                "traffic_source": (os.path.relpath(pmc_traffic_path(n_local), ROOT)
+                                   + ("" if world == 1 else f" (a {n_local}-buffer shard on one GPU, x {world})"))
                 if tr else None,
                 "alg_bytes_per_step": alg_job,
                 "alg_bytes_def": "in + out + 2048 * (n_extract + n_ref) (SURVEY.md §8(d))"}

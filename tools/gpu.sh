@@ -56,13 +56,17 @@ for step in "$@"; do
             -- python3 bench.py $a > "$out/trace.log" 2>&1 || die trace $? "$out/trace.log"
         echo "trace ok" ;;
     pmc)
+        # (pmc:--total,S: a rank-sized shard of S buffers on this GPU -> pmc_traffic_cfg5_bS.json)
+        a=${arg//,/ }
+        sfx=""
+        [ -n "$arg" ] && sfx="_b${arg##*,}"
         for c in FETCH_SIZE WRITE_SIZE; do
-            timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d "$out/pmc/$c" -o run -- python3 $PMC_BENCH \
-                > "$out/pmc_$c.log" 2>&1 || die "pmc $c" $? "$out/pmc_$c.log"
+            timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d "$out/pmc$sfx/$c" -o run -- python3 $PMC_BENCH $a \
+                > "$out/pmc${sfx}_$c.log" 2>&1 || die "pmc $c" $? "$out/pmc${sfx}_$c.log"
         done
-        python tools/pmc_traffic.py "$out/pmc" "$out/pmc_traffic_cfg5.json" auto > "$out/pmc_traffic.log" 2>&1 \
-            || die pmc_traffic $? "$out/pmc_traffic.log"
-        tail -3 "$out/pmc_traffic.log" ;;
+        python tools/pmc_traffic.py "$out/pmc$sfx" "$out/pmc_traffic_cfg5$sfx.json" auto > "$out/pmc_traffic$sfx.log" 2>&1 \
+            || die pmc_traffic $? "$out/pmc_traffic$sfx.log"
+        tail -3 "$out/pmc_traffic$sfx.log" ;;
     pmcinst)
         i=0
         for c in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \

@@ -47,7 +47,9 @@ def steps(disp, n=3):
 
 def main():
     d, out_path = sys.argv[1], sys.argv[2]
-    log = os.path.join(os.path.dirname(os.path.normpath(d)), "pmc_FETCH_SIZE.log")
+    # (the FETCH_SIZE pass's bench output: PMC_DIR/../<basename(PMC_DIR)>_FETCH_SIZE.log)
+    nd = os.path.normpath(d)
+    log = os.path.join(os.path.dirname(nd), os.path.basename(nd) + "_FETCH_SIZE.log")
     line = json.loads([x for x in open(log).read().splitlines() if x.startswith("{")][-1]) \
         if os.path.exists(log) else None
     # (auto: the sub-batches of the bench line the FETCH_SIZE pass printed)
@@ -68,7 +70,8 @@ def main():
         for i in st:
             per_kernel[write[i][0]][1] += write[i][1] / len(ws)
     kib = sum(2 * f + w for f, w in per_kernel.values())
-    rec = {"steps_averaged": len(fs), "sub_batches": sub_batches,
+    buffers = int(line["config"]["buffers_per_gpu"]) if line else 32768
+    rec = {"steps_averaged": len(fs), "sub_batches": sub_batches, "buffers": buffers,
            "traffic_bytes_per_step": int(kib * 1024), "alg_bytes_per_step": alg,
            "traffic_over_alg": round(kib * 1024 / alg, 3),
            "per_kernel_bytes": {k: {"fetch_x2": int(2 * f * 1024), "write": int(w * 1024)}
