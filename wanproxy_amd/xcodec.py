@@ -244,14 +244,18 @@ def _as_u8(b) -> np.ndarray:
 
 
 def _pack(bufs):
+    """The buffers back to back in a per-thread staging arena (valid until the thread's next
+    _pack: the callers hand it to one library call; a fresh 64 MiB array per call paid its page
+    faults every batch)."""
     lens = np.array([len(b) for b in bufs], dtype=np.uint64)
     offs = np.zeros(len(bufs), dtype=np.uint64)
     if len(bufs) > 1:
         offs[1:] = np.cumsum(lens)[:-1]
-    arena = np.concatenate([_as_u8(b) for b in bufs]) if len(bufs) else np.zeros(0, np.uint8)
-    if arena.size == 0:
-        arena = np.zeros(1, np.uint8)
-    return np.ascontiguousarray(arena), offs, lens
+    total = int(lens.sum())
+    arena = _scratch("pack", total)
+    if total:
+        np.concatenate([_as_u8(b) for b in bufs], out=arena[:total])
+    return arena, offs, lens
 
 
 class XCodecCache:
