@@ -129,9 +129,10 @@ int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_o
  * the host (declaration growth, cross-buffer conflicts: rare) completes those inside the poll
  * or wait that finishes it.  xc_encode_run = submit + wait.  On a memory cache where a stateful
  * stream entered a hash twice with other bytes (the release build's XCodecMemoryCache::enter,
- * DESIGN.md §5.6) a device-resident run fails with XC_EINVAL, from the submit or from the call that
- * finishes it, and leaves the cache as it was before the run; xc_encode_batch_host and
- * xc_encode_streams run such batches. */
+ * DESIGN.md §5.6) the device hands the run back and the library replays it on the host through the
+ * recent window's engine (as xc_encode_batch_host / xc_encode_streams do), writing the streams,
+ * lengths and stream results into the run's arenas: same results, slower (a submit refused before
+ * any launch is replayed inside the submit; its poll / wait then returns at once). */
 int xc_encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_out_len);
 int xc_encode_poll(xc_plan *p, int *done);
 int xc_encode_wait(xc_plan *p);

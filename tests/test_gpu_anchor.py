@@ -230,6 +230,10 @@ def test_anchor_scan_recent_window_after_collisions(gpu_ctx, oracle_mod, monkeyp
     e = [np.concatenate([W.gen(97, 500), x, W.gen(98, 200)]), np.concatenate([y, x, W.gen(99, 64)])]
     assert w.XCodecEncoder(cache).encode_batch(e) == oc.encode_batch(e)
     assert len(cache) == len(oc)
+    # (f) a device-resident run on that cache: replayed by the library into the run's arenas
+    f = [np.concatenate([x, W.gen(0x9A, 700)]), np.concatenate([W.gen(0x9B, 90), y]), W.gen(0x9C, 5000)]
+    _same(_plan_run(gpu_ctx, cache, f)[0], oc.encode_batch(f))
+    assert len(cache) == len(oc)
 
 
 @pytest.mark.parametrize("ch", [0x41, 0xF1])

@@ -133,3 +133,32 @@ def test_duplicate_enter_then_batches_and_lookups(gpu_ctx, oracle_mod):
     # a direct lookup: the window's bytes or the map's (a remember when the map answers)
     assert gc.lookup(h) == oc.lookup(h)
     assert len(gc) == len(oc)
+    # device-resident runs on that cache (xc_encode_run, and submit + poll): the library replays
+    # them through the recent window's engine into the run's arenas
+    for k, use_poll in enumerate((False, True)):
+        more = [_cat(W.gen(30 + k, 64), y, x), _cat(x, W.gen(40 + k, 2100)), W.gen(50 + k, 3000)]
+        assert _device_run(gc, more, use_poll) == oc.encode_batch(more), use_poll
+        assert len(gc) == len(oc)
+
+
+def _device_run(cache, bufs, use_poll):
+    import torch
+    import wanproxy_amd as w
+    plan = w.EncodePlan(cache, [len(b) for b in bufs])
+    arena = np.zeros(plan.in_bytes, np.uint8)
+    for i, b in enumerate(bufs):
+        arena[int(plan.in_off[i]):int(plan.in_off[i]) + len(b)] = b
+    d_in = torch.from_numpy(arena).cuda()
+    d_out = torch.zeros(plan.out_bytes, dtype=torch.uint8, device="cuda")
+    d_len = torch.zeros(len(bufs), dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    if use_poll:
+        plan.submit(d_in.data_ptr(), d_out.data_ptr(), d_len.data_ptr())
+        while not plan.poll():
+            pass
+    else:
+        plan.run(d_in.data_ptr(), d_out.data_ptr(), d_len.data_ptr())
+    cache.ctx.sync()
+    out, lens = d_out.cpu().numpy(), d_len.cpu().numpy()
+    plan.close()
+    return [out[int(plan.out_off[i]):int(plan.out_off[i]) + int(lens[i])].tobytes() for i in range(len(bufs))]

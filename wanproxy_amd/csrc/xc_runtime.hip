@@ -3109,19 +3109,93 @@ extern "C" int xc_plan_set_completion(xc_plan *p, int mode)
     return XC_OK;
 }
 
-// The library's host paths take an XC__SLOW run to the replay engine; a device-resident caller
-// gets the documented code (the cache is as before the run: a duplicate enter was rolled back).
-static int public_rc(const xc_plan *p, int rc)
+struct ReplayOut {
+    const xc_plan *p;
+    std::vector<uint8_t> *out;
+    std::vector<uint64_t> *len;
+};
+
+static int replay_take(void *ctx, uint64_t i, const uint8_t *o, uint64_t n, const uint8_t *)
 {
-    if (rc == XC__SLOW && p && !p->host_path)
-        return fail(XC_EINVAL, "device-resident run on a cache with a hash entered twice by a stateful stream: "
-                               "run it through xc_encode_batch_host / xc_encode_streams (the recent window's replay)");
+    ReplayOut &r = *(ReplayOut *)ctx;
+    if (n > 2 * r.p->len[i] + 16) return fail(XC_EDEVICE, "replayed stream longer than its slot");
+    if (n) memcpy(r.out->data() + r.p->out_off[i], o, n);
+    (*r.len)[i] = n;
+    return XC_OK;
+}
+
+// A device-resident run the device path hands back (XC__SLOW: a hash entered twice by a stateful
+// stream is in the recent window, or the run entered one; the cache is as before the run): the
+// recent window's replay (xc_memcache.cpp, the host paths' engine) over the run's input arena, its
+// streams and lengths (and stream results) written where the device run puts them.  Rare: only a
+// stateful connection's carried candidate enters a hash twice (xcodec_cache.h:182-188).
+static int replay_device_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_out_len)
+{
+    xc_cache *c = p->cache;
+    const uint32_t nb = p->nb;
+    if (!c->mem) return fail(XC_EDEVICE, "replay without a memory cache");
+    int rc = set_dev(c->ctx);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(c->ctx->stream));
+    if (nb == 0) return XC_OK;
+    std::vector<uint8_t> in(p->in_bytes);
+    HIPCHK(hipMemcpy(in.data(), d_in, p->in_bytes, hipMemcpyDeviceToHost));
+    std::vector<const uint8_t *> head(nb), tail(nb, in.data());
+    std::vector<uint64_t> hl(nb), tl(nb, 0), start(nb, 0), rbase(nb, 0), olen(nb, 0);
+    std::vector<int64_t> cand(nb, -1), rcand(nb, -1);
+    std::vector<uint32_t> flags(nb, 0);
+    const bool streams = p->P.stream_st != nullptr;
+    for (uint32_t i = 0; i < nb; i++) {
+        head[i] = in.data() + p->in_off[i];
+        hl[i] = p->len[i];
+        if (streams) {  // (the states xc_plan_set_streams uploaded)
+            const uint4 &s = p->st_dev[i];
+            start[i] = s.x;
+            cand[i] = s.y == NONE ? -1 : (int64_t)s.y;
+            flags[i] = s.z;
+        }
+    }
+    const uint64_t extent = p->out_off[nb - 1] + 2 * p->len[nb - 1] + 16;
+    std::vector<uint8_t> out(extent, 0);
+    ReplayOut r{p, &out, &olen};
+    rc = xc__mem_encode_gather(c->mem, nb, head.data(), hl.data(), tail.data(), tl.data(), start.data(), cand.data(),
+                               flags.data(), rbase.data(), rcand.data(), replay_take, &r);
+    if (rc) return rc;
+    HIPCHK(hipMemcpy(d_out, out.data(), extent, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d_out_len, olen.data(), nb * 8, hipMemcpyHostToDevice));
+    if (streams) {
+        std::vector<uint2> res(nb);
+        for (uint32_t i = 0; i < nb; i++)
+            res[i] = make_uint2((uint32_t)rbase[i], rcand[i] < 0 ? NONE : (uint32_t)rcand[i]);
+        HIPCHK(hipMemcpy(p->d_stream_res, res.data(), nb * sizeof(uint2), hipMemcpyHostToDevice));
+        p->res_staged = false;
+    }
+    return XC_OK;
+}
+
+// The library's host paths take an XC__SLOW run to the replay engine themselves; a device-resident
+// run is replayed here, into its arenas.
+static int public_rc(xc_plan *p, int rc, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_out_len)
+{
+    if (rc == XC__SLOW && p && !p->host_path) return replay_device_run(p, d_in, d_out, d_out_len);
     return rc;
+}
+
+static int public_rc(xc_plan *p, int rc)
+{
+    return p ? public_rc(p, rc, p->P.in, p->P.out, p->P.out_len) : rc;
 }
 
 extern "C" int xc_encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64_t *d_out_len)
 {
-    return public_rc(p, encode_submit(p, d_in, d_out, d_out_len));
+    const int rc = encode_submit(p, d_in, d_out, d_out_len);
+    if (rc != XC__SLOW || !p || p->host_path) return rc;
+    // (refused before any launch: replayed now, its status for the poll / wait that finishes it)
+    const int r = public_rc(p, rc, d_in, d_out, d_out_len);
+    p->parked = true;
+    p->parked_rc = r;
+    p->parked_msg = r ? g_err : std::string();
+    return XC_OK;
 }
 
 extern "C" int xc_encode_poll(xc_plan *p, int *done)
@@ -3142,7 +3216,7 @@ extern "C" int xc_cache_quiesce(xc_cache *c)
     int rc = set_dev(c->ctx);
     if (rc || !c->busy) return rc;
     xc_plan *p = (xc_plan *)c->busy;
-    const int r = encode_wait(p);
+    const int r = public_rc(p, encode_wait(p));
     p->parked = true;
     p->parked_rc = r;
     p->parked_msg = r ? g_err : std::string();
@@ -3153,7 +3227,7 @@ extern "C" int xc_encode_run(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, ui
 {
     int rc = encode_submit(p, d_in, d_out, d_out_len);
     if (!rc) rc = encode_wait(p);
-    return public_rc(p, rc);
+    return public_rc(p, rc, d_in, d_out, d_out_len);
 }
 
 extern "C" int xc_host_alloc(xc_ctx *ctx, uint64_t bytes, void **out)
