@@ -20,7 +20,7 @@ ctx = w.Context(0)
 pool = W.pool(64)
 t_end = time.time() + budget
 fails = 0
-runs = {"encode": 0, "streams": 0, "decode": 0, "coss": 0, "plan": 0}
+runs = {"encode": 0, "streams": 0, "decode": 0, "coss": 0, "plan": 0, "dup": 0}
 while time.time() < t_end:
     if seed % 10 == 0:
         print("progress seed", seed, runs, "fails", fails, flush=True)
@@ -71,6 +71,37 @@ while time.time() < t_end:
                     raise AssertionError("coss decode differs")
             od.close()
             gd.close()
+            seed += 1
+            continue
+        if kind == "dup":
+            # a hash entered twice (test_gpu_dup's scenario, random order of the later calls), then
+            # batches, device-resident runs (replayed by the library) and stream calls mixing x / y
+            import test_gpu_dup as D
+            want, gc, oc = D._run(ctx, oracle, 8, D._calls(bool(rng.random() < 0.7), int(rng.choice([0, 40, 70]))),
+                                  bool(rng.random() < 0.5))
+            x, y = D._collision_pair()
+            p = W.pool(D.POOL)
+            ge, oe = w.XCodecStreamEncoder(gc), oracle.Encoder(oc)
+            for _ in range(int(rng.integers(2, 6))):
+                parts = [x, y, p[2048 * int(rng.integers(D.POOL)):][:2048], W.gen(int(rng.integers(1 << 30)), 700)]
+                bufs = [np.concatenate([parts[int(k)] for k in rng.integers(0, 4, int(rng.integers(1, 5)))])
+                        for _ in range(int(rng.integers(1, 5)))]
+                r = rng.random()
+                if r < 0.4:
+                    if D._device_run(gc, bufs, bool(rng.random() < 0.5)) != oc.encode_batch(bufs):
+                        raise AssertionError("dup device run differs")
+                elif r < 0.7:
+                    if w.XCodecEncoder(gc).encode_batch(bufs) != oc.encode_batch(bufs):
+                        raise AssertionError("dup batch differs")
+                else:
+                    for b in bufs:
+                        if ge.encode(b) != oe.encode(b):
+                            raise AssertionError("dup stream call differs")
+                if len(gc) != len(oc):
+                    raise AssertionError("dup sizes differ")
+            if ge.flush() != oe.flush():
+                raise AssertionError("dup final flush differs")
+            gc.close()
             seed += 1
             continue
         oc = oracle.Cache()
