@@ -162,3 +162,67 @@ def _device_run(cache, bufs, use_poll):
     out, lens = d_out.cpu().numpy(), d_len.cpu().numpy()
     plan.close()
     return [out[int(plan.out_off[i]):int(plan.out_off[i]) + int(lens[i])].tobytes() for i in range(len(bufs))]
+
+
+def _device_run_streams(cache, bufs, start, cand, flags):
+    """A device-resident run with per-buffer stream states (xc_plan_set_streams): the streams, then
+    the stream results (xc_plan_stream_results)."""
+    import torch
+    import wanproxy_amd as w
+    from wanproxy_amd.xcodec import _check, load_library
+    lib = load_library()
+    plan = w.EncodePlan(cache, [len(b) for b in bufs])
+    _check(lib.xc_plan_set_streams(plan.h, np.asarray(start, np.uint64), np.asarray(cand, np.int64),
+                                   np.asarray(flags, np.uint32)))
+    arena = np.zeros(plan.in_bytes, np.uint8)
+    for i, b in enumerate(bufs):
+        arena[int(plan.in_off[i]):int(plan.in_off[i]) + len(b)] = b
+    d_in = torch.from_numpy(arena).cuda()
+    d_out = torch.zeros(plan.out_bytes, dtype=torch.uint8, device="cuda")
+    d_len = torch.zeros(len(bufs), dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    plan.run(d_in.data_ptr(), d_out.data_ptr(), d_len.data_ptr())
+    cache.ctx.sync()
+    out, lens = d_out.cpu().numpy(), d_len.cpu().numpy()
+    rb, rc = np.zeros(len(bufs), np.uint64), np.zeros(len(bufs), np.int64)
+    _check(lib.xc_plan_stream_results(plan.h, rb, rc))
+    got = [out[int(plan.out_off[i]):int(plan.out_off[i]) + int(lens[i])].tobytes() for i in range(len(bufs))]
+    subs = plan.stats().sub_batches  # (0: no device pass ran, the run was replayed)
+    plan.close()
+    return got, rb.tolist(), rc.tolist(), subs
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_device_replay_matches_the_device_path_with_stream_state(gpu_ctx, monkeypatch, seed):
+    """The replay of a device-resident run (xc_runtime.hip replay_device_run) against the device path
+    on the same cache state, with per-buffer stream states (resume offset, carried candidate,
+    no-flush: xcodec_encoder.cc:60-82,175-201 between calls): the same streams, stream results and
+    cache size.  XC_FORCE_REPLAY=1 (tests only) sends the run to the replay."""
+    import wanproxy_amd as w
+    rng = np.random.default_rng(seed)
+    warm = W.pool_warmup_buffers(POOL)
+    p = W.pool(POOL)
+    bufs, start, cand, flags = [], [], [], []
+    for i in range(16):
+        segs = [p[2048 * k:2048 * (k + 1)] for k in rng.integers(0, POOL, int(rng.integers(1, 5)))]
+        b = np.concatenate([W.gen(100 * seed + i, int(rng.integers(0, 3000)))] + segs +
+                           [W.gen(200 * seed + i, int(rng.integers(0, 500)))])
+        a = int(rng.integers(0, min(len(b), 6000) + 1))
+        c = int(rng.integers(max(0, a - 4095), a - 2048 + 1)) if a >= 2048 and rng.random() < 0.6 else -1
+        bufs.append(b)
+        start.append(a)
+        cand.append(c)
+        flags.append(int(rng.random() < 0.5))
+    res = []
+    for force in ("0", "1"):
+        monkeypatch.setenv("XC_FORCE_REPLAY", force)
+        gc = w.XCodecCache(gpu_ctx, 1 << 12)
+        w.XCodecEncoder(gc).encode_batch(warm)
+        got, rb, rc, subs = _device_run_streams(gc, bufs, start, cand, flags)
+        assert (subs == 0) == (force == "1"), (force, subs)
+        res.append((got, rb, rc, len(gc)))
+        gc.close()
+    assert any(c >= 0 for c in cand) and any(f for f in flags)
+    for i in range(len(bufs)):
+        assert res[0][0][i] == res[1][0][i], f"buffer {i}: stream differs"
+    assert res[0][1:] == res[1][1:]

@@ -2794,6 +2794,10 @@ static int encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64
         // a hash entered twice may answer with other bytes than the device holds: the host paths
         // replay such runs (xc_memcache.cpp)
         if (xc__mem_live(c->mem)) return fail(XC__SLOW, "a hash entered twice is in the recent window");
+        // (XC_FORCE_REPLAY=1, tests only, read per run: a device-resident run takes the replay, so that
+        // its results can be compared with the device path's on the same state)
+        const char *fr = getenv("XC_FORCE_REPLAY");
+        if (fr && atoi(fr) && !p->host_path) return fail(XC__SLOW, "replay forced");
         p->count0 = -1;
         if (p->P.stream_st && p->cand_carried) {  // (only a carried candidate can enter a hash twice)
             uint32_t n = 0;
