@@ -61,7 +61,7 @@ def parse():
                     help="KEY=VAL set only for the per-kernel diagnostic steps after the timed region and "
                          "the verification (timing ablations, e.g. XC_ABL_EMIT=4)")
     ap.add_argument("--decode-streams", type=int, default=4096, help="cfg4: streams decoded per step")
-    ap.add_argument("--only", choices=["cfg2", "cfg3", "cfg4"],
+    ap.add_argument("--only", choices=["cfg2", "cfg3", "cfg4", "shard8"],
                     help="run just that leg (one GPU) and print its JSON object (kernel traces, A/B)")
     ap.add_argument("--no-live", action="store_true", help="skip the steady-state (live cache) leg")
     ap.add_argument("--tail-steps", type=int, default=0,
@@ -111,7 +111,7 @@ def verify_outputs(out: np.ndarray, out_off, lens: np.ndarray, case: str, bufs, 
     return {"verified_buffers": n, "verified_against": "oracle run"}
 
 
-def bench_encode_leg(ctx, warm, bufs, steps, case):
+def bench_encode_leg(ctx, warm, bufs, steps, case, input_ready=False):
     """One more encode configuration of BASELINE.json (device resident, one GPU): every step
     restores the cache snapshot (the warm pool, or empty for a cold cache) and encodes bufs."""
     import torch
@@ -125,6 +125,7 @@ def bench_encode_leg(ctx, warm, bufs, steps, case):
     lens = np.array([b.size for b in bufs], np.uint64)
     plan = w.EncodePlan(cache, lens)
     plan.set_completion(True)  # (stream ordered: every read below follows a device synchronize)
+    plan.set_input_ready(input_ready)  # (the shard8 leg: written once before the steps, as in the headline)
     arena = np.zeros(plan.in_bytes, np.uint8)
     for i, b in enumerate(bufs):
         arena[int(plan.in_off[i]):int(plan.in_off[i]) + b.size] = b
@@ -419,6 +420,9 @@ def main():
             print(json.dumps(bench_decode(args, ctx, W.pool_warmup_buffers())))
         elif args.only == "cfg2":
             print(json.dumps(bench_encode_leg(ctx, None, W.random_buffers(256), args.steps, "cfg2")))
+        elif args.only == "shard8":
+            print(json.dumps(bench_encode_leg(ctx, W.pool_warmup_buffers(), list(W.repeat_shard(32768, 0x5555, 0, 8)),
+                                              args.steps, "cfg5_g8_r0", input_ready=True)))
         else:
             print(json.dumps(bench_encode_leg(ctx, W.pool_warmup_buffers(), list(W.repeat_shard(4096, 0x77)),
                                               args.steps, "cfg3")))
@@ -633,6 +637,10 @@ def main():
             "cfg3": dict(bench_encode_leg(ctx, warm, list(W.repeat_shard(4096, 0x77)), max(args.steps, LEG_STEPS),
                                           "cfg3"),
                          workload="4096 x 64 KiB, 50% repeats, seed 0x77, warm pool cache"),
+            "shard8": dict(bench_encode_leg(ctx, warm, list(W.repeat_shard(32768, 0x5555, 0, 8)),
+                                            max(args.steps, LEG_STEPS), "cfg5_g8_r0", input_ready=True),
+                           workload="rank 0's shard of cfg5 at N=8 (4096 x 64 KiB, buffers i = 0 mod 8), warm "
+                                    "pool cache: the per-GPU unit of the 8-GPU metric, on one GPU"),
         }
 
     if rank == 0 and not args.no_cpu:

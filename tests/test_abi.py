@@ -94,3 +94,19 @@ def test_device_placement_of_caches(monkeypatch):
     assert a == [lib.xc_device_place(u, 16, 8) for u in uuids]  # the same UUID, the same device
     assert set(a) == set(range(8))
     assert lib.xc_device_place(uuids[0], 16, 0) == -22
+
+
+def test_pack_of_a_view_of_the_staging_arena():
+    """_pack reuses a per-thread staging arena; an input that is a view of that arena (a nested
+    call's result) must still be packed byte for byte (np.concatenate(out=) over an
+    aliased input)."""
+    import numpy as np
+    from wanproxy_amd import xcodec
+    a, _, _ = xcodec._pack([np.arange(5000, dtype=np.uint32).view(np.uint8)])
+    first = a[:20000].copy()
+    view = a[3:9003]  # aliases the arena
+    other = np.full(777, 7, np.uint8)
+    got, offs, lens = xcodec._pack([other, view])
+    assert list(lens) == [777, 9000] and list(offs) == [0, 777]
+    assert np.array_equal(got[:777], other)
+    assert np.array_equal(got[777:9777], first[3:9003])

@@ -421,3 +421,57 @@ def test_early_hashing_after_an_async_restore(gpu_ctx, oracle_mod, monkeypatch):
         _same(got, want[k])
     assert early[1::2] == [1, 1, 1], early  # (every B run hashed ahead: the A run before it ran clean)
     plan.close()
+
+
+def test_many_anchor_runs_of_one_plan(gpu_ctx, oracle_mod, monkeypatch):
+    """Hundreds of anchor-scanned runs of ONE plan (its declaration set reused, cleared as keys and
+    values only) over distinct inputs on a live cache: fresh data, aligned pool repeats and repeats of
+    earlier runs at unaligned offsets (declarations the predictions miss: another declaration round,
+    redone step by step).  Every run finishes and equals the oracle (the set's lo32 keys
+    must not fill up across runs)."""
+    import torch
+    import wanproxy_amd as w
+    monkeypatch.setenv("XC_SCAN", "anchor")
+    cache, oc, pool = _pool_cache(gpu_ctx, oracle_mod, 256, cap=1 << 12)
+    lens = [65536, 40000, 65536, 12345, 65536, 30001]
+    plan = w.EncodePlan(cache, lens)
+    plan.set_scan("anchor")
+    d_in = torch.zeros(plan.in_bytes, dtype=torch.uint8, device="cuda")
+    d_out = torch.zeros(plan.out_bytes, dtype=torch.uint8, device="cuda")
+    d_len = torch.zeros(len(lens), dtype=torch.int64, device="cuda")
+    prev = None
+    scans = redone = 0
+    for k in range(300):
+        rng = np.random.default_rng(0x9000 + k)
+        bufs = []
+        for i, n in enumerate(lens):
+            kind = (k + i) % 3
+            if kind == 0 or prev is None:
+                b = W.gen(0x9100 + 8 * k + i, n)
+            elif kind == 1:  # aligned pool repeats between fresh bytes
+                s = int(rng.integers(0, 200)) * 2048
+                b = np.concatenate([pool[s:s + 8192], W.gen(0x9200 + 8 * k + i, n)])[:n]
+            else:  # an earlier run's bytes at an unaligned offset
+                o = int(rng.integers(1, 2047))
+                b = np.concatenate([W.gen(0x9300 + 8 * k + i, o), prev[(i + 1) % len(lens)]])[:n]
+            if len(b) < n:
+                b = np.concatenate([b, W.gen(0x9400 + 8 * k + i, n - len(b))])
+            bufs.append(b)
+        arena = np.zeros(plan.in_bytes, np.uint8)
+        for i, b in enumerate(bufs):
+            arena[int(plan.in_off[i]):int(plan.in_off[i]) + len(b)] = b
+        d_in.copy_(torch.from_numpy(arena))
+        torch.cuda.synchronize()
+        plan.run(d_in.data_ptr(), d_out.data_ptr(), d_len.data_ptr())
+        gpu_ctx.sync()
+        out = d_out.cpu().numpy()
+        ln = d_len.cpu().numpy()
+        got = [out[int(plan.out_off[i]):int(plan.out_off[i]) + int(ln[i])].tobytes() for i in range(len(bufs))]
+        _same(got, oc.encode_batch(bufs))
+        st = plan.stats()
+        scans += int(st.anchor_scans)
+        redone += int(st.redone)
+        prev = bufs
+    plan.close()
+    assert scans >= 250 and redone > 0, (scans, redone)
+    assert len(cache) == len(oc)

@@ -276,3 +276,53 @@ def test_quiesced_run_status_is_not_dropped(gpu_ctx, oracle_mod):
     plan.wait()
     _same(outputs(), oc.encode_batch(bufs), "next run")
     plan.close()
+
+
+def test_pipelined_stream_ordered_runs_over_distinct_inputs(gpu_ctx, oracle_mod, monkeypatch):
+    """The bench's pattern with distinct inputs: one plan, input ready at submit, stream-ordered
+    completion, runs submitted back to back with no device synchronisation in between, so that run
+    k + 1's early block hashing (every sub-batch, side stream) is enqueued while run k's last
+    sub-batch still emits.  Sub-batches >= 1 of run k + 1 wait for run k's last emit (it
+    reads the same block arrays).  Every buffer of every run equals the sequential oracle's."""
+    import torch
+    import wanproxy_amd as w
+    monkeypatch.setenv("XC_SUB_MB", "2")
+    pool = W.pool(512)
+    warm = [pool[i:i + 65536] for i in range(0, len(pool), 65536)]
+    cache = w.XCodecCache(gpu_ctx, 1 << 15)
+    oc = oracle_mod.Cache()
+    _same(w.XCodecEncoder(cache).encode_batch(warm), oc.encode_batch(warm), "warm-up")
+    n, runs = 96, 8
+    plan = w.EncodePlan(cache, [65536] * n)
+    plan.set_completion(True)
+    plan.set_input_ready(True)
+    batches, d_in, d_out, d_len = [], [], [], []
+    for k in range(runs):
+        bufs = W.repeat_buffers(n, 0x6500 + k, np_segments=512, pool_bytes=pool)
+        if k:  # content of the run before at shifted offsets: same shapes, other bytes
+            bufs[40] = _cat(W.gen(0x6600 + k, 999), batches[-1][41][:65536 - 999])
+        batches.append(bufs)
+        arena = np.zeros(plan.in_bytes, np.uint8)
+        for i, b in enumerate(bufs):
+            arena[int(plan.in_off[i]):int(plan.in_off[i]) + len(b)] = b
+        d_in.append(torch.from_numpy(arena).cuda())
+        d_out.append(torch.zeros(plan.out_bytes, dtype=torch.uint8, device="cuda"))
+        d_len.append(torch.zeros(n, dtype=torch.int64, device="cuda"))
+    torch.cuda.synchronize()
+    early = []
+    for k in range(runs):
+        plan.submit(d_in[k].data_ptr(), d_out[k].data_ptr(), d_len[k].data_ptr())
+        plan.wait()
+        st = plan.stats()
+        early.append(int(st.early_hashed))
+        assert st.sub_batches >= 3, st.sub_batches
+    gpu_ctx.sync()
+    torch.cuda.synchronize()
+    for k in range(runs):
+        out = d_out[k].cpu().numpy()
+        lens = d_len[k].cpu().numpy()
+        got = [out[int(plan.out_off[i]):int(plan.out_off[i]) + int(lens[i])].tobytes() for i in range(n)]
+        _same(got, oc.encode_batch(batches[k]), f"run {k}")
+    assert sum(early) >= runs // 2, early
+    assert len(cache) == len(oc)
+    plan.close()

@@ -8,6 +8,8 @@
 #   smoke          __graft_entry__.smoke()
 #   bench[:ARGS]   python bench.py ARGS (',' for ' ') -> bench.json
 #   trace[:ARGS]   rocprofv3 --kernel-trace --stats over bench.py ARGS (default: --no-cpu --no-e2e --no-live --steps 10)
+#   leg:LEG[,N]    python bench.py --only LEG --steps N (default 200) -> leg_LEG.json
+#   legtrace:LEG   rocprofv3 --kernel-trace over bench.py --only LEG --steps 40 -> timeline_LEG.txt
 #   pmc            FETCH_SIZE and WRITE_SIZE passes (separate runs) -> pmc_traffic_cfg5.json (stamped)
 #   pmcinst        two SQ counter passes (VALU / LDS / waits) over one cfg5 step -> pmc_inst/
 #   py:SCRIPT[:ARGS]  python SCRIPT ARGS
@@ -55,6 +57,18 @@ for step in "$@"; do
         timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run \
             -- python3 bench.py $a > "$out/trace.log" 2>&1 || die trace $? "$out/trace.log"
         echo "trace ok" ;;
+    leg)
+        lg=${arg%%,*}
+        n=200
+        [ "$lg" != "$arg" ] && n=${arg#*,}
+        timeout -k 10 300 python bench.py --only $lg --steps $n > "$out/leg_$lg.json" 2> "$out/leg_$lg.err" \
+            || die "leg $lg" $? "$out/leg_$lg.err"
+        python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['value'], d['ms_per_step'], d['roofline']['frac'], d['verified_buffers'])" "$out/leg_$lg.json" $lg ;;
+    legtrace)
+        timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/lt_$arg" -o run \
+            -- python3 bench.py --only $arg --steps 40 > "$out/lt_$arg.log" 2>&1 || die "legtrace $arg" $? "$out/lt_$arg.log"
+        python3 tools/timeline.py "$out/lt_$arg/run_kernel_trace.csv" 40 > "$out/timeline_$arg.txt" || die timeline $? "$out/lt_$arg.log"
+        echo "legtrace $arg ok" ;;
     pmc)
         # (pmc:--total,S: a rank-sized shard of S buffers on this GPU -> pmc_traffic_cfg5_bS.json)
         a=${arg//,/ }

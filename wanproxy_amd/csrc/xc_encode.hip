@@ -1422,7 +1422,14 @@ __device__ __forceinline__ void decl_hash(const PlanDev &P, uint32_t b)
             if (l == 0) {
                 P.tok_h[tt] = h;
                 const uint64_t v = ((uint64_t)b << 32) | P.tok_dpos[tt];
-                set_insert(P.dset, h, v, true, nullptr, nullptr);
+                // (an anchor-scanned sub-batch's set is keys and values only: k_clear_set leaves its
+                // filters and lo32 keys alone, so nothing may be added to them)
+                if (P.anc_scan) {
+                    uint32_t slot;
+                    set_insert_kv(P.dset, h, v, &slot);
+                } else {
+                    set_insert(P.dset, h, v, true, nullptr, nullptr);
+                }
                 // not in the set the positions were scanned against: another round is needed
                 if (__hip_atomic_load(&P.ctl[CTL_GREW], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
                     atomicOr(&P.ctl[CTL_GREW], 1u);

@@ -1329,10 +1329,11 @@ struct xc_plan {
     // xc_plan_set_input_ready: the input is complete when a run is submitted, so the run's first
     // sub-batch is hashed on the side stream at once, beside the previous run's last kernels
     // (early_ok: the previous run of this plan went through the asynchronous pass unchanged;
-    // ev_sb0: after its first sub-batch's last kernel that reads the block arrays)
+    // ev_sb0: after its first sub-batch's last kernel that reads the block arrays; ev_last: after its
+    // last sub-batch's emit, the last reader of every later sub-batch's block arrays)
     bool input_ready = false, early_ok = false;
-    bool rec_sb0 = false;  // (this run records ev_sb0: only a plan of several sub-batches with its input ready uses it)
-    hipEvent_t ev_sb0 = nullptr;
+    bool rec_sb0 = false;  // (this run records ev_sb0 and ev_last: only a plan of several sub-batches with its input ready uses them)
+    hipEvent_t ev_sb0 = nullptr, ev_last = nullptr;
     // The emit of a large sub-batch (its wire bytes and segment-store copies) runs on its own stream
     // es, beside the next sub-batch's predictions and anchor scan; the main stream joins it before
     // the next resolve (the first reader of the new segments' bytes) and at the pass's end.
@@ -1710,6 +1711,7 @@ extern "C" int xc_encode_plan_create_sub(xc_cache *c, const uint64_t *lengths, u
     for (auto &e : p->ev_hash) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (auto &e : p->ev_go) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&p->ev_sb0, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&p->ev_last, hipEventDisableTiming));
     HIPCHK(hipMemcpyAsync(p->d_blk_base, blk_base.data(), (nbuf + 1) * 4, hipMemcpyHostToDevice, s));
     P.blk_base = p->d_blk_base;
     HIPCHK(dmalloc(&P.buf_next, nb1 * 4));
@@ -2048,6 +2050,7 @@ extern "C" int xc_plan_destroy(xc_plan *p)
     for (auto e : p->ev_go)
         if (e) hipEventDestroy(e);
     if (p->ev_sb0) hipEventDestroy(p->ev_sb0);
+    if (p->ev_last) hipEventDestroy(p->ev_last);
     pool_free(p->h_lenpos);
     pool_free(p->h_st);
     if (p->es) {
@@ -2869,7 +2872,12 @@ static int encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64
         const uint32_t *lim = p->P.sb_count + (p->sub.size() - 2);
         const uint32_t upto = early_all ? (uint32_t)p->sub.size() - 1 : 1u;
         for (uint32_t k = 0; k < upto; k++)
-            if ((rc = enqueue_block_hash(p, k, k == 0 ? p->ev_sb0 : nullptr, p->hs, false, lim, floor))) return rc;
+            // (sub-batch 0 after the previous run's sub-batch 0 emit; the later ones, chained behind it,
+            // after the previous run's last emit: its k_insert / k_emit read those block arrays after the
+            // stream-ordered completion let the host return)
+            if ((rc = enqueue_block_hash(p, k, k == 0 ? p->ev_sb0 : k == 1 ? p->ev_last : nullptr, p->hs, false, lim,
+                                         floor)))
+                return rc;
         hashed = upto;
         p->early_runs++;
         p->stats.early_hashed = 1;
@@ -2900,6 +2908,7 @@ static int encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64
             if (rc) return rc;
         }
         if ((rc = join_emit(p))) return rc;  // (the pass's results complete in the context stream's order)
+        if (p->rec_sb0) HIPCHK(hipEventRecord(p->ev_last, s));  // (the next run's early hashing of sub-batches >= 1)
         if (!pub) HIPCHK(hipMemcpyAsync(p->h_ctl, p->P.ctl, CTL_WORDS * 4, hipMemcpyDeviceToHost, s));
         if ((rc = record_ctl(p))) return rc;
         // the tail check right behind the pass (after its event: the host's wait does not cover it),

@@ -253,8 +253,13 @@ def _pack(bufs):
         offs[1:] = np.cumsum(lens)[:-1]
     total = int(lens.sum())
     arena = _scratch("pack", total)
+    parts = [_as_u8(b) for b in bufs]
+    # (a buffer that is itself a view of this thread's staging arena, e.g. from a nested call, would be
+    # overwritten while it is copied: such a call packs into a fresh array)
+    if any(p.size and np.shares_memory(p, arena) for p in parts):
+        arena = np.empty(max(total, 1), np.uint8)
     if total:
-        np.concatenate([_as_u8(b) for b in bufs], out=arena[:total])
+        np.concatenate(parts, out=arena[:total])
     return arena, offs, lens
 
 
