@@ -110,3 +110,31 @@ def test_pack_of_a_view_of_the_staging_arena():
     assert list(lens) == [777, 9000] and list(offs) == [0, 777]
     assert np.array_equal(got[:777], other)
     assert np.array_equal(got[777:9777], first[3:9003])
+
+
+def test_release_library_reads_only_documented_knobs():
+    """The release library's environment surface (wanproxy_amd/csrc/xc_env.h): getenv reads only the
+    documented deployment knobs, each named in a test; ablations and diagnostics go through abl_env,
+    which is a constant nullptr unless the library is built with -DXC_ABLATIONS=1."""
+    import glob
+    knobs = {"XC_DEVICE", "XC_DEVICE_POLICY", "XC_SUB_MB", "XC_CHUNK_BLOCKS", "XC_NO_SHADOW", "XC_SCAN",
+             "XC_ANCHOR_MIN_KEYS", "XC_REPLAY_THREADS", "XC_GRAPH", "XC_FORCE_REPLAY"}
+    seen = set()
+    for f in sorted(glob.glob(os.path.join(ROOT, "wanproxy_amd", "csrc", "*.*"))):
+        if not f.endswith((".hip", ".h", ".cpp")):
+            continue
+        src = open(f).read()
+        for m in re.finditer(r"getenv\(([^)]*)\)", src):
+            arg = m.group(1).strip()
+            if os.path.basename(f) == "xc_env.h" and arg == "name":
+                continue  # (abl_env itself, under #if XC_ABLATIONS)
+            name = arg.strip('"')
+            assert name in knobs, f"{os.path.basename(f)} reads {arg}"
+            seen.add(name)
+    assert seen == knobs, knobs - seen
+    env_h = open(os.path.join(ROOT, "wanproxy_amd", "csrc", "xc_env.h")).read()
+    assert re.search(r"#if XC_ABLATIONS\s+return getenv\(name\);\s+#else", env_h)
+    tests = "".join(open(t).read().split("def test_release_library_reads_only_documented_knobs")[0]
+                    for t in glob.glob(os.path.join(ROOT, "tests", "*.py")))
+    for k in knobs:
+        assert re.search(rf"\b{k}\b", tests), f"{k} is named in no test"

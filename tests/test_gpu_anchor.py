@@ -475,3 +475,20 @@ def test_many_anchor_runs_of_one_plan(gpu_ctx, oracle_mod, monkeypatch):
     plan.close()
     assert scans >= 250 and redone > 0, (scans, redone)
     assert len(cache) == len(oc)
+
+
+@pytest.mark.parametrize("min_keys,anchored", [("1", True), ("1000000000", False)])
+def test_anchor_min_keys_knob(gpu_ctx, oracle_mod, monkeypatch, min_keys, anchored):
+    """XC_ANCHOR_MIN_KEYS (the cached + new keys from which a plan in AUTO mode scans through the
+    anchor index, 200 000 by default): a 1-key threshold anchor-scans a small cache's runs, a huge one
+    never; both encode the oracle's bytes."""
+    monkeypatch.delenv("XC_SCAN", raising=False)
+    monkeypatch.setenv("XC_ANCHOR_MIN_KEYS", min_keys)
+    monkeypatch.setenv("XC_SUB_MB", "1")
+    cache, oc, pool = _pool_cache(gpu_ctx, oracle_mod)
+    bufs = W.repeat_buffers(40, 0x5252, np_segments=512, pool_bytes=pool)
+    bufs[5] = np.concatenate([W.gen(0x5253, 1111), bufs[3][:50000]])
+    got, st = _plan_run(gpu_ctx, cache, bufs, mode="auto")
+    _same(got, oc.encode_batch(bufs))
+    assert (st.anchor_scans > 0) == anchored, (st.anchor_scans, st.sub_batches)
+    assert len(cache) == len(oc)

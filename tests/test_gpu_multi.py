@@ -26,12 +26,14 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_bench_sharded_ranks_on_one_gpu(world):
+    """world = 8 is the driver's 8-GPU launch shape (8 processes, 8 HIP contexts, gloo, each rank's
+    4096-buffer shard as one sub-batch), here with all ranks on the one GPU."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--steps", "2", "--warmup", "1", "--no-cpu"]
-    env = dict(os.environ, OMP_NUM_THREADS="4")
+    env = dict(os.environ, OMP_NUM_THREADS=str(max(1, 16 // world)))
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=env, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
     line = [x for x in out.stdout.splitlines() if x.startswith("{")][-1]

@@ -115,3 +115,18 @@ def test_whole_run_replay_with_hash_zero_and_repeats():
     finally:
         lib.xc__mem_free(m_run)
         lib.xc__mem_free(m_seq)
+
+
+@pytest.mark.parametrize("threads", ["0", "1", "3"])
+def test_replay_threads_knob(threads):
+    """XC_REPLAY_THREADS (the helper threads of the whole-run replay, read once per process): with
+    none, one or three helpers the window still equals the FIFO model's (a fresh process each)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, XC_REPLAY_THREADS=threads)
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider",
+                        os.path.join(root, "tests", "test_window_replay.py"), "-k", "fifo or zero_and_repeats"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]

@@ -11,7 +11,8 @@ cd "$out"/w/csrc
 if [ -n "$XC_VARIANT_SED" ]; then sed -i "$XC_VARIANT_SED" ${XC_VARIANT_FILE:-xc_encode.hip}; fi  # (a source edit for the variant)
 FL="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -Wno-unused-value $*"
 for f in xc_encode xc_decode xc_runtime; do /opt/rocm/bin/hipcc $FL -c $f.hip -o $f.o & done
-for f in *.cpp; do g++ -O2 -std=c++17 -fPIC -Wall -c $f -o ${f%.cpp}.o; done
+DF=$(printf "%s\n" "$@" | { grep "^-D" || true; } | tr "\n" " ")  # (the -D flags reach the host-only sources too)
+for f in *.cpp; do g++ -O2 -std=c++17 -fPIC -Wall $DF -c $f -o ${f%.cpp}.o; done
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$root"/wanproxy_amd/libxcodec_hip_b.so *.o
 rm -rf "$out"

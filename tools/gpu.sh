@@ -10,6 +10,7 @@
 #   trace[:ARGS]   rocprofv3 --kernel-trace --stats over bench.py ARGS (default: --no-cpu --no-e2e --no-live --steps 10)
 #   leg:LEG[,N]    python bench.py --only LEG --steps N (default 200) -> leg_LEG.json
 #   legtrace:LEG   rocprofv3 --kernel-trace over bench.py --only LEG --steps 40 -> timeline_LEG.txt
+#   ranks          bench.py --total 32768 / 16384 / 8192 / 4096 (one rank's shard of the 1/2/4/8-GPU job on this GPU)
 #   pmc            FETCH_SIZE and WRITE_SIZE passes (separate runs) -> pmc_traffic_cfg5.json (stamped)
 #   pmcinst        two SQ counter passes (VALU / LDS / waits) over one cfg5 step -> pmc_inst/
 #   py:SCRIPT[:ARGS]  python SCRIPT ARGS
@@ -69,6 +70,12 @@ for step in "$@"; do
             -- python3 bench.py --only $arg --steps 40 > "$out/lt_$arg.log" 2>&1 || die "legtrace $arg" $? "$out/lt_$arg.log"
         python3 tools/timeline.py "$out/lt_$arg/run_kernel_trace.csv" 40 > "$out/timeline_$arg.txt" || die timeline $? "$out/lt_$arg.log"
         echo "legtrace $arg ok" ;;
+    ranks)
+        for tot in 32768 16384 8192 4096; do
+            timeout -k 10 300 python bench.py --no-cpu --no-e2e --no-legs --no-live --no-decode --steps 20 --total $tot \
+                > "$out/ranks_$tot.json" 2> "$out/ranks_$tot.err" || die "ranks $tot" $? "$out/ranks_$tot.err"
+            python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); s=d['stats']; print('total', sys.argv[2], d['value'], d['ms_per_step'], s['sub_batches'], s['anchor_scans'], s['early_hashed'], d['verified_buffers'])" "$out/ranks_$tot.json" $tot
+        done ;;
     pmc)
         # (pmc:--total,S: a rank-sized shard of S buffers on this GPU -> pmc_traffic_cfg5_bS.json)
         a=${arg//,/ }

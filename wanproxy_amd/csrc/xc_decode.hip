@@ -27,6 +27,7 @@
 
 #include "../../include/xcodec_hip.h"
 #include "xc_kernels.h"
+#include "xc_env.h"
 
 namespace xc {
 
@@ -86,74 +87,6 @@ __device__ __forceinline__ void dctl_publish(const DecDev &D)
     __threadfence_system();
 }
 
-// Tokenizer window: 1 KiB of the stream in registers (lane l: bytes w0 + 16 l .. + 15) and the
-// lane's mask of F1 bytes at positions in [from, n).
-struct DWin {
-    uint32_t w0;
-    uint4 v;
-    uint32_t m;
-};
-
-__device__ __forceinline__ uint32_t magic_mask16(const uint4 &v)
-{
-    uint32_t m = 0;
-    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int k = 0; k < 4; k++)
-#pragma unroll
-        for (int b = 0; b < 4; b++)
-            m |= ((d[k] >> (8 * b)) & 0xffu) == XC_MAGIC ? 1u << (4 * k + b) : 0u;
-    return m;
-}
-
-// Keep only mask bits of positions in [from, n).
-__device__ __forceinline__ uint32_t clip16(uint32_t m, uint32_t base, uint32_t from, uint32_t n)
-{
-    if (from > base) m = from - base >= 16u ? 0u : m & (0xFFFFu << (from - base));
-    if (n < base + 16u) m = n <= base ? 0u : m & ((1u << (n - base)) - 1u);
-    return m;
-}
-
-__device__ __forceinline__ void dwin_load(DWin &w, const uint8_t *s, uint32_t p, uint32_t n)
-{
-    // the stream arena is padded past every stream, so a whole window is always readable
-    w.w0 = p & ~15u;
-    const uint32_t base = w.w0 + 16u * lane_id();
-    w.v = *(const uint4 *)(s + base);
-    w.m = clip16(magic_mask16(w.v), base, p, n);
-}
-
-// Byte x of the stream, w0 <= x < w0 + 1024 (x uniform): from the window registers.
-__device__ __forceinline__ uint32_t dwin_byte(const DWin &w, uint32_t x)
-{
-    const uint32_t r = x - w.w0, k = (r >> 2) & 3u;
-    const uint32_t d = k == 0 ? w.v.x : k == 1 ? w.v.y : k == 2 ? w.v.z : w.v.w;
-    return (readlane(d, (int)(r >> 4)) >> (8 * (r & 3u))) & 0xffu;
-}
-
-// Dword i of the window (uniform i): lane i / 4 holds dwords 4 l .. 4 l + 3.
-__device__ __forceinline__ uint32_t dwin_dword(const DWin &w, uint32_t i)
-{
-    const uint32_t k = i & 3u;
-    const uint32_t d = k == 0 ? w.v.x : k == 1 ? w.v.y : k == 2 ? w.v.z : w.v.w;
-    return readlane(d, (int)(i >> 2));
-}
-
-// The big-endian 64-bit value at bytes x .. x + 7 of the window, w0 <= x, x + 8 <= w0 + 1024 (x
-// uniform): three dwords instead of eight single bytes.
-__device__ __forceinline__ uint64_t dwin_be64(const DWin &w, uint32_t x)
-{
-    const uint32_t r = x - w.w0, i = r >> 2, sh = 8u * (r & 3u);
-    const uint32_t d0 = dwin_dword(w, i), d1 = dwin_dword(w, i + 1u);
-    const uint32_t d2 = (r & 3u) ? dwin_dword(w, i + 2u) : 0u;  // (i + 2 stays inside the window then)
-    const uint32_t lo = sh ? (d0 >> sh) | (d1 << (32u - sh)) : d0;  // bytes x .. x + 3, little endian
-    const uint32_t hi = sh ? (d1 >> sh) | (d2 << (32u - sh)) : d1;
-    return ((uint64_t)__builtin_bswap32(lo) << 32) | __builtin_bswap32(hi);
-}
-
-// Tokenizer (xcodec_decoder.cc:85-173), one wave per stream: tokens are found inside 1 KiB
-// register windows (ESC and REF tokens, and the REF hash bytes, without another load); only an
-// EXTRACT, whose 2048-byte payload is skipped, or the window's end, loads a new window.
 __device__ __forceinline__ void dclear_range(const DecDev &D, uint32_t n_lo, uint32_t n_full, uint32_t i0,
                                              uint32_t stride);
 __device__ __forceinline__ void dset_clear_range(const DevSet &s, uint32_t n_lo, uint32_t n_full, uint32_t i0,
@@ -165,7 +98,7 @@ __device__ __forceinline__ void dset_clear_range(const DevSet &s, uint32_t n_lo,
 // becomes a stream of independent loads.  Each window's F1 positions are a 64-bit mask per lane
 // (lane l: positions 64 l ..); its bytes go to the wave's LDS copy, from which the op byte and a
 // REF's hash bytes are read (a token whose 10 bytes cross the window's end reads them from memory).
-// Token semantics as k_dtok_win (xcodec_decoder.cc:85-173).
+// Token semantics: xcodec_decoder.cc:85-173.
 constexpr uint32_t DTOK_WIN = 4096;
 
 __device__ __forceinline__ uint32_t magic_mask4(uint32_t d)
@@ -397,7 +330,6 @@ __global__ __launch_bounds__(64) void k_dtok(DecDev D, int fill, int first, uint
     if (HASH && xn) flush();
     if (l == 0) D.tok_cnt[j] = nt;
 }
-template __global__ void k_dtok<false, true>(DecDev, int, int, uint32_t, uint32_t);
 template __global__ void k_dtok<true, true>(DecDev, int, int, uint32_t, uint32_t);
 template __global__ void k_dtok<true, false>(DecDev, int, int, uint32_t, uint32_t);
 
@@ -434,86 +366,6 @@ __global__ __launch_bounds__(64) void k_dprobe(DecDev D)
             D.t_src[tb + t] = st == R_OKCACHE ? v : 0;
         }
     }
-}
-
-// The round-2 tokenizer (kept for A/B): F1 search in 1 KiB register windows loaded on demand.
-__global__ __launch_bounds__(64) void k_dtok_win(DecDev D, int fill, int first, uint32_t n_lo, uint32_t n_full)
-{
-    const uint32_t j = blockIdx.x;
-    if (first) {
-        if (j == 0 && threadIdx.x < DCTL_WORDS) D.ctl[threadIdx.x] = 0u;
-        if (j < D.ns && threadIdx.x == 0) D.s_lim[j] = 0xFFFFFFFFu;
-        dclear_range(D, n_lo, n_full, j * 64u + threadIdx.x, gridDim.x * 64u);
-    }
-    if (j >= D.ns) return;
-    const uint8_t *s = D.in + D.in_off[j];
-    const uint32_t n = D.in_len[j];
-    const uint32_t tb = fill ? D.tok_base[j] : 0u;
-    uint32_t nt = 0, lb = 0, p = 0;
-    auto put = [&](uint32_t op, uint32_t le, uint64_t h) {
-        if (fill && lane_id() == 0) {
-            D.t_lb[tb + nt] = lb;
-            D.t_le[tb + nt] = le;
-            D.t_op[tb + nt] = op;
-            D.t_h[tb + nt] = h;
-        }
-        nt++;
-    };
-    DWin w;
-    dwin_load(w, s, 0u, n);
-    // after an EXTRACT, the 2 KiB that follow the next 2050 bytes are read ahead into L2: the window
-    // after the next EXTRACT payload when up to 1 KiB of REF / escape tokens separate the two
-    // (one memory latency less per EXTRACT); consumed at the next EXTRACT, so nothing waits on them
-    uint4 ra = make_uint4(0, 0, 0, 0), rb = ra;
-    uint32_t sink = 0;
-    for (;;) {
-        const uint64_t b = ballot(w.m != 0u);
-        if (!b) {
-            p = max(p, w.w0 + 1024u);  // (an ESC / REF may end past the window)
-            if (p >= n) { put(T_END, n, 0); break; }
-            dwin_load(w, s, p, n);
-            continue;
-        }
-        const int f = __ffsll((unsigned long long)b) - 1;
-        const uint32_t q = w.w0 + 16u * (uint32_t)f + (uint32_t)__builtin_ctz(readlane(w.m, f));
-        if (q + 1u >= n) { put(T_WAIT, q, 0); break; }
-        const uint32_t op = q + 1u < w.w0 + 1024u ? dwin_byte(w, q + 1u) : s[q + 1u];
-        if (op == 0x00u) {  // escape: stays inside the literal run
-            p = q + 2u;
-            w.m = clip16(w.m, w.w0 + 16u * lane_id(), p, n);
-            continue;
-        }
-        if (op == 0x01u) {
-            if (n - q < 2u + XC_SEG) { put(T_WAIT, q, 0); break; }
-            put(T_EXTRACT, q, 0);
-            lb = p = q + 2u + XC_SEG;
-            sink ^= ra.x ^ rb.y;
-            dwin_load(w, s, p, n);
-            const uint32_t ahead = (p + 2u + XC_SEG) & ~15u;
-            if (ahead + 2048u <= n) {
-                ra = *(const uint4 *)(s + ahead + 16u * lane_id());
-                rb = *(const uint4 *)(s + ahead + 1024u + 16u * lane_id());
-            }
-            continue;
-        }
-        if (op == 0x02u) {
-            if (n - q < 10u) { put(T_WAIT, q, 0); break; }
-            uint64_t h = 0;
-            if (q + 10u <= w.w0 + 1024u) {
-                h = dwin_be64(w, q + 2u);
-            } else {
-                for (uint32_t k = 0; k < 8; k++) h = (h << 8) | s[q + 2u + k];
-            }
-            put(T_REF, q, h);
-            lb = p = q + 10u;
-            w.m = clip16(w.m, w.w0 + 16u * lane_id(), p, n);
-            continue;
-        }
-        put(T_BADOP, q, 0);
-        break;
-    }
-    if (lane_id() == 0) D.tok_cnt[j] = nt;
-    if ((sink ^ ra.z ^ rb.w) == 0x9E3779B9u && n == 0u) D.ctl[DCTL_WORDS - 1] = 1u;  // (never: keeps the reads)
 }
 
 // k_dres1 / k_dres2 grids: (streams, DRES_WAVES), wave y taking tokens y, y + DRES_WAVES, ...
@@ -1319,10 +1171,9 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
     }
     // the parse of this run's input on the side stream at once (input ready), into the token set the
     // run before this one did not use (its last reader, two runs back, is long done)
-    static const bool old_tok = getenv("XC_DTOK_WIN") && atoi(getenv("XC_DTOK_WIN"));
-    // XC_DTOK_NOHASH=1 (experiments): round 0's hashes and probes in k_dres1<true>, as before
-    static const bool tok_hash = !old_tok && !(getenv("XC_DTOK_NOHASH") && atoi(getenv("XC_DTOK_NOHASH")));
-    const bool early = p->input_ready && tok_hash && !p->internal;
+    // (round 0's hashes are taken by the tokenizer as it passes each payload: a separate k_dres1<true>
+    // measured cfg4 914 against 940 GiB/s; the round-2 1 KiB-window tokenizer 905 against 928, §5.1)
+    const bool early = p->input_ready && !p->internal;
     if (early) {
         if (!p->ps) {  // (the second token set, the side stream and its events, once)
             xc_dplan::TokSet &t1 = p->tset[1];
@@ -1396,8 +1247,7 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
     const int64_t count0 = xc__cache_host_count(p->cache);
     xc__cache_count_unknown(p->cache);
     // tokens, with the prologue (control words, provider limits, round 0's provider table)
-    // (XC_DTOK_WIN=1, experiments: the round-2 tokenizer)
-    if (tok_hash && !early) {  // (the batch table cleared before the tokenizer inserts into it)
+    if (!early) {  // (the batch table cleared before the tokenizer inserts into it)
         hipLaunchKernelGGL(k_dclear, dim3(512), dim3(256), 0, s, D, p->n_lo, p->n_full);
         DHIP(hipGetLastError());
     }
@@ -1409,8 +1259,7 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
         Dq.clr_full = p->n_full;
         hipLaunchKernelGGL(k_dprobe, dim3(ns), dim3(64), 0, s, Dq);
     } else {
-        auto tok = old_tok ? k_dtok_win : tok_hash ? k_dtok<true, true> : k_dtok<false, true>;
-        hipLaunchKernelGGL(tok, dim3(std::max<uint32_t>(ns, 256u)), dim3(64), 0, s, D, 1, 1, p->n_lo, p->n_full);
+        hipLaunchKernelGGL((k_dtok<true, true>), dim3(std::max<uint32_t>(ns, 256u)), dim3(64), 0, s, D, 1, 1, p->n_lo, p->n_full);
     }
     DHIP(hipGetLastError());
     // one provider-resolution round (a fresh batch table each time; round 0's came with k_dtok)
@@ -1419,8 +1268,6 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
             hipLaunchKernelGGL(k_dclear, dim3(512), dim3(256), 0, s, D, p->n_lo, p->n_full);
             DHIP(hipGetLastError());
             hipLaunchKernelGGL(k_dres1<false>, dim3(ns, DRES_WAVES), dim3(64), 0, s, D);
-        } else if (!tok_hash) {
-            hipLaunchKernelGGL(k_dres1<true>, dim3(ns, DRES_WAVES), dim3(64), 0, s, D);
         }
         DHIP(hipGetLastError());
         hipLaunchKernelGGL(k_dres2, dim3(ns), dim3(64), 0, s, D);  // (a wave per stream)
@@ -1446,7 +1293,8 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
             p->h_ctl[DCTL_WORDS - 1] = 0xFFFFFFFFu;
             Da.ctl_host = p->d_hctl;
         }
-        static const uint32_t dfin_grid = getenv("XC_DFIN_GRID") ? (uint32_t)atoi(getenv("XC_DFIN_GRID")) : DFIN_GRID;
+        // (XC_DFIN_GRID, -DXC_ABLATIONS builds: another grid)
+        static const uint32_t dfin_grid = abl_env("XC_DFIN_GRID") ? (uint32_t)atoi(abl_env("XC_DFIN_GRID")) : DFIN_GRID;
         hipLaunchKernelGGL(k_dfin, dim3(std::max(1u, std::min(dfin_grid, (ns + DFIN_WAVES - 1) / DFIN_WAVES))),
                            dim3(64 * DFIN_WAVES), 0, s, Da, r);
         DHIP(hipGetLastError());  // (slots first: k_demit fills them)

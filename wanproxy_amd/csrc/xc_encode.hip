@@ -21,10 +21,8 @@
 #include "xc_kernels.h"
 
 // Timing ablations (XC_ABL_BH, XC_ABL_EMIT: the results are wrong) only in builds with
-// -DXC_ABLATIONS=1 (tools/build_variant.sh): production kernels carry no such branch.
-#ifndef XC_ABLATIONS
-#define XC_ABLATIONS 0
-#endif
+// -DXC_ABLATIONS=1 (tools/build_variant.sh, xc_env.h): production kernels carry no such branch.
+#include "xc_env.h"
 
 namespace xc {
 
@@ -1687,8 +1685,7 @@ __global__ __launch_bounds__(256, 4) void k_blockhash(DeclArgs a)
     const uint32_t n = nfull > k0 ? min(BLK_GROUP, nfull - k0) : 0u;
     const uint32_t na = ANC ? min(BLK_GROUP, (len + XC_SEG - 1u) / XC_SEG - k0) : n;
     uint32_t w[BLK_GROUP][8];  // (kept for the compares below)
-    if (ANC && (a.nt & 1)) wave_load_blocks<BLK_GROUP, true>(base + (size_t)k0 * XC_SEG, na, w);
-    else wave_load_blocks<BLK_GROUP>(base + (size_t)k0 * XC_SEG, na, w);
+    wave_load_blocks<BLK_GROUP>(base + (size_t)k0 * XC_SEG, na, w);
     const uint64_t h = block_group_hash<BLK_GROUP>(w);
     const uint32_t l = lane_id();
     const uint32_t gi = P.blk_base[b] + k0 + l;
@@ -1708,7 +1705,7 @@ __global__ __launch_bounds__(256, 4) void k_blockhash(DeclArgs a)
     uint64_t akey = ANC_NONE;
     // XC_ABL_BH (timing ablations only: the results are wrong; in builds with -DXC_ABLATIONS=1):
     // 2 = no anchors at all
-    const uint32_t abl = XC_ABLATIONS ? (uint32_t)a.nt & ~1u : 0u;
+    const uint32_t abl = XC_ABLATIONS ? (uint32_t)a.nt : 0u;
     if (ANC && !(abl & 2u))
         akey = group_anchors(P, g, k0, len, n, na, base, w, tiles[(threadIdx.x >> 6) & (ANC ? 3 : 0)],
                              lists[(threadIdx.x >> 6) & (ANC ? 3 : 0)], abl, drop);

@@ -269,7 +269,7 @@ struct DeclArgs {
     // k_blockhash on the side stream: the cache count below which entries are complete while it
     // runs (P.sb_count of the sub-batch the main stream is in); null: no block compares
     const uint32_t *limit;
-    int nt;  // k_blockhash<.., true>: non-temporal block loads (XC_BH_NT, experiments)
+    int nt;  // k_blockhash: the XC_ABL_BH timing-ablation bits (-DXC_ABLATIONS builds; 0 otherwise)
     // k_blockhash<false, true> with compares (limit): no anchor records for a block whose block and
     // the one before are cached (every proposal of them would fall on an aligned window or in a
     // predicted REF's shadow; the async pass's shadows are on: xc_plan.shadow)

@@ -33,6 +33,7 @@
 #include <vector>
 
 #include "../../include/xcodec_hip.h"
+#include "xc_env.h"
 
 extern "C" int xc__set_error(int code, const char *msg);
 extern "C" int xc__encode_batch_host_coll(xc_cache *c, const uint8_t *in, const uint64_t *in_off,
@@ -521,7 +522,7 @@ int encode(C *c, std::vector<CItem> items, uint8_t *out, const uint64_t *out_off
            uint64_t *out_len, uint64_t *res_base, int64_t *res_cand)
 {
     // (XC_REPLAY_PROF=1: passes, their items and the time of each phase, to stderr)
-    static const bool prof = getenv("XC_REPLAY_PROF") && atoi(getenv("XC_REPLAY_PROF"));
+    static const bool prof = xc::abl_flag("XC_REPLAY_PROF");  // (-DXC_ABLATIONS builds)
     using clk = std::chrono::steady_clock;
     double t_dev = 0, t_ev = 0, t_rep = 0, t_set = 0, t_mir = 0;
     uint64_t n_set = 0, n_mir = 0, n_held = 0;

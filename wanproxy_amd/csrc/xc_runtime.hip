@@ -25,6 +25,7 @@
 
 #include "../../include/xcodec_hip.h"
 #include "xc_kernels.h"
+#include "xc_env.h"
 
 
 using namespace xc;
@@ -222,17 +223,9 @@ extern "C" int xc_ctx_create(int dev, xc_ctx **out)
     HIPCHK(hipSetDevice(dev));
     xc_ctx *c = new xc_ctx();
     c->dev = dev;
-    {
-        // XC_STREAM_PRIO=1 (experiments): the context stream at the highest priority, so that its
-        // latency-bound kernels are dispatched ahead of the side stream's block hashing (the side
-        // stream's own priority: xc_plan creation below)
-        const char *e = getenv("XC_STREAM_PRIO");
-        int lo = 0, hi = 0;
-        if (e && atoi(e) == 1 && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
-            HIPCHK(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi));
-        else
-            HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    }
+    // (at the default priority: the context stream high and the side stream low starved the block
+    // hashing, cfg5 -7.5 %)
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, dev));
     c->n_cu = prop.multiProcessorCount;
@@ -1481,13 +1474,9 @@ extern "C" int xc_encode_plan_create_sub(xc_cache *c, const uint64_t *lengths, u
         uint64_t total = 0;
         for (uint32_t i = 0; i < nbuf; i++) total += lengths[i];
         const uint64_t sub_max = sub_bytes(total, sub_bytes_max);
-        // XC_FIRST_SUB_MB (experiments): the first sub-batch's bound (its block hashing has
-        // nothing to overlap with)
-        const char *fe = getenv("XC_FIRST_SUB_MB");
-        const uint64_t first_max = fe && atol(fe) > 0 ? (uint64_t)atol(fe) << 20 : sub_max;
         for (uint32_t i = 0; i < nbuf; i++) {
             if (lengths[i] > MAX_BUF) return fail(XC_EINVAL, "buffer longer than 1 MiB");
-            if (cnt && (bytes + lengths[i] > (p->sub.size() == 1 ? first_max : sub_max) || cnt >= SUB_BUFS)) {
+            if (cnt && (bytes + lengths[i] > sub_max || cnt >= SUB_BUFS)) {
                 p->sub.push_back(i);
                 maxdecl = std::max(maxdecl, decl);
                 max_sub_blocks = std::max(max_sub_blocks, blocks);
@@ -1516,7 +1505,7 @@ extern "C" int xc_encode_plan_create_sub(xc_cache *c, const uint64_t *lengths, u
             p->scan_unit = o[1];
             if (max_sub_blocks / ((uint64_t)o[0] * o[1]) >= waves) break;
         }
-        const char *e = getenv("XC_CHUNK_BLOCKS");  // (tuning experiments: force a chunk length, unit 1)
+        const char *e = getenv("XC_CHUNK_BLOCKS");  // (deployment tuning: force a chunk length, unit 1)
         if (e && atoi(e) >= 1 && atoi(e) <= (int)CHUNK_BLOCKS) {
             p->chunk_len = (uint32_t)atoi(e) * XC_SEG;
             p->scan_unit = 1;
@@ -1691,19 +1680,9 @@ extern "C" int xc_encode_plan_create_sub(xc_cache *c, const uint64_t *lengths, u
     // the declaration set's level-2 filter is the combined one (cache | declarations): every
     // declaration insert lands there directly, and the declaration-layer scans test a superset
     P.dset.l2 = p->d_l2mix;
-    if (!c->ctx->side) {
-        // XC_STREAM_PRIO (experiments): 1 = the context stream high, the side stream low; 2 = the
-        // side stream (block hashing) high: cfg5 A/B 869-870 -> 874-875 GiB/s, but a stream of
-        // another priority on the device slows the decoder's streams (cfg4 1370 -> 826 GiB/s with
-        // an idle high-priority side stream, profiles/r05/ab/side_priority_r5s.txt): not the default
-        const char *e = getenv("XC_STREAM_PRIO");
-        const int mode = e ? atoi(e) : 0;
-        int lo = 0, hi = 0;
-        if (mode && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
-            HIPCHK(hipStreamCreateWithPriority(&c->ctx->side, hipStreamNonBlocking, mode == 1 ? lo : hi));
-        else
-            HIPCHK(hipStreamCreateWithFlags(&c->ctx->side, hipStreamNonBlocking));
-    }
+    // (the side stream at the default priority too: at the highest, cfg5 869-870 -> 874-875 GiB/s but
+    // the decoder's streams ran slower beside it, cfg4 1370 -> 826, profiles/r05/ab/side_priority_r5s.txt)
+    if (!c->ctx->side) HIPCHK(hipStreamCreateWithFlags(&c->ctx->side, hipStreamNonBlocking));
     p->hs = c->ctx->side;
     HIPCHK(hipEventCreateWithFlags(&p->ev_start, hipEventDisableTiming));
     p->ev_hash.assign(p->sub.size(), nullptr);
@@ -1879,15 +1858,7 @@ static int hits_enqueue(xc_plan *p)
     HIPCHK(hipStreamWaitEvent(c->hl_stream, c->hl_packed, 0));
     // the slot to pinned memory by the copy engine (no compute units: a kernel writing only the
     // filled words across PCIe took ~250 us of CU slots beside the next run, cfg5)
-    // (XC_HITS_KERNEL=1: that kernel, for A/B)
-    static const bool hk = getenv("XC_HITS_KERNEL") && atoi(getenv("XC_HITS_KERNEL"));
-    if (hk) {
-        hipLaunchKernelGGL(k_hits_out, dim3(std::min<uint32_t>((p->nb + 3) / 4, 64u)), dim3(256), 0, c->hl_stream,
-                           (const uint64_t *)sl.d, sl.hd, (const uint32_t *)sl.dtb, p->nb);
-        HIPCHK(hipGetLastError());
-    } else {
-        HIPCHK(hipMemcpyAsync(sl.h, sl.d, (size_t)p->hit_base[p->nb] * 8, hipMemcpyDeviceToHost, c->hl_stream));
-    }
+    HIPCHK(hipMemcpyAsync(sl.h, sl.d, (size_t)p->hit_base[p->nb] * 8, hipMemcpyDeviceToHost, c->hl_stream));
     HIPCHK(hipEventRecord(sl.ev, c->hl_stream));
     sl.copying = true;
     sl.host_sync = false;
@@ -2285,13 +2256,13 @@ static hipError_t pass_state(xc_plan *p)
     return published(p) ? hipSuccess : hipStreamQuery(p->cache->ctx->stream);
 }
 
-// A publication poll asks the stream whether it drained only after XC_QUERY_US (2000) us without a
+// A publication poll asks the stream whether it drained only after 2000 us without a
 // publication (checked every 256 polls): hipStreamQuery on a stream with kernels in flight enqueues
 // a marker behind them, whose release leaves the device idle for ~6 us before the next kernel (the
 // decoder's emit -> the next restore, cfg4).  A pass that publishes nothing still ends the poll.
 extern "C" bool xc__query_due(int64_t *t0)
 {
-    static const int64_t lim = getenv("XC_QUERY_US") ? atoll(getenv("XC_QUERY_US")) * 1000 : 2000000;
+    static const int64_t lim = abl_env("XC_QUERY_US") ? atoll(abl_env("XC_QUERY_US")) * 1000 : 2000000;
     const int64_t t = std::chrono::duration_cast<std::chrono::nanoseconds>(
                           std::chrono::steady_clock::now().time_since_epoch()).count();
     if (*t0 == 0) *t0 = t;
@@ -2371,12 +2342,12 @@ static int launch_scan(xc_plan *p, const Layer &L, const DevSet &set, uint32_t c
     if (p->timing) p->ktimes.scan_bytes += p->chunk_bytes[ck_hi] - p->chunk_bytes[ck_lo];
     uint32_t need = (ck_hi - ck_lo + SCAN_WAVES * p->scan_unit - 1) / (SCAN_WAVES * p->scan_unit);
     uint32_t grid = std::min<uint32_t>(need, (uint32_t)ctx->n_cu);
-    // XC_SCAN_GRID=n (tuning experiments): at most n scan workgroups, the other CUs left to the
+    // XC_SCAN_GRID=n (-DXC_ABLATIONS builds): at most n scan workgroups, the other CUs left to the
     // kernels of other streams
-    static const uint32_t grid_cap = getenv("XC_SCAN_GRID") ? (uint32_t)atoi(getenv("XC_SCAN_GRID")) : 0u;
+    static const uint32_t grid_cap = abl_env("XC_SCAN_GRID") ? (uint32_t)atoi(abl_env("XC_SCAN_GRID")) : 0u;
     if (grid_cap) grid = std::min(grid, grid_cap);
-    // XC_SCAN_ABLATION=m (timing experiments only: results are wrong) runs k_scan<m> in the pipeline
-    static const int abl = getenv("XC_SCAN_ABLATION") ? atoi(getenv("XC_SCAN_ABLATION")) : 0;
+    // XC_SCAN_ABLATION=m (-DXC_ABLATIONS builds, timing only: results are wrong) runs k_scan<m>
+    static const int abl = abl_env("XC_SCAN_ABLATION") ? atoi(abl_env("XC_SCAN_ABLATION")) : 0;
     auto kern = abl == 1 ? k_scan<1> : abl == 2 ? k_scan<2> : abl == 3 ? k_scan<3> : abl == 4 ? k_scan<4>
               : abl == 5 ? k_scan<5> : k_scan<0>;
     if (abl) a.mode = (uint32_t)abl;
@@ -2439,14 +2410,14 @@ static int launch_emit(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t jc, uint32
     const bool slots = jc > j0 && jc - j0 <= EMIT_SLOTS_MAX;
     // (the pass's last sub-batch publishes the control words: from the emit when it takes the
     // slots, else from k_alloc; the non-slot emit never reads ctl_host)
-    const char *abl = getenv("XC_ABL_EMIT");  // (read per launch: a diagnostic run sets it late)
+    // (XC_ABL_EMIT, -DXC_ABLATIONS builds: read per launch, a diagnostic run sets it late)
+    const char *abl = abl_env("XC_ABL_EMIT");
     // the cache enters in k_insert for large sub-batches (cfg5's 8192 buffers: A/B 751 -> 766 GiB/s);
     // below that the launch costs more than it saves (cfg3's 4096: 650 -> 634), and they stay in
-    // the emit workgroups (XC_EMIT_INSERT=1: always there, as in round 2)
-    static const bool in_emit = getenv("XC_EMIT_INSERT") && atoi(getenv("XC_EMIT_INSERT"));
+    // the emit workgroups
     const uint32_t ab = abl ? (uint32_t)atoi(abl) : 0u;
     EmitArgs e{p->P, j0, jc, gate_sb, p->emit_ctl_host, p->P.sb_count + sb, p->emit_pub_final, ab,
-               !slots && !in_emit && jc - j0 >= INSERT_SPLIT_MIN ? 1u : 0u};
+               !slots && jc - j0 >= INSERT_SPLIT_MIN ? 1u : 0u};
     if (!slots) {
         hipLaunchKernelGGL(k_alloc, dim3(1), dim3(1024), 0, s, e);
         HIPCHK(hipGetLastError());
@@ -2461,47 +2432,11 @@ static int launch_emit(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t jc, uint32
     const bool wide = (uint64_t)(jc - j0) * EMIT_WAVES < (uint64_t)p->cache->ctx->n_cu * 16u;
     auto kern = wide ? (slots ? k_emit<16, true> : k_emit<16, false>)
                      : (slots ? k_emit<EMIT_WAVES, true> : k_emit<EMIT_WAVES, false>);
-    // XC_EMIT_OWN=1 (experiments): the asynchronous pass's large sub-batches on the emit stream,
-    // after the cache inserts, beside the next sub-batch's predictions and anchor scan (cfg5 A/B
-    // -1.3 %: the emit's bandwidth beside the side stream's block hashing; not the default)
-    static const bool emit_main = !(getenv("XC_EMIT_OWN") && atoi(getenv("XC_EMIT_OWN")));
-    // (timing runs keep it in order: the per-kernel spans are of serialized launches)
-    // (a run of one sub-batch has no next sub-batch to overlap: and its pass may be captured as a graph)
-    const bool own = !slots && gate_sb != NONE && !p->host_path && !emit_main && !p->timing && p->sub.size() > 2;
-    hipStream_t es = s;
-    if (own) {
-        if (!p->es) {
-            HIPCHK(hipStreamCreateWithFlags(&p->es, hipStreamNonBlocking));
-            HIPCHK(hipEventCreateWithFlags(&p->ev_ins, hipEventDisableTiming));
-            HIPCHK(hipEventCreateWithFlags(&p->ev_emit, hipEventDisableTiming));
-        }
-        HIPCHK(hipEventRecord(p->ev_ins, s));
-        HIPCHK(hipStreamWaitEvent(p->es, p->ev_ins, 0));
-        es = p->es;
-    }
-    hipLaunchKernelGGL(kern, dim3(jc - j0), dim3(64 * (wide ? 16 : EMIT_WAVES)), 0, es, e);
+    // (in the context stream's order: on a stream of its own, beside the next sub-batch's predictions
+    // and anchor scan, cfg5 measured -1.3 %)
+    hipLaunchKernelGGL(kern, dim3(jc - j0), dim3(64 * (wide ? 16 : EMIT_WAVES)), 0, s, e);
     HIPCHK(hipGetLastError());
-    if (own) {
-        HIPCHK(hipEventRecord(p->ev_emit, es));
-        p->emit_open = true;
-    }
     return XC_OK;
-}
-
-// The main stream waits for the emit on the emit stream (its segments' bytes, its wire bytes).
-static int join_emit(xc_plan *p)
-{
-    if (!p->emit_open) return XC_OK;
-    HIPCHK(hipStreamWaitEvent(p->cache->ctx->stream, p->ev_emit, 0));
-    p->emit_open = false;
-    return XC_OK;
-}
-
-// XC_BH_GATED=1 (experiments): side-stream block hashing one sub-batch ahead, as in round 2
-static bool bh_gated()
-{
-    static const bool g = getenv("XC_BH_GATED") && atoi(getenv("XC_BH_GATED"));
-    return g;
 }
 
 // Predicted declarations (aligned blocks absent from the cache), then one scan of every
@@ -2519,26 +2454,23 @@ static int enqueue_block_hash(xc_plan *p, uint32_t k, hipEvent_t after, hipStrea
     const uint32_t g0 = p->grp_base[p->sub[k]], g1 = p->grp_base[p->sub[k + 1]];
     // a range of block groups; on the side stream (sub-batch k - 1 on the main stream) the block
     // compares against the entries complete when k - 1 started
-    static const int bh_nt = getenv("XC_BH_NT") ? atoi(getenv("XC_BH_NT")) : 0;
     // (chained hashing may run while the main stream is several sub-batches behind: its compares
-    // take the entries complete at the run's start; gated, those complete when k - 1 started)
-    // XC_ABL_BH=m (timing ablations of the block hashing, read per launch: bench.py --diag-env sets
-    // it for the diagnostic steps only; the results are wrong): 2 no anchors, 4 no records, 8 no G tile
-    const char *abl_bh = getenv("XC_ABL_BH");
-    const int nt_abl = bh_nt | (abl_bh ? atoi(abl_bh) & ~1 : 0);
-    DeclArgs d{p->P, g0, g1, limit ? limit : side && k > 0 ? p->P.sb_count + (bh_gated() ? k - 1 : 0) : nullptr,
+    // take the entries complete at the run's start)
+    // XC_ABL_BH=m (-DXC_ABLATIONS builds: timing ablations of the block hashing, read per launch,
+    // bench.py --diag-env sets it for the diagnostic steps only; the results are wrong): 2 no anchors,
+    // 4 no records, 8 no G tile
+    const char *abl_bh = abl_env("XC_ABL_BH");
+    const int nt_abl = abl_bh ? atoi(abl_bh) & ~1 : 0;
+    DeclArgs d{p->P, g0, g1, limit ? limit : side && k > 0 ? p->P.sb_count : nullptr,
                nt_abl, p->shadow, limit_cap};
-    // XC_ABL_SKIP_BLOCKHASH=1 (timing experiments only, valid when every run reads the same input):
+    // XC_ABL_SKIP_BLOCKHASH=1 (-DXC_ABLATIONS builds, timing only, valid when every run reads the same input):
     // the side stream's block hashing after the plan's first run is skipped
-    static const bool skip = getenv("XC_ABL_SKIP_BLOCKHASH") && atoi(getenv("XC_ABL_SKIP_BLOCKHASH"));
+    static const bool skip = abl_flag("XC_ABL_SKIP_BLOCKHASH");
     if (g1 > g0 && !(skip && side && p->runs_done > 0)) {
         KSpan span(p, XC_K_BLOCKHASH, st);
         auto kern = predict ? (p->anc_run ? k_blockhash<true, true> : k_blockhash<true, false>)
                             : (p->anc_run ? k_blockhash<false, true> : k_blockhash<false, false>);
-        // XC_BH_LDS=n (experiments): n KiB of dynamic LDS per side-stream block-hashing workgroup,
-        // capping how many share a CU with the main stream's kernels
-        static const uint32_t bh_lds = getenv("XC_BH_LDS") ? (uint32_t)atoi(getenv("XC_BH_LDS")) << 10 : 0u;
-        hipLaunchKernelGGL(kern, dim3((g1 - g0 + 3) / 4), dim3(256), side ? bh_lds : 0u, st, d);
+        hipLaunchKernelGGL(kern, dim3((g1 - g0 + 3) / 4), dim3(256), 0, st, d);
         HIPCHK(hipGetLastError());
     }
     if (side) HIPCHK(hipEventRecord(p->ev_hash[k], st));
@@ -2591,11 +2523,10 @@ static int launch_first_round(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t s1,
     // the next sub-batch's block hashes run beside this scan (memory-bound beside LDS/L2-bound)
     // every later sub-batch's blocks back to back on the side stream, the first after this
     // sub-batch's predictions: the side stream never waits for the main one, whose sub-batch k then
-    // rarely waits for k's hashes (XC_BH_GATED=1: one sub-batch ahead, each hashed beside the scan
-    // before it, as in round 2)
+    // rarely waits for k's hashes (round 2 hashed one sub-batch ahead, beside the scan before it)
     if (chain) {
         if (!go_early) HIPCHK(hipEventRecord(p->ev_go[sb], s));
-        const uint32_t last = bh_gated() ? sb + 1 : (uint32_t)p->sub.size() - 2;
+        const uint32_t last = (uint32_t)p->sub.size() - 2;
         for (uint32_t k = sb + 1; k <= last; k++)
             if ((rc = enqueue_block_hash(p, k, k == sb + 1 ? p->ev_go[sb] : nullptr, p->hs))) return rc;
     }
@@ -2604,8 +2535,7 @@ static int launch_first_round(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t s1,
     } else if ((rc = launch_scan(p, p->P.S, p->P.cache, ck_lo, ck_hi, &p->P.dset, shadow))) {
         return rc;
     }
-    // (the previous sub-batch's emit wrote the segments this resolve may compare)
-    if ((rc = join_emit(p))) return rc;
+    // (the previous sub-batch's emit, earlier in the stream, wrote the segments this resolve may compare)
     if ((rc = launch_resolve(p, p->P.S, 2, ck_lo, ck_hi))) return rc;
     return launch_walk_round(p, j0, s1, 0, shadow);
 }
@@ -2845,11 +2775,9 @@ static int encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64
     // complete when the previous run's last sub-batch started: immutable since, nothing else having
     // written the cache; a restore in between only unmaps later entries, which the predictions then
     // do not name)
-    // (XC_NO_EARLY=1: A/B experiments)
-    static const bool no_early = getenv("XC_NO_EARLY") && atoi(getenv("XC_NO_EARLY"));
     const bool early = p->input_ready && p->early_ok && c->last_plan == p && p->sub.size() > 2 &&
-                       !p->P.stream_st && !p->host_path && !use_graph(p) && !p->timing && !no_early;
-    static const bool dbg_early = getenv("XC_DEBUG_EARLY") && atoi(getenv("XC_DEBUG_EARLY"));
+                       !p->P.stream_st && !p->host_path && !use_graph(p) && !p->timing;
+    static const bool dbg_early = abl_flag("XC_DEBUG_EARLY");
     if (dbg_early)
         fprintf(stderr, "early=%d input_ready=%d early_ok=%d last=%d nsub=%zu stream=%d host=%d graph=%d timing=%d\n",
                 (int)early, (int)p->input_ready, (int)p->early_ok, (int)(c->last_plan == p), p->sub.size() - 1,
@@ -2861,8 +2789,6 @@ static int encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64
     // which k_blockpredict, after it, finds too)
     const uint32_t floor = c->removed_floor;
     c->removed_floor = 0xFFFFFFFFu;
-    // (XC_EARLY_ALL=0, A/B: only sub-batch 0 ahead, the later ones chained after its set clear)
-    static const bool early_all = !(getenv("XC_EARLY_ALL") && !atoi(getenv("XC_EARLY_ALL")));
     uint32_t hashed = 0;
     if (early) {
         // every sub-batch's blocks ahead, back to back on the side stream (their compares take the
@@ -2870,7 +2796,7 @@ static int encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64
         // the main stream then records no start event for them (an event between two of its
         // kernels idles the device ~6 us) and sub-batch 1's hashing starts as soon as 0's ends
         const uint32_t *lim = p->P.sb_count + (p->sub.size() - 2);
-        const uint32_t upto = early_all ? (uint32_t)p->sub.size() - 1 : 1u;
+        const uint32_t upto = (uint32_t)p->sub.size() - 1;
         for (uint32_t k = 0; k < upto; k++)
             // (sub-batch 0 after the previous run's sub-batch 0 emit; the later ones, chained behind it,
             // after the previous run's last emit: its k_insert / k_emit read those block arrays after the
@@ -2907,17 +2833,13 @@ static int encode_submit(xc_plan *p, const uint8_t *d_in, uint8_t *d_out, uint64
             p->emit_pub_final = 0;
             if (rc) return rc;
         }
-        if ((rc = join_emit(p))) return rc;  // (the pass's results complete in the context stream's order)
         if (p->rec_sb0) HIPCHK(hipEventRecord(p->ev_last, s));  // (the next run's early hashing of sub-batches >= 1)
         if (!pub) HIPCHK(hipMemcpyAsync(p->h_ctl, p->P.ctl, CTL_WORDS * 4, hipMemcpyDeviceToHost, s));
         if ((rc = record_ctl(p))) return rc;
         // the tail check right behind the pass (after its event: the host's wait does not cover it),
-        // so that it does not wait for the host's turn (XC_TAIL_LATE=1: from encode_finish, as before)
-        static const bool late = getenv("XC_TAIL_LATE") && atoi(getenv("XC_TAIL_LATE"));
-        if (!late) {
-            if ((rc = launch_tailcheck(p))) return rc;
-            p->tail_enqueued = true;
-        }
+        // so that it does not wait for the host's turn
+        if ((rc = launch_tailcheck(p))) return rc;
+        p->tail_enqueued = true;
     }
     p->inflight = true;
     c->busy = p;
@@ -2934,7 +2856,8 @@ static int launch_tailcheck(xc_plan *p)
     // a small grid (the tail is a few buffers: ~100 blocks on cfg5): the next run's early block hashing
     // fills the CUs meanwhile, and each workgroup of a wide grid waits for a slot, even one with
     // nothing to do (1024 workgroups: 340 us per cfg5 step instead of 30)
-    static const uint32_t grid = getenv("XC_TAIL_GRID") ? (uint32_t)atoi(getenv("XC_TAIL_GRID")) : 64u;
+    // (XC_TAIL_GRID, -DXC_ABLATIONS builds: another grid)
+    static const uint32_t grid = abl_env("XC_TAIL_GRID") ? (uint32_t)atoi(abl_env("XC_TAIL_GRID")) : 64u;
     hipLaunchKernelGGL(k_tailcheck, dim3(std::max(1u, grid)), dim3(256), 0, s, p->P, p->nb, p->d_tcnt, p->d_tlist);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_tailfinal, dim3(std::min<uint32_t>(p->nb, std::max(1u, grid))), dim3(64), 0, s, p->P, p->nb,
@@ -2945,7 +2868,7 @@ static int launch_tailcheck(xc_plan *p)
 
 static bool dbg_finish()
 {
-    static const bool d = getenv("XC_DEBUG_EARLY") && atoi(getenv("XC_DEBUG_EARLY"));
+    static const bool d = abl_flag("XC_DEBUG_EARLY");
     return d;
 }
 
@@ -2972,7 +2895,7 @@ static int encode_finish(xc_plan *p)
         if (ctl[CTL_ERROR]) break;
         p->stats.redone++;
         if (ctl[CTL_AFAIL]) {
-            static const bool dbg_af = getenv("XC_DEBUG_AFAIL") && atoi(getenv("XC_DEBUG_AFAIL"));
+            static const bool dbg_af = abl_flag("XC_DEBUG_AFAIL");
             if (dbg_af) fprintf(stderr, "anchor fallback: sub-batch %zu, flags %u\n", si, ctl[CTL_AFAIL]);
             // the anchor index cannot decide this sub-batch: the exact scan redoes it, and the
             // rest of the run (a collision or an anchorless segment may concern later ones too)
@@ -2989,7 +2912,6 @@ static int encode_finish(xc_plan *p)
         // the rest asynchronously again: k_alloc's gate stops at the next sub-batch needing the host
         for (size_t k = si; k < nsub; k++)
             if ((rc = encode_sub_async(p, (uint32_t)k))) return rc;
-        if ((rc = join_emit(p))) return rc;
         if ((rc = read_ctl(p, ctl))) return rc;
         fresh = true;
     }
@@ -3019,7 +2941,7 @@ static int encode_finish(xc_plan *p)
             HIPCHK(hipMemcpyAsync(&bad, c->ctl + CTL_ANCLESS, 4, hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));
             if (bad) c->anc_bad = std::min(c->anc_bad, ~bad);
-            static const bool dbg_anc = getenv("XC_DEBUG_ANC") && atoi(getenv("XC_DEBUG_ANC"));
+            static const bool dbg_anc = abl_flag("XC_DEBUG_ANC");
             if (dbg_anc && bad && ~bad < c->dev_cap) {
                 std::vector<uint8_t> sb(XC_SEG);
                 uint64_t key = 0;
@@ -3046,8 +2968,9 @@ static int encode_finish(xc_plan *p)
         }
         // its lookup hits, for the recent window (none: no REF, no collision recorded, no tail
         // check behind the run that could record one)
-        // (XC_NO_HITS=1: none at all, a timing diagnostic only: the window model is then wrong)
-        static const bool no_hits = getenv("XC_NO_HITS") && atoi(getenv("XC_NO_HITS"));
+        // (XC_NO_HITS=1, -DXC_ABLATIONS builds: none at all, a timing diagnostic only: the window model
+        // is then wrong)
+        static const bool no_hits = abl_flag("XC_NO_HITS");
         if (!no_hits && (ctl[CTL_NREF] || ctl[CTL_COLLS] || p->anc_any)) {
             if ((rc = hits_flush(c))) return rc;
             // (a small host-path run: into pinned memory now, its host's synchronisation follows)
