@@ -10,6 +10,7 @@
 #   trace[:ARGS]   rocprofv3 --kernel-trace --stats over bench.py ARGS (default: --no-cpu --no-e2e --no-live --steps 10)
 #   leg:LEG[,N]    python bench.py --only LEG --steps N (default 200) -> leg_LEG.json
 #   legtrace:LEG   rocprofv3 --kernel-trace over bench.py --only LEG --steps 40 -> timeline_LEG.txt
+#   steptrace      rocprofv3 --kernel-trace of cfg5 production steps (--tail-steps 3) -> step_timeline.txt, stats csv
 #   ranks          bench.py --total 32768 / 16384 / 8192 / 4096 (one rank's shard of the 1/2/4/8-GPU job on this GPU)
 #   pmc            FETCH_SIZE and WRITE_SIZE passes (separate runs) -> pmc_traffic_cfg5.json (stamped)
 #   pmcinst        two SQ counter passes (VALU / LDS / waits) over one cfg5 step -> pmc_inst/
@@ -70,6 +71,14 @@ for step in "$@"; do
             -- python3 bench.py --only $arg --steps 40 > "$out/lt_$arg.log" 2>&1 || die "legtrace $arg" $? "$out/lt_$arg.log"
         python3 tools/timeline.py "$out/lt_$arg/run_kernel_trace.csv" 40 > "$out/timeline_$arg.txt" || die timeline $? "$out/lt_$arg.log"
         echo "legtrace $arg ok" ;;
+    steptrace)
+        timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/st" -o run \
+            -- python3 bench.py --no-cpu --no-e2e --no-live --no-legs --no-decode --steps 6 --tail-steps 3 \
+            > "$out/steptrace.log" 2>&1 || die steptrace $? "$out/steptrace.log"
+        python3 tools/timeline.py "$out/st/run_kernel_trace.csv" 75 > "$out/step_timeline.txt" || die timeline $? "$out/steptrace.log"
+        cp "$out/st/run_kernel_stats.csv" "$out/step_kernel_stats.csv"
+        rm -rf "$out/st"
+        tail -4 "$out/step_timeline.txt" ;;
     ranks)
         for tot in 32768 16384 8192 4096; do
             timeout -k 10 300 python bench.py --no-cpu --no-e2e --no-legs --no-live --no-decode --steps 20 --total $tot \

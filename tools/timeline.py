@@ -18,3 +18,15 @@ for r in rows:
     prev_end[q] = e
     name = r["Kernel_Name"].split("(")[0].replace("void xc::", "").replace("xc::", "")
     print(f"q{q:>2} {(s - t0) / 1e3:9.1f} {(e - s) / 1e3:8.1f} gap {gap:7.1f}  {name[:60]}")
+# step lengths (restore to restore: the k_undo_known launches) and each queue's busy time per step
+starts = [int(r["Start_Timestamp"]) for r in rows if "k_undo_known" in r["Kernel_Name"]]
+if len(starts) >= 2:
+    print("# step lengths (restore to restore), us:", ", ".join(f"{(b - a) / 1e3:.1f}" for a, b in zip(starts, starts[1:])))
+    for a, b in zip(starts, starts[1:]):
+        busy = {}
+        for r in rows:
+            s, e = max(int(r["Start_Timestamp"]), a), min(int(r["End_Timestamp"]), b)
+            if e > s:
+                q = r.get("Queue_Id", "?")
+                busy[q] = busy.get(q, 0) + e - s
+        print("# busy per queue in the step, us:", ", ".join(f"q{q} {v / 1e3:.1f}" for q, v in sorted(busy.items())))

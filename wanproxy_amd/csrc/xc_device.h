@@ -344,10 +344,11 @@ __device__ __forceinline__ uint4 load16_unaligned(const uint8_t *p)
 #endif
 struct PayloadRegs {
     uint4 a0, a1;  // slot-aligned chunks: src + 16 l, src + 1024 + 16 l
-    uint4 b0, b1;  // wire-aligned chunks
     uint32_t hb, tb;
 };
 
+// The loads only (the wire-aligned chunks are made from a0 / a1 at the store, so that the registers
+// of a payload in flight are its 32 bytes per lane, not twice that: the emit's occupancy).
 __device__ __forceinline__ void payload_load(const uint8_t *src, const uint8_t *out, PayloadRegs &r)
 {
     const uint32_t l = lane_id();
@@ -360,40 +361,44 @@ __device__ __forceinline__ void payload_load(const uint8_t *src, const uint8_t *
         r.a0 = load16_unaligned(src + 16u * l);
         r.a1 = load16_unaligned(src + 1024u + 16u * l);
     }
-    r.b0 = r.a0;
-    r.b1 = r.a1;
-    if (head) {
-        // the wire-aligned chunk of lane l is bytes head .. head + 15 of (chunk l, chunk l + 1): the
-        // next lane's words by a DPP wave shift (lane 63's successor: lane 0 of the second half),
-        // then a funnel by head bytes; no second read of src
-        const uint32_t c0[4] = {r.a0.x, r.a0.y, r.a0.z, r.a0.w}, c1[4] = {r.a1.x, r.a1.y, r.a1.z, r.a1.w};
-        uint32_t n0[4], n1[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t first1 = readlane(c1[k], 0);
-            n0[k] = (uint32_t)__builtin_amdgcn_update_dpp((int)first1, (int)c0[k], 0x130, 0xf, 0xf, false);  // wave_shl:1
-            n1[k] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c1[k], 0x130, 0xf, 0xf, false);
-        }
-        const uint32_t dh = head >> 2, bh = 8u * (head & 3u);
-        auto fun = [&](const uint32_t (&c)[4], const uint32_t (&nx)[4]) {
-            uint32_t d[8] = {c[0], c[1], c[2], c[3], nx[0], nx[1], nx[2], nx[3]};
-            uint32_t o[5];
-#pragma unroll
-            for (int k = 0; k < 5; k++)  // dwords dh .. dh + 4 of the 32 bytes (dh uniform)
-                o[k] = dh == 0 ? d[k] : dh == 1 ? d[k + 1] : dh == 2 ? d[k + 2] : d[min(k + 3, 7)];
-            uint4 v;
-            v.x = bh ? (o[0] >> bh) | (o[1] << (32u - bh)) : o[0];
-            v.y = bh ? (o[1] >> bh) | (o[2] << (32u - bh)) : o[1];
-            v.z = bh ? (o[2] >> bh) | (o[3] << (32u - bh)) : o[2];
-            v.w = bh ? (o[3] >> bh) | (o[4] << (32u - bh)) : o[3];
-            return v;
-        };
-        r.b0 = fun(c0, n0);
-        r.b1 = fun(c1, n1);
-    }
     const uint32_t t0 = head + 16u * nbody;
     r.hb = l < head ? src[l] : 0u;
     r.tb = t0 + l < XC_SEG ? src[t0 + l] : 0u;
+}
+
+// The wire-aligned chunks of a payload for a wire address with `head` bytes to its next 16-byte
+// boundary: lane l's chunk is bytes head .. head + 15 of (chunk l, chunk l + 1), the next lane's words
+// by a DPP wave shift (lane 63's successor: lane 0 of the second half), then a funnel by head bytes;
+// no second read of src.
+__device__ __forceinline__ void payload_wire(const PayloadRegs &r, uint32_t head, uint4 &b0, uint4 &b1)
+{
+    b0 = r.a0;
+    b1 = r.a1;
+    if (!head) return;
+    const uint32_t c0[4] = {r.a0.x, r.a0.y, r.a0.z, r.a0.w}, c1[4] = {r.a1.x, r.a1.y, r.a1.z, r.a1.w};
+    uint32_t n0[4], n1[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t first1 = readlane(c1[k], 0);
+        n0[k] = (uint32_t)__builtin_amdgcn_update_dpp((int)first1, (int)c0[k], 0x130, 0xf, 0xf, false);  // wave_shl:1
+        n1[k] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c1[k], 0x130, 0xf, 0xf, false);
+    }
+    const uint32_t dh = head >> 2, bh = 8u * (head & 3u);
+    auto fun = [&](const uint32_t (&c)[4], const uint32_t (&nx)[4]) {
+        uint32_t d[8] = {c[0], c[1], c[2], c[3], nx[0], nx[1], nx[2], nx[3]};
+        uint32_t o[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++)  // dwords dh .. dh + 4 of the 32 bytes (dh uniform)
+            o[k] = dh == 0 ? d[k] : dh == 1 ? d[k + 1] : dh == 2 ? d[k + 2] : d[min(k + 3, 7)];
+        uint4 v;
+        v.x = bh ? (o[0] >> bh) | (o[1] << (32u - bh)) : o[0];
+        v.y = bh ? (o[1] >> bh) | (o[2] << (32u - bh)) : o[1];
+        v.z = bh ? (o[2] >> bh) | (o[3] << (32u - bh)) : o[2];
+        v.w = bh ? (o[3] >> bh) | (o[4] << (32u - bh)) : o[3];
+        return v;
+    };
+    b0 = fun(c0, n0);
+    b1 = fun(c1, n1);
 }
 
 // 16-byte store, non-temporal (the wire bytes and the segment store are not read back by this
@@ -419,8 +424,10 @@ __device__ __forceinline__ void payload_store(uint8_t *out, uint8_t *seg, const 
         store16((uint4 *)seg + l, r.a0);
         store16((uint4 *)seg + l + 64u, r.a1);
     }
-    if (l < nbody) store16(out + head + 16u * l, r.b0);
-    if (l + 64u < nbody) store16(out + head + 1024u + 16u * l, r.b1);
+    uint4 b0, b1;
+    payload_wire(r, head, b0, b1);
+    if (l < nbody) store16(out + head + 16u * l, b0);
+    if (l + 64u < nbody) store16(out + head + 1024u + 16u * l, b1);
     if (l < head) out[l] = (uint8_t)r.hb;
     if (t0 + l < XC_SEG) out[t0 + l] = (uint8_t)r.tb;
 }

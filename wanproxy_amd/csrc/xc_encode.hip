@@ -1895,11 +1895,12 @@ __device__ __forceinline__ void ctl_publish(const EmitArgs &a)
 // cache slot idx, one lane per token, the whole wave present: the hash tables (undo record) and, on
 // an anchor run, the anchor index (an aligned block's key from k_blockhash, any other segment's
 // computed here, wave-wide, one at a time).
+template <bool ANC>
 __device__ __forceinline__ void enter_tokens(const PlanDev &P, uint32_t b, const uint8_t *base, uint32_t tb,
                                              uint32_t t, bool ext, uint32_t idx)
 {
     const uint32_t l = lane_id();
-    if (P.anc_run) {
+    if (ANC && P.anc_run) {
         const uint32_t sg = ext ? P.tok_seg[tb + t] : 0u;
         uint64_t key = ext && (sg & (XC_SEG - 1u)) == 0u ? P.blk_anc[P.blk_base[b] + sg / XC_SEG] : ANC_NONE;
         // (an aligned block without a level-0 anchor too: its key of a later level)
@@ -1937,6 +1938,8 @@ __device__ __forceinline__ void enter_tokens(const PlanDev &P, uint32_t b, const
 // The cache enters of buffers [j0, j1) (a sub-batch without in-emit slots), one wave per buffer, so
 // that every insert of the sub-batch is in flight at once instead of on one wave of each emit
 // workgroup (the emit's critical path): after k_alloc (its slots), before k_emit.
+// ANC: the run indexes anchors (a run on the exact scan compiles without that path: 22 VGPRs, not 86)
+template <bool ANC>
 __global__ __launch_bounds__(256) void k_insert(EmitArgs a)
 {
     if (aborted(a.P)) return;
@@ -1952,17 +1955,22 @@ __global__ __launch_bounds__(256) void k_insert(EmitArgs a)
         const uint32_t t = t0 + l;
         const bool ext = t < n && P.tok_op[tb + t] == OP_EXTRACT;
         const uint64_t em = ballot(ext);
-        enter_tokens(P, b, base, tb, t, ext, slot0 + carry + mbcnt(em));
+        enter_tokens<ANC>(P, b, base, tb, t, ext, slot0 + carry + mbcnt(em));
         carry += (uint32_t)__popcll(em);
     }
 }
+template __global__ void k_insert<false>(EmitArgs);
+template __global__ void k_insert<true>(EmitArgs);
 
 // SLOTS: k_alloc's work too (sub-batches of <= EMIT_SLOTS_MAX buffers), with no extra round trip
 // on a workgroup's path: the gate words, the sub-batch's start count (P.sb_count, written by
 // k_clear_set: the cache count does not change before this kernel) and every buffer's buf_next /
 // buf_nref are loaded with the token metadata; this buffer's first slot is the start count plus
 // the buf_next of the buffers before it, and workgroup 0 publishes the totals.
-template <uint32_t EMIT_WAVES, bool SLOTS>
+// INS: the cache enters in this kernel (0: none, k_insert ran before it; 1: enters; 2: enters and
+// anchor keys).  The anchor path alone takes the kernel from 54 to 84 VGPRs (5 instead of 8
+// workgroups of 4 waves per CU), so each launch compiles only what its run needs.
+template <uint32_t EMIT_WAVES, bool SLOTS, int INS>
 __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
 {
     if (emit_aborted(a)) return;
@@ -2060,11 +2068,11 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
     if (SLOTS && threadIdx.x == 0) P.buf_slot[b] = slot0;  // (the tail check's visibility test)
     // XCodecMemoryCache::enter of this buffer's declarations (SLOTS, or k_insert not split off): the
     // wave with the smallest token group (wave 0 did the prefix), one lane per EXTRACT token
-    if (wave == EMIT_WAVES - 1u && !(eabl & 4u) && (SLOTS || !a.split_ins)) {
+    if (INS && wave == EMIT_WAVES - 1u && !(eabl & 4u)) {
         for (uint32_t t0 = 0; t0 < n; t0 += 64u) {
             const uint32_t t = t0 + l;
             const bool ext = t < n && P.tok_op[tb + t] == OP_EXTRACT;
-            enter_tokens(P, b, base, tb, t, ext, ext ? slot0 + ord[t] : 0u);
+            enter_tokens<INS == 2>(P, b, base, tb, t, ext, ext ? slot0 + ord[t] : 0u);
         }
     }
     // wire bytes: wave w takes a contiguous group of tokens, one per lane, so the group's
@@ -2131,10 +2139,16 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
     }
 }
 
-template __global__ void k_emit<4, false>(EmitArgs);
-template __global__ void k_emit<16, false>(EmitArgs);
-template __global__ void k_emit<4, true>(EmitArgs);
-template __global__ void k_emit<16, true>(EmitArgs);
+template __global__ void k_emit<4, false, 0>(EmitArgs);
+template __global__ void k_emit<16, false, 0>(EmitArgs);
+template __global__ void k_emit<4, false, 1>(EmitArgs);
+template __global__ void k_emit<16, false, 1>(EmitArgs);
+template __global__ void k_emit<4, false, 2>(EmitArgs);
+template __global__ void k_emit<16, false, 2>(EmitArgs);
+template __global__ void k_emit<4, true, 1>(EmitArgs);
+template __global__ void k_emit<16, true, 1>(EmitArgs);
+template __global__ void k_emit<4, true, 2>(EmitArgs);
+template __global__ void k_emit<16, true, 2>(EmitArgs);
 
 // One workgroup: cache slots for the declarations of buffers [j0, j1) in buffer order
 // (exclusive prefix of buf_next on top of the current segment count), plus run totals.
@@ -2771,11 +2785,16 @@ __device__ __forceinline__ uint32_t tail_first(const PlanDev &P, uint32_t nb)
 }
 
 // One wave per aligned block of the tail's buffers (window ends [s, s + 2048); block 0: the first
-// window, 2047), all of them in flight across the chip: full hashes by the rolling recurrences of
-// both halves (k_scan's, plus the bits half), the looked-up ends (not a REF's, not in the 2047 ends
-// after one) probed in the cache's full table; collisions into the buffer's scratch list (tcnt,
-// tlist), which k_tailfinal sorts into its records.
-__global__ __launch_bounds__(256) void k_tailcheck(PlanDev P, uint32_t nb, uint32_t *tcnt, uint4 *tlist)
+// window, 2047), all of them in flight across the chip: the low 32 bits of every full hash by the
+// rolling recurrence of the bytes half (k_scan's), the looked-up ends (not a REF's, not in the 2047
+// ends after one) tested in the cache's level-2 filter; only its few positives take the bits half
+// and a probe of the full table; collisions into the buffer's scratch list (tcnt, tlist), which
+// k_tailfinal sorts into its records.
+// At most 96 VGPRs (5 waves per SIMD): the kernel runs behind the run's last emit while the next
+// run's block hashing (128 VGPRs, 4 waves per SIMD) fills the chip on the side stream, and a wave
+// that needs more registers than one block-hashing wave frees waited for the hashing's end (171
+// VGPRs: 342 us per cfg5 step instead of 30, profiles/r05/step_timeline_r5fin.txt).
+__global__ __launch_bounds__(256, 5) void k_tailcheck(PlanDev P, uint32_t nb, uint32_t *tcnt, uint4 *tlist)
 {
     if (aborted(P)) return;  // (enqueued behind a pass that stopped: the host's redo runs it again)
     __shared__ uint32_t refs[4][4];
@@ -2830,6 +2849,8 @@ __global__ __launch_bounds__(256) void k_tailcheck(PlanDev P, uint32_t nb, uint3
             load32_aligned(base + s - XC_SEG + 32u * l, pw);
             load32_aligned(base + s + 32u * l, w);
         }
+        // H = bits << 36 | bytes (xcodec_hash.h:155-174), both halves by k_scan's rolling recurrences,
+        // 16 window ends at a time (registers: the kernel's 96-VGPR bound)
         const BlockSums ps = block_sums(pw, l), cs = block_sums(w, l);
         const BlockSums pf = block_sums_ffs(pw, l), cf = block_sums_ffs(w, l);
         const uint32_t sufA = ps.totA - ps.preA, sufC = ps.totC - ps.preC;
@@ -2838,47 +2859,63 @@ __global__ __launch_bounds__(256) void k_tailcheck(PlanDev P, uint32_t nb, uint3
         const uint32_t fA = pf.totA - pf.preA, fC = pf.totC - pf.preC;
         uint32_t Uf = fA + cf.preA;
         uint32_t Vf = (XC_SEG + 32u * l) * fA - fC + 32u * l * cf.preA - cf.preC;
-        uint64_t h[32];
-        uint32_t fw[32];
-#pragma unroll
-        for (int d = 0; d < 8; d++) {
-#pragma unroll
-            for (int kk = 0; kk < 4; kk++) {
-                const uint32_t ib = (w[d] >> (8 * kk)) & 0xffu, ob = (pw[d] >> (8 * kk)) & 0xffu;
-                const uint32_t fi = ffs8(ib), fo = ffs8(ob);
-                U += ib - ob;
-                V += U + (uint32_t)__mul24((int)ob, -2048);
-                Uf += fi - fo;
-                Vf += Uf - XC_SEG * fo;
-                h[4 * d + kk] = ((uint64_t)((Uf << 16) + Vf) << 36) + ((U << 20) + V);
-            }
-        }
-        // the cache's level-2 filter first (2 MB, L2-resident: every key of the table has its bits,
-        // set_insert), the table only for its few positives
-#pragma unroll
-        for (int t = 0; t < 32; t++) fw[t] = P.cache.l2[(live >> t) & 1u ? l2_word(l2_mix((uint32_t)h[t])) : 0u];
         uint32_t hit = 0;
 #pragma unroll
-        for (int t = 0; t < 32; t++) {
-            if (!((live >> t) & 1u) || !l2_test(fw[t], l2_mix((uint32_t)h[t]))) continue;
-            uint64_t v;
-            if (set_find(P.cache, h[t], &v)) hit |= 1u << t;
+        for (int h16 = 0; h16 < 2; h16++) {
+            uint32_t lo[16], hb[16];
+#pragma unroll
+            for (int d = 0; d < 4; d++) {
+#pragma unroll
+                for (int kk = 0; kk < 4; kk++) {
+                    const uint32_t ib = (w[4 * h16 + d] >> (8 * kk)) & 0xffu, ob = (pw[4 * h16 + d] >> (8 * kk)) & 0xffu;
+                    U += ib - ob;
+                    V += U + (uint32_t)__mul24((int)ob, -2048);
+                    const uint32_t fi = ffs8(ib), fo = ffs8(ob);
+                    Uf += fi - fo;
+                    Vf += Uf - XC_SEG * fo;
+                    lo[4 * d + kk] = (U << 20) + V;
+                    hb[4 * d + kk] = (Uf << 16) + Vf;
+                }
+            }
+            // the cache's level-2 filter first (2 MB, L2-resident: every key of the table has its bits,
+            // set_insert), the table only for its few positives
+            const uint32_t lv = live >> (16 * h16);
+            uint32_t cand = 0;
+#pragma unroll
+            for (int t8 = 0; t8 < 16; t8 += 8) {
+                uint32_t fw[8];
+#pragma unroll
+                for (int t = 0; t < 8; t++) fw[t] = P.cache.l2[(lv >> (t8 + t)) & 1u ? l2_word(l2_mix(lo[t8 + t])) : 0u];
+#pragma unroll
+                for (int t = 0; t < 8; t++)
+                    if (((lv >> (t8 + t)) & 1u) && l2_test(fw[t], l2_mix(lo[t8 + t]))) cand |= 1u << (t8 + t);
+            }
+            while (cand) {
+                const uint32_t t = (uint32_t)__builtin_ctz(cand);
+                cand &= cand - 1u;
+                uint32_t x = lo[0], y = hb[0];
+#pragma unroll
+                for (int tt = 1; tt < 16; tt++) {
+                    x = t == (uint32_t)tt ? lo[tt] : x;
+                    y = t == (uint32_t)tt ? hb[tt] : y;
+                }
+                uint64_t v;
+                if (set_find(P.cache, ((uint64_t)y << 36) + x, &v)) hit |= 1u << (16u * h16 + t);
+            }
         }
         for (;;) {
             const uint64_t m = ballot(hit != 0u);
             if (!m) break;
             const int f = __ffsll((unsigned long long)m) - 1;
             const uint32_t t = (uint32_t)__builtin_ctz(readlane(hit, f));
-            uint64_t hh = h[0];
-#pragma unroll
-            for (int tt = 1; tt < 32; tt++) hh = t == (uint32_t)tt ? h[tt] : hh;
-            hh = readlane64(hh, f);
             if ((int)l == f) hit &= hit - 1u;
+            const uint32_t q = readlane(q0, f) + t;
+            const uint8_t *win = base + q - (XC_SEG - 1u);
+            const uint64_t hh = wave_window_hash(win);  // (the hit's full hash again, wave-wide: rare)
             uint64_t v = 0;
             if (set_find(P.cache, hh, &v)) {
-                const uint32_t q = readlane(q0, f) + t, vv = uniform((uint32_t)v);
+                const uint32_t vv = uniform((uint32_t)v);
                 if (!tail_visible(P, b, q, vv)) continue;
-                const uint8_t *win = base + q - (XC_SEG - 1u);
                 if (wave_equal2048(win, seg_at(P.segs, vv))) continue;  // (the walk's REF)
                 if (l == 0) {
                     const uint32_t kq = atomicAdd(&tcnt[b], 1u);

@@ -313,7 +313,7 @@ struct PackArgs {
 constexpr uint32_t ERR_PACK_CAP = 8;
 
 template <int MODE> __global__ void k_scan(ScanArgs a);
-template <uint32_t NW, bool SLOTS> __global__ void k_emit(EmitArgs a);
+template <uint32_t NW, bool SLOTS, int INS> __global__ void k_emit(EmitArgs a);
 __global__ void k_pack_offsets(PackArgs a);
 __global__ void k_pack_copy(PackArgs a);
 __global__ void k_resolve(ResolveArgs a);
@@ -330,7 +330,7 @@ __global__ void k_tailfinal(PlanDev P, uint32_t nb, uint32_t *tcnt, const uint4 
 __global__ void k_blockpredict(DeclArgs a);
 __global__ void k_or_words(uint4 *dst, const uint4 *a, const uint4 *b, uint32_t n);
 __global__ void k_alloc(EmitArgs a);
-__global__ void k_insert(EmitArgs a);
+template <bool ANC> __global__ void k_insert(EmitArgs a);
 __global__ void k_clear_set(DevSet s, uint32_t n_lo, uint32_t n_full, uint4 *l2mix, const uint4 *cache_l2,
                             uint32_t *fmix, const uint32_t *cache_filt, uint32_t fold, const uint32_t *count,
                             uint32_t *count_out, uint32_t *ctl_zero, AncSet danc, uint4 *amix, const uint4 *cache_afilt);

@@ -2425,13 +2425,18 @@ static int launch_emit(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t jc, uint32
     if (jc <= j0) return XC_OK;
     KSpan span(p, XC_K_EMIT);
     if (e.split_ins && !(ab & 4u)) {
-        hipLaunchKernelGGL(k_insert, dim3((jc - j0 + 3) / 4), dim3(256), 0, s, e);
+        hipLaunchKernelGGL(p->P.anc_run ? k_insert<true> : k_insert<false>, dim3((jc - j0 + 3) / 4), dim3(256), 0, s, e);
         HIPCHK(hipGetLastError());
     }
     // one workgroup per buffer: 4 waves when the buffers alone fill the chip, 16 for few buffers
     const bool wide = (uint64_t)(jc - j0) * EMIT_WAVES < (uint64_t)p->cache->ctx->n_cu * 16u;
-    auto kern = wide ? (slots ? k_emit<16, true> : k_emit<16, false>)
-                     : (slots ? k_emit<EMIT_WAVES, true> : k_emit<EMIT_WAVES, false>);
+    // (the cache enters: in k_insert, or here with or without the anchor index)
+    const int ins = e.split_ins && !(ab & 4u) ? 0 : p->P.anc_run ? 2 : 1;
+    auto kern = wide ? (slots ? (ins == 2 ? k_emit<16, true, 2> : k_emit<16, true, 1>)
+                              : (ins == 0 ? k_emit<16, false, 0> : ins == 2 ? k_emit<16, false, 2> : k_emit<16, false, 1>))
+                     : (slots ? (ins == 2 ? k_emit<EMIT_WAVES, true, 2> : k_emit<EMIT_WAVES, true, 1>)
+                              : (ins == 0 ? k_emit<EMIT_WAVES, false, 0>
+                                          : ins == 2 ? k_emit<EMIT_WAVES, false, 2> : k_emit<EMIT_WAVES, false, 1>));
     // (in the context stream's order: on a stream of its own, beside the next sub-batch's predictions
     // and anchor scan, cfg5 measured -1.3 %)
     hipLaunchKernelGGL(kern, dim3(jc - j0), dim3(64 * (wide ? 16 : EMIT_WAVES)), 0, s, e);
