@@ -11,6 +11,7 @@
 #   leg:LEG[,N]    python bench.py --only LEG --steps N (default 200) -> leg_LEG.json
 #   legtrace:LEG   rocprofv3 --kernel-trace over bench.py --only LEG --steps 40 -> timeline_LEG.txt
 #   steptrace      rocprofv3 --kernel-trace of cfg5 production steps (--tail-steps 3) -> step_timeline.txt, stats csv
+#   calib          tools/fetch_calib under FETCH_SIZE / WRITE_SIZE / TCC request-counter passes -> pmc_calib.json
 #   ranks          bench.py --total 32768 / 16384 / 8192 / 4096 (one rank's shard of the 1/2/4/8-GPU job on this GPU)
 #   pmc            FETCH_SIZE and WRITE_SIZE passes (separate runs) -> pmc_traffic_cfg5.json (stamped)
 #   pmcinst        two SQ counter passes (VALU / LDS / waits) over one cfg5 step -> pmc_inst/
@@ -79,6 +80,17 @@ for step in "$@"; do
         cp "$out/st/run_kernel_stats.csv" "$out/step_kernel_stats.csv"
         rm -rf "$out/st"
         tail -4 "$out/step_timeline.txt" ;;
+    calib)
+        /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 tools/fetch_calib.hip -o /tmp/fetch_calib || die calib-build 1 /dev/null
+        mkdir -p "$out/calib"
+        timeout -k 10 120 /tmp/fetch_calib > "$out/calib/fetch_calib.csv" || die calib-run $? "$out/calib/fetch_calib.csv"
+        i=0
+        for c in FETCH_SIZE WRITE_SIZE "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_BUBBLE_sum"; do
+            i=$((i + 1))
+            timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d "$out/calib/p$i" -o run -- /tmp/fetch_calib \
+                > "$out/calib/p$i.log" 2>&1 || die "calib p$i" $? "$out/calib/p$i.log"
+        done
+        python tools/pmc_calib.py "$out/calib" "$out/pmc_calib.json" || die pmc_calib 1 /dev/null ;;
     ranks)
         for tot in 32768 16384 8192 4096; do
             timeout -k 10 300 python bench.py --no-cpu --no-e2e --no-legs --no-live --no-decode --steps 20 --total $tot \

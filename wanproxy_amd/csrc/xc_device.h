@@ -344,16 +344,14 @@ __device__ __forceinline__ uint4 load16_unaligned(const uint8_t *p)
 #endif
 struct PayloadRegs {
     uint4 a0, a1;  // slot-aligned chunks: src + 16 l, src + 1024 + 16 l
-    uint32_t hb, tb;
 };
 
 // The loads only (the wire-aligned chunks are made from a0 / a1 at the store, so that the registers
 // of a payload in flight are its 32 bytes per lane, not twice that: the emit's occupancy).
 __device__ __forceinline__ void payload_load(const uint8_t *src, const uint8_t *out, PayloadRegs &r)
 {
+    (void)out;
     const uint32_t l = lane_id();
-    const uint32_t head = (uint32_t)((16u - ((uintptr_t)out & 15u)) & 15u);
-    const uint32_t nbody = (XC_SEG - head) >> 4;
     if (((uintptr_t)src & 15u) == 0u) {  // (aligned blocks, segment-store slots): one load each
         r.a0 = *(const uint4 *)(src + 16u * l);
         r.a1 = *(const uint4 *)(src + 1024u + 16u * l);
@@ -361,9 +359,13 @@ __device__ __forceinline__ void payload_load(const uint8_t *src, const uint8_t *
         r.a0 = load16_unaligned(src + 16u * l);
         r.a1 = load16_unaligned(src + 1024u + 16u * l);
     }
-    const uint32_t t0 = head + 16u * nbody;
-    r.hb = l < head ? src[l] : 0u;
-    r.tb = t0 + l < XC_SEG ? src[t0 + l] : 0u;
+}
+
+// Byte x (< 16) of a uint4 whose four words are wave-uniform.
+__device__ __forceinline__ uint32_t byte_of4(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t x)
+{
+    const uint32_t w = x < 4u ? w0 : x < 8u ? w1 : x < 12u ? w2 : w3;
+    return (w >> (8u * (x & 3u))) & 0xffu;
 }
 
 // The wire-aligned chunks of a payload for a wire address with `head` bytes to its next 16-byte
@@ -428,8 +430,14 @@ __device__ __forceinline__ void payload_store(uint8_t *out, uint8_t *seg, const 
     payload_wire(r, head, b0, b1);
     if (l < nbody) store16(out + head + 16u * l, b0);
     if (l + 64u < nbody) store16(out + head + 1024u + 16u * l, b1);
-    if (l < head) out[l] = (uint8_t)r.hb;
-    if (t0 + l < XC_SEG) out[t0 + l] = (uint8_t)r.tb;
+    // the head bytes (payload 0 .. head - 1: lane 0's first chunk) and the tail bytes (t0 .. 2047: lane
+    // 63's last chunk), from the registers (no byte loads)
+    if (head) {
+        const uint32_t h0 = readlane(r.a0.x, 0), h1 = readlane(r.a0.y, 0), h2 = readlane(r.a0.z, 0), h3 = readlane(r.a0.w, 0);
+        if (l < head) out[l] = (uint8_t)byte_of4(h0, h1, h2, h3, l);
+        const uint32_t e0 = readlane(r.a1.x, 63), e1 = readlane(r.a1.y, 63), e2 = readlane(r.a1.z, 63), e3 = readlane(r.a1.w, 63);
+        if (t0 + l < XC_SEG) out[t0 + l] = (uint8_t)byte_of4(e0, e1, e2, e3, t0 + l - (XC_SEG - 16u));
+    }
 }
 
 __device__ __forceinline__ void payload_store_seg(uint8_t *seg, const PayloadRegs &r)

@@ -1847,10 +1847,13 @@ __device__ __forceinline__ uint32_t write_escaped(uint8_t *dst, const uint8_t *p
 }
 
 
+// Payloads a wave has in flight: 4 since the emit compiles without the anchor path and keeps 32 bytes
+// per lane per payload (78 VGPRs; 2 before: cfg5 864 -> 876 GiB/s, cfg3 711 -> 717, one box,
+// profiles/r06/ab/emit_pay_r6i.txt; round 3 measured 4 slower when the kernel had 84 VGPRs at 2)
 #ifndef XC_EMIT_PAY
-#define XC_EMIT_PAY 2
+#define XC_EMIT_PAY 4
 #endif
-constexpr int EMIT_PAY = XC_EMIT_PAY;  // payloads a wave has in flight
+constexpr int EMIT_PAY = XC_EMIT_PAY;
 
 // k_alloc's gate (a sub-batch that needs the host stops the device pipeline here).
 __device__ __forceinline__ bool gate_stop(const EmitArgs &a)
@@ -2668,9 +2671,13 @@ __global__ __launch_bounds__(256) void k_anc_backfill(PlanDev P, uint32_t from, 
 // Restore: the anchor-table slots the segments [from, to) took are emptied (a snapshot's later
 // entries are all removed together, so no probe chain of a kept key passes through them); the
 // filter from the snapshot when snap is given.
-__global__ void k_anc_undo(AncSet s, const uint32_t *aundo, uint32_t from, uint32_t to, uint4 *filt, const uint4 *snap)
+// (word / value: the cache's anchorless word as of the snapshot, set here rather than by a 4-byte
+// copy from pageable host memory: one API call less in the host's turn between two runs)
+__global__ void k_anc_undo(AncSet s, const uint32_t *aundo, uint32_t from, uint32_t to, uint4 *filt, const uint4 *snap,
+                           uint32_t *word, uint32_t value)
 {
     const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+    if (word && i0 == 0) *word = value;
     for (uint32_t i = from + i0; i < to; i += stride) {
         const uint32_t a = aundo[i];
         if (a != NONE) s.keys[a] = XC_EMPTY64;

@@ -322,7 +322,8 @@ template <bool PREDICT, bool ANC> __global__ void k_blockhash(DeclArgs a);
 __global__ void k_aprop(AScanArgs a);
 __global__ void k_aevents(AScanArgs a);
 __global__ void k_anc_backfill(PlanDev P, uint32_t from, uint32_t to, uint32_t *ctl);
-__global__ void k_anc_undo(AncSet s, const uint32_t *aundo, uint32_t from, uint32_t to, uint4 *filt, const uint4 *snap);
+__global__ void k_anc_undo(AncSet s, const uint32_t *aundo, uint32_t from, uint32_t to, uint4 *filt, const uint4 *snap,
+                           uint32_t *word, uint32_t value);
 __global__ void k_anc_rehash(AncSet to, const uint64_t *anc_of, uint32_t n, uint32_t *aslot, uint32_t *owner);
 __global__ void k_anc_owner(uint32_t *aundo, const uint32_t *aslot, uint32_t n, const uint32_t *owner);
 __global__ void k_tailcheck(PlanDev P, uint32_t nb, uint32_t *tcnt, uint4 *tlist);

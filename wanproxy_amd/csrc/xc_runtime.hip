@@ -653,12 +653,13 @@ static int cache_anc_catch_up(xc_cache *c)
 }
 
 // After a restore: the device's anchorless word as of the snapshot (a segment without an anchor
-// below the snapshot's count was learned by the snapshot's catch-up).
-static int cache_anc_bad_reset(xc_cache *c)
+// below the snapshot's count was learned by the snapshot's catch-up).  copy: written by a copy here,
+// else by the k_anc_undo launched with the value.
+static int cache_anc_bad_reset(xc_cache *c, bool copy = true)
 {
     if (c->anc_bad >= c->snap_count) c->anc_bad = NONE;
     c->anc_bad_word = c->anc_bad == NONE ? 0u : ~c->anc_bad;
-    HIPCHK(hipMemcpyAsync(c->ctl + CTL_ANCLESS, &c->anc_bad_word, 4, hipMemcpyHostToDevice, c->ctx->stream));
+    if (copy) HIPCHK(hipMemcpyAsync(c->ctl + CTL_ANCLESS, &c->anc_bad_word, 4, hipMemcpyHostToDevice, c->ctx->stream));
     return XC_OK;
 }
 
@@ -670,12 +671,14 @@ static int cache_anc_restore(xc_cache *c)
     hipStream_t s = c->ctx->stream;
     const uint32_t to = std::max(c->anc_upto, c->snap_count);
     const uint32_t n = std::max<uint32_t>(to - c->snap_count, ANC_FILT_WORDS / 4);
+    cache_anc_bad_reset(c, false);
     hipLaunchKernelGGL(k_anc_undo, dim3(std::min<uint32_t>((n + 255) / 256, 2048)), dim3(256), 0, s, c->set.a,
-                       (const uint32_t *)c->aundo, c->snap_count, to, (uint4 *)c->set.a.filt, (const uint4 *)c->snap_afilt);
+                       (const uint32_t *)c->aundo, c->snap_count, to, (uint4 *)c->set.a.filt, (const uint4 *)c->snap_afilt,
+                       c->ctl + CTL_ANCLESS, c->anc_bad_word);
     HIPCHK(hipGetLastError());
     c->anc_upto = std::min(c->anc_upto, c->snap_anc_upto);
     c->anc_dirty = false;
-    return cache_anc_bad_reset(c);
+    return XC_OK;
 }
 
 // Rebuild the cache's tables for `ncap` segments, keeping the entries with a segment index below
@@ -1473,10 +1476,16 @@ extern "C" int xc_encode_plan_create_sub(xc_cache *c, const uint64_t *lengths, u
         uint64_t decl = 0, maxdecl = 0;
         uint64_t total = 0;
         for (uint32_t i = 0; i < nbuf; i++) total += lengths[i];
-        const uint64_t sub_max = sub_bytes(total, sub_bytes_max);
+        uint64_t sub_max = sub_bytes(total, sub_bytes_max);
+        // (XC_FIRST_PCT=p, -DXC_ABLATIONS builds: two sub-batches, the first p % of the run)
+        uint64_t first_max = sub_max;
+        if (const char *fp = abl_env("XC_FIRST_PCT"); fp && atoi(fp) > 0 && atoi(fp) < 100) {
+            first_max = ((total * (uint64_t)atoi(fp) / 100 + (1u << 20) - 1) >> 20) << 20;
+            sub_max = std::max<uint64_t>(total - first_max, 1u << 20);
+        }
         for (uint32_t i = 0; i < nbuf; i++) {
             if (lengths[i] > MAX_BUF) return fail(XC_EINVAL, "buffer longer than 1 MiB");
-            if (cnt && (bytes + lengths[i] > sub_max || cnt >= SUB_BUFS)) {
+            if (cnt && (bytes + lengths[i] > (p->sub.size() == 1 ? first_max : sub_max) || cnt >= SUB_BUFS)) {
                 p->sub.push_back(i);
                 maxdecl = std::max(maxdecl, decl);
                 max_sub_blocks = std::max(max_sub_blocks, blocks);
