@@ -664,6 +664,10 @@ __device__ __forceinline__ void write_unescaped(uint8_t *dst, const uint8_t *p, 
 
 constexpr uint32_t DMAX_TOK = 2048;
 constexpr uint32_t DEMIT_WAVES = 4;
+#ifndef XC_DEMIT_PAY
+#define XC_DEMIT_PAY 2
+#endif
+constexpr uint32_t DEMIT_PAY = XC_DEMIT_PAY;  // payloads a wave has in flight
 
 
 // Output offsets (executed tokens only), then the bytes.  One workgroup (8 waves) per stream,
@@ -753,21 +757,22 @@ __global__ __launch_bounds__(64 * DEMIT_WAVES) void k_demit(DecDev D)
                 const uint32_t flb = readlane(lb, f);
                 write_unescaped(out + off[readlane(i, f)], s + flb, readlane(le, f) - flb);
             }
+            // DEMIT_PAY payloads in flight (their loads first, then the stores)
             for (uint64_t m = ballot(from != 0); m;) {
-                const int f0 = __ffsll((unsigned long long)m) - 1;
-                m &= m - 1;
-                const int f1 = m ? __ffsll((unsigned long long)m) - 1 : -1;
-                if (m) m &= m - 1;
-                uint8_t *d0 = out + off[readlane(i, f0) + 1u] - XC_SEG;
-                PayloadRegs r0, r1;
-                payload_load((const uint8_t *)(uintptr_t)dreadlane64(from, f0), d0, r0);
-                uint8_t *d1 = nullptr;
-                if (f1 >= 0) {
-                    d1 = out + off[readlane(i, f1) + 1u] - XC_SEG;
-                    payload_load((const uint8_t *)(uintptr_t)dreadlane64(from, f1), d1, r1);
+                int f[DEMIT_PAY];
+                PayloadRegs r[DEMIT_PAY];
+#pragma unroll
+                for (int k = 0; k < (int)DEMIT_PAY; k++) {
+                    f[k] = m ? __ffsll((unsigned long long)m) - 1 : -1;
+                    if (m) m &= m - 1;
+                    if (f[k] >= 0)
+                        payload_load((const uint8_t *)(uintptr_t)dreadlane64(from, f[k]), nullptr, r[k]);
                 }
-                payload_store(d0, (uint8_t *)(uintptr_t)dreadlane64(seg, f0), r0);
-                if (f1 >= 0) payload_store(d1, (uint8_t *)(uintptr_t)dreadlane64(seg, f1), r1);
+#pragma unroll
+                for (int k = 0; k < (int)DEMIT_PAY; k++)
+                    if (f[k] >= 0)
+                        payload_store(out + off[readlane(i, f[k]) + 1u] - XC_SEG,
+                                      (uint8_t *)(uintptr_t)dreadlane64(seg, f[k]), r[k]);
             }
         }
     }
