@@ -2142,6 +2142,169 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit(EmitArgs a)
     }
 }
 
+// The wire bytes of a wave's token group (one token per lane, `live`): F1-escaped literal runs from
+// off (the token's wire offset), the op bytes, then the EXTRACT payloads to the wire and into their
+// cache slots (the lane's `slot`), EMIT_PAY at a time.
+__device__ __forceinline__ void emit_group(const PlanDev &P, uint8_t *out, const uint8_t *base, bool live, uint32_t lb,
+                                           uint32_t le, uint32_t op, uint32_t seg, uint64_t h, uint32_t off,
+                                           uint32_t slot, uint32_t eabl)
+{
+    const uint32_t l = lane_id();
+    // literal runs, F1-escaped (wave-cooperative, one run at a time)
+    for (uint64_t m = ballot(live && le > lb); m; m &= m - 1) {
+        const int f = __ffsll((unsigned long long)m) - 1;
+        const uint32_t flb = readlane(lb, f);
+        const uint32_t len = write_escaped(out + readlane(off, f), base + flb, readlane(le, f) - flb);
+        if ((int)l == f) off += len;
+    }
+    uint8_t *o = out + off;
+    if (live && op == OP_REF) {
+        o[0] = (uint8_t)XC_MAGIC;
+        o[1] = (uint8_t)OP_REF;
+#pragma unroll
+        for (int k = 0; k < 8; k++) o[2 + k] = (uint8_t)(h >> (8 * (7 - k)));
+    } else if (live && op == OP_EXTRACT) {
+        o[0] = (uint8_t)XC_MAGIC;
+        o[1] = (uint8_t)OP_EXTRACT;
+    }
+    // payloads to the wire and into the slots k_alloc reserved, EMIT_PAY at a time
+    for (uint64_t m = ballot(live && op == OP_EXTRACT && !(eabl & 8u)); m;) {
+        int f[EMIT_PAY];
+        uint32_t ii[EMIT_PAY];
+        uint8_t *d[EMIT_PAY];
+        PayloadRegs r[EMIT_PAY];
+#pragma unroll
+        for (int g = 0; g < EMIT_PAY; g++) {
+            f[g] = m ? __ffsll((unsigned long long)m) - 1 : -1;
+            if (m) m &= m - 1;
+            if (f[g] >= 0) {
+                ii[g] = readlane(slot, f[g]);
+                d[g] = out + readlane(off, f[g]) + 2u;
+                payload_load(base + readlane(seg, f[g]), d[g], r[g]);
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < EMIT_PAY; g++)
+            if (f[g] >= 0) {
+                uint8_t *sg = ii[g] < P.seg_cap && !(eabl & 1u) ? seg_at(P.segs, ii[g]) : nullptr;
+                if (eabl & 2u) {
+                    if (sg) payload_store_seg(sg, r[g]);
+                } else {
+                    payload_store(d[g], sg, r[g]);
+                }
+            }
+    }
+}
+
+// k_emit's one-pass form, for plans whose buffers have at most 64 tokens per wave (the host's bound
+// 2 len / 2048 + 3; every 64 KiB proxy read): wave w loads its contiguous token group once, sizes it
+// (escaped literals + op bytes), scans it in registers, and after one barrier (the group totals and
+// EXTRACT counts of the waves before it) enters its declarations and writes its bytes.  SLOTS / INS as
+// for k_emit.
+template <uint32_t EMIT_WAVES, bool SLOTS, int INS>
+__global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit1(EmitArgs a)
+{
+    if (emit_aborted(a)) return;
+    const uint32_t eabl = XC_ABLATIONS ? a.abl : 0u;  // (XC_ABL_EMIT timing ablations: -DXC_ABLATIONS=1 builds)
+    __shared__ uint4 red[EMIT_WAVES];
+    __shared__ uint2 grp[EMIT_WAVES];  // (one pass: each wave's wire bytes and EXTRACT tokens)
+    const PlanDev &P = a.P;
+    const uint32_t b = a.j0 + blockIdx.x;
+    if (b >= a.j1) return;
+    const uint32_t wave = threadIdx.x >> 6, l = lane_id();
+    uint32_t s_pre = 0, s_tot = 0, s_ref = 0, s_stop = 0, s_base = 0;
+    if (SLOTS) {
+        for (uint32_t i = a.j0 + threadIdx.x; i < a.j1; i += 64u * EMIT_WAVES) {
+            const uint32_t v = P.buf_next[i];
+            s_tot += v;
+            s_ref += P.buf_nref[i];
+            if (i < b) s_pre += v;
+        }
+        if (threadIdx.x == 0) {
+            s_stop = gate_stop(a) ? 1u : 0u;
+            s_base = *a.base;
+        }
+    }
+    const uint8_t *base = P.in + P.buf_off[b];
+    uint8_t *out = P.out + P.out_off[b];
+    const uint32_t tb = P.tok_base[b], n = min(P.tok_cnt[b], MAX_TOK);
+    const uint32_t G = (n + EMIT_WAVES - 1u) / EMIT_WAVES;
+    const uint32_t g_end = min(n, (wave + 1u) * G);
+
+    // this lane's token of the wave's group, kept in registers to the end
+    uint32_t lb = 0, le = 0, op = OP_END, seg = 0;
+    uint64_t h = 0;
+    const uint32_t t = wave * G + l;
+    const bool live = t < g_end;
+    if (live) {
+        lb = P.tok_lb[tb + t];
+        le = P.tok_le[tb + t];
+        op = P.tok_op[tb + t];
+        seg = P.tok_seg[tb + t];
+        h = P.tok_h[tb + t];
+    }
+    uint32_t esc = le - lb;
+    for (uint64_t m = ballot(le > lb); m; m &= m - 1) {  // F1 bytes of non-empty literal runs
+        const int f = __ffsll((unsigned long long)m) - 1;
+        const uint32_t flb = readlane(lb, f), fle = readlane(le, f);
+        const uint32_t c = count_magic(base + flb, fle - flb);
+        if ((int)l == f) esc += c;
+    }
+    const uint32_t tsz = live ? esc + (op == OP_EXTRACT ? 2u + XC_SEG : op == OP_REF ? 10u : 0u) : 0u;
+    const uint32_t inc = wave_incl_scan(tsz);
+    const uint32_t nx = (uint32_t)__popcll(ballot(live && op == OP_EXTRACT));
+    const uint32_t tot = readlane(inc, 63);
+    if (l == 0) grp[wave] = make_uint2(tot, nx);
+    if (SLOTS) {
+        const uint32_t x = wave_sum(s_pre), y = wave_sum(s_tot), z = wave_sum(s_ref);
+        if (l == 0) red[wave] = make_uint4(x, y, z, wave == 0 ? (s_stop | (s_base << 1)) : 0u);
+    }
+    __syncthreads();
+    if (SLOTS) {
+        uint4 t = make_uint4(0, 0, 0, 0);
+        for (uint32_t k = 0; k < EMIT_WAVES; k++) {
+            t.x += red[k].x;
+            t.y += red[k].y;
+            t.z += red[k].z;
+        }
+        if (red[0].w & 1u) {  // the gate: every workgroup decides the same
+            if (blockIdx.x == 0 && threadIdx.x == 0) {
+                gate_abort(a);
+                ctl_publish(a);
+            }
+            return;
+        }
+        s_base = red[0].w >> 1;
+        s_pre = t.x;
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            const uint32_t count = s_base + t.y;
+            *P.seg_count = count;
+            P.ctl[CTL_COUNT] = count;
+            P.ctl[CTL_NEXTRACT] += t.y;
+            P.ctl[CTL_NREF] += t.z;
+            if (count > P.seg_cap) P.ctl[CTL_ERROR] |= ERR_CAPACITY;
+            if (a.pub_final) ctl_publish(a);
+        }
+    }
+    const uint32_t slot0 = SLOTS ? s_base + s_pre : P.buf_slot[b];
+    if (SLOTS && threadIdx.x == 0) P.buf_slot[b] = slot0;  // (the tail check's visibility test)
+    uint32_t off = inc - tsz, xo = 0, total = 0;
+    for (uint32_t k = 0; k < EMIT_WAVES; k++) {
+        const uint2 gk = grp[k];
+        total += gk.x;
+        if (k < wave) {
+            off += gk.x;
+            xo += gk.y;
+        }
+    }
+    if (threadIdx.x == 0) P.out_len[b] = total;
+    const bool ext = live && op == OP_EXTRACT;
+    const uint32_t slot = slot0 + xo + mbcnt(ballot(ext));
+    // XCodecMemoryCache::enter of the group's declarations (xcodec_cache.h:182-188), every wave its own
+    if (INS && !(eabl & 4u)) enter_tokens<INS == 2>(P, b, base, tb, wave * G + l, ext, ext ? slot : 0u);
+    emit_group(P, out, base, live, lb, le, op, seg, h, off, slot, eabl);
+}
+
 template __global__ void k_emit<4, false, 0>(EmitArgs);
 template __global__ void k_emit<16, false, 0>(EmitArgs);
 template __global__ void k_emit<4, false, 1>(EmitArgs);
@@ -2152,6 +2315,11 @@ template __global__ void k_emit<4, true, 1>(EmitArgs);
 template __global__ void k_emit<16, true, 1>(EmitArgs);
 template __global__ void k_emit<4, true, 2>(EmitArgs);
 template __global__ void k_emit<16, true, 2>(EmitArgs);
+template __global__ void k_emit1<4, false, 0>(EmitArgs);
+template __global__ void k_emit1<4, false, 1>(EmitArgs);
+template __global__ void k_emit1<4, false, 2>(EmitArgs);
+template __global__ void k_emit1<4, true, 1>(EmitArgs);
+template __global__ void k_emit1<4, true, 2>(EmitArgs);
 
 // One workgroup: cache slots for the declarations of buffers [j0, j1) in buffer order
 // (exclusive prefix of buf_next on top of the current segment count), plus run totals.

@@ -314,6 +314,7 @@ constexpr uint32_t ERR_PACK_CAP = 8;
 
 template <int MODE> __global__ void k_scan(ScanArgs a);
 template <uint32_t NW, bool SLOTS, int INS> __global__ void k_emit(EmitArgs a);
+template <uint32_t NW, bool SLOTS, int INS> __global__ void k_emit1(EmitArgs a);
 __global__ void k_pack_offsets(PackArgs a);
 __global__ void k_pack_copy(PackArgs a);
 __global__ void k_resolve(ResolveArgs a);

@@ -2441,11 +2441,14 @@ static int launch_emit(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t jc, uint32
     const bool wide = (uint64_t)(jc - j0) * EMIT_WAVES < (uint64_t)p->cache->ctx->n_cu * 16u;
     // (the cache enters: in k_insert, or here with or without the anchor index)
     const int ins = e.split_ins && !(ab & 4u) ? 0 : p->P.anc_run ? 2 : 1;
-    auto kern = wide ? (slots ? (ins == 2 ? k_emit<16, true, 2> : k_emit<16, true, 1>)
-                              : (ins == 0 ? k_emit<16, false, 0> : ins == 2 ? k_emit<16, false, 2> : k_emit<16, false, 1>))
-                     : (slots ? (ins == 2 ? k_emit<EMIT_WAVES, true, 2> : k_emit<EMIT_WAVES, true, 1>)
-                              : (ins == 0 ? k_emit<EMIT_WAVES, false, 0>
-                                          : ins == 2 ? k_emit<EMIT_WAVES, false, 2> : k_emit<EMIT_WAVES, false, 1>));
+    // (one pass: the plan's longest buffer has at most 64 tokens per emit wave, 2 len / 2048 + 3; for
+    // the 4-wave emit only: cfg5 872-873 -> 877-879 GiB/s, cfg3 +-0, but the 16-wave one of a few
+    // buffers 222-225 -> 215 (cfg2), profiles/r06/ab/emit_one_pass_r6q.txt)
+    const bool one = !wide && 2u * p->max_decl - 1u <= 64u * EMIT_WAVES;
+#define XC_EMIT_PICK(K, W)                                                                                       \
+    (slots ? (ins == 2 ? K<W, true, 2> : K<W, true, 1>) : (ins == 0 ? K<W, false, 0> : ins == 2 ? K<W, false, 2> : K<W, false, 1>))
+    auto kern = wide ? XC_EMIT_PICK(k_emit, 16) : one ? XC_EMIT_PICK(k_emit1, EMIT_WAVES) : XC_EMIT_PICK(k_emit, EMIT_WAVES);
+#undef XC_EMIT_PICK
     // (in the context stream's order: on a stream of its own, beside the next sub-batch's predictions
     // and anchor scan, cfg5 measured -1.3 %)
     hipLaunchKernelGGL(kern, dim3(jc - j0), dim3(64 * (wide ? 16 : EMIT_WAVES)), 0, s, e);
