@@ -35,7 +35,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 SEG = 2048
 GOLD = os.path.join(ROOT, "tests", "golden", "fullsize_digests.npz")
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r05")
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r06")
 # The secondary legs (cfg2, cfg3, cfg4) time at least this many steps: their steps are 0.07-0.36 ms, so
 # 20 steps (a few ms) measured the first steps' launch ramp too (cfg4: 1319-1333 GiB/s over 20 steps,
 # 1367-1379 over 200, profiles/r05/ab/leg_steps_r5d.txt)
@@ -59,7 +59,7 @@ def parse():
     ap.add_argument("--no-legs", action="store_true", help="skip the cfg2 / cfg3 encode lines")
     ap.add_argument("--diag-env", default="",
                     help="KEY=VAL set only for the per-kernel diagnostic steps after the timed region and "
-                         "the verification (timing ablations, e.g. XC_ABL_EMIT=4)")
+                         "the verification (timing ablations of -DXC_ABLATIONS=1 builds, e.g. XC_ABL_EMIT=4)")
     ap.add_argument("--decode-streams", type=int, default=4096, help="cfg4: streams decoded per step")
     ap.add_argument("--only", choices=["cfg2", "cfg3", "cfg4", "shard8"],
                     help="run just that leg (one GPU) and print its JSON object (kernel traces, A/B)")
@@ -377,7 +377,7 @@ def pmc_traffic_path(buffers: int) -> str:
 
 def pmc_traffic(sub_batches: int, buffers: int = 32768):
     """HBM bytes per step of the whole encode pipeline from the committed rocprofv3 PMC passes of
-    this command (tools/gpu.sh pmc -> tools/pmc_traffic.py -> profiles/r05/), or None when the
+    this command (tools/gpu.sh pmc -> tools/pmc_traffic.py -> profiles/r06/), or None when the
     record was taken with other library sources than these (its src_stamp) or another layout."""
     from wanproxy_amd.provenance import source_stamp
     tp = pmc_traffic_path(buffers)

@@ -42,7 +42,7 @@ def test_bench_sharded_ranks_on_one_gpu(world):
     assert r["verified_buffers"] == 32768, r["verified_against"]
     assert "cfg5_g%d" % world in r["verified_against"]
     assert r["roofline"]["peak"] == 8000.0 * world and r["value"] > 0
-    # the committed PMC record of a rank-sized shard (profiles/r05/pmc_traffic_cfg5_b*.json), when it
+    # the committed PMC record of a rank-sized shard (profiles/r06/pmc_traffic_cfg5_b*.json), when it
     # was taken with these library sources, gives the line's traffic: a rank's bytes x N
     import bench
     rec = bench.pmc_traffic(int(r["stats"]["sub_batches"]), 32768 // world)

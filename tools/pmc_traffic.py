@@ -7,11 +7,15 @@ stream, the records of shadowed blocks dropped, as in the timed steps; round 4's
 diagnostic steps, whose first sub-batch is hashed in line without those drops).  Each of those steps spans the dispatches from its
 restore kernel to the next one (the last to the end); only the library's kernels (xc::) count.
 
-FETCH_SIZE and WRITE_SIZE are in KiB.  Per MI355X_MICROARCH.md (HBM section), on gfx950
-FETCH_SIZE reports half the bytes of wide coalesced streaming reads (16 B per lane), so it is
-doubled; WRITE_SIZE is exact for 16-B-per-lane streaming stores.  Narrow gathers (the scan's filter
-and set probes, the tables' random reads) are not calibrated: doubling them overstates them, so the
-figure is an upper bound on the bytes the step moves.
+FETCH_SIZE and WRITE_SIZE are in KiB.  The correction is calibrated on this GPU by tools/fetch_calib.hip
+(tools/gpu.sh calib -> profiles/r06/pmc_calib.json): every read request the L2 sends to memory is one
+128-byte line (TCC_EA0_RDREQ x 128 = the known bytes of coalesced reads of 1, 4, 8, 16 and 32 B per
+lane, exactly), and FETCH_SIZE tallies each at 64 B (TCC_BUBBLE and TCC_EA0_RDREQ_32B are 0): 0.500 x
+the bytes for every streaming width, and 64 B per random 4-, 8- or 16-byte gather (one request, RDREQ
+1.00 per access).  So FETCH_SIZE is doubled for every kernel, gathers included: the counters do not
+tell a gather's request size apart, so a gather counts as the 128-byte line it lands in (an upper
+bound if the fabric fetched 64 B for it); WRITE_SIZE reads 1.000 x the bytes of 1-, 4-, 8- and 16-byte
+stores.
 
 usage: python tools/pmc_traffic.py PMC_DIR OUT_JSON SUB_BATCHES|auto [ALG_BYTES_PER_STEP]
 (PMC_DIR holds FETCH_SIZE/ and WRITE_SIZE/ runs (tools/gpu.sh pmc), or p3/ and p4/; without
@@ -76,7 +80,9 @@ def main():
            "traffic_over_alg": round(kib * 1024 / alg, 3),
            "per_kernel_bytes": {k: {"fetch_x2": int(2 * f * 1024), "write": int(w * 1024)}
                                 for k, (f, w) in sorted(per_kernel.items(), key=lambda x: -(2 * x[1][0] + x[1][1]))},
-           "correction": "FETCH_SIZE x2 (gfx950 wide streaming reads), WRITE_SIZE x1; KiB -> bytes",
+           "correction": "FETCH_SIZE x2 for every kernel (gfx950: each 128-B read request tallied at 64 B, "
+                         "calibrated for streaming reads of 1-32 B per lane and 4-16 B gathers, "
+                         "profiles/r06/pmc_calib.json), WRITE_SIZE x1 (calibrated); KiB -> bytes",
            # the sources the passes ran (bench.py attaches the record only to the same sources)
            "src_stamp": source_stamp(),
            "commit": subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True,

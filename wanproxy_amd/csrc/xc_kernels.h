@@ -298,7 +298,10 @@ struct EmitArgs {
 #define XC_EMIT_SLOTS_MAX 1024
 #endif
 constexpr uint32_t EMIT_SLOTS_MAX = XC_EMIT_SLOTS_MAX;
-constexpr uint32_t INSERT_SPLIT_MIN = 8192;  // sub-batches of at least this many buffers enter the cache in k_insert
+#ifndef XC_INSERT_SPLIT_MIN
+#define XC_INSERT_SPLIT_MIN 8192
+#endif
+constexpr uint32_t INSERT_SPLIT_MIN = XC_INSERT_SPLIT_MIN;  // sub-batches of at least this many buffers enter the cache in k_insert
 
 // Packing a sub-batch's encoded streams, in buffer order, into one caller buffer (pinned host
 // memory written over PCIe by the kernel, or device memory): the end-to-end host path.

@@ -2421,12 +2421,19 @@ static int launch_emit(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t jc, uint32
     // slots, else from k_alloc; the non-slot emit never reads ctl_host)
     // (XC_ABL_EMIT, -DXC_ABLATIONS builds: read per launch, a diagnostic run sets it late)
     const char *abl = abl_env("XC_ABL_EMIT");
-    // the cache enters in k_insert for large sub-batches (cfg5's 8192 buffers: A/B 751 -> 766 GiB/s);
-    // below that the launch costs more than it saves (cfg3's 4096: 650 -> 634), and they stay in
-    // the emit workgroups
     const uint32_t ab = abl ? (uint32_t)atoi(abl) : 0u;
+    // one workgroup per buffer: 4 waves when the buffers alone fill the chip, 16 for few buffers
+    const bool wide = (uint64_t)(jc - j0) * EMIT_WAVES < (uint64_t)p->cache->ctx->n_cu * 16u;
+    // (one pass: the plan's longest buffer has at most 64 tokens per emit wave, 2 len / 2048 + 3; for
+    // the 4-wave emit only: cfg5 872-873 -> 877-879 GiB/s, cfg3 +-0, but the 16-wave one of a few
+    // buffers 222-225 -> 215 (cfg2), profiles/r06/ab/emit_one_pass_r6q.txt)
+    const bool one = !wide && 2u * p->max_decl - 1u <= 64u * EMIT_WAVES;
+    // the two-pass emit's cache enters go to k_insert for large sub-batches (cfg5's 8192 buffers: A/B
+    // 751 -> 766 GiB/s; below that the launch cost more than it saved, cfg3's 4096: 650 -> 634): there
+    // one wave per workgroup enters the whole buffer; the one-pass emit spreads them over its waves and
+    // keeps them (cfg5 875-880 -> 884-886 GiB/s against k_insert, profiles/r06/ab/emit_inserts_r6s.txt)
     EmitArgs e{p->P, j0, jc, gate_sb, p->emit_ctl_host, p->P.sb_count + sb, p->emit_pub_final, ab,
-               !slots && jc - j0 >= INSERT_SPLIT_MIN ? 1u : 0u};
+               !slots && !one && jc - j0 >= INSERT_SPLIT_MIN ? 1u : 0u};
     if (!slots) {
         hipLaunchKernelGGL(k_alloc, dim3(1), dim3(1024), 0, s, e);
         HIPCHK(hipGetLastError());
@@ -2437,14 +2444,8 @@ static int launch_emit(xc_plan *p, uint32_t sb, uint32_t j0, uint32_t jc, uint32
         hipLaunchKernelGGL(p->P.anc_run ? k_insert<true> : k_insert<false>, dim3((jc - j0 + 3) / 4), dim3(256), 0, s, e);
         HIPCHK(hipGetLastError());
     }
-    // one workgroup per buffer: 4 waves when the buffers alone fill the chip, 16 for few buffers
-    const bool wide = (uint64_t)(jc - j0) * EMIT_WAVES < (uint64_t)p->cache->ctx->n_cu * 16u;
     // (the cache enters: in k_insert, or here with or without the anchor index)
     const int ins = e.split_ins && !(ab & 4u) ? 0 : p->P.anc_run ? 2 : 1;
-    // (one pass: the plan's longest buffer has at most 64 tokens per emit wave, 2 len / 2048 + 3; for
-    // the 4-wave emit only: cfg5 872-873 -> 877-879 GiB/s, cfg3 +-0, but the 16-wave one of a few
-    // buffers 222-225 -> 215 (cfg2), profiles/r06/ab/emit_one_pass_r6q.txt)
-    const bool one = !wide && 2u * p->max_decl - 1u <= 64u * EMIT_WAVES;
 #define XC_EMIT_PICK(K, W)                                                                                       \
     (slots ? (ins == 2 ? K<W, true, 2> : K<W, true, 1>) : (ins == 0 ? K<W, false, 0> : ins == 2 ? K<W, false, 2> : K<W, false, 1>))
     auto kern = wide ? XC_EMIT_PICK(k_emit, 16) : one ? XC_EMIT_PICK(k_emit1, EMIT_WAVES) : XC_EMIT_PICK(k_emit, EMIT_WAVES);
