@@ -59,6 +59,8 @@ for step in "$@"; do
         [ -z "$a" ] && a="--no-cpu --no-e2e --no-live --steps 10"
         timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run \
             -- python3 bench.py $a > "$out/trace.log" 2>&1 || die trace $? "$out/trace.log"
+        cp "$out/trace/run_kernel_stats.csv" "$out/bench_kernel_stats.csv"
+        rm -rf "$out/trace"
         echo "trace ok" ;;
     leg)
         lg=${arg%%,*}
