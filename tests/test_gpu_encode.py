@@ -625,3 +625,30 @@ def test_block_walk_falls_back_on_any_event(gpu_ctx, oracle_mod, monkeypatch, bl
             parts.append(W.gen(7000 + 16 * j + k, 37 + 211 * ((j + k) % 9)))  # shifts the next copy
         bufs.append(np.concatenate(parts))
     _check(gpu_ctx, oracle_mod, bufs, warm=[[pool[i:i + 65536] for i in range(0, len(pool), 65536)]])
+
+
+@pytest.mark.parametrize("n,long_buf,scan", [(1024, False, "exact"), (1100, False, "exact"), (1024, False, "anchor"),
+                                             (1100, True, "exact"), (1100, True, "anchor")])
+def test_emit_forms(gpu_ctx, oracle_mod, monkeypatch, n, long_buf, scan):
+    """The emit's forms for sub-batches of >= 1024 buffers (4 waves per buffer): one pass (k_emit1,
+    every buffer <= 64 tokens per wave) with the slots inside it (exactly 1024 buffers) or from k_alloc,
+    with the cache enters with or without the anchor index; and the two-pass k_emit once one buffer can
+    hold more tokens (300 KiB).  Pool repeats, fresh bytes, escape-heavy literals, shifted repeats of
+    earlier buffers: every buffer against the oracle."""
+    monkeypatch.setenv("XC_SCAN", scan)
+    pool = W.pool(512)
+    warm = [[pool[i:i + 65536] for i in range(0, len(pool), 65536)]]
+    base = W.repeat_buffers(n, 0x7100 + n + long_buf, np_segments=512, pool_bytes=pool)
+    bufs = []
+    for i in range(n):
+        b = base[i][:16384].copy()
+        if i % 7 == 3:
+            b = _esc(9000 + i, 0x7200 + i)
+        elif i % 11 == 5 and i > 20:
+            b = np.concatenate([W.gen(0x7300 + i, 1 + i % 2047), bufs[i - 13][:12000]])
+        bufs.append(b)
+    if long_buf:
+        bufs[n // 2] = np.concatenate([pool[:150000], W.gen(0x7400, 150000), _esc(7000, 0x7401)])
+    st = _plan_run(gpu_ctx, oracle_mod, bufs, warm)
+    assert st.sub_batches == 1, st.sub_batches
+    assert (st.anchor_scans > 0) == (scan == "anchor"), st.anchor_scans
