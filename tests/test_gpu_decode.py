@@ -270,3 +270,132 @@ def test_device_resident_resolution_rounds(gpu_ctx, oracle_mod, input_ready):
             assert int(r64[n + i]) == cons, (rep, i, "consumed")
             assert (int(r64[2 * n + i]) if r32[n + i] else None) == unk, (rep, i, "unknown")
             assert out[o:o + int(r64[i])].tobytes() == data, (rep, i, "bytes")
+
+
+@pytest.mark.parametrize("input_ready", [False, True])
+def test_device_resident_cache_hits_and_collisions(gpu_ctx, oracle_mod, input_ready):
+    """EXTRACTs whose hash the cache already holds, through the device-resident plan three times
+    back to back over a restored snapshot: the same bytes (a cache hit, nothing entered) and other
+    bytes under the same hash (a collision: the stream stops there), among ordinary streams and
+    EXTRACTs past a stop (xcodec_decoder.cc:101-132).  With the input ready, round 0's cache probes
+    run in k_dres2<true> after the side stream's parse; a plan whose output capacities are too
+    small still fails there (the output bound goes to k_dfin through s_cnt)."""
+    import torch
+    import wanproxy_amd as w
+    x, y = _collision_pair(3)
+    hx = oracle_mod.hash_segment(x)
+    segs = [W.gen(0x7900 + i, 2048) for i in range(6)]
+    ext = lambda s: b"\xf1\x01" + s.tobytes()  # noqa: E731
+    ref = lambda h: b"\xf1\x02" + int(h).to_bytes(8, "big")  # noqa: E731
+    pool = W.pool(64)
+    eo = oracle_mod.Cache()
+    streams = eo.encode_batch(W.repeat_buffers(10, 0x7A, 50, np_segments=64, pool_bytes=pool))
+    streams[1:1] = [b"pre" + ext(x) + b"post" + ext(segs[0]), b"aa" + ext(y) + b"bb" + ext(segs[1]),
+                    ext(segs[2]) + ext(x) + ref(hx) + ext(segs[3]), ref(hx) + ext(y) + ext(segs[4]),
+                    ext(segs[5]) + b"q" * 3000 + ext(x)]
+    warm = [ext(x)]
+    oc = oracle_mod.Cache()
+    oc.decode_batch(warm)
+    want = oc.decode_batch(streams)
+    assert any(st == 0 for st, _, _, _ in want)  # (the collisions stop their streams)
+    gc = w.XCodecCache(gpu_ctx, 1 << 14)
+    w.XCodecDecoder(gc).decode_batch(warm)
+    gc.snapshot()
+    lens = np.array([len(s) for s in streams], np.uint64)
+    plan = w.DecodePlan(gc, lens, lens * 205 + 16)
+    arena = np.zeros(plan.in_bytes, np.uint8)
+    for i, s in enumerate(streams):
+        arena[int(plan.in_off[i]):int(plan.in_off[i]) + len(s)] = np.frombuffer(s, np.uint8)
+    n = len(streams)
+    d_in = torch.from_numpy(arena).cuda()
+    plan.set_completion(True)
+    plan.set_input_ready(input_ready)
+    sets = [(torch.zeros(plan.out_bytes, dtype=torch.uint8, device="cuda"),
+             torch.zeros(3 * n, dtype=torch.int64, device="cuda"),
+             torch.zeros(2 * n, dtype=torch.int32, device="cuda")) for _ in range(3)]
+    torch.cuda.synchronize()
+    for d_out, u64, i32 in sets:
+        gc.restore_async()
+        plan.run(d_in.data_ptr(), d_out.data_ptr(), u64.data_ptr(), u64.data_ptr() + 8 * n,
+                 i32.data_ptr(), u64.data_ptr() + 16 * n, i32.data_ptr() + 4 * n)
+    gpu_ctx.sync()
+    torch.cuda.synchronize()
+    for rep, (d_out, u64, i32) in enumerate(sets):
+        out = d_out.cpu().numpy()
+        r64 = u64.cpu().numpy().astype(np.uint64)
+        r32 = i32.cpu().numpy()
+        for i, (st, data, cons, unk) in enumerate(want):
+            o = int(plan.out_off[i])
+            assert int(r32[i]) == st, (rep, i, "status")
+            assert int(r64[n + i]) == cons, (rep, i, "consumed")
+            assert (int(r64[2 * n + i]) if r32[n + i] else None) == unk, (rep, i, "unknown")
+            assert out[o:o + int(r64[i])].tobytes() == data, (rep, i, "bytes")
+    assert len(gc) == len(oc)
+    # capacities too small for stream 1's output: the run fails, the cache is as restored
+    small = w.DecodePlan(gc, lens, np.maximum(lens, 1))
+    small.set_completion(True)
+    small.set_input_ready(input_ready)
+    d_out, u64, i32 = sets[0]
+    gc.restore()
+    n0 = len(gc)
+    with pytest.raises(w.XCodecError):
+        small.run(d_in.data_ptr(), d_out.data_ptr(), u64.data_ptr(), u64.data_ptr() + 8 * n,
+                  i32.data_ptr(), u64.data_ptr() + 16 * n, i32.data_ptr() + 4 * n)
+    gpu_ctx.sync()
+    assert len(gc) == n0
+
+
+@pytest.mark.parametrize("n", [5000, 17000])
+def test_device_resident_many_streams(gpu_ctx, oracle_mod, n):
+    """Many small streams whose segments repeat across streams (an EXTRACT in one stream, REFs to
+    it in later ones; some streams stop on an unknown REF first, so REFs to their EXTRACTs need a
+    second resolution round, and some at their end),
+    through the device-resident plan with the input ready, twice over a restored snapshot (k_dfin's
+    slot prefix over 5000 and 17000 streams: 4 and 17 streams per thread)."""
+    import torch
+    import wanproxy_amd as w
+    pool = W.pool(64)
+    eo = oracle_mod.Cache()
+    streams = eo.encode_batch(W.repeat_buffers(n, 0x7B + n, 50, slots=2, np_segments=64, pool_bytes=pool))
+    for i in range(7, n, 97):  # an unknown REF after the stream's own bytes
+        streams[i] = streams[i] + b"\xf1\x02" + int(0x1234567 + i).to_bytes(8, "big")
+    for i in range(11, n, 89):  # one before them: the stream's EXTRACTs never run, so later REFs
+        streams[i] = b"\xf1\x02" + int(0x7654321 + i).to_bytes(8, "big") + streams[i]  # need a round more
+    want = oracle_mod.Cache().decode_batch(streams)
+    gc = w.XCodecCache(gpu_ctx, 1 << 16)
+    gc.snapshot()
+    lens = np.array([len(s) for s in streams], np.uint64)
+    plan = w.DecodePlan(gc, lens, lens * 205 + 16)
+    arena = np.zeros(plan.in_bytes, np.uint8)
+    for i, s in enumerate(streams):
+        arena[int(plan.in_off[i]):int(plan.in_off[i]) + len(s)] = np.frombuffer(s, np.uint8)
+    d_in = torch.from_numpy(arena).cuda()
+    plan.set_completion(True)
+    plan.set_input_ready(True)
+    sets = [(torch.zeros(plan.out_bytes, dtype=torch.uint8, device="cuda"),
+             torch.zeros(3 * n, dtype=torch.int64, device="cuda"),
+             torch.zeros(2 * n, dtype=torch.int32, device="cuda")) for _ in range(2)]
+    torch.cuda.synchronize()
+    for d_out, u64, i32 in sets:
+        gc.restore_async()
+        plan.run(d_in.data_ptr(), d_out.data_ptr(), u64.data_ptr(), u64.data_ptr() + 8 * n,
+                 i32.data_ptr(), u64.data_ptr() + 16 * n, i32.data_ptr() + 4 * n)
+    gpu_ctx.sync()
+    torch.cuda.synchronize()
+    off = np.array([int(plan.out_off[i]) for i in range(n)])
+    for rep, (d_out, u64, i32) in enumerate(sets):
+        out = d_out.cpu().numpy()
+        r64 = u64.cpu().numpy().astype(np.uint64)
+        r32 = i32.cpu().numpy()
+        for i, (st, data, cons, unk) in enumerate(want):
+            assert int(r32[i]) == st, (rep, i, "status")
+            assert int(r64[n + i]) == cons, (rep, i, "consumed")
+            assert (int(r64[2 * n + i]) if r32[n + i] else None) == unk, (rep, i, "unknown")
+            assert out[off[i]:off[i] + int(r64[i])].tobytes() == data, (rep, i, "bytes")
+    oc = oracle_mod.Cache()
+    oc.decode_batch(streams)
+    assert len(gc) == len(oc)
+    st = plan.stats()
+    assert st.rounds >= 2
+    n_ref = sum(s.count(b"\xf1\x02") for s in streams)  # (an upper bound: escapes aside)
+    assert 0 < st.n_ref <= n_ref and st.n_extract >= st.n_entered > 0

@@ -59,7 +59,7 @@ struct DecDev {
     uint32_t seg_cap;
     uint2 *undo;
     DevSet dset;
-    DevSet dset_other;          // k_dprobe clears it (when clr_full): the other token set's table,
+    DevSet dset_other;          // k_dres2<true> clears it (when clr_full): the other token set's table,
     uint32_t clr_lo, clr_full;  // whose last reader, the run before's k_dres2, is done
     uint32_t *ctl;
     int count;                 // k_dfin: count executed REF / EXTRACT tokens into ctl
@@ -68,6 +68,7 @@ struct DecDev {
 
 enum : uint32_t {
     DCTL_FIX = 0, DCTL_ERR = 1, DCTL_NENTER = 2, DCTL_NREF = 3, DCTL_NEXTRACT = 4,
+    DCTL_MAYBE = 5,   // k_dfin: an output may not fit (workgroup 0's sum of k_dres2's flags)
     DCTL_TICKET = 6,  // k_dfin's finished workgroups (its last one resets it)
     DCTL_WORDS = 8
 };
@@ -85,6 +86,12 @@ __device__ __forceinline__ void dctl_publish(const DecDev &D)
     __threadfence_system();
     D.ctl_host[DCTL_WORDS - 1] = 0u;
     __threadfence_system();
+}
+
+// Emit kernels stand down while a resolution round asks for another one.
+__device__ __forceinline__ bool fix_pending(const DecDev &D)
+{
+    return __builtin_amdgcn_readfirstlane((int)*(volatile const uint32_t *)&D.ctl[DCTL_FIX]) != 0;
 }
 
 __device__ __forceinline__ void dclear_range(const DecDev &D, uint32_t n_lo, uint32_t n_full, uint32_t i0,
@@ -179,7 +186,7 @@ __device__ __forceinline__ void ring_read32(const uint32_t *ring, uint32_t x, ui
 // k_dclear before this kernel: its inserts must not race with a clear).
 // PROBE = false (with HASH): the parse alone, input-only work (tokens and every EXTRACT's hash): it
 // runs on a side stream as soon as a run is submitted with its input ready, beside the previous
-// run's emit; k_dprobe then does round 0's probes and inserts on the context stream.
+// run's emit; k_dres2<true> then does round 0's cache probes on the context stream.
 template <bool HASH, bool PROBE>
 __global__ __launch_bounds__(64) void k_dtok(DecDev D, int fill, int first, uint32_t n_lo, uint32_t n_full)
 {
@@ -215,7 +222,7 @@ __global__ __launch_bounds__(64) void k_dtok(DecDev D, int fill, int first, uint
         if (!PROBE) {
             // every EXTRACT into the batch table (cleared before the parse): the table is consulted
             // only for hashes the cache lacks, and a hash the cache holds is held for every token
-            // that carries it, so entering those too changes no answer (k_dprobe probes the cache)
+            // that carries it, so entering those too changes no answer (k_dres2<true> probes the cache)
             if (ex) prov_insert(D.dset, xh, ((uint64_t)j << 32) | xt);  // (round 0: no limit)
             if (ex && fill) D.t_h[tb + xt] = xh;
             xn = 0;
@@ -332,41 +339,6 @@ __global__ __launch_bounds__(64) void k_dtok(DecDev D, int fill, int first, uint
 }
 template __global__ void k_dtok<true, true>(DecDev, int, int, uint32_t, uint32_t);
 template __global__ void k_dtok<true, false>(DecDev, int, int, uint32_t, uint32_t);
-
-// Round 0 after an early parse (k_dtok<true, false>, which entered every EXTRACT in the batch table):
-// one wave per stream, its EXTRACT tokens 64 at a time, one lane per token: the cache probe (a hit's
-// payload compared wave-wide: rare; xcodec_decoder.cc:101-132); with the run's prologue (control
-// words, provider limits), as k_dtok's first launch does.
-__global__ __launch_bounds__(64) void k_dprobe(DecDev D)
-{
-    const uint32_t j = blockIdx.x, l = lane_id();
-    if (j == 0 && threadIdx.x < DCTL_WORDS) D.ctl[threadIdx.x] = 0u;
-    if (D.clr_full) dset_clear_range(D.dset_other, D.clr_lo, D.clr_full, j * 64u + l, gridDim.x * 64u);
-    if (j >= D.ns) return;
-    if (l == 0) D.s_lim[j] = 0xFFFFFFFFu;
-    const uint8_t *s = D.in + D.in_off[j];
-    const uint32_t tb = D.tok_base[j], n = D.tok_cnt[j];
-    for (uint32_t t0 = 0; t0 < n; t0 += 64u) {
-        const uint32_t t = t0 + l;
-        const bool ex = t < n && D.t_op[tb + t] == T_EXTRACT;
-        if (!ballot(ex)) continue;
-        const uint64_t h = ex ? D.t_h[tb + t] : 0ull;
-        uint64_t v = 0;
-        uint32_t st = 0;
-        const bool hit = ex && set_find(D.cache, h, &v);
-        if (ex && !hit) st = R_PENDING;
-        for (uint64_t mh = ballot(hit); mh; mh &= mh - 1) {
-            const int fh = __ffsll((unsigned long long)mh) - 1;
-            const uint32_t le = D.t_le[tb + readlane(t, fh)];
-            const bool eq = wave_equal2048(s + le + 2u, seg_at(D.segs, dreadlane64(v, fh)));
-            if ((int)l == fh) st = eq ? R_OKCACHE : R_COLL;
-        }
-        if (ex) {
-            D.t_stat[tb + t] = st;
-            D.t_src[tb + t] = st == R_OKCACHE ? v : 0;
-        }
-    }
-}
 
 // k_dres1 / k_dres2 grids: (streams, DRES_WAVES), wave y taking tokens y, y + DRES_WAVES, ...
 #ifndef XC_DRES_WAVES
@@ -491,13 +463,25 @@ __global__ __launch_bounds__(64) void k_dres1(DecDev D)
 // EXTRACT (ENTER) among its executed tokens, kept in t_src (unused for ENTER tokens); s_slot[j] =
 // the stream's ENTER count (k_dfin prefixes it). Tokens past the stop are left as they were: no
 // later kernel reads them.
+// PROBE (round 0 after an early parse, k_dtok<true, false>): round 0's cache probes in the same
+// pass, so the context stream runs no kernel between the parse and this one: the run's prologue
+// (control words, provider limits, the other token set's table cleared) and every EXTRACT's cache
+// probe (a hit's payload compared wave-wide: rare; xcodec_decoder.cc:101-132) before its provider
+// lookup (a separate probe kernel: cfg4 1398-1399 against 1428-1435 GiB/s, ab/dres2_probe_r6dp.txt).
+// The output-bound flag goes to k_dfin in bit 31 of s_cnt[j].x (no atomic on a control word
+// that workgroup 0 zeroes here).
+template <bool PROBE>
 __global__ __launch_bounds__(64) void k_dres2(DecDev D)
 {
-    const uint32_t j = blockIdx.x;
+    const uint32_t l = lane_id(), j = blockIdx.x;
+    if (PROBE) {
+        if (j == 0 && threadIdx.x < DCTL_WORDS) D.ctl[threadIdx.x] = 0u;
+        if (D.clr_full) dset_clear_range(D.dset_other, D.clr_lo, D.clr_full, j * 64u + l, gridDim.x * 64u);
+        if (j < D.ns && threadIdx.x == 0) D.s_lim[j] = 0xFFFFFFFFu;
+    }
     if (j >= D.ns) return;
     const uint8_t *s = D.in + D.in_off[j];
     const uint32_t tb = D.tok_base[j], n = D.tok_cnt[j];
-    const uint32_t l = lane_id();
     uint32_t stop = n, nr = 0, ne = 0, nent = 0;
     uint64_t lit = 0;  // literal bytes of the executed tokens and the stop token (escapes counted twice)
     for (uint32_t t0 = 0; t0 < n; t0 += 64u) {
@@ -510,11 +494,17 @@ __global__ __launch_bounds__(64) void k_dres2(DecDev D)
         const uint64_t self = ((uint64_t)j << 32) | t;
         uint32_t st = 0;
         uint64_t src = 0, pv = 0;
-        bool wst = false, wsrc = false, cmp = false;
+        bool wst = false, wsrc = false, cmp = false, chit = false;
         if (op == T_EXTRACT) {
-            st = D.t_stat[tb + t];  // (round 0's cache probe, or k_dres1's)
+            const uint64_t h = D.t_h[tb + t];
+            if (PROBE) {  // the cache first; a hit's bytes are compared below
+                chit = set_find(D.cache, h, &pv);
+                st = chit ? R_COLL : R_PENDING;
+                wst = wsrc = true;
+            } else {
+                st = D.t_stat[tb + t];  // (round 0's cache probe, or k_dres1's)
+            }
             if (st == R_PENDING) {
-                const uint64_t h = D.t_h[tb + t];
                 uint64_t v;
                 st = R_ENTER;
                 wst = wsrc = true;
@@ -539,6 +529,16 @@ __global__ __launch_bounds__(64) void k_dres2(DecDev D)
         } else if (t < n) {
             wst = true;
         }
+        if (PROBE)  // a cached hash: the payload against the cached segment, wave-wide (rare)
+            for (uint64_t m = ballot(chit); m; m &= m - 1) {
+                const int f = __ffsll((unsigned long long)m) - 1;
+                const uint32_t tf = readlane(t, f);
+                const bool eq = wave_equal2048(s + D.t_le[tb + tf] + 2u, seg_at(D.segs, dreadlane64(pv, f)));
+                if ((int)l == f) {
+                    st = eq ? R_OKCACHE : R_COLL;
+                    src = eq ? pv : 0;
+                }
+            }
         for (uint64_t m = ballot(cmp); m; m &= m - 1) {
             const int f = __ffsll((unsigned long long)m) - 1;
             const uint64_t v = dreadlane64(pv, f);
@@ -565,24 +565,25 @@ __global__ __launch_bounds__(64) void k_dres2(DecDev D)
             break;
         }
     }
-    if (l != 0) return;
     // the output is at most the literal bytes plus a segment per executed EXTRACT / REF: when
     // that may exceed the capacity, only k_demit's exact sizes decide (no early publication)
-    if (lit + (uint64_t)XC_SEG * (nr + ne) > D.out_cap[j]) atomicOr(&D.ctl[DCTL_ERR], DERR_MAYBE_OUT);
-    // stop = the stopping token; its literal is output
-    D.s_stop[j] = stop + 1u;
-    D.s_slot[j] = nent;
-    D.s_cnt[j] = make_uint2(nr, ne);  // (one device-wide atomic per stream serializes: k_dfin sums)
-    const uint32_t op = D.t_op[tb + stop], le = D.t_le[tb + stop];
-    int32_t status = 1, hu = 0;
-    uint64_t cons = le, unk = 0;
-    if (op == T_BADOP) status = 0;
-    else if (op == T_REF) { hu = 1; unk = D.t_h[tb + stop]; }           // unknown REF
-    else if (op == T_EXTRACT) { status = 0; cons = le + 2u; }           // collision
-    D.status[j] = status;
-    D.consumed[j] = cons;
-    D.has_unknown[j] = hu;
-    D.unknown[j] = unk;
+    const uint32_t maybe_out = lit + (uint64_t)XC_SEG * (nr + ne) > D.out_cap[j] ? 0x80000000u : 0u;
+    if (l == 0) {
+        // stop = the stopping token; its literal is output
+        D.s_stop[j] = stop + 1u;
+        D.s_slot[j] = nent;  // (k_dfin prefixes the counts and ORs the flags into DCTL_ERR)
+        D.s_cnt[j] = make_uint2(nr | maybe_out, ne);
+        const uint32_t op = D.t_op[tb + stop], le = D.t_le[tb + stop];
+        int32_t status = 1, hu = 0;
+        uint64_t cons = le, unk = 0;
+        if (op == T_BADOP) status = 0;
+        else if (op == T_REF) { hu = 1; unk = D.t_h[tb + stop]; }           // unknown REF
+        else if (op == T_EXTRACT) { status = 0; cons = le + 2u; }           // collision
+        D.status[j] = status;
+        D.consumed[j] = cons;
+        D.has_unknown[j] = hu;
+        D.unknown[j] = unk;
+    }
 }
 
 __device__ __forceinline__ void dset_clear_range(const DevSet &s, uint32_t n_lo, uint32_t n_full, uint32_t i0,
@@ -616,11 +617,6 @@ __global__ void k_dclear(DecDev D, uint32_t n_lo, uint32_t n_full)
     }
 }
 
-// Emit kernels stand down while a resolution round asks for another one.
-__device__ __forceinline__ bool fix_pending(const DecDev &D)
-{
-    return __builtin_amdgcn_readfirstlane((int)*(volatile const uint32_t *)&D.ctl[DCTL_FIX]) != 0;
-}
 
 __global__ void k_dlim(DecDev D, int init)
 {
@@ -791,11 +787,14 @@ __global__ __launch_bounds__(64 * DEMIT_WAVES) void k_demit(DecDev D)
     }
 }
 
-// The end of a resolution round. Its consistency first, one wave per stream: every provider used by
-// an executed token must itself be executed, and (after round 0) the executed tokens must be
-// exactly the eligible providers. Then the last workgroup to finish (a ticket in the control words)
-// takes the cache slots of the streams' ENTER tokens: the exclusive prefix of the per-stream counts
-// k_dres2 left in s_slot, on top of the current segment count, and publishes the control words.
+// The end of a resolution round. Workgroup 0 takes the cache slots of the streams' ENTER tokens:
+// the exclusive prefix of the per-stream counts k_dres2 left in s_slot, on top of the current
+// segment count.  Beside it the other workgroups check the round's consistency, one wave per
+// stream: every provider used by an executed token must itself be executed, and (after round 0)
+// the executed tokens must be exactly the eligible providers.  The last workgroup to finish (a
+// ticket in the control words) commits the segment count unless another round is due, and
+// publishes the control words.  (The slots after the checks, in the last workgroup: k_dfin
+// 13.6 us a cfg4 step, ab/dfin_split_r6dfs.txt: 1430-1437 against 1467-1473 GiB/s.)
 constexpr uint32_t DFIN_WAVES = 16, DFIN_REG = 8, DFIN_GRID = 128;
 __global__ __launch_bounds__(64 * DFIN_WAVES) void k_dfin(DecDev D, int round)
 {
@@ -803,106 +802,115 @@ __global__ __launch_bounds__(64 * DFIN_WAVES) void k_dfin(DecDev D, int round)
     __shared__ uint2 csum[DFIN_WAVES];
     __shared__ uint32_t last;
     const uint32_t wave = threadIdx.x >> 6, l = lane_id();
-    // (a grid of at most DFIN_GRID workgroups, each wave a stride of streams: every workgroup takes a
-    // ticket below, and device-scope atomics on one word serialize across the XCDs)
-    for (uint32_t j = blockIdx.x * DFIN_WAVES + wave; j < D.ns; j += gridDim.x * DFIN_WAVES) {
-        const uint32_t tb = D.tok_base[j], ex = D.s_stop[j] - 1u;
-        if (round > 0 && l == 0 && ex != D.s_lim[j]) atomicOr(&D.ctl[DCTL_FIX], 1u);
-        for (uint32_t t = l; t < ex; t += 64u) {
-            const uint64_t src = D.t_src[tb + t];
-            const uint32_t st = D.t_stat[tb + t];
-            if ((st == R_OKPROV || st == R_COLL) && (src & SRC_PROV)) {
-                const uint32_t pj = (uint32_t)((src >> 32) & 0x7FFFFFFFu), pt = (uint32_t)src;
-                if (pt + 1u >= D.s_stop[pj]) atomicOr(&D.ctl[DCTL_FIX], 1u);
+    const uint32_t start = *D.seg_count;
+    if (blockIdx.x == 0) {
+        // workgroup 0: the slots, at once (a FIX decided by the others leaves them unused): a
+        // contiguous range of streams per thread, its sums, a block prefix, its slots (up to
+        // DFIN_REG streams per thread with every load in flight at once)
+        const uint32_t per = (D.ns + 64u * DFIN_WAVES - 1u) / (64u * DFIN_WAVES);
+        const uint32_t j0 = min(D.ns, threadIdx.x * per), j1 = min(D.ns, j0 + per);
+        uint32_t sum = 0, nr = 0, ne = 0;  // ENTER tokens; executed REF / EXTRACT tokens (decode statistics)
+        uint32_t mo = 0;                   // k_dres2's output-bound flags (bit 31 of s_cnt.x)
+        uint32_t v[DFIN_REG];
+        if (per <= DFIN_REG) {
+            uint2 c[DFIN_REG];
+#pragma unroll
+            for (uint32_t k = 0; k < DFIN_REG; k++) {
+                const bool in = j0 + k < j1;
+                v[k] = in ? D.s_slot[j0 + k] : 0u;
+                c[k] = in ? D.s_cnt[j0 + k] : make_uint2(0, 0);
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < DFIN_REG; k++) {
+                sum += v[k];
+                nr += c[k].x & 0x7FFFFFFFu;
+                mo |= c[k].x;
+                ne += c[k].y;
+            }
+        } else {
+            for (uint32_t j = j0; j < j1; j++) {
+                sum += D.s_slot[j];
+                const uint2 c = D.s_cnt[j];
+                nr += c.x & 0x7FFFFFFFu;
+                mo |= c.x;
+                ne += c.y;
+            }
+        }
+        const uint32_t inc = wave_incl_scan(sum);
+        nr = wave_sum(nr) | (ballot(mo >> 31) ? 0x80000000u : 0u);
+        ne = wave_sum(ne);
+        if (l == 63) wsum[wave] = inc;
+        if (l == 0) csum[wave] = make_uint2(nr, ne);
+        __syncthreads();
+        uint32_t o = start + inc - sum;
+        for (uint32_t k = 0; k < wave; k++) o += wsum[k];
+        if (per <= DFIN_REG) {
+#pragma unroll
+            for (uint32_t k = 0; k < DFIN_REG; k++)
+                if (j0 + k < j1) {
+                    D.s_slot[j0 + k] = o;
+                    o += v[k];
+                }
+        } else {
+            for (uint32_t j = j0; j < j1; j++) {
+                const uint32_t x = D.s_slot[j];
+                D.s_slot[j] = o;
+                o += x;
+            }
+        }
+        if (threadIdx.x == 0) {  // (the totals for the last workgroup)
+            uint32_t tot = 0, mw = 0;
+            uint2 t = make_uint2(0, 0);
+            for (uint32_t k = 0; k < DFIN_WAVES; k++) {
+                tot += wsum[k];
+                t.x += csum[k].x & 0x7FFFFFFFu;
+                mw |= csum[k].x;
+                t.y += csum[k].y;
+            }
+            D.ctl[DCTL_MAYBE] = mw >> 31;
+            if (D.count) {
+                D.ctl[DCTL_NREF] = t.x;
+                D.ctl[DCTL_NEXTRACT] = t.y;
+            }
+            D.ctl[DCTL_NENTER] = tot;
+        }
+    } else {
+        // the others: the round's consistency, each wave a stride of streams (a grid of at most
+        // DFIN_GRID + 1 workgroups: every workgroup takes a ticket below, and device-scope atomics
+        // on one word serialize across the XCDs)
+        for (uint32_t j = (blockIdx.x - 1u) * DFIN_WAVES + wave; j < D.ns; j += (gridDim.x - 1u) * DFIN_WAVES) {
+            const uint32_t tb = D.tok_base[j], ex = D.s_stop[j] - 1u;
+            if (round > 0 && l == 0 && ex != D.s_lim[j]) atomicOr(&D.ctl[DCTL_FIX], 1u);
+            for (uint32_t t = l; t < ex; t += 64u) {
+                const uint64_t src = D.t_src[tb + t];
+                const uint32_t st = D.t_stat[tb + t];
+                if ((st == R_OKPROV || st == R_COLL) && (src & SRC_PROV)) {
+                    const uint32_t pj = (uint32_t)((src >> 32) & 0x7FFFFFFFu), pt = (uint32_t)src;
+                    if (pt + 1u >= D.s_stop[pj]) atomicOr(&D.ctl[DCTL_FIX], 1u);
+                }
             }
         }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        __threadfence();  // (release: this workgroup's FIX)
+        __threadfence();  // (release: this workgroup's FIX, or workgroup 0's slots and totals)
         last = atomicAdd(&D.ctl[DCTL_TICKET], 1u) == gridDim.x - 1u;
     }
     __syncthreads();
-    if (!last) return;
-    __threadfence();  // (acquire: every workgroup's FIX)
+    if (!last || threadIdx.x != 0) return;
+    __threadfence();  // (acquire: every workgroup's words)
+    D.ctl[DCTL_TICKET] = 0u;
     if (fix_pending(D)) {  // another resolution round: the host decides it now
-        if (threadIdx.x == 0) {
-            D.ctl[DCTL_TICKET] = 0u;
-            dctl_publish(D);
-        }
+        dctl_publish(D);
         return;
     }
-    // a contiguous range of streams per thread: its sums, a block prefix, its slots (up to
-    // DFIN_REG streams per thread with every load in flight at once)
-    const uint32_t start = *D.seg_count;
-    const uint32_t per = (D.ns + 64u * DFIN_WAVES - 1u) / (64u * DFIN_WAVES);
-    const uint32_t j0 = min(D.ns, threadIdx.x * per), j1 = min(D.ns, j0 + per);
-    uint32_t sum = 0, nr = 0, ne = 0;  // ENTER tokens; executed REF / EXTRACT tokens (decode statistics)
-    uint32_t v[DFIN_REG];
-    if (per <= DFIN_REG) {
-        uint2 c[DFIN_REG];
-#pragma unroll
-        for (uint32_t k = 0; k < DFIN_REG; k++) {
-            const bool in = j0 + k < j1;
-            v[k] = in ? D.s_slot[j0 + k] : 0u;
-            c[k] = in ? D.s_cnt[j0 + k] : make_uint2(0, 0);
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < DFIN_REG; k++) {
-            sum += v[k];
-            nr += c[k].x;
-            ne += c[k].y;
-        }
-    } else {
-        for (uint32_t j = j0; j < j1; j++) {
-            sum += D.s_slot[j];
-            const uint2 c = D.s_cnt[j];
-            nr += c.x;
-            ne += c.y;
-        }
-    }
-    const uint32_t inc = wave_incl_scan(sum);
-    nr = wave_sum(nr);
-    ne = wave_sum(ne);
-    if (l == 63) wsum[wave] = inc;
-    if (l == 0) csum[wave] = make_uint2(nr, ne);
-    __syncthreads();
-    uint32_t o = start + inc - sum;
-    for (uint32_t k = 0; k < wave; k++) o += wsum[k];
-    if (per <= DFIN_REG) {
-#pragma unroll
-        for (uint32_t k = 0; k < DFIN_REG; k++)
-            if (j0 + k < j1) {
-                D.s_slot[j0 + k] = o;
-                o += v[k];
-            }
-    } else {
-        for (uint32_t j = j0; j < j1; j++) {
-            const uint32_t x = D.s_slot[j];
-            D.s_slot[j] = o;
-            o += x;
-        }
-    }
-    if (threadIdx.x == 0) {
-        uint32_t carry = start;
-        uint2 t = make_uint2(0, 0);
-        for (uint32_t k = 0; k < DFIN_WAVES; k++) {
-            carry += wsum[k];
-            t.x += csum[k].x;
-            t.y += csum[k].y;
-        }
-        if (D.count) {
-            D.ctl[DCTL_NREF] = t.x;
-            D.ctl[DCTL_NEXTRACT] = t.y;
-        }
-        D.ctl[DCTL_TICKET] = 0u;
-        *D.seg_count = carry;
-        D.ctl[DCTL_NENTER] = carry - start;
-        if (carry > D.seg_cap) D.ctl[DCTL_ERR] |= 2u;
-        // final unless an output may overflow (k_demit then sets bit 1): the rest of the run
-        // changes no control word
-        if (!(D.ctl[DCTL_ERR] & DERR_MAYBE_OUT)) dctl_publish(D);
-    }
+    const uint32_t carry = start + D.ctl[DCTL_NENTER];
+    *D.seg_count = carry;
+    if (D.ctl[DCTL_MAYBE]) D.ctl[DCTL_ERR] |= DERR_MAYBE_OUT;
+    if (carry > D.seg_cap) D.ctl[DCTL_ERR] |= 2u;
+    // final unless an output may overflow (k_demit then sets bit 1): the rest of the run
+    // changes no control word
+    if (!(D.ctl[DCTL_ERR] & DERR_MAYBE_OUT)) dctl_publish(D);
 }
 
 }  // namespace xc
@@ -982,7 +990,7 @@ struct xc_dplan {
     hipEvent_t ev_parsed = nullptr, ev_free = nullptr;
     bool settled = false;
     // the batch provider tables of the two token sets: an early run's parse enters its EXTRACTs in
-    // dsets[tcur], which the early run before it cleared in its k_dprobe (clean[tcur]; done before
+    // dsets[tcur], which the early run before it cleared in its k_dres2 (clean[tcur]; done before
     // the parse starts, as above), or else the side stream clears first
     DevSet dsets[2] = {};
     bool clean[2] = {false, false};
@@ -1256,13 +1264,14 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
         hipLaunchKernelGGL(k_dclear, dim3(512), dim3(256), 0, s, D, p->n_lo, p->n_full);
         DHIP(hipGetLastError());
     }
-    if (early) {  // round 0 behind the side stream's parse
+    // round 0 behind the side stream's parse: k_dres2<true> takes the prologue and the cache probes
+    // (and clears the other set's table for the next early run on it)
+    DecDev Dq = D;
+    if (early) {
         DHIP(hipStreamWaitEvent(s, p->ev_parsed, 0));
-        DecDev Dq = D;  // (and the other set's table cleared for the next early run on it)
         Dq.dset_other = p->dsets[p->tcur ^ 1];
         Dq.clr_lo = p->n_lo;
         Dq.clr_full = p->n_full;
-        hipLaunchKernelGGL(k_dprobe, dim3(ns), dim3(64), 0, s, Dq);
     } else {
         hipLaunchKernelGGL((k_dtok<true, true>), dim3(std::max<uint32_t>(ns, 256u)), dim3(64), 0, s, D, 1, 1, p->n_lo, p->n_full);
     }
@@ -1275,7 +1284,9 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
             hipLaunchKernelGGL(k_dres1<false>, dim3(ns, DRES_WAVES), dim3(64), 0, s, D);
         }
         DHIP(hipGetLastError());
-        hipLaunchKernelGGL(k_dres2, dim3(ns), dim3(64), 0, s, D);  // (a wave per stream)
+        // (a wave per stream; round 0 after an early parse: with the prologue and the cache probes)
+        if (early && r == 0) hipLaunchKernelGGL(k_dres2<true>, dim3(ns), dim3(64), 0, s, Dq);
+        else hipLaunchKernelGGL(k_dres2<false>, dim3(ns), dim3(64), 0, s, D);
         DHIP(hipGetLastError());
         return XC_OK;
     };
@@ -1300,8 +1311,8 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
         }
         // (XC_DFIN_GRID, -DXC_ABLATIONS builds: another grid)
         static const uint32_t dfin_grid = abl_env("XC_DFIN_GRID") ? (uint32_t)atoi(abl_env("XC_DFIN_GRID")) : DFIN_GRID;
-        hipLaunchKernelGGL(k_dfin, dim3(std::max(1u, std::min(dfin_grid, (ns + DFIN_WAVES - 1) / DFIN_WAVES))),
-                           dim3(64 * DFIN_WAVES), 0, s, Da, r);
+        hipLaunchKernelGGL(k_dfin, dim3(1u + std::max(1u, std::min(dfin_grid, (ns + DFIN_WAVES - 1) / DFIN_WAVES))),
+                           dim3(64 * DFIN_WAVES), 0, s, Da, r);  // (workgroup 0: the slots)
         DHIP(hipGetLastError());  // (slots first: k_demit fills them)
         hipLaunchKernelGGL(k_demit, dim3(ns), dim3(64 * DEMIT_WAVES), 0, s, D);
         DHIP(hipGetLastError());
