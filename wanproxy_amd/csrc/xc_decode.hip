@@ -48,6 +48,7 @@ struct DecDev {
     uint32_t *s_lim;           // tokens eligible as EXTRACT providers this round
     uint32_t *s_slot;          // first cache slot of the stream's entered segments
     uint2 *s_cnt;              // executed (REF, EXTRACT) tokens of the stream (k_dfin sums them)
+    uint32_t *s_xp;            // an executed token of the stream has a provider in another stream
     uint8_t *out;
     const uint64_t *out_off;
     const uint64_t *out_cap;
@@ -482,21 +483,26 @@ __global__ __launch_bounds__(64) void k_dres2(DecDev D)
     if (j >= D.ns) return;
     const uint8_t *s = D.in + D.in_off[j];
     const uint32_t tb = D.tok_base[j], n = D.tok_cnt[j];
+    const uint64_t cap = D.out_cap[j];
     uint32_t stop = n, nr = 0, ne = 0, nent = 0;
+    uint32_t sop = T_END, sle = 0;  // the stopping token's op and end (its lane's registers)
+    uint64_t sh = 0;
+    bool xprov = false;  // an executed token with a provider in another stream (k_dfin checks it)
     uint64_t lit = 0;  // literal bytes of the executed tokens and the stop token (escapes counted twice)
     for (uint32_t t0 = 0; t0 < n; t0 += 64u) {
         const uint32_t t = t0 + l;
-        uint32_t op = T_END, ll = 0;
+        uint32_t op = T_END, ll = 0, le = 0;
         if (t < n) {
             op = D.t_op[tb + t];
-            ll = D.t_le[tb + t] - D.t_lb[tb + t];
+            le = D.t_le[tb + t];
+            ll = le - D.t_lb[tb + t];
         }
         const uint64_t self = ((uint64_t)j << 32) | t;
         uint32_t st = 0;
-        uint64_t src = 0, pv = 0;
+        uint64_t src = 0, pv = 0, h = 0;
         bool wst = false, wsrc = false, cmp = false, chit = false;
         if (op == T_EXTRACT) {
-            const uint64_t h = D.t_h[tb + t];
+            h = D.t_h[tb + t];
             if (PROBE) {  // the cache first; a hit's bytes are compared below
                 chit = set_find(D.cache, h, &pv);
                 st = chit ? R_COLL : R_PENDING;
@@ -515,7 +521,7 @@ __global__ __launch_bounds__(64) void k_dres2(DecDev D)
                 }
             }
         } else if (op == T_REF) {
-            const uint64_t h = D.t_h[tb + t];
+            h = D.t_h[tb + t];
             uint64_t v;
             st = R_UNKNOWN;
             wst = wsrc = true;
@@ -532,8 +538,7 @@ __global__ __launch_bounds__(64) void k_dres2(DecDev D)
         if (PROBE)  // a cached hash: the payload against the cached segment, wave-wide (rare)
             for (uint64_t m = ballot(chit); m; m &= m - 1) {
                 const int f = __ffsll((unsigned long long)m) - 1;
-                const uint32_t tf = readlane(t, f);
-                const bool eq = wave_equal2048(s + D.t_le[tb + tf] + 2u, seg_at(D.segs, dreadlane64(pv, f)));
+                const bool eq = wave_equal2048(s + readlane(le, f) + 2u, seg_at(D.segs, dreadlane64(pv, f)));
                 if ((int)l == f) {
                     st = eq ? R_OKCACHE : R_COLL;
                     src = eq ? pv : 0;
@@ -542,10 +547,9 @@ __global__ __launch_bounds__(64) void k_dres2(DecDev D)
         for (uint64_t m = ballot(cmp); m; m &= m - 1) {
             const int f = __ffsll((unsigned long long)m) - 1;
             const uint64_t v = dreadlane64(pv, f);
-            const uint32_t tf = readlane(t, f);
             const uint32_t pj = (uint32_t)(v >> 32), pt = (uint32_t)v;
             const uint8_t *pp = D.in + D.in_off[pj] + D.t_le[D.tok_base[pj] + pt] + 2u;
-            const bool eq = wave_equal2048(s + D.t_le[tb + tf] + 2u, pp);
+            const bool eq = wave_equal2048(s + readlane(le, f) + 2u, pp);
             if ((int)l == f) st = eq ? R_OKPROV : R_COLL;
         }
         // the first token of these 64 that stops the decode
@@ -553,6 +557,8 @@ __global__ __launch_bounds__(64) void k_dres2(DecDev D)
         const uint32_t k = brk ? (uint32_t)__ffsll((unsigned long long)brk) - 1u : 64u;
         lit += wave_sum(l <= k ? ll : 0u);
         const bool ex = l < k && t < n;
+        xprov |= ballot(ex && (st == R_OKPROV || st == R_COLL) && (src & SRC_PROV) &&
+                        (uint32_t)((src >> 32) & 0x7FFFFFFFu) != j) != 0ull;
         nr += (uint32_t)__popcll(ballot(ex && op == T_REF));
         ne += (uint32_t)__popcll(ballot(ex && op == T_EXTRACT));
         const uint64_t em = ballot(ex && st == R_ENTER);
@@ -562,23 +568,26 @@ __global__ __launch_bounds__(64) void k_dres2(DecDev D)
         if (wsrc) D.t_src[tb + t] = src;
         if (brk) {
             stop = t0 + k;
+            sop = readlane(op, k);
+            sle = readlane(le, k);
+            sh = dreadlane64(h, k);
             break;
         }
     }
     // the output is at most the literal bytes plus a segment per executed EXTRACT / REF: when
     // that may exceed the capacity, only k_demit's exact sizes decide (no early publication)
-    const uint32_t maybe_out = lit + (uint64_t)XC_SEG * (nr + ne) > D.out_cap[j] ? 0x80000000u : 0u;
+    const uint32_t maybe_out = lit + (uint64_t)XC_SEG * (nr + ne) > cap ? 0x80000000u : 0u;
     if (l == 0) {
         // stop = the stopping token; its literal is output
         D.s_stop[j] = stop + 1u;
         D.s_slot[j] = nent;  // (k_dfin prefixes the counts and ORs the flags into DCTL_ERR)
         D.s_cnt[j] = make_uint2(nr | maybe_out, ne);
-        const uint32_t op = D.t_op[tb + stop], le = D.t_le[tb + stop];
+        D.s_xp[j] = xprov ? 1u : 0u;
         int32_t status = 1, hu = 0;
-        uint64_t cons = le, unk = 0;
-        if (op == T_BADOP) status = 0;
-        else if (op == T_REF) { hu = 1; unk = D.t_h[tb + stop]; }           // unknown REF
-        else if (op == T_EXTRACT) { status = 0; cons = le + 2u; }           // collision
+        uint64_t cons = sle, unk = 0;
+        if (sop == T_BADOP) status = 0;
+        else if (sop == T_REF) { hu = 1; unk = sh; }                        // unknown REF
+        else if (sop == T_EXTRACT) { status = 0; cons = sle + 2u; }         // collision
         D.status[j] = status;
         D.consumed[j] = cons;
         D.has_unknown[j] = hu;
@@ -879,8 +888,9 @@ __global__ __launch_bounds__(64 * DFIN_WAVES) void k_dfin(DecDev D, int round)
         // DFIN_GRID + 1 workgroups: every workgroup takes a ticket below, and device-scope atomics
         // on one word serialize across the XCDs)
         for (uint32_t j = (blockIdx.x - 1u) * DFIN_WAVES + wave; j < D.ns; j += (gridDim.x - 1u) * DFIN_WAVES) {
-            const uint32_t tb = D.tok_base[j], ex = D.s_stop[j] - 1u;
+            const uint32_t tb = D.tok_base[j], ex = D.s_stop[j] - 1u, xp = D.s_xp[j];
             if (round > 0 && l == 0 && ex != D.s_lim[j]) atomicOr(&D.ctl[DCTL_FIX], 1u);
+            if (!xp) continue;  // (no provider in another stream: nothing to check)
             for (uint32_t t = l; t < ex; t += 64u) {
                 const uint64_t src = D.t_src[tb + t];
                 const uint32_t st = D.t_stat[tb + t];
@@ -1104,6 +1114,7 @@ extern "C" int xc_decode_plan_create(xc_cache *c, const uint64_t *in_len, const 
     d_ilen = (uint32_t *)(d_ocap + std::max<uint32_t>(ns, 1));
     d_tbase = d_ilen + std::max<uint32_t>(ns, 1);
     DA(&D.tok_cnt, ns); DA(&D.s_stop, ns); DA(&D.s_slot, ns); DA(&D.s_cnt, ns); DA(&D.s_lim, ns); DA(&D.ctl, DCTL_WORDS);
+    DA(&D.s_xp, ns);
     DA(&D.t_lb, ntok); DA(&D.t_le, ntok); DA(&D.t_op, ntok); DA(&D.t_stat, ntok); DA(&D.t_h, ntok);
     DA(&D.t_src, ntok);
     // The batch provider tables (two when the parse runs ahead, dsets[1] below) are keys and values
@@ -1228,6 +1239,7 @@ extern "C" int xc_decode_run(xc_dplan *p, const uint8_t *d_in, uint8_t *d_out, u
     } else {
         p->clean[p->tcur] = false;  // (this run's tokenizer enters into p->D.dset = dsets[tcur])
     }
+
     DecDev D = p->D;
     D.in = d_in;
     D.out = d_out;
