@@ -1,5 +1,7 @@
 """Long randomized parity campaign on the GPU (beyond tests/test_gpu_fuzz.py's 16 seeds): batch
-encodes, stateful stream calls and decodes of truncated / corrupted streams, each against the oracle.
+encodes, stateful stream calls and decodes of truncated / corrupted streams (through XCodecDecoder, and
+through a device-resident DecodePlan with the input ready: the early parse and round 0 in k_dres2<true>),
+each against the oracle.
 Runs seeds until the time budget is spent; prints every failing seed.
 usage: python tools/fuzz_campaign.py SECONDS [FIRST_SEED]"""
 import os
@@ -20,7 +22,56 @@ ctx = w.Context(0)
 pool = W.pool(64)
 t_end = time.time() + budget
 fails = 0
-runs = {"encode": 0, "streams": 0, "decode": 0, "coss": 0, "plan": 0, "dup": 0}
+runs = {"encode": 0, "streams": 0, "decode": 0, "coss": 0, "plan": 0, "dup": 0, "dplan": 0}
+
+
+def mangle(rng, streams):
+    out = []
+    for s in streams:
+        s = bytearray(s)
+        r = rng.random()
+        if r < 0.3 and s:
+            s = s[:int(rng.integers(len(s)))]          # truncated (a stream cut mid-token)
+        elif r < 0.45 and s:
+            s[int(rng.integers(len(s)))] = 0xF1         # a stray magic byte
+        elif r < 0.55 and len(s) > 10:
+            k = int(rng.integers(len(s) - 1))
+            s[k:k + 2] = bytes([0xF1, 0x02])            # a REF to an unknown hash
+        out.append(bytes(s))
+    return out
+
+
+def plan_decode(gd, streams, reps):
+    """streams through a DecodePlan (stream ordered, input ready), `reps` runs over the cache's
+    snapshot; the results of each run as decode_batch's tuples"""
+    import torch
+    lens = np.array([len(x) for x in streams], np.uint64)
+    plan = w.DecodePlan(gd, lens, lens * 205 + 16)
+    plan.set_completion(True)
+    plan.set_input_ready(True)
+    arena = np.zeros(plan.in_bytes, np.uint8)
+    for i, x in enumerate(streams):
+        arena[int(plan.in_off[i]):int(plan.in_off[i]) + len(x)] = np.frombuffer(x, np.uint8)
+    n = len(streams)
+    d_in = torch.from_numpy(arena).cuda()
+    sets = [(torch.zeros(plan.out_bytes, dtype=torch.uint8, device="cuda"),
+             torch.zeros(3 * n, dtype=torch.int64, device="cuda"),
+             torch.zeros(2 * n, dtype=torch.int32, device="cuda")) for _ in range(reps)]
+    torch.cuda.synchronize()
+    for d_out, u64, i32 in sets:
+        gd.restore_async()
+        plan.run(d_in.data_ptr(), d_out.data_ptr(), u64.data_ptr(), u64.data_ptr() + 8 * n,
+                 i32.data_ptr(), u64.data_ptr() + 16 * n, i32.data_ptr() + 4 * n)
+    ctx.sync()
+    torch.cuda.synchronize()
+    res = []
+    for d_out, u64, i32 in sets:
+        out, r64, r32 = d_out.cpu().numpy(), u64.cpu().numpy().astype(np.uint64), i32.cpu().numpy()
+        res.append([(int(r32[i]), out[int(plan.out_off[i]):int(plan.out_off[i]) + int(r64[i])].tobytes(),
+                     int(r64[n + i]), int(r64[2 * n + i]) if r32[n + i] else None) for i in range(n)])
+    plan.close()
+    return res
+
 while time.time() < t_end:
     if seed % 10 == 0:
         print("progress seed", seed, runs, "fails", fails, flush=True)
@@ -173,21 +224,23 @@ while time.time() < t_end:
             for c in range(n):
                 if ge[c].flush() != oe[c].flush():
                     raise AssertionError("final flush differs")
+        elif kind == "dplan":
+            bufs = F._batch(rng, pool)
+            mangled = mangle(rng, oc.encode_batch(bufs))
+            if rng.random() < 0.5:  # the same segments twice in the batch: EXTRACTs with earlier providers
+                mangled = mangled + mangled[:int(rng.integers(1, len(mangled) + 1))]
+            od, gd = oracle.Cache(), w.XCodecCache(ctx, 1 << 14)
+            od.decode_batch(oracle.Cache().encode_batch(warm))
+            w.XCodecDecoder(gd).decode_batch(oracle.Cache().encode_batch(warm))
+            gd.snapshot()
+            want = od.decode_batch(mangled)
+            for got in plan_decode(gd, mangled, 2):
+                if got != want:
+                    raise AssertionError("plan decode differs")
         else:
             bufs = F._batch(rng, pool)
             streams = oc.encode_batch(bufs)
-            mangled = []
-            for s in streams:
-                s = bytearray(s)
-                r = rng.random()
-                if r < 0.3 and s:
-                    s = s[:int(rng.integers(len(s)))]          # truncated (a stream cut mid-token)
-                elif r < 0.45 and s:
-                    s[int(rng.integers(len(s)))] = 0xF1         # a stray magic byte
-                elif r < 0.55 and len(s) > 10:
-                    k = int(rng.integers(len(s) - 1))
-                    s[k:k + 2] = bytes([0xF1, 0x02])            # a REF to an unknown hash
-                mangled.append(bytes(s))
+            mangled = mangle(rng, streams)
             od, gd = oracle.Cache(), w.XCodecCache(ctx, 1 << 12)
             od.decode_batch(oracle.Cache().encode_batch(warm))
             w.XCodecDecoder(gd).decode_batch(oracle.Cache().encode_batch(warm))
