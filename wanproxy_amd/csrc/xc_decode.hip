@@ -669,10 +669,12 @@ __device__ __forceinline__ void write_unescaped(uint8_t *dst, const uint8_t *p, 
 
 constexpr uint32_t DMAX_TOK = 2048;
 constexpr uint32_t DEMIT_WAVES = 4;
+// payloads a wave has in flight: 3 (one box, bench.py --only cfg4: 1491-1497 against 1469-1484 GiB/s at
+// 2, profiles/r06/ab/demit_pay3_r6dg.txt; 4 and 6 were slower, demit_pay_r6l.txt)
 #ifndef XC_DEMIT_PAY
-#define XC_DEMIT_PAY 2
+#define XC_DEMIT_PAY 3
 #endif
-constexpr uint32_t DEMIT_PAY = XC_DEMIT_PAY;  // payloads a wave has in flight
+constexpr uint32_t DEMIT_PAY = XC_DEMIT_PAY;
 
 
 // Output offsets (executed tokens only), then the bytes.  One workgroup (8 waves) per stream,
