@@ -3,18 +3,20 @@
 // Reference: XCodecDecoder::decode (xcodec/xcodec_decoder.cc:76-176), one call per stream,
 // streams in index order, one shared XCodecMemoryCache.  Pipeline:
 //
-//   k_dtok     one wave per stream: F1 search in 1 KiB register windows -> tokens
-//              (literal run [lb, le) with F1 00 escapes, then the op at le); also the run's
-//              prologue (control words, provider limits, round 0's provider table)
-//   k_dres1    (round 0: H of every EXTRACT payload first, xcodec_hash.h:166-174)
-//              EXTRACT vs the cache: equal -> ok, different -> collision (decode returns
-//              false, xcodec_decoder.cc:120-132); absent -> candidate provider, min-merged
-//              by (stream, token) into the batch table
+//   k_dtok     one wave per stream: F1 search in 4 KiB windows loaded two ahead -> tokens
+//              (literal run [lb, le) with F1 00 escapes, then the op at le); every EXTRACT
+//              payload hashed as it is passed (H, xcodec_hash.h:166-174) and entered in the
+//              batch provider table, min-merged by (stream, token).  With the input ready it
+//              runs on a side stream beside the previous run's emit; else also the run's
+//              prologue and round 0's cache probes (k_dtok<true, true>)
+//   k_dres1    later rounds only: EXTRACT vs the cache (equal -> ok, different -> collision,
+//              decode returns false, xcodec_decoder.cc:120-132; absent -> candidate provider)
 //   k_dres2    every token against cache + earlier providers: REF data source or unknown
 //              (xcodec_decoder.cc:142-166); later duplicate EXTRACTs compared with the first;
-//              per stream the first token that stops the decode, ENTER ordinals
-//   k_dfin     round consistency (a provider past its own stream's stop: the host re-resolves,
-//              rare), then in its last workgroup the cache slots of the ENTER tokens
+//              per stream the first token that stops the decode, ENTER ordinals.  Round 0
+//              after an early parse: the prologue and the EXTRACT cache probes too
+//   k_dfin     workgroup 0: the cache slots of the ENTER tokens; the others: round
+//              consistency (a provider past its own stream's stop: the host re-resolves, rare)
 //   k_demit    unescape literals, copy EXTRACT payloads (first-seen ones into their cache
 //              slots too), gather REF segments; enter the first-seen hashes in the cache
 #include <hip/hip_runtime.h>
@@ -677,10 +679,10 @@ constexpr uint32_t DEMIT_WAVES = 4;
 constexpr uint32_t DEMIT_PAY = XC_DEMIT_PAY;
 
 
-// Output offsets (executed tokens only), then the bytes.  One workgroup (8 waves) per stream,
-// tokens in blocks of DMAX_TOK: sizes lane-parallel (one token per lane; escapes counted only
-// in non-empty literal runs), a prefix, then each wave writes a contiguous token group with
-// two 2048-byte copies in flight.
+// Output offsets (executed tokens only), then the bytes.  One workgroup (DEMIT_WAVES waves) per
+// stream, tokens in blocks of DMAX_TOK: sizes lane-parallel (one token per lane; escapes counted
+// only in non-empty literal runs), a prefix, then each wave writes a contiguous token group with
+// DEMIT_PAY 2048-byte copies in flight.
 __global__ __launch_bounds__(64 * DEMIT_WAVES) void k_demit(DecDev D)
 {
     if (fix_pending(D)) return;
