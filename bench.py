@@ -221,11 +221,22 @@ def bench_decode(args, ctx, warm):
         raise SystemExit("bench: decode round trip differs from the original buffers")
     enc_bytes, dec_bytes = int(lens.sum()), n * W.BUF
     alg = enc_bytes + dec_bytes + SEG * (int(st.n_entered) + int(st.n_ref))
+    # the step's HBM traffic from the PMC record of these library sources (tools/pmc_dec.sh), if any
+    from wanproxy_amd.provenance import source_stamp
+    tr = None
+    tp = os.path.join(PROFILE_DIR, "pmc_traffic_cfg4.json")
+    if n == 4096 and os.path.exists(tp):
+        rec = json.load(open(tp))
+        if rec.get("src_stamp") == source_stamp() and rec.get("alg_bytes_per_step") == alg:
+            tr = rec
     return {"workload": "cfg4", "streams": n, "value": round(dec_bytes / el / 2**30, 3),
             "unit": "GiB/s decoded (device resident)", "ms_per_step": round(el * 1e3, 3), "steps": steps,
             "enc_GiBs": round(enc_bytes / el / 2**30, 3),
             "roofline": {"bound": "hbm", "alg_bytes_per_step": alg, "achieved": round(alg / el / 1e9, 1),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(alg / el / 1e9 / HBM_PEAK_GBS, 4)},
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(alg / el / 1e9 / HBM_PEAK_GBS, 4),
+                         "traffic": tr["traffic_bytes_per_step"] if tr else None,
+                         "traffic_over_alg": tr["traffic_over_alg"] if tr else None,
+                         "traffic_source": os.path.relpath(tp, ROOT) if tr else None},
             "stats": {"n_extract": int(st.n_extract), "n_ref": int(st.n_ref), "n_entered": int(st.n_entered),
                       "rounds": int(st.rounds)},
             "verified_streams": n}

@@ -21,6 +21,19 @@ print("kernel, dispatches, read bytes per dispatch (FETCH_SIZE x2), written byte
 for k, (f, w, n) in sorted(agg.items(), key=lambda x: -(x[1][0] + x[1][1])):
     if n:
         print(f"{k[:60]:60s} {n:5d} {f / n / 1e6:10.1f} MB {w / n / 1e6:10.1f} MB")
+# the step record bench.py attaches to its decode object (same library sources only): the kernels of a
+# timed step (the restore, round 0 in k_dres2<true>, the parse, k_dfin, k_demit), per dispatch
+import json, os
+sys.path.insert(0, os.getcwd())
+from wanproxy_amd.provenance import source_stamp
+step = ("k_demit", "k_dtok<true, false>", "k_dres2<true>", "k_dfin", "k_undo_known")
+per = {k: {"read": int(f / n), "write": int(w / n)} for k, (f, w, n) in agg.items() if n and k.split("::")[-1] in step}
+line = json.loads([x for x in open(f"{d}/FETCH_SIZE.log").read().splitlines() if x.startswith("{")][-1])
+alg = int(line["roofline"]["alg_bytes_per_step"])
+tot = sum(v["read"] + v["write"] for v in per.values())
+json.dump({"traffic_bytes_per_step": tot, "alg_bytes_per_step": alg, "traffic_over_alg": round(tot / alg, 3),
+           "per_kernel_bytes": per, "correction": "FETCH_SIZE x2, WRITE_SIZE x1 (profiles/r06/pmc_calib.json)",
+           "src_stamp": source_stamp()}, open(f"{d}/pmc_traffic_cfg4.json", "w"), indent=1)
 PY
 rm -rf $out/FETCH_SIZE $out/WRITE_SIZE
 cat $out/pmc_dec.txt
